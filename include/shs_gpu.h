@@ -1,0 +1,131 @@
+/*
+ * shs_gpu.h -- C ABI of libshs_gpu.so, the MI355X (gfx950) replacement for the shs_renderer
+ * triangle scan-conversion hot path.
+ *
+ * The reference has no C ABI/FFI; it has three C++ seams, and every entry point
+ * below names the seam it replaces.  Paths are relative to /root/reference/cpp-folders/src/.
+ *
+ *   Seam 1 (legacy draw-call seam): RendererSystem::process(dt) -> draw_triangle_tile(Canvas&,
+ *     ZBuffer&, verts, norms, std::function VS, std::function FS, tile_min, tile_max)
+ *     hello-3d-primitives/hello_pipeline_blinn_phong_shading.cpp:189-313 (and the Phong :204,
+ *     Gouraud :186-236, Flat :194-247 copies).  Replaced by shs_render_legacy(): the std::function
+ *     shaders become the shading-model enum + POD uniform block of shs_legacy_draw, the per-tile job
+ *     loop becomes one enqueue on the context's HIP stream.
+ *   Seam 2 (library rasterize_mesh) and Seam 3 (IRenderPass plugin) are later rows.
+ *
+ * Conventions: every function returns int status (0 = SHS_OK), never throws; a
+ * context is used by one host thread at a time; host buffers are caller-owned and use the exact
+ * reference layouts (RGBA8 canvas rows bottom-up, f32 depth in screen rows for the legacy path);
+ * matrices are column-major float[16] exactly as glm::mat4 stores them.  No torch types cross.
+ */
+#ifndef SHS_GPU_H
+#define SHS_GPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHS_OK 0
+#define SHS_ERR_INVALID (-1)     /* bad argument (null pointer, bad size, unknown id)      */
+#define SHS_ERR_HIP (-2)         /* HIP runtime error (message via shs_last_error)         */
+#define SHS_ERR_NO_DEVICE (-3)   /* no gfx950 device / device index out of range           */
+#define SHS_ERR_OVERFLOW (-4)    /* internal bin capacity exceeded; frame re-issued        */
+
+/* Shading models of the legacy pipelines (the FS/VS pairs each hello_pipeline_* demo binds). */
+#define SHS_SHADING_FLAT 0         /* hello_pipeline_flat_shading.cpp:46-98         */
+#define SHS_SHADING_GOURAUD 1      /* hello_pipeline_gouraud_shading.cpp:46-89       */
+#define SHS_SHADING_PHONG 2        /* hello_pipeline_phong_shading.cpp:47-108        */
+#define SHS_SHADING_BLINN_PHONG 3  /* hello_pipeline_blinn_phong_shading.cpp:48-97   */
+
+typedef struct shs_ctx shs_ctx;
+
+/* One legacy draw = one object of the scene loop (blinn_phong_shading.cpp:272-305): the
+ * reference's `Uniforms` POD (:36-42) plus the mesh handle and shading model.
+ *   model      : Uniforms::model; for SHS_SHADING_FLAT this is Uniforms::mv (flat_shading.cpp:35)
+ *   light_dir  : Uniforms::light_dir (world); for SHS_SHADING_FLAT: Uniforms::light_dir_view      */
+typedef struct shs_legacy_draw {
+    int32_t mesh_id;
+    int32_t shading;
+    float mvp[16];
+    float model[16];
+    float light_dir[3];
+    float camera_pos[3];
+    uint8_t color[4];
+} shs_legacy_draw;
+
+/* Per-frame description.  ref_tile_w/h are the reference's tile-job size (TILE_SIZE_X/Y = 80,
+ * blinn_phong_shading.cpp:29-30): the legacy raster clamps each triangle's bounding box to the
+ * tile that runs it, and the GPU path reproduces that visited-pixel set exactly.
+ * shard_rank/shard_count select the 32x32 GPU tiles this device owns (tile % count == rank);
+ * (0,1) renders the whole frame. */
+typedef struct shs_frame_desc {
+    int32_t width, height;
+    int32_t ref_tile_w, ref_tile_h;
+    int32_t shard_rank, shard_count;
+    uint32_t flags;               /* SHS_FRAME_* */
+    uint8_t clear_color[4];       /* Canvas::fill_pixel colour, {0,0,0,255} in every demo      */
+} shs_frame_desc;
+
+#define SHS_FRAME_PREQUANT 1u     /* also keep the shader's pre-truncation floats (tests)     */
+
+typedef struct shs_raster_stats {
+    uint64_t tri_input;           /* triangles submitted (rasterizer.hpp:208 tri_input)        */
+    uint64_t tri_setup;           /* triangles surviving setup culls (area<=0, |denom|<1e-5)   */
+    uint64_t tri_ghost;           /* triangles needing the exact tile-clamp ("ghost") pass     */
+    uint64_t bin_entries;         /* (tile, triangle) pairs binned                              */
+    uint64_t covered_pixels;      /* final pixels with depth != clear (shaded Mpix/s numerator) */
+} shs_raster_stats;
+
+/* ---- context ---------------------------------------------------------------------------- */
+int shs_create(int device, shs_ctx **out);
+int shs_destroy(shs_ctx *ctx);
+const char *shs_last_error(shs_ctx *ctx);
+/* Run on a caller-provided hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL
+ * restores the context's own stream. */
+int shs_set_stream(shs_ctx *ctx, void *hip_stream);
+void *shs_get_stream(shs_ctx *ctx);
+int shs_synchronize(shs_ctx *ctx);
+
+/* ---- geometry (replaces the ModelGeometry vectors the tile jobs read,
+ *      shs_renderer.hpp:1296-1298; uploaded once, device resident) ------------------------ */
+int shs_mesh_upload_soup(shs_ctx *ctx, const float *positions, const float *normals, int32_t n_tris,
+                         int32_t *mesh_id);
+int shs_mesh_release(shs_ctx *ctx, int32_t mesh_id);
+
+/* ---- the hot path (Seam 1) --------------------------------------------------------------- */
+/* Clears the frame (Canvas::fill_pixel + ZBuffer::clear) and rasterises all draws in order,
+ * asynchronously on the context stream.  Results stay in device memory until shs_resolve. */
+int shs_render_legacy(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws);
+
+/* Copy the frame into caller-owned host buffers (blocking).  color: W*H*4 bytes, canvas rows
+ * (Canvas::buffer() layout); depth: W*H floats, screen rows (ZBuffer::buffer() as the legacy
+ * pipelines index it).  Either pointer may be NULL. */
+int shs_resolve(shs_ctx *ctx, uint8_t *color, float *depth);
+/* Pre-truncation shader floats, W*H*4 (canvas rows), only when SHS_FRAME_PREQUANT was set. */
+int shs_resolve_prequant(shs_ctx *ctx, float *prequant);
+/* Device pointers of the current frame (zero-copy hand-off to torch / RCCL). */
+int shs_device_framebuffers(shs_ctx *ctx, void **color_dev, void **depth_dev);
+int shs_get_stats(shs_ctx *ctx, shs_raster_stats *stats);
+
+/* Per-kernel device timing of the last frame, recorded with HIP events on the context stream
+ * (setup+count, scan, scatter, raster) in milliseconds.  Enabled by shs_enable_timing(ctx, 1). */
+int shs_enable_timing(shs_ctx *ctx, int enable);
+int shs_last_kernel_ms(shs_ctx *ctx, float *ms4);
+
+/* ---- host helpers: GLM restatements the reference host code computes with glm -----------
+ * (Camera3D::update shs_renderer.hpp:1224-1236; MonkeyObject::get_world_matrix
+ *  blinn_phong_shading.cpp:122-128).  The drop-in host keeps its own glm code; these exist so
+ *  non-C++ callers (tests, bench) can build identical uniforms. */
+int shs_camera3d(const float position[3], float horizontal_angle, float vertical_angle, float fov_deg,
+                 float z_near, float z_far, float view16[16], float proj16[16]);
+int shs_model_trs(const float position[3], float rotation_deg_y, const float scale[3], float out16[16]);
+int shs_mat4_mul(const float a16[16], const float b16[16], float out16[16]);
+
+/* Library/ABI version for integration checks. */
+int shs_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,475 @@
+// shs_abi.cpp -- host side of libshs_gpu.so: the C ABI declared in include/shs_gpu.h.
+//
+// Owns device-resident meshes, the per-frame workspace (triangle records, tile bins, framebuffers)
+// and the HIP stream the four kernels of shs_legacy.hip are enqueued on.  Replaces the tile-job
+// submission loop of RendererSystem::process (hello_pipeline_blinn_phong_shading.cpp:244-313).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/shs_gpu.h"
+#include "shs_device.hpp"
+#include "shs_glm.hpp"
+#include "shs_internal.hpp"
+
+using shs_dev::DrawGPU;
+using shs_dev::FrameBuffers;
+using shs_dev::FrameParams;
+using shs_dev::TriRec;
+
+namespace {
+struct Mesh {
+    float *pos = nullptr;
+    float *nrm = nullptr;
+    int32_t n_tris = 0;
+    bool live = false;
+};
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;  // elements
+};
+}  // namespace
+
+struct shs_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::vector<Mesh> meshes;
+
+    DevBuf<DrawGPU> draws;
+    DevBuf<int32_t> draw_base;
+    DevBuf<TriRec> recs;
+    DevBuf<uint32_t> tile_count, tile_offset, tile_cursor;
+    DevBuf<uint32_t> list, ghost;
+    DevBuf<uint32_t> counters;
+    DevBuf<uint8_t> color;
+    DevBuf<float> depth;
+    DevBuf<float4> prequant;
+
+    // pinned staging for the per-frame draw table (2 slots, guarded by events)
+    DrawGPU *h_draws[2] = {nullptr, nullptr};
+    int32_t *h_base[2] = {nullptr, nullptr};
+    size_t h_cap = 0;
+    hipEvent_t slot_ev[2] = {nullptr, nullptr};
+    bool slot_used[2] = {false, false};
+    int slot = 0;
+    uint32_t *h_counters = nullptr;  // pinned, C_NCOUNTERS
+
+    // last frame (re-issued if a bin capacity overflowed)
+    shs_frame_desc frame{};
+    std::vector<shs_legacy_draw> last_draws;
+    bool have_frame = false;
+    bool need_check = false;
+    int last_n_tris = 0;
+    int last_n_tiles = 0;
+
+    bool timing = false;
+    hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    float last_ms[4] = {0, 0, 0, 0};
+};
+
+#define HIP_TRY(ctx, expr)                                                                       \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) {                                                                  \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                      \
+            return SHS_ERR_HIP;                                                                  \
+        }                                                                                        \
+    } while (0)
+
+template <typename T>
+static int ensure(shs_ctx *ctx, DevBuf<T> &b, size_t n) {
+    if (n <= b.cap && b.p) return SHS_OK;
+    size_t want = std::max<size_t>(n, 16);
+    if (b.p) {
+        // the old buffer may still be read by queued work on the stream
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&b.p), want * sizeof(T)));
+    b.cap = want;
+    return SHS_OK;
+}
+
+template <typename T>
+static void release(DevBuf<T> &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+}
+
+static int set_dev(shs_ctx *ctx) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return SHS_OK;
+}
+
+extern "C" {
+
+int shs_abi_version(void) { return 1; }
+
+int shs_create(int device, shs_ctx **out) {
+    if (!out) return SHS_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return SHS_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SHS_ERR_NO_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        std::fprintf(stderr, "shs_gpu: device %d is %s, this build targets gfx950 only\n", device, prop.gcnArchName);
+        return SHS_ERR_NO_DEVICE;
+    }
+    shs_ctx *ctx = new shs_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return SHS_ERR_HIP;
+    }
+    ctx->stream = ctx->own_stream;
+    for (int i = 0; i < 2; ++i)
+        if (hipEventCreateWithFlags(&ctx->slot_ev[i], hipEventDisableTiming) != hipSuccess) { delete ctx; return SHS_ERR_HIP; }
+    for (int i = 0; i < 5; ++i)
+        if (hipEventCreate(&ctx->tev[i]) != hipSuccess) { delete ctx; return SHS_ERR_HIP; }
+    if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_counters), shs_dev::C_NCOUNTERS * sizeof(uint32_t)) != hipSuccess) {
+        delete ctx;
+        return SHS_ERR_HIP;
+    }
+    std::memset(ctx->h_counters, 0, shs_dev::C_NCOUNTERS * sizeof(uint32_t));
+    if (ensure(ctx, ctx->counters, shs_dev::C_NCOUNTERS) != SHS_OK) { delete ctx; return SHS_ERR_HIP; }
+    *out = ctx;
+    return SHS_OK;
+}
+
+int shs_destroy(shs_ctx *ctx) {
+    if (!ctx) return SHS_ERR_INVALID;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto &m : ctx->meshes) {
+        if (m.pos) (void)hipFree(m.pos);
+        if (m.nrm) (void)hipFree(m.nrm);
+    }
+    release(ctx->draws); release(ctx->draw_base); release(ctx->recs);
+    release(ctx->tile_count); release(ctx->tile_offset); release(ctx->tile_cursor);
+    release(ctx->list); release(ctx->ghost); release(ctx->counters);
+    release(ctx->color); release(ctx->depth); release(ctx->prequant);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->h_draws[i]) (void)hipHostFree(ctx->h_draws[i]);
+        if (ctx->h_base[i]) (void)hipHostFree(ctx->h_base[i]);
+        if (ctx->slot_ev[i]) (void)hipEventDestroy(ctx->slot_ev[i]);
+    }
+    for (int i = 0; i < 5; ++i)
+        if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
+    if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return SHS_OK;
+}
+
+const char *shs_last_error(shs_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int shs_set_stream(shs_ctx *ctx, void *s) {
+    if (!ctx) return SHS_ERR_INVALID;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->stream = s ? reinterpret_cast<hipStream_t>(s) : ctx->own_stream;
+    return SHS_OK;
+}
+
+void *shs_get_stream(shs_ctx *ctx) { return ctx ? reinterpret_cast<void *>(ctx->stream) : nullptr; }
+
+int shs_mesh_upload_soup(shs_ctx *ctx, const float *positions, const float *normals, int32_t n_tris, int32_t *mesh_id) {
+    if (!ctx || !positions || !normals || n_tris <= 0 || !mesh_id) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    Mesh m;
+    const size_t bytes = (size_t)n_tris * 9 * sizeof(float);
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.pos), bytes));
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.nrm), bytes));
+    HIP_TRY(ctx, hipMemcpy(m.pos, positions, bytes, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(m.nrm, normals, bytes, hipMemcpyHostToDevice));
+    m.n_tris = n_tris;
+    m.live = true;
+    ctx->meshes.push_back(m);
+    *mesh_id = (int32_t)ctx->meshes.size() - 1;
+    return SHS_OK;
+}
+
+int shs_mesh_release(shs_ctx *ctx, int32_t id) {
+    if (!ctx || id < 0 || id >= (int32_t)ctx->meshes.size() || !ctx->meshes[id].live) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    Mesh &m = ctx->meshes[id];
+    HIP_TRY(ctx, hipFree(m.pos));
+    HIP_TRY(ctx, hipFree(m.nrm));
+    m = Mesh{};
+    return SHS_OK;
+}
+
+static void build_draw(const shs_legacy_draw &in, const Mesh &m, int32_t base, DrawGPU &o) {
+    std::memset(&o, 0, sizeof o);
+    o.pos = m.pos;
+    o.nrm = m.nrm;
+    o.tri_base = base;
+    o.n_tris = m.n_tris;
+    o.shading = in.shading;
+    std::memcpy(o.mvp, in.mvp, sizeof o.mvp);
+    std::memcpy(o.model, in.model, sizeof o.model);
+    using namespace shs_host;
+    if (in.shading == SHS_SHADING_FLAT) {
+        // flat_shading.cpp:54 normal = mat3(u.mv) * n ; FS :76 l = normalize(u.light_dir_view)
+        for (int c = 0; c < 3; ++c)
+            for (int r = 0; r < 3; ++r) o.nmat[c * 3 + r] = in.model[c * 4 + r];
+        const vec3 l = gnormalize(vec3{in.light_dir[0], in.light_dir[1], in.light_dir[2]});
+        o.light[0] = l.x; o.light[1] = l.y; o.light[2] = l.z;
+    } else {
+        // mat3(transpose(inverse(model))) and normalize(-light_dir): per-vertex / per-fragment in the
+        // reference, uniform across the draw, hence computed once here with the same operations
+        normal_matrix(in.model, o.nmat);
+        const vec3 l = gnormalize(gneg(vec3{in.light_dir[0], in.light_dir[1], in.light_dir[2]}));
+        o.light[0] = l.x; o.light[1] = l.y; o.light[2] = l.z;
+    }
+    o.cam[0] = in.camera_pos[0]; o.cam[1] = in.camera_pos[1]; o.cam[2] = in.camera_pos[2];
+    for (int i = 0; i < 3; ++i) {
+        o.ocol[i] = (float)in.color[i] / 255.0f;   // glm::vec3(r,g,b) / 255.0f
+        o.colf[i] = (float)in.color[i];            // int colour promoted in u.color.r * intensity
+    }
+}
+
+static int enqueue_frame(shs_ctx *ctx) {
+    const shs_frame_desc &f = ctx->frame;
+    const int n_draws = (int)ctx->last_draws.size();
+    const int tiles_x = (f.width + shs_dev::TILE - 1) / shs_dev::TILE;
+    const int tiles_y = (f.height + shs_dev::TILE - 1) / shs_dev::TILE;
+    const int n_tiles = tiles_x * tiles_y;
+    const size_t npx = (size_t)f.width * f.height;
+
+    int64_t total = 0;
+    for (const auto &d : ctx->last_draws) total += ctx->meshes[d.mesh_id].n_tris;
+    if (total > 0x3fffffff) { ctx->err = "too many triangles in one frame"; return SHS_ERR_INVALID; }
+    const int n_tris = (int)total;
+
+    if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1))) return SHS_ERR_HIP;
+    if (ensure(ctx, ctx->tile_count, n_tiles) || ensure(ctx, ctx->tile_offset, n_tiles) || ensure(ctx, ctx->tile_cursor, n_tiles))
+        return SHS_ERR_HIP;
+    if (!ctx->list.p && ensure(ctx, ctx->list, std::max<size_t>(1 << 16, (size_t)n_tris * 4))) return SHS_ERR_HIP;
+    if (!ctx->ghost.p && ensure(ctx, ctx->ghost, std::max<size_t>(1 << 12, (size_t)n_tris / 8))) return SHS_ERR_HIP;
+    if (ensure(ctx, ctx->color, npx * 4) || ensure(ctx, ctx->depth, npx)) return SHS_ERR_HIP;
+    const bool want_pq = (f.flags & SHS_FRAME_PREQUANT) != 0;
+    if (want_pq && ensure(ctx, ctx->prequant, npx)) return SHS_ERR_HIP;
+    if (ensure(ctx, ctx->draws, std::max(n_draws, 1)) || ensure(ctx, ctx->draw_base, std::max(n_draws, 1))) return SHS_ERR_HIP;
+
+    // pinned staging slot for the draw table
+    const int s = ctx->slot;
+    ctx->slot ^= 1;
+    if (ctx->slot_used[s]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[s]));
+    if ((size_t)n_draws > ctx->h_cap) {
+        for (int i = 0; i < 2; ++i) {
+            if (i != s && ctx->slot_used[i]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[i]));
+            if (ctx->h_draws[i]) HIP_TRY(ctx, hipHostFree(ctx->h_draws[i]));
+            if (ctx->h_base[i]) HIP_TRY(ctx, hipHostFree(ctx->h_base[i]));
+            ctx->h_draws[i] = nullptr;
+            ctx->h_base[i] = nullptr;
+        }
+        const size_t cap = std::max<size_t>(n_draws, 64);
+        for (int i = 0; i < 2; ++i) {
+            HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_draws[i]), cap * sizeof(DrawGPU)));
+            HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_base[i]), cap * sizeof(int32_t)));
+        }
+        ctx->h_cap = cap;
+    }
+    int32_t base = 0;
+    for (int i = 0; i < n_draws; ++i) {
+        const shs_legacy_draw &d = ctx->last_draws[i];
+        build_draw(d, ctx->meshes[d.mesh_id], base, ctx->h_draws[s][i]);
+        ctx->h_base[s][i] = base;
+        base += ctx->meshes[d.mesh_id].n_tris;
+    }
+
+    hipStream_t st = ctx->stream;
+    if (n_draws > 0) {
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->draws.p, ctx->h_draws[s], n_draws * sizeof(DrawGPU), hipMemcpyHostToDevice, st));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->draw_base.p, ctx->h_base[s], n_draws * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    }
+    HIP_TRY(ctx, hipEventRecord(ctx->slot_ev[s], st));
+    ctx->slot_used[s] = true;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->counters.p, 0, shs_dev::C_NCOUNTERS * sizeof(uint32_t), st));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->tile_count.p, 0, n_tiles * sizeof(uint32_t), st));
+
+    FrameParams fp;
+    fp.W = f.width; fp.H = f.height;
+    fp.rtw = f.ref_tile_w; fp.rth = f.ref_tile_h;
+    fp.rank = f.shard_rank; fp.count = f.shard_count;
+    fp.tiles_x = tiles_x; fp.tiles_y = tiles_y;
+    fp.n_tris = n_tris; fp.n_draws = n_draws;
+    fp.clear_rgba = (uint32_t)f.clear_color[0] | ((uint32_t)f.clear_color[1] << 8) | ((uint32_t)f.clear_color[2] << 16) |
+                    ((uint32_t)f.clear_color[3] << 24);
+    fp.flags = f.flags;
+    fp.list_capacity = (uint32_t)std::min<size_t>(ctx->list.cap, 0xffffffffu);
+    fp.ghost_capacity = (uint32_t)std::min<size_t>(ctx->ghost.cap, 0xffffffffu);
+
+    FrameBuffers fb;
+    fb.draws = ctx->draws.p; fb.draw_base = ctx->draw_base.p; fb.recs = ctx->recs.p;
+    fb.tile_count = ctx->tile_count.p; fb.tile_offset = ctx->tile_offset.p; fb.tile_cursor = ctx->tile_cursor.p;
+    fb.tile_list = ctx->list.p; fb.ghost_list = ctx->ghost.p; fb.counters = ctx->counters.p;
+    fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;
+
+    const int owned = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[0], st));
+    HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, st));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[1], st));
+    HIP_TRY(ctx, shs_internal::launch_scan(fp, fb, n_tiles, st));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[2], st));
+    HIP_TRY(ctx, shs_internal::launch_scatter(fp, fb, st));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[3], st));
+    HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, owned, st));
+    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[4], st));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->counters.p, shs_dev::C_NCOUNTERS * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    ctx->have_frame = true;
+    ctx->need_check = true;
+    ctx->last_n_tris = n_tris;
+    ctx->last_n_tiles = n_tiles;
+    return SHS_OK;
+}
+
+// Wait for the frame; if a bin capacity overflowed, grow it and re-issue the frame.
+static int finish_frame(shs_ctx *ctx) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (!ctx->need_check) return SHS_OK;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        const uint32_t ov = ctx->h_counters[shs_dev::C_OVERFLOW];
+        if (!ov) break;
+        if (ov & 1u) {
+            const size_t need = (size_t)ctx->h_counters[shs_dev::C_BINS];
+            release(ctx->list);
+            if (ensure(ctx, ctx->list, need + need / 4 + 1024)) return SHS_ERR_HIP;
+        }
+        if (ov & 2u) {
+            const size_t need = (size_t)ctx->h_counters[shs_dev::C_GHOST];
+            release(ctx->ghost);
+            if (ensure(ctx, ctx->ghost, need + need / 4 + 1024)) return SHS_ERR_HIP;
+        }
+        int rc = enqueue_frame(ctx);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    if (ctx->h_counters[shs_dev::C_OVERFLOW]) { ctx->err = "bin capacity overflow persisted"; return SHS_ERR_OVERFLOW; }
+    if (ctx->timing) {
+        for (int i = 0; i < 4; ++i) HIP_TRY(ctx, hipEventElapsedTime(&ctx->last_ms[i], ctx->tev[i], ctx->tev[i + 1]));
+    }
+    ctx->need_check = false;
+    return SHS_OK;
+}
+
+int shs_render_legacy(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws) {
+    if (!ctx || !frame || n_draws < 0 || (n_draws > 0 && !draws)) return SHS_ERR_INVALID;
+    const shs_frame_desc &f = *frame;
+    if (f.width <= 0 || f.height <= 0 || f.width > 16384 || f.height > 16384) { ctx->err = "bad frame size"; return SHS_ERR_INVALID; }
+    if (f.ref_tile_w <= 0 || f.ref_tile_h <= 0) { ctx->err = "bad reference tile size"; return SHS_ERR_INVALID; }
+    if (f.shard_count <= 0 || f.shard_rank < 0 || f.shard_rank >= f.shard_count) { ctx->err = "bad shard"; return SHS_ERR_INVALID; }
+    for (int i = 0; i < n_draws; ++i) {
+        const int id = draws[i].mesh_id;
+        if (id < 0 || id >= (int)ctx->meshes.size() || !ctx->meshes[id].live) { ctx->err = "bad mesh id"; return SHS_ERR_INVALID; }
+        if (draws[i].shading < SHS_SHADING_FLAT || draws[i].shading > SHS_SHADING_BLINN_PHONG) {
+            ctx->err = "bad shading model";
+            return SHS_ERR_INVALID;
+        }
+    }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    // No host sync here: a still-pending previous frame is superseded by this one (it rewrites every
+    // pixel); only the newest frame's overflow flags are checked (and the frame re-issued) when the
+    // caller synchronises / resolves.
+    ctx->frame = f;
+    ctx->last_draws.assign(draws, draws + n_draws);
+    return enqueue_frame(ctx);
+}
+
+int shs_synchronize(shs_ctx *ctx) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    return finish_frame(ctx);
+}
+
+int shs_resolve(shs_ctx *ctx, uint8_t *color, float *depth) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (!ctx->have_frame) { ctx->err = "no frame rendered"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    const size_t npx = (size_t)ctx->frame.width * ctx->frame.height;
+    if (color) HIP_TRY(ctx, hipMemcpy(color, ctx->color.p, npx * 4, hipMemcpyDeviceToHost));
+    if (depth) HIP_TRY(ctx, hipMemcpy(depth, ctx->depth.p, npx * sizeof(float), hipMemcpyDeviceToHost));
+    return SHS_OK;
+}
+
+int shs_resolve_prequant(shs_ctx *ctx, float *pq) {
+    if (!ctx || !pq) return SHS_ERR_INVALID;
+    if (!ctx->have_frame || !(ctx->frame.flags & SHS_FRAME_PREQUANT)) { ctx->err = "frame has no prequant buffer"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    const size_t npx = (size_t)ctx->frame.width * ctx->frame.height;
+    HIP_TRY(ctx, hipMemcpy(pq, ctx->prequant.p, npx * sizeof(float4), hipMemcpyDeviceToHost));
+    return SHS_OK;
+}
+
+int shs_device_framebuffers(shs_ctx *ctx, void **color_dev, void **depth_dev) {
+    if (!ctx || !ctx->have_frame) return SHS_ERR_INVALID;
+    if (color_dev) *color_dev = ctx->color.p;
+    if (depth_dev) *depth_dev = ctx->depth.p;
+    return SHS_OK;
+}
+
+int shs_get_stats(shs_ctx *ctx, shs_raster_stats *st) {
+    if (!ctx || !st || !ctx->have_frame) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    st->tri_input = (uint64_t)ctx->last_n_tris;
+    st->tri_setup = ctx->h_counters[shs_dev::C_SETUP];
+    st->tri_ghost = ctx->h_counters[shs_dev::C_GHOST];
+    st->bin_entries = ctx->h_counters[shs_dev::C_BINS];
+    st->covered_pixels = ctx->h_counters[shs_dev::C_COVERED];
+    return SHS_OK;
+}
+
+int shs_enable_timing(shs_ctx *ctx, int enable) {
+    if (!ctx) return SHS_ERR_INVALID;
+    ctx->timing = enable != 0;
+    return SHS_OK;
+}
+
+int shs_last_kernel_ms(shs_ctx *ctx, float *ms4) {
+    if (!ctx || !ms4) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    std::memcpy(ms4, ctx->last_ms, sizeof ctx->last_ms);
+    return SHS_OK;
+}
+
+int shs_camera3d(const float position[3], float ha, float va, float fov, float zn, float zf, float view16[16], float proj16[16]) {
+    if (!position || !view16 || !proj16) return SHS_ERR_INVALID;
+    shs_host::camera3d(shs_host::vec3{position[0], position[1], position[2]}, ha, va, fov, zn, zf, view16, proj16);
+    return SHS_OK;
+}
+
+int shs_model_trs(const float position[3], float rot_deg_y, const float scl[3], float out16[16]) {
+    if (!position || !scl || !out16) return SHS_ERR_INVALID;
+    shs_host::model_trs(shs_host::vec3{position[0], position[1], position[2]}, rot_deg_y,
+                        shs_host::vec3{scl[0], scl[1], scl[2]}, out16);
+    return SHS_OK;
+}
+
+int shs_mat4_mul(const float a[16], const float b[16], float out[16]) {
+    if (!a || !b || !out) return SHS_ERR_INVALID;
+    shs_host::mul(a, b, out);
+    return SHS_OK;
+}
+
+}  // extern "C"

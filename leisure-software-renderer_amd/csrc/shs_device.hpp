@@ -1,0 +1,121 @@
+// shs_device.hpp -- device data layout and the bit-exact per-pixel arithmetic of the legacy
+// shs_renderer path, shared by the setup / raster kernels (shs_legacy.hip).
+//
+// Every floating-point expression here restates a reference line operation for operation; the
+// kernels are compiled with -ffp-contract=off and correctly rounded f32 divide/sqrt, so each
+// operation rounds exactly as the reference's x86-64 SSE build (-O3, no FMA) does.
+// Paths are relative to /root/reference/cpp-folders/src/.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace shs_dev {
+
+// ---- HBM layouts -------------------------------------------------------------------------
+// Per-draw uniform block (one entry per object of the scene loop, blinn_phong_shading.cpp:272-282).
+struct alignas(16) DrawGPU {
+    const float *pos;        // mesh soup positions, 9 floats per triangle
+    const float *nrm;        // mesh soup normals
+    int32_t tri_base;        // global index of this draw's first triangle (submission order)
+    int32_t n_tris;
+    int32_t shading;         // SHS_SHADING_*
+    int32_t pad0;
+    float mvp[16];           // Uniforms::mvp
+    float model[16];         // Uniforms::model (Flat: Uniforms::mv)
+    float nmat[12];          // mat3(transpose(inverse(model))) (Flat: mat3(mv)), col-major, 9 used
+    float light[4];          // normalize(-light_dir) (Flat: normalize(light_dir_view))
+    float cam[4];            // Uniforms::camera_pos
+    float ocol[4];           // vec3(color.rgb) / 255.0f
+    float colf[4];           // (float)color.rgb (Flat FS multiplies the int colour)
+};
+
+// Per-triangle raster record written by k_setup, 96 B (6 x float4), read by k_raster through LDS.
+// Holds exactly the per-triangle quantities of Canvas::barycentric_coordinate
+// (shs_renderer.hpp:802-821) that do not depend on the pixel, plus the NDC z of the corners.
+struct alignas(16) TriRec {
+    float ax, ay, v0x, v0y;          // A, v0 = B - A
+    float v1x, v1y, d00, d01;        // v1 = C - A, d00 = v0.v0, d01 = v0.v1
+    float d11, denom, z0, z1;        // d11 = v1.v1, denom = d00*d11 - d01*d01, screen z
+    float z2;
+    uint32_t flags;                  // TRI_CULLED | TRI_GHOST
+    int32_t draw;                    // index into the draw table
+    int32_t local;                   // triangle index inside the draw's mesh
+    int32_t ix0, ix1, iy0, iy1;      // integer bbox [floor(min), floor(max)] clamped to the screen
+    float fminx, fmaxx, fminy, fmaxy;// float bbox of the screen-space corners
+};
+static_assert(sizeof(TriRec) == 96, "TriRec must stay 96 B");
+
+constexpr uint32_t TRI_CULLED = 1u;
+constexpr uint32_t TRI_GHOST = 2u;
+
+constexpr int TILE = 32;             // GPU screen tile (32x32 px, one 256-thread workgroup)
+constexpr int CHUNK = 256;           // triangle records staged in LDS per pass
+
+// counters[] slots
+constexpr int C_GHOST = 0, C_SETUP = 1, C_BINS = 2, C_OVERFLOW = 3, C_COVERED = 4, C_NCOUNTERS = 8;
+
+struct FrameParams {
+    int32_t W, H;
+    int32_t rtw, rth;                // reference tile-job size (80x80)
+    int32_t rank, count;             // shard ownership of GPU tiles
+    int32_t tiles_x, tiles_y;
+    int32_t n_tris, n_draws;
+    uint32_t clear_rgba;
+    uint32_t flags;
+    uint32_t list_capacity;
+    uint32_t ghost_capacity;
+};
+
+struct FrameBuffers {
+    const DrawGPU *draws;
+    const int32_t *draw_base;        // n_draws entries, ascending tri_base
+    TriRec *recs;
+    uint32_t *tile_count;            // n_tiles
+    uint32_t *tile_offset;           // n_tiles
+    uint32_t *tile_cursor;           // n_tiles
+    uint32_t *tile_list;             // list_capacity
+    uint32_t *ghost_list;            // ghost_capacity
+    uint32_t *counters;              // C_NCOUNTERS
+    uint8_t *color;                  // W*H*4, canvas rows
+    float *depth;                    // W*H, screen rows
+    float4 *prequant;                // W*H (optional)
+};
+
+// ---- GLM scalar semantics (glm/detail/func_common.inl) -------------------------------------
+__device__ __forceinline__ float g_min(float x, float y) { return (y < x) ? y : x; }
+__device__ __forceinline__ float g_max(float x, float y) { return (x < y) ? y : x; }
+__device__ __forceinline__ float g_clamp01(float x) { return g_min(g_max(x, 0.0f), 1.0f); }
+
+struct f3 { float x, y, z; };
+__device__ __forceinline__ float dot3(f3 a, f3 b) { float x = a.x * b.x, y = a.y * b.y, z = a.z * b.z; return (x + y) + z; }
+__device__ __forceinline__ f3 sc3(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 add3(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 sub3(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 normalize3(f3 v) { float inv = 1.0f / sqrtf(dot3(v, v)); return sc3(v, inv); }
+
+// glm mat4*vec4 with w = 1: (m0*x + m1*y) + (m2*z + m3*1)
+__device__ __forceinline__ void m4p(const float *m, float x, float y, float z, float &ox, float &oy, float &oz, float &ow) {
+    ox = (m[0] * x + m[4] * y) + (m[8] * z + m[12] * 1.0f);
+    oy = (m[1] * x + m[5] * y) + (m[9] * z + m[13] * 1.0f);
+    oz = (m[2] * x + m[6] * y) + (m[10] * z + m[14] * 1.0f);
+    ow = (m[3] * x + m[7] * y) + (m[11] * z + m[15] * 1.0f);
+}
+// glm mat3*vec3: left to right
+__device__ __forceinline__ f3 m3v(const float *m, f3 v) {
+    return {m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z, m[2] * v.x + m[5] * v.y + m[8] * v.z};
+}
+
+// Canvas::barycentric_coordinate body after the per-triangle part (shs_renderer.hpp:809-820);
+// the |denom| < 1e-5 early-out is per triangle and culled in k_setup.
+__device__ __forceinline__ void bary(const TriRec &r, float Px, float Py, float &u, float &v, float &w) {
+    const float vpx = Px - r.ax, vpy = Py - r.ay;
+    const float t0 = vpx * r.v0x, t1 = vpy * r.v0y;
+    const float d20 = t0 + t1;
+    const float t2 = vpx * r.v1x, t3 = vpy * r.v1y;
+    const float d21 = t2 + t3;
+    v = (r.d11 * d20 - r.d01 * d21) / r.denom;
+    w = (r.d00 * d21 - r.d01 * d20) / r.denom;
+    u = (1.0f - v) - w;
+}
+
+}  // namespace shs_dev

@@ -1,0 +1,186 @@
+"""shs_gpu -- Python mirror of the shs_renderer legacy draw-call API over libshs_gpu.so.
+
+The reference drives its hot path from C++ (`RendererSystem::process` -> `draw_triangle_tile`,
+cpp-folders/src/hello-3d-primitives/hello_pipeline_blinn_phong_shading.cpp:244-313).  This module
+is the thin host layer the tests and bench use: it owns a context (`shs_create`), uploads meshes
+once (`shs_mesh_upload_soup`, the ModelGeometry soup), enqueues frames (`shs_render_legacy`) and
+resolves framebuffers into the reference layouts (`shs_resolve`).  Every call goes through the C ABI
+into the gfx950 kernels; there is no CPU path here.
+"""
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _abi
+from ._abi import (FRAME_PREQUANT, SHADING_BLINN_PHONG, SHADING_FLAT, SHADING_GOURAUD, SHADING_NAMES,
+                   SHADING_PHONG, FrameDesc, LegacyDraw, RasterStats)
+
+__all__ = [
+    "ShsError", "Context", "Frame", "Draw", "SHADING_FLAT", "SHADING_GOURAUD", "SHADING_PHONG",
+    "SHADING_BLINN_PHONG", "SHADING_NAMES", "FRAME_PREQUANT", "lib",
+]
+
+lib = _abi.lib
+
+
+class ShsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"shs_gpu error {code}: {msg}")
+        self.code = code
+
+
+def _fptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+@dataclass
+class Draw:
+    """One object of the legacy scene loop: the reference's `Uniforms` + mesh + shading model."""
+    mesh: object                 # Mesh (positions/normals float32 [n,9]) or an uploaded mesh id
+    shading: int
+    mvp: np.ndarray              # float32[16], column-major (glm::mat4 storage)
+    model: np.ndarray            # float32[16] (Flat: Uniforms::mv)
+    light_dir: np.ndarray        # float32[3]  (Flat: light_dir_view)
+    camera_pos: np.ndarray       # float32[3]
+    color: tuple = (60, 100, 200, 255)
+
+
+@dataclass
+class Frame:
+    width: int
+    height: int
+    ref_tile: tuple = (80, 80)   # TILE_SIZE_X/Y of the legacy pipelines
+    shard_rank: int = 0
+    shard_count: int = 1
+    clear_color: tuple = (0, 0, 0, 255)
+    prequant: bool = False
+
+    def desc(self) -> FrameDesc:
+        d = FrameDesc()
+        d.width, d.height = self.width, self.height
+        d.ref_tile_w, d.ref_tile_h = self.ref_tile
+        d.shard_rank, d.shard_count = self.shard_rank, self.shard_count
+        d.flags = FRAME_PREQUANT if self.prequant else 0
+        for i in range(4):
+            d.clear_color[i] = self.clear_color[i]
+        return d
+
+
+class Context:
+    """A libshs_gpu context bound to one HIP device (one host thread at a time)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = lib()
+        h = ctypes.c_void_p()
+        rc = self._lib.shs_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise ShsError(rc, f"shs_create(device={device}) failed (no gfx950 device?)")
+        self._h = h
+        self._meshes = {}
+        self._frame = None
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ShsError(rc, self._lib.shs_last_error(self._h).decode(errors="replace"))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.shs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- geometry -----------------------------------------------------------------------------
+    def upload_mesh(self, mesh) -> int:
+        key = id(mesh)
+        if key in self._meshes:
+            return self._meshes[key][0]
+        pos = np.ascontiguousarray(mesh.positions, dtype=np.float32)
+        nrm = np.ascontiguousarray(mesh.normals, dtype=np.float32)
+        assert pos.shape == nrm.shape and pos.shape[-1] == 9
+        mid = ctypes.c_int32()
+        self._check(self._lib.shs_mesh_upload_soup(self._h, _fptr(pos), _fptr(nrm), pos.shape[0], ctypes.byref(mid)))
+        self._meshes[key] = (mid.value, mesh)
+        return mid.value
+
+    # -- frames -------------------------------------------------------------------------------
+    def _draw_array(self, draws):
+        arr = (LegacyDraw * max(len(draws), 1))()
+        for i, d in enumerate(draws):
+            a = arr[i]
+            a.mesh_id = d.mesh if isinstance(d.mesh, int) else self.upload_mesh(d.mesh)
+            a.shading = int(d.shading)
+            for k in range(16):
+                a.mvp[k] = float(d.mvp[k])
+                a.model[k] = float(d.model[k])
+            for k in range(3):
+                a.light_dir[k] = float(d.light_dir[k])
+                a.camera_pos[k] = float(d.camera_pos[k])
+            for k in range(4):
+                a.color[k] = int(d.color[k])
+        return arr
+
+    def prepare(self, frame: Frame, draws):
+        """Build the ctypes frame/draw arrays once (re-used by render_prepared in timed loops)."""
+        return frame, frame.desc(), self._draw_array(draws), len(draws)
+
+    def render_prepared(self, prepared):
+        frame, desc, arr, n = prepared
+        self._check(self._lib.shs_render_legacy(self._h, ctypes.byref(desc), arr, n))
+        self._frame = frame
+
+    def render(self, frame: Frame, draws):
+        self.render_prepared(self.prepare(frame, draws))
+
+    def synchronize(self):
+        self._check(self._lib.shs_synchronize(self._h))
+
+    def resolve(self):
+        f = self._frame
+        color = np.empty((f.height, f.width, 4), dtype=np.uint8)
+        depth = np.empty((f.height, f.width), dtype=np.float32)
+        self._check(self._lib.shs_resolve(self._h, color.ctypes.data_as(ctypes.c_void_p),
+                                          depth.ctypes.data_as(ctypes.c_void_p)))
+        return color, depth
+
+    def resolve_prequant(self):
+        f = self._frame
+        pq = np.empty((f.height, f.width, 4), dtype=np.float32)
+        self._check(self._lib.shs_resolve_prequant(self._h, pq.ctypes.data_as(ctypes.c_void_p)))
+        return pq
+
+    def device_framebuffers(self):
+        c, d = ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(self._lib.shs_device_framebuffers(self._h, ctypes.byref(c), ctypes.byref(d)))
+        return c.value, d.value
+
+    def stats(self) -> dict:
+        s = RasterStats()
+        self._check(self._lib.shs_get_stats(self._h, ctypes.byref(s)))
+        return {k: int(getattr(s, k)) for k, _ in RasterStats._fields_}
+
+    def enable_timing(self, on=True):
+        self._check(self._lib.shs_enable_timing(self._h, 1 if on else 0))
+
+    def kernel_ms(self):
+        ms = (ctypes.c_float * 4)()
+        self._check(self._lib.shs_last_kernel_ms(self._h, ms))
+        return {"setup": ms[0], "scan": ms[1], "scatter": ms[2], "raster": ms[3]}
+
+    def set_stream(self, hip_stream):
+        self._check(self._lib.shs_set_stream(self._h, ctypes.c_void_p(hip_stream)))
+
+    @property
+    def stream(self):
+        return self._lib.shs_get_stream(self._h)

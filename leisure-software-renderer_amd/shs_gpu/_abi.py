@@ -1,0 +1,108 @@
+"""ctypes declarations of include/shs_gpu.h (libshs_gpu.so, built in-tree for gfx950).
+
+The product path: every call goes through the C ABI into the HIP kernels.  There is no CPU
+fallback -- if the shared library is missing or fails to load, importing this module raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libshs_gpu.so")
+
+SHS_OK = 0
+SHS_ERR_INVALID = -1
+SHS_ERR_HIP = -2
+SHS_ERR_NO_DEVICE = -3
+SHS_ERR_OVERFLOW = -4
+
+SHADING_FLAT = 0
+SHADING_GOURAUD = 1
+SHADING_PHONG = 2
+SHADING_BLINN_PHONG = 3
+SHADING_NAMES = {"flat": 0, "gouraud": 1, "phong": 2, "blinn_phong": 3}
+
+FRAME_PREQUANT = 1
+
+
+class LegacyDraw(ctypes.Structure):
+    _fields_ = [
+        ("mesh_id", ctypes.c_int32),
+        ("shading", ctypes.c_int32),
+        ("mvp", ctypes.c_float * 16),
+        ("model", ctypes.c_float * 16),
+        ("light_dir", ctypes.c_float * 3),
+        ("camera_pos", ctypes.c_float * 3),
+        ("color", ctypes.c_uint8 * 4),
+    ]
+
+
+class FrameDesc(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("ref_tile_w", ctypes.c_int32),
+        ("ref_tile_h", ctypes.c_int32),
+        ("shard_rank", ctypes.c_int32),
+        ("shard_count", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("clear_color", ctypes.c_uint8 * 4),
+    ]
+
+
+class RasterStats(ctypes.Structure):
+    _fields_ = [
+        ("tri_input", ctypes.c_uint64),
+        ("tri_setup", ctypes.c_uint64),
+        ("tri_ghost", ctypes.c_uint64),
+        ("bin_entries", ctypes.c_uint64),
+        ("covered_pixels", ctypes.c_uint64),
+    ]
+
+
+# (name, restype, argtypes) for every symbol include/shs_gpu.h declares.
+_P = ctypes.c_void_p
+_F = ctypes.POINTER(ctypes.c_float)
+SIGNATURES = [
+    ("shs_abi_version", ctypes.c_int, []),
+    ("shs_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
+    ("shs_destroy", ctypes.c_int, [_P]),
+    ("shs_last_error", ctypes.c_char_p, [_P]),
+    ("shs_set_stream", ctypes.c_int, [_P, _P]),
+    ("shs_get_stream", _P, [_P]),
+    ("shs_synchronize", ctypes.c_int, [_P]),
+    ("shs_mesh_upload_soup", ctypes.c_int, [_P, _F, _F, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    ("shs_mesh_release", ctypes.c_int, [_P, ctypes.c_int32]),
+    ("shs_render_legacy", ctypes.c_int, [_P, ctypes.POINTER(FrameDesc), ctypes.POINTER(LegacyDraw), ctypes.c_int32]),
+    ("shs_resolve", ctypes.c_int, [_P, _P, _P]),
+    ("shs_resolve_prequant", ctypes.c_int, [_P, _P]),
+    ("shs_device_framebuffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    ("shs_get_stats", ctypes.c_int, [_P, ctypes.POINTER(RasterStats)]),
+    ("shs_enable_timing", ctypes.c_int, [_P, ctypes.c_int]),
+    ("shs_last_kernel_ms", ctypes.c_int, [_P, _F]),
+    ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),
+    ("shs_model_trs", ctypes.c_int, [_F, ctypes.c_float, _F, _F]),
+    ("shs_mat4_mul", ctypes.c_int, [_F, _F, _F]),
+]
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libshs_gpu.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback for the raster path)")
+    lib = ctypes.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        _LIB = load()
+    return _LIB

@@ -1,0 +1,30 @@
+"""Shared test helpers: parity assertions between the HIP path and the oracle."""
+import numpy as np
+
+FLT_MAX = np.finfo(np.float32).max
+TOL = 1e-5  # per-channel tolerance on shaded floats in [0,1] (BASELINE.json north_star)
+
+
+def assert_depth_bitexact(gpu_d, ref_d):
+    g = gpu_d.view(np.uint32)
+    r = ref_d.view(np.uint32)
+    bad = np.argwhere(g != r)
+    assert bad.size == 0, f"{len(bad)} depth words differ, first at {bad[:5].tolist()}: gpu={gpu_d[tuple(bad[0])]!r} ref={ref_d[tuple(bad[0])]!r}"
+
+
+def assert_color_parity(gpu_c, ref_c, gpu_pq=None, ref_pq=None):
+    """Coverage (alpha + which pixels were written) must match exactly.  A shaded byte may differ only
+    by 1 and only where both shaders' pre-truncation floats agree within TOL*255 -- i.e. a uint8
+    truncation boundary split by an ulp-level libm difference (powf)."""
+    assert np.array_equal(gpu_c[..., 3], ref_c[..., 3])
+    diff = gpu_c != ref_c
+    n = int(diff.sum())
+    if n == 0:
+        return 0
+    assert gpu_pq is not None and ref_pq is not None, f"{n} colour bytes differ and no prequant to explain them"
+    idx = np.argwhere(diff)
+    d8 = np.abs(gpu_c.astype(np.int16) - ref_c.astype(np.int16))[diff]
+    assert d8.max() <= 1, f"colour byte differs by {d8.max()}"
+    dp = np.abs(gpu_pq[..., :3] - ref_pq[..., :3])[diff[..., :3]] if diff[..., :3].any() else np.zeros(0)
+    assert (dp <= TOL * 255.0).all(), f"pre-truncation floats differ by {dp.max()} (> {TOL * 255})"
+    return n
