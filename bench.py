@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""bench.py -- Mtri/s + shaded Mpix/s of the shs_renderer legacy hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): Suzanne (monkey.rawobj, 967 triangles) Blinn-Phong +
+z-buffer at 1920x1080, the reference scene of hello_pipeline_blinn_phong_shading.cpp:152-153 and
+its Viewer((0,5,-20)) camera.  One step = one full frame through the HIP path: clear, vertex
+transform, setup, tile binning, coverage + z resolve, Blinn-Phong shading of the visible pixels and
+the colour (RGBA8 canvas rows) + depth (f32 screen rows) write.  Inputs (mesh, per-frame uniform
+table) are resident in HBM / pinned host memory before the timed region; the per-frame uniform
+upload is inside it.
+
+N > 1 (torchrun, one process per GPU): frame-parallel -- every rank renders its own frame of the
+same workload (camera yaw offset per rank), no data-path collective; "scaling": "weak".
+
+Also reported (rank 0, N = 1):
+  roofline      dominant kernel (k_raster): SURVEY.md 8(d) algorithmic bytes per frame
+                (N_tri*72 + W*H*8) / its mean HIP-event duration over the timed region, against
+                8 TB/s; "traffic" = HBM bytes per k_raster dispatch from rocprofv3 PMC counters
+                (FETCH_SIZE x2 [gfx950 half-count correction] + WRITE_SIZE, KiB units), collected in
+                separate child passes before this process touches the GPU.
+  cpu_baseline  the oracle (CPU restatement of the reference's 80x80 tile-job path, gcc -O3) timed
+                on this host's cores on a bounded sample of the same frames.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "leisure-software-renderer_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "Mtri/s + shaded Mpix/s at 1920×1080 Blinn-Phong; 1/2/4/8 MI355X scaling"
+HBM_PEAK_GBS = 8000.0
+WORKLOADS = {
+    "c2": "C2: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 1920x1080, 1 frame per step",
+    "c1": "C1: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 800x600, 1 frame per step",
+    "c3": "C3: 64-instance Suzanne grid, Phong, 1920x1080, 1 frame per step",
+}
+
+
+def algorithmic_bytes(frame, draws):
+    """every input read once (fp32 soup: 3 x (pos 12 + normal 12) = 72 B/tri) and
+    every output written once (RGBA8 4 B + f32 depth 4 B per pixel), clears fused."""
+    n_tri = sum(d.mesh.n_tris for d in draws)
+    return n_tri * 72 + frame.width * frame.height * 8, n_tri
+
+
+def build_workload(name, rank=0):
+    from shs_gpu import scene
+    # frame-parallel ranks render different frames: the camera yaw advances 3 degrees per rank
+    return scene.config(name, yaw=3.0 * rank)
+
+
+def run_gpu(args, rank, local_rank, world, dist):
+    import shs_gpu
+    frame, draws = build_workload(args.config, rank)
+    ctx = shs_gpu.Context(local_rank)
+    prepared = ctx.prepare(frame, draws)
+    for _ in range(max(args.warmup, 1)):
+        ctx.render_prepared(prepared)
+    ctx.synchronize()
+    stats = ctx.stats()
+
+    def barrier_sync():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    ctx.enable_timing(True)
+    ctx.timing_reset()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.render_prepared(prepared)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    n_frames, kms = ctx.timing_read()
+    ctx.enable_timing(False)
+    ctx.close()
+    return frame, draws, stats, elapsed, n_frames, kms
+
+
+def collect_pmc(args):
+    """rocprofv3 --pmc child passes (one counter per pass: FETCH_SIZE costs 3 TCC slots and
+    WRITE_SIZE 2, they do not fit together).  Returns bytes per k_raster dispatch or None."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="shs_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+                   sys.executable, os.path.abspath(__file__), "--child", "--config", args.config,
+                   "--steps", "20", "--warmup", "3"]
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=300, text=True)
+            if r.returncode != 0:
+                return None, f"rocprofv3 {counter} rc={r.returncode}: {r.stdout[-400:]}"
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if not files:
+                return None, f"no counter_collection.csv for {counter}"
+            vals = []
+            for f in files:
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if "k_raster" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                            vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None, f"no k_raster rows for {counter}"
+            vals = vals[3:] if len(vals) > 6 else vals   # drop warmup dispatches
+            out[counter] = sum(vals) / len(vals)
+    except Exception as e:  # the measurement is optional; never fail the bench line over it
+        return None, f"pmc failed: {e!r}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    # gfx950: FETCH_SIZE counts half the bytes of a wide coalesced read (MI355X_MICROARCH.md HBM);
+    # WRITE_SIZE is exact for 16-B-per-lane stores (k_raster's colour/depth stores); unit KiB.
+    traffic = (2.0 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024.0
+    return {"fetch_kib": out["FETCH_SIZE"], "write_kib": out["WRITE_SIZE"], "bytes": traffic}, None
+
+
+def cpu_baseline(args):
+    """The oracle (CPU restatement of the reference tile-job path) on this host, bounded sample."""
+    from oracle import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    frame, draws = build_workload(args.config, 0)
+    n_tri = sum(d.mesh.n_tris for d in draws)
+    oracle.render_legacy(frame.width, frame.height, draws, threads=threads)  # warm
+    frames = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.render_legacy(frame.width, frame.height, draws, threads=threads)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or frames >= 100000:
+            break
+    return {"value": round(n_tri * frames / el / 1e6, 4), "unit": "Mtri/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} frames of the same workload ({frame.width}x{frame.height}, {n_tri} tris), "
+                      f"{el:.1f} s wall, 80x80 tile jobs on {threads} threads (oracle/shs_oracle.c, gcc -O3)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    if args.child:  # profiled child: just render
+        run_gpu(args, 0, 0, 1, None)
+        return
+
+    pmc, pmc_err = (None, "skipped")
+    if world == 1 and not args.no_pmc:
+        pmc, pmc_err = collect_pmc(args)   # before this process initialises the GPU
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local_rank)
+        dist_mod.init_process_group("nccl")
+        dist = dist_mod
+
+    frame, draws, stats, elapsed, n_frames, kms = run_gpu(args, rank, local_rank, world, dist)
+    B, n_tri = algorithmic_bytes(frame, draws)
+
+    el_max = elapsed
+    covered = stats["covered_pixels"]
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t.item())
+        c = torch.tensor([covered], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        covered_total = float(c.item())
+    else:
+        covered_total = float(covered)
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    steps = args.steps
+    value = world * n_tri * steps / el_max / 1e6
+    mpix = covered_total * steps / el_max / 1e6
+    t_raster_ms = kms["raster"]
+    achieved = B / (t_raster_ms * 1e-3) / 1e9 if t_raster_ms > 0 else None
+    roofline = {
+        "kernel": "k_raster",
+        "bound": "hbm",
+        "achieved": round(achieved, 2) if achieved else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "traffic": round(pmc["bytes"]) if pmc else None,
+        "algorithmic_bytes": B,
+        "kernel_ms": round(t_raster_ms, 5),
+    }
+    if pmc is None:
+        roofline["traffic_note"] = pmc_err
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mtri/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el_max / steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: Suzanne soup from the reference's assets/obj/monkey/monkey.rawobj (967 tris), "
+                "reference scene constants (camera (0,5,-20) fov60, light, colour)",
+        "config": {"workload": WORKLOADS[args.config], "width": frame.width, "height": frame.height,
+                   "tris_per_frame": n_tri, "frames_per_step_per_gpu": 1,
+                   "parallelism": f"frame-parallel x{world}" if world > 1 else "single GPU"},
+        "shaded_mpix_s": round(mpix, 3),
+        "frame_stats": stats,
+        "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
+        "timed_frames_with_events": n_frames,
+        "roofline": roofline,
+    }
+    if world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

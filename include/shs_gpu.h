@@ -57,7 +57,8 @@ typedef struct shs_legacy_draw {
 /* Per-frame description.  ref_tile_w/h are the reference's tile-job size (TILE_SIZE_X/Y = 80,
  * blinn_phong_shading.cpp:29-30): the legacy raster clamps each triangle's bounding box to the
  * tile that runs it, and the GPU path reproduces that visited-pixel set exactly.
- * shard_rank/shard_count select the 32x32 GPU tiles this device owns (tile % count == rank);
+ * shard_rank/shard_count select the GPU tiles (shs_gpu_tile_size() px square, row-major) this
+ * device owns (tile % count == rank);
  * (0,1) renders the whole frame. */
 typedef struct shs_frame_desc {
     int32_t width, height;
@@ -72,9 +73,12 @@ typedef struct shs_frame_desc {
 typedef struct shs_raster_stats {
     uint64_t tri_input;           /* triangles submitted (rasterizer.hpp:208 tri_input)        */
     uint64_t tri_setup;           /* triangles surviving setup culls (area<=0, |denom|<1e-5)   */
-    uint64_t tri_ghost;           /* triangles needing the exact tile-clamp ("ghost") pass     */
+    uint64_t tri_ghost;           /* slivers whose tile-clamp pixels near the bbox are tested   */
     uint64_t bin_entries;         /* (tile, triangle) pairs binned                              */
     uint64_t covered_pixels;      /* final pixels with depth != clear (shaded Mpix/s numerator) */
+    uint64_t tri_ghost_unbounded; /* ... with no error bound: tested by every tile             */
+    uint64_t spilled;             /* bin entries beyond the per-tile capacity                    */
+    uint64_t max_tile_bin;        /* fullest 32x32 tile's triangle count                         */
 } shs_raster_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */
@@ -109,9 +113,13 @@ int shs_device_framebuffers(shs_ctx *ctx, void **color_dev, void **depth_dev);
 int shs_get_stats(shs_ctx *ctx, shs_raster_stats *stats);
 
 /* Per-kernel device timing of the last frame, recorded with HIP events on the context stream
- * (setup+count, scan, scatter, raster) in milliseconds.  Enabled by shs_enable_timing(ctx, 1). */
+ * (k_setup, k_ghost, unused, k_raster) in milliseconds.  Enabled by shs_enable_timing(ctx, 1). */
 int shs_enable_timing(shs_ctx *ctx, int enable);
 int shs_last_kernel_ms(shs_ctx *ctx, float *ms4);
+/* Sums of the same four kernel durations over every frame enqueued since shs_timing_reset
+ * (events recorded on the context stream around each kernel, harvested lazily). */
+int shs_timing_reset(shs_ctx *ctx);
+int shs_timing_read(shs_ctx *ctx, double *sum_ms4, int64_t *n_frames);
 
 /* ---- host helpers: GLM restatements the reference host code computes with glm -----------
  * (Camera3D::update shs_renderer.hpp:1224-1236; MonkeyObject::get_world_matrix
@@ -121,9 +129,20 @@ int shs_camera3d(const float position[3], float horizontal_angle, float vertical
                  float z_near, float z_far, float view16[16], float proj16[16]);
 int shs_model_trs(const float position[3], float rotation_deg_y, const float scale[3], float out16[16]);
 int shs_mat4_mul(const float a16[16], const float b16[16], float out16[16]);
+int shs_mat4_inverse(const float m16[16], float out16[16]);
 
-/* Library/ABI version for integration checks. */
+/* Debug / test hook: copy the last frame's per-triangle raster records (96 B each, layout
+ * shs_dev::TriRec in csrc/shs_device.hpp) into caller memory; returns the count via n_out. */
+int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out);
+
+/* Tuning knobs.  SHS_OPT_BIN_CAPACITY: initial per-tile bin capacity (entries past it spill to a
+ * global list and stay exact; the context grows the capacity to the fullest tile it observes). */
+#define SHS_OPT_BIN_CAPACITY 1
+int shs_set_option(shs_ctx *ctx, int option, int64_t value);
+
+/* Library/ABI version for integration checks; edge of the square GPU screen tile (shard unit). */
 int shs_abi_version(void);
+int shs_gpu_tile_size(void);
 
 #ifdef __cplusplus
 }

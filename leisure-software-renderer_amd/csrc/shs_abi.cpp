@@ -44,18 +44,24 @@ struct shs_ctx {
     std::vector<Mesh> meshes;
 
     DevBuf<DrawGPU> draws;
-    DevBuf<int32_t> draw_base;
     DevBuf<TriRec> recs;
-    DevBuf<uint32_t> tile_count, tile_offset, tile_cursor;
-    DevBuf<uint32_t> list, ghost;
-    DevBuf<uint32_t> counters;
+    DevBuf<uint32_t> tile_count;     // zero between frames
+    DevBuf<uint32_t> bins;           // n_tiles * bin_cap
+    DevBuf<uint2> spill;
+    DevBuf<uint32_t> ghost;          // unbounded ghost triangles
+    DevBuf<uint32_t> counters;       // 2 parity sets
+    DevBuf<uint2> tile_stat;         // per-tile (covered, bin entries)
+    std::vector<uint2> h_tile_stat;
+    uint64_t last_covered = 0, last_bins = 0, last_maxbin = 0;
+    uint32_t bin_cap = 256;
+    uint32_t frame_index = 0;        // parity of the counter set
+    uint32_t last_parity = 0;
     DevBuf<uint8_t> color;
     DevBuf<float> depth;
     DevBuf<float4> prequant;
 
     // pinned staging for the per-frame draw table (2 slots, guarded by events)
     DrawGPU *h_draws[2] = {nullptr, nullptr};
-    int32_t *h_base[2] = {nullptr, nullptr};
     size_t h_cap = 0;
     hipEvent_t slot_ev[2] = {nullptr, nullptr};
     bool slot_used[2] = {false, false};
@@ -73,6 +79,13 @@ struct shs_ctx {
     bool timing = false;
     hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     float last_ms[4] = {0, 0, 0, 0};
+    // ring of per-frame kernel events, harvested lazily: sums of kernel durations over many frames
+    static constexpr int RING = 64;
+    hipEvent_t ring_ev[RING][5] = {};
+    bool ring_pending[RING] = {};
+    int ring_next = 0;
+    double acc_ms[4] = {0, 0, 0, 0};
+    int64_t acc_frames = 0;
 };
 
 #define HIP_TRY(ctx, expr)                                                                       \
@@ -116,6 +129,8 @@ extern "C" {
 
 int shs_abi_version(void) { return 1; }
 
+int shs_gpu_tile_size(void) { return shs_dev::TILE; }
+
 int shs_create(int device, shs_ctx **out) {
     if (!out) return SHS_ERR_INVALID;
     *out = nullptr;
@@ -143,7 +158,11 @@ int shs_create(int device, shs_ctx **out) {
         return SHS_ERR_HIP;
     }
     std::memset(ctx->h_counters, 0, shs_dev::C_NCOUNTERS * sizeof(uint32_t));
-    if (ensure(ctx, ctx->counters, shs_dev::C_NCOUNTERS) != SHS_OK) { delete ctx; return SHS_ERR_HIP; }
+    if (ensure(ctx, ctx->counters, 2 * shs_dev::C_NCOUNTERS) != SHS_OK ||
+        hipMemset(ctx->counters.p, 0, 2 * shs_dev::C_NCOUNTERS * sizeof(uint32_t)) != hipSuccess) {
+        delete ctx;
+        return SHS_ERR_HIP;
+    }
     *out = ctx;
     return SHS_OK;
 }
@@ -156,17 +175,18 @@ int shs_destroy(shs_ctx *ctx) {
         if (m.pos) (void)hipFree(m.pos);
         if (m.nrm) (void)hipFree(m.nrm);
     }
-    release(ctx->draws); release(ctx->draw_base); release(ctx->recs);
-    release(ctx->tile_count); release(ctx->tile_offset); release(ctx->tile_cursor);
-    release(ctx->list); release(ctx->ghost); release(ctx->counters);
+    release(ctx->draws); release(ctx->recs); release(ctx->tile_count); release(ctx->bins);
+    release(ctx->spill); release(ctx->ghost); release(ctx->counters); release(ctx->tile_stat);
     release(ctx->color); release(ctx->depth); release(ctx->prequant);
     for (int i = 0; i < 2; ++i) {
         if (ctx->h_draws[i]) (void)hipHostFree(ctx->h_draws[i]);
-        if (ctx->h_base[i]) (void)hipHostFree(ctx->h_base[i]);
         if (ctx->slot_ev[i]) (void)hipEventDestroy(ctx->slot_ev[i]);
     }
     for (int i = 0; i < 5; ++i)
         if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
+    for (int k = 0; k < shs_ctx::RING; ++k)
+        for (int i = 0; i < 5; ++i)
+            if (ctx->ring_ev[k][i]) (void)hipEventDestroy(ctx->ring_ev[k][i]);
     if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -241,6 +261,26 @@ static void build_draw(const shs_legacy_draw &in, const Mesh &m, int32_t base, D
     }
 }
 
+static int harvest_slot(shs_ctx *ctx, int k) {
+    if (!ctx->ring_pending[k]) return SHS_OK;
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ring_ev[k][4]));
+    float ms[4];
+    for (int i = 0; i < 4; ++i) HIP_TRY(ctx, hipEventElapsedTime(&ms[i], ctx->ring_ev[k][i], ctx->ring_ev[k][i + 1]));
+    for (int i = 0; i < 4; ++i) { ctx->acc_ms[i] += ms[i]; ctx->last_ms[i] = ms[i]; }
+    ctx->acc_frames++;
+    ctx->ring_pending[k] = false;
+    return SHS_OK;
+}
+
+static int harvest_all(shs_ctx *ctx) {
+    // oldest first
+    for (int j = 0; j < shs_ctx::RING; ++j) {
+        int rc = harvest_slot(ctx, (ctx->ring_next + j) % shs_ctx::RING);
+        if (rc) return rc;
+    }
+    return SHS_OK;
+}
+
 static int enqueue_frame(shs_ctx *ctx) {
     const shs_frame_desc &f = ctx->frame;
     const int n_draws = (int)ctx->last_draws.size();
@@ -255,81 +295,102 @@ static int enqueue_frame(shs_ctx *ctx) {
     const int n_tris = (int)total;
 
     if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1))) return SHS_ERR_HIP;
-    if (ensure(ctx, ctx->tile_count, n_tiles) || ensure(ctx, ctx->tile_offset, n_tiles) || ensure(ctx, ctx->tile_cursor, n_tiles))
-        return SHS_ERR_HIP;
-    if (!ctx->list.p && ensure(ctx, ctx->list, std::max<size_t>(1 << 16, (size_t)n_tris * 4))) return SHS_ERR_HIP;
-    if (!ctx->ghost.p && ensure(ctx, ctx->ghost, std::max<size_t>(1 << 12, (size_t)n_tris / 8))) return SHS_ERR_HIP;
+    if (ctx->tile_count.cap < (size_t)n_tiles || !ctx->tile_count.p) {
+        if (ensure(ctx, ctx->tile_count, n_tiles)) return SHS_ERR_HIP;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->tile_count.p, 0, ctx->tile_count.cap * sizeof(uint32_t), ctx->stream));
+    }
+    if (ensure(ctx, ctx->bins, (size_t)n_tiles * ctx->bin_cap)) return SHS_ERR_HIP;
+    if (ctx->tile_stat.cap < (size_t)n_tiles || !ctx->tile_stat.p) {
+        if (ensure(ctx, ctx->tile_stat, n_tiles)) return SHS_ERR_HIP;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->tile_stat.p, 0, ctx->tile_stat.cap * sizeof(uint2), ctx->stream));
+    }
+    if (!ctx->spill.p && ensure(ctx, ctx->spill, 1 << 16)) return SHS_ERR_HIP;
+    if (!ctx->ghost.p && ensure(ctx, ctx->ghost, 1 << 12)) return SHS_ERR_HIP;
     if (ensure(ctx, ctx->color, npx * 4) || ensure(ctx, ctx->depth, npx)) return SHS_ERR_HIP;
     const bool want_pq = (f.flags & SHS_FRAME_PREQUANT) != 0;
     if (want_pq && ensure(ctx, ctx->prequant, npx)) return SHS_ERR_HIP;
-    if (ensure(ctx, ctx->draws, std::max(n_draws, 1)) || ensure(ctx, ctx->draw_base, std::max(n_draws, 1))) return SHS_ERR_HIP;
 
-    // pinned staging slot for the draw table
-    const int s = ctx->slot;
-    ctx->slot ^= 1;
-    if (ctx->slot_used[s]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[s]));
-    if ((size_t)n_draws > ctx->h_cap) {
-        for (int i = 0; i < 2; ++i) {
-            if (i != s && ctx->slot_used[i]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[i]));
-            if (ctx->h_draws[i]) HIP_TRY(ctx, hipHostFree(ctx->h_draws[i]));
-            if (ctx->h_base[i]) HIP_TRY(ctx, hipHostFree(ctx->h_base[i]));
-            ctx->h_draws[i] = nullptr;
-            ctx->h_base[i] = nullptr;
-        }
-        const size_t cap = std::max<size_t>(n_draws, 64);
-        for (int i = 0; i < 2; ++i) {
-            HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_draws[i]), cap * sizeof(DrawGPU)));
-            HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_base[i]), cap * sizeof(int32_t)));
-        }
-        ctx->h_cap = cap;
-    }
-    int32_t base = 0;
-    for (int i = 0; i < n_draws; ++i) {
-        const shs_legacy_draw &d = ctx->last_draws[i];
-        build_draw(d, ctx->meshes[d.mesh_id], base, ctx->h_draws[s][i]);
-        ctx->h_base[s][i] = base;
-        base += ctx->meshes[d.mesh_id].n_tris;
-    }
-
+    // per-draw uniform blocks: kernel arguments for small scenes, a device table otherwise
+    shs_dev::KArgDraws ka;
+    std::memset(&ka, 0, sizeof ka);
     hipStream_t st = ctx->stream;
-    if (n_draws > 0) {
+    int32_t base = 0;
+    if (n_draws <= shs_dev::KARG_DRAWS) {
+        for (int i = 0; i < n_draws; ++i) {
+            const shs_legacy_draw &d = ctx->last_draws[i];
+            build_draw(d, ctx->meshes[d.mesh_id], base, ka.d[i]);
+            base += ctx->meshes[d.mesh_id].n_tris;
+        }
+    } else {
+        if (ensure(ctx, ctx->draws, n_draws)) return SHS_ERR_HIP;
+        const int s = ctx->slot;
+        ctx->slot ^= 1;
+        if (ctx->slot_used[s]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[s]));
+        if ((size_t)n_draws > ctx->h_cap) {
+            for (int i = 0; i < 2; ++i) {
+                if (i != s && ctx->slot_used[i]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[i]));
+                if (ctx->h_draws[i]) HIP_TRY(ctx, hipHostFree(ctx->h_draws[i]));
+                ctx->h_draws[i] = nullptr;
+            }
+            const size_t cap = std::max<size_t>(n_draws, 64);
+            for (int i = 0; i < 2; ++i)
+                HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_draws[i]), cap * sizeof(DrawGPU)));
+            ctx->h_cap = cap;
+        }
+        for (int i = 0; i < n_draws; ++i) {
+            const shs_legacy_draw &d = ctx->last_draws[i];
+            build_draw(d, ctx->meshes[d.mesh_id], base, ctx->h_draws[s][i]);
+            base += ctx->meshes[d.mesh_id].n_tris;
+        }
         HIP_TRY(ctx, hipMemcpyAsync(ctx->draws.p, ctx->h_draws[s], n_draws * sizeof(DrawGPU), hipMemcpyHostToDevice, st));
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->draw_base.p, ctx->h_base[s], n_draws * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(ctx, hipEventRecord(ctx->slot_ev[s], st));
+        ctx->slot_used[s] = true;
     }
-    HIP_TRY(ctx, hipEventRecord(ctx->slot_ev[s], st));
-    ctx->slot_used[s] = true;
-    HIP_TRY(ctx, hipMemsetAsync(ctx->counters.p, 0, shs_dev::C_NCOUNTERS * sizeof(uint32_t), st));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->tile_count.p, 0, n_tiles * sizeof(uint32_t), st));
 
     FrameParams fp;
+    std::memset(&fp, 0, sizeof fp);
     fp.W = f.width; fp.H = f.height;
     fp.rtw = f.ref_tile_w; fp.rth = f.ref_tile_h;
     fp.rank = f.shard_rank; fp.count = f.shard_count;
     fp.tiles_x = tiles_x; fp.tiles_y = tiles_y;
+    fp.rt_x = (f.width + f.ref_tile_w - 1) / f.ref_tile_w;
+    fp.rt_y = (f.height + f.ref_tile_h - 1) / f.ref_tile_h;
     fp.n_tris = n_tris; fp.n_draws = n_draws;
     fp.clear_rgba = (uint32_t)f.clear_color[0] | ((uint32_t)f.clear_color[1] << 8) | ((uint32_t)f.clear_color[2] << 16) |
                     ((uint32_t)f.clear_color[3] << 24);
     fp.flags = f.flags;
-    fp.list_capacity = (uint32_t)std::min<size_t>(ctx->list.cap, 0xffffffffu);
-    fp.ghost_capacity = (uint32_t)std::min<size_t>(ctx->ghost.cap, 0xffffffffu);
+    fp.bin_cap = ctx->bin_cap;
+    fp.spill_cap = (uint32_t)std::min<size_t>(ctx->spill.cap, 0xffffffffu);
+    fp.ghost_cap = (uint32_t)std::min<size_t>(ctx->ghost.cap, 0xffffffffu);
+    fp.parity = ctx->frame_index & 1u;
 
     FrameBuffers fb;
-    fb.draws = ctx->draws.p; fb.draw_base = ctx->draw_base.p; fb.recs = ctx->recs.p;
-    fb.tile_count = ctx->tile_count.p; fb.tile_offset = ctx->tile_offset.p; fb.tile_cursor = ctx->tile_cursor.p;
-    fb.tile_list = ctx->list.p; fb.ghost_list = ctx->ghost.p; fb.counters = ctx->counters.p;
+    fb.draws = ctx->draws.p; fb.recs = ctx->recs.p; fb.tile_count = ctx->tile_count.p; fb.bins = ctx->bins.p;
+    fb.spill = ctx->spill.p; fb.ghost_list = ctx->ghost.p; fb.counters = ctx->counters.p;
+    fb.tile_stat = ctx->tile_stat.p;
     fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;
 
     const int owned = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
-    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[0], st));
-    HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, st));
-    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[1], st));
-    HIP_TRY(ctx, shs_internal::launch_scan(fp, fb, n_tiles, st));
-    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[2], st));
-    HIP_TRY(ctx, shs_internal::launch_scatter(fp, fb, st));
-    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[3], st));
-    HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, owned, st));
-    if (ctx->timing) HIP_TRY(ctx, hipEventRecord(ctx->tev[4], st));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_counters, ctx->counters.p, shs_dev::C_NCOUNTERS * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    hipEvent_t *ev = nullptr;
+    if (ctx->timing) {
+        const int k = ctx->ring_next;
+        ctx->ring_next = (k + 1) % shs_ctx::RING;
+        if (harvest_slot(ctx, k)) return SHS_ERR_HIP;
+        if (!ctx->ring_ev[k][0])
+            for (int i = 0; i < 5; ++i) HIP_TRY(ctx, hipEventCreate(&ctx->ring_ev[k][i]));
+        ev = ctx->ring_ev[k];
+        ctx->ring_pending[k] = true;
+    }
+    // kernel durations: [0] k_setup, [1] [2] (unused), [3] k_raster
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], st));
+    HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, ka, st));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], st));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], st));
+    HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, ka, owned, st));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], st));
+    ctx->last_parity = fp.parity;
+    ctx->frame_index++;
     ctx->have_frame = true;
     ctx->need_check = true;
     ctx->last_n_tris = n_tris;
@@ -337,20 +398,41 @@ static int enqueue_frame(shs_ctx *ctx) {
     return SHS_OK;
 }
 
-// Wait for the frame; if a bin capacity overflowed, grow it and re-issue the frame.
+static uint32_t next_pow2(uint32_t v) {
+    uint32_t p = 1;
+    while (p < v && p < (1u << 30)) p <<= 1;
+    return p;
+}
+
+// Wait for the frame and read its counters; if a capacity overflowed, grow it and re-issue the frame.
 static int finish_frame(shs_ctx *ctx) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (!ctx->need_check) return SHS_OK;
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        const uint32_t ov = ctx->h_counters[shs_dev::C_OVERFLOW];
-        if (!ov) break;
-        if (ov & 1u) {
-            const size_t need = (size_t)ctx->h_counters[shs_dev::C_BINS];
-            release(ctx->list);
-            if (ensure(ctx, ctx->list, need + need / 4 + 1024)) return SHS_ERR_HIP;
+    for (int attempt = 0; attempt < 6; ++attempt) {
+        HIP_TRY(ctx, hipMemcpy(ctx->h_counters, ctx->counters.p + ctx->last_parity * shs_dev::C_NCOUNTERS,
+                               shs_dev::C_NCOUNTERS * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        const uint32_t *c = ctx->h_counters;
+        // per-tile stats of the owned tiles -> covered pixels, bin entries, fullest tile
+        ctx->h_tile_stat.resize(ctx->last_n_tiles);
+        HIP_TRY(ctx, hipMemcpy(ctx->h_tile_stat.data(), ctx->tile_stat.p, ctx->last_n_tiles * sizeof(uint2),
+                               hipMemcpyDeviceToHost));
+        ctx->last_covered = ctx->last_bins = ctx->last_maxbin = 0;
+        for (int t = ctx->frame.shard_rank; t < ctx->last_n_tiles; t += ctx->frame.shard_count) {
+            ctx->last_covered += ctx->h_tile_stat[t].x;
+            ctx->last_bins += ctx->h_tile_stat[t].y;
+            ctx->last_maxbin = std::max<uint64_t>(ctx->last_maxbin, ctx->h_tile_stat[t].y);
         }
-        if (ov & 2u) {
-            const size_t need = (size_t)ctx->h_counters[shs_dev::C_GHOST];
+        // adapt the per-tile bin capacity to the fullest tile (spilled entries stay exact)
+        if (ctx->last_maxbin > ctx->bin_cap) ctx->bin_cap = next_pow2((uint32_t)std::min<uint64_t>(ctx->last_maxbin, 1u << 30));
+        const uint32_t ov = c[shs_dev::C_OVERFLOW];
+        if (!ov) break;
+        if (ov & shs_dev::OV_SPILL) {
+            const size_t need = c[shs_dev::C_SPILL];
+            release(ctx->spill);
+            if (ensure(ctx, ctx->spill, need + need / 4 + 1024)) return SHS_ERR_HIP;
+        }
+        if (ov & shs_dev::OV_GHOST) {
+            const size_t need = c[shs_dev::C_UNBOUNDED];
             release(ctx->ghost);
             if (ensure(ctx, ctx->ghost, need + need / 4 + 1024)) return SHS_ERR_HIP;
         }
@@ -358,10 +440,8 @@ static int finish_frame(shs_ctx *ctx) {
         if (rc) return rc;
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
-    if (ctx->h_counters[shs_dev::C_OVERFLOW]) { ctx->err = "bin capacity overflow persisted"; return SHS_ERR_OVERFLOW; }
-    if (ctx->timing) {
-        for (int i = 0; i < 4; ++i) HIP_TRY(ctx, hipEventElapsedTime(&ctx->last_ms[i], ctx->tev[i], ctx->tev[i + 1]));
-    }
+    if (ctx->h_counters[shs_dev::C_OVERFLOW]) { ctx->err = "capacity overflow persisted"; return SHS_ERR_OVERFLOW; }
+    if (ctx->timing && harvest_all(ctx)) return SHS_ERR_HIP;
     ctx->need_check = false;
     return SHS_OK;
 }
@@ -433,14 +513,39 @@ int shs_get_stats(shs_ctx *ctx, shs_raster_stats *st) {
     st->tri_input = (uint64_t)ctx->last_n_tris;
     st->tri_setup = ctx->h_counters[shs_dev::C_SETUP];
     st->tri_ghost = ctx->h_counters[shs_dev::C_GHOST];
-    st->bin_entries = ctx->h_counters[shs_dev::C_BINS];
-    st->covered_pixels = ctx->h_counters[shs_dev::C_COVERED];
+    st->bin_entries = ctx->last_bins;
+    st->tri_ghost_unbounded = ctx->h_counters[shs_dev::C_UNBOUNDED];
+    st->spilled = ctx->h_counters[shs_dev::C_SPILL];
+    st->max_tile_bin = ctx->last_maxbin;
+    st->covered_pixels = ctx->last_covered;
     return SHS_OK;
 }
 
 int shs_enable_timing(shs_ctx *ctx, int enable) {
     if (!ctx) return SHS_ERR_INVALID;
     ctx->timing = enable != 0;
+    return SHS_OK;
+}
+
+int shs_timing_reset(shs_ctx *ctx) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    if (harvest_all(ctx)) return SHS_ERR_HIP;
+    for (int i = 0; i < 4; ++i) ctx->acc_ms[i] = 0.0;
+    ctx->acc_frames = 0;
+    return SHS_OK;
+}
+
+int shs_timing_read(shs_ctx *ctx, double *sum_ms4, int64_t *n_frames) {
+    if (!ctx || !sum_ms4 || !n_frames) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    if (harvest_all(ctx)) return SHS_ERR_HIP;
+    for (int i = 0; i < 4; ++i) sum_ms4[i] = ctx->acc_ms[i];
+    *n_frames = ctx->acc_frames;
     return SHS_OK;
 }
 
@@ -451,6 +556,31 @@ int shs_last_kernel_ms(shs_ctx *ctx, float *ms4) {
     if (rc) return rc;
     std::memcpy(ms4, ctx->last_ms, sizeof ctx->last_ms);
     return SHS_OK;
+}
+
+int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out) {
+    if (!ctx || !n_out || !ctx->have_frame) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    *n_out = ctx->last_n_tris;
+    if (out && capacity > 0) {
+        const size_t n = (size_t)std::min<int64_t>(capacity, ctx->last_n_tris);
+        HIP_TRY(ctx, hipMemcpy(out, ctx->recs.p, n * sizeof(TriRec), hipMemcpyDeviceToHost));
+    }
+    return SHS_OK;
+}
+
+int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (option == SHS_OPT_BIN_CAPACITY) {
+        if (value < 1 || value > (1 << 24)) return SHS_ERR_INVALID;
+        if (set_dev(ctx)) return SHS_ERR_HIP;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        ctx->bin_cap = (uint32_t)value;
+        return SHS_OK;
+    }
+    return SHS_ERR_INVALID;
 }
 
 int shs_camera3d(const float position[3], float ha, float va, float fov, float zn, float zf, float view16[16], float proj16[16]) {
@@ -469,6 +599,12 @@ int shs_model_trs(const float position[3], float rot_deg_y, const float scl[3], 
 int shs_mat4_mul(const float a[16], const float b[16], float out[16]) {
     if (!a || !b || !out) return SHS_ERR_INVALID;
     shs_host::mul(a, b, out);
+    return SHS_OK;
+}
+
+int shs_mat4_inverse(const float m[16], float out[16]) {
+    if (!m || !out) return SHS_ERR_INVALID;
+    shs_host::inverse(m, out);
     return SHS_OK;
 }
 

@@ -37,48 +37,68 @@ struct alignas(16) TriRec {
     float v1x, v1y, d00, d01;        // v1 = C - A, d00 = v0.v0, d01 = v0.v1
     float d11, denom, z0, z1;        // d11 = v1.v1, denom = d00*d11 - d01*d01, screen z
     float z2;
-    uint32_t flags;                  // TRI_CULLED | TRI_GHOST
+    uint32_t flags;                  // TRI_CULLED | TRI_GHOST | TRI_UNBOUNDED
     int32_t draw;                    // index into the draw table
     int32_t local;                   // triangle index inside the draw's mesh
-    int32_t ix0, ix1, iy0, iy1;      // integer bbox [floor(min), floor(max)] clamped to the screen
+    uint32_t ibx, iby;               // integer bbox [floor(min), floor(max)] clamped to the screen,
+                                     // packed int16 (lo | hi << 16)
+    uint32_t gbx, gby;               // cull/bin box: the ibox, or for a ghost the danger box
     float fminx, fmaxx, fminy, fmaxy;// float bbox of the screen-space corners
 };
 static_assert(sizeof(TriRec) == 96, "TriRec must stay 96 B");
 
 constexpr uint32_t TRI_CULLED = 1u;
-constexpr uint32_t TRI_GHOST = 2u;
+constexpr uint32_t TRI_GHOST = 2u;       // tile-clamp pixels near the bbox may pass: test them
+constexpr uint32_t TRI_UNBOUNDED = 4u;   // ... anywhere on screen (global list, every tile)
 
-constexpr int TILE = 32;             // GPU screen tile (32x32 px, one 256-thread workgroup)
+__device__ __forceinline__ uint32_t pack16(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
+__device__ __forceinline__ int lo16(uint32_t v) { return (int)(int16_t)(v & 0xffffu); }
+__device__ __forceinline__ int hi16(uint32_t v) { return (int)(int16_t)(v >> 16); }
+
+constexpr int TILE = 16;             // GPU screen tile (16x16 px, one 256-thread workgroup)
 constexpr int CHUNK = 256;           // triangle records staged in LDS per pass
 
-// counters[] slots
-constexpr int C_GHOST = 0, C_SETUP = 1, C_BINS = 2, C_OVERFLOW = 3, C_COVERED = 4, C_NCOUNTERS = 8;
+// counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one)
+constexpr int C_GHOST = 0, C_SETUP = 1, C_UNBOUNDED = 2, C_OVERFLOW = 3, C_COVERED = 4, C_MAXBIN = 5, C_SPILL = 6,
+              C_BINS = 7, C_NCOUNTERS = 8;
+constexpr uint32_t OV_SPILL = 1u, OV_GHOST = 2u;
+
+// Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);
+// larger scenes read the device draw table.
+constexpr int KARG_DRAWS = 6;
 
 struct FrameParams {
     int32_t W, H;
     int32_t rtw, rth;                // reference tile-job size (80x80)
     int32_t rank, count;             // shard ownership of GPU tiles
     int32_t tiles_x, tiles_y;
+    int32_t rt_x, rt_y;              // reference tiles across / down
     int32_t n_tris, n_draws;
     uint32_t clear_rgba;
     uint32_t flags;
-    uint32_t list_capacity;
-    uint32_t ghost_capacity;
+    uint32_t bin_cap;                // per-tile bin capacity
+    uint32_t spill_cap;
+    uint32_t ghost_cap;              // unbounded-ghost list capacity
+    uint32_t parity;                 // counter set used by this frame
+    uint32_t pad0, pad1;
 };
 
 struct FrameBuffers {
-    const DrawGPU *draws;
-    const int32_t *draw_base;        // n_draws entries, ascending tri_base
+    const DrawGPU *draws;            // device draw table (n_draws > KARG_DRAWS)
     TriRec *recs;
-    uint32_t *tile_count;            // n_tiles
-    uint32_t *tile_offset;           // n_tiles
-    uint32_t *tile_cursor;           // n_tiles
-    uint32_t *tile_list;             // list_capacity
-    uint32_t *ghost_list;            // ghost_capacity
-    uint32_t *counters;              // C_NCOUNTERS
+    uint32_t *tile_count;            // n_tiles, zero between frames (k_raster re-zeroes)
+    uint32_t *bins;                  // n_tiles * bin_cap
+    uint2 *spill;                    // (tile, tri) pairs beyond bin_cap
+    uint32_t *ghost_list;            // unbounded ghost triangles (ghost_cap)
+    uint32_t *counters;              // 2 * C_NCOUNTERS
+    uint2 *tile_stat;                // n_tiles: (covered pixels, bin entries) of the last frame
     uint8_t *color;                  // W*H*4, canvas rows
     float *depth;                    // W*H, screen rows
     float4 *prequant;                // W*H (optional)
+};
+
+struct KArgDraws {
+    DrawGPU d[KARG_DRAWS];
 };
 
 // ---- GLM scalar semantics (glm/detail/func_common.inl) -------------------------------------

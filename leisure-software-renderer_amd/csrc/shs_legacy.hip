@@ -3,18 +3,25 @@
 // Replaces RendererSystem::process + draw_triangle_tile + the four legacy shader pairs
 // (cpp-folders/src/hello-3d-primitives/hello_pipeline_{blinn_phong,phong,gouraud,flat}_shading.cpp).
 //
-// Pipeline per frame (all on one HIP stream):
+// Pipeline per frame: two launches on one HIP stream, no memsets, no copies for <= 6 draws.
 //   k_setup   one thread per triangle: VS x3 (mvp), clip_to_screen, area/denominator culls, the
-//             per-triangle half of barycentric_coordinate, 96-B raster record, bin counts.
-//   k_scan    one workgroup: exclusive scan of per-tile counts -> list offsets.
-//   k_scatter one thread per triangle: triangle ids into per-tile lists (unordered).
-//   k_raster  one workgroup per 32x32 tile: stage the tile's records in LDS, each lane resolves
-//             4 pixels to the lexicographic minimum (z, submission index) -- identical to the
-//             reference's in-order strict-less z test (first triangle with the minimal z wins) --
-//             then shades only the winners and writes colour (canvas rows) and depth (screen
-//             rows) once, coalesced, with the clear fused.
-// The z-buffer therefore never round-trips through HBM: HBM sees each input once and each
-// output pixel once.
+//             per-triangle half of barycentric_coordinate, a 96-B raster record, and the triangle
+//             id appended straight into the per-tile bins its bin box touches (unordered; a spill
+//             list past the bin capacity).
+//   k_raster  one 256-thread workgroup per 16x16 tile, one pixel per lane (8x8 block per wave):
+//             stage the tile's records in LDS, resolve every pixel to the lexicographic minimum
+//             (z, submission index) -- identical to the reference's in-order strict-less z test
+//             (the first triangle with the minimal z wins) -- then shade only the winners and write
+//             colour (canvas rows) and depth (screen rows) once, with the clear fused.
+// The z-buffer never round-trips through HBM: HBM sees each input once and each output once.
+//
+// Tile-clamp semantics.  draw_triangle_tile clamps a triangle's bbox to the 80x80 tile job that
+// runs it (blinn_phong_shading.cpp:208-224), so the reference also tests pixels OUTSIDE the
+// triangle's bbox (the clamped edge rows/columns/corners of every other tile).  Such a pixel is
+// >= 0.49 px outside the bbox, so an exact barycentric is <= -(distance)/(2*extent); k_setup
+// bounds barycentric_coordinate's float error (an affine function of the distance) and proves
+// those pixels rejected, except inside a small "danger box" around slivers (TRI_GHOST): k_raster
+// then evaluates the reference's exact visited set there.  DESIGN.md has the derivation.
 #include <float.h>
 
 #include "shs_device.hpp"
@@ -24,51 +31,64 @@ namespace shs_dev {
 
 // ---- k_setup --------------------------------------------------------------------------------
 
-// Sound filter for the reference's tile-clamp "ghost" pixels.  draw_triangle_tile clamps each
-// triangle's bbox to the tile that runs it (blinn_phong_shading.cpp:208-215), so every triangle is
-// tested against pixels of every tile -- also pixels outside its own bbox.  Those pixels are at
-// least 0.5 px outside the bbox, so some exact barycentric is <= -0.49/(2*extent); this returns
-// false only when a forward error bound of barycentric_coordinate's float arithmetic proves the
-// computed (u,v,w) keep a negative component there.  Triangles it cannot clear (slivers) are
-// rasterised over the reference's exact visited-pixel set by every tile (ghost list).  DESIGN.md
-// "Tile-clamp semantics" has the derivation.
-__device__ bool ghost_risk(const TriRec &r) {
+// Forward error bound of barycentric_coordinate (u, v, w) at a pixel whose centre lies rx / ry px
+// outside the triangle's float bbox: E = e0 + ex*rx + ey*ry (u = 2^-24; dot products carry 2u,
+// the two-product differences 6u, the divide and 1-v-w a few u more; 25 % slack).  Such a pixel
+// has min exact barycentric <= -max(rx/(2Wx), ry/(2Wy)), so it is provably rejected when
+// E < max(...), i.e. outside the box expanded by 2*W*m0, m0 = e0 / (1 - 2(ex*Wx + ey*Wy)).
+// Returns the expansion (dgx, dgy) >= 0, or (-1, -1) if no bound exists (then every visited pixel
+// is tested).
+__device__ __noinline__ double2 danger_margin(const TriRec &r) {
+    const double2 none = make_double2(-1.0, -1.0);
     const double u = 5.9604644775390625e-08;  // 2^-24
     const double a = fabs((double)r.v0x), b = fabs((double)r.v0y);
     const double c = fabs((double)r.v1x), d = fabs((double)r.v1y);
     const double Wx = (double)r.fmaxx - (double)r.fminx, Wy = (double)r.fmaxy - (double)r.fminy;
-    if (!(Wx > 0.0) || !(Wy > 0.0)) return true;
+    if (!(Wx > 0.0) || !(Wy > 0.0)) return none;
     const double A00 = a * a + b * b, A11 = c * c + d * d, A01 = a * c + b * d;
     const double Dabs = fabs((double)r.denom);
     const double ED = 6.1 * u * (A00 * A11 + A01 * A01);
     const double Dlow = Dabs - ED;
-    if (!(Dlow > 0.0) || !(Dabs < 1e300)) return true;
+    if (!(Dlow > 0.0) || !(Dabs < 1e300)) return none;
     const double K1 = 7.2 * u + ED / Dlow;
     const double p0 = Wx + 0.01, q0 = Wy + 0.01;
     const double A20 = p0 * a + q0 * b, A21 = p0 * c + q0 * d;
     const double Nv0 = A11 * A20 + A01 * A21, Nvx = A11 * a + A01 * c, Nvy = A11 * b + A01 * d;
     const double Nw0 = A00 * A21 + A01 * A20, Nwx = A00 * c + A01 * a, Nwy = A00 * d + A01 * b;
     const double s = K1 / Dabs * (2.0 + 2.0 * u);
-    double e0 = (Nv0 + Nw0) * s + u * (2.0 + (2.0 * Nv0 + Nw0) / Dlow);
-    double ex = (Nvx + Nwx) * s + u * (2.0 * Nvx + Nwx) / Dlow;
-    double ey = (Nvy + Nwy) * s + u * (2.0 * Nvy + Nwy) / Dlow;
-    e0 *= 1.25; ex *= 1.25; ey *= 1.25;
-    const double Wm = Wx > Wy ? Wx : Wy;
-    const bool safe = (ex <= 1.0 / (8.0 * Wx)) && (ey <= 1.0 / (8.0 * Wy)) && (e0 <= 0.49 / (8.0 * Wm));
-    return !safe;
+    const double e0 = 1.25 * ((Nv0 + Nw0) * s + u * (2.0 + (2.0 * Nv0 + Nw0) / Dlow));
+    const double ex = 1.25 * ((Nvx + Nwx) * s + u * (2.0 * Nvx + Nwx) / Dlow);
+    const double ey = 1.25 * ((Nvy + Nwy) * s + u * (2.0 * Nvy + Nwy) / Dlow);
+    const double S = ex * Wx + ey * Wy;
+    if (!(S < 0.5)) return none;
+    const double m0 = e0 / (1.0 - 2.0 * S);
+    const double dgx = 2.0 * Wx * m0, dgy = 2.0 * Wy * m0;
+    return (dgx < 1e6 && dgy < 1e6) ? make_double2(dgx, dgy) : none;
 }
 
 __device__ __forceinline__ bool finitef(float x) { return fabsf(x) <= FLT_MAX; }
 
-__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb) {
+__device__ __forceinline__ const DrawGPU *draw_table(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka) {
+    return fp.n_draws <= KARG_DRAWS ? ka.d : fb.draws;
+}
+
+// floor of a finite float, clamped into [lo, hi] before the conversion
+__device__ __forceinline__ int floor_clamped(float x, int lo, int hi) {
+    return (int)fminf(fmaxf(floorf(x), (float)lo), (float)hi);
+}
+
+__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     const int gid = blockIdx.x * 256 + threadIdx.x;
+    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
+    if (blockIdx.x == 0 && threadIdx.x < C_NCOUNTERS) fb.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
     if (gid >= fp.n_tris) return;
+    const DrawGPU *draws = draw_table(fp, fb, ka);
     int lo = 0, hi = fp.n_draws - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (fb.draw_base[mid] <= gid) lo = mid; else hi = mid - 1;
+        if (draws[mid].tri_base <= gid) lo = mid; else hi = mid - 1;
     }
-    const DrawGPU &dr = fb.draws[lo];
+    const DrawGPU &dr = draws[lo];
     const int local = gid - dr.tri_base;
     const float *p = dr.pos + 9 * (size_t)local;
 
@@ -112,17 +132,32 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb) 
     // compare, shs_renderer.hpp:816) returns bc = -1 everywhere.
     if (!finite || area <= 0.0f || !((double)fabsf(r.denom) >= 1e-5)) flags |= TRI_CULLED;
 
-    int ix0 = 0, ix1 = -1, iy0 = 0, iy1 = -1;
+    int ix0 = 0, ix1 = -1, iy0 = 0, iy1 = -1;     // integer bbox (empty by default)
+    int gx0 = 0, gx1 = -1, gy0 = 0, gy1 = -1;     // bin box
     if (!(flags & TRI_CULLED)) {
+        ix0 = floor_clamped(r.fminx, 0, fp.W);
+        ix1 = floor_clamped(r.fmaxx, -1, fp.W - 1);
+        iy0 = floor_clamped(r.fminy, 0, fp.H);
+        iy1 = floor_clamped(r.fmaxy, -1, fp.H - 1);
+        // Straight-line selects after one out-of-line call: ROCm 7.2 hipcc mis-allocated a value
+        // kept live across an inlined danger_margin() on a divergent path (found by
+        // test_config_blinn_phong[c1]); keep this region free of values live across branches.
         const bool dfin = finitef(r.d00) && finitef(r.d01) && finitef(r.d11) && finitef(r.denom);
-        if (!dfin || ghost_risk(r)) flags |= TRI_GHOST;
-        ix0 = (int)fminf(fmaxf(floorf(r.fminx), 0.0f), (float)fp.W);
-        ix1 = (int)fminf(fmaxf(floorf(r.fmaxx), -1.0f), (float)(fp.W - 1));
-        iy0 = (int)fminf(fmaxf(floorf(r.fminy), 0.0f), (float)fp.H);
-        iy1 = (int)fminf(fmaxf(floorf(r.fmaxy), -1.0f), (float)(fp.H - 1));
+        const double2 dg = dfin ? danger_margin(r) : make_double2(-1.0, -1.0);
+        const bool unbounded = !(dg.x >= 0.0);
+        const bool ghost = unbounded || dg.x >= 0.49 || dg.y >= 0.49;
+        // expansion of the bin box beyond the float bbox: 0 (ibox), danger + 1 px, or the screen
+        const double exx = unbounded ? 1e30 : (ghost ? dg.x + 1.0 : 0.0);
+        const double exy = unbounded ? 1e30 : (ghost ? dg.y + 1.0 : 0.0);
+        gx0 = floor_clamped((float)((double)r.fminx - exx), 0, fp.W);
+        gx1 = floor_clamped((float)((double)r.fmaxx + exx), -1, fp.W - 1);
+        gy0 = floor_clamped((float)((double)r.fminy - exy), 0, fp.H);
+        gy1 = floor_clamped((float)((double)r.fmaxy + exy), -1, fp.H - 1);
+        flags |= (ghost ? TRI_GHOST : 0u) | (unbounded ? TRI_UNBOUNDED : 0u);
     }
     r.flags = flags;
-    r.ix0 = ix0; r.ix1 = ix1; r.iy0 = iy0; r.iy1 = iy1;
+    r.ibx = pack16(ix0, ix1); r.iby = pack16(iy0, iy1);
+    r.gbx = pack16(gx0, gx1); r.gby = pack16(gy0, gy1);
     {
         const float4 *src = reinterpret_cast<const float4 *>(&r);
         float4 *dst = reinterpret_cast<float4 *>(&fb.recs[gid]);
@@ -130,72 +165,34 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb) 
         for (int j = 0; j < 6; ++j) dst[j] = src[j];
     }
     if (flags & TRI_CULLED) return;
-    atomicAdd(&fb.counters[C_SETUP], 1u);
-    if (flags & TRI_GHOST) {
-        const uint32_t slot = atomicAdd(&fb.counters[C_GHOST], 1u);
-        if (slot < fp.ghost_capacity) fb.ghost_list[slot] = (uint32_t)gid;
-        else atomicOr(&fb.counters[C_OVERFLOW], 2u);
-        return;
+    atomicAdd(&cnt[C_SETUP], 1u);
+    if (flags & TRI_GHOST) atomicAdd(&cnt[C_GHOST], 1u);
+    if (flags & TRI_UNBOUNDED) {
+        const uint32_t slot = atomicAdd(&cnt[C_UNBOUNDED], 1u);
+        if (slot < fp.ghost_cap) fb.ghost_list[slot] = (uint32_t)gid;
+        else atomicOr(&cnt[C_OVERFLOW], OV_GHOST);
+        return;   // every tile reads the unbounded list; not binned
     }
-    if (ix0 > ix1 || iy0 > iy1) return;
-    const int tx0 = ix0 / TILE, tx1 = ix1 / TILE, ty0 = iy0 / TILE, ty1 = iy1 / TILE;
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-            const int t = ty * fp.tiles_x + tx;
-            if (t % fp.count == fp.rank) atomicAdd(&fb.tile_count[t], 1u);
-        }
-}
-
-// ---- k_scan ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_scan(FrameParams fp, FrameBuffers fb, int n_tiles) {
-    __shared__ uint32_t s[1024];
-    const int tid = threadIdx.x;
-    const int per = (n_tiles + 1023) / 1024;
-    const int b = tid * per, e = min(b + per, n_tiles);
-    uint32_t sum = 0;
-    for (int i = b; i < e; ++i) sum += fb.tile_count[i];
-    s[tid] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = tid >= off ? s[tid - off] : 0u;
-        __syncthreads();
-        s[tid] += v;
-        __syncthreads();
-    }
-    uint32_t run = s[tid] - sum;  // exclusive prefix
-    for (int i = b; i < e; ++i) {
-        fb.tile_offset[i] = run;
-        fb.tile_cursor[i] = run;
-        run += fb.tile_count[i];
-    }
-    if (tid == 1023) {
-        fb.counters[C_BINS] = s[1023];
-        if (s[1023] > fp.list_capacity) atomicOr(&fb.counters[C_OVERFLOW], 1u);
-    }
-}
-
-// ---- k_scatter ------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_scatter(FrameParams fp, FrameBuffers fb) {
-    const int gid = blockIdx.x * 256 + threadIdx.x;
-    if (gid >= fp.n_tris) return;
-    const int4 q = reinterpret_cast<const int4 *>(&fb.recs[gid])[3];   // z2, flags, draw, local
-    const uint32_t flags = (uint32_t)q.y;
-    if (flags & (TRI_CULLED | TRI_GHOST)) return;
-    const int4 bb = reinterpret_cast<const int4 *>(&fb.recs[gid])[4];  // ix0, ix1, iy0, iy1
-    if (bb.x > bb.y || bb.z > bb.w) return;
-    const int tx0 = bb.x / TILE, tx1 = bb.y / TILE, ty0 = bb.z / TILE, ty1 = bb.w / TILE;
+    if (gx0 > gx1 || gy0 > gy1) return;
+    const int tx0 = gx0 / TILE, tx1 = gx1 / TILE, ty0 = gy0 / TILE, ty1 = gy1 / TILE;
     for (int ty = ty0; ty <= ty1; ++ty)
         for (int tx = tx0; tx <= tx1; ++tx) {
             const int t = ty * fp.tiles_x + tx;
             if (t % fp.count != fp.rank) continue;
-            const uint32_t pos = atomicAdd(&fb.tile_cursor[t], 1u);
-            if (pos < fp.list_capacity) fb.tile_list[pos] = (uint32_t)gid;
+            const uint32_t pos = atomicAdd(&fb.tile_count[t], 1u);
+            if (pos < fp.bin_cap) {
+                fb.bins[(size_t)t * fp.bin_cap + pos] = (uint32_t)gid;
+            } else {
+                const uint32_t sp = atomicAdd(&cnt[C_SPILL], 1u);
+                if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t, (uint32_t)gid);
+                else atomicOr(&cnt[C_OVERFLOW], OV_SPILL);
+            }
         }
 }
 
 // ---- k_raster -------------------------------------------------------------------------------
 
-__device__ __forceinline__ TriRec rec_from_lds(const float4 *s) {
+__device__ __forceinline__ TriRec rec_from(const float4 *s) {
     TriRec r;
     float4 *d = reinterpret_cast<float4 *>(&r);
 #pragma unroll
@@ -205,8 +202,8 @@ __device__ __forceinline__ TriRec rec_from_lds(const float4 *s) {
 
 // Fragment shaders of the four legacy pipelines, evaluated for the winning triangle only.
 // Returns the pre-truncation floats; the caller truncates to uint8 exactly like the reference.
-__device__ void shade_winner(const FrameBuffers &fb, const TriRec &r, float u, float v, float w, float pre[3]) {
-    const DrawGPU &dr = fb.draws[r.draw];
+__device__ __forceinline__ void shade_winner(const DrawGPU *draws, const TriRec &r, float u, float v, float w, float pre[3]) {
+    const DrawGPU &dr = draws[r.draw];
     const float *P = dr.pos + 9 * (size_t)r.local;
     const float *N = dr.nrm + 9 * (size_t)r.local;
     const int sh = dr.shading;
@@ -291,168 +288,165 @@ __device__ __forceinline__ void resolve(float z, uint32_t id, float &bz, uint32_
     if (z < bz || (z == bz && id < bid)) { bz = z; bid = id; }
 }
 
-__global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb) {
+struct PixelCtx {
+    int px, py;
+    float Px, Py;
+    float rtminx, rtmaxx, rtminy, rtmaxy;   // reference tile-job bounds of this pixel
+};
+
+// One triangle against this lane's pixel.  ibox pixels are always in the reference's visited set;
+// outside it only ghost triangles can pass, and only where the tile clamp visits the pixel.
+__device__ __forceinline__ void raster_one(const PixelCtx &pc, const TriRec &r, uint32_t id, float &bz, uint32_t &bid) {
+    const bool in_ibox = pc.px >= lo16(r.ibx) && pc.px <= hi16(r.ibx) && pc.py >= lo16(r.iby) && pc.py <= hi16(r.iby);
+    bool test = in_ibox;
+    if (r.flags & TRI_GHOST) {
+        const bool in_gbox = pc.px >= lo16(r.gbx) && pc.px <= hi16(r.gbx) && pc.py >= lo16(r.gby) && pc.py <= hi16(r.gby);
+        if (!in_ibox && in_gbox) {
+            // draw_triangle_tile's visited rectangle in this pixel's tile job (blinn_phong_shading.cpp:208-224)
+            const float bminx = g_max(pc.rtminx, g_min(pc.rtmaxx, r.fminx));
+            const float bmaxx = g_min(pc.rtmaxx, g_max(pc.rtminx, r.fmaxx));
+            const float bminy = g_max(pc.rtminy, g_min(pc.rtmaxy, r.fminy));
+            const float bmaxy = g_min(pc.rtmaxy, g_max(pc.rtminy, r.fmaxy));
+            test = !(bminx > bmaxx || bminy > bmaxy) && pc.px >= (int)bminx && pc.px <= (int)bmaxx &&
+                   pc.py >= (int)bminy && pc.py <= (int)bmaxy;
+        }
+    }
+    if (test) {
+        float u, v, w;
+        bary(r, pc.Px, pc.Py, u, v, w);
+        if (!(u < 0 || v < 0 || w < 0)) {
+            const float z = (u * r.z0 + v * r.z1) + w * r.z2;
+            resolve(z, id, bz, bid);
+        }
+    }
+}
+
+// Speed-only XCD pairing: blocks b and b+8 (dealt to the same XCD) render horizontally adjacent
+// tiles, so both 64-B halves of each 128-B colour/depth row segment are written through one L2.
+__device__ __forceinline__ int tile_of_block(int b, int n_owned) {
+    const int g = b >> 4;
+    if ((g << 4) + 16 > n_owned) return b;          // ragged last group: identity
+    return (g << 4) + ((b & 7) << 1) + ((b >> 3) & 1);
+}
+
+__global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ float4 s_rec[CHUNK * 6];
     __shared__ uint32_t s_id[CHUNK];
     __shared__ float s_bz[TILE * TILE];
     __shared__ uint32_t s_bid[TILE * TILE];
-    __shared__ uint32_t s_cov;
+    __shared__ uint32_t s_cov, s_n;
 
-    const int tile = fp.rank + (int)blockIdx.x * fp.count;
+    const int n_owned = (fp.tiles_x * fp.tiles_y - fp.rank + fp.count - 1) / fp.count;
+    const int tile = fp.rank + tile_of_block((int)blockIdx.x, n_owned) * fp.count;
     const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
     const int X0 = tx * TILE, Y0 = ty * TILE;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
+    const DrawGPU *draws = draw_table(fp, fb, ka);
     if (tid == 0) s_cov = 0;
 
-    // raster lane mapping: wave owns rows [8w, 8w+8) of the tile, lane owns column lane&31 and
-    // rows (lane>>5) + {0,2,4,6}
-    const int px = X0 + (lane & 31);
-    const int pyb = Y0 + wave * 8 + (lane >> 5);
-    const float Px = (float)px + 0.5f;
-    const int wy0 = Y0 + wave * 8, wy1 = wy0 + 7, wx0 = X0, wx1 = X0 + TILE - 1;
-    float bz[4];
-    uint32_t bid[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { bz[k] = FLT_MAX; bid[k] = 0u; }
+    // raster lane mapping: wave -> 8x8 block (wave&1, wave>>1), lane -> pixel (lane&7, lane>>3)
+    const int bx0 = X0 + (wave & 1) * 8, by0 = Y0 + (wave >> 1) * 8;
+    PixelCtx pc;
+    pc.px = bx0 + (lane & 7);
+    pc.py = by0 + (lane >> 3);
+    pc.Px = (float)pc.px + 0.5f;
+    pc.Py = (float)pc.py + 0.5f;
+    {
+        const int rx = (pc.px / fp.rtw) * fp.rtw, ry = (pc.py / fp.rth) * fp.rth;
+        pc.rtminx = (float)rx;
+        pc.rtmaxx = (float)(min(rx + fp.rtw, fp.W) - 1);
+        pc.rtminy = (float)ry;
+        pc.rtmaxy = (float)(min(ry + fp.rth, fp.H) - 1);
+    }
+    float bz = FLT_MAX;
+    uint32_t bid = 0u;
 
-    // reference tile-job bounds of this lane's pixels (ghost path only)
-    const float rtminx = (float)((px / fp.rtw) * fp.rtw);
-    const float rtmaxx = (float)(min((px / fp.rtw) * fp.rtw + fp.rtw, fp.W) - 1);
+    const uint32_t n_bin_total = fb.tile_count[tile];
+    const uint32_t n_bin = n_bin_total < fp.bin_cap ? n_bin_total : fp.bin_cap;
+    const uint32_t *bin = fb.bins + (size_t)tile * fp.bin_cap;
+    uint32_t n_spill = 0;
+    if (n_bin_total > fp.bin_cap) {   // this tile spilled: scan the (small) spill list too
+        n_spill = cnt[C_SPILL];
+        if (n_spill > fp.spill_cap) n_spill = fp.spill_cap;
+    }
+    uint32_t n_unb = cnt[C_UNBOUNDED];
+    if (n_unb > fp.ghost_cap) n_unb = fp.ghost_cap;
 
-    const uint32_t cap = fp.list_capacity;
-    const uint32_t off = fb.tile_offset[tile];
-    uint32_t n_list = fb.tile_count[tile];
-    if (off >= cap) n_list = 0; else if (n_list > cap - off) n_list = cap - off;
-    uint32_t n_ghost = fb.counters[C_GHOST];
-    if (n_ghost > fp.ghost_capacity) n_ghost = fp.ghost_capacity;
-
-    for (int pass = 0; pass < 2; ++pass) {
-        const uint32_t n = pass == 0 ? n_list : n_ghost;
-        const uint32_t *list = pass == 0 ? fb.tile_list + off : fb.ghost_list;
+    // pass 0: the tile's bin; 1: spill entries of this tile; 2: unbounded ghosts (every tile)
+    for (int pass = 0; pass < 3; ++pass) {
+        const uint32_t n = pass == 0 ? n_bin : (pass == 1 ? n_spill : n_unb);
         for (uint32_t base = 0; base < n; base += CHUNK) {
-            const int cnt = (int)min((uint32_t)CHUNK, n - base);
             __syncthreads();
-            if (tid < cnt) {
-                const uint32_t id = list[base + tid];
-                s_id[tid] = id;
-                const float4 *src = reinterpret_cast<const float4 *>(&fb.recs[id]);
+            if (tid == 0) s_n = 0;
+            __syncthreads();
+            if (base + tid < n) {
+                uint32_t id = 0xffffffffu;
+                if (pass == 0) {
+                    id = bin[base + tid];
+                } else if (pass == 1) {
+                    const uint2 e = fb.spill[base + tid];
+                    if ((int)e.x == tile) id = e.y;
+                } else {
+                    id = fb.ghost_list[base + tid];
+                }
+                if (id != 0xffffffffu) {
+                    const uint32_t slot = atomicAdd(&s_n, 1u);
+                    s_id[slot] = id;
+                    const float4 *src = reinterpret_cast<const float4 *>(&fb.recs[id]);
 #pragma unroll
-                for (int j = 0; j < 6; ++j) s_rec[tid * 6 + j] = src[j];
+                    for (int j = 0; j < 6; ++j) s_rec[slot * 6 + j] = src[j];
+                }
             }
             __syncthreads();
-            for (int j = 0; j < cnt; ++j) {
-                const uint32_t id = s_id[j];
-                if (pass == 0) {
-                    const int4 bb = reinterpret_cast<const int4 *>(&s_rec[j * 6])[4];
-                    if (bb.y < wx0 || bb.x > wx1 || bb.w < wy0 || bb.z > wy1) continue;  // wave-uniform
-                    const TriRec r = rec_from_lds(&s_rec[j * 6]);
-                    const bool inx = px >= r.ix0 && px <= r.ix1;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int py = pyb + 2 * k;
-                        if (inx && py >= r.iy0 && py <= r.iy1) {
-                            float u, v, w;
-                            bary(r, Px, (float)py + 0.5f, u, v, w);
-                            if (!(u < 0 || v < 0 || w < 0)) {
-                                const float z = (u * r.z0 + v * r.z1) + w * r.z2;
-                                resolve(z, id, bz[k], bid[k]);
-                            }
-                        }
-                    }
-                } else {
-                    // ghost triangle: the exact visited set of the reference tile-job loop
-                    // (blinn_phong_shading.cpp:208-224) for each pixel's 80x80 reference tile
-                    const TriRec r = rec_from_lds(&s_rec[j * 6]);
-                    const float bminx = g_max(rtminx, g_min(rtmaxx, r.fminx));
-                    const float bmaxx = g_min(rtmaxx, g_max(rtminx, r.fmaxx));
-                    const bool inx = !(bminx > bmaxx) && px >= (int)bminx && px <= (int)bmaxx;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int py = pyb + 2 * k;
-                        const int rty = (py / fp.rth) * fp.rth;
-                        const float rtminy = (float)rty;
-                        const float rtmaxy = (float)(min(rty + fp.rth, fp.H) - 1);
-                        const float bminy = g_max(rtminy, g_min(rtmaxy, r.fminy));
-                        const float bmaxy = g_min(rtmaxy, g_max(rtminy, r.fmaxy));
-                        if (inx && py < fp.H && !(bminy > bmaxy) && py >= (int)bminy && py <= (int)bmaxy) {
-                            float u, v, w;
-                            bary(r, Px, (float)py + 0.5f, u, v, w);
-                            if (!(u < 0 || v < 0 || w < 0)) {
-                                const float z = (u * r.z0 + v * r.z1) + w * r.z2;
-                                resolve(z, id, bz[k], bid[k]);
-                            }
-                        }
-                    }
-                }
+            const int m = (int)s_n;
+            for (int j = 0; j < m; ++j) {
+                const uint4 bb = reinterpret_cast<const uint4 *>(&s_rec[j * 6])[4];   // ibx iby gbx gby
+                if (hi16(bb.z) < bx0 || lo16(bb.z) > bx0 + 7 || hi16(bb.w) < by0 || lo16(bb.w) > by0 + 7) continue;
+                raster_one(pc, rec_from(&s_rec[j * 6]), s_id[j], bz, bid);
             }
         }
     }
 
-    // hand the per-pixel winners to the output mapping through LDS
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int ly = wave * 8 + (lane >> 5) + 2 * k;
-        s_bz[ly * TILE + (lane & 31)] = bz[k];
-        s_bid[ly * TILE + (lane & 31)] = bid[k];
-    }
+    // hand the per-pixel winners to the row-major output mapping through LDS
+    s_bz[(pc.py - Y0) * TILE + (pc.px - X0)] = bz;
+    s_bid[(pc.py - Y0) * TILE + (pc.px - X0)] = bid;
     __syncthreads();
 
-    // output mapping: thread -> row tid>>3, 4 consecutive pixels: 8 threads cover one 32-px row
-    // (128 B of colour + 128 B of depth, full lines)
-    const int ly = tid >> 3, lx0 = (tid & 7) * 4;
-    const int y = Y0 + ly;
+    // output mapping: thread -> pixel (tid & 15, tid >> 4): 16 lanes cover one 64-B row segment of
+    // colour and one of depth
+    const int x = X0 + (tid & (TILE - 1)), y = Y0 + tid / TILE;
     uint32_t covered = 0;
-    if (y < fp.H) {
-        uint32_t rgba[4];
-        float dep[4];
-        float4 pq[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float z = s_bz[ly * TILE + lx0 + j];
-            const uint32_t id = s_bid[ly * TILE + lx0 + j];
-            dep[j] = z;
-            rgba[j] = fp.clear_rgba;
-            pq[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            const int x = X0 + lx0 + j;
-            if (z < FLT_MAX && x < fp.W) {
-                ++covered;
-                const float4 *src = reinterpret_cast<const float4 *>(&fb.recs[id]);
-                TriRec r;
-                float4 *d = reinterpret_cast<float4 *>(&r);
-#pragma unroll
-                for (int q = 0; q < 6; ++q) d[q] = src[q];
-                float u, v, w;
-                bary(r, (float)x + 0.5f, (float)y + 0.5f, u, v, w);
-                float pre[3];
-                shade_winner(fb, r, u, v, w, pre);
-                const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
-                rgba[j] = cr | (cg << 8) | (cb << 16) | (255u << 24);
-                pq[j] = make_float4(pre[0], pre[1], pre[2], 1.0f);
-            }
+    if (x < fp.W && y < fp.H) {
+        const float z = s_bz[tid];
+        const uint32_t id = s_bid[tid];
+        uint32_t rgba = fp.clear_rgba;
+        float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (z < FLT_MAX) {
+            covered = 1;
+            const TriRec r = rec_from(reinterpret_cast<const float4 *>(&fb.recs[id]));
+            float u, v, w;
+            bary(r, (float)x + 0.5f, (float)y + 0.5f, u, v, w);
+            float pre[3];
+            shade_winner(draws, r, u, v, w, pre);
+            const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
+            rgba = cr | (cg << 8) | (cb << 16) | (255u << 24);
+            pq = make_float4(pre[0], pre[1], pre[2], 1.0f);
         }
-        const int x0 = X0 + lx0;
-        const size_t crow = (size_t)(fp.H - 1 - y) * fp.W;
-        const size_t drow = (size_t)y * fp.W;
-        if (x0 + 3 < fp.W && (fp.W & 3) == 0) {
-            *reinterpret_cast<uint4 *>(fb.color + (crow + x0) * 4) = make_uint4(rgba[0], rgba[1], rgba[2], rgba[3]);
-            *reinterpret_cast<float4 *>(fb.depth + drow + x0) = make_float4(dep[0], dep[1], dep[2], dep[3]);
-        } else {
-            for (int j = 0; j < 4; ++j)
-                if (x0 + j < fp.W) {
-                    *reinterpret_cast<uint32_t *>(fb.color + (crow + x0 + j) * 4) = rgba[j];
-                    fb.depth[drow + x0 + j] = dep[j];
-                }
-        }
-        if (fb.prequant) {
-            for (int j = 0; j < 4; ++j)
-                if (x0 + j < fp.W) fb.prequant[crow + x0 + j] = pq[j];
-        }
+        const size_t co = (size_t)(fp.H - 1 - y) * fp.W + x;
+        reinterpret_cast<uint32_t *>(fb.color)[co] = rgba;
+        fb.depth[(size_t)y * fp.W + x] = z;
+        if (fb.prequant) fb.prequant[co] = pq;
     }
-    // covered-pixel count: wave reduction, one LDS atomic per wave, one global atomic per tile
+    // covered-pixel count: wave reduction, one LDS atomic per wave; per-tile stats go to their own
+    // slot (no same-address global atomics across workgroups) and the host sums them at sync
     for (int o = 32; o > 0; o >>= 1) covered += __shfl_down(covered, o);
     if (lane == 0) atomicAdd(&s_cov, covered);
     __syncthreads();
-    if (tid == 0) atomicAdd(&fb.counters[C_COVERED], s_cov);
+    if (tid == 0) {
+        fb.tile_stat[tile] = make_uint2(s_cov, n_bin_total);
+        fb.tile_count[tile] = 0u;   // bins are empty for the next frame (no memset launch)
+    }
 }
 
 }  // namespace shs_dev
@@ -461,23 +455,14 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb)
 namespace shs_internal {
 using namespace shs_dev;
 
-hipError_t launch_setup(const FrameParams &fp, const FrameBuffers &fb, hipStream_t s) {
-    if (fp.n_tris <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_setup, dim3((fp.n_tris + 255) / 256), dim3(256), 0, s, fp, fb);
+hipError_t launch_setup(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, hipStream_t s) {
+    hipLaunchKernelGGL(k_setup, dim3(fp.n_tris > 0 ? (fp.n_tris + 255) / 256 : 1), dim3(256), 0, s, fp, fb, ka);
     return hipGetLastError();
 }
-hipError_t launch_scan(const FrameParams &fp, const FrameBuffers &fb, int n_tiles, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, fp, fb, n_tiles);
-    return hipGetLastError();
-}
-hipError_t launch_scatter(const FrameParams &fp, const FrameBuffers &fb, hipStream_t s) {
-    if (fp.n_tris <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_scatter, dim3((fp.n_tris + 255) / 256), dim3(256), 0, s, fp, fb);
-    return hipGetLastError();
-}
-hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, int n_owned_tiles, hipStream_t s) {
+hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, int n_owned_tiles,
+                         hipStream_t s) {
     if (n_owned_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_raster, dim3(n_owned_tiles), dim3(256), 0, s, fp, fb);
+    hipLaunchKernelGGL(k_raster, dim3(n_owned_tiles), dim3(256), 0, s, fp, fb, ka);
     return hipGetLastError();
 }
 }  // namespace shs_internal

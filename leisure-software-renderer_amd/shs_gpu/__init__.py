@@ -176,7 +176,35 @@ class Context:
     def kernel_ms(self):
         ms = (ctypes.c_float * 4)()
         self._check(self._lib.shs_last_kernel_ms(self._h, ms))
-        return {"setup": ms[0], "scan": ms[1], "scatter": ms[2], "raster": ms[3]}
+        return {"setup": ms[0], "raster": ms[3]}
+
+    def timing_reset(self):
+        self._check(self._lib.shs_timing_reset(self._h))
+
+    def timing_read(self):
+        """-> (frames, {kernel: mean ms}) over every frame since timing_reset()."""
+        s = (ctypes.c_double * 4)()
+        n = ctypes.c_int64()
+        self._check(self._lib.shs_timing_read(self._h, s, ctypes.byref(n)))
+        k = max(n.value, 1)
+        return n.value, {"setup": s[0] / k, "raster": s[3] / k}
+
+    TRIREC_DTYPE = np.dtype([
+        ("ax", "<f4"), ("ay", "<f4"), ("v0x", "<f4"), ("v0y", "<f4"), ("v1x", "<f4"), ("v1y", "<f4"),
+        ("d00", "<f4"), ("d01", "<f4"), ("d11", "<f4"), ("denom", "<f4"), ("z0", "<f4"), ("z1", "<f4"),
+        ("z2", "<f4"), ("flags", "<u4"), ("draw", "<i4"), ("local", "<i4"), ("ibx", "<u4"), ("iby", "<u4"),
+        ("gbx", "<u4"), ("gby", "<u4"), ("fminx", "<f4"), ("fmaxx", "<f4"), ("fminy", "<f4"), ("fmaxy", "<f4")])
+
+    def debug_records(self):
+        """The last frame's per-triangle raster records (structured numpy array)."""
+        n = ctypes.c_int64()
+        self._check(self._lib.shs_debug_records(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=self.TRIREC_DTYPE)
+        self._check(self._lib.shs_debug_records(self._h, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)))
+        return out
+
+    def set_bin_capacity(self, cap: int):
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_BIN_CAPACITY, int(cap)))
 
     def set_stream(self, hip_stream):
         self._check(self._lib.shs_set_stream(self._h, ctypes.c_void_p(hip_stream)))

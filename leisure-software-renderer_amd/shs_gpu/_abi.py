@@ -22,6 +22,7 @@ SHADING_BLINN_PHONG = 3
 SHADING_NAMES = {"flat": 0, "gouraud": 1, "phong": 2, "blinn_phong": 3}
 
 FRAME_PREQUANT = 1
+OPT_BIN_CAPACITY = 1
 
 
 class LegacyDraw(ctypes.Structure):
@@ -56,6 +57,9 @@ class RasterStats(ctypes.Structure):
         ("tri_ghost", ctypes.c_uint64),
         ("bin_entries", ctypes.c_uint64),
         ("covered_pixels", ctypes.c_uint64),
+        ("tri_ghost_unbounded", ctypes.c_uint64),
+        ("spilled", ctypes.c_uint64),
+        ("max_tile_bin", ctypes.c_uint64),
     ]
 
 
@@ -64,6 +68,7 @@ _P = ctypes.c_void_p
 _F = ctypes.POINTER(ctypes.c_float)
 SIGNATURES = [
     ("shs_abi_version", ctypes.c_int, []),
+    ("shs_gpu_tile_size", ctypes.c_int, []),
     ("shs_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
     ("shs_destroy", ctypes.c_int, [_P]),
     ("shs_last_error", ctypes.c_char_p, [_P]),
@@ -79,9 +84,14 @@ SIGNATURES = [
     ("shs_get_stats", ctypes.c_int, [_P, ctypes.POINTER(RasterStats)]),
     ("shs_enable_timing", ctypes.c_int, [_P, ctypes.c_int]),
     ("shs_last_kernel_ms", ctypes.c_int, [_P, _F]),
+    ("shs_timing_reset", ctypes.c_int, [_P]),
+    ("shs_timing_read", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+    ("shs_debug_records", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    ("shs_set_option", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int64]),
     ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),
     ("shs_model_trs", ctypes.c_int, [_F, ctypes.c_float, _F, _F]),
     ("shs_mat4_mul", ctypes.c_int, [_F, _F, _F]),
+    ("shs_mat4_inverse", ctypes.c_int, [_F, _F]),
 ]
 
 

@@ -167,3 +167,20 @@ def config(name, **kw):
     if name == "c3":
         return grid_scene(1920, 1080, **kw)
     raise KeyError(name)
+
+
+def build_named(spec):
+    """Rebuild a scene from a JSON-able spec (used by tests/golden fixtures):
+    {"kind": "config", "name": "c1"} or
+    {"kind": "monkey", "width", "height", "shading", "yaw", "pitch", "rotation", "cam"} or
+    {"kind": "grid", "width", "height", "n", "shading"}."""
+    k = spec["kind"]
+    if k == "config":
+        return config(spec["name"])
+    if k == "monkey":
+        return monkey_scene(spec["width"], spec["height"], spec["shading"], yaw=spec.get("yaw", 0.0),
+                            pitch=spec.get("pitch", 0.0), rotation=spec.get("rotation", 0.0),
+                            cam_pos=tuple(spec.get("cam", CAM_POS)))
+    if k == "grid":
+        return grid_scene(spec["width"], spec["height"], n=spec.get("n", 8), shading=spec.get("shading", SHADING_PHONG))
+    raise KeyError(k)

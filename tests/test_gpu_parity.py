@@ -164,7 +164,7 @@ def test_shards_compose_to_full_frame(gpu_ctx):
     full_c, full_d = gpu_ctx.resolve()
     out_c = np.zeros_like(full_c)
     out_d = np.zeros_like(full_d)
-    T = 32
+    T = shs_gpu.lib().shs_gpu_tile_size()
     tx = (frame.width + T - 1) // T
     for rank in range(3):
         f = shs_gpu.Frame(640, 480, shard_rank=rank, shard_count=3)
@@ -196,3 +196,64 @@ def test_4k_full_frame_properties(gpu_ctx):
     assert cov.sum() > 100000
     assert np.isfinite(d1[cov]).all()
     assert (c1[..., 3] == 255).all()
+
+
+def test_bin_spill_path_exact(gpu_ctx, oracle_mod):
+    """Tiny per-tile bin capacity: most entries spill to the global list; results stay exact."""
+    import shs_gpu
+    from shs_gpu.scene import Mesh
+    rng = np.random.default_rng(23)
+    W, H = 200, 160
+    pos, nrm = _ndc_soup(rng, W, H, 600)
+    ctx = shs_gpu.Context(0)
+    try:
+        ctx.set_bin_capacity(2)
+        frame = shs_gpu.Frame(W, H)
+        stats, _ = _check(ctx, oracle_mod, frame, [_identity_draw(Mesh(pos, nrm), 3)])
+        assert stats["spilled"] > 0
+    finally:
+        ctx.close()
+
+
+def test_many_draws_device_table(gpu_ctx, oracle_mod):
+    """More draws than fit in kernel arguments -> the uniform table is uploaded to HBM."""
+    from shs_gpu import scene
+    frame, draws = scene.grid_scene(480, 360, n=3, shading=3)
+    assert len(draws) > 6
+    _check(gpu_ctx, oracle_mod, frame, draws)
+
+
+def _hair_soup(rng, W, H, n):
+    """Extremely thin slivers (third vertex within 0.02 px of the long edge): their float
+    barycentrics can pass at pixels outside their own bbox, which the reference only tests where its
+    80x80 tile clamp visits them."""
+    tris = []
+    for _ in range(n):
+        c = rng.uniform([0, 0], [W, H])
+        d = rng.normal(size=2); d /= np.linalg.norm(d)
+        L = rng.uniform(20, 400)
+        nrm = np.array([-d[1], d[0]])
+        p = np.stack([c, c + d * L, c + d * L * rng.uniform(0.05, 0.95) + nrm * rng.uniform(-0.02, 0.02)])
+        z = rng.uniform(-0.9, 0.9, size=3)
+        x = p[:, 0] / (0.5 * (W - 1)) - 1.0
+        y = 1.0 - p[:, 1] / (0.5 * (H - 1))
+        tris.append(np.stack([x, y, z], axis=1).reshape(9))
+    pos = np.asarray(tris, dtype=np.float32)
+    return pos, rng.normal(size=pos.shape).astype(np.float32)
+
+
+def test_hair_slivers_tile_clamp_ghosts(gpu_ctx, oracle_mod):
+    """The reference's tile clamp changes the image for these slivers (ghost pixels exist: the oracle's
+    80x80-tile render differs from its single-tile render); the GPU matches both bit-exactly."""
+    import shs_gpu
+    from shs_gpu.scene import Mesh
+    rng = np.random.default_rng(99)
+    W, H = 400, 300
+    pos, nrm = _hair_soup(rng, W, H, 3000)
+    draw = _identity_draw(Mesh(pos, nrm), 3)
+    c80, d80, _ = oracle_mod.render_legacy(W, H, [draw], tile=(80, 80), threads=8)
+    c1, d1, _ = oracle_mod.render_legacy(W, H, [draw], tile=(W, H), threads=8)
+    assert not np.array_equal(d80.view(np.uint32), d1.view(np.uint32)), "scene has no tile-clamp ghost pixels"
+    stats, _ = _check(gpu_ctx, oracle_mod, shs_gpu.Frame(W, H, ref_tile=(80, 80)), [draw])
+    assert stats["tri_ghost_unbounded"] > 0
+    _check(gpu_ctx, oracle_mod, shs_gpu.Frame(W, H, ref_tile=(W, H)), [draw])

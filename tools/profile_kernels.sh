@@ -1,0 +1,12 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + stats of a bench run; summary CSV copied to profiles/<tag>_kernel_stats.csv
+# usage (on the GPU box): bash tools/profile_kernels.sh <tag> [bench args...]
+set -e
+TAG=$1; shift
+R=$(pwd)
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --no-pmc --no-cpu "$@" > "$R/gpurun_out/prof_$TAG.log" 2>&1
+cd "$R"
+cp gpurun_out/prof_$TAG/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
+cut -d, -f1-4 gpurun_out/${TAG}_kernel_stats.csv
