@@ -45,6 +45,7 @@ struct shs_ctx {
 
     DevBuf<DrawGPU> draws;
     DevBuf<TriRec> recs;
+    DevBuf<shs_dev::ShadeRec> shade;
     DevBuf<uint32_t> tile_count;     // zero between frames
     DevBuf<uint32_t> bins;           // n_tiles * bin_cap
     DevBuf<uint2> spill;
@@ -175,7 +176,7 @@ int shs_destroy(shs_ctx *ctx) {
         if (m.pos) (void)hipFree(m.pos);
         if (m.nrm) (void)hipFree(m.nrm);
     }
-    release(ctx->draws); release(ctx->recs); release(ctx->tile_count); release(ctx->bins);
+    release(ctx->draws); release(ctx->recs); release(ctx->shade); release(ctx->tile_count); release(ctx->bins);
     release(ctx->spill); release(ctx->ghost); release(ctx->counters); release(ctx->tile_stat);
     release(ctx->color); release(ctx->depth); release(ctx->prequant);
     for (int i = 0; i < 2; ++i) {
@@ -294,7 +295,8 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (total > 0x3fffffff) { ctx->err = "too many triangles in one frame"; return SHS_ERR_INVALID; }
     const int n_tris = (int)total;
 
-    if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1))) return SHS_ERR_HIP;
+    if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1)) || ensure(ctx, ctx->shade, (size_t)std::max(n_tris, 1)))
+        return SHS_ERR_HIP;
     if (ctx->tile_count.cap < (size_t)n_tiles || !ctx->tile_count.p) {
         if (ensure(ctx, ctx->tile_count, n_tiles)) return SHS_ERR_HIP;
         HIP_TRY(ctx, hipMemsetAsync(ctx->tile_count.p, 0, ctx->tile_count.cap * sizeof(uint32_t), ctx->stream));
@@ -365,7 +367,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.parity = ctx->frame_index & 1u;
 
     FrameBuffers fb;
-    fb.draws = ctx->draws.p; fb.recs = ctx->recs.p; fb.tile_count = ctx->tile_count.p; fb.bins = ctx->bins.p;
+    fb.draws = ctx->draws.p; fb.recs = ctx->recs.p; fb.shade = ctx->shade.p; fb.tile_count = ctx->tile_count.p; fb.bins = ctx->bins.p;
     fb.spill = ctx->spill.p; fb.ghost_list = ctx->ghost.p; fb.counters = ctx->counters.p;
     fb.tile_stat = ctx->tile_stat.p;
     fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;

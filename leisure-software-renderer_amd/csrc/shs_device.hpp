@@ -47,6 +47,17 @@ struct alignas(16) TriRec {
 };
 static_assert(sizeof(TriRec) == 96, "TriRec must stay 96 B");
 
+// Per-triangle shading varyings written by k_setup (the legacy VS outputs of the three corners the
+// winning pixels interpolate), 80 B: Blinn-Phong/Phong: world_pos[3] then normalize(N*n)[3];
+// Gouraud: the clamped per-vertex colour[3] (carried in world_pos, gouraud_shading.cpp:71);
+// Flat: mat3(mv)*n[3] (flat_shading.cpp:54).
+struct alignas(16) ShadeRec {
+    float v[18];
+    int32_t shading;
+    int32_t draw;
+};
+static_assert(sizeof(ShadeRec) == 80, "ShadeRec must stay 80 B");
+
 constexpr uint32_t TRI_CULLED = 1u;
 constexpr uint32_t TRI_GHOST = 2u;       // tile-clamp pixels near the bbox may pass: test them
 constexpr uint32_t TRI_UNBOUNDED = 4u;   // ... anywhere on screen (global list, every tile)
@@ -55,7 +66,7 @@ __device__ __forceinline__ uint32_t pack16(int lo, int hi) { return (uint32_t)(l
 __device__ __forceinline__ int lo16(uint32_t v) { return (int)(int16_t)(v & 0xffffu); }
 __device__ __forceinline__ int hi16(uint32_t v) { return (int)(int16_t)(v >> 16); }
 
-constexpr int TILE = 16;             // GPU screen tile (16x16 px, one 256-thread workgroup)
+constexpr int TILE = 32;             // GPU screen tile (32x32 px, one 256-thread workgroup)
 constexpr int CHUNK = 256;           // triangle records staged in LDS per pass
 
 // counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one)
@@ -86,6 +97,7 @@ struct FrameParams {
 struct FrameBuffers {
     const DrawGPU *draws;            // device draw table (n_draws > KARG_DRAWS)
     TriRec *recs;
+    ShadeRec *shade;                 // n_tris
     uint32_t *tile_count;            // n_tiles, zero between frames (k_raster re-zeroes)
     uint32_t *bins;                  // n_tiles * bin_cap
     uint2 *spill;                    // (tile, tri) pairs beyond bin_cap

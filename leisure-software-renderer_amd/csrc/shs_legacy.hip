@@ -8,11 +8,12 @@
 //             per-triangle half of barycentric_coordinate, a 96-B raster record, and the triangle
 //             id appended straight into the per-tile bins its bin box touches (unordered; a spill
 //             list past the bin capacity).
-//   k_raster  one 256-thread workgroup per 16x16 tile, one pixel per lane (8x8 block per wave):
+//   k_raster  one 256-thread workgroup per 32x32 tile (8x8 blocks, a column of four per wave):
 //             stage the tile's records in LDS, resolve every pixel to the lexicographic minimum
 //             (z, submission index) -- identical to the reference's in-order strict-less z test
-//             (the first triangle with the minimal z wins) -- then shade only the winners and write
-//             colour (canvas rows) and depth (screen rows) once, with the clear fused.
+//             (the first triangle with the minimal z wins) -- then shade only the winners from the
+//             per-triangle varyings k_setup wrote, and write colour (canvas rows) and depth (screen
+//             rows) once, with the clear fused (empty tiles take a clear-only fast path).
 // The z-buffer never round-trips through HBM: HBM sees each input once and each output once.
 //
 // Tile-clamp semantics.  draw_triangle_tile clamps a triangle's bbox to the 80x80 tile job that
@@ -38,7 +39,7 @@ namespace shs_dev {
 // E < max(...), i.e. outside the box expanded by 2*W*m0, m0 = e0 / (1 - 2(ex*Wx + ey*Wy)).
 // Returns the expansion (dgx, dgy) >= 0, or (-1, -1) if no bound exists (then every visited pixel
 // is tested).
-__device__ __noinline__ double2 danger_margin(const TriRec &r) {
+__device__ __forceinline__ double2 danger_margin(const TriRec &r) {
     const double2 none = make_double2(-1.0, -1.0);
     const double u = 5.9604644775390625e-08;  // 2^-24
     const double a = fabs((double)r.v0x), b = fabs((double)r.v0y);
@@ -139,8 +140,8 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
         ix1 = floor_clamped(r.fmaxx, -1, fp.W - 1);
         iy0 = floor_clamped(r.fminy, 0, fp.H);
         iy1 = floor_clamped(r.fmaxy, -1, fp.H - 1);
-        // Straight-line selects after one out-of-line call: ROCm 7.2 hipcc mis-allocated a value
-        // kept live across an inlined danger_margin() on a divergent path (found by
+        // Straight-line selects after the bound: ROCm 7.2 hipcc mis-allocated a value kept live
+        // across danger_margin() on a divergent path when this was an if / else-if chain (found by
         // test_config_blinn_phong[c1]); keep this region free of values live across branches.
         const bool dfin = finitef(r.d00) && finitef(r.d01) && finitef(r.d11) && finitef(r.denom);
         const double2 dg = dfin ? danger_margin(r) : make_double2(-1.0, -1.0);
@@ -165,6 +166,54 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
         for (int j = 0; j < 6; ++j) dst[j] = src[j];
     }
     if (flags & TRI_CULLED) return;
+
+    // Shading varyings of the three corners (the VS outputs the FS interpolates), computed once per
+    // triangle instead of once per winning pixel.
+    {
+        ShadeRec sr;
+        sr.shading = dr.shading;
+        sr.draw = lo;
+        const float *N = dr.nrm + 9 * (size_t)local;
+        if (dr.shading == 0) {
+            // Flat VS (flat_shading.cpp:54): normal = mat3(mv) * n
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const f3 n = m3v(dr.nmat, f3{N[3 * k], N[3 * k + 1], N[3 * k + 2]});
+                sr.v[3 * k] = n.x; sr.v[3 * k + 1] = n.y; sr.v[3 * k + 2] = n.z;
+            }
+        } else {
+            const f3 L = {dr.light[0], dr.light[1], dr.light[2]};
+            const f3 cam = {dr.cam[0], dr.cam[1], dr.cam[2]};
+            const f3 oc = {dr.ocol[0], dr.ocol[1], dr.ocol[2]};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                float x, y, z, ww;
+                m4p(dr.model, p[3 * k], p[3 * k + 1], p[3 * k + 2], x, y, z, ww);
+                const f3 wp = {x, y, z};
+                const f3 nr = normalize3(m3v(dr.nmat, f3{N[3 * k], N[3 * k + 1], N[3 * k + 2]}));
+                if (dr.shading == 1) {
+                    // Gouraud VS (gouraud_shading.cpp:46-77): Blinn-Phong per vertex, shininess 32
+                    const f3 viewDir = normalize3(sub3(cam, wp));
+                    const float diff = g_max(dot3(nr, L), 0.0f);
+                    const f3 half = normalize3(add3(L, viewDir));
+                    const float spec = (float)pow((double)g_max(dot3(nr, half), 0.0f), 32.0);
+                    const float sum = (0.15f + diff * 1.0f) + (0.5f * spec) * 1.0f;
+                    sr.v[3 * k] = g_clamp01(sum * oc.x);
+                    sr.v[3 * k + 1] = g_clamp01(sum * oc.y);
+                    sr.v[3 * k + 2] = g_clamp01(sum * oc.z);
+                } else {
+                    // Phong / Blinn-Phong VS (blinn_phong_shading.cpp:48-57)
+                    sr.v[3 * k] = wp.x; sr.v[3 * k + 1] = wp.y; sr.v[3 * k + 2] = wp.z;
+                    sr.v[9 + 3 * k] = nr.x; sr.v[9 + 3 * k + 1] = nr.y; sr.v[9 + 3 * k + 2] = nr.z;
+                }
+            }
+        }
+        const float4 *src = reinterpret_cast<const float4 *>(&sr);
+        float4 *dst = reinterpret_cast<float4 *>(&fb.shade[gid]);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) dst[j] = src[j];
+    }
+
     atomicAdd(&cnt[C_SETUP], 1u);
     if (flags & TRI_GHOST) atomicAdd(&cnt[C_GHOST], 1u);
     if (flags & TRI_UNBOUNDED) {
@@ -175,6 +224,32 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
     }
     if (gx0 > gx1 || gy0 > gy1) return;
     const int tx0 = gx0 / TILE, tx1 = gx1 / TILE, ty0 = gy0 / TILE, ty1 = gy1 / TILE;
+    const int ntx = tx1 - tx0 + 1, nty = ty1 - ty0 + 1;
+    if (ntx * nty <= 4) {
+        // common case: issue every bin append before consuming any position (one round trip)
+        int t[4];
+        uint32_t pos[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int kx = tx0 + (k % ntx), ky = ty0 + (k / ntx);
+            t[k] = (k < ntx * nty) ? ky * fp.tiles_x + kx : -1;
+            if (t[k] >= 0 && t[k] % fp.count != fp.rank) t[k] = -1;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pos[k] = t[k] >= 0 ? atomicAdd(&fb.tile_count[t[k]], 1u) : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (t[k] < 0) continue;
+            if (pos[k] < fp.bin_cap) {
+                fb.bins[(size_t)t[k] * fp.bin_cap + pos[k]] = (uint32_t)gid;
+            } else {
+                const uint32_t sp = atomicAdd(&cnt[C_SPILL], 1u);
+                if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t[k], (uint32_t)gid);
+                else atomicOr(&cnt[C_OVERFLOW], OV_SPILL);
+            }
+        }
+        return;
+    }
     for (int ty = ty0; ty <= ty1; ++ty)
         for (int tx = tx0; tx <= tx1; ++tx) {
             const int t = ty * fp.tiles_x + tx;
@@ -200,20 +275,14 @@ __device__ __forceinline__ TriRec rec_from(const float4 *s) {
     return r;
 }
 
-// Fragment shaders of the four legacy pipelines, evaluated for the winning triangle only.
-// Returns the pre-truncation floats; the caller truncates to uint8 exactly like the reference.
-__device__ __forceinline__ void shade_winner(const DrawGPU *draws, const TriRec &r, float u, float v, float w, float pre[3]) {
-    const DrawGPU &dr = draws[r.draw];
-    const float *P = dr.pos + 9 * (size_t)r.local;
-    const float *N = dr.nrm + 9 * (size_t)r.local;
-    const int sh = dr.shading;
-    if (sh == 0) {
-        // Flat (flat_shading.cpp:46-98): VS normal = mat3(mv) * n; interpolated normal normalised;
-        // FS: n = normalize(n), l = normalize(light_dir_view), intensity = min(0.2 + max(n.l,0), 1)
-        f3 n[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) n[k] = m3v(dr.nmat, f3{N[3 * k], N[3 * k + 1], N[3 * k + 2]});
-        const f3 in_n = normalize3(add3(add3(sc3(n[0], u), sc3(n[1], v)), sc3(n[2], w)));
+// Fragment shaders of the four legacy pipelines for the winning triangle, from its per-corner
+// varyings.  Returns the pre-truncation floats; the caller truncates to uint8 like the reference.
+__device__ __forceinline__ void shade_winner(const DrawGPU &dr, const ShadeRec &sr, float u, float v, float w, float pre[3]) {
+    const f3 a0 = {sr.v[0], sr.v[1], sr.v[2]}, a1 = {sr.v[3], sr.v[4], sr.v[5]}, a2 = {sr.v[6], sr.v[7], sr.v[8]};
+    if (sr.shading == 0) {
+        // Flat FS (flat_shading.cpp:69-98): the interpolated normal is normalised in
+        // draw_triangle_tile and again in the FS; intensity = min(0.2 + max(n.l, 0), 1)
+        const f3 in_n = normalize3(add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w)));
         const f3 nn = normalize3(in_n);
         const f3 l = {dr.light[0], dr.light[1], dr.light[2]};
         const float diffuse = g_max(dot3(nn, l), 0.0f);
@@ -224,44 +293,25 @@ __device__ __forceinline__ void shade_winner(const DrawGPU *draws, const TriRec 
         pre[2] = dr.colf[2] * intensity;
         return;
     }
-    f3 wp[3], nr[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        float x, y, z, ww;
-        m4p(dr.model, P[3 * k], P[3 * k + 1], P[3 * k + 2], x, y, z, ww);
-        wp[k] = f3{x, y, z};
-        nr[k] = normalize3(m3v(dr.nmat, f3{N[3 * k], N[3 * k + 1], N[3 * k + 2]}));
-    }
-    const f3 L = {dr.light[0], dr.light[1], dr.light[2]};
-    const f3 cam = {dr.cam[0], dr.cam[1], dr.cam[2]};
-    const f3 oc = {dr.ocol[0], dr.ocol[1], dr.ocol[2]};
-    if (sh == 1) {
-        // Gouraud (gouraud_shading.cpp:46-89): Blinn-Phong (shininess 32, powf) per vertex, the
-        // clamped colour interpolated through world_pos, FS truncates colour*255.
-        f3 col[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const f3 viewDir = normalize3(sub3(cam, wp[k]));
-            const float diff = g_max(dot3(nr[k], L), 0.0f);
-            const f3 half = normalize3(add3(L, viewDir));
-            const float spec = (float)pow((double)g_max(dot3(nr[k], half), 0.0f), 32.0);
-            const float s = (0.15f + diff * 1.0f) + (0.5f * spec) * 1.0f;
-            col[k] = f3{g_clamp01(s * oc.x), g_clamp01(s * oc.y), g_clamp01(s * oc.z)};
-        }
-        const f3 c = add3(add3(sc3(col[0], u), sc3(col[1], v)), sc3(col[2], w));
+    if (sr.shading == 1) {
+        // Gouraud FS (gouraud_shading.cpp:80-89): interpolated colour * 255
+        const f3 c = add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w));
         pre[0] = c.x * 255.0f;
         pre[1] = c.y * 255.0f;
         pre[2] = c.z * 255.0f;
         return;
     }
     // Phong / Blinn-Phong: normal and world position interpolated (blinn_phong_shading.cpp:235-236)
-    const f3 in_n = normalize3(add3(add3(sc3(nr[0], u), sc3(nr[1], v)), sc3(nr[2], w)));
-    const f3 in_w = add3(add3(sc3(wp[0], u), sc3(wp[1], v)), sc3(wp[2], w));
+    const f3 n0 = {sr.v[9], sr.v[10], sr.v[11]}, n1 = {sr.v[12], sr.v[13], sr.v[14]}, n2 = {sr.v[15], sr.v[16], sr.v[17]};
+    const f3 in_n = normalize3(add3(add3(sc3(n0, u), sc3(n1, v)), sc3(n2, w)));
+    const f3 in_w = add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w));
+    const f3 L = {dr.light[0], dr.light[1], dr.light[2]};
+    const f3 cam = {dr.cam[0], dr.cam[1], dr.cam[2]};
     const f3 norm = normalize3(in_n);
     const f3 viewDir = normalize3(sub3(cam, in_w));
     const float diff = g_max(dot3(norm, L), 0.0f);
     float specular;
-    if (sh == 2) {
+    if (sr.shading == 2) {
         // Phong (phong_shading.cpp:70-108): reflect(-L, N) = I - N*dot(N,I)*2, spec 0.8,
         // pow(float, int 32) resolves to std::pow(double, double)
         const f3 I = {-L.x, -L.y, -L.z};
@@ -276,65 +326,74 @@ __device__ __forceinline__ void shade_winner(const DrawGPU *draws, const TriRec 
         const float spec = (float)pow((double)g_max(dot3(norm, half), 0.0f), 64.0);
         specular = (0.5f * spec) * 1.0f;
     }
+    const f3 oc = {dr.ocol[0], dr.ocol[1], dr.ocol[2]};
     const float s = (0.15f + diff * 1.0f) + specular;
     pre[0] = g_clamp01(s * oc.x) * 255.0f;
     pre[1] = g_clamp01(s * oc.y) * 255.0f;
     pre[2] = g_clamp01(s * oc.z) * 255.0f;
 }
 
-__device__ __forceinline__ void resolve(float z, uint32_t id, float &bz, uint32_t &bid) {
-    // In-order strict-less z test == lexicographic min of (z, submission index); NaN never wins,
-    // z == FLT_MAX never beats the FLT_MAX clear (bid sentinel 0 makes id < bid false).
-    if (z < bz || (z == bz && id < bid)) { bz = z; bid = id; }
-}
-
-struct PixelCtx {
-    int px, py;
-    float Px, Py;
-    float rtminx, rtmaxx, rtminy, rtmaxy;   // reference tile-job bounds of this pixel
+// Per-pixel winner state: depth, submission index and the winner's (v, w) (u is recomputed
+// exactly as (1 - v) - w, shs_renderer.hpp:819).
+struct Best {
+    float z;
+    uint32_t id;
+    float v, w;
 };
 
-// One triangle against this lane's pixel.  ibox pixels are always in the reference's visited set;
-// outside it only ghost triangles can pass, and only where the tile clamp visits the pixel.
-__device__ __forceinline__ void raster_one(const PixelCtx &pc, const TriRec &r, uint32_t id, float &bz, uint32_t &bid) {
-    const bool in_ibox = pc.px >= lo16(r.ibx) && pc.px <= hi16(r.ibx) && pc.py >= lo16(r.iby) && pc.py <= hi16(r.iby);
+__device__ __forceinline__ void resolve(float z, uint32_t id, float v, float w, Best &b) {
+    // In-order strict-less z test == lexicographic min of (z, submission index); NaN never wins,
+    // z == FLT_MAX never beats the FLT_MAX clear (id sentinel 0 makes id < b.id false).
+    if (z < b.z || (z == b.z && id < b.id)) { b.z = z; b.id = id; b.v = v; b.w = w; }
+}
+
+// One triangle against one pixel.  ibox pixels are always in the reference's visited set; outside
+// it only ghost triangles can pass, and only where the tile clamp visits the pixel.
+__device__ __forceinline__ void raster_px(int px, int py, float rtminx, float rtmaxx, float rtminy, float rtmaxy,
+                                          const TriRec &r, uint32_t id, Best &b) {
+    const bool in_ibox = px >= lo16(r.ibx) && px <= hi16(r.ibx) && py >= lo16(r.iby) && py <= hi16(r.iby);
     bool test = in_ibox;
     if (r.flags & TRI_GHOST) {
-        const bool in_gbox = pc.px >= lo16(r.gbx) && pc.px <= hi16(r.gbx) && pc.py >= lo16(r.gby) && pc.py <= hi16(r.gby);
+        const bool in_gbox = px >= lo16(r.gbx) && px <= hi16(r.gbx) && py >= lo16(r.gby) && py <= hi16(r.gby);
         if (!in_ibox && in_gbox) {
             // draw_triangle_tile's visited rectangle in this pixel's tile job (blinn_phong_shading.cpp:208-224)
-            const float bminx = g_max(pc.rtminx, g_min(pc.rtmaxx, r.fminx));
-            const float bmaxx = g_min(pc.rtmaxx, g_max(pc.rtminx, r.fmaxx));
-            const float bminy = g_max(pc.rtminy, g_min(pc.rtmaxy, r.fminy));
-            const float bmaxy = g_min(pc.rtmaxy, g_max(pc.rtminy, r.fmaxy));
-            test = !(bminx > bmaxx || bminy > bmaxy) && pc.px >= (int)bminx && pc.px <= (int)bmaxx &&
-                   pc.py >= (int)bminy && pc.py <= (int)bmaxy;
+            const float bminx = g_max(rtminx, g_min(rtmaxx, r.fminx));
+            const float bmaxx = g_min(rtmaxx, g_max(rtminx, r.fmaxx));
+            const float bminy = g_max(rtminy, g_min(rtmaxy, r.fminy));
+            const float bmaxy = g_min(rtmaxy, g_max(rtminy, r.fmaxy));
+            test = !(bminx > bmaxx || bminy > bmaxy) && px >= (int)bminx && px <= (int)bmaxx && py >= (int)bminy &&
+                   py <= (int)bmaxy;
         }
     }
     if (test) {
         float u, v, w;
-        bary(r, pc.Px, pc.Py, u, v, w);
+        bary(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);
         if (!(u < 0 || v < 0 || w < 0)) {
             const float z = (u * r.z0 + v * r.z1) + w * r.z2;
-            resolve(z, id, bz, bid);
+            resolve(z, id, v, w, b);
         }
     }
 }
 
-// Speed-only XCD pairing: blocks b and b+8 (dealt to the same XCD) render horizontally adjacent
-// tiles, so both 64-B halves of each 128-B colour/depth row segment are written through one L2.
+// Speed-only XCD grouping: blocks b and b+8 (dealt to the same XCD) render horizontally adjacent
+// tiles, so neighbouring row segments are written through one L2.
 __device__ __forceinline__ int tile_of_block(int b, int n_owned) {
     const int g = b >> 4;
     if ((g << 4) + 16 > n_owned) return b;          // ragged last group: identity
     return (g << 4) + ((b & 7) << 1) + ((b >> 3) & 1);
 }
 
+constexpr int NB = TILE / 8;   // 8x8 blocks per tile edge (4): wave w owns block column w
+
 __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
+    // LDS carve: records (reused for the winners' (v, w) after the raster passes), ids, z, id
     __shared__ float4 s_rec[CHUNK * 6];
     __shared__ uint32_t s_id[CHUNK];
     __shared__ float s_bz[TILE * TILE];
     __shared__ uint32_t s_bid[TILE * TILE];
     __shared__ uint32_t s_cov, s_n;
+    float *s_bv = reinterpret_cast<float *>(s_rec);
+    float *s_bw = s_bv + TILE * TILE;
 
     const int n_owned = (fp.tiles_x * fp.tiles_y - fp.rank + fp.count - 1) / fp.count;
     const int tile = fp.rank + tile_of_block((int)blockIdx.x, n_owned) * fp.count;
@@ -343,26 +402,50 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
     const DrawGPU *draws = draw_table(fp, fb, ka);
-    if (tid == 0) s_cov = 0;
-
-    // raster lane mapping: wave -> 8x8 block (wave&1, wave>>1), lane -> pixel (lane&7, lane>>3)
-    const int bx0 = X0 + (wave & 1) * 8, by0 = Y0 + (wave >> 1) * 8;
-    PixelCtx pc;
-    pc.px = bx0 + (lane & 7);
-    pc.py = by0 + (lane >> 3);
-    pc.Px = (float)pc.px + 0.5f;
-    pc.Py = (float)pc.py + 0.5f;
-    {
-        const int rx = (pc.px / fp.rtw) * fp.rtw, ry = (pc.py / fp.rth) * fp.rth;
-        pc.rtminx = (float)rx;
-        pc.rtmaxx = (float)(min(rx + fp.rtw, fp.W) - 1);
-        pc.rtminy = (float)ry;
-        pc.rtmaxy = (float)(min(ry + fp.rth, fp.H) - 1);
-    }
-    float bz = FLT_MAX;
-    uint32_t bid = 0u;
 
     const uint32_t n_bin_total = fb.tile_count[tile];
+    uint32_t n_unb = cnt[C_UNBOUNDED];
+    if (n_unb > fp.ghost_cap) n_unb = fp.ghost_cap;
+
+    // output mapping: thread -> row tid>>3, 4 consecutive pixels (16-B colour and depth stores;
+    // 8 threads cover a 128-B row segment of each)
+    const int oy = Y0 + (tid >> 3), ox = X0 + (tid & 7) * 4;
+    const size_t crow = (size_t)(fp.H - 1 - oy) * fp.W, drow = (size_t)oy * fp.W;
+    const bool vec_ok = ox + 3 < fp.W && (fp.W & 3) == 0;
+
+    if (n_bin_total == 0 && n_unb == 0) {
+        // empty tile: the fused clear (Canvas::fill_pixel + ZBuffer::clear), nothing else
+        if (oy < fp.H) {
+            const uint32_t c = fp.clear_rgba;
+            if (vec_ok) {
+                *reinterpret_cast<uint4 *>(fb.color + (crow + ox) * 4) = make_uint4(c, c, c, c);
+                *reinterpret_cast<float4 *>(fb.depth + drow + ox) = make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+            } else {
+                for (int j = 0; j < 4; ++j)
+                    if (ox + j < fp.W) {
+                        reinterpret_cast<uint32_t *>(fb.color)[crow + ox + j] = c;
+                        fb.depth[drow + ox + j] = FLT_MAX;
+                    }
+            }
+            if (fb.prequant)
+                for (int j = 0; j < 4; ++j)
+                    if (ox + j < fp.W) fb.prequant[crow + ox + j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (tid == 0) fb.tile_stat[tile] = make_uint2(0u, 0u);
+        return;
+    }
+    if (tid == 0) s_cov = 0;
+
+    // raster mapping: wave w owns the 8-px column of blocks (w, 0..3); lane -> (lane&7, lane>>3)
+    const int px = X0 + wave * 8 + (lane & 7);
+    const int py0 = Y0 + (lane >> 3);
+    const int rx = (px / fp.rtw) * fp.rtw;
+    const float rtminx = (float)rx, rtmaxx = (float)(min(rx + fp.rtw, fp.W) - 1);
+    const int bxl = X0 + wave * 8;
+    Best best[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) { best[i].z = FLT_MAX; best[i].id = 0u; best[i].v = 0.f; best[i].w = 0.f; }
+
     const uint32_t n_bin = n_bin_total < fp.bin_cap ? n_bin_total : fp.bin_cap;
     const uint32_t *bin = fb.bins + (size_t)tile * fp.bin_cap;
     uint32_t n_spill = 0;
@@ -370,8 +453,6 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
         n_spill = cnt[C_SPILL];
         if (n_spill > fp.spill_cap) n_spill = fp.spill_cap;
     }
-    uint32_t n_unb = cnt[C_UNBOUNDED];
-    if (n_unb > fp.ghost_cap) n_unb = fp.ghost_cap;
 
     // pass 0: the tile's bin; 1: spill entries of this tile; 2: unbounded ghosts (every tile)
     for (int pass = 0; pass < 3; ++pass) {
@@ -402,41 +483,88 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
             const int m = (int)s_n;
             for (int j = 0; j < m; ++j) {
                 const uint4 bb = reinterpret_cast<const uint4 *>(&s_rec[j * 6])[4];   // ibx iby gbx gby
-                if (hi16(bb.z) < bx0 || lo16(bb.z) > bx0 + 7 || hi16(bb.w) < by0 || lo16(bb.w) > by0 + 7) continue;
-                raster_one(pc, rec_from(&s_rec[j * 6]), s_id[j], bz, bid);
+                if (hi16(bb.z) < bxl || lo16(bb.z) > bxl + 7 || hi16(bb.w) < Y0 || lo16(bb.w) > Y0 + TILE - 1) continue;
+                const TriRec r = rec_from(&s_rec[j * 6]);
+                const uint32_t id = s_id[j];
+#pragma unroll
+                for (int i = 0; i < NB; ++i) {
+                    const int by = Y0 + 8 * i;
+                    if (hi16(bb.w) < by || lo16(bb.w) > by + 7) continue;        // block cull (uniform)
+                    const int py = py0 + 8 * i;
+                    const int ry = (py / fp.rth) * fp.rth;
+                    raster_px(px, py, rtminx, rtmaxx, (float)ry, (float)(min(ry + fp.rth, fp.H) - 1), r, id, best[i]);
+                }
             }
         }
     }
+    __syncthreads();   // s_rec is reused below
 
-    // hand the per-pixel winners to the row-major output mapping through LDS
-    s_bz[(pc.py - Y0) * TILE + (pc.px - X0)] = bz;
-    s_bid[(pc.py - Y0) * TILE + (pc.px - X0)] = bid;
+    // hand the winners to the row-major output mapping through LDS
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int o = (py0 - Y0 + 8 * i) * TILE + (px - X0);
+        s_bz[o] = best[i].z;
+        s_bid[o] = best[i].id;
+        s_bv[o] = best[i].v;
+        s_bw[o] = best[i].w;
+    }
     __syncthreads();
 
-    // output mapping: thread -> pixel (tid & 15, tid >> 4): 16 lanes cover one 64-B row segment of
-    // colour and one of depth
-    const int x = X0 + (tid & (TILE - 1)), y = Y0 + tid / TILE;
     uint32_t covered = 0;
-    if (x < fp.W && y < fp.H) {
-        const float z = s_bz[tid];
-        const uint32_t id = s_bid[tid];
-        uint32_t rgba = fp.clear_rgba;
-        float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (z < FLT_MAX) {
-            covered = 1;
-            const TriRec r = rec_from(reinterpret_cast<const float4 *>(&fb.recs[id]));
-            float u, v, w;
-            bary(r, (float)x + 0.5f, (float)y + 0.5f, u, v, w);
-            float pre[3];
-            shade_winner(draws, r, u, v, w, pre);
-            const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
-            rgba = cr | (cg << 8) | (cb << 16) | (255u << 24);
-            pq = make_float4(pre[0], pre[1], pre[2], 1.0f);
+    if (oy < fp.H) {
+        uint32_t rgba[4];
+        float dep[4];
+        float4 pq[4];
+        const int lo = (tid >> 3) * TILE + (tid & 7) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            dep[j] = s_bz[lo + j];
+            rgba[j] = fp.clear_rgba;
+            pq[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        const size_t co = (size_t)(fp.H - 1 - y) * fp.W + x;
-        reinterpret_cast<uint32_t *>(fb.color)[co] = rgba;
-        fb.depth[(size_t)y * fp.W + x] = z;
-        if (fb.prequant) fb.prequant[co] = pq;
+        // shade the winners two pixels at a time: both varyings loads in flight before any math
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            ShadeRec sr[2];
+            bool win[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int j = 2 * h + q;
+                win[q] = dep[j] < FLT_MAX && ox + j < fp.W;
+                if (win[q]) {
+                    const float4 *src = reinterpret_cast<const float4 *>(&fb.shade[s_bid[lo + j]]);
+                    float4 *d = reinterpret_cast<float4 *>(&sr[q]);
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) d[k] = src[k];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int j = 2 * h + q;
+                if (!win[q]) continue;
+                ++covered;
+                const float v = s_bv[lo + j], w = s_bw[lo + j];
+                const float u = (1.0f - v) - w;
+                float pre[3];
+                shade_winner(draws[sr[q].draw], sr[q], u, v, w, pre);
+                const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
+                rgba[j] = cr | (cg << 8) | (cb << 16) | (255u << 24);
+                pq[j] = make_float4(pre[0], pre[1], pre[2], 1.0f);
+            }
+        }
+        if (vec_ok) {
+            *reinterpret_cast<uint4 *>(fb.color + (crow + ox) * 4) = make_uint4(rgba[0], rgba[1], rgba[2], rgba[3]);
+            *reinterpret_cast<float4 *>(fb.depth + drow + ox) = make_float4(dep[0], dep[1], dep[2], dep[3]);
+        } else {
+            for (int j = 0; j < 4; ++j)
+                if (ox + j < fp.W) {
+                    reinterpret_cast<uint32_t *>(fb.color)[crow + ox + j] = rgba[j];
+                    fb.depth[drow + ox + j] = dep[j];
+                }
+        }
+        if (fb.prequant)
+            for (int j = 0; j < 4; ++j)
+                if (ox + j < fp.W) fb.prequant[crow + ox + j] = pq[j];
     }
     // covered-pixel count: wave reduction, one LDS atomic per wave; per-tile stats go to their own
     // slot (no same-address global atomics across workgroups) and the host sums them at sync
