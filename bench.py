@@ -63,6 +63,7 @@ def build_workload(name, rank=0):
 def run_gpu(args, rank, local_rank, world, dist):
     import shs_gpu
     frame, draws = build_workload(args.config, rank)
+    frame.debug_flags = args.debug_flags   # timing experiments only (wrong images)
     ctx = shs_gpu.Context(local_rank)
     prepared = ctx.prepare(frame, draws)
     for _ in range(max(args.warmup, 1)):
@@ -161,6 +162,7 @@ def main():
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--debug-flags", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -76,9 +76,10 @@ typedef struct shs_raster_stats {
     uint64_t tri_ghost;           /* slivers whose tile-clamp pixels near the bbox are tested   */
     uint64_t bin_entries;         /* (tile, triangle) pairs binned                              */
     uint64_t covered_pixels;      /* final pixels with depth != clear (shaded Mpix/s numerator) */
-    uint64_t tri_ghost_unbounded; /* ... with no error bound: tested by every tile             */
+    uint64_t tri_ghost_unbounded; /* ... with no error bound: every visited pixel tested        */
     uint64_t spilled;             /* bin entries beyond the per-tile capacity                    */
     uint64_t max_tile_bin;        /* fullest 32x32 tile's triangle count                         */
+    uint64_t ghost_fragments;     /* passing tile-clamp pixels of unbounded slivers outside bbox */
 } shs_raster_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */
@@ -138,6 +139,9 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
 /* Tuning knobs.  SHS_OPT_BIN_CAPACITY: initial per-tile bin capacity (entries past it spill to a
  * global list and stay exact; the context grows the capacity to the fullest tile it observes). */
 #define SHS_OPT_BIN_CAPACITY 1
+/* SHS_OPT_RASTER_MODE: 0 auto (small scenes scan every triangle's bin box per tile, large scenes
+ * build per-tile bins), 1 force scan, 2 force bins.  Results are identical in every mode. */
+#define SHS_OPT_RASTER_MODE 2
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 
 /* Library/ABI version for integration checks; edge of the square GPU screen tile (shard unit). */

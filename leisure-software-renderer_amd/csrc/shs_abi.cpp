@@ -49,12 +49,14 @@ struct shs_ctx {
     DevBuf<uint32_t> tile_count;     // zero between frames
     DevBuf<uint32_t> bins;           // n_tiles * bin_cap
     DevBuf<uint2> spill;
-    DevBuf<uint32_t> ghost;          // unbounded ghost triangles
+    DevBuf<shs_dev::GhostFrag> frags; // ghost fragments
+    DevBuf<uint2> boxes;             // per-triangle bin boxes
     DevBuf<uint32_t> counters;       // 2 parity sets
     DevBuf<uint2> tile_stat;         // per-tile (covered, bin entries)
     std::vector<uint2> h_tile_stat;
     uint64_t last_covered = 0, last_bins = 0, last_maxbin = 0;
     uint32_t bin_cap = 256;
+    int force_mode = 0;              // 0 auto, 1 scan, 2 bin (SHS_OPT_RASTER_MODE)
     uint32_t frame_index = 0;        // parity of the counter set
     uint32_t last_parity = 0;
     DevBuf<uint8_t> color;
@@ -177,7 +179,7 @@ int shs_destroy(shs_ctx *ctx) {
         if (m.nrm) (void)hipFree(m.nrm);
     }
     release(ctx->draws); release(ctx->recs); release(ctx->shade); release(ctx->tile_count); release(ctx->bins);
-    release(ctx->spill); release(ctx->ghost); release(ctx->counters); release(ctx->tile_stat);
+    release(ctx->spill); release(ctx->frags); release(ctx->counters); release(ctx->tile_stat); release(ctx->boxes);
     release(ctx->color); release(ctx->depth); release(ctx->prequant);
     for (int i = 0; i < 2; ++i) {
         if (ctx->h_draws[i]) (void)hipHostFree(ctx->h_draws[i]);
@@ -264,9 +266,12 @@ static void build_draw(const shs_legacy_draw &in, const Mesh &m, int32_t base, D
 
 static int harvest_slot(shs_ctx *ctx, int k) {
     if (!ctx->ring_pending[k]) return SHS_OK;
-    HIP_TRY(ctx, hipEventSynchronize(ctx->ring_ev[k][4]));
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ring_ev[k][2]));
     float ms[4];
-    for (int i = 0; i < 4; ++i) HIP_TRY(ctx, hipEventElapsedTime(&ms[i], ctx->ring_ev[k][i], ctx->ring_ev[k][i + 1]));
+    // [0] k_setup (ev0..ev1), [3] k_raster (ev1..ev2: k_raster starts when k_setup ends)
+    ms[1] = ms[2] = 0.0f;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms[0], ctx->ring_ev[k][0], ctx->ring_ev[k][1]));
+    HIP_TRY(ctx, hipEventElapsedTime(&ms[3], ctx->ring_ev[k][1], ctx->ring_ev[k][2]));
     for (int i = 0; i < 4; ++i) { ctx->acc_ms[i] += ms[i]; ctx->last_ms[i] = ms[i]; }
     ctx->acc_frames++;
     ctx->ring_pending[k] = false;
@@ -295,7 +300,8 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (total > 0x3fffffff) { ctx->err = "too many triangles in one frame"; return SHS_ERR_INVALID; }
     const int n_tris = (int)total;
 
-    if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1)) || ensure(ctx, ctx->shade, (size_t)std::max(n_tris, 1)))
+    if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1)) || ensure(ctx, ctx->shade, (size_t)std::max(n_tris, 1)) ||
+        ensure(ctx, ctx->boxes, (size_t)std::max(n_tris, 1)))
         return SHS_ERR_HIP;
     if (ctx->tile_count.cap < (size_t)n_tiles || !ctx->tile_count.p) {
         if (ensure(ctx, ctx->tile_count, n_tiles)) return SHS_ERR_HIP;
@@ -307,7 +313,7 @@ static int enqueue_frame(shs_ctx *ctx) {
         HIP_TRY(ctx, hipMemsetAsync(ctx->tile_stat.p, 0, ctx->tile_stat.cap * sizeof(uint2), ctx->stream));
     }
     if (!ctx->spill.p && ensure(ctx, ctx->spill, 1 << 16)) return SHS_ERR_HIP;
-    if (!ctx->ghost.p && ensure(ctx, ctx->ghost, 1 << 12)) return SHS_ERR_HIP;
+    if (!ctx->frags.p && ensure(ctx, ctx->frags, 1 << 12)) return SHS_ERR_HIP;
     if (ensure(ctx, ctx->color, npx * 4) || ensure(ctx, ctx->depth, npx)) return SHS_ERR_HIP;
     const bool want_pq = (f.flags & SHS_FRAME_PREQUANT) != 0;
     if (want_pq && ensure(ctx, ctx->prequant, npx)) return SHS_ERR_HIP;
@@ -363,13 +369,19 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.flags = f.flags;
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ctx->spill.cap, 0xffffffffu);
-    fp.ghost_cap = (uint32_t)std::min<size_t>(ctx->ghost.cap, 0xffffffffu);
+    fp.frag_cap = (uint32_t)std::min<size_t>(ctx->frags.cap, 0xffffffffu);
+    {   // ~4K ghost waves per frame: small scenes split each sliver group over many waves
+        const int n_groups = std::max(1, (n_tris + 31) / 32);
+        fp.ghost_slices = (uint32_t)std::min(64, std::max(1, 4096 / n_groups));
+    }
     fp.parity = ctx->frame_index & 1u;
+    fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
 
     FrameBuffers fb;
     fb.draws = ctx->draws.p; fb.recs = ctx->recs.p; fb.shade = ctx->shade.p; fb.tile_count = ctx->tile_count.p; fb.bins = ctx->bins.p;
-    fb.spill = ctx->spill.p; fb.ghost_list = ctx->ghost.p; fb.counters = ctx->counters.p;
+    fb.spill = ctx->spill.p; fb.frags = ctx->frags.p; fb.counters = ctx->counters.p;
     fb.tile_stat = ctx->tile_stat.p;
+    fb.boxes = ctx->boxes.p;
     fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;
 
     const int owned = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
@@ -387,10 +399,8 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], st));
     HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, ka, st));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], st));
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], st));
     HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, ka, owned, st));
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[4], st));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));
     ctx->last_parity = fp.parity;
     ctx->frame_index++;
     ctx->have_frame = true;
@@ -433,10 +443,10 @@ static int finish_frame(shs_ctx *ctx) {
             release(ctx->spill);
             if (ensure(ctx, ctx->spill, need + need / 4 + 1024)) return SHS_ERR_HIP;
         }
-        if (ov & shs_dev::OV_GHOST) {
-            const size_t need = c[shs_dev::C_UNBOUNDED];
-            release(ctx->ghost);
-            if (ensure(ctx, ctx->ghost, need + need / 4 + 1024)) return SHS_ERR_HIP;
+        if (ov & shs_dev::OV_FRAG) {
+            const size_t need = c[shs_dev::C_FRAG];
+            release(ctx->frags);
+            if (ensure(ctx, ctx->frags, need + need / 4 + 1024)) return SHS_ERR_HIP;
         }
         int rc = enqueue_frame(ctx);
         if (rc) return rc;
@@ -519,6 +529,7 @@ int shs_get_stats(shs_ctx *ctx, shs_raster_stats *st) {
     st->tri_ghost_unbounded = ctx->h_counters[shs_dev::C_UNBOUNDED];
     st->spilled = ctx->h_counters[shs_dev::C_SPILL];
     st->max_tile_bin = ctx->last_maxbin;
+    st->ghost_fragments = ctx->h_counters[shs_dev::C_FRAG];
     st->covered_pixels = ctx->last_covered;
     return SHS_OK;
 }
@@ -575,6 +586,11 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
 
 int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
     if (!ctx) return SHS_ERR_INVALID;
+    if (option == SHS_OPT_RASTER_MODE) {
+        if (value < 0 || value > 2) return SHS_ERR_INVALID;
+        ctx->force_mode = (int)value;
+        return SHS_OK;
+    }
     if (option == SHS_OPT_BIN_CAPACITY) {
         if (value < 1 || value > (1 << 24)) return SHS_ERR_INVALID;
         if (set_dev(ctx)) return SHS_ERR_HIP;

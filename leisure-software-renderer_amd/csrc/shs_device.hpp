@@ -68,15 +68,32 @@ __device__ __forceinline__ int hi16(uint32_t v) { return (int)(int16_t)(v >> 16)
 
 constexpr int TILE = 32;             // GPU screen tile (32x32 px, one 256-thread workgroup)
 constexpr int CHUNK = 256;           // triangle records staged in LDS per pass
+constexpr int CAND = 1024;           // candidate ids gathered per round (4 per thread)
+constexpr int SCAN_MAX_TRIS = 8192;  // scenes up to this size skip binning (scan mode)
 
 // counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one)
 constexpr int C_GHOST = 0, C_SETUP = 1, C_UNBOUNDED = 2, C_OVERFLOW = 3, C_COVERED = 4, C_MAXBIN = 5, C_SPILL = 6,
-              C_BINS = 7, C_NCOUNTERS = 8;
-constexpr uint32_t OV_SPILL = 1u, OV_GHOST = 2u;
+              C_FRAG = 7, C_NCOUNTERS = 8;
+constexpr uint32_t OV_SPILL = 1u, OV_FRAG = 2u;
+
+// Timing-experiment switches (frame flags bits 8+; results are WRONG with any of them set): they
+// let bench --debug-flags attribute kernel time to phases.  Never set by the product path.
+constexpr uint32_t DBG_SKIP_GHOST = 1u << 8, DBG_SKIP_SHADE = 1u << 9, DBG_CLEAR_ONLY = 1u << 10,
+                   DBG_SKIP_BIN = 1u << 11;
 
 // Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);
 // larger scenes read the device draw table.
 constexpr int KARG_DRAWS = 6;
+
+// A pixel the reference's tile clamp makes an unbounded sliver visit outside its bbox and whose
+// barycentrics pass (rare): resolved by k_raster like any other candidate.
+struct alignas(16) GhostFrag {
+    uint32_t xy;     // x | y << 16
+    float z;
+    uint32_t id;     // submission index
+    float v, w;      // barycentrics for shading (u = (1 - v) - w)
+    uint32_t pad[3];
+};
 
 struct FrameParams {
     int32_t W, H;
@@ -89,9 +106,11 @@ struct FrameParams {
     uint32_t flags;
     uint32_t bin_cap;                // per-tile bin capacity
     uint32_t spill_cap;
-    uint32_t ghost_cap;              // unbounded-ghost list capacity
+    uint32_t frag_cap;               // ghost fragment capacity
+    uint32_t ghost_slices;           // ghost waves per GHOST_GROUP triangles (k_setup)
     uint32_t parity;                 // counter set used by this frame
-    uint32_t pad0, pad1;
+    uint32_t scan_mode;              // 1: no bins, every tile scans all bin boxes (small scenes)
+    uint32_t pad0;
 };
 
 struct FrameBuffers {
@@ -101,7 +120,8 @@ struct FrameBuffers {
     uint32_t *tile_count;            // n_tiles, zero between frames (k_raster re-zeroes)
     uint32_t *bins;                  // n_tiles * bin_cap
     uint2 *spill;                    // (tile, tri) pairs beyond bin_cap
-    uint32_t *ghost_list;            // unbounded ghost triangles (ghost_cap)
+    GhostFrag *frags;                // tile-clamp pixels of unbounded slivers that pass (frag_cap)
+    uint2 *boxes;                    // n_tris: packed bin box (gbx, gby); empty for culled
     uint32_t *counters;              // 2 * C_NCOUNTERS
     uint2 *tile_stat;                // n_tiles: (covered pixels, bin entries) of the last frame
     uint8_t *color;                  // W*H*4, canvas rows

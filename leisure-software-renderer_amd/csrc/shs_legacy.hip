@@ -78,22 +78,28 @@ __device__ __forceinline__ int floor_clamped(float x, int lo, int hi) {
     return (int)fminf(fmaxf(floorf(x), (float)lo), (float)hi);
 }
 
-__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
-    const int gid = blockIdx.x * 256 + threadIdx.x;
-    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
-    if (blockIdx.x == 0 && threadIdx.x < C_NCOUNTERS) fb.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
-    if (gid >= fp.n_tris) return;
-    const DrawGPU *draws = draw_table(fp, fb, ka);
-    int lo = 0, hi = fp.n_draws - 1;
+__device__ __forceinline__ TriRec rec_from(const float4 *s) {
+    TriRec r;
+    float4 *d = reinterpret_cast<float4 *>(&r);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) d[j] = s[j];
+    return r;
+}
+
+__device__ __forceinline__ int find_draw(const DrawGPU *draws, int n_draws, int gid) {
+    int lo = 0, hi = n_draws - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (draws[mid].tri_base <= gid) lo = mid; else hi = mid - 1;
     }
-    const DrawGPU &dr = draws[lo];
-    const int local = gid - dr.tri_base;
-    const float *p = dr.pos + 9 * (size_t)local;
+    return lo;
+}
 
-    // VS position (mvp * vec4(p,1)) + Canvas::clip_to_screen (shs_renderer.hpp:823-831)
+// Per-triangle setup of draw_triangle_tile: VS position (mvp * vec4(p,1)), Canvas::clip_to_screen
+// (shs_renderer.hpp:823-831), the area cull (blinn_phong_shading.cpp:219-220), the per-triangle
+// half of barycentric_coordinate, the integer bbox and the bin box (flags/boxes as in TriRec).
+__device__ __forceinline__ TriRec make_rec(const FrameParams &fp, const DrawGPU &dr, int draw, int local) {
+    const float *p = dr.pos + 9 * (size_t)local;
     float sx[3], sy[3], sz[3];
     const float fw = (float)(fp.W - 1), fh = (float)(fp.H - 1);
 #pragma unroll
@@ -116,7 +122,7 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
     }
     r.denom = r.d00 * r.d11 - r.d01 * r.d01;
     r.z0 = sz[0]; r.z1 = sz[1]; r.z2 = sz[2];
-    r.draw = lo;
+    r.draw = draw;
     r.local = local;
     r.fminx = g_min(g_min(sx[0], sx[1]), sx[2]);
     r.fmaxx = g_max(g_max(sx[0], sx[1]), sx[2]);
@@ -127,7 +133,6 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
     bool finite = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) finite = finite && finitef(sx[k]) && finitef(sy[k]);
-    // area test of draw_triangle_tile (blinn_phong_shading.cpp:219-220)
     const float area = (sx[1] - sx[0]) * (sy[2] - sy[0]) - (sy[1] - sy[0]) * (sx[2] - sx[0]);
     // A non-finite corner makes denom NaN for every pixel (no write); |denom| < 1e-5 (a double
     // compare, shs_renderer.hpp:816) returns bc = -1 everywhere.
@@ -147,9 +152,10 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
         const double2 dg = dfin ? danger_margin(r) : make_double2(-1.0, -1.0);
         const bool unbounded = !(dg.x >= 0.0);
         const bool ghost = unbounded || dg.x >= 0.49 || dg.y >= 0.49;
-        // expansion of the bin box beyond the float bbox: 0 (ibox), danger + 1 px, or the screen
-        const double exx = unbounded ? 1e30 : (ghost ? dg.x + 1.0 : 0.0);
-        const double exy = unbounded ? 1e30 : (ghost ? dg.y + 1.0 : 0.0);
+        // expansion of the bin box beyond the float bbox: 0 (the ibox) or the danger margin + 1 px;
+        // unbounded slivers keep their ibox here and k_setup's ghost waves cover the rest
+        const double exx = (ghost && !unbounded) ? dg.x + 1.0 : 0.0;
+        const double exy = (ghost && !unbounded) ? dg.y + 1.0 : 0.0;
         gx0 = floor_clamped((float)((double)r.fminx - exx), 0, fp.W);
         gx1 = floor_clamped((float)((double)r.fmaxx + exx), -1, fp.W - 1);
         gy0 = floor_clamped((float)((double)r.fminy - exy), 0, fp.H);
@@ -159,12 +165,153 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
     r.flags = flags;
     r.ibx = pack16(ix0, ix1); r.iby = pack16(iy0, iy1);
     r.gbx = pack16(gx0, gx1); r.gby = pack16(gy0, gy1);
+    return r;
+}
+
+// Ghost waves: the pixels the reference's tile clamp makes an unbounded sliver visit OUTSIDE its
+// integer bbox (blinn_phong_shading.cpp:208-224: per 80x80 tile job, the bbox clamped to the tile).
+// One wave per GHOST_GROUP triangles recomputes their records (make_rec is deterministic); for each
+// unbounded sliver the wave enumerates those pixels lane-parallel (per reference tile: a corner
+// pixel, or a row / column segment) and appends every pixel whose barycentrics pass as a fragment.
+constexpr int GHOST_GROUP = 32;
+
+// LDS hand-off between lanes of ONE wave: the wave's LDS operations execute in order, so only the
+// compiler must be kept from reordering (no s_barrier: the four waves of a ghost block diverge).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct GhostScratch {          // per-wave LDS
+    float4 rec[6];
+    int pref[64], w[64], x0[64], y0[64];
+};
+
+__device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
+                                           uint32_t *cnt, int group, int slice, GhostScratch &gs) {
+    const int lane = threadIdx.x & 63;
+    const int gid = group * GHOST_GROUP + lane;
+    TriRec r;
+    bool unb = false;
+    if (lane < GHOST_GROUP && gid < fp.n_tris) {
+        const int d = find_draw(draws, fp.n_draws, gid);
+        r = make_rec(fp, draws[d], d, gid - draws[d].tri_base);
+        unb = (r.flags & TRI_UNBOUNDED) != 0;
+    }
+    uint64_t todo = __ballot(unb);
+    const int n_rt = fp.rt_x * fp.rt_y;
+    while (todo) {
+        const int src = __ffsll((unsigned long long)todo) - 1;
+        todo &= todo - 1;
+        if (lane == src) {
+            const float4 *q = reinterpret_cast<const float4 *>(&r);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) gs.rec[j] = q[j];
+        }
+        wave_lds_sync();
+        const TriRec t = rec_from(gs.rec);
+        const uint32_t tri = (uint32_t)(group * GHOST_GROUP + src);
+        const int ix0 = lo16(t.ibx), ix1 = hi16(t.ibx), iy0 = lo16(t.iby), iy1 = hi16(t.iby);
+        for (int rb = 0; rb < n_rt; rb += 64) {
+            // lane -> reference tile rb + lane: its clamped visited rectangle and pixel count
+            const int rt = rb + lane;
+            int lx0 = 0, ly0 = 0, w = 1, npx = 0;
+            if (rt < n_rt) {
+                const int rx = rt % fp.rt_x, ry = rt / fp.rt_x;
+                const float tminx = (float)(rx * fp.rtw), tmaxx = (float)(min(rx * fp.rtw + fp.rtw, fp.W) - 1);
+                const float tminy = (float)(ry * fp.rth), tmaxy = (float)(min(ry * fp.rth + fp.rth, fp.H) - 1);
+                const float bminx = g_max(tminx, g_min(tmaxx, t.fminx)), bmaxx = g_min(tmaxx, g_max(tminx, t.fmaxx));
+                const float bminy = g_max(tminy, g_min(tmaxy, t.fminy)), bmaxy = g_min(tmaxy, g_max(tminy, t.fmaxy));
+                if (!(bminx > bmaxx || bminy > bmaxy)) {
+                    lx0 = (int)bminx; ly0 = (int)bminy;
+                    const int lx1 = (int)bmaxx, ly1 = (int)bmaxy;
+                    const bool inside = lx0 >= ix0 && lx1 <= ix1 && ly0 >= iy0 && ly1 <= iy1;
+                    w = lx1 - lx0 + 1;
+                    npx = inside ? 0 : w * (ly1 - ly0 + 1);
+                }
+            }
+            // wave-inclusive prefix of the pixel counts (all lanes active here)
+            int incl = npx;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            const int total = __shfl(incl, 63);
+            gs.pref[lane] = incl;
+            gs.w[lane] = w;
+            gs.x0[lane] = lx0;
+            gs.y0[lane] = ly0;
+            wave_lds_sync();
+            // this wave's slice of the pixel index space (fp.ghost_slices waves share each group)
+            for (int k = slice * 64 + lane; k < total; k += 64 * (int)fp.ghost_slices) {
+                int lo = 0, hi = 63;                         // owner: first lane with pref > k
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (gs.pref[mid] > k) hi = mid; else lo = mid + 1;
+                }
+                const int off = k - (lo ? gs.pref[lo - 1] : 0);
+                const int wq = gs.w[lo];
+                const int px = gs.x0[lo] + off % wq, py = gs.y0[lo] + off / wq;
+                if (px >= ix0 && px <= ix1 && py >= iy0 && py <= iy1) continue;   // k_raster's part
+                const int tl = (py / TILE) * fp.tiles_x + px / TILE;
+                if (tl % fp.count != fp.rank) continue;
+                float u, v, ww;
+                bary(t, (float)px + 0.5f, (float)py + 0.5f, u, v, ww);
+                if (u < 0 || v < 0 || ww < 0) continue;
+                const float z = (u * t.z0 + v * t.z1) + ww * t.z2;
+                if (!(z < FLT_MAX)) continue;   // NaN / FLT_MAX never pass the strict z test
+                const uint32_t slot = atomicAdd(&cnt[C_FRAG], 1u);
+                if (slot < fp.frag_cap) {
+                    GhostFrag g;
+                    g.xy = (uint32_t)px | ((uint32_t)py << 16);
+                    g.z = z;
+                    g.id = tri;
+                    g.v = v;
+                    g.w = ww;
+                    g.pad[0] = g.pad[1] = g.pad[2] = 0u;
+                    fb.frags[slot] = g;
+                } else {
+                    atomicOr(&cnt[C_OVERFLOW], OV_FRAG);
+                }
+            }
+            wave_lds_sync();   // the next reference-tile batch overwrites gs
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
+    __shared__ GhostScratch s_ghost[4];
+    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
+    const DrawGPU *draws = draw_table(fp, fb, ka);
+    const int setup_blocks = (fp.n_tris + 255) / 256;
+    // zero the other parity set for the next frame (block 0 exists even for an empty frame)
+    if (blockIdx.x == 0 && threadIdx.x < C_NCOUNTERS) fb.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
+    if ((int)blockIdx.x >= setup_blocks) {
+        const int wave = threadIdx.x >> 6;
+        const int gw = ((int)blockIdx.x - setup_blocks) * 4 + wave;
+        const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
+        if (gw < n_groups * (int)fp.ghost_slices && !(fp.flags & DBG_SKIP_GHOST))
+            ghost_wave(fp, fb, draws, cnt, gw / (int)fp.ghost_slices, gw % (int)fp.ghost_slices, s_ghost[wave]);
+        return;
+    }
+    const int gid = blockIdx.x * 256 + threadIdx.x;
+    if (gid >= fp.n_tris) return;
+    const int lo = find_draw(draws, fp.n_draws, gid);
+    const DrawGPU &dr = draws[lo];
+    const int local = gid - dr.tri_base;
+    const float *p = dr.pos + 9 * (size_t)local;
+    TriRec r = make_rec(fp, dr, lo, local);
+    const uint32_t flags = r.flags;
     {
         const float4 *src = reinterpret_cast<const float4 *>(&r);
         float4 *dst = reinterpret_cast<float4 *>(&fb.recs[gid]);
 #pragma unroll
         for (int j = 0; j < 6; ++j) dst[j] = src[j];
     }
+    fb.boxes[gid] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
+    const int gx0 = lo16(r.gbx), gx1 = hi16(r.gbx), gy0 = lo16(r.gby), gy1 = hi16(r.gby);
     if (flags & TRI_CULLED) return;
 
     // Shading varyings of the three corners (the VS outputs the FS interpolates), computed once per
@@ -216,13 +363,9 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
 
     atomicAdd(&cnt[C_SETUP], 1u);
     if (flags & TRI_GHOST) atomicAdd(&cnt[C_GHOST], 1u);
-    if (flags & TRI_UNBOUNDED) {
-        const uint32_t slot = atomicAdd(&cnt[C_UNBOUNDED], 1u);
-        if (slot < fp.ghost_cap) fb.ghost_list[slot] = (uint32_t)gid;
-        else atomicOr(&cnt[C_OVERFLOW], OV_GHOST);
-        return;   // every tile reads the unbounded list; not binned
-    }
-    if (gx0 > gx1 || gy0 > gy1) return;
+    if (flags & TRI_UNBOUNDED) atomicAdd(&cnt[C_UNBOUNDED], 1u);
+    if (fp.scan_mode) return;   // small scene: k_raster scans the bin boxes; no bins
+    if (gx0 > gx1 || gy0 > gy1 || (fp.flags & DBG_SKIP_BIN)) return;
     const int tx0 = gx0 / TILE, tx1 = gx1 / TILE, ty0 = gy0 / TILE, ty1 = gy1 / TILE;
     const int ntx = tx1 - tx0 + 1, nty = ty1 - ty0 + 1;
     if (ntx * nty <= 4) {
@@ -267,13 +410,6 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
 
 // ---- k_raster -------------------------------------------------------------------------------
 
-__device__ __forceinline__ TriRec rec_from(const float4 *s) {
-    TriRec r;
-    float4 *d = reinterpret_cast<float4 *>(&r);
-#pragma unroll
-    for (int j = 0; j < 6; ++j) d[j] = s[j];
-    return r;
-}
 
 // Fragment shaders of the four legacy pipelines for the winning triangle, from its per-corner
 // varyings.  Returns the pre-truncation floats; the caller truncates to uint8 like the reference.
@@ -386,13 +522,13 @@ __device__ __forceinline__ int tile_of_block(int b, int n_owned) {
 constexpr int NB = TILE / 8;   // 8x8 blocks per tile edge (4): wave w owns block column w
 
 __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
-    // LDS carve: records (reused for the winners' (v, w) after the raster passes), ids, z, id
     __shared__ float4 s_rec[CHUNK * 6];
     __shared__ uint32_t s_id[CHUNK];
+    __shared__ uint32_t s_cand[CAND];
     __shared__ float s_bz[TILE * TILE];
     __shared__ uint32_t s_bid[TILE * TILE];
-    __shared__ uint32_t s_cov, s_n;
-    float *s_bv = reinterpret_cast<float *>(s_rec);
+    __shared__ uint32_t s_cov, s_nc;
+    float *s_bv = reinterpret_cast<float *>(s_rec);    // reused once the raster passes are done
     float *s_bw = s_bv + TILE * TILE;
 
     const int n_owned = (fp.tiles_x * fp.tiles_y - fp.rank + fp.count - 1) / fp.count;
@@ -402,88 +538,73 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
     const DrawGPU *draws = draw_table(fp, fb, ka);
-
-    const uint32_t n_bin_total = fb.tile_count[tile];
-    uint32_t n_unb = cnt[C_UNBOUNDED];
-    if (n_unb > fp.ghost_cap) n_unb = fp.ghost_cap;
-
-    // output mapping: thread -> row tid>>3, 4 consecutive pixels (16-B colour and depth stores;
-    // 8 threads cover a 128-B row segment of each)
-    const int oy = Y0 + (tid >> 3), ox = X0 + (tid & 7) * 4;
-    const size_t crow = (size_t)(fp.H - 1 - oy) * fp.W, drow = (size_t)oy * fp.W;
-    const bool vec_ok = ox + 3 < fp.W && (fp.W & 3) == 0;
-
-    if (n_bin_total == 0 && n_unb == 0) {
-        // empty tile: the fused clear (Canvas::fill_pixel + ZBuffer::clear), nothing else
-        if (oy < fp.H) {
-            const uint32_t c = fp.clear_rgba;
-            if (vec_ok) {
-                *reinterpret_cast<uint4 *>(fb.color + (crow + ox) * 4) = make_uint4(c, c, c, c);
-                *reinterpret_cast<float4 *>(fb.depth + drow + ox) = make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
-            } else {
-                for (int j = 0; j < 4; ++j)
-                    if (ox + j < fp.W) {
-                        reinterpret_cast<uint32_t *>(fb.color)[crow + ox + j] = c;
-                        fb.depth[drow + ox + j] = FLT_MAX;
-                    }
-            }
-            if (fb.prequant)
-                for (int j = 0; j < 4; ++j)
-                    if (ox + j < fp.W) fb.prequant[crow + ox + j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        if (tid == 0) fb.tile_stat[tile] = make_uint2(0u, 0u);
-        return;
-    }
     if (tid == 0) s_cov = 0;
+
+    // candidate sources.  scan mode: every triangle's bin box.  bin mode: the tile's bin, then the
+    // spill list (entries of this tile).
+    uint32_t n_bin_total = 0, n_bin = 0, n_spill = 0, n_items;
+    if (fp.scan_mode) {
+        n_items = (uint32_t)fp.n_tris;
+    } else {
+        n_bin_total = fb.tile_count[tile];
+        n_bin = n_bin_total < fp.bin_cap ? n_bin_total : fp.bin_cap;
+        if (n_bin_total > fp.bin_cap) n_spill = min(cnt[C_SPILL], fp.spill_cap);
+        n_items = n_bin + n_spill;
+    }
+    if (fp.flags & DBG_CLEAR_ONLY) n_items = 0;
+    const uint32_t *bin = fb.bins + (size_t)tile * fp.bin_cap;
+    const int tx1 = X0 + TILE - 1, ty1 = Y0 + TILE - 1;
 
     // raster mapping: wave w owns the 8-px column of blocks (w, 0..3); lane -> (lane&7, lane>>3)
     const int px = X0 + wave * 8 + (lane & 7);
     const int py0 = Y0 + (lane >> 3);
-    const int rx = (px / fp.rtw) * fp.rtw;
-    const float rtminx = (float)rx, rtmaxx = (float)(min(rx + fp.rtw, fp.W) - 1);
+    const int rxs = (px / fp.rtw) * fp.rtw;
+    const float rtminx = (float)rxs, rtmaxx = (float)(min(rxs + fp.rtw, fp.W) - 1);
     const int bxl = X0 + wave * 8;
     Best best[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) { best[i].z = FLT_MAX; best[i].id = 0u; best[i].v = 0.f; best[i].w = 0.f; }
 
-    const uint32_t n_bin = n_bin_total < fp.bin_cap ? n_bin_total : fp.bin_cap;
-    const uint32_t *bin = fb.bins + (size_t)tile * fp.bin_cap;
-    uint32_t n_spill = 0;
-    if (n_bin_total > fp.bin_cap) {   // this tile spilled: scan the (small) spill list too
-        n_spill = cnt[C_SPILL];
-        if (n_spill > fp.spill_cap) n_spill = fp.spill_cap;
-    }
-
-    // pass 0: the tile's bin; 1: spill entries of this tile; 2: unbounded ghosts (every tile)
-    for (int pass = 0; pass < 3; ++pass) {
-        const uint32_t n = pass == 0 ? n_bin : (pass == 1 ? n_spill : n_unb);
-        for (uint32_t base = 0; base < n; base += CHUNK) {
-            __syncthreads();
-            if (tid == 0) s_n = 0;
-            __syncthreads();
-            if (base + tid < n) {
-                uint32_t id = 0xffffffffu;
-                if (pass == 0) {
-                    id = bin[base + tid];
-                } else if (pass == 1) {
-                    const uint2 e = fb.spill[base + tid];
-                    if ((int)e.x == tile) id = e.y;
-                } else {
-                    id = fb.ghost_list[base + tid];
-                }
-                if (id != 0xffffffffu) {
-                    const uint32_t slot = atomicAdd(&s_n, 1u);
-                    s_id[slot] = id;
-                    const float4 *src = reinterpret_cast<const float4 *>(&fb.recs[id]);
+    for (uint32_t base = 0; base < n_items; base += CAND) {
+        __syncthreads();
+        if (tid == 0) s_nc = 0;
+        __syncthreads();
+        // gather up to CAND candidate ids (4 independent loads per thread, one round trip)
 #pragma unroll
-                    for (int j = 0; j < 6; ++j) s_rec[slot * 6 + j] = src[j];
-                }
+        for (int k = 0; k < CAND / 256; ++k) {
+            const uint32_t item = base + tid + 256u * k;
+            if (item >= n_items) continue;
+            uint32_t id = 0xffffffffu;
+            if (fp.scan_mode) {
+                const uint2 bx = fb.boxes[item];
+                if (!(hi16(bx.x) < X0 || lo16(bx.x) > tx1 || hi16(bx.y) < Y0 || lo16(bx.y) > ty1)) id = item;
+            } else if (item < n_bin) {
+                id = bin[item];
+            } else {
+                const uint2 e = fb.spill[item - n_bin];
+                if ((int)e.x == tile) id = e.y;
+            }
+            if (id != 0xffffffffu) s_cand[atomicAdd(&s_nc, 1u)] = id;
+        }
+        __syncthreads();
+        const uint32_t nc = s_nc;
+        for (uint32_t c = 0; c < nc; c += CHUNK) {
+            const int m = (int)min((uint32_t)CHUNK, nc - c);
+            if (c > 0) __syncthreads();
+            if (tid < m) {
+                const uint32_t id = s_cand[c + tid];
+                s_id[tid] = id;
+                const float4 *src = reinterpret_cast<const float4 *>(&fb.recs[id]);
+                float4 q[6];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) q[j] = src[j];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) s_rec[tid * 6 + j] = q[j];
             }
             __syncthreads();
-            const int m = (int)s_n;
             for (int j = 0; j < m; ++j) {
                 const uint4 bb = reinterpret_cast<const uint4 *>(&s_rec[j * 6])[4];   // ibx iby gbx gby
-                if (hi16(bb.z) < bxl || lo16(bb.z) > bxl + 7 || hi16(bb.w) < Y0 || lo16(bb.w) > Y0 + TILE - 1) continue;
+                if (hi16(bb.z) < bxl || lo16(bb.z) > bxl + 7 || hi16(bb.w) < Y0 || lo16(bb.w) > ty1) continue;
                 const TriRec r = rec_from(&s_rec[j * 6]);
                 const uint32_t id = s_id[j];
 #pragma unroll
@@ -495,6 +616,18 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
                     raster_px(px, py, rtminx, rtmaxx, (float)ry, (float)(min(ry + fp.rth, fp.H) - 1), r, id, best[i]);
                 }
             }
+        }
+    }
+    // tile-clamp pixels of unbounded slivers outside their bbox that passed (k_setup ghost waves)
+    {
+        const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
+        for (uint32_t f = 0; f < n_frag; ++f) {
+            const GhostFrag g = fb.frags[f];
+            const int gx = (int)(g.xy & 0xffffu), gy = (int)(g.xy >> 16);
+            if (gx != px) continue;
+#pragma unroll
+            for (int i = 0; i < NB; ++i)
+                if (gy == py0 + 8 * i) resolve(g.z, g.id, g.v, g.w, best[i]);
         }
     }
     __syncthreads();   // s_rec is reused below
@@ -510,8 +643,12 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
     }
     __syncthreads();
 
+    // output mapping: thread -> row tid>>3, 4 consecutive pixels (16-B colour and depth stores;
+    // 8 threads cover a 128-B row segment of each)
+    const int oy = Y0 + (tid >> 3), ox = X0 + (tid & 7) * 4;
     uint32_t covered = 0;
     if (oy < fp.H) {
+        const size_t crow = (size_t)(fp.H - 1 - oy) * fp.W, drow = (size_t)oy * fp.W;
         uint32_t rgba[4];
         float dep[4];
         float4 pq[4];
@@ -532,6 +669,8 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
                 const int j = 2 * h + q;
                 win[q] = dep[j] < FLT_MAX && ox + j < fp.W;
                 if (win[q]) {
+                    ++covered;
+                    if (fp.flags & DBG_SKIP_SHADE) { win[q] = false; continue; }
                     const float4 *src = reinterpret_cast<const float4 *>(&fb.shade[s_bid[lo + j]]);
                     float4 *d = reinterpret_cast<float4 *>(&sr[q]);
 #pragma unroll
@@ -542,7 +681,6 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
             for (int q = 0; q < 2; ++q) {
                 const int j = 2 * h + q;
                 if (!win[q]) continue;
-                ++covered;
                 const float v = s_bv[lo + j], w = s_bw[lo + j];
                 const float u = (1.0f - v) - w;
                 float pre[3];
@@ -552,7 +690,7 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
                 pq[j] = make_float4(pre[0], pre[1], pre[2], 1.0f);
             }
         }
-        if (vec_ok) {
+        if (ox + 3 < fp.W && (fp.W & 3) == 0) {
             *reinterpret_cast<uint4 *>(fb.color + (crow + ox) * 4) = make_uint4(rgba[0], rgba[1], rgba[2], rgba[3]);
             *reinterpret_cast<float4 *>(fb.depth + drow + ox) = make_float4(dep[0], dep[1], dep[2], dep[3]);
         } else {
@@ -573,7 +711,7 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
     __syncthreads();
     if (tid == 0) {
         fb.tile_stat[tile] = make_uint2(s_cov, n_bin_total);
-        fb.tile_count[tile] = 0u;   // bins are empty for the next frame (no memset launch)
+        if (!fp.scan_mode) fb.tile_count[tile] = 0u;   // bins are empty for the next frame
     }
 }
 
@@ -584,7 +722,12 @@ namespace shs_internal {
 using namespace shs_dev;
 
 hipError_t launch_setup(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, hipStream_t s) {
-    hipLaunchKernelGGL(k_setup, dim3(fp.n_tris > 0 ? (fp.n_tris + 255) / 256 : 1), dim3(256), 0, s, fp, fb, ka);
+    // setup blocks (one thread per triangle) + ghost blocks (4 waves; each group of GHOST_GROUP
+    // triangles is shared by fp.ghost_slices waves)
+    const int setup_blocks = (fp.n_tris + 255) / 256;
+    const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
+    const int ghost_blocks = (n_groups * (int)fp.ghost_slices + 3) / 4;
+    hipLaunchKernelGGL(k_setup, dim3(setup_blocks > 0 ? setup_blocks + ghost_blocks : 1), dim3(256), 0, s, fp, fb, ka);
     return hipGetLastError();
 }
 hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, int n_owned_tiles,

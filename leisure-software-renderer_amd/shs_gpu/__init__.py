@@ -55,13 +55,14 @@ class Frame:
     shard_count: int = 1
     clear_color: tuple = (0, 0, 0, 255)
     prequant: bool = False
+    debug_flags: int = 0         # timing experiments only (bits 8+, wrong images)
 
     def desc(self) -> FrameDesc:
         d = FrameDesc()
         d.width, d.height = self.width, self.height
         d.ref_tile_w, d.ref_tile_h = self.ref_tile
         d.shard_rank, d.shard_count = self.shard_rank, self.shard_count
-        d.flags = FRAME_PREQUANT if self.prequant else 0
+        d.flags = (FRAME_PREQUANT if self.prequant else 0) | (int(self.debug_flags) & ~0xff)
         for i in range(4):
             d.clear_color[i] = self.clear_color[i]
         return d
@@ -202,6 +203,10 @@ class Context:
         out = np.zeros(n.value, dtype=self.TRIREC_DTYPE)
         self._check(self._lib.shs_debug_records(self._h, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)))
         return out
+
+    def set_raster_mode(self, mode: int):
+        """0 auto, 1 scan (no bins), 2 bins."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_RASTER_MODE, int(mode)))
 
     def set_bin_capacity(self, cap: int):
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_BIN_CAPACITY, int(cap)))

@@ -23,6 +23,7 @@ SHADING_NAMES = {"flat": 0, "gouraud": 1, "phong": 2, "blinn_phong": 3}
 
 FRAME_PREQUANT = 1
 OPT_BIN_CAPACITY = 1
+OPT_RASTER_MODE = 2
 
 
 class LegacyDraw(ctypes.Structure):
@@ -60,6 +61,7 @@ class RasterStats(ctypes.Structure):
         ("tri_ghost_unbounded", ctypes.c_uint64),
         ("spilled", ctypes.c_uint64),
         ("max_tile_bin", ctypes.c_uint64),
+        ("ghost_fragments", ctypes.c_uint64),
     ]
 
 

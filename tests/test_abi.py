@@ -34,7 +34,7 @@ def test_struct_layouts():
     from shs_gpu import _abi
     assert ctypes.sizeof(_abi.LegacyDraw) == 4 + 4 + 64 + 64 + 12 + 12 + 4
     assert ctypes.sizeof(_abi.FrameDesc) == 7 * 4 + 4
-    assert ctypes.sizeof(_abi.RasterStats) == 8 * 8
+    assert ctypes.sizeof(_abi.RasterStats) == 9 * 8
 
 
 def test_invalid_arguments_fail_loudly():

@@ -207,6 +207,7 @@ def test_bin_spill_path_exact(gpu_ctx, oracle_mod):
     pos, nrm = _ndc_soup(rng, W, H, 600)
     ctx = shs_gpu.Context(0)
     try:
+        ctx.set_raster_mode(2)      # bins (this scene would auto-select scan mode)
         ctx.set_bin_capacity(2)
         frame = shs_gpu.Frame(W, H)
         stats, _ = _check(ctx, oracle_mod, frame, [_identity_draw(Mesh(pos, nrm), 3)])
@@ -257,3 +258,53 @@ def test_hair_slivers_tile_clamp_ghosts(gpu_ctx, oracle_mod):
     stats, _ = _check(gpu_ctx, oracle_mod, shs_gpu.Frame(W, H, ref_tile=(80, 80)), [draw])
     assert stats["tri_ghost_unbounded"] > 0
     _check(gpu_ctx, oracle_mod, shs_gpu.Frame(W, H, ref_tile=(W, H)), [draw])
+
+
+@pytest.fixture(scope="module", params=[1, 2], ids=["scan", "bins"])
+def mode_ctx(request):
+    import shs_gpu
+    ctx = shs_gpu.Context(0)
+    ctx.set_raster_mode(request.param)
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("what", ["c1", "c3", "soup", "hair", "ties"])
+def test_both_raster_modes_exact(mode_ctx, oracle_mod, what):
+    """Scan mode (every tile scans all bin boxes) and bin mode (per-tile bins, spill, unbounded list)
+    give identical, oracle-exact frames."""
+    import shs_gpu
+    from shs_gpu import scene
+    from shs_gpu.scene import Mesh
+    if what in ("c1", "c3"):
+        frame, draws = scene.config(what)
+    elif what == "soup":
+        rng = np.random.default_rng(31)
+        pos, nrm = _ndc_soup(rng, 333, 241, 1500)
+        frame, draws = shs_gpu.Frame(333, 241), [_identity_draw(Mesh(pos, nrm), 2)]
+    elif what == "hair":
+        rng = np.random.default_rng(99)
+        pos, nrm = _hair_soup(rng, 400, 300, 3000)
+        frame, draws = shs_gpu.Frame(400, 300), [_identity_draw(Mesh(pos, nrm), 3)]
+    else:
+        rng = np.random.default_rng(8)
+        pos, nrm = _ndc_soup(rng, 256, 192, 800, kind="small", zq=[0.25, 0.5, -0.0, 0.0])
+        frame, draws = shs_gpu.Frame(256, 192), [_identity_draw(Mesh(pos, nrm), 1)]
+    _check(mode_ctx, oracle_mod, frame, draws)
+
+
+def test_counters_reset_across_empty_frame(gpu_ctx, oracle_mod):
+    """Per-frame counters (ghost fragments, spill, overflow) are zeroed even when a frame has no
+    triangles: hair-sliver frame (ghost fragments emitted) -> empty frame -> C1 must match the oracle."""
+    import shs_gpu
+    from shs_gpu import scene
+    from shs_gpu.scene import Mesh
+    rng = np.random.default_rng(99)
+    pos, nrm = _hair_soup(rng, 400, 300, 3000)
+    gpu_ctx.render(shs_gpu.Frame(400, 300), [_identity_draw(Mesh(pos, nrm), 3)])
+    gpu_ctx.resolve()
+    assert gpu_ctx.stats()["tri_ghost_unbounded"] > 0
+    gpu_ctx.render(shs_gpu.Frame(64, 64), [])
+    gpu_ctx.resolve()
+    frame, draws = scene.config("c1")
+    _check(gpu_ctx, oracle_mod, frame, draws)
