@@ -142,7 +142,16 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
 /* SHS_OPT_RASTER_MODE: 0 auto (small scenes scan every triangle's bin box per tile, large scenes
  * build per-tile bins), 1 force scan, 2 force bins.  Results are identical in every mode. */
 #define SHS_OPT_RASTER_MODE 2
+/* SHS_OPT_TIMELINE: 1 = record every workgroup's start / end time (s_memrealtime, 100 MHz) of the
+ * frames that follow (profiling aid; read with shs_debug_timeline), 0 = off. */
+#define SHS_OPT_TIMELINE 3
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
+
+/* Debug / profiling hook: the last frame's workgroup timeline.  out[0..7] = {k_setup grid, k_raster
+ * grid, setup blocks, ghost blocks, clear blocks, stride S, 0, 0} (k_setup's block roles in that
+ * order), then S slots per k_setup workgroup followed by S per k_raster workgroup: start, end, and
+ * phase marks of the workgroup's thread 0 (0 where a phase did not run). */
+int shs_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out);
 
 /* Library/ABI version for integration checks; edge of the square GPU screen tile (shard unit). */
 int shs_abi_version(void);

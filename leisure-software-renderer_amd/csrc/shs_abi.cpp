@@ -46,15 +46,23 @@ struct shs_ctx {
     DevBuf<DrawGPU> draws;
     DevBuf<TriRec> recs;
     DevBuf<shs_dev::ShadeRec> shade;
-    DevBuf<uint32_t> tile_count;     // zero between frames
+    DevBuf<uint32_t> tile_count;     // 2 parity sets of per-bin-tile counts
     DevBuf<uint32_t> bins;           // n_tiles * bin_cap
     DevBuf<uint2> spill;
     DevBuf<shs_dev::GhostFrag> frags; // ghost fragments
     DevBuf<uint2> boxes;             // per-triangle bin boxes
     DevBuf<uint32_t> counters;       // 2 parity sets
-    DevBuf<uint2> tile_stat;         // per-tile (covered, bin entries)
-    std::vector<uint2> h_tile_stat;
-    uint64_t last_covered = 0, last_bins = 0, last_maxbin = 0;
+    DevBuf<uint32_t> busy;           // per raster tile
+    DevBuf<uint4> blk_stat;          // per setup block
+    DevBuf<uint2> rstat;             // per raster block
+    DevBuf<uint64_t> timeline;       // SHS_OPT_TIMELINE
+    bool want_timeline = false;
+    int last_setup_grid = 0, last_ghost_blocks = 0, last_clear_blocks = 0;
+    std::vector<uint4> h_blk_stat;
+    std::vector<uint2> h_rstat;
+    uint64_t geom_key = ~0ull;       // (tiles, shard) of the last frame: a change resets the counts
+    int last_setup_blocks = 0, last_raster_grid = 0;
+    uint64_t last_covered = 0, last_bins = 0, last_maxbin = 0, last_setup = 0, last_ghost = 0, last_unb = 0;
     uint32_t bin_cap = 256;
     int force_mode = 0;              // 0 auto, 1 scan, 2 bin (SHS_OPT_RASTER_MODE)
     uint32_t frame_index = 0;        // parity of the counter set
@@ -179,7 +187,8 @@ int shs_destroy(shs_ctx *ctx) {
         if (m.nrm) (void)hipFree(m.nrm);
     }
     release(ctx->draws); release(ctx->recs); release(ctx->shade); release(ctx->tile_count); release(ctx->bins);
-    release(ctx->spill); release(ctx->frags); release(ctx->counters); release(ctx->tile_stat); release(ctx->boxes);
+    release(ctx->spill); release(ctx->frags); release(ctx->counters); release(ctx->busy); release(ctx->boxes);
+    release(ctx->blk_stat); release(ctx->rstat); release(ctx->timeline);
     release(ctx->color); release(ctx->depth); release(ctx->prequant);
     for (int i = 0; i < 2; ++i) {
         if (ctx->h_draws[i]) (void)hipHostFree(ctx->h_draws[i]);
@@ -293,6 +302,8 @@ static int enqueue_frame(shs_ctx *ctx) {
     const int tiles_x = (f.width + shs_dev::TILE - 1) / shs_dev::TILE;
     const int tiles_y = (f.height + shs_dev::TILE - 1) / shs_dev::TILE;
     const int n_tiles = tiles_x * tiles_y;
+    const int rtiles_y = (f.height + shs_dev::RTH - 1) / shs_dev::RTH;
+    const int n_rt = tiles_x * rtiles_y;
     const size_t npx = (size_t)f.width * f.height;
 
     int64_t total = 0;
@@ -303,15 +314,28 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1)) || ensure(ctx, ctx->shade, (size_t)std::max(n_tris, 1)) ||
         ensure(ctx, ctx->boxes, (size_t)std::max(n_tris, 1)))
         return SHS_ERR_HIP;
-    if (ctx->tile_count.cap < (size_t)n_tiles || !ctx->tile_count.p) {
-        if (ensure(ctx, ctx->tile_count, n_tiles)) return SHS_ERR_HIP;
+    // Bin counts (2 parity sets) and busy flags are kept zero by the kernels themselves (k_setup's
+    // clear blocks zero the next frame's counts, k_raster resets the flags it consumed); they are
+    // reset here only when the buffers are new or the tile geometry / shard changes.
+    const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)f.shard_rank << 16) ^
+                          (uint64_t)f.shard_count;
+    bool reset = gkey != ctx->geom_key;
+    if (ctx->tile_count.cap < 2 * (size_t)n_tiles || !ctx->tile_count.p) {
+        if (ensure(ctx, ctx->tile_count, 2 * (size_t)n_tiles)) return SHS_ERR_HIP;
+        reset = true;
+    }
+    if (ctx->busy.cap < (size_t)n_rt || !ctx->busy.p) {
+        if (ensure(ctx, ctx->busy, n_rt)) return SHS_ERR_HIP;
+        reset = true;
+    }
+    if (reset) {
         HIP_TRY(ctx, hipMemsetAsync(ctx->tile_count.p, 0, ctx->tile_count.cap * sizeof(uint32_t), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->busy.p, 0, ctx->busy.cap * sizeof(uint32_t), ctx->stream));
+        ctx->geom_key = gkey;
     }
     if (ensure(ctx, ctx->bins, (size_t)n_tiles * ctx->bin_cap)) return SHS_ERR_HIP;
-    if (ctx->tile_stat.cap < (size_t)n_tiles || !ctx->tile_stat.p) {
-        if (ensure(ctx, ctx->tile_stat, n_tiles)) return SHS_ERR_HIP;
-        HIP_TRY(ctx, hipMemsetAsync(ctx->tile_stat.p, 0, ctx->tile_stat.cap * sizeof(uint2), ctx->stream));
-    }
+    const int setup_blocks = (n_tris + 255) / 256;
+    if (ensure(ctx, ctx->blk_stat, (size_t)std::max(setup_blocks, 1))) return SHS_ERR_HIP;
     if (!ctx->spill.p && ensure(ctx, ctx->spill, 1 << 16)) return SHS_ERR_HIP;
     if (!ctx->frags.p && ensure(ctx, ctx->frags, 1 << 12)) return SHS_ERR_HIP;
     if (ensure(ctx, ctx->color, npx * 4) || ensure(ctx, ctx->depth, npx)) return SHS_ERR_HIP;
@@ -361,6 +385,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.rtw = f.ref_tile_w; fp.rth = f.ref_tile_h;
     fp.rank = f.shard_rank; fp.count = f.shard_count;
     fp.tiles_x = tiles_x; fp.tiles_y = tiles_y;
+    fp.rtiles_y = rtiles_y;
     fp.rt_x = (f.width + f.ref_tile_w - 1) / f.ref_tile_w;
     fp.rt_y = (f.height + f.ref_tile_h - 1) / f.ref_tile_h;
     fp.n_tris = n_tris; fp.n_draws = n_draws;
@@ -376,15 +401,32 @@ static int enqueue_frame(shs_ctx *ctx) {
     }
     fp.parity = ctx->frame_index & 1u;
     fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
+    const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
+    const int n_groups = (n_tris + 31) / 32;
+    fp.setup_blocks = setup_blocks;
+    fp.ghost_blocks = (n_groups * (int)fp.ghost_slices + 3) / 4;
+    fp.clear_blocks = (n_tiles + shs_dev::CLEAR_BT_PER_BLOCK - 1) / shs_dev::CLEAR_BT_PER_BLOCK;
+    fp.n_owned_rt = owned_bt * (shs_dev::TILE / shs_dev::RTH);
+    // persistent raster grid: one resident wave of workgroups (k_raster runs 4 per CU)
+    const int raster_grid = std::max(1, std::min(fp.n_owned_rt, 256 * 4));
+    if (ensure(ctx, ctx->rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
+    fp.setup_grid = std::max(1, fp.setup_blocks + fp.ghost_blocks + fp.clear_blocks);
+    if (ctx->want_timeline) {
+        const size_t n = (size_t)shs_dev::TL_STRIDE * (fp.setup_grid + raster_grid);
+        if (ensure(ctx, ctx->timeline, n)) return SHS_ERR_HIP;
+        HIP_TRY(ctx, hipMemsetAsync(ctx->timeline.p, 0, n * sizeof(uint64_t), st));
+    }
 
     FrameBuffers fb;
     fb.draws = ctx->draws.p; fb.recs = ctx->recs.p; fb.shade = ctx->shade.p; fb.tile_count = ctx->tile_count.p; fb.bins = ctx->bins.p;
     fb.spill = ctx->spill.p; fb.frags = ctx->frags.p; fb.counters = ctx->counters.p;
-    fb.tile_stat = ctx->tile_stat.p;
+    fb.busy = ctx->busy.p;
+    fb.blk_stat = ctx->blk_stat.p;
+    fb.rstat = ctx->rstat.p;
+    fb.timeline = ctx->want_timeline ? ctx->timeline.p : nullptr;
     fb.boxes = ctx->boxes.p;
     fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;
 
-    const int owned = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     hipEvent_t *ev = nullptr;
     if (ctx->timing) {
         const int k = ctx->ring_next;
@@ -399,7 +441,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], st));
     HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, ka, st));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], st));
-    HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, ka, owned, st));
+    HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, ka, raster_grid, st));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));
     ctx->last_parity = fp.parity;
     ctx->frame_index++;
@@ -407,6 +449,11 @@ static int enqueue_frame(shs_ctx *ctx) {
     ctx->need_check = true;
     ctx->last_n_tris = n_tris;
     ctx->last_n_tiles = n_tiles;
+    ctx->last_setup_blocks = setup_blocks;
+    ctx->last_raster_grid = raster_grid;
+    ctx->last_setup_grid = fp.setup_grid;
+    ctx->last_ghost_blocks = fp.ghost_blocks;
+    ctx->last_clear_blocks = fp.clear_blocks;
     return SHS_OK;
 }
 
@@ -424,15 +471,22 @@ static int finish_frame(shs_ctx *ctx) {
         HIP_TRY(ctx, hipMemcpy(ctx->h_counters, ctx->counters.p + ctx->last_parity * shs_dev::C_NCOUNTERS,
                                shs_dev::C_NCOUNTERS * sizeof(uint32_t), hipMemcpyDeviceToHost));
         const uint32_t *c = ctx->h_counters;
-        // per-tile stats of the owned tiles -> covered pixels, bin entries, fullest tile
-        ctx->h_tile_stat.resize(ctx->last_n_tiles);
-        HIP_TRY(ctx, hipMemcpy(ctx->h_tile_stat.data(), ctx->tile_stat.p, ctx->last_n_tiles * sizeof(uint2),
+        // per-block statistics: setup blocks (triangle classes, bin entries), raster blocks
+        // (covered pixels, fullest bin tile)
+        ctx->h_blk_stat.resize(ctx->last_setup_blocks);
+        ctx->h_rstat.resize(ctx->last_raster_grid);
+        if (ctx->last_setup_blocks)
+            HIP_TRY(ctx, hipMemcpy(ctx->h_blk_stat.data(), ctx->blk_stat.p, ctx->last_setup_blocks * sizeof(uint4),
+                                   hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(ctx->h_rstat.data(), ctx->rstat.p, ctx->last_raster_grid * sizeof(uint2),
                                hipMemcpyDeviceToHost));
-        ctx->last_covered = ctx->last_bins = ctx->last_maxbin = 0;
-        for (int t = ctx->frame.shard_rank; t < ctx->last_n_tiles; t += ctx->frame.shard_count) {
-            ctx->last_covered += ctx->h_tile_stat[t].x;
-            ctx->last_bins += ctx->h_tile_stat[t].y;
-            ctx->last_maxbin = std::max<uint64_t>(ctx->last_maxbin, ctx->h_tile_stat[t].y);
+        ctx->last_covered = ctx->last_bins = ctx->last_maxbin = ctx->last_setup = ctx->last_ghost = ctx->last_unb = 0;
+        for (const uint4 &b : ctx->h_blk_stat) {
+            ctx->last_setup += b.x; ctx->last_ghost += b.y; ctx->last_unb += b.z; ctx->last_bins += b.w;
+        }
+        for (const uint2 &r : ctx->h_rstat) {
+            ctx->last_covered += r.x;
+            ctx->last_maxbin = std::max<uint64_t>(ctx->last_maxbin, r.y);
         }
         // adapt the per-tile bin capacity to the fullest tile (spilled entries stay exact)
         if (ctx->last_maxbin > ctx->bin_cap) ctx->bin_cap = next_pow2((uint32_t)std::min<uint64_t>(ctx->last_maxbin, 1u << 30));
@@ -523,10 +577,10 @@ int shs_get_stats(shs_ctx *ctx, shs_raster_stats *st) {
     int rc = finish_frame(ctx);
     if (rc) return rc;
     st->tri_input = (uint64_t)ctx->last_n_tris;
-    st->tri_setup = ctx->h_counters[shs_dev::C_SETUP];
-    st->tri_ghost = ctx->h_counters[shs_dev::C_GHOST];
+    st->tri_setup = ctx->last_setup;
+    st->tri_ghost = ctx->last_ghost;
     st->bin_entries = ctx->last_bins;
-    st->tri_ghost_unbounded = ctx->h_counters[shs_dev::C_UNBOUNDED];
+    st->tri_ghost_unbounded = ctx->last_unb;
     st->spilled = ctx->h_counters[shs_dev::C_SPILL];
     st->max_tile_bin = ctx->last_maxbin;
     st->ghost_fragments = ctx->h_counters[shs_dev::C_FRAG];
@@ -584,11 +638,34 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
     return SHS_OK;
 }
 
+int shs_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out) {
+    if (!ctx || !n_out || !ctx->have_frame) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    if (!ctx->want_timeline || !ctx->timeline.p) { ctx->err = "timeline not enabled"; return SHS_ERR_INVALID; }
+    const size_t pairs = (size_t)ctx->last_setup_grid + ctx->last_raster_grid;
+    *n_out = (int64_t)(8 + shs_dev::TL_STRIDE * pairs);
+    if (out && capacity >= *n_out) {
+        const uint64_t head[8] = {(uint64_t)ctx->last_setup_grid, (uint64_t)ctx->last_raster_grid,
+                                  (uint64_t)ctx->last_setup_blocks, (uint64_t)ctx->last_ghost_blocks,
+                                  (uint64_t)ctx->last_clear_blocks, (uint64_t)shs_dev::TL_STRIDE, 0, 0};
+        std::memcpy(out, head, sizeof head);
+        HIP_TRY(ctx, hipMemcpy(out + 8, ctx->timeline.p, shs_dev::TL_STRIDE * pairs * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    }
+    return SHS_OK;
+}
+
 int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
     if (!ctx) return SHS_ERR_INVALID;
     if (option == SHS_OPT_RASTER_MODE) {
         if (value < 0 || value > 2) return SHS_ERR_INVALID;
         ctx->force_mode = (int)value;
+        return SHS_OK;
+    }
+    if (option == SHS_OPT_TIMELINE) {
+        if (value < 0 || value > 1) return SHS_ERR_INVALID;
+        ctx->want_timeline = value != 0;
         return SHS_OK;
     }
     if (option == SHS_OPT_BIN_CAPACITY) {

@@ -7,6 +7,7 @@
 // Paths are relative to /root/reference/cpp-folders/src/.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace shs_dev {
@@ -28,6 +29,11 @@ struct alignas(16) DrawGPU {
     float ocol[4];           // vec3(color.rgb) / 255.0f
     float colf[4];           // (float)color.rgb (Flat FS multiplies the int colour)
 };
+
+static_assert(offsetof(DrawGPU, light) % 16 == 0 && offsetof(DrawGPU, cam) == offsetof(DrawGPU, light) + 16 &&
+                  offsetof(DrawGPU, ocol) == offsetof(DrawGPU, light) + 32 &&
+                  offsetof(DrawGPU, colf) == offsetof(DrawGPU, light) + 48,
+              "shading uniforms are read as 4 consecutive float4s");
 
 // Per-triangle raster record written by k_setup, 96 B (6 x float4), read by k_raster through LDS.
 // Holds exactly the per-triangle quantities of Canvas::barycentric_coordinate
@@ -60,26 +66,31 @@ static_assert(sizeof(ShadeRec) == 80, "ShadeRec must stay 80 B");
 
 constexpr uint32_t TRI_CULLED = 1u;
 constexpr uint32_t TRI_GHOST = 2u;       // tile-clamp pixels near the bbox may pass: test them
-constexpr uint32_t TRI_UNBOUNDED = 4u;   // ... anywhere on screen (global list, every tile)
+constexpr uint32_t TRI_UNBOUNDED = 4u;   // ... anywhere on screen, or too far out to bin: every visited
+                                         // pixel outside the ibox is tested by k_setup's ghost waves
 
 __device__ __forceinline__ uint32_t pack16(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
 __device__ __forceinline__ int lo16(uint32_t v) { return (int)(int16_t)(v & 0xffffu); }
 __device__ __forceinline__ int hi16(uint32_t v) { return (int)(int16_t)(v >> 16); }
 
-constexpr int TILE = 32;             // GPU screen tile (32x32 px, one 256-thread workgroup)
+constexpr int TILE = 32;             // bin tile and shard unit (32x32 px)
+constexpr int RTW = 32, RTH = 8;     // raster tile: one 256-thread workgroup, a wave per 8x8 block,
+                                     // one pixel per lane; four raster tiles per bin tile
 constexpr int CHUNK = 256;           // triangle records staged in LDS per pass
 constexpr int CAND = 1024;           // candidate ids gathered per round (4 per thread)
-constexpr int SCAN_MAX_TRIS = 8192;  // scenes up to this size skip binning (scan mode)
+constexpr int SCAN_MAX_TRIS = 4096;  // scenes up to this size skip binning (scan mode)
+constexpr int CLEAR_BT_PER_BLOCK = 4;// bin tiles cleared per k_setup clear block
+constexpr double GHOST_MAX_EXPAND = 48.0;  // larger danger boxes are handled as TRI_UNBOUNDED
 
-// counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one)
-constexpr int C_GHOST = 0, C_SETUP = 1, C_UNBOUNDED = 2, C_OVERFLOW = 3, C_COVERED = 4, C_MAXBIN = 5, C_SPILL = 6,
-              C_FRAG = 7, C_NCOUNTERS = 8;
+// counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one).
+// Only the append positions and the overflow flags live here; statistics go to per-block slots.
+constexpr int C_OVERFLOW = 0, C_SPILL = 1, C_FRAG = 2, C_NCOUNTERS = 4;
 constexpr uint32_t OV_SPILL = 1u, OV_FRAG = 2u;
 
 // Timing-experiment switches (frame flags bits 8+; results are WRONG with any of them set): they
 // let bench --debug-flags attribute kernel time to phases.  Never set by the product path.
 constexpr uint32_t DBG_SKIP_GHOST = 1u << 8, DBG_SKIP_SHADE = 1u << 9, DBG_CLEAR_ONLY = 1u << 10,
-                   DBG_SKIP_BIN = 1u << 11;
+                   DBG_SKIP_BIN = 1u << 11, DBG_SKIP_CLEAR = 1u << 12;
 
 // Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);
 // larger scenes read the device draw table.
@@ -98,36 +109,45 @@ struct alignas(16) GhostFrag {
 struct FrameParams {
     int32_t W, H;
     int32_t rtw, rth;                // reference tile-job size (80x80)
-    int32_t rank, count;             // shard ownership of GPU tiles
-    int32_t tiles_x, tiles_y;
+    int32_t rank, count;             // shard ownership of 32x32 bin tiles (tile % count == rank)
+    int32_t tiles_x, tiles_y;        // bin tiles (raster tiles across == tiles_x)
+    int32_t rtiles_y;                // raster tile rows
     int32_t rt_x, rt_y;              // reference tiles across / down
     int32_t n_tris, n_draws;
     uint32_t clear_rgba;
     uint32_t flags;
-    uint32_t bin_cap;                // per-tile bin capacity
+    uint32_t bin_cap;                // per-bin-tile capacity
     uint32_t spill_cap;
     uint32_t frag_cap;               // ghost fragment capacity
     uint32_t ghost_slices;           // ghost waves per GHOST_GROUP triangles (k_setup)
-    uint32_t parity;                 // counter set used by this frame
-    uint32_t scan_mode;              // 1: no bins, every tile scans all bin boxes (small scenes)
-    uint32_t pad0;
+    uint32_t parity;                 // counter / bin-count set used by this frame
+    uint32_t scan_mode;              // 1: no bins, busy raster tiles scan all bin boxes (small scenes)
+    int32_t setup_blocks, ghost_blocks, clear_blocks;   // k_setup block roles, in this order
+    int32_t n_owned_rt;              // raster tiles of the owned bin tiles (4 per bin tile)
+    int32_t setup_grid;              // k_setup grid (k_raster's timeline slots follow)
 };
 
 struct FrameBuffers {
     const DrawGPU *draws;            // device draw table (n_draws > KARG_DRAWS)
     TriRec *recs;
     ShadeRec *shade;                 // n_tris
-    uint32_t *tile_count;            // n_tiles, zero between frames (k_raster re-zeroes)
-    uint32_t *bins;                  // n_tiles * bin_cap
-    uint2 *spill;                    // (tile, tri) pairs beyond bin_cap
+    uint32_t *tile_count;            // 2 parity sets x n_bin_tiles; k_setup zeroes the next frame's set
+    uint32_t *bins;                  // n_bin_tiles * bin_cap
+    uint2 *spill;                    // (bin tile, tri) pairs beyond bin_cap
     GhostFrag *frags;                // tile-clamp pixels of unbounded slivers that pass (frag_cap)
     uint2 *boxes;                    // n_tris: packed bin box (gbx, gby); empty for culled
     uint32_t *counters;              // 2 * C_NCOUNTERS
-    uint2 *tile_stat;                // n_tiles: (covered pixels, bin entries) of the last frame
+    uint32_t *busy;                  // per raster tile: 1 = has candidates / fragments (k_raster resets)
+    uint4 *blk_stat;                 // per setup block: (set up, ghost, unbounded, bin entries)
+    uint2 *rstat;                    // per raster block: (covered pixels, fullest bin seen)
+    uint64_t *timeline;              // optional: TL_STRIDE slots per workgroup, k_setup then k_raster:
+                                     // start, end, then phase marks of thread 0 (first busy tile)
     uint8_t *color;                  // W*H*4, canvas rows
     float *depth;                    // W*H, screen rows
     float4 *prequant;                // W*H (optional)
 };
+
+constexpr int TL_STRIDE = 12;
 
 struct KArgDraws {
     DrawGPU d[KARG_DRAWS];
@@ -157,17 +177,31 @@ __device__ __forceinline__ f3 m3v(const float *m, f3 v) {
     return {m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z, m[2] * v.x + m[5] * v.y + m[8] * v.z};
 }
 
-// Canvas::barycentric_coordinate body after the per-triangle part (shs_renderer.hpp:809-820);
-// the |denom| < 1e-5 early-out is per triangle and culled in k_setup.
-__device__ __forceinline__ void bary(const TriRec &r, float Px, float Py, float &u, float &v, float &w) {
+// Canvas::barycentric_coordinate body after the per-triangle part (shs_renderer.hpp:809-820) and
+// draw_triangle_tile's inside test (blinn_phong_shading.cpp:226: u < 0 || v < 0 || w < 0 rejects);
+// the |denom| < 1e-5 early-out is per triangle and culled in k_setup.  Returns true when the pixel
+// passes, with (u, v, w) rounded exactly as the reference.
+//
+// Exact early-out: v = nv / denom is certainly negative (so the pixel is rejected) when nv and
+// denom have opposite signs and |nv| > |denom| * 2^-100 -- the quotient is then a nonzero negative
+// float (no underflow to -0, which would pass).  NaN or infinite numerators/denominators never take
+// the early-out (every comparison with NaN is false; |denom| = inf makes the threshold inf).  The
+// two divides, the costliest part, then run only for pixels inside or at the edge of the triangle.
+__device__ __forceinline__ bool bary_pass(const TriRec &r, float Px, float Py, float &u, float &v, float &w) {
     const float vpx = Px - r.ax, vpy = Py - r.ay;
     const float t0 = vpx * r.v0x, t1 = vpy * r.v0y;
     const float d20 = t0 + t1;
     const float t2 = vpx * r.v1x, t3 = vpy * r.v1y;
     const float d21 = t2 + t3;
-    v = (r.d11 * d20 - r.d01 * d21) / r.denom;
-    w = (r.d00 * d21 - r.d01 * d20) / r.denom;
+    const float nv = r.d11 * d20 - r.d01 * d21;
+    const float nw = r.d00 * d21 - r.d01 * d20;
+    const float thr = fabsf(r.denom) * 0x1p-100f;   // exact: |denom| >= 1e-5 keeps it normal
+    const bool dneg = r.denom < 0.0f;
+    if (((nv < 0.0f) != dneg && fabsf(nv) > thr) || ((nw < 0.0f) != dneg && fabsf(nw) > thr)) return false;
+    v = nv / r.denom;
+    w = nw / r.denom;
     u = (1.0f - v) - w;
+    return !(u < 0 || v < 0 || w < 0);
 }
 
 }  // namespace shs_dev

@@ -8,5 +8,5 @@ namespace shs_internal {
 hipError_t launch_setup(const shs_dev::FrameParams &fp, const shs_dev::FrameBuffers &fb, const shs_dev::KArgDraws &ka,
                         hipStream_t s);
 hipError_t launch_raster(const shs_dev::FrameParams &fp, const shs_dev::FrameBuffers &fb, const shs_dev::KArgDraws &ka,
-                         int n_owned_tiles, hipStream_t s);
+                         int grid, hipStream_t s);
 }  // namespace shs_internal

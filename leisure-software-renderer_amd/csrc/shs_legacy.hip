@@ -4,17 +4,21 @@
 // (cpp-folders/src/hello-3d-primitives/hello_pipeline_{blinn_phong,phong,gouraud,flat}_shading.cpp).
 //
 // Pipeline per frame: two launches on one HIP stream, no memsets, no copies for <= 6 draws.
-//   k_setup   one thread per triangle: VS x3 (mvp), clip_to_screen, area/denominator culls, the
-//             per-triangle half of barycentric_coordinate, a 96-B raster record, and the triangle
-//             id appended straight into the per-tile bins its bin box touches (unordered; a spill
-//             list past the bin capacity).
-//   k_raster  one 256-thread workgroup per 32x32 tile (8x8 blocks, a column of four per wave):
-//             stage the tile's records in LDS, resolve every pixel to the lexicographic minimum
-//             (z, submission index) -- identical to the reference's in-order strict-less z test
-//             (the first triangle with the minimal z wins) -- then shade only the winners from the
-//             per-triangle varyings k_setup wrote, and write colour (canvas rows) and depth (screen
-//             rows) once, with the clear fused (empty tiles take a clear-only fast path).
-// The z-buffer never round-trips through HBM: HBM sees each input once and each output once.
+//   k_setup   three block roles in one grid:
+//             setup  one thread per triangle: VS x3 (mvp), clip_to_screen, area/denominator culls,
+//                    the per-triangle half of barycentric_coordinate (a 96-B raster record), the
+//                    per-corner shading varyings, "busy" marks on the raster tiles its bin box
+//                    touches and (large scenes) appends into per-bin-tile lists;
+//             ghost  the reference's tile-clamp pixels of unbounded slivers (see below);
+//             clear  streaming clear of the colour / depth planes (16-B stores).
+//   k_raster  persistent: each workgroup takes the busy 32x8 raster tiles of its share; a wave owns
+//             an 8x8 block, one pixel per lane.  Candidates (bin box overlaps the tile) are staged
+//             in LDS; each pixel resolves to the lexicographic minimum (z, submission index) --
+//             identical to the reference's in-order strict-less z test (the first triangle with
+//             the minimal z wins); only the winner is shaded, then colour (canvas rows) and depth
+//             (screen rows) are written as whole 128-B row segments.
+// The z-buffer never round-trips through HBM: each busy tile's pixels are written once more on
+// top of the clear, everything else exactly once.
 //
 // Tile-clamp semantics.  draw_triangle_tile clamps a triangle's bbox to the 80x80 tile job that
 // runs it (blinn_phong_shading.cpp:208-224), so the reference also tests pixels OUTSIDE the
@@ -22,7 +26,10 @@
 // >= 0.49 px outside the bbox, so an exact barycentric is <= -(distance)/(2*extent); k_setup
 // bounds barycentric_coordinate's float error (an affine function of the distance) and proves
 // those pixels rejected, except inside a small "danger box" around slivers (TRI_GHOST): k_raster
-// then evaluates the reference's exact visited set there.  DESIGN.md has the derivation.
+// then evaluates the reference's exact visited set there.  Slivers with no usable bound
+// (TRI_UNBOUNDED) keep their own bbox for binning; k_setup's ghost waves test every pixel the
+// reference visits outside it and hand the rare passing ones to k_raster as fragments.
+// DESIGN.md has the derivation.
 #include <float.h>
 
 #include "shs_device.hpp"
@@ -51,15 +58,16 @@ __device__ __forceinline__ double2 danger_margin(const TriRec &r) {
     const double ED = 6.1 * u * (A00 * A11 + A01 * A01);
     const double Dlow = Dabs - ED;
     if (!(Dlow > 0.0) || !(Dabs < 1e300)) return none;
-    const double K1 = 7.2 * u + ED / Dlow;
+    const double iDlow = 1.0 / Dlow, iDabs = 1.0 / Dabs;   // (the 1.25 slack covers the products' rounding)
+    const double K1 = 7.2 * u + ED * iDlow;
     const double p0 = Wx + 0.01, q0 = Wy + 0.01;
     const double A20 = p0 * a + q0 * b, A21 = p0 * c + q0 * d;
     const double Nv0 = A11 * A20 + A01 * A21, Nvx = A11 * a + A01 * c, Nvy = A11 * b + A01 * d;
     const double Nw0 = A00 * A21 + A01 * A20, Nwx = A00 * c + A01 * a, Nwy = A00 * d + A01 * b;
-    const double s = K1 / Dabs * (2.0 + 2.0 * u);
-    const double e0 = 1.25 * ((Nv0 + Nw0) * s + u * (2.0 + (2.0 * Nv0 + Nw0) / Dlow));
-    const double ex = 1.25 * ((Nvx + Nwx) * s + u * (2.0 * Nvx + Nwx) / Dlow);
-    const double ey = 1.25 * ((Nvy + Nwy) * s + u * (2.0 * Nvy + Nwy) / Dlow);
+    const double s = K1 * iDabs * (2.0 + 2.0 * u);
+    const double e0 = 1.25 * ((Nv0 + Nw0) * s + u * (2.0 + (2.0 * Nv0 + Nw0) * iDlow));
+    const double ex = 1.25 * ((Nvx + Nwx) * s + u * (2.0 * Nvx + Nwx) * iDlow);
+    const double ey = 1.25 * ((Nvy + Nwy) * s + u * (2.0 * Nvy + Nwy) * iDlow);
     const double S = ex * Wx + ey * Wy;
     if (!(S < 0.5)) return none;
     const double m0 = e0 / (1.0 - 2.0 * S);
@@ -69,8 +77,24 @@ __device__ __forceinline__ double2 danger_margin(const TriRec &r) {
 
 __device__ __forceinline__ bool finitef(float x) { return fabsf(x) <= FLT_MAX; }
 
-__device__ __forceinline__ const DrawGPU *draw_table(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka) {
-    return fp.n_draws <= KARG_DRAWS ? ka.d : fb.draws;
+// x^(2^k) for the shaders' integer shininess (32, 64), by k squarings in double, narrowed to
+// float.  The reference's powf / pow(double) results are the correctly rounded (or <= 1 ulp double)
+// power; the squaring chain is within (2^k - 1) double ulps of the exact value, so the float
+// result agrees except within ~1e-14 relative of a float rounding boundary -- far inside the
+// 1e-5 shaded-float tolerance (north_star).
+template <int K>
+__device__ __forceinline__ float pow2k(float x) {
+    double d = (double)x;
+#pragma unroll
+    for (int i = 0; i < K; ++i) d = d * d;
+    return (float)d;
+}
+
+// The draw table: the kernel-argument copy (KARG, <= KARG_DRAWS draws) or the device table.  A
+// compile-time choice, so the pointer keeps its address space (uniform indices -> scalar loads).
+template <bool KARG>
+__device__ __forceinline__ const DrawGPU *draw_table(const FrameBuffers &fb, const KArgDraws &ka) {
+    return KARG ? ka.d : fb.draws;
 }
 
 // floor of a finite float, clamped into [lo, hi] before the conversion
@@ -98,8 +122,14 @@ __device__ __forceinline__ int find_draw(const DrawGPU *draws, int n_draws, int 
 // Per-triangle setup of draw_triangle_tile: VS position (mvp * vec4(p,1)), Canvas::clip_to_screen
 // (shs_renderer.hpp:823-831), the area cull (blinn_phong_shading.cpp:219-220), the per-triangle
 // half of barycentric_coordinate, the integer bbox and the bin box (flags/boxes as in TriRec).
-__device__ __forceinline__ TriRec make_rec(const FrameParams &fp, const DrawGPU &dr, int draw, int local) {
-    const float *p = dr.pos + 9 * (size_t)local;
+// Load a soup triangle's 9 floats into registers (before any store of the caller, so the compiler
+// never has to re-read them behind a possibly aliasing store).
+__device__ __forceinline__ void load9(const float *src, float (&v)[9]) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v[k] = src[k];
+}
+
+__device__ __forceinline__ TriRec make_rec(const FrameParams &fp, const DrawGPU &dr, int draw, int local, const float (&p)[9]) {
     float sx[3], sy[3], sz[3];
     const float fw = (float)(fp.W - 1), fh = (float)(fp.H - 1);
 #pragma unroll
@@ -150,7 +180,9 @@ __device__ __forceinline__ TriRec make_rec(const FrameParams &fp, const DrawGPU 
         // test_config_blinn_phong[c1]); keep this region free of values live across branches.
         const bool dfin = finitef(r.d00) && finitef(r.d01) && finitef(r.d11) && finitef(r.denom);
         const double2 dg = dfin ? danger_margin(r) : make_double2(-1.0, -1.0);
-        const bool unbounded = !(dg.x >= 0.0);
+        // no bound, or a danger box too large to bin cheaply: the ghost waves take the pixels outside
+        // the ibox (exact either way)
+        const bool unbounded = !(dg.x >= 0.0) || dg.x > GHOST_MAX_EXPAND || dg.y > GHOST_MAX_EXPAND;
         const bool ghost = unbounded || dg.x >= 0.49 || dg.y >= 0.49;
         // expansion of the bin box beyond the float bbox: 0 (the ibox) or the danger margin + 1 px;
         // unbounded slivers keep their ibox here and k_setup's ghost waves cover the rest
@@ -168,39 +200,145 @@ __device__ __forceinline__ TriRec make_rec(const FrameParams &fp, const DrawGPU 
     return r;
 }
 
-// Ghost waves: the pixels the reference's tile clamp makes an unbounded sliver visit OUTSIDE its
-// integer bbox (blinn_phong_shading.cpp:208-224: per 80x80 tile job, the bbox clamped to the tile).
-// One wave per GHOST_GROUP triangles recomputes their records (make_rec is deterministic); for each
-// unbounded sliver the wave enumerates those pixels lane-parallel (per reference tile: a corner
-// pixel, or a row / column segment) and appends every pixel whose barycentrics pass as a fragment.
-constexpr int GHOST_GROUP = 32;
-
+// ---- wave helpers -----------------------------------------------------------------------------
 // LDS hand-off between lanes of ONE wave: the wave's LDS operations execute in order, so only the
-// compiler must be kept from reordering (no s_barrier: the four waves of a ghost block diverge).
+// compiler must be kept from reordering (no s_barrier: waves of a ghost block diverge).
 __device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __asm__ volatile("" ::: "memory");
 }
 
-struct GhostScratch {          // per-wave LDS
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+}
+
+// Wave-aggregated appends to NK per-key counters (call with the whole wave converged).  Lanes with
+// key[k] >= 0 get a unique slot of counter[key[k]]; each distinct key costs ONE returning atomic, and
+// all of them are issued before any return value is consumed (one memory round trip in total).
+template <int NK>
+__device__ __forceinline__ void wave_append(uint32_t *counter, const int (&key)[NK], uint32_t (&slot)[NK]) {
+    const int lane = __lane_id();
+    uint32_t add[NK], rank[NK], leader[NK], ret[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        add[k] = 0u; rank[k] = 0u; leader[k] = 0u;
+        uint64_t pending = __ballot(key[k] >= 0);
+        while (pending) {
+            const int first = __ffsll((unsigned long long)pending) - 1;
+            const int lk = __shfl(key[k], first);
+            const uint64_t peers = __ballot(key[k] == lk) & pending;
+            if (lane == first) add[k] = (uint32_t)__popcll(peers);
+            if ((peers >> lane) & 1ull) { leader[k] = (uint32_t)first; rank[k] = lanes_below(peers); }
+            pending &= ~peers;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NK; ++k) ret[k] = add[k] ? atomicAdd(&counter[key[k]], add[k]) : 0u;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) slot[k] = __shfl(ret[k], (int)leader[k]) + rank[k];
+}
+
+// Single-counter wave append (converged wave): slot for lanes with want.
+__device__ __forceinline__ uint32_t wave_append1(uint32_t *counter, bool want) {
+    const uint64_t m = __ballot(want);
+    if (!m) return 0u;
+    const int first = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0u;
+    if (__lane_id() == first) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    return __shfl(base, first) + lanes_below(m);
+}
+
+// Index of the draw owning triangle gid, and whether the whole wave shares it (then the draw's
+// uniforms are read with scalar loads).
+__device__ __forceinline__ int wave_draw(const DrawGPU *draws, int n_draws, int gid, bool valid, bool &uniform) {
+    const int lo = valid ? find_draw(draws, n_draws, gid) : 0;
+    const int lo0 = __builtin_amdgcn_readfirstlane(lo);
+    uniform = __ballot(valid && lo != lo0) == 0;
+    return uniform ? lo0 : lo;
+}
+
+// Profiling marks (SHS_OPT_TIMELINE): thread 0 stamps phase k of its workgroup.
+__device__ __forceinline__ void tl_mark(uint64_t *tl, int slot, int k) {
+    if (tl && threadIdx.x == 0) tl[TL_STRIDE * slot + 2 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ bool owned_bin_tile(const FrameParams &fp, int bx, int by) {
+    return ((by * fp.tiles_x + bx) % fp.count) == fp.rank;
+}
+
+// ---- ghost waves ------------------------------------------------------------------------------
+// The pixels the reference's tile clamp makes an unbounded sliver visit OUTSIDE its integer bbox
+// (blinn_phong_shading.cpp:208-224: per 80x80 tile job, the float bbox clamped to the tile).  The
+// visited set is separable: in reference-tile column c the x-range is [(int)max(tminx, min(tmaxx,
+// fminx)), (int)min(tmaxx, max(tminx, fmaxx))] -- one edge column for the columns left (tmaxx <
+// fminx, a prefix) or right (tminx > fmaxx, a suffix) of the bbox, the bbox's own span for the
+// overlapping columns -- and likewise in y.  With Xout / Yout the edge columns / rows and Xin /
+// Yin the overlapping spans, the visited pixels outside the ibox are (Xout x (Yout u Yin)) u
+// (Xin x Yout): enumerated lane-parallel by index arithmetic.  One wave per (GHOST_GROUP
+// triangles, slice) recomputes the group's records (make_rec is deterministic) and takes every
+// fp.ghost_slices-th 64-pixel batch of each unbounded sliver in the group.
+constexpr int GHOST_GROUP = 32;
+
+struct SliverSpan {
+    int cl, cr, ru, rd;             // edge columns left / right, edge rows above / below
+    int xi0, xi1, yi0, yi1;         // overlapping spans (empty when lo > hi)
+};
+
+// Count the reference-tile columns (rows) entirely before / after [fmin, fmax]; span of the rest.
+__device__ __forceinline__ void classify_axis(int n_rt, int rts, int extent, float fmin, float fmax, int &before,
+                                              int &after, int &lo, int &hi) {
+    before = 0; after = 0;
+    for (int c0 = 0; c0 < n_rt; c0 += 64) {
+        const int c = c0 + __lane_id();
+        const bool valid = c < n_rt;
+        const float tmin = (float)(c * rts), tmax = (float)(min(c * rts + rts, extent) - 1);
+        before += __popcll(__ballot(valid && tmax < fmin));
+        after += __popcll(__ballot(valid && tmin > fmax));
+    }
+    lo = 0; hi = -1;
+    if (before + after < n_rt) {
+        const int c0 = before, c1 = n_rt - 1 - after;
+        lo = (int)g_max((float)(c0 * rts), fmin);
+        hi = (int)g_min((float)(min(c1 * rts + rts, extent) - 1), fmax);
+    }
+}
+
+// i-th edge column (row): the first `before` are the right edges of the leading tiles, the rest
+// the left edges of the trailing ones.
+__device__ __forceinline__ int edge_coord(int i, int before, int n_rt, int after, int rts, int extent) {
+    return i < before ? min((i + 1) * rts, extent) - 1 : (n_rt - after + (i - before)) * rts;
+}
+
+struct GhostScratch {           // per-wave LDS
     float4 rec[6];
-    int pref[64], w[64], x0[64], y0[64];
 };
 
 __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
                                            uint32_t *cnt, int group, int slice, GhostScratch &gs) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int gid = group * GHOST_GROUP + lane;
     TriRec r;
     bool unb = false;
-    if (lane < GHOST_GROUP && gid < fp.n_tris) {
-        const int d = find_draw(draws, fp.n_draws, gid);
-        r = make_rec(fp, draws[d], d, gid - draws[d].tri_base);
+    const bool valid = lane < GHOST_GROUP && gid < fp.n_tris;
+    bool uni;
+    const int d = wave_draw(draws, fp.n_draws, gid, valid, uni);
+    if (valid) {
+        if (uni) {
+            const int du = __builtin_amdgcn_readfirstlane(d);
+            const int local = gid - draws[du].tri_base;
+            float p[9];
+            load9(draws[du].pos + 9 * (size_t)local, p);
+            r = make_rec(fp, draws[du], du, local, p);
+        } else {
+            const int local = gid - draws[d].tri_base;
+            float p[9];
+            load9(draws[d].pos + 9 * (size_t)local, p);
+            r = make_rec(fp, draws[d], d, local, p);
+        }
         unb = (r.flags & TRI_UNBOUNDED) != 0;
     }
     uint64_t todo = __ballot(unb);
-    const int n_rt = fp.rt_x * fp.rt_y;
+    const int stride = 64 * (int)fp.ghost_slices;
     while (todo) {
         const int src = __ffsll((unsigned long long)todo) - 1;
         todo &= todo - 1;
@@ -211,116 +349,95 @@ __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuf
         }
         wave_lds_sync();
         const TriRec t = rec_from(gs.rec);
+        wave_lds_sync();   // gs.rec is rewritten by the next sliver
         const uint32_t tri = (uint32_t)(group * GHOST_GROUP + src);
         const int ix0 = lo16(t.ibx), ix1 = hi16(t.ibx), iy0 = lo16(t.iby), iy1 = hi16(t.iby);
-        for (int rb = 0; rb < n_rt; rb += 64) {
-            // lane -> reference tile rb + lane: its clamped visited rectangle and pixel count
-            const int rt = rb + lane;
-            int lx0 = 0, ly0 = 0, w = 1, npx = 0;
-            if (rt < n_rt) {
-                const int rx = rt % fp.rt_x, ry = rt / fp.rt_x;
-                const float tminx = (float)(rx * fp.rtw), tmaxx = (float)(min(rx * fp.rtw + fp.rtw, fp.W) - 1);
-                const float tminy = (float)(ry * fp.rth), tmaxy = (float)(min(ry * fp.rth + fp.rth, fp.H) - 1);
-                const float bminx = g_max(tminx, g_min(tmaxx, t.fminx)), bmaxx = g_min(tmaxx, g_max(tminx, t.fmaxx));
-                const float bminy = g_max(tminy, g_min(tmaxy, t.fminy)), bmaxy = g_min(tmaxy, g_max(tminy, t.fmaxy));
-                if (!(bminx > bmaxx || bminy > bmaxy)) {
-                    lx0 = (int)bminx; ly0 = (int)bminy;
-                    const int lx1 = (int)bmaxx, ly1 = (int)bmaxy;
-                    const bool inside = lx0 >= ix0 && lx1 <= ix1 && ly0 >= iy0 && ly1 <= iy1;
-                    w = lx1 - lx0 + 1;
-                    npx = inside ? 0 : w * (ly1 - ly0 + 1);
+        SliverSpan sp;
+        classify_axis(fp.rt_x, fp.rtw, fp.W, t.fminx, t.fmaxx, sp.cl, sp.cr, sp.xi0, sp.xi1);
+        classify_axis(fp.rt_y, fp.rth, fp.H, t.fminy, t.fmaxy, sp.ru, sp.rd, sp.yi0, sp.yi1);
+        const int nxo = sp.cl + sp.cr, nyo = sp.ru + sp.rd;
+        const int nxi = max(sp.xi1 - sp.xi0 + 1, 0), nyi = max(sp.yi1 - sp.yi0 + 1, 0);
+        const int ny = nyo + nyi;
+        const int64_t total_a = (int64_t)nxo * ny, total = total_a + (int64_t)nxi * nyo;
+        for (int64_t kb = (int64_t)slice * 64; kb < total; kb += stride) {
+            const int64_t k = kb + lane;
+            bool pass = false;
+            int px = 0, py = 0;
+            float z = 0.f, u = 0.f, v = 0.f, w = 0.f;
+            if (k < total) {
+                if (k < total_a) {
+                    const int xi = (int)(k / ny), yi = (int)(k % ny);
+                    px = edge_coord(xi, sp.cl, fp.rt_x, sp.cr, fp.rtw, fp.W);
+                    py = yi < nyo ? edge_coord(yi, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H) : sp.yi0 + (yi - nyo);
+                } else {
+                    const int64_t kk = k - total_a;
+                    px = sp.xi0 + (int)(kk / nyo);
+                    py = edge_coord((int)(kk % nyo), sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H);
+                }
+                const bool in_ibox = px >= ix0 && px <= ix1 && py >= iy0 && py <= iy1;   // k_raster's part
+                if (!in_ibox && owned_bin_tile(fp, px / TILE, py / TILE) && bary_pass(t, (float)px + 0.5f, (float)py + 0.5f, u, v, w)) {
+                    z = (u * t.z0 + v * t.z1) + w * t.z2;
+                    pass = z < FLT_MAX;   // NaN / FLT_MAX never pass the strict z test
                 }
             }
-            // wave-inclusive prefix of the pixel counts (all lanes active here)
-            int incl = npx;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(incl, o);
-                if (lane >= o) incl += v;
-            }
-            const int total = __shfl(incl, 63);
-            gs.pref[lane] = incl;
-            gs.w[lane] = w;
-            gs.x0[lane] = lx0;
-            gs.y0[lane] = ly0;
-            wave_lds_sync();
-            // this wave's slice of the pixel index space (fp.ghost_slices waves share each group)
-            for (int k = slice * 64 + lane; k < total; k += 64 * (int)fp.ghost_slices) {
-                int lo = 0, hi = 63;                         // owner: first lane with pref > k
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (gs.pref[mid] > k) hi = mid; else lo = mid + 1;
-                }
-                const int off = k - (lo ? gs.pref[lo - 1] : 0);
-                const int wq = gs.w[lo];
-                const int px = gs.x0[lo] + off % wq, py = gs.y0[lo] + off / wq;
-                if (px >= ix0 && px <= ix1 && py >= iy0 && py <= iy1) continue;   // k_raster's part
-                const int tl = (py / TILE) * fp.tiles_x + px / TILE;
-                if (tl % fp.count != fp.rank) continue;
-                float u, v, ww;
-                bary(t, (float)px + 0.5f, (float)py + 0.5f, u, v, ww);
-                if (u < 0 || v < 0 || ww < 0) continue;
-                const float z = (u * t.z0 + v * t.z1) + ww * t.z2;
-                if (!(z < FLT_MAX)) continue;   // NaN / FLT_MAX never pass the strict z test
-                const uint32_t slot = atomicAdd(&cnt[C_FRAG], 1u);
+            const uint32_t slot = wave_append1(&cnt[C_FRAG], pass);
+            if (pass) {
                 if (slot < fp.frag_cap) {
                     GhostFrag g;
                     g.xy = (uint32_t)px | ((uint32_t)py << 16);
                     g.z = z;
                     g.id = tri;
                     g.v = v;
-                    g.w = ww;
+                    g.w = w;
                     g.pad[0] = g.pad[1] = g.pad[2] = 0u;
                     fb.frags[slot] = g;
+                    fb.busy[(py / RTH) * fp.tiles_x + px / RTW] = 1u;
                 } else {
                     atomicOr(&cnt[C_OVERFLOW], OV_FRAG);
                 }
             }
-            wave_lds_sync();   // the next reference-tile batch overwrites gs
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
-    __shared__ GhostScratch s_ghost[4];
-    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
-    const DrawGPU *draws = draw_table(fp, fb, ka);
-    const int setup_blocks = (fp.n_tris + 255) / 256;
-    // zero the other parity set for the next frame (block 0 exists even for an empty frame)
-    if (blockIdx.x == 0 && threadIdx.x < C_NCOUNTERS) fb.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
-    if ((int)blockIdx.x >= setup_blocks) {
-        const int wave = threadIdx.x >> 6;
-        const int gw = ((int)blockIdx.x - setup_blocks) * 4 + wave;
-        const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
-        if (gw < n_groups * (int)fp.ghost_slices && !(fp.flags & DBG_SKIP_GHOST))
-            ghost_wave(fp, fb, draws, cnt, gw / (int)fp.ghost_slices, gw % (int)fp.ghost_slices, s_ghost[wave]);
-        return;
-    }
-    const int gid = blockIdx.x * 256 + threadIdx.x;
-    if (gid >= fp.n_tris) return;
-    const int lo = find_draw(draws, fp.n_draws, gid);
-    const DrawGPU &dr = draws[lo];
-    const int local = gid - dr.tri_base;
-    const float *p = dr.pos + 9 * (size_t)local;
-    TriRec r = make_rec(fp, dr, lo, local);
-    const uint32_t flags = r.flags;
-    {
-        const float4 *src = reinterpret_cast<const float4 *>(&r);
-        float4 *dst = reinterpret_cast<float4 *>(&fb.recs[gid]);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) dst[j] = src[j];
-    }
-    fb.boxes[gid] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
-    const int gx0 = lo16(r.gbx), gx1 = hi16(r.gbx), gy0 = lo16(r.gby), gy1 = hi16(r.gby);
-    if (flags & TRI_CULLED) return;
+// ---- k_setup ----------------------------------------------------------------------------------
 
-    // Shading varyings of the three corners (the VS outputs the FS interpolates), computed once per
-    // triangle instead of once per winning pixel.
-    {
-        ShadeRec sr;
+// Busy marks and bin appends of one bin box.  Small boxes are done per lane (batched, one memory
+// round trip); lanes with large boxes are served one at a time by the whole wave.
+constexpr int SMALL_RT = 8;   // raster tiles a lane marks by itself
+constexpr int SMALL_BT = 4;   // bin tiles a lane appends to by itself
+
+__device__ __forceinline__ void append_bin(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int t, uint32_t pos,
+                                           uint32_t id) {
+    if (pos < fp.bin_cap) {
+        fb.bins[(size_t)t * fp.bin_cap + pos] = id;
+    } else {
+        const uint32_t sp = atomicAdd(&cnt[C_SPILL], 1u);
+        if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t, id);
+        else atomicOr(&cnt[C_OVERFLOW], OV_SPILL);
+    }
+}
+
+// The per-triangle part of k_setup: raster record r and shading varyings sr (the caller stores
+// both, coalesced).
+__device__ __forceinline__ void setup_tri(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU &dr, int lo,
+                                          int gid, TriRec &r, ShadeRec &sr) {
+    const int local = gid - dr.tri_base;
+    float p[9], N[9];
+    load9(dr.pos + 9 * (size_t)local, p);
+    load9(dr.nrm + 9 * (size_t)local, N);
+    r = make_rec(fp, dr, lo, local, p);
+    tl_mark(fb.timeline, blockIdx.x, 4);
+    fb.boxes[gid] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
+    sr.shading = dr.shading;
+    sr.draw = lo;
+    if (!(r.flags & TRI_CULLED)) {
+        // Shading varyings of the three corners (the VS outputs the FS interpolates), computed
+        // once per triangle instead of once per winning pixel.
         sr.shading = dr.shading;
         sr.draw = lo;
-        const float *N = dr.nrm + 9 * (size_t)local;
+#pragma unroll
+        for (int j = 0; j < 18; ++j) sr.v[j] = 0.0f;
         if (dr.shading == 0) {
             // Flat VS (flat_shading.cpp:54): normal = mat3(mv) * n
 #pragma unroll
@@ -343,7 +460,7 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
                     const f3 viewDir = normalize3(sub3(cam, wp));
                     const float diff = g_max(dot3(nr, L), 0.0f);
                     const f3 half = normalize3(add3(L, viewDir));
-                    const float spec = (float)pow((double)g_max(dot3(nr, half), 0.0f), 32.0);
+                    const float spec = pow2k<5>(g_max(dot3(nr, half), 0.0f));   // glm::pow(x, 32.0f)
                     const float sum = (0.15f + diff * 1.0f) + (0.5f * spec) * 1.0f;
                     sr.v[3 * k] = g_clamp01(sum * oc.x);
                     sr.v[3 * k + 1] = g_clamp01(sum * oc.y);
@@ -355,78 +472,224 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
                 }
             }
         }
-        const float4 *src = reinterpret_cast<const float4 *>(&sr);
-        float4 *dst = reinterpret_cast<float4 *>(&fb.shade[gid]);
-#pragma unroll
-        for (int j = 0; j < 5; ++j) dst[j] = src[j];
     }
-
-    atomicAdd(&cnt[C_SETUP], 1u);
-    if (flags & TRI_GHOST) atomicAdd(&cnt[C_GHOST], 1u);
-    if (flags & TRI_UNBOUNDED) atomicAdd(&cnt[C_UNBOUNDED], 1u);
-    if (fp.scan_mode) return;   // small scene: k_raster scans the bin boxes; no bins
-    if (gx0 > gx1 || gy0 > gy1 || (fp.flags & DBG_SKIP_BIN)) return;
-    const int tx0 = gx0 / TILE, tx1 = gx1 / TILE, ty0 = gy0 / TILE, ty1 = gy1 / TILE;
-    const int ntx = tx1 - tx0 + 1, nty = ty1 - ty0 + 1;
-    if (ntx * nty <= 4) {
-        // common case: issue every bin append before consuming any position (one round trip)
-        int t[4];
-        uint32_t pos[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int kx = tx0 + (k % ntx), ky = ty0 + (k / ntx);
-            t[k] = (k < ntx * nty) ? ky * fp.tiles_x + kx : -1;
-            if (t[k] >= 0 && t[k] % fp.count != fp.rank) t[k] = -1;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) pos[k] = t[k] >= 0 ? atomicAdd(&fb.tile_count[t[k]], 1u) : 0u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (t[k] < 0) continue;
-            if (pos[k] < fp.bin_cap) {
-                fb.bins[(size_t)t[k] * fp.bin_cap + pos[k]] = (uint32_t)gid;
-            } else {
-                const uint32_t sp = atomicAdd(&cnt[C_SPILL], 1u);
-                if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t[k], (uint32_t)gid);
-                else atomicOr(&cnt[C_OVERFLOW], OV_SPILL);
-            }
-        }
-        return;
-    }
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-            const int t = ty * fp.tiles_x + tx;
-            if (t % fp.count != fp.rank) continue;
-            const uint32_t pos = atomicAdd(&fb.tile_count[t], 1u);
-            if (pos < fp.bin_cap) {
-                fb.bins[(size_t)t * fp.bin_cap + pos] = (uint32_t)gid;
-            } else {
-                const uint32_t sp = atomicAdd(&cnt[C_SPILL], 1u);
-                if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t, (uint32_t)gid);
-                else atomicOr(&cnt[C_OVERFLOW], OV_SPILL);
-            }
-        }
 }
 
-// ---- k_raster -------------------------------------------------------------------------------
+// Write the wave's per-lane records (N float4 each, lanes [0, n_valid)) to dst[0 .. n_valid*N)
+// through the wave's LDS scratch: every store instruction covers 1 KB of contiguous HBM instead of
+// 64 strided 16-B pieces.
+template <int N>
+__device__ __forceinline__ void wave_store_coalesced(float4 *dst, const float4 (&v)[N], int n_valid, float4 *scratch) {
+    const int lane = __lane_id();
+#pragma unroll
+    for (int j = 0; j < N; ++j) scratch[lane * N + j] = v[j];
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int f = k * 64 + lane;
+        if (f < n_valid * N) dst[f] = scratch[f];
+    }
+    wave_lds_sync();
+}
 
+__device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, uint32_t *cnt,
+                            uint32_t (&s_stat)[4], float4 *wscratch) {
+    const int tid = threadIdx.x, lane = __lane_id();
+    const int gid = blockIdx.x * 256 + tid;
+    if (tid < 4) s_stat[tid] = 0u;
+    __syncthreads();
+    const bool valid = gid < fp.n_tris;
+    uint32_t flags = TRI_CULLED;
+    int gx0 = 0, gx1 = -1, gy0 = 0, gy1 = -1;
+    bool uni;
+    const int lo = wave_draw(draws, fp.n_draws, gid, valid, uni);
+    tl_mark(fb.timeline, blockIdx.x, 0);
+    TriRec r;
+    ShadeRec sr;
+    if (valid) {
+        if (uni) {
+            const int lu = __builtin_amdgcn_readfirstlane(lo);
+            setup_tri(fp, fb, draws[lu], lu, gid, r, sr);
+        } else {
+            setup_tri(fp, fb, draws[lo], lo, gid, r, sr);
+        }
+        flags = r.flags;
+        gx0 = lo16(r.gbx); gx1 = hi16(r.gbx); gy0 = lo16(r.gby); gy1 = hi16(r.gby);
+    }
+    {   // coalesced record / varyings stores (the wave's triangles are consecutive)
+        const int wbase = (int)blockIdx.x * 256 + (tid & ~63);
+        const int n_valid = max(0, min(64, fp.n_tris - wbase));
+        wave_store_coalesced<6>(reinterpret_cast<float4 *>(fb.recs + wbase), reinterpret_cast<const float4(&)[6]>(r),
+                                n_valid, wscratch);
+        wave_store_coalesced<5>(reinterpret_cast<float4 *>(fb.shade + wbase), reinterpret_cast<const float4(&)[5]>(sr),
+                                n_valid, wscratch);
+    }
+    tl_mark(fb.timeline, blockIdx.x, 1);
+    const bool live = valid && !(flags & TRI_CULLED) && gx0 <= gx1 && gy0 <= gy1;
+    if (!live) { gx0 = 0; gx1 = -1; gy0 = 0; gy1 = -1; }
+
+    // -- busy marks on the raster tiles (32x8) of the bin box (owned bin tiles only)
+    const int rx0 = gx0 / RTW, rx1 = live ? gx1 / RTW : -1, ry0 = gy0 / RTH, ry1 = live ? gy1 / RTH : -1;
+    const int n_rt = live ? (rx1 - rx0 + 1) * (ry1 - ry0 + 1) : 0;
+    if (n_rt > 0 && n_rt <= SMALL_RT) {
+        for (int ry = ry0; ry <= ry1; ++ry)
+            for (int rx = rx0; rx <= rx1; ++rx)
+                if (owned_bin_tile(fp, rx, ry / (TILE / RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+    }
+    {
+        uint64_t big = __ballot(n_rt > SMALL_RT);
+        while (big) {
+            const int src = __ffsll((unsigned long long)big) - 1;
+            big &= big - 1;
+            const int bx0 = __shfl(rx0, src), bx1 = __shfl(rx1, src), by0 = __shfl(ry0, src), by1 = __shfl(ry1, src);
+            const int nx = bx1 - bx0 + 1, n = nx * (by1 - by0 + 1);
+            for (int k = lane; k < n; k += 64) {
+                const int rx = bx0 + k % nx, ry = by0 + k / nx;
+                if (owned_bin_tile(fp, rx, ry / (TILE / RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+            }
+        }
+    }
+
+    tl_mark(fb.timeline, blockIdx.x, 2);
+    // -- bin appends (large scenes): bin tiles of the bin box
+    uint32_t n_bin = 0;
+    if (!fp.scan_mode && !(fp.flags & DBG_SKIP_BIN)) {
+        uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
+        const int bx0 = gx0 / TILE, bx1 = live ? gx1 / TILE : -1, by0 = gy0 / TILE, by1 = live ? gy1 / TILE : -1;
+        const int nbx = bx1 - bx0 + 1, n_bt = live ? nbx * (by1 - by0 + 1) : 0;
+        int key[SMALL_BT];
+        uint32_t pos[SMALL_BT];
+#pragma unroll
+        for (int k = 0; k < SMALL_BT; ++k) {
+            const int bx = bx0 + (k % max(nbx, 1)), by = by0 + k / max(nbx, 1);
+            key[k] = (n_bt <= SMALL_BT && k < n_bt && owned_bin_tile(fp, bx, by)) ? by * fp.tiles_x + bx : -1;
+        }
+        wave_append<SMALL_BT>(tcount, key, pos);
+#pragma unroll
+        for (int k = 0; k < SMALL_BT; ++k)
+            if (key[k] >= 0) { append_bin(fp, fb, cnt, key[k], pos[k], (uint32_t)gid); ++n_bin; }
+        uint64_t big = __ballot(n_bt > SMALL_BT);
+        while (big) {
+            const int src = __ffsll((unsigned long long)big) - 1;
+            big &= big - 1;
+            const int cx0 = __shfl(bx0, src), cx1 = __shfl(bx1, src), cy0 = __shfl(by0, src), cy1 = __shfl(by1, src);
+            const uint32_t id = (uint32_t)__shfl(gid, src);
+            const int nx = cx1 - cx0 + 1, n = nx * (cy1 - cy0 + 1);
+            uint32_t mine = 0;
+            for (int k = lane; k < n; k += 64) {
+                const int bx = cx0 + k % nx, by = cy0 + k / nx;
+                if (!owned_bin_tile(fp, bx, by)) continue;
+                const int t = by * fp.tiles_x + bx;
+                append_bin(fp, fb, cnt, t, atomicAdd(&tcount[t], 1u), id);
+                ++mine;
+            }
+            for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o);
+            const uint32_t tot = __shfl(mine, 0);
+            if (lane == src) n_bin += tot;
+        }
+    }
+
+    tl_mark(fb.timeline, blockIdx.x, 3);
+    // -- per-block statistics (no same-address global atomics)
+    const uint64_t m_setup = __ballot(valid && !(flags & TRI_CULLED));
+    const uint64_t m_ghost = __ballot(valid && !(flags & TRI_CULLED) && (flags & TRI_GHOST));
+    const uint64_t m_unb = __ballot(valid && !(flags & TRI_CULLED) && (flags & TRI_UNBOUNDED));
+    for (int o = 32; o > 0; o >>= 1) n_bin += __shfl_down(n_bin, o);
+    if (lane == 0) {
+        atomicAdd(&s_stat[0], (uint32_t)__popcll(m_setup));
+        atomicAdd(&s_stat[1], (uint32_t)__popcll(m_ghost));
+        atomicAdd(&s_stat[2], (uint32_t)__popcll(m_unb));
+        atomicAdd(&s_stat[3], n_bin);
+    }
+    __syncthreads();
+    if (tid == 0) fb.blk_stat[blockIdx.x] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
+}
+
+// Clear of CLEAR_BT_PER_BLOCK bin tiles (colour canvas rows, depth screen rows, 16-B stores; owned
+// tiles only) and zeroing of their bin counts for the next frame (every tile).
+__device__ __forceinline__ void clear_block(const FrameParams &fp, const FrameBuffers &fb, int cb) {
+    const int tid = threadIdx.x;
+    const int n_bt = fp.tiles_x * fp.tiles_y;
+    uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
+    const int r = tid >> 3, seg = tid & 7;   // 32 rows x 8 16-B segments per tile
+    for (int i = 0; i < CLEAR_BT_PER_BLOCK; ++i) {
+        const int t = cb * CLEAR_BT_PER_BLOCK + i;
+        if (t >= n_bt) break;
+        if (tid == 0) next_count[t] = 0u;
+        if (t % fp.count != fp.rank || (fp.flags & DBG_SKIP_CLEAR)) continue;
+        const int bx = t % fp.tiles_x, by = t / fp.tiles_x;
+        const int y = by * TILE + r, x = bx * TILE + seg * 4;
+        if (y >= fp.H || x >= fp.W) continue;
+        const size_t crow = (size_t)(fp.H - 1 - y) * fp.W, drow = (size_t)y * fp.W;
+        if (x + 3 < fp.W && (fp.W & 3) == 0) {
+            const uint32_t c = fp.clear_rgba;
+            *reinterpret_cast<uint4 *>(fb.color + (crow + x) * 4) = make_uint4(c, c, c, c);
+            *reinterpret_cast<float4 *>(fb.depth + drow + x) = make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+        } else {
+            for (int j = 0; j < 4 && x + j < fp.W; ++j) {
+                reinterpret_cast<uint32_t *>(fb.color)[crow + x + j] = fp.clear_rgba;
+                fb.depth[drow + x + j] = FLT_MAX;
+            }
+        }
+        if (fb.prequant)
+            for (int j = 0; j < 4 && x + j < fp.W; ++j) fb.prequant[crow + x + j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+template <bool KARG>
+__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
+    __shared__ GhostScratch s_ghost[4];
+    __shared__ uint32_t s_stat[4];
+    __shared__ float4 s_wscratch[4][64 * 6];   // per-wave store staging (setup role)
+    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
+    const DrawGPU *draws = draw_table<KARG>(fb, ka);
+    const int b = (int)blockIdx.x;
+    const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
+    // zero the other counter set for the next frame (block 0 exists even for an empty frame)
+    if (b == 0 && threadIdx.x < C_NCOUNTERS) fb.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
+    if (b < fp.setup_blocks) {
+        setup_block(fp, fb, draws, cnt, s_stat, s_wscratch[threadIdx.x >> 6]);
+    } else if (b < fp.setup_blocks + fp.ghost_blocks) {
+        const int wave = threadIdx.x >> 6;
+        const int gw = (b - fp.setup_blocks) * 4 + wave;
+        const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
+        if (gw < n_groups * (int)fp.ghost_slices && !(fp.flags & DBG_SKIP_GHOST))
+            ghost_wave(fp, fb, draws, cnt, gw / (int)fp.ghost_slices, gw % (int)fp.ghost_slices, s_ghost[wave]);
+    } else {
+        clear_block(fp, fb, b - fp.setup_blocks - fp.ghost_blocks);
+    }
+    if (fb.timeline) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            fb.timeline[TL_STRIDE * b] = t_start;
+            fb.timeline[TL_STRIDE * b + 1] = __builtin_amdgcn_s_memrealtime();
+            fb.timeline[TL_STRIDE * b + 10] = c_start;
+            fb.timeline[TL_STRIDE * b + 11] = __builtin_amdgcn_s_memtime();
+        }
+    }
+}
+
+// ---- k_raster ---------------------------------------------------------------------------------
 
 // Fragment shaders of the four legacy pipelines for the winning triangle, from its per-corner
 // varyings.  Returns the pre-truncation floats; the caller truncates to uint8 like the reference.
-__device__ __forceinline__ void shade_winner(const DrawGPU &dr, const ShadeRec &sr, float u, float v, float w, float pre[3]) {
+// du = the draw's {light, cam, ocol, colf} float4s (DrawGPU::light.. or the LDS copy).
+__device__ __forceinline__ void shade_winner(const float4 *du, const ShadeRec &sr, float u, float v, float w, float pre[3]) {
+    const float4 dl = du[0], dc = du[1], doc = du[2], dcf = du[3];
     const f3 a0 = {sr.v[0], sr.v[1], sr.v[2]}, a1 = {sr.v[3], sr.v[4], sr.v[5]}, a2 = {sr.v[6], sr.v[7], sr.v[8]};
     if (sr.shading == 0) {
         // Flat FS (flat_shading.cpp:69-98): the interpolated normal is normalised in
         // draw_triangle_tile and again in the FS; intensity = min(0.2 + max(n.l, 0), 1)
         const f3 in_n = normalize3(add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w)));
         const f3 nn = normalize3(in_n);
-        const f3 l = {dr.light[0], dr.light[1], dr.light[2]};
+        const f3 l = {dl.x, dl.y, dl.z};
         const float diffuse = g_max(dot3(nn, l), 0.0f);
         float intensity = 0.2f + diffuse;
         if (intensity > 1.0f) intensity = 1.0f;
-        pre[0] = dr.colf[0] * intensity;
-        pre[1] = dr.colf[1] * intensity;
-        pre[2] = dr.colf[2] * intensity;
+        pre[0] = dcf.x * intensity;
+        pre[1] = dcf.y * intensity;
+        pre[2] = dcf.z * intensity;
         return;
     }
     if (sr.shading == 1) {
@@ -441,8 +704,8 @@ __device__ __forceinline__ void shade_winner(const DrawGPU &dr, const ShadeRec &
     const f3 n0 = {sr.v[9], sr.v[10], sr.v[11]}, n1 = {sr.v[12], sr.v[13], sr.v[14]}, n2 = {sr.v[15], sr.v[16], sr.v[17]};
     const f3 in_n = normalize3(add3(add3(sc3(n0, u), sc3(n1, v)), sc3(n2, w)));
     const f3 in_w = add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w));
-    const f3 L = {dr.light[0], dr.light[1], dr.light[2]};
-    const f3 cam = {dr.cam[0], dr.cam[1], dr.cam[2]};
+    const f3 L = {dl.x, dl.y, dl.z};
+    const f3 cam = {dc.x, dc.y, dc.z};
     const f3 norm = normalize3(in_n);
     const f3 viewDir = normalize3(sub3(cam, in_w));
     const float diff = g_max(dot3(norm, L), 0.0f);
@@ -454,39 +717,42 @@ __device__ __forceinline__ void shade_winner(const DrawGPU &dr, const ShadeRec &
         const float dn = dot3(norm, I);
         const f3 t = sc3(sc3(norm, dn), 2.0f);
         const f3 refl = sub3(I, t);
-        const float spec = (float)pow((double)g_max(dot3(viewDir, refl), 0.0f), 32.0);
+        const float spec = pow2k<5>(g_max(dot3(viewDir, refl), 0.0f));
         specular = (0.8f * spec) * 1.0f;
     } else {
         // Blinn-Phong (blinn_phong_shading.cpp:63-97): powf(max(N.H,0), 64), spec 0.5
         const f3 half = normalize3(add3(L, viewDir));
-        const float spec = (float)pow((double)g_max(dot3(norm, half), 0.0f), 64.0);
+        const float spec = pow2k<6>(g_max(dot3(norm, half), 0.0f));
         specular = (0.5f * spec) * 1.0f;
     }
-    const f3 oc = {dr.ocol[0], dr.ocol[1], dr.ocol[2]};
+    const f3 oc = {doc.x, doc.y, doc.z};
     const float s = (0.15f + diff * 1.0f) + specular;
     pre[0] = g_clamp01(s * oc.x) * 255.0f;
     pre[1] = g_clamp01(s * oc.y) * 255.0f;
     pre[2] = g_clamp01(s * oc.z) * 255.0f;
 }
 
-// Per-pixel winner state: depth, submission index and the winner's (v, w) (u is recomputed
-// exactly as (1 - v) - w, shs_renderer.hpp:819).
+// Per-pixel winner state: depth, submission index, the winner's (v, w) (u is recomputed exactly as
+// (1 - v) - w, shs_renderer.hpp:819) and its position in the tile's candidate sequence (to find its
+// staged shading varyings; ~0u for a ghost fragment).
 struct Best {
     float z;
     uint32_t id;
     float v, w;
+    uint32_t pos;
 };
 
-__device__ __forceinline__ void resolve(float z, uint32_t id, float v, float w, Best &b) {
+__device__ __forceinline__ void resolve(float z, uint32_t id, float v, float w, uint32_t pos, Best &b) {
     // In-order strict-less z test == lexicographic min of (z, submission index); NaN never wins,
     // z == FLT_MAX never beats the FLT_MAX clear (id sentinel 0 makes id < b.id false).
-    if (z < b.z || (z == b.z && id < b.id)) { b.z = z; b.id = id; b.v = v; b.w = w; }
+    if (z < b.z || (z == b.z && id < b.id)) { b.z = z; b.id = id; b.v = v; b.w = w; b.pos = pos; }
 }
 
 // One triangle against one pixel.  ibox pixels are always in the reference's visited set; outside
-// it only ghost triangles can pass, and only where the tile clamp visits the pixel.
+// it only bounded ghosts are tested here, and only where the tile clamp visits the pixel (the
+// unbounded slivers' outside pixels arrive as ghost fragments).
 __device__ __forceinline__ void raster_px(int px, int py, float rtminx, float rtmaxx, float rtminy, float rtmaxy,
-                                          const TriRec &r, uint32_t id, Best &b) {
+                                          const TriRec &r, uint32_t id, uint32_t pos, Best &b) {
     const bool in_ibox = px >= lo16(r.ibx) && px <= hi16(r.ibx) && py >= lo16(r.iby) && py <= hi16(r.iby);
     bool test = in_ibox;
     if (r.flags & TRI_GHOST) {
@@ -501,217 +767,272 @@ __device__ __forceinline__ void raster_px(int px, int py, float rtminx, float rt
                    py <= (int)bmaxy;
         }
     }
-    if (test) {
-        float u, v, w;
-        bary(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);
-        if (!(u < 0 || v < 0 || w < 0)) {
-            const float z = (u * r.z0 + v * r.z1) + w * r.z2;
-            resolve(z, id, v, w, b);
-        }
+    float u, v, w;
+    if (test && bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w)) {
+        const float z = (u * r.z0 + v * r.z1) + w * r.z2;
+        resolve(z, id, v, w, pos, b);
     }
 }
 
-// Speed-only XCD grouping: blocks b and b+8 (dealt to the same XCD) render horizontally adjacent
-// tiles, so neighbouring row segments are written through one L2.
-__device__ __forceinline__ int tile_of_block(int b, int n_owned) {
-    const int g = b >> 4;
-    if ((g << 4) + 16 > n_owned) return b;          // ragged last group: identity
-    return (g << 4) + ((b & 7) << 1) + ((b >> 3) & 1);
-}
+constexpr int RCHUNK = 128;        // candidates staged per pass (record + shading varyings)
+constexpr int LDS_DRAWS = 64;      // draws whose shading uniforms are kept in LDS
 
-constexpr int NB = TILE / 8;   // 8x8 blocks per tile edge (4): wave w owns block column w
+struct RasterShared {
+    float4 rec[RCHUNK * 6];           // staged triangle records (12 KB)
+    float4 shd[RCHUNK * 5];           // staged shading varyings (10 KB)
+    uint32_t id[RCHUNK];
+    uint32_t cand[CAND];
+    float4 du[LDS_DRAWS * 4];         // per-draw {light, cam, ocol, colf} (4 KB)
+    uint32_t oc[RTH * RTW];           // output staging: colour
+    float od[RTH * RTW];              // output staging: depth
+    int busy[256];                    // this workgroup's busy tiles
+    uint32_t nc, nbusy, cov, maxbin;
+};
 
-__global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
-    __shared__ float4 s_rec[CHUNK * 6];
-    __shared__ uint32_t s_id[CHUNK];
-    __shared__ uint32_t s_cand[CAND];
-    __shared__ float s_bz[TILE * TILE];
-    __shared__ uint32_t s_bid[TILE * TILE];
-    __shared__ uint32_t s_cov, s_nc;
-    float *s_bv = reinterpret_cast<float *>(s_rec);    // reused once the raster passes are done
-    float *s_bw = s_bv + TILE * TILE;
-
-    const int n_owned = (fp.tiles_x * fp.tiles_y - fp.rank + fp.count - 1) / fp.count;
-    const int tile = fp.rank + tile_of_block((int)blockIdx.x, n_owned) * fp.count;
-    const int tx = tile % fp.tiles_x, ty = tile / fp.tiles_x;
-    const int X0 = tx * TILE, Y0 = ty * TILE;
+// One busy raster tile: gather candidates, resolve, shade, write.  rt = raster-tile index
+// (row * tiles_x + column).  pbx: this thread's prefetched bin boxes of triangles tid + 256k (scan
+// mode with n_tris <= CAND).
+__device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, const uint32_t *cnt,
+                            int rt, const uint2 (&pbx)[CAND / 256], bool prefetched, RasterShared &sh, uint64_t *tl) {
+    const int tls = fp.setup_grid + (int)blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
-    const DrawGPU *draws = draw_table(fp, fb, ka);
-    if (tid == 0) s_cov = 0;
+    const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
+    const int X0 = col * RTW, Y0 = row * RTH;
+    const int X1 = X0 + RTW - 1, Y1 = Y0 + RTH - 1;
+    const int bt = (row / (TILE / RTH)) * fp.tiles_x + col;
 
-    // candidate sources.  scan mode: every triangle's bin box.  bin mode: the tile's bin, then the
-    // spill list (entries of this tile).
+    // candidate sources.  scan mode: every triangle's bin box.  bin mode: the bin tile's list, then
+    // the spill list (entries of this bin tile).
     uint32_t n_bin_total = 0, n_bin = 0, n_spill = 0, n_items;
     if (fp.scan_mode) {
         n_items = (uint32_t)fp.n_tris;
     } else {
-        n_bin_total = fb.tile_count[tile];
+        n_bin_total = fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + bt];
         n_bin = n_bin_total < fp.bin_cap ? n_bin_total : fp.bin_cap;
         if (n_bin_total > fp.bin_cap) n_spill = min(cnt[C_SPILL], fp.spill_cap);
         n_items = n_bin + n_spill;
+        if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
     }
-    if (fp.flags & DBG_CLEAR_ONLY) n_items = 0;
-    const uint32_t *bin = fb.bins + (size_t)tile * fp.bin_cap;
-    const int tx1 = X0 + TILE - 1, ty1 = Y0 + TILE - 1;
+    const uint32_t *bin = fb.bins + (size_t)bt * fp.bin_cap;
 
-    // raster mapping: wave w owns the 8-px column of blocks (w, 0..3); lane -> (lane&7, lane>>3)
-    const int px = X0 + wave * 8 + (lane & 7);
-    const int py0 = Y0 + (lane >> 3);
-    const int rxs = (px / fp.rtw) * fp.rtw;
-    const float rtminx = (float)rxs, rtmaxx = (float)(min(rxs + fp.rtw, fp.W) - 1);
+    // this lane's pixel: wave w owns the 8x8 block at (X0 + 8w, Y0)
     const int bxl = X0 + wave * 8;
-    Best best[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) { best[i].z = FLT_MAX; best[i].id = 0u; best[i].v = 0.f; best[i].w = 0.f; }
+    const int px = bxl + (lane & 7), py = Y0 + (lane >> 3);
+    const int rxs = (px / fp.rtw) * fp.rtw, rys = (py / fp.rth) * fp.rth;
+    const float rtminx = (float)rxs, rtmaxx = (float)(min(rxs + fp.rtw, fp.W) - 1);
+    const float rtminy = (float)rys, rtmaxy = (float)(min(rys + fp.rth, fp.H) - 1);
+    Best best;
+    best.z = FLT_MAX; best.id = 0u; best.v = 0.f; best.w = 0.f; best.pos = ~0u;
+    uint32_t seq = 0;                  // candidates staged so far (positions of the sequence)
+    uint32_t hits = 0;                 // candidates this wave rasterized (profiling)
+    uint32_t last_lo = 0, last_hi = 0; // positions held in sh.shd after the loops
 
     for (uint32_t base = 0; base < n_items; base += CAND) {
         __syncthreads();
-        if (tid == 0) s_nc = 0;
+        if (tid == 0) sh.nc = 0;
         __syncthreads();
         // gather up to CAND candidate ids (4 independent loads per thread, one round trip)
+        uint32_t ids[CAND / 256];
+        uint2 bx[CAND / 256];
 #pragma unroll
         for (int k = 0; k < CAND / 256; ++k) {
             const uint32_t item = base + tid + 256u * k;
-            if (item >= n_items) continue;
             uint32_t id = 0xffffffffu;
-            if (fp.scan_mode) {
-                const uint2 bx = fb.boxes[item];
-                if (!(hi16(bx.x) < X0 || lo16(bx.x) > tx1 || hi16(bx.y) < Y0 || lo16(bx.y) > ty1)) id = item;
-            } else if (item < n_bin) {
-                id = bin[item];
-            } else {
-                const uint2 e = fb.spill[item - n_bin];
-                if ((int)e.x == tile) id = e.y;
-            }
-            if (id != 0xffffffffu) s_cand[atomicAdd(&s_nc, 1u)] = id;
-        }
-        __syncthreads();
-        const uint32_t nc = s_nc;
-        for (uint32_t c = 0; c < nc; c += CHUNK) {
-            const int m = (int)min((uint32_t)CHUNK, nc - c);
-            if (c > 0) __syncthreads();
-            if (tid < m) {
-                const uint32_t id = s_cand[c + tid];
-                s_id[tid] = id;
-                const float4 *src = reinterpret_cast<const float4 *>(&fb.recs[id]);
-                float4 q[6];
-#pragma unroll
-                for (int j = 0; j < 6; ++j) q[j] = src[j];
-#pragma unroll
-                for (int j = 0; j < 6; ++j) s_rec[tid * 6 + j] = q[j];
-            }
-            __syncthreads();
-            for (int j = 0; j < m; ++j) {
-                const uint4 bb = reinterpret_cast<const uint4 *>(&s_rec[j * 6])[4];   // ibx iby gbx gby
-                if (hi16(bb.z) < bxl || lo16(bb.z) > bxl + 7 || hi16(bb.w) < Y0 || lo16(bb.w) > ty1) continue;
-                const TriRec r = rec_from(&s_rec[j * 6]);
-                const uint32_t id = s_id[j];
-#pragma unroll
-                for (int i = 0; i < NB; ++i) {
-                    const int by = Y0 + 8 * i;
-                    if (hi16(bb.w) < by || lo16(bb.w) > by + 7) continue;        // block cull (uniform)
-                    const int py = py0 + 8 * i;
-                    const int ry = (py / fp.rth) * fp.rth;
-                    raster_px(px, py, rtminx, rtmaxx, (float)ry, (float)(min(ry + fp.rth, fp.H) - 1), r, id, best[i]);
+            if (item < n_items) {
+                if (fp.scan_mode) {
+                    id = item;
+                } else if (item < n_bin) {
+                    id = bin[item];
+                } else {
+                    const uint2 e = fb.spill[item - n_bin];
+                    if ((int)e.x == bt) id = e.y;
                 }
             }
+            ids[k] = id;
+        }
+        if (prefetched) {
+#pragma unroll
+            for (int k = 0; k < CAND / 256; ++k) bx[k] = pbx[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < CAND / 256; ++k) bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < CAND / 256; ++k) {
+            const bool hit = ids[k] != 0xffffffffu && !(hi16(bx[k].x) < X0 || lo16(bx[k].x) > X1 || hi16(bx[k].y) < Y0 ||
+                                                       lo16(bx[k].y) > Y1);
+            const uint64_t m = __ballot(hit);
+            uint32_t basew = 0;
+            if (lane == 0 && m) basew = atomicAdd(&sh.nc, (uint32_t)__popcll(m));
+            basew = __shfl(basew, 0);
+            if (hit) sh.cand[basew + lanes_below(m)] = ids[k];
+        }
+        __syncthreads();
+        tl_mark(tl, tls, 1);
+        const uint32_t nc = sh.nc;
+        for (uint32_t c = 0; c < nc; c += RCHUNK) {
+            const int m = (int)min((uint32_t)RCHUNK, nc - c);
+            if (c > 0) __syncthreads();
+            // stage records (6 float4 each) then shading varyings (5 each): consecutive lanes load
+            // consecutive float4s of one record, so a load instruction touches ~11 records' lines
+            if (tid < m) sh.id[tid] = sh.cand[c + tid];
+            {
+                constexpr int NQ = (RCHUNK * 11 + 255) / 256;
+                float4 q[NQ];
+                float4 *dst[NQ];
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) {
+                    const int f = tid + 256 * k;
+                    const bool isrec = f < 6 * m;
+                    const int g = isrec ? f : f - 6 * m;
+                    const int per = isrec ? 6 : 5;
+                    const int ci = g / per, part = g - ci * per;
+                    const bool ok = f < 11 * m;
+                    const uint32_t id = sh.cand[c + (ok ? ci : 0)];
+                    const float4 *src = isrec ? reinterpret_cast<const float4 *>(&fb.recs[id]) + part
+                                              : reinterpret_cast<const float4 *>(&fb.shade[id]) + part;
+                    dst[k] = ok ? (isrec ? &sh.rec[f] : &sh.shd[g]) : nullptr;
+                    q[k] = ok ? *src : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int k = 0; k < NQ; ++k)
+                    if (dst[k]) *dst[k] = q[k];
+            }
+            __syncthreads();
+            tl_mark(tl, tls, 2);
+            // this wave's candidates: bin box overlaps its 8x8 block (64 tested per ballot)
+            for (int j0 = 0; j0 < m; j0 += 64) {
+                const int j = j0 + lane;
+                bool hit = false;
+                if (j < m) {
+                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[j * 6])[4];   // ibx iby gbx gby
+                    hit = !(hi16(bb.z) < bxl || lo16(bb.z) > bxl + 7 || hi16(bb.w) < Y0 || lo16(bb.w) > Y1);
+                }
+                uint64_t mk = __ballot(hit);
+                hits += (uint32_t)__popcll(mk);
+                while (mk) {
+                    const int jj = j0 + __ffsll((unsigned long long)mk) - 1;
+                    mk &= mk - 1;
+                    const TriRec r = rec_from(&sh.rec[jj * 6]);
+                    raster_px(px, py, rtminx, rtmaxx, rtminy, rtmaxy, r, sh.id[jj], seq + (uint32_t)jj, best);
+                }
+            }
+            last_lo = seq;
+            seq += (uint32_t)m;
+            last_hi = seq;
         }
     }
+    tl_mark(tl, tls, 3);
     // tile-clamp pixels of unbounded slivers outside their bbox that passed (k_setup ghost waves)
     {
         const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
         for (uint32_t f = 0; f < n_frag; ++f) {
             const GhostFrag g = fb.frags[f];
-            const int gx = (int)(g.xy & 0xffffu), gy = (int)(g.xy >> 16);
-            if (gx != px) continue;
-#pragma unroll
-            for (int i = 0; i < NB; ++i)
-                if (gy == py0 + 8 * i) resolve(g.z, g.id, g.v, g.w, best[i]);
+            if ((int)(g.xy & 0xffffu) == px && (int)(g.xy >> 16) == py) resolve(g.z, g.id, g.v, g.w, ~0u, best);
         }
     }
-    __syncthreads();   // s_rec is reused below
 
-    // hand the winners to the row-major output mapping through LDS
+    // shade this lane's winner (varyings from LDS when its candidate is in the last staged pass)
+    uint32_t rgba = fp.clear_rgba;
+    const bool covered = best.z < FLT_MAX && px < fp.W && py < fp.H;
+    if (covered && !(fp.flags & DBG_SKIP_SHADE)) {
+        ShadeRec sr;
+        float4 *d = reinterpret_cast<float4 *>(&sr);
+        if (best.pos >= last_lo && best.pos < last_hi) {
+            const int t = (int)(best.pos - last_lo);
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-        const int o = (py0 - Y0 + 8 * i) * TILE + (px - X0);
-        s_bz[o] = best[i].z;
-        s_bid[o] = best[i].id;
-        s_bv[o] = best[i].v;
-        s_bw[o] = best[i].w;
-    }
-    __syncthreads();
-
-    // output mapping: thread -> row tid>>3, 4 consecutive pixels (16-B colour and depth stores;
-    // 8 threads cover a 128-B row segment of each)
-    const int oy = Y0 + (tid >> 3), ox = X0 + (tid & 7) * 4;
-    uint32_t covered = 0;
-    if (oy < fp.H) {
-        const size_t crow = (size_t)(fp.H - 1 - oy) * fp.W, drow = (size_t)oy * fp.W;
-        uint32_t rgba[4];
-        float dep[4];
-        float4 pq[4];
-        const int lo = (tid >> 3) * TILE + (tid & 7) * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            dep[j] = s_bz[lo + j];
-            rgba[j] = fp.clear_rgba;
-            pq[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        // shade the winners two pixels at a time: both varyings loads in flight before any math
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            ShadeRec sr[2];
-            bool win[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int j = 2 * h + q;
-                win[q] = dep[j] < FLT_MAX && ox + j < fp.W;
-                if (win[q]) {
-                    ++covered;
-                    if (fp.flags & DBG_SKIP_SHADE) { win[q] = false; continue; }
-                    const float4 *src = reinterpret_cast<const float4 *>(&fb.shade[s_bid[lo + j]]);
-                    float4 *d = reinterpret_cast<float4 *>(&sr[q]);
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) d[k] = src[k];
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int j = 2 * h + q;
-                if (!win[q]) continue;
-                const float v = s_bv[lo + j], w = s_bw[lo + j];
-                const float u = (1.0f - v) - w;
-                float pre[3];
-                shade_winner(draws[sr[q].draw], sr[q], u, v, w, pre);
-                const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
-                rgba[j] = cr | (cg << 8) | (cb << 16) | (255u << 24);
-                pq[j] = make_float4(pre[0], pre[1], pre[2], 1.0f);
-            }
-        }
-        if (ox + 3 < fp.W && (fp.W & 3) == 0) {
-            *reinterpret_cast<uint4 *>(fb.color + (crow + ox) * 4) = make_uint4(rgba[0], rgba[1], rgba[2], rgba[3]);
-            *reinterpret_cast<float4 *>(fb.depth + drow + ox) = make_float4(dep[0], dep[1], dep[2], dep[3]);
+            for (int k = 0; k < 5; ++k) d[k] = sh.shd[t * 5 + k];
         } else {
-            for (int j = 0; j < 4; ++j)
-                if (ox + j < fp.W) {
-                    reinterpret_cast<uint32_t *>(fb.color)[crow + ox + j] = rgba[j];
-                    fb.depth[drow + ox + j] = dep[j];
-                }
+            const float4 *src = reinterpret_cast<const float4 *>(&fb.shade[best.id]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) d[k] = src[k];
         }
-        if (fb.prequant)
-            for (int j = 0; j < 4; ++j)
-                if (ox + j < fp.W) fb.prequant[crow + ox + j] = pq[j];
+        const float u = (1.0f - best.v) - best.w;
+        const float4 *du = sr.draw < LDS_DRAWS ? &sh.du[sr.draw * 4] : reinterpret_cast<const float4 *>(draws[sr.draw].light);
+        float pre[3];
+        shade_winner(du, sr, u, best.v, best.w, pre);
+        const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
+        rgba = cr | (cg << 8) | (cb << 16) | (255u << 24);
+        if (fb.prequant) fb.prequant[(size_t)(fp.H - 1 - py) * fp.W + px] = make_float4(pre[0], pre[1], pre[2], 1.0f);
     }
-    // covered-pixel count: wave reduction, one LDS atomic per wave; per-tile stats go to their own
-    // slot (no same-address global atomics across workgroups) and the host sums them at sync
-    for (int o = 32; o > 0; o >>= 1) covered += __shfl_down(covered, o);
-    if (lane == 0) atomicAdd(&s_cov, covered);
+    tl_mark(tl, tls, 4);
+    if (tl && tid == 0) { tl[TL_STRIDE * tls + 8] = seq; tl[TL_STRIDE * tls + 9] = hits; }
+    const uint64_t cm = __ballot(covered);
+    if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
+    __syncthreads();   // previous tile's output staging is free
+    const int o = (lane >> 3) * RTW + wave * 8 + (lane & 7);
+    sh.oc[o] = rgba;
+    sh.od[o] = best.z;
+    __syncthreads();
+    // output: wave w writes rows 2w, 2w+1 of the tile (two 128-B segments per plane)
+    {
+        const int r = 2 * wave + (lane >> 5), x = X0 + (lane & 31), y = Y0 + r;
+        if (y < fp.H && x < fp.W) {
+            reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - y) * fp.W + x] = sh.oc[r * RTW + (lane & 31)];
+            fb.depth[(size_t)y * fp.W + x] = sh.od[r * RTW + (lane & 31)];
+        }
+    }
+    if (tid == 0) fb.busy[rt] = 0u;   // clean for the next frame
+    tl_mark(tl, tls, 5);
+}
+
+// Persistent raster: workgroup b takes owned raster tiles j = b, b + G, b + 2G, ... and renders
+// the busy ones (the rest were cleared by k_setup).
+template <bool KARG>
+__global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
+    __shared__ RasterShared sh;
+    const int tid = threadIdx.x;
+    const uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
+    const DrawGPU *draws = draw_table<KARG>(fb, ka);
+    const int G = (int)gridDim.x;
+    const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
+    // per-draw shading uniforms into LDS; small scan-mode scenes: every bin box into registers
+    for (int i = tid; i < min(fp.n_draws, LDS_DRAWS) * 4; i += 256)
+        sh.du[i] = reinterpret_cast<const float4 *>(draws[i >> 2].light)[i & 3];
+    const bool prefetched = fp.scan_mode && fp.n_tris <= CAND;
+    uint2 pbx[CAND / 256];
+#pragma unroll
+    for (int k = 0; k < CAND / 256; ++k) {
+        const int i = tid + 256 * k;
+        pbx[k] = (prefetched && i < fp.n_tris) ? fb.boxes[i] : make_uint2(0u, 0u);
+    }
+    for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
+        __syncthreads();
+        if (tid == 0) sh.nbusy = 0;
+        __syncthreads();
+        const int j = j0 + tid * G;
+        if (j < fp.n_owned_rt) {
+            // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it
+            const int t = fp.rank + (j >> 2) * fp.count;
+            const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / RTH) + (j & 3);
+            if (row < fp.rtiles_y) {
+                const int rt = row * fp.tiles_x + col;
+                if (fb.busy[rt]) sh.busy[atomicAdd(&sh.nbusy, 1u)] = rt;
+            }
+        }
+        __syncthreads();
+        tl_mark(fb.timeline, fp.setup_grid + (int)blockIdx.x, 0);
+        const int nb = (int)sh.nbusy;
+        for (int i = 0; i < nb; ++i) {
+            const int rt = sh.busy[i];
+            if (fp.flags & DBG_CLEAR_ONLY) {
+                if (tid == 0) fb.busy[rt] = 0u;
+                continue;
+            }
+            raster_tile(fp, fb, draws, cnt, rt, pbx, prefetched, sh, (i == 0 && j0 == (int)blockIdx.x) ? fb.timeline : nullptr);
+        }
+    }
     __syncthreads();
     if (tid == 0) {
-        fb.tile_stat[tile] = make_uint2(s_cov, n_bin_total);
-        if (!fp.scan_mode) fb.tile_count[tile] = 0u;   // bins are empty for the next frame
+        fb.rstat[blockIdx.x] = make_uint2(sh.cov, sh.maxbin);
+        if (fb.timeline) {
+            fb.timeline[TL_STRIDE * (fp.setup_grid + blockIdx.x)] = t_start;
+            fb.timeline[TL_STRIDE * (fp.setup_grid + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
+            fb.timeline[TL_STRIDE * (fp.setup_grid + blockIdx.x) + 10] = c_start;
+            fb.timeline[TL_STRIDE * (fp.setup_grid + blockIdx.x) + 11] = __builtin_amdgcn_s_memtime();
+        }
     }
 }
 
@@ -722,18 +1043,20 @@ namespace shs_internal {
 using namespace shs_dev;
 
 hipError_t launch_setup(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, hipStream_t s) {
-    // setup blocks (one thread per triangle) + ghost blocks (4 waves; each group of GHOST_GROUP
-    // triangles is shared by fp.ghost_slices waves)
-    const int setup_blocks = (fp.n_tris + 255) / 256;
-    const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
-    const int ghost_blocks = (n_groups * (int)fp.ghost_slices + 3) / 4;
-    hipLaunchKernelGGL(k_setup, dim3(setup_blocks > 0 ? setup_blocks + ghost_blocks : 1), dim3(256), 0, s, fp, fb, ka);
+    const int grid = fp.setup_blocks + fp.ghost_blocks + fp.clear_blocks;
+    if (fp.n_draws <= KARG_DRAWS)
+        hipLaunchKernelGGL(k_setup<true>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
+    else
+        hipLaunchKernelGGL(k_setup<false>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
     return hipGetLastError();
 }
-hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, int n_owned_tiles,
-                         hipStream_t s) {
-    if (n_owned_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_raster, dim3(n_owned_tiles), dim3(256), 0, s, fp, fb, ka);
+
+hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, int grid, hipStream_t s) {
+    if (fp.n_draws <= KARG_DRAWS)
+        hipLaunchKernelGGL(k_raster<true>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
+    else
+        hipLaunchKernelGGL(k_raster<false>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
     return hipGetLastError();
 }
+
 }  // namespace shs_internal

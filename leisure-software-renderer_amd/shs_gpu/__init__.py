@@ -208,6 +208,21 @@ class Context:
         """0 auto, 1 scan (no bins), 2 bins."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_RASTER_MODE, int(mode)))
 
+    def set_timeline(self, enable: bool):
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_TIMELINE, 1 if enable else 0))
+
+    def debug_timeline(self):
+        """Last frame's workgroup timeline: (header dict, setup [n,2], raster [n,2]) in 10-ns ticks."""
+        n = ctypes.c_int64()
+        self._check(self._lib.shs_debug_timeline(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        self._check(self._lib.shs_debug_timeline(self._h, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)))
+        hs, hr, stride = int(out[0]), int(out[1]), int(out[5])
+        head = {"setup_grid": hs, "raster_grid": hr, "setup_blocks": int(out[2]), "ghost_blocks": int(out[3]),
+                "clear_blocks": int(out[4])}
+        slots = out[8:].reshape(-1, stride)
+        return head, slots[:hs], slots[hs:hs + hr]
+
     def set_bin_capacity(self, cap: int):
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_BIN_CAPACITY, int(cap)))
 

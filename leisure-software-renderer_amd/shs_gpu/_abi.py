@@ -24,6 +24,7 @@ SHADING_NAMES = {"flat": 0, "gouraud": 1, "phong": 2, "blinn_phong": 3}
 FRAME_PREQUANT = 1
 OPT_BIN_CAPACITY = 1
 OPT_RASTER_MODE = 2
+OPT_TIMELINE = 3
 
 
 class LegacyDraw(ctypes.Structure):
@@ -90,6 +91,7 @@ SIGNATURES = [
     ("shs_timing_read", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     ("shs_debug_records", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_set_option", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int64]),
+    ("shs_debug_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),
     ("shs_model_trs", ctypes.c_int, [_F, ctypes.c_float, _F, _F]),
     ("shs_mat4_mul", ctypes.c_int, [_F, _F, _F]),
