@@ -334,7 +334,7 @@ static int enqueue_frame(shs_ctx *ctx) {
         ctx->geom_key = gkey;
     }
     if (ensure(ctx, ctx->bins, (size_t)n_tiles * ctx->bin_cap)) return SHS_ERR_HIP;
-    const int setup_blocks = (n_tris + 255) / 256;
+    const int setup_blocks = (n_tris + 63) / 64;   // a quad of lanes per triangle
     if (ensure(ctx, ctx->blk_stat, (size_t)std::max(setup_blocks, 1))) return SHS_ERR_HIP;
     if (!ctx->spill.p && ensure(ctx, ctx->spill, 1 << 16)) return SHS_ERR_HIP;
     if (!ctx->frags.p && ensure(ctx, ctx->frags, 1 << 12)) return SHS_ERR_HIP;
@@ -396,16 +396,16 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.spill_cap = (uint32_t)std::min<size_t>(ctx->spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ctx->frags.cap, 0xffffffffu);
     {   // ~4K ghost waves per frame: small scenes split each sliver group over many waves
-        const int n_groups = std::max(1, (n_tris + 31) / 32);
+        const int n_groups = std::max(1, (n_tris + 15) / 16);
         fp.ghost_slices = (uint32_t)std::min(64, std::max(1, 4096 / n_groups));
     }
     fp.parity = ctx->frame_index & 1u;
     fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
-    const int n_groups = (n_tris + 31) / 32;
+    const int n_groups = (n_tris + 15) / 16;
     fp.setup_blocks = setup_blocks;
     fp.ghost_blocks = (n_groups * (int)fp.ghost_slices + 3) / 4;
-    fp.clear_blocks = (n_tiles + shs_dev::CLEAR_BT_PER_BLOCK - 1) / shs_dev::CLEAR_BT_PER_BLOCK;
+    fp.clear_blocks = 0;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / shs_dev::RTH);
     // persistent raster grid: one resident wave of workgroups (k_raster runs 4 per CU)
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt, 256 * 4));

@@ -79,7 +79,6 @@ constexpr int RTW = 32, RTH = 8;     // raster tile: one 256-thread workgroup, a
 constexpr int CHUNK = 256;           // triangle records staged in LDS per pass
 constexpr int CAND = 1024;           // candidate ids gathered per round (4 per thread)
 constexpr int SCAN_MAX_TRIS = 4096;  // scenes up to this size skip binning (scan mode)
-constexpr int CLEAR_BT_PER_BLOCK = 4;// bin tiles cleared per k_setup clear block
 constexpr double GHOST_MAX_EXPAND = 48.0;  // larger danger boxes are handled as TRI_UNBOUNDED
 
 // counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one).
@@ -90,7 +89,8 @@ constexpr uint32_t OV_SPILL = 1u, OV_FRAG = 2u;
 // Timing-experiment switches (frame flags bits 8+; results are WRONG with any of them set): they
 // let bench --debug-flags attribute kernel time to phases.  Never set by the product path.
 constexpr uint32_t DBG_SKIP_GHOST = 1u << 8, DBG_SKIP_SHADE = 1u << 9, DBG_CLEAR_ONLY = 1u << 10,
-                   DBG_SKIP_BIN = 1u << 11, DBG_SKIP_CLEAR = 1u << 12;
+                   DBG_SKIP_BIN = 1u << 11, DBG_SKIP_CLEAR = 1u << 12,
+                   DBG_TWICE = 1u << 13;
 
 // Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);
 // larger scenes read the device draw table.
@@ -122,7 +122,8 @@ struct FrameParams {
     uint32_t ghost_slices;           // ghost waves per GHOST_GROUP triangles (k_setup)
     uint32_t parity;                 // counter / bin-count set used by this frame
     uint32_t scan_mode;              // 1: no bins, busy raster tiles scan all bin boxes (small scenes)
-    int32_t setup_blocks, ghost_blocks, clear_blocks;   // k_setup block roles, in this order
+    int32_t setup_blocks, ghost_blocks, clear_blocks;   // k_setup block roles, in this order (no
+                                                        // clear blocks: k_raster clears)
     int32_t n_owned_rt;              // raster tiles of the owned bin tiles (4 per bin tile)
     int32_t setup_grid;              // k_setup grid (k_raster's timeline slots follow)
 };

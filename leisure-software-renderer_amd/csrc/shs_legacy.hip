@@ -129,18 +129,19 @@ __device__ __forceinline__ void load9(const float *src, float (&v)[9]) {
     for (int k = 0; k < 9; ++k) v[k] = src[k];
 }
 
-__device__ __forceinline__ TriRec make_rec(const FrameParams &fp, const DrawGPU &dr, int draw, int local, const float (&p)[9]) {
-    float sx[3], sy[3], sz[3];
-    const float fw = (float)(fp.W - 1), fh = (float)(fp.H - 1);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        float cx, cy, cz, cw;
-        m4p(dr.mvp, p[3 * k + 0], p[3 * k + 1], p[3 * k + 2], cx, cy, cz, cw);
-        const float nx = cx / cw, ny = cy / cw, nz = cz / cw;
-        sx[k] = (nx + 1.0f) * 0.5f * fw;
-        sy[k] = (1.0f - ny) * 0.5f * fh;
-        sz[k] = nz;
-    }
+// VS position of one corner (mvp * vec4(p, 1)) and Canvas::clip_to_screen (shs_renderer.hpp:823-831).
+__device__ __forceinline__ void vertex_screen(const FrameParams &fp, const float *mvp, float x, float y, float z, float &sx,
+                                              float &sy, float &sz) {
+    float cx, cy, cz, cw;
+    m4p(mvp, x, y, z, cx, cy, cz, cw);
+    const float nx = cx / cw, ny = cy / cw, nz = cz / cw;
+    sx = (nx + 1.0f) * 0.5f * (float)(fp.W - 1);
+    sy = (1.0f - ny) * 0.5f * (float)(fp.H - 1);
+    sz = nz;
+}
+
+__device__ __forceinline__ TriRec rec_from_screen(const FrameParams &fp, int draw, int local, const float (&sx)[3],
+                                                  const float (&sy)[3], const float (&sz)[3]) {
     TriRec r;
     r.ax = sx[0]; r.ay = sy[0];
     r.v0x = sx[1] - sx[0]; r.v0y = sy[1] - sy[0];
@@ -198,6 +199,41 @@ __device__ __forceinline__ TriRec make_rec(const FrameParams &fp, const DrawGPU 
     r.ibx = pack16(ix0, ix1); r.iby = pack16(iy0, iy1);
     r.gbx = pack16(gx0, gx1); r.gby = pack16(gy0, gy1);
     return r;
+}
+
+__device__ __forceinline__ TriRec make_rec(const FrameParams &fp, const DrawGPU &dr, int draw, int local, const float (&p)[9]) {
+    float sx[3], sy[3], sz[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) vertex_screen(fp, dr.mvp, p[3 * k], p[3 * k + 1], p[3 * k + 2], sx[k], sy[k], sz[k]);
+    return rec_from_screen(fp, draw, local, sx, sy, sz);
+}
+
+// ---- quad-lane triangle setup ---------------------------------------------------------------
+// Four lanes per triangle (q = lane & 3): lanes 0..2 transform one corner each (the reference's VS
+// runs per corner), the screen corners are exchanged within the quad, and every lane of the quad
+// then holds the triangle's record.  Cuts the per-thread dependency chain of setup ~3x.
+__device__ __forceinline__ float quad_bcast(float v, int k) {
+    // DPP quad_perm(k, k, k, k)
+    int r;
+    switch (k) {
+        case 0: r = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x00, 0xf, 0xf, false); break;
+        case 1: r = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x55, 0xf, 0xf, false); break;
+        case 2: r = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0xaa, 0xf, 0xf, false); break;
+        default: r = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0xff, 0xf, 0xf, false); break;
+    }
+    return __int_as_float(r);
+}
+
+// Record of the quad's triangle (all four lanes return it); p3 = this lane's corner (q < 3; lane 3
+// repeats corner 2).
+__device__ __forceinline__ TriRec quad_make_rec(const FrameParams &fp, const DrawGPU &dr, int draw, int local,
+                                                const float (&p3)[3]) {
+    float vx, vy, vz;
+    vertex_screen(fp, dr.mvp, p3[0], p3[1], p3[2], vx, vy, vz);
+    float sx[3], sy[3], sz[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sx[k] = quad_bcast(vx, k); sy[k] = quad_bcast(vy, k); sz[k] = quad_bcast(vz, k); }
+    return rec_from_screen(fp, draw, local, sx, sy, sz);
 }
 
 // ---- wave helpers -----------------------------------------------------------------------------
@@ -275,9 +311,9 @@ __device__ __forceinline__ bool owned_bin_tile(const FrameParams &fp, int bx, in
 // overlapping columns -- and likewise in y.  With Xout / Yout the edge columns / rows and Xin /
 // Yin the overlapping spans, the visited pixels outside the ibox are (Xout x (Yout u Yin)) u
 // (Xin x Yout): enumerated lane-parallel by index arithmetic.  One wave per (GHOST_GROUP
-// triangles, slice) recomputes the group's records (make_rec is deterministic) and takes every
+// triangles, slice) recomputes the group's records (quad setup, deterministic) and takes every
 // fp.ghost_slices-th 64-pixel batch of each unbounded sliver in the group.
-constexpr int GHOST_GROUP = 32;
+constexpr int GHOST_GROUP = 16;   // triangles per wave (a quad of lanes each)
 
 struct SliverSpan {
     int cl, cr, ru, rd;             // edge columns left / right, edge rows above / below
@@ -313,31 +349,49 @@ struct GhostScratch {           // per-wave LDS
     float4 rec[6];
 };
 
+// The quad's triangle index, draw and this lane's corner, with the wave-uniform draw fast path.
+struct QuadTri {
+    int tri, draw, local;
+    bool valid, uniform;
+};
+
+__device__ __forceinline__ QuadTri quad_tri(const DrawGPU *draws, int n_draws, int n_tris, int tri) {
+    QuadTri t;
+    t.tri = tri;
+    t.valid = tri < n_tris;
+    t.draw = wave_draw(draws, n_draws, tri, t.valid, t.uniform);
+    return t;
+}
+
+// Record of the quad's triangle through the draw's uniforms (scalar loads when wave-uniform).
+__device__ __forceinline__ TriRec quad_record(const FrameParams &fp, const DrawGPU *draws, QuadTri &t) {
+    const int q = __lane_id() & 3, qv = q < 3 ? q : 2;
+    TriRec r;
+    if (t.uniform) {
+        const int d = __builtin_amdgcn_readfirstlane(t.draw);
+        const DrawGPU &dr = draws[d];
+        t.local = t.tri - dr.tri_base;
+        const float *P = dr.pos + 9 * (size_t)t.local + 3 * qv;
+        const float p3[3] = {P[0], P[1], P[2]};
+        r = quad_make_rec(fp, dr, d, t.local, p3);
+    } else {
+        const DrawGPU &dr = draws[t.draw];
+        t.local = t.tri - dr.tri_base;
+        const float *P = dr.pos + 9 * (size_t)t.local + 3 * qv;
+        const float p3[3] = {P[0], P[1], P[2]};
+        r = quad_make_rec(fp, dr, t.draw, t.local, p3);
+    }
+    return r;
+}
+
 __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
                                            uint32_t *cnt, int group, int slice, GhostScratch &gs) {
     const int lane = __lane_id();
-    const int gid = group * GHOST_GROUP + lane;
+    QuadTri qt = quad_tri(draws, fp.n_draws, fp.n_tris, group * GHOST_GROUP + (lane >> 2));
     TriRec r;
-    bool unb = false;
-    const bool valid = lane < GHOST_GROUP && gid < fp.n_tris;
-    bool uni;
-    const int d = wave_draw(draws, fp.n_draws, gid, valid, uni);
-    if (valid) {
-        if (uni) {
-            const int du = __builtin_amdgcn_readfirstlane(d);
-            const int local = gid - draws[du].tri_base;
-            float p[9];
-            load9(draws[du].pos + 9 * (size_t)local, p);
-            r = make_rec(fp, draws[du], du, local, p);
-        } else {
-            const int local = gid - draws[d].tri_base;
-            float p[9];
-            load9(draws[d].pos + 9 * (size_t)local, p);
-            r = make_rec(fp, draws[d], d, local, p);
-        }
-        unb = (r.flags & TRI_UNBOUNDED) != 0;
-    }
-    uint64_t todo = __ballot(unb);
+    if (qt.valid) r = quad_record(fp, draws, qt);
+    // one lane per quad votes
+    uint64_t todo = __ballot(qt.valid && (lane & 3) == 0 && (r.flags & TRI_UNBOUNDED) && !(r.flags & TRI_CULLED));
     const int stride = 64 * (int)fp.ghost_slices;
     while (todo) {
         const int src = __ffsll((unsigned long long)todo) - 1;
@@ -350,7 +404,7 @@ __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuf
         wave_lds_sync();
         const TriRec t = rec_from(gs.rec);
         wave_lds_sync();   // gs.rec is rewritten by the next sliver
-        const uint32_t tri = (uint32_t)(group * GHOST_GROUP + src);
+        const uint32_t tri = (uint32_t)(group * GHOST_GROUP + (src >> 2));
         const int ix0 = lo16(t.ibx), ix1 = hi16(t.ibx), iy0 = lo16(t.iby), iy1 = hi16(t.iby);
         SliverSpan sp;
         classify_axis(fp.rt_x, fp.rtw, fp.W, t.fminx, t.fmaxx, sp.cl, sp.cr, sp.xi0, sp.xi1);
@@ -402,11 +456,6 @@ __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuf
 
 // ---- k_setup ----------------------------------------------------------------------------------
 
-// Busy marks and bin appends of one bin box.  Small boxes are done per lane (batched, one memory
-// round trip); lanes with large boxes are served one at a time by the whole wave.
-constexpr int SMALL_RT = 8;   // raster tiles a lane marks by itself
-constexpr int SMALL_BT = 4;   // bin tiles a lane appends to by itself
-
 __device__ __forceinline__ void append_bin(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int t, uint32_t pos,
                                            uint32_t id) {
     if (pos < fp.bin_cap) {
@@ -418,126 +467,137 @@ __device__ __forceinline__ void append_bin(const FrameParams &fp, const FrameBuf
     }
 }
 
-// The per-triangle part of k_setup: raster record r and shading varyings sr (the caller stores
-// both, coalesced).
-__device__ __forceinline__ void setup_tri(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU &dr, int lo,
-                                          int gid, TriRec &r, ShadeRec &sr) {
-    const int local = gid - dr.tri_base;
-    float p[9], N[9];
-    load9(dr.pos + 9 * (size_t)local, p);
-    load9(dr.nrm + 9 * (size_t)local, N);
-    r = make_rec(fp, dr, lo, local, p);
-    tl_mark(fb.timeline, blockIdx.x, 4);
-    fb.boxes[gid] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
-    sr.shading = dr.shading;
-    sr.draw = lo;
-    if (!(r.flags & TRI_CULLED)) {
-        // Shading varyings of the three corners (the VS outputs the FS interpolates), computed
-        // once per triangle instead of once per winning pixel.
-        sr.shading = dr.shading;
-        sr.draw = lo;
+// This lane's corner's shading varyings (the VS outputs the FS interpolates): a = world position
+// (Phong / Blinn-Phong), the clamped Gouraud colour, or the Flat view-space normal; nr = the
+// normalised world normal (Phong / Blinn-Phong).
+__device__ __forceinline__ void corner_varyings(const DrawGPU &dr, const float (&p3)[3], const float (&n3)[3], f3 &a, f3 &nr) {
+    nr = f3{0.f, 0.f, 0.f};
+    if (dr.shading == 0) {
+        a = m3v(dr.nmat, f3{n3[0], n3[1], n3[2]});   // Flat VS (flat_shading.cpp:54): mat3(mv) * n
+        return;
+    }
+    float x, y, z, ww;
+    m4p(dr.model, p3[0], p3[1], p3[2], x, y, z, ww);
+    const f3 wp = {x, y, z};
+    const f3 n = normalize3(m3v(dr.nmat, f3{n3[0], n3[1], n3[2]}));
+    if (dr.shading == 1) {
+        // Gouraud VS (gouraud_shading.cpp:46-77): Blinn-Phong per vertex, shininess 32
+        const f3 L = {dr.light[0], dr.light[1], dr.light[2]};
+        const f3 cam = {dr.cam[0], dr.cam[1], dr.cam[2]};
+        const f3 viewDir = normalize3(sub3(cam, wp));
+        const float diff = g_max(dot3(n, L), 0.0f);
+        const f3 half = normalize3(add3(L, viewDir));
+        const float spec = pow2k<5>(g_max(dot3(n, half), 0.0f));   // glm::pow(x, 32.0f)
+        const float sum = (0.15f + diff * 1.0f) + (0.5f * spec) * 1.0f;
+        a = f3{g_clamp01(sum * dr.ocol[0]), g_clamp01(sum * dr.ocol[1]), g_clamp01(sum * dr.ocol[2])};
+        return;
+    }
+    // Phong / Blinn-Phong VS (blinn_phong_shading.cpp:48-57)
+    a = wp;
+    nr = n;
+}
+
+// Quad: corner varyings of lane q (< 3), assembled into the triangle's 80-B ShadeRec; lane q
+// stores floats [5q, 5q + 5) so the quad writes the record contiguously.
+__device__ __forceinline__ void quad_store_shade(const FrameBuffers &fb, int tri, int draw, int shading, const f3 &a,
+                                                 const f3 &nr) {
+    const int q = __lane_id() & 3;
+    float f[20];
 #pragma unroll
-        for (int j = 0; j < 18; ++j) sr.v[j] = 0.0f;
-        if (dr.shading == 0) {
-            // Flat VS (flat_shading.cpp:54): normal = mat3(mv) * n
+    for (int k = 0; k < 3; ++k) {
+        f[3 * k] = quad_bcast(a.x, k); f[3 * k + 1] = quad_bcast(a.y, k); f[3 * k + 2] = quad_bcast(a.z, k);
+        f[9 + 3 * k] = quad_bcast(nr.x, k); f[9 + 3 * k + 1] = quad_bcast(nr.y, k); f[9 + 3 * k + 2] = quad_bcast(nr.z, k);
+    }
+    f[18] = __int_as_float(shading);
+    f[19] = __int_as_float(draw);
+    float *dst = reinterpret_cast<float *>(&fb.shade[tri]) + 5 * q;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const f3 n = m3v(dr.nmat, f3{N[3 * k], N[3 * k + 1], N[3 * k + 2]});
-                sr.v[3 * k] = n.x; sr.v[3 * k + 1] = n.y; sr.v[3 * k + 2] = n.z;
-            }
-        } else {
-            const f3 L = {dr.light[0], dr.light[1], dr.light[2]};
-            const f3 cam = {dr.cam[0], dr.cam[1], dr.cam[2]};
-            const f3 oc = {dr.ocol[0], dr.ocol[1], dr.ocol[2]};
+    for (int j = 0; j < 5; ++j) {
+        float x = f[j];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                float x, y, z, ww;
-                m4p(dr.model, p[3 * k], p[3 * k + 1], p[3 * k + 2], x, y, z, ww);
-                const f3 wp = {x, y, z};
-                const f3 nr = normalize3(m3v(dr.nmat, f3{N[3 * k], N[3 * k + 1], N[3 * k + 2]}));
-                if (dr.shading == 1) {
-                    // Gouraud VS (gouraud_shading.cpp:46-77): Blinn-Phong per vertex, shininess 32
-                    const f3 viewDir = normalize3(sub3(cam, wp));
-                    const float diff = g_max(dot3(nr, L), 0.0f);
-                    const f3 half = normalize3(add3(L, viewDir));
-                    const float spec = pow2k<5>(g_max(dot3(nr, half), 0.0f));   // glm::pow(x, 32.0f)
-                    const float sum = (0.15f + diff * 1.0f) + (0.5f * spec) * 1.0f;
-                    sr.v[3 * k] = g_clamp01(sum * oc.x);
-                    sr.v[3 * k + 1] = g_clamp01(sum * oc.y);
-                    sr.v[3 * k + 2] = g_clamp01(sum * oc.z);
-                } else {
-                    // Phong / Blinn-Phong VS (blinn_phong_shading.cpp:48-57)
-                    sr.v[3 * k] = wp.x; sr.v[3 * k + 1] = wp.y; sr.v[3 * k + 2] = wp.z;
-                    sr.v[9 + 3 * k] = nr.x; sr.v[9 + 3 * k + 1] = nr.y; sr.v[9 + 3 * k + 2] = nr.z;
-                }
-            }
+        for (int qq = 1; qq < 4; ++qq) x = q == qq ? f[5 * qq + j] : x;
+        dst[j] = x;
+    }
+}
+
+// Quad: lane q stores floats [6q, 6q + 6) of the 96-B record.
+__device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, const TriRec &r) {
+    const int q = __lane_id() & 3;
+    const float *f = reinterpret_cast<const float *>(&r);
+    float2 *dst = reinterpret_cast<float2 *>(reinterpret_cast<float *>(&fb.recs[tri]) + 6 * q);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        float x = f[2 * j], y = f[2 * j + 1];
+#pragma unroll
+        for (int qq = 1; qq < 4; ++qq) {
+            x = q == qq ? f[6 * qq + 2 * j] : x;
+            y = q == qq ? f[6 * qq + 2 * j + 1] : y;
         }
+        dst[j] = make_float2(x, y);
     }
 }
 
-// Write the wave's per-lane records (N float4 each, lanes [0, n_valid)) to dst[0 .. n_valid*N)
-// through the wave's LDS scratch: every store instruction covers 1 KB of contiguous HBM instead of
-// 64 strided 16-B pieces.
-template <int N>
-__device__ __forceinline__ void wave_store_coalesced(float4 *dst, const float4 (&v)[N], int n_valid, float4 *scratch) {
-    const int lane = __lane_id();
-#pragma unroll
-    for (int j = 0; j < N; ++j) scratch[lane * N + j] = v[j];
-    wave_lds_sync();
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        const int f = k * 64 + lane;
-        if (f < n_valid * N) dst[f] = scratch[f];
-    }
-    wave_lds_sync();
+// Record, varyings and their stores for the quad's triangle; returns the flags and the bin box.
+__device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU &dr, int d,
+                                               int tri, uint2 &gbox) {
+    const int q = __lane_id() & 3, qv = q < 3 ? q : 2;
+    const int local = tri - dr.tri_base;
+    const float *P = dr.pos + 9 * (size_t)local + 3 * qv;
+    const float *Nn = dr.nrm + 9 * (size_t)local + 3 * qv;
+    const float p3[3] = {P[0], P[1], P[2]};
+    const float n3[3] = {Nn[0], Nn[1], Nn[2]};
+    const TriRec r = quad_make_rec(fp, dr, d, local, p3);
+    tl_mark(fb.timeline, blockIdx.x, 4);
+    f3 a, nr;
+    corner_varyings(dr, p3, n3, a, nr);
+    quad_store_rec(fb, tri, r);
+    quad_store_shade(fb, tri, d, dr.shading, a, nr);
+    if (q == 0) fb.boxes[tri] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
+    gbox = make_uint2(r.gbx, r.gby);
+    return r.flags;
 }
 
-__device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, uint32_t *cnt,
-                            uint32_t (&s_stat)[4], float4 *wscratch) {
-    const int tid = threadIdx.x, lane = __lane_id();
-    const int gid = blockIdx.x * 256 + tid;
+constexpr int SMALL_RT = 16;  // raster tiles a quad marks by itself (4 per lane)
+constexpr int SMALL_BT = 8;   // bin tiles a quad appends to by itself (2 per lane)
+
+// One setup workgroup: 64 triangles, a quad of lanes each.
+__device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
+                                            uint32_t *cnt, uint32_t (&s_stat)[4]) {
+    const int tid = threadIdx.x, lane = __lane_id(), q = lane & 3;
     if (tid < 4) s_stat[tid] = 0u;
     __syncthreads();
-    const bool valid = gid < fp.n_tris;
+    QuadTri qt = quad_tri(draws, fp.n_draws, fp.n_tris, (int)blockIdx.x * 64 + (tid >> 2));
+    const int tri = qt.tri;
     uint32_t flags = TRI_CULLED;
     int gx0 = 0, gx1 = -1, gy0 = 0, gy1 = -1;
-    bool uni;
-    const int lo = wave_draw(draws, fp.n_draws, gid, valid, uni);
     tl_mark(fb.timeline, blockIdx.x, 0);
-    TriRec r;
-    ShadeRec sr;
-    if (valid) {
-        if (uni) {
-            const int lu = __builtin_amdgcn_readfirstlane(lo);
-            setup_tri(fp, fb, draws[lu], lu, gid, r, sr);
+    if (qt.valid) {
+        uint2 gb;
+        if (qt.uniform) {
+            const int d = __builtin_amdgcn_readfirstlane(qt.draw);
+            flags = setup_quad(fp, fb, draws[d], d, tri, gb);
         } else {
-            setup_tri(fp, fb, draws[lo], lo, gid, r, sr);
+            flags = setup_quad(fp, fb, draws[qt.draw], qt.draw, tri, gb);
         }
-        flags = r.flags;
-        gx0 = lo16(r.gbx); gx1 = hi16(r.gbx); gy0 = lo16(r.gby); gy1 = hi16(r.gby);
-    }
-    {   // coalesced record / varyings stores (the wave's triangles are consecutive)
-        const int wbase = (int)blockIdx.x * 256 + (tid & ~63);
-        const int n_valid = max(0, min(64, fp.n_tris - wbase));
-        wave_store_coalesced<6>(reinterpret_cast<float4 *>(fb.recs + wbase), reinterpret_cast<const float4(&)[6]>(r),
-                                n_valid, wscratch);
-        wave_store_coalesced<5>(reinterpret_cast<float4 *>(fb.shade + wbase), reinterpret_cast<const float4(&)[5]>(sr),
-                                n_valid, wscratch);
+        gx0 = lo16(gb.x); gx1 = hi16(gb.x); gy0 = lo16(gb.y); gy1 = hi16(gb.y);
     }
     tl_mark(fb.timeline, blockIdx.x, 1);
-    const bool live = valid && !(flags & TRI_CULLED) && gx0 <= gx1 && gy0 <= gy1;
+    const bool live = qt.valid && !(flags & TRI_CULLED) && gx0 <= gx1 && gy0 <= gy1;
     if (!live) { gx0 = 0; gx1 = -1; gy0 = 0; gy1 = -1; }
+    const bool sharded = fp.count > 1;
 
-    // -- busy marks on the raster tiles (32x8) of the bin box (owned bin tiles only)
+    // -- busy marks on the raster tiles (32x8) of the bin box (owned bin tiles only), the quad's
+    //    four lanes taking every fourth tile
     const int rx0 = gx0 / RTW, rx1 = live ? gx1 / RTW : -1, ry0 = gy0 / RTH, ry1 = live ? gy1 / RTH : -1;
-    const int n_rt = live ? (rx1 - rx0 + 1) * (ry1 - ry0 + 1) : 0;
+    const int nrx = rx1 - rx0 + 1, n_rt = live ? nrx * (ry1 - ry0 + 1) : 0;
     if (n_rt > 0 && n_rt <= SMALL_RT) {
-        for (int ry = ry0; ry <= ry1; ++ry)
-            for (int rx = rx0; rx <= rx1; ++rx)
-                if (owned_bin_tile(fp, rx, ry / (TILE / RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+        for (int k = q; k < n_rt; k += 4) {
+            const int rx = rx0 + k % nrx, ry = ry0 + k / nrx;
+            if (!sharded || owned_bin_tile(fp, rx, ry / (TILE / RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+        }
     }
     {
-        uint64_t big = __ballot(n_rt > SMALL_RT);
+        uint64_t big = __ballot(n_rt > SMALL_RT && q == 0);
         while (big) {
             const int src = __ffsll((unsigned long long)big) - 1;
             big &= big - 1;
@@ -545,40 +605,41 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
             const int nx = bx1 - bx0 + 1, n = nx * (by1 - by0 + 1);
             for (int k = lane; k < n; k += 64) {
                 const int rx = bx0 + k % nx, ry = by0 + k / nx;
-                if (owned_bin_tile(fp, rx, ry / (TILE / RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+                if (!sharded || owned_bin_tile(fp, rx, ry / (TILE / RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
             }
         }
     }
-
     tl_mark(fb.timeline, blockIdx.x, 2);
-    // -- bin appends (large scenes): bin tiles of the bin box
+
+    // -- bin appends (large scenes): bin tiles of the bin box, two per quad lane
     uint32_t n_bin = 0;
     if (!fp.scan_mode && !(fp.flags & DBG_SKIP_BIN)) {
         uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
         const int bx0 = gx0 / TILE, bx1 = live ? gx1 / TILE : -1, by0 = gy0 / TILE, by1 = live ? gy1 / TILE : -1;
-        const int nbx = bx1 - bx0 + 1, n_bt = live ? nbx * (by1 - by0 + 1) : 0;
-        int key[SMALL_BT];
-        uint32_t pos[SMALL_BT];
+        const int nbx = max(bx1 - bx0 + 1, 1), n_bt = live ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0;
+        int key[2];
+        uint32_t pos[2];
 #pragma unroll
-        for (int k = 0; k < SMALL_BT; ++k) {
-            const int bx = bx0 + (k % max(nbx, 1)), by = by0 + k / max(nbx, 1);
-            key[k] = (n_bt <= SMALL_BT && k < n_bt && owned_bin_tile(fp, bx, by)) ? by * fp.tiles_x + bx : -1;
+        for (int k = 0; k < 2; ++k) {
+            const int i = q + 4 * k;
+            const int bx = bx0 + i % nbx, by = by0 + i / nbx;
+            key[k] = (n_bt <= SMALL_BT && i < n_bt && (!sharded || owned_bin_tile(fp, bx, by))) ? by * fp.tiles_x + bx : -1;
         }
-        wave_append<SMALL_BT>(tcount, key, pos);
+        wave_append<2>(tcount, key, pos);
 #pragma unroll
-        for (int k = 0; k < SMALL_BT; ++k)
-            if (key[k] >= 0) { append_bin(fp, fb, cnt, key[k], pos[k], (uint32_t)gid); ++n_bin; }
-        uint64_t big = __ballot(n_bt > SMALL_BT);
+        for (int k = 0; k < 2; ++k)
+            if (key[k] >= 0) { append_bin(fp, fb, cnt, key[k], pos[k], (uint32_t)tri); ++n_bin; }
+        uint64_t big = __ballot(n_bt > SMALL_BT && q == 0);
         while (big) {
             const int src = __ffsll((unsigned long long)big) - 1;
             big &= big - 1;
             const int cx0 = __shfl(bx0, src), cx1 = __shfl(bx1, src), cy0 = __shfl(by0, src), cy1 = __shfl(by1, src);
-            const uint32_t id = (uint32_t)__shfl(gid, src);
+            const uint32_t id = (uint32_t)__shfl(tri, src);
             const int nx = cx1 - cx0 + 1, n = nx * (cy1 - cy0 + 1);
             uint32_t mine = 0;
             for (int k = lane; k < n; k += 64) {
                 const int bx = cx0 + k % nx, by = cy0 + k / nx;
-                if (!owned_bin_tile(fp, bx, by)) continue;
+                if (sharded && !owned_bin_tile(fp, bx, by)) continue;
                 const int t = by * fp.tiles_x + bx;
                 append_bin(fp, fb, cnt, t, atomicAdd(&tcount[t], 1u), id);
                 ++mine;
@@ -588,12 +649,13 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
             if (lane == src) n_bin += tot;
         }
     }
-
     tl_mark(fb.timeline, blockIdx.x, 3);
-    // -- per-block statistics (no same-address global atomics)
-    const uint64_t m_setup = __ballot(valid && !(flags & TRI_CULLED));
-    const uint64_t m_ghost = __ballot(valid && !(flags & TRI_CULLED) && (flags & TRI_GHOST));
-    const uint64_t m_unb = __ballot(valid && !(flags & TRI_CULLED) && (flags & TRI_UNBOUNDED));
+
+    // -- per-block statistics (no same-address global atomics); one lane per quad counts
+    const bool lead = qt.valid && q == 0 && !(flags & TRI_CULLED);
+    const uint64_t m_setup = __ballot(lead);
+    const uint64_t m_ghost = __ballot(lead && (flags & TRI_GHOST));
+    const uint64_t m_unb = __ballot(lead && (flags & TRI_UNBOUNDED));
     for (int o = 32; o > 0; o >>= 1) n_bin += __shfl_down(n_bin, o);
     if (lane == 0) {
         atomicAdd(&s_stat[0], (uint32_t)__popcll(m_setup));
@@ -605,59 +667,31 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     if (tid == 0) fb.blk_stat[blockIdx.x] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
 }
 
-// Clear of CLEAR_BT_PER_BLOCK bin tiles (colour canvas rows, depth screen rows, 16-B stores; owned
-// tiles only) and zeroing of their bin counts for the next frame (every tile).
-__device__ __forceinline__ void clear_block(const FrameParams &fp, const FrameBuffers &fb, int cb) {
-    const int tid = threadIdx.x;
-    const int n_bt = fp.tiles_x * fp.tiles_y;
-    uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
-    const int r = tid >> 3, seg = tid & 7;   // 32 rows x 8 16-B segments per tile
-    for (int i = 0; i < CLEAR_BT_PER_BLOCK; ++i) {
-        const int t = cb * CLEAR_BT_PER_BLOCK + i;
-        if (t >= n_bt) break;
-        if (tid == 0) next_count[t] = 0u;
-        if (t % fp.count != fp.rank || (fp.flags & DBG_SKIP_CLEAR)) continue;
-        const int bx = t % fp.tiles_x, by = t / fp.tiles_x;
-        const int y = by * TILE + r, x = bx * TILE + seg * 4;
-        if (y >= fp.H || x >= fp.W) continue;
-        const size_t crow = (size_t)(fp.H - 1 - y) * fp.W, drow = (size_t)y * fp.W;
-        if (x + 3 < fp.W && (fp.W & 3) == 0) {
-            const uint32_t c = fp.clear_rgba;
-            *reinterpret_cast<uint4 *>(fb.color + (crow + x) * 4) = make_uint4(c, c, c, c);
-            *reinterpret_cast<float4 *>(fb.depth + drow + x) = make_float4(FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
-        } else {
-            for (int j = 0; j < 4 && x + j < fp.W; ++j) {
-                reinterpret_cast<uint32_t *>(fb.color)[crow + x + j] = fp.clear_rgba;
-                fb.depth[drow + x + j] = FLT_MAX;
-            }
-        }
-        if (fb.prequant)
-            for (int j = 0; j < 4 && x + j < fp.W; ++j) fb.prequant[crow + x + j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-}
-
 template <bool KARG>
 __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
-    __shared__ float4 s_wscratch[4][64 * 6];   // per-wave store staging (setup role)
     uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
     const DrawGPU *draws = draw_table<KARG>(fb, ka);
     const int b = (int)blockIdx.x;
     const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
-    // zero the other counter set for the next frame (block 0 exists even for an empty frame)
+    // zero the other counter set and bin counts for the next frame (block 0 exists even for an
+    // empty frame)
     if (b == 0 && threadIdx.x < C_NCOUNTERS) fb.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
+    {
+        const int n_bt = fp.tiles_x * fp.tiles_y;
+        uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
+        for (int t = b * 256 + (int)threadIdx.x; t < n_bt; t += (int)gridDim.x * 256) next_count[t] = 0u;
+    }
     if (b < fp.setup_blocks) {
-        setup_block(fp, fb, draws, cnt, s_stat, s_wscratch[threadIdx.x >> 6]);
+        setup_block(fp, fb, draws, cnt, s_stat);
     } else if (b < fp.setup_blocks + fp.ghost_blocks) {
         const int wave = threadIdx.x >> 6;
         const int gw = (b - fp.setup_blocks) * 4 + wave;
         const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
         if (gw < n_groups * (int)fp.ghost_slices && !(fp.flags & DBG_SKIP_GHOST))
             ghost_wave(fp, fb, draws, cnt, gw / (int)fp.ghost_slices, gw % (int)fp.ghost_slices, s_ghost[wave]);
-    } else {
-        clear_block(fp, fb, b - fp.setup_blocks - fp.ghost_blocks);
     }
     if (fb.timeline) {
         __syncthreads();
@@ -732,74 +766,73 @@ __device__ __forceinline__ void shade_winner(const float4 *du, const ShadeRec &s
     pre[2] = g_clamp01(s * oc.z) * 255.0f;
 }
 
-// Per-pixel winner state: depth, submission index, the winner's (v, w) (u is recomputed exactly as
-// (1 - v) - w, shs_renderer.hpp:819) and its position in the tile's candidate sequence (to find its
-// staged shading varyings; ~0u for a ghost fragment).
-struct Best {
-    float z;
-    uint32_t id;
-    float v, w;
-    uint32_t pos;
-};
+// Order-preserving key of the z test: the reference's in-order strict-less test keeps, per pixel, the
+// lexicographic minimum of (z, submission index) (the first triangle with the minimal z wins), so
+// a 64-bit key (orderable z bits << 32 | index) resolved by atomic min in LDS is exact and
+// independent of the order candidates are processed in.  -0 and +0 compare equal in the
+// reference, so -0 maps to +0's key; NaN and z >= FLT_MAX never pass (never written).
+constexpr unsigned long long KEY_EMPTY = ~0ull;
 
-__device__ __forceinline__ void resolve(float z, uint32_t id, float v, float w, uint32_t pos, Best &b) {
-    // In-order strict-less z test == lexicographic min of (z, submission index); NaN never wins,
-    // z == FLT_MAX never beats the FLT_MAX clear (id sentinel 0 makes id < b.id false).
-    if (z < b.z || (z == b.z && id < b.id)) { b.z = z; b.id = id; b.v = v; b.w = w; b.pos = pos; }
+__device__ __forceinline__ unsigned long long z_key(float z, uint32_t id) {
+    uint32_t b = __float_as_uint(z);
+    b = (b << 1) == 0u ? 0u : b;                                 // -0 -> +0
+    const uint32_t ord = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    return ((unsigned long long)ord << 32) | id;
 }
 
-// One triangle against one pixel.  ibox pixels are always in the reference's visited set; outside
-// it only bounded ghosts are tested here, and only where the tile clamp visits the pixel (the
-// unbounded slivers' outside pixels arrive as ghost fragments).
-__device__ __forceinline__ void raster_px(int px, int py, float rtminx, float rtmaxx, float rtminy, float rtmaxy,
-                                          const TriRec &r, uint32_t id, uint32_t pos, Best &b) {
+// One (triangle, pixel) test: the pixel is in the reference's visited set for this triangle
+// (inside the ibox, or for a bounded ghost where its tile job's clamped rectangle covers it) and
+// its barycentrics pass; returns z.
+__device__ __forceinline__ bool pixel_test(const FrameParams &fp, const TriRec &r, int px, int py, float &z) {
     const bool in_ibox = px >= lo16(r.ibx) && px <= hi16(r.ibx) && py >= lo16(r.iby) && py <= hi16(r.iby);
     bool test = in_ibox;
-    if (r.flags & TRI_GHOST) {
-        const bool in_gbox = px >= lo16(r.gbx) && px <= hi16(r.gbx) && py >= lo16(r.gby) && py <= hi16(r.gby);
-        if (!in_ibox && in_gbox) {
-            // draw_triangle_tile's visited rectangle in this pixel's tile job (blinn_phong_shading.cpp:208-224)
-            const float bminx = g_max(rtminx, g_min(rtmaxx, r.fminx));
-            const float bmaxx = g_min(rtmaxx, g_max(rtminx, r.fmaxx));
-            const float bminy = g_max(rtminy, g_min(rtmaxy, r.fminy));
-            const float bmaxy = g_min(rtmaxy, g_max(rtminy, r.fmaxy));
-            test = !(bminx > bmaxx || bminy > bmaxy) && px >= (int)bminx && px <= (int)bmaxx && py >= (int)bminy &&
-                   py <= (int)bmaxy;
-        }
+    if (!in_ibox && (r.flags & TRI_GHOST)) {
+        // draw_triangle_tile's visited rectangle in this pixel's tile job (blinn_phong_shading.cpp:208-224)
+        const int rxs = (px / fp.rtw) * fp.rtw, rys = (py / fp.rth) * fp.rth;
+        const float rtminx = (float)rxs, rtmaxx = (float)(min(rxs + fp.rtw, fp.W) - 1);
+        const float rtminy = (float)rys, rtmaxy = (float)(min(rys + fp.rth, fp.H) - 1);
+        const float bminx = g_max(rtminx, g_min(rtmaxx, r.fminx));
+        const float bmaxx = g_min(rtmaxx, g_max(rtminx, r.fmaxx));
+        const float bminy = g_max(rtminy, g_min(rtmaxy, r.fminy));
+        const float bmaxy = g_min(rtmaxy, g_max(rtminy, r.fmaxy));
+        test = !(bminx > bmaxx || bminy > bmaxy) && px >= (int)bminx && px <= (int)bmaxx && py >= (int)bminy &&
+               py <= (int)bmaxy;
     }
     float u, v, w;
-    if (test && bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w)) {
-        const float z = (u * r.z0 + v * r.z1) + w * r.z2;
-        resolve(z, id, v, w, pos, b);
-    }
+    if (!(test && bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w))) return false;
+    z = (u * r.z0 + v * r.z1) + w * r.z2;
+    return z < FLT_MAX;   // NaN and FLT_MAX never beat the FLT_MAX clear
 }
 
-constexpr int RCHUNK = 128;        // candidates staged per pass (record + shading varyings)
+constexpr int RCHUNK = 128;        // candidate records staged per pass
 constexpr int LDS_DRAWS = 64;      // draws whose shading uniforms are kept in LDS
 
 struct RasterShared {
     float4 rec[RCHUNK * 6];           // staged triangle records (12 KB)
-    float4 shd[RCHUNK * 5];           // staged shading varyings (10 KB)
+    unsigned long long key[RTH * RTW];// per-pixel (z, index) keys (2 KB)
     uint32_t id[RCHUNK];
     uint32_t cand[CAND];
+    unsigned long long wmask[4];      // per-wave candidate-start masks (pair windows)
     float4 du[LDS_DRAWS * 4];         // per-draw {light, cam, ocol, colf} (4 KB)
-    uint32_t oc[RTH * RTW];           // output staging: colour
-    float od[RTH * RTW];              // output staging: depth
     int busy[256];                    // this workgroup's busy tiles
     uint32_t nc, nbusy, cov, maxbin;
 };
 
-// One busy raster tile: gather candidates, resolve, shade, write.  rt = raster-tile index
-// (row * tiles_x + column).  pbx: this thread's prefetched bin boxes of triangles tid + 256k (scan
-// mode with n_tris <= CAND).
-__device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, const uint32_t *cnt,
-                            int rt, const uint2 (&pbx)[CAND / 256], bool prefetched, RasterShared &sh, uint64_t *tl) {
-    const int tls = fp.setup_grid + (int)blockIdx.x;
+// One busy raster tile.  Candidates (bin box overlaps the tile) are staged in LDS; every (candidate,
+// pixel of its clipped bin box) pair is one lane-task, dealt evenly over the workgroup by a prefix
+// sum of the box areas; passing pairs atomic-min their key into the tile's LDS key array.  Then
+// each thread owns one pixel: the winner's record and varyings are fetched by index, (u, v, w)
+// recomputed with the identical arithmetic, the pixel shaded and written.
+__device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
+                                            const uint32_t *cnt, int rt, const uint2 (&pbx)[CAND / 256], bool prefetched,
+                                            RasterShared &sh, uint64_t *tl) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tls = fp.setup_grid + (int)blockIdx.x;
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
     const int X0 = col * RTW, Y0 = row * RTH;
     const int X1 = X0 + RTW - 1, Y1 = Y0 + RTH - 1;
     const int bt = (row / (TILE / RTH)) * fp.tiles_x + col;
+    __syncthreads();   // the previous tile's key resets are done
 
     // candidate sources.  scan mode: every triangle's bin box.  bin mode: the bin tile's list, then
     // the spill list (entries of this bin tile).
@@ -814,18 +847,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
         if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
     }
     const uint32_t *bin = fb.bins + (size_t)bt * fp.bin_cap;
-
-    // this lane's pixel: wave w owns the 8x8 block at (X0 + 8w, Y0)
-    const int bxl = X0 + wave * 8;
-    const int px = bxl + (lane & 7), py = Y0 + (lane >> 3);
-    const int rxs = (px / fp.rtw) * fp.rtw, rys = (py / fp.rth) * fp.rth;
-    const float rtminx = (float)rxs, rtmaxx = (float)(min(rxs + fp.rtw, fp.W) - 1);
-    const float rtminy = (float)rys, rtmaxy = (float)(min(rys + fp.rth, fp.H) - 1);
-    Best best;
-    best.z = FLT_MAX; best.id = 0u; best.v = 0.f; best.w = 0.f; best.pos = ~0u;
-    uint32_t seq = 0;                  // candidates staged so far (positions of the sequence)
-    uint32_t hits = 0;                 // candidates this wave rasterized (profiling)
-    uint32_t last_lo = 0, last_hi = 0; // positions held in sh.shd after the loops
+    uint32_t seq = 0;   // candidates processed (profiling)
+    int pairs = 0;      // (candidate, pixel) tasks (profiling)
 
     for (uint32_t base = 0; base < n_items; base += CAND) {
         __syncthreads();
@@ -859,8 +882,11 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
         }
 #pragma unroll
         for (int k = 0; k < CAND / 256; ++k) {
-            const bool hit = ids[k] != 0xffffffffu && !(hi16(bx[k].x) < X0 || lo16(bx[k].x) > X1 || hi16(bx[k].y) < Y0 ||
-                                                       lo16(bx[k].y) > Y1);
+            // non-empty bin box overlapping the tile (so its clipped box holds >= 1 pixel: the pair
+            // mapping below relies on it; off-screen triangles have empty boxes like [W, W-1])
+            const int gx0 = lo16(bx[k].x), gx1 = hi16(bx[k].x), gy0 = lo16(bx[k].y), gy1 = hi16(bx[k].y);
+            const bool hit = ids[k] != 0xffffffffu && gx0 <= gx1 && gy0 <= gy1 && gx1 >= X0 && gx0 <= X1 && gy1 >= Y0 &&
+                             gy0 <= Y1;
             const uint64_t m = __ballot(hit);
             uint32_t basew = 0;
             if (lane == 0 && m) basew = atomicAdd(&sh.nc, (uint32_t)__popcll(m));
@@ -873,111 +899,149 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
         for (uint32_t c = 0; c < nc; c += RCHUNK) {
             const int m = (int)min((uint32_t)RCHUNK, nc - c);
             if (c > 0) __syncthreads();
-            // stage records (6 float4 each) then shading varyings (5 each): consecutive lanes load
-            // consecutive float4s of one record, so a load instruction touches ~11 records' lines
+            // stage records: consecutive lanes load consecutive float4s of one record
             if (tid < m) sh.id[tid] = sh.cand[c + tid];
             {
-                constexpr int NQ = (RCHUNK * 11 + 255) / 256;
+                constexpr int NQ = RCHUNK * 6 / 256;
                 float4 q[NQ];
-                float4 *dst[NQ];
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) {
                     const int f = tid + 256 * k;
-                    const bool isrec = f < 6 * m;
-                    const int g = isrec ? f : f - 6 * m;
-                    const int per = isrec ? 6 : 5;
-                    const int ci = g / per, part = g - ci * per;
-                    const bool ok = f < 11 * m;
-                    const uint32_t id = sh.cand[c + (ok ? ci : 0)];
-                    const float4 *src = isrec ? reinterpret_cast<const float4 *>(&fb.recs[id]) + part
-                                              : reinterpret_cast<const float4 *>(&fb.shade[id]) + part;
-                    dst[k] = ok ? (isrec ? &sh.rec[f] : &sh.shd[g]) : nullptr;
-                    q[k] = ok ? *src : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const int ci = f / 6;
+                    q[k] = f < 6 * m ? reinterpret_cast<const float4 *>(&fb.recs[sh.cand[c + min(ci, m - 1)]])[f - 6 * ci]
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
 #pragma unroll
-                for (int k = 0; k < NQ; ++k)
-                    if (dst[k]) *dst[k] = q[k];
+                for (int k = 0; k < NQ; ++k) {
+                    const int f = tid + 256 * k;
+                    if (f < 6 * m) sh.rec[f] = q[k];
+                }
             }
             __syncthreads();
             tl_mark(tl, tls, 2);
-            // this wave's candidates: bin box overlaps its 8x8 block (64 tested per ballot)
-            for (int j0 = 0; j0 < m; j0 += 64) {
-                const int j = j0 + lane;
-                bool hit = false;
-                if (j < m) {
-                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[j * 6])[4];   // ibx iby gbx gby
-                    hit = !(hi16(bb.z) < bxl || lo16(bb.z) > bxl + 7 || hi16(bb.w) < Y0 || lo16(bb.w) > Y1);
+            // Pair tasks.  Wave w takes the staged candidates c = w + 4l (lane l holds candidate l of
+            // its list): clipped bin box in the tile, area, and the wave-inclusive prefix of the areas.
+            // The wave then walks its (candidate, pixel) pairs 64 at a time; a pair's owner is found
+            // by counting the candidate starts at or before it (ballot + 64-bit start mask), no search.
+            {
+                const int c = wave + 4 * lane;
+                int area = 0, bx0 = 0, by0 = 0, bw = 1;
+                if (c < m) {
+                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[c * 6])[4];   // ibx iby gbx gby
+                    const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
+                    const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
+                    if (x0 <= x1 && y0 <= y1) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
                 }
-                uint64_t mk = __ballot(hit);
-                hits += (uint32_t)__popcll(mk);
-                while (mk) {
-                    const int jj = j0 + __ffsll((unsigned long long)mk) - 1;
-                    mk &= mk - 1;
-                    const TriRec r = rec_from(&sh.rec[jj * 6]);
-                    raster_px(px, py, rtminx, rtmaxx, rtminy, rtmaxy, r, sh.id[jj], seq + (uint32_t)jj, best);
+                int incl = area;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(incl, o);
+                    if (lane >= o) incl += v;
+                }
+                const int start = incl - area;
+                const int total = __shfl(incl, 63);
+                pairs += total;
+                for (int k0 = 0; k0 < total; k0 += 64) {
+                    // candidates starting inside [k0, k0 + 64): one bit each (areas >= 1: distinct starts)
+                    const bool in_win = area > 0 && start >= k0 && start < k0 + 64;
+                    if (lane == 0) sh.wmask[wave] = 0ull;
+                    wave_lds_sync();
+                    if (in_win) atomicOr(&sh.wmask[wave], 1ull << (start - k0));
+                    wave_lds_sync();
+                    const unsigned long long M = sh.wmask[wave];
+                    const int before = __popcll(__ballot(area > 0 && start < k0));
+                    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                    const int o = before + __popcll(M & upto) - 1;            // owner (wave list index)
+                    const int k = k0 + lane;
+                    const int ostart = __shfl(start, o), ox0 = __shfl(bx0, o), oy0 = __shfl(by0, o), ow = __shfl(bw, o);
+                    if (k < total) {
+                        const int local = k - ostart;
+                        const int ly = local / ow, lx = local - ly * ow;
+                        const int oc = wave + 4 * o;
+                        const TriRec r = rec_from(&sh.rec[oc * 6]);
+                        float z;
+                        if (pixel_test(fp, r, ox0 + lx, oy0 + ly, z))
+                            atomicMin(&sh.key[(oy0 + ly - Y0) * RTW + (ox0 + lx - X0)], z_key(z, sh.id[oc]));
+                    }
                 }
             }
-            last_lo = seq;
             seq += (uint32_t)m;
-            last_hi = seq;
         }
     }
     tl_mark(tl, tls, 3);
     // tile-clamp pixels of unbounded slivers outside their bbox that passed (k_setup ghost waves)
     {
         const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
-        for (uint32_t f = 0; f < n_frag; ++f) {
+        for (uint32_t f = tid; f < n_frag; f += 256) {
             const GhostFrag g = fb.frags[f];
-            if ((int)(g.xy & 0xffffu) == px && (int)(g.xy >> 16) == py) resolve(g.z, g.id, g.v, g.w, ~0u, best);
+            const int gx = (int)(g.xy & 0xffffu), gy = (int)(g.xy >> 16);
+            if (gx >= X0 && gx <= X1 && gy >= Y0 && gy <= Y1) atomicMin(&sh.key[(gy - Y0) * RTW + (gx - X0)], z_key(g.z, g.id));
         }
     }
+    __syncthreads();
 
-    // shade this lane's winner (varyings from LDS when its candidate is in the last staged pass)
+    // one pixel per thread: resolve, shade the winner, write (rows of 32 px: 128-B segments)
+    const int px = X0 + (tid & 31), py = Y0 + (tid >> 5);
+    const unsigned long long key = sh.key[tid];
+    sh.key[tid] = KEY_EMPTY;   // clean for the next tile (read above, by this thread only)
     uint32_t rgba = fp.clear_rgba;
-    const bool covered = best.z < FLT_MAX && px < fp.W && py < fp.H;
-    if (covered && !(fp.flags & DBG_SKIP_SHADE)) {
+    float depth = FLT_MAX;
+    float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
+    if (covered) {
+        const uint32_t id = (uint32_t)key;
+        TriRec r;
         ShadeRec sr;
-        float4 *d = reinterpret_cast<float4 *>(&sr);
-        if (best.pos >= last_lo && best.pos < last_hi) {
-            const int t = (int)(best.pos - last_lo);
+        {
+            const float4 *s4 = reinterpret_cast<const float4 *>(&fb.recs[id]);
+            const float4 *h4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
+            float4 *d4 = reinterpret_cast<float4 *>(&r);
+            float4 *e4 = reinterpret_cast<float4 *>(&sr);
 #pragma unroll
-            for (int k = 0; k < 5; ++k) d[k] = sh.shd[t * 5 + k];
-        } else {
-            const float4 *src = reinterpret_cast<const float4 *>(&fb.shade[best.id]);
+            for (int k = 0; k < 6; ++k) d4[k] = s4[k];
 #pragma unroll
-            for (int k = 0; k < 5; ++k) d[k] = src[k];
+            for (int k = 0; k < 5; ++k) e4[k] = h4[k];
         }
-        const float u = (1.0f - best.v) - best.w;
-        const float4 *du = sr.draw < LDS_DRAWS ? &sh.du[sr.draw * 4] : reinterpret_cast<const float4 *>(draws[sr.draw].light);
-        float pre[3];
-        shade_winner(du, sr, u, best.v, best.w, pre);
-        const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
-        rgba = cr | (cg << 8) | (cb << 16) | (255u << 24);
-        if (fb.prequant) fb.prequant[(size_t)(fp.H - 1 - py) * fp.W + px] = make_float4(pre[0], pre[1], pre[2], 1.0f);
+        float u, v, w;
+        bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
+        depth = (u * r.z0 + v * r.z1) + w * r.z2;
+        if (!(fp.flags & DBG_SKIP_SHADE)) {
+            const float4 *du = sr.draw < LDS_DRAWS ? &sh.du[sr.draw * 4] : reinterpret_cast<const float4 *>(draws[sr.draw].light);
+            float pre[3];
+            shade_winner(du, sr, u, v, w, pre);
+            const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
+            rgba = cr | (cg << 8) | (cb << 16) | (255u << 24);
+            pq = make_float4(pre[0], pre[1], pre[2], 1.0f);
+        }
     }
     tl_mark(tl, tls, 4);
-    if (tl && tid == 0) { tl[TL_STRIDE * tls + 8] = seq; tl[TL_STRIDE * tls + 9] = hits; }
+    if (tl && tid == 0) { tl[TL_STRIDE * tls + 8] = seq; tl[TL_STRIDE * tls + 9] = (uint64_t)pairs; }
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
-    __syncthreads();   // previous tile's output staging is free
-    const int o = (lane >> 3) * RTW + wave * 8 + (lane & 7);
-    sh.oc[o] = rgba;
-    sh.od[o] = best.z;
-    __syncthreads();
-    // output: wave w writes rows 2w, 2w+1 of the tile (two 128-B segments per plane)
-    {
-        const int r = 2 * wave + (lane >> 5), x = X0 + (lane & 31), y = Y0 + r;
-        if (y < fp.H && x < fp.W) {
-            reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - y) * fp.W + x] = sh.oc[r * RTW + (lane & 31)];
-            fb.depth[(size_t)y * fp.W + x] = sh.od[r * RTW + (lane & 31)];
-        }
+    if (px < fp.W && py < fp.H) {
+        reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - py) * fp.W + px] = rgba;
+        fb.depth[(size_t)py * fp.W + px] = depth;
+        if (fb.prequant) fb.prequant[(size_t)(fp.H - 1 - py) * fp.W + px] = pq;
     }
     if (tid == 0) fb.busy[rt] = 0u;   // clean for the next frame
     tl_mark(tl, tls, 5);
 }
 
-// Persistent raster: workgroup b takes owned raster tiles j = b, b + G, b + 2G, ... and renders
-// the busy ones (the rest were cleared by k_setup).
+// A tile with no candidates: the clear, one pixel per thread (rows of 32 px: 128-B segments).
+__device__ __forceinline__ void clear_tile(const FrameParams &fp, const FrameBuffers &fb, int rt) {
+    const int tid = threadIdx.x;
+    const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
+    const int px = col * RTW + (tid & 31), py = row * RTH + (tid >> 5);
+    if (px < fp.W && py < fp.H) {
+        const size_t c = (size_t)(fp.H - 1 - py) * fp.W + px;
+        reinterpret_cast<uint32_t *>(fb.color)[c] = fp.clear_rgba;
+        fb.depth[(size_t)py * fp.W + px] = FLT_MAX;
+        if (fb.prequant) fb.prequant[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+// Persistent raster: workgroup b takes owned raster tiles j = b, b + G, b + 2G, ...: the busy ones
+// are rasterized, the others cleared -- every pixel of the frame is written exactly once.
 template <bool KARG>
 __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
@@ -988,6 +1052,7 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
     const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
+    sh.key[tid] = KEY_EMPTY;
     // per-draw shading uniforms into LDS; small scan-mode scenes: every bin box into registers
     for (int i = tid; i < min(fp.n_draws, LDS_DRAWS) * 4; i += 256)
         sh.du[i] = reinterpret_cast<const float4 *>(draws[i >> 2].light)[i & 3];
@@ -998,10 +1063,12 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
         const int i = tid + 256 * k;
         pbx[k] = (prefetched && i < fp.n_tris) ? fb.boxes[i] : make_uint2(0u, 0u);
     }
+    bool first = true;
     for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
         __syncthreads();
         if (tid == 0) sh.nbusy = 0;
         __syncthreads();
+        // thread t checks owned raster tile j0 + t*G: busy ones are queued, the others cleared
         const int j = j0 + tid * G;
         if (j < fp.n_owned_rt) {
             // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it
@@ -1009,20 +1076,28 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
             const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / RTH) + (j & 3);
             if (row < fp.rtiles_y) {
                 const int rt = row * fp.tiles_x + col;
-                if (fb.busy[rt]) sh.busy[atomicAdd(&sh.nbusy, 1u)] = rt;
+                if (fb.busy[rt]) sh.busy[atomicAdd(&sh.nbusy, 1u) & 0xffffu] = rt;
+                else sh.busy[255 - atomicAdd(&sh.nbusy, 0x10000u) / 0x10000u] = rt;   // clear list from the top
             }
         }
         __syncthreads();
-        tl_mark(fb.timeline, fp.setup_grid + (int)blockIdx.x, 0);
-        const int nb = (int)sh.nbusy;
+        tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
+        const int nb = (int)(sh.nbusy & 0xffffu), ne = (int)(sh.nbusy >> 16);
+        // busy tiles first (latency-bound), then the clears (streaming stores that other workgroups'
+        // busy tiles overlap with)
         for (int i = 0; i < nb; ++i) {
             const int rt = sh.busy[i];
             if (fp.flags & DBG_CLEAR_ONLY) {
+                __syncthreads();
+                clear_tile(fp, fb, rt);
                 if (tid == 0) fb.busy[rt] = 0u;
                 continue;
             }
-            raster_tile(fp, fb, draws, cnt, rt, pbx, prefetched, sh, (i == 0 && j0 == (int)blockIdx.x) ? fb.timeline : nullptr);
+            if (fp.flags & DBG_TWICE) raster_tile(fp, fb, draws, cnt, rt, pbx, prefetched, sh, nullptr);   // warm run
+            raster_tile(fp, fb, draws, cnt, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
+            first = false;
         }
+        for (int i = 0; i < ne; ++i) clear_tile(fp, fb, sh.busy[255 - i]);
     }
     __syncthreads();
     if (tid == 0) {

@@ -1,0 +1,96 @@
+"""Screen-tile sharding of one frame across ranks.
+
+Rank r of N renders only the bin tiles with `tile % N == r` (shs_frame_desc.shard_rank/count; a tile
+is shs_gpu_tile_size() px square, row-major).  The owned tiles of every rank are then gathered into
+the full frame on rank 0.  On GPUs the collective runs over RCCL ("nccl" backend) on device tensors;
+the same code runs over gloo on CPU tensors (tests/test_shard.py).
+
+Only the owned tiles travel: each rank packs its tiles' pixels contiguously (colour RGBA8 as int32
+words, depth as f32 bits), the ranks exchange equal-size padded buffers with all_gather, and rank 0
+scatters them back into canvas / screen rows.
+"""
+import numpy as np
+
+try:
+    import torch
+except ImportError:  # pragma: no cover - torch is present in this image
+    torch = None
+
+
+def owned_tiles(width, height, tile, rank, count):
+    """Row-major tile indices owned by `rank` (tile % count == rank)."""
+    tx = (width + tile - 1) // tile
+    ty = (height + tile - 1) // tile
+    return np.arange(rank, tx * ty, count, dtype=np.int64)
+
+
+def _tile_slices(t, width, height, tile):
+    tx = (width + tile - 1) // tile
+    x0, y0 = (t % tx) * tile, (t // tx) * tile
+    return y0, min(y0 + tile, height), x0, min(x0 + tile, width)
+
+
+def pack_owned(color, depth, tile, rank, count):
+    """Pack the owned tiles of (color [H,W,4] uint8 canvas rows, depth [H,W] f32 screen rows) into
+    one int32 vector: per tile, its colour words then its depth bits, tiles in index order."""
+    height, width = depth.shape
+    words = color.view(np.uint32).reshape(height, width)
+    dbits = depth.view(np.uint32)
+    parts = []
+    for t in owned_tiles(width, height, tile, rank, count):
+        y0, y1, x0, x1 = _tile_slices(t, width, height, tile)
+        # colour lives in canvas rows: screen row y is canvas row H-1-y
+        parts.append(words[height - y1:height - y0, x0:x1][::-1].ravel())
+        parts.append(dbits[y0:y1, x0:x1].ravel())
+    if not parts:
+        return np.zeros(0, np.int32)
+    return np.concatenate(parts).view(np.int32)
+
+
+def unpack_into(color, depth, packed, tile, rank, count):
+    """Inverse of pack_owned: write rank's tiles into the full frame buffers."""
+    height, width = depth.shape
+    words = color.view(np.uint32).reshape(height, width)
+    dbits = depth.view(np.uint32)
+    data = np.asarray(packed).view(np.uint32)
+    off = 0
+    for t in owned_tiles(width, height, tile, rank, count):
+        y0, y1, x0, x1 = _tile_slices(t, width, height, tile)
+        n = (y1 - y0) * (x1 - x0)
+        words[height - y1:height - y0, x0:x1] = data[off:off + n].reshape(y1 - y0, x1 - x0)[::-1]
+        off += n
+        dbits[y0:y1, x0:x1] = data[off:off + n].reshape(y1 - y0, x1 - x0)
+        off += n
+    return off
+
+
+def packed_len(width, height, tile, rank, count):
+    n = 0
+    for t in owned_tiles(width, height, tile, rank, count):
+        y0, y1, x0, x1 = _tile_slices(t, width, height, tile)
+        n += 2 * (y1 - y0) * (x1 - x0)
+    return n
+
+
+def gather_frame(dist, color, depth, tile, device=None):
+    """Collective: every rank passes its shard-rendered (color, depth) host buffers (only its own
+    tiles meaningful); rank 0 returns the composed full frame, other ranks return None.
+    `device` selects where the exchange buffers live ("cuda:k" for RCCL, None/cpu for gloo)."""
+    rank, count = dist.get_rank(), dist.get_world_size()
+    height, width = depth.shape
+    mine = pack_owned(color, depth, tile, rank, count)
+    longest = max(packed_len(width, height, tile, r, count) for r in range(count))
+    buf = np.zeros(longest, np.int32)
+    buf[:mine.size] = mine
+    t = torch.from_numpy(buf)
+    if device is not None:
+        t = t.to(device)
+    outs = [torch.empty_like(t) for _ in range(count)]
+    dist.all_gather(outs, t)
+    if rank != 0:
+        return None
+    full_c = np.zeros_like(color)
+    full_d = np.zeros_like(depth)
+    for r in range(count):
+        unpack_into(full_c, full_d, outs[r].cpu().numpy(), tile, r, count)
+    return full_c, full_d

@@ -70,7 +70,7 @@ def main():
         busy = r[r[:, 7] != 0]
         if len(busy):
             k = int(np.argmax(r[:, 1].astype(np.int64) - r[:, 0].astype(np.int64)))
-            print(f"  raster first-tile candidates: median {np.median(busy[:, 8]):.0f} max {busy[:, 8].max()} | wave-0 hits "
+            print(f"  raster first-tile candidates: median {np.median(busy[:, 8]):.0f} max {busy[:, 8].max()} | pair tasks "
                   f"median {np.median(busy[:, 9]):.0f} max {busy[:, 9].max()} | slowest wg: cand {r[k, 8]} hits {r[k, 9]}")
         for nm, arr in (("setup", s), ("raster", r)):
             dt = arr[:, 1].astype(np.int64) - arr[:, 0].astype(np.int64)
