@@ -13,9 +13,10 @@ N > 1 (torchrun, one process per GPU): frame-parallel -- every rank renders its 
 same workload (camera yaw offset per rank), no data-path collective; "scaling": "weak".
 
 Also reported (rank 0, N = 1):
-  roofline      dominant kernel (k_raster): SURVEY.md 8(d) algorithmic bytes per frame
-                (N_tri*72 + W*H*8) / its mean HIP-event duration over the timed region, against
-                8 TB/s; "traffic" = HBM bytes per k_raster dispatch from rocprofv3 PMC counters
+  roofline      dominant kernel (k_raster, which writes every output byte of the frame): SURVEY.md
+                8(d) algorithmic bytes per frame (N_tri*72 + W*H*8) / its mean HIP-event duration
+                over the timed region, against 8 TB/s (frame_frac: the same bytes over k_setup +
+                k_raster); "traffic" = HBM bytes per k_raster dispatch from rocprofv3 PMC counters
                 (FETCH_SIZE x2 [gfx950 half-count correction] + WRITE_SIZE, KiB units), collected in
                 separate child passes before this process touches the GPU.
   cpu_baseline  the oracle (CPU restatement of the reference's 80x80 tile-job path, gcc -O3) timed
@@ -223,6 +224,11 @@ def main():
         "algorithmic_bytes": B,
         "kernel_ms": round(t_raster_ms, 5),
     }
+    # the whole frame's device time (k_setup + k_raster) against the same bytes, for reference
+    t_frame_ms = kms.get("setup", 0.0) + t_raster_ms
+    if t_frame_ms > 0:
+        roofline["frame_kernels_ms"] = round(t_frame_ms, 5)
+        roofline["frame_frac"] = round(B / (t_frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if pmc is None:
         roofline["traffic_note"] = pmc_err
     line = {

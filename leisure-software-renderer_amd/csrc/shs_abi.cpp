@@ -163,7 +163,7 @@ int shs_create(int device, shs_ctx **out) {
     for (int i = 0; i < 2; ++i)
         if (hipEventCreateWithFlags(&ctx->slot_ev[i], hipEventDisableTiming) != hipSuccess) { delete ctx; return SHS_ERR_HIP; }
     for (int i = 0; i < 5; ++i)
-        if (hipEventCreate(&ctx->tev[i]) != hipSuccess) { delete ctx; return SHS_ERR_HIP; }
+        if (hipEventCreateWithFlags(&ctx->tev[i], hipEventDisableSystemFence) != hipSuccess) { delete ctx; return SHS_ERR_HIP; }
     if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_counters), shs_dev::C_NCOUNTERS * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
         return SHS_ERR_HIP;
@@ -433,7 +433,7 @@ static int enqueue_frame(shs_ctx *ctx) {
         ctx->ring_next = (k + 1) % shs_ctx::RING;
         if (harvest_slot(ctx, k)) return SHS_ERR_HIP;
         if (!ctx->ring_ev[k][0])
-            for (int i = 0; i < 5; ++i) HIP_TRY(ctx, hipEventCreate(&ctx->ring_ev[k][i]));
+            for (int i = 0; i < 5; ++i) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ring_ev[k][i], hipEventDisableSystemFence));
         ev = ctx->ring_ev[k];
         ctx->ring_pending[k] = true;
     }
