@@ -157,6 +157,100 @@ int shs_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n
 int shs_abi_version(void);
 int shs_gpu_tile_size(void);
 
+/* =========================================================================================
+ * Library path -- Seam 2 (rasterize_mesh, shs-renderer-lib/include/shs/sw_render/rasterizer.hpp
+ * :181-442) and Seam 3 (PassShadowMap, passes/pass_shadow_map.hpp:44-206; PassPBRForward,
+ * passes/pass_pbr_forward.hpp:49-214).  The std::function ShaderProgram becomes a program enum
+ * + the POD uniform block below.  Paths relative to shs-renderer-lib/include/shs/.
+ * ========================================================================================= */
+#define SHS_PROGRAM_PBR_MR 0        /* make_pbr_mr_program          shader/builtin_shaders.hpp:154-214 */
+#define SHS_PROGRAM_BLINN_PHONG 1   /* make_blinn_phong_program     :105-152                         */
+#define SHS_PROGRAM_DEBUG_ALBEDO 2  /* make_debug_view_shader_program(DebugViewMode) :221-245        */
+#define SHS_PROGRAM_DEBUG_NORMAL 3
+#define SHS_PROGRAM_DEBUG_DEPTH 4
+
+#define SHS_CULL_NONE 0             /* RasterizerCullMode (rasterizer.hpp:26-31) */
+#define SHS_CULL_BACK 1
+#define SHS_CULL_FRONT 2
+
+/* MeshData (resources/mesh.hpp:23-43): n_verts vec3 positions; normals / uvs may be shorter than
+ * positions (missing entries read as (0,1,0) / (0,0), rasterizer.hpp:196-202) or NULL; indices NULL
+ * = non-indexed soup (3 consecutive positions per triangle).  Device resident from here on. */
+int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const float *normals, int32_t n_normals,
+                    const float *uvs, int32_t n_uvs, const uint32_t *indices, int64_t n_indices, int32_t *mesh_id);
+
+/* One rasterize_mesh call as PassPBRForward issues it per RenderItem: the ShaderUniforms fields the
+ * builtin programs read (shader/types.hpp:87-116) and RasterizerConfig's cull mode / front face.
+ * shadow != 0: u.shadow_map = the context's shadow map (last shs_render_shadow_map). */
+typedef struct shs_lib_draw {
+    int32_t mesh_id;
+    int32_t program;              /* SHS_PROGRAM_* */
+    int32_t cull_mode;            /* SHS_CULL_* */
+    int32_t front_face_ccw;
+    float model[16], viewproj[16], prev_model[16], prev_viewproj[16];
+    float light_dir_ws[3], light_color[3], light_intensity, camera_pos[3];
+    float base_color[3], metallic, roughness, ao;
+    int32_t shadow;
+    float light_viewproj[16];
+    float shadow_bias_const, shadow_bias_slope;
+    int32_t shadow_pcf_radius;
+    float shadow_pcf_step, shadow_strength;
+    int32_t enable_motion_vectors;
+} shs_lib_draw;
+
+#define SHS_LIB_DEPTH_MOTION 1u   /* RasterizerTarget::depth_motion present: z test, depth + motion */
+#define SHS_LIB_BG_GRADIENT 2u    /* PassPBRForward's no-sky background gradient, else clear_hdr     */
+
+/* The pass's render targets: RT_ColorHDR (W*H RGBA32F, rows y-up) and RT_ColorDepthMotion (depth
+ * cleared to 1 with zn / zf for the linear depth, motion cleared to 0).  shard_rank / shard_count as
+ * in shs_frame_desc (32x32 tiles, tile % count == rank). */
+typedef struct shs_lib_frame {
+    int32_t width, height;
+    int32_t shard_rank, shard_count;
+    uint32_t flags;               /* SHS_LIB_* */
+    float zn, zf;
+    float clear_hdr[4];
+} shs_lib_frame;
+
+typedef struct shs_lib_stats {
+    uint64_t tri_input;           /* RasterizerStats (rasterizer.hpp:48-53) */
+    uint64_t tri_after_clip;
+    uint64_t tri_raster;
+    uint64_t covered_pixels;      /* pixels whose depth != clear (shaded Mpix/s numerator) */
+    uint64_t max_tile_bin;
+    uint64_t spilled;
+    uint64_t clipped_extra;       /* fan triangles beyond the first of clipped input triangles */
+} shs_lib_stats;
+
+/* PassPBRForward::execute: clear (gradient / clear_hdr, depth 1, motion 0) and one rasterize_mesh per
+ * draw, in order, asynchronously on the context stream. */
+int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_lib_draw *draws, int32_t n_draws);
+/* Copy the pass's targets into caller-owned buffers: hdr W*H*4 floats, depth W*H, motion W*H*2
+ * (row y = bottom-up, exactly PixelBuffer2D::at(x, y)); any pointer may be NULL. */
+int shs_resolve_lib(shs_ctx *ctx, float *hdr, float *depth, float *motion);
+int shs_get_lib_stats(shs_ctx *ctx, shs_lib_stats *stats);
+int shs_lib_device_targets(shs_ctx *ctx, void **hdr_dev, void **depth_dev, void **motion_dev);
+
+/* A shadow caster (RenderItem with casts_shadow): mesh + model matrix. */
+typedef struct shs_shadow_caster {
+    int32_t mesh_id;
+    float model[16];
+} shs_shadow_caster;
+
+/* PassShadowMap::execute into the context's RT_ShadowDepth (w*h f32, cleared to 1): scene AABB of the
+ * casters' mesh bounds, build_dir_light_camera_aabb(sun_dir, aabb, 10, w) (camera/light_camera.hpp
+ * :33-98), then the depth pass.  light_viewproj_out (optional) receives ctx.shadow.light_viewproj. */
+int shs_render_shadow_map(shs_ctx *ctx, int32_t w, int32_t h, const float sun_dir[3], const shs_shadow_caster *casters,
+                          int32_t n_casters, float light_viewproj_out[16]);
+int shs_resolve_shadow_map(shs_ctx *ctx, float *depth);
+
+/* Host GLM restatements for non-C++ callers (camera/convention.hpp; pass_pbr_forward.hpp:136-141). */
+int shs_look_at_lh(const float eye[3], const float center[3], const float up[3], float out16[16]);
+int shs_perspective_lh_no(float fovy_radians, float aspect, float zn, float zf, float out16[16]);
+int shs_model_euler(const float pos[3], const float rot_euler[3], const float scl[3], float out16[16]);
+int shs_dir_light_camera_aabb(const float sun_dir[3], const float aabb_min[3], const float aabb_max[3], float extra_margin,
+                              uint32_t resolution, float view16[16], float proj16[16], float viewproj16[16]);
+
 #ifdef __cplusplus
 }
 #endif

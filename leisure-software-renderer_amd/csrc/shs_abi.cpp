@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/shs_gpu.h"
+#include "shs_ctx.hpp"
 #include "shs_device.hpp"
 #include "shs_glm.hpp"
 #include "shs_internal.hpp"
@@ -20,121 +21,6 @@ using shs_dev::DrawGPU;
 using shs_dev::FrameBuffers;
 using shs_dev::FrameParams;
 using shs_dev::TriRec;
-
-namespace {
-struct Mesh {
-    float *pos = nullptr;
-    float *nrm = nullptr;
-    int32_t n_tris = 0;
-    bool live = false;
-};
-
-template <typename T>
-struct DevBuf {
-    T *p = nullptr;
-    size_t cap = 0;  // elements
-};
-}  // namespace
-
-struct shs_ctx {
-    int device = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    std::string err;
-    std::vector<Mesh> meshes;
-
-    DevBuf<DrawGPU> draws;
-    DevBuf<TriRec> recs;
-    DevBuf<shs_dev::ShadeRec> shade;
-    DevBuf<uint32_t> tile_count;     // 2 parity sets of per-bin-tile counts
-    DevBuf<uint32_t> bins;           // n_tiles * bin_cap
-    DevBuf<uint2> spill;
-    DevBuf<shs_dev::GhostFrag> frags; // ghost fragments
-    DevBuf<uint2> boxes;             // per-triangle bin boxes
-    DevBuf<uint32_t> counters;       // 2 parity sets
-    DevBuf<uint32_t> busy;           // per raster tile
-    DevBuf<uint4> blk_stat;          // per setup block
-    DevBuf<uint2> rstat;             // per raster block
-    DevBuf<uint64_t> timeline;       // SHS_OPT_TIMELINE
-    bool want_timeline = false;
-    int last_setup_grid = 0, last_ghost_blocks = 0, last_clear_blocks = 0;
-    std::vector<uint4> h_blk_stat;
-    std::vector<uint2> h_rstat;
-    uint64_t geom_key = ~0ull;       // (tiles, shard) of the last frame: a change resets the counts
-    int last_setup_blocks = 0, last_raster_grid = 0;
-    uint64_t last_covered = 0, last_bins = 0, last_maxbin = 0, last_setup = 0, last_ghost = 0, last_unb = 0;
-    uint32_t bin_cap = 256;
-    int force_mode = 0;              // 0 auto, 1 scan, 2 bin (SHS_OPT_RASTER_MODE)
-    uint32_t frame_index = 0;        // parity of the counter set
-    uint32_t last_parity = 0;
-    DevBuf<uint8_t> color;
-    DevBuf<float> depth;
-    DevBuf<float4> prequant;
-
-    // pinned staging for the per-frame draw table (2 slots, guarded by events)
-    DrawGPU *h_draws[2] = {nullptr, nullptr};
-    size_t h_cap = 0;
-    hipEvent_t slot_ev[2] = {nullptr, nullptr};
-    bool slot_used[2] = {false, false};
-    int slot = 0;
-    uint32_t *h_counters = nullptr;  // pinned, C_NCOUNTERS
-
-    // last frame (re-issued if a bin capacity overflowed)
-    shs_frame_desc frame{};
-    std::vector<shs_legacy_draw> last_draws;
-    bool have_frame = false;
-    bool need_check = false;
-    int last_n_tris = 0;
-    int last_n_tiles = 0;
-
-    bool timing = false;
-    hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    float last_ms[4] = {0, 0, 0, 0};
-    // ring of per-frame kernel events, harvested lazily: sums of kernel durations over many frames
-    static constexpr int RING = 64;
-    hipEvent_t ring_ev[RING][5] = {};
-    bool ring_pending[RING] = {};
-    int ring_next = 0;
-    double acc_ms[4] = {0, 0, 0, 0};
-    int64_t acc_frames = 0;
-};
-
-#define HIP_TRY(ctx, expr)                                                                       \
-    do {                                                                                         \
-        hipError_t e_ = (expr);                                                                  \
-        if (e_ != hipSuccess) {                                                                  \
-            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                      \
-            return SHS_ERR_HIP;                                                                  \
-        }                                                                                        \
-    } while (0)
-
-template <typename T>
-static int ensure(shs_ctx *ctx, DevBuf<T> &b, size_t n) {
-    if (n <= b.cap && b.p) return SHS_OK;
-    size_t want = std::max<size_t>(n, 16);
-    if (b.p) {
-        // the old buffer may still be read by queued work on the stream
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        HIP_TRY(ctx, hipFree(b.p));
-        b.p = nullptr;
-        b.cap = 0;
-    }
-    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&b.p), want * sizeof(T)));
-    b.cap = want;
-    return SHS_OK;
-}
-
-template <typename T>
-static void release(DevBuf<T> &b) {
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-}
-
-static int set_dev(shs_ctx *ctx) {
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    return SHS_OK;
-}
 
 extern "C" {
 
@@ -185,7 +71,10 @@ int shs_destroy(shs_ctx *ctx) {
     for (auto &m : ctx->meshes) {
         if (m.pos) (void)hipFree(m.pos);
         if (m.nrm) (void)hipFree(m.nrm);
+        if (m.uv) (void)hipFree(m.uv);
+        if (m.idx) (void)hipFree(m.idx);
     }
+    shs_lib_release(ctx);
     release(ctx->draws); release(ctx->recs); release(ctx->shade); release(ctx->tile_count); release(ctx->bins);
     release(ctx->spill); release(ctx->frags); release(ctx->counters); release(ctx->busy); release(ctx->boxes);
     release(ctx->blk_stat); release(ctx->rstat); release(ctx->timeline);
@@ -239,6 +128,8 @@ int shs_mesh_release(shs_ctx *ctx, int32_t id) {
     Mesh &m = ctx->meshes[id];
     HIP_TRY(ctx, hipFree(m.pos));
     HIP_TRY(ctx, hipFree(m.nrm));
+    if (m.uv) HIP_TRY(ctx, hipFree(m.uv));
+    if (m.idx) HIP_TRY(ctx, hipFree(m.idx));
     m = Mesh{};
     return SHS_OK;
 }
@@ -520,7 +411,10 @@ int shs_render_legacy(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legac
     if (f.shard_count <= 0 || f.shard_rank < 0 || f.shard_rank >= f.shard_count) { ctx->err = "bad shard"; return SHS_ERR_INVALID; }
     for (int i = 0; i < n_draws; ++i) {
         const int id = draws[i].mesh_id;
-        if (id < 0 || id >= (int)ctx->meshes.size() || !ctx->meshes[id].live) { ctx->err = "bad mesh id"; return SHS_ERR_INVALID; }
+        if (id < 0 || id >= (int)ctx->meshes.size() || !ctx->meshes[id].live || ctx->meshes[id].lib) {
+            ctx->err = "bad mesh id (not a legacy soup mesh)";
+            return SHS_ERR_INVALID;
+        }
         if (draws[i].shading < SHS_SHADING_FLAT || draws[i].shading > SHS_SHADING_BLINN_PHONG) {
             ctx->err = "bad shading model";
             return SHS_ERR_INVALID;

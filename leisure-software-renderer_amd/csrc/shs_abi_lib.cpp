@@ -1,0 +1,498 @@
+// shs_abi_lib.cpp -- host side of the library raster path of libshs_gpu.so (include/shs_gpu.h,
+// "Library path"): MeshData upload, PassShadowMap, PassPBRForward (rasterize_mesh per item) and
+// the resolves.  Paths are relative to /root/reference/cpp-folders/src/shs-renderer-lib/include/shs/.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/shs_gpu.h"
+#include "shs_ctx.hpp"
+#include "shs_glm.hpp"
+#include "shs_lib_device.hpp"
+#include "shs_lib_internal.hpp"
+
+using shs_dev::LibBuffers;
+using shs_dev::LibDrawGPU;
+using shs_dev::LibFrameParams;
+using Work = shs_ctx::LibWork;
+
+namespace {
+
+constexpr int SCAN_MAX_PRIMS = 4096;   // smaller passes scan every primitive's box per busy tile
+
+void release_work(Work &w) {
+    release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase);
+    release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
+    release(w.spill); release(w.blk_stat); release(w.rstat);
+    for (int i = 0; i < 2; ++i) {
+        if (w.h_draws[i]) (void)hipHostFree(w.h_draws[i]);
+        if (w.slot_ev[i]) (void)hipEventDestroy(w.slot_ev[i]);
+        w.h_draws[i] = nullptr;
+        w.slot_ev[i] = nullptr;
+    }
+}
+
+// Per-draw block: the uniform-only products of the reference's per-vertex / per-fragment code,
+// computed once with the same float operations (shs_glm.hpp restates GLM's op order).
+void build_lib_draw(const shs_lib_draw &in, const Mesh &m, int32_t base, LibDrawGPU &o) {
+    using namespace shs_host;
+    std::memset(&o, 0, sizeof o);
+    o.pos = m.pos; o.nrm = m.nrm; o.uv = m.uv; o.idx = m.idx;
+    o.n_verts = m.n_verts;
+    o.tri_base = base;
+    o.n_tris = m.n_tris;
+    o.program = in.program;
+    o.cull_mode = in.cull_mode;
+    o.front_ccw = in.front_face_ccw != 0;
+    o.shadow = in.shadow != 0;
+    o.motion = in.enable_motion_vectors != 0;
+    std::memcpy(o.model, in.model, sizeof o.model);
+    std::memcpy(o.viewproj, in.viewproj, sizeof o.viewproj);
+    lib_normal_matrix(in.model, o.nmat);                       // builtin_shaders.hpp:93-95
+    if (std::fabs(det4(in.model)) > 1e-10f) {                  // rasterizer.hpp:296-308
+        float inv[16];
+        inverse(in.model, inv);
+        mul(in.prev_model, inv, o.c2p);
+    } else {
+        identity(o.c2p);
+    }
+    std::memcpy(o.prev_vp, in.prev_viewproj, sizeof o.prev_vp);
+    std::memcpy(o.light_vp, in.light_viewproj, sizeof o.light_vp);
+    const vec3 L = gnormalize(gneg(vec3{in.light_dir_ws[0], in.light_dir_ws[1], in.light_dir_ws[2]}));
+    o.L[0] = L.x; o.L[1] = L.y; o.L[2] = L.z;
+    for (int i = 0; i < 3; ++i) {
+        o.cam[i] = in.camera_pos[i];
+        o.lcol[i] = in.light_color[i];
+        o.base[i] = in.base_color[i];
+    }
+    o.lcol[3] = in.light_intensity;
+    o.base[3] = in.metallic;
+    o.mat[0] = in.roughness;
+    o.mat[1] = in.ao;
+    o.mat[2] = in.shadow_strength;
+    // ShadowParams as the builtin FS builds them: pcf_radius = max(0, r), pcf_step = max(1, step)
+    o.shp[0] = in.shadow_bias_const;
+    o.shp[1] = in.shadow_bias_slope;
+    const int32_t rad = std::max(0, in.shadow_pcf_radius);
+    std::memcpy(&o.shp[2], &rad, sizeof rad);
+    o.shp[3] = (1.0f < in.shadow_pcf_step) ? in.shadow_pcf_step : 1.0f;
+}
+
+// Upload the draw table through the work's pinned 2-slot staging.
+int upload_draws(shs_ctx *ctx, Work &w, const std::vector<LibDrawGPU> &d) {
+    const size_t n = std::max<size_t>(d.size(), 1);
+    if (ensure(ctx, w.draws, n)) return SHS_ERR_HIP;
+    const int s = w.slot;
+    w.slot ^= 1;
+    if (!w.slot_ev[0])
+        for (int i = 0; i < 2; ++i) HIP_TRY(ctx, hipEventCreateWithFlags(&w.slot_ev[i], hipEventDisableTiming));
+    if (w.slot_used[s]) HIP_TRY(ctx, hipEventSynchronize(w.slot_ev[s]));
+    if (n > w.h_cap) {
+        for (int i = 0; i < 2; ++i) {
+            if (i != s && w.slot_used[i]) HIP_TRY(ctx, hipEventSynchronize(w.slot_ev[i]));
+            if (w.h_draws[i]) HIP_TRY(ctx, hipHostFree(w.h_draws[i]));
+            w.h_draws[i] = nullptr;
+        }
+        const size_t cap = std::max<size_t>(n, 16);
+        for (int i = 0; i < 2; ++i) HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&w.h_draws[i]), cap * sizeof(LibDrawGPU)));
+        w.h_cap = cap;
+    }
+    if (!d.empty()) {
+        std::memcpy(w.h_draws[s], d.data(), d.size() * sizeof(LibDrawGPU));
+        HIP_TRY(ctx, hipMemcpyAsync(w.draws.p, w.h_draws[s], d.size() * sizeof(LibDrawGPU), hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, hipEventRecord(w.slot_ev[s], ctx->stream));
+    w.slot_used[s] = true;
+    return SHS_OK;
+}
+
+// Enqueue one pass (w.last_fp / w.last_draws describe it): workspace sizing, draw upload, the two
+// kernels.  shadow: PassShadowMap's depth pass into ctx->shadow_map.
+int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
+    LibFrameParams fp = w.last_fp;
+    const int W = fp.W, H = fp.H;
+    const int tiles_x = (W + shs_dev::TILE - 1) / shs_dev::TILE, tiles_y = (H + shs_dev::TILE - 1) / shs_dev::TILE;
+    const int n_tiles = tiles_x * tiles_y;
+    const int rtiles_y = (H + 7) / 8;
+    const int n_rt = tiles_x * rtiles_y;
+    int64_t total = 0;
+    for (const auto &d : w.last_draws) total += d.n_tris;
+    if (total > (1 << 27)) { ctx->err = "too many triangles in one pass"; return SHS_ERR_INVALID; }
+    const int n_tris = (int)total;
+    if (w.extra_cap == 0) w.extra_cap = (uint32_t)std::max(4096, n_tris / 4);
+    const size_t n_slots = (size_t)std::max(n_tris, 1) + (shadow ? 0 : w.extra_cap);
+    if (ensure(ctx, w.recs, n_slots) || ensure(ctx, w.boxes, n_slots)) return SHS_ERR_HIP;
+    if (!shadow && (ensure(ctx, w.shade, n_slots) || ensure(ctx, w.xbase, (size_t)std::max(n_tris, 1)))) return SHS_ERR_HIP;
+    const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count;
+    bool reset = gkey != w.geom_key;
+    if (w.tile_count.cap < 2 * (size_t)n_tiles || !w.tile_count.p) {
+        if (ensure(ctx, w.tile_count, 2 * (size_t)n_tiles)) return SHS_ERR_HIP;
+        reset = true;
+    }
+    if (w.busy.cap < (size_t)n_rt || !w.busy.p) {
+        if (ensure(ctx, w.busy, n_rt)) return SHS_ERR_HIP;
+        reset = true;
+    }
+    if (!w.counters.p) {
+        if (ensure(ctx, w.counters, 2 * shs_dev::LC_N)) return SHS_ERR_HIP;
+        reset = true;
+    }
+    if (reset) {
+        HIP_TRY(ctx, hipMemsetAsync(w.tile_count.p, 0, w.tile_count.cap * sizeof(uint32_t), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(w.busy.p, 0, w.busy.cap * sizeof(uint32_t), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(w.counters.p, 0, w.counters.cap * sizeof(uint32_t), ctx->stream));
+        w.geom_key = gkey;
+    }
+    if (ensure(ctx, w.bins, (size_t)n_tiles * w.bin_cap)) return SHS_ERR_HIP;
+    if (!w.spill.p && ensure(ctx, w.spill, 1 << 16)) return SHS_ERR_HIP;
+    const int setup_blocks = std::max(1, (n_tris + 255) / 256);
+    if (ensure(ctx, w.blk_stat, (size_t)setup_blocks)) return SHS_ERR_HIP;
+    if (upload_draws(ctx, w, w.last_draws)) return SHS_ERR_HIP;
+
+    fp.tiles_x = tiles_x; fp.tiles_y = tiles_y; fp.rtiles_y = rtiles_y;
+    fp.n_tris = n_tris;
+    fp.n_draws = (int)w.last_draws.size();
+    fp.bin_cap = w.bin_cap;
+    fp.spill_cap = (uint32_t)std::min<size_t>(w.spill.cap, 0xffffffffu);
+    fp.extra_cap = shadow ? 0u : w.extra_cap;
+    fp.parity = w.frame_index & 1u;
+    fp.scan_mode = n_tris <= SCAN_MAX_PRIMS ? 1u : 0u;
+    fp.setup_blocks = setup_blocks;
+    const int owned_bt = (n_tiles - fp.rank + fp.count - 1) / fp.count;
+    fp.n_owned_rt = owned_bt * (shs_dev::TILE / 8);
+    const int raster_grid = std::max(1, std::min(fp.n_owned_rt, 256 * 4));
+    if (ensure(ctx, w.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
+
+    LibBuffers fb;
+    std::memset(&fb, 0, sizeof fb);
+    fb.draws = w.draws.p; fb.recs = w.recs.p; fb.shade = w.shade.p; fb.boxes = w.boxes.p; fb.xbase = w.xbase.p;
+    fb.tile_count = w.tile_count.p; fb.bins = w.bins.p; fb.spill = w.spill.p; fb.counters = w.counters.p;
+    fb.busy = w.busy.p; fb.blk_stat = w.blk_stat.p; fb.rstat = w.rstat.p;
+    if (shadow) {
+        fb.depth = ctx->shadow_map.p;
+    } else {
+        fb.hdr = ctx->lib_hdr.p; fb.depth = ctx->lib_depth.p; fb.motion = ctx->lib_motion.p;
+        fb.shadow_map = ctx->have_shadow ? ctx->shadow_map.p : nullptr;
+    }
+    HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, ctx->stream));
+    HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, raster_grid, ctx->stream));
+    w.last_parity = fp.parity;
+    w.frame_index++;
+    w.last_setup_blocks = setup_blocks;
+    w.last_raster_grid = raster_grid;
+    w.last_n_tris = n_tris;
+    w.need_check = true;
+    w.done = true;
+    return SHS_OK;
+}
+
+uint32_t next_pow2(uint64_t v) {
+    uint32_t p = 1;
+    while (p < v && p < (1u << 30)) p <<= 1;
+    return p;
+}
+
+// Read one pass's counters and statistics; grows what overflowed and returns true then.
+int check_pass(shs_ctx *ctx, Work &w, bool &grew) {
+    grew = false;
+    if (!w.need_check) return SHS_OK;
+    uint32_t *c = ctx->h_lib_counters;
+    HIP_TRY(ctx, hipMemcpy(c, w.counters.p + w.last_parity * shs_dev::LC_N, shs_dev::LC_N * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost));
+    std::vector<uint2> bs(w.last_setup_blocks), rs(w.last_raster_grid);
+    HIP_TRY(ctx, hipMemcpy(bs.data(), w.blk_stat.p, bs.size() * sizeof(uint2), hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(rs.data(), w.rstat.p, rs.size() * sizeof(uint2), hipMemcpyDeviceToHost));
+    w.st_clip = w.st_raster = w.st_covered = w.st_maxbin = 0;
+    for (const uint2 &b : bs) { w.st_clip += b.x; w.st_raster += b.y; }
+    for (const uint2 &r : rs) { w.st_covered += r.x; w.st_maxbin = std::max<uint64_t>(w.st_maxbin, r.y); }
+    w.st_spill = c[shs_dev::LC_SPILL];
+    w.st_extra = c[shs_dev::LC_EXTRA];
+    if (w.st_maxbin > w.bin_cap) w.bin_cap = next_pow2(std::min<uint64_t>(w.st_maxbin, 1u << 24));
+    const uint32_t ov = c[shs_dev::LC_OVERFLOW];
+    if (ov & shs_dev::LOV_SPILL) {
+        const size_t need = c[shs_dev::LC_SPILL];
+        release(w.spill);
+        if (ensure(ctx, w.spill, need + need / 4 + 1024)) return SHS_ERR_HIP;
+        grew = true;
+    }
+    if (ov & shs_dev::LOV_EXTRA) {
+        w.extra_cap = (uint32_t)std::min<uint64_t>((uint64_t)c[shs_dev::LC_EXTRA] + c[shs_dev::LC_EXTRA] / 4 + 4096, 1u << 28);
+        grew = true;
+    }
+    w.need_check = false;
+    return SHS_OK;
+}
+
+// Wait for the enqueued passes; a pass that overflowed a capacity is re-issued (and a camera pass
+// that sampled a re-issued shadow map with it).
+int lib_finish(shs_ctx *ctx) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (int attempt = 0; attempt < 6; ++attempt) {
+        bool g_sh = false, g_cam = false;
+        if (check_pass(ctx, ctx->lib_shadow, g_sh) || check_pass(ctx, ctx->lib_cam, g_cam)) return SHS_ERR_HIP;
+        if (!g_sh && !g_cam) return SHS_OK;
+        if (g_sh && enqueue_pass(ctx, ctx->lib_shadow, true)) return SHS_ERR_HIP;
+        if ((g_cam || (g_sh && ctx->cam_after_shadow)) && ctx->lib_cam.done && enqueue_pass(ctx, ctx->lib_cam, false))
+            return SHS_ERR_HIP;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    ctx->err = "capacity overflow persisted";
+    return SHS_ERR_OVERFLOW;
+}
+
+int check_lib_mesh(shs_ctx *ctx, int32_t id) {
+    if (id < 0 || id >= (int)ctx->meshes.size() || !ctx->meshes[id].live || !ctx->meshes[id].lib) {
+        ctx->err = "bad mesh id (not a library mesh)";
+        return SHS_ERR_INVALID;
+    }
+    return SHS_OK;
+}
+
+}  // namespace
+
+void shs_lib_release(shs_ctx *ctx) {
+    release_work(ctx->lib_cam);
+    release_work(ctx->lib_shadow);
+    release(ctx->lib_hdr); release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
+    if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
+    ctx->h_lib_counters = nullptr;
+}
+
+extern "C" {
+
+int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const float *normals, int32_t n_normals,
+                    const float *uvs, int32_t n_uvs, const uint32_t *indices, int64_t n_indices, int32_t *mesh_id) {
+    if (!ctx || !positions || n_verts <= 0 || !mesh_id || n_normals < 0 || n_uvs < 0 || n_indices < 0 ||
+        (n_normals > 0 && !normals) || (n_uvs > 0 && !uvs) || (n_indices > 0 && !indices))
+        return SHS_ERR_INVALID;
+    const int64_t n_tris = indices ? n_indices / 3 : n_verts / 3;
+    if (n_tris > (1 << 27)) { ctx->err = "mesh too large"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    // read_v's defaults (rasterizer.hpp:196-202) materialised: normal (0,1,0), uv (0,0)
+    std::vector<float> nrm((size_t)n_verts * 3), uv((size_t)n_verts * 2, 0.0f);
+    for (int32_t i = 0; i < n_verts; ++i) {
+        const bool hn = i < n_normals;
+        nrm[3 * (size_t)i] = hn ? normals[3 * (size_t)i] : 0.0f;
+        nrm[3 * (size_t)i + 1] = hn ? normals[3 * (size_t)i + 1] : 1.0f;
+        nrm[3 * (size_t)i + 2] = hn ? normals[3 * (size_t)i + 2] : 0.0f;
+        if (i < n_uvs) { uv[2 * (size_t)i] = uvs[2 * (size_t)i]; uv[2 * (size_t)i + 1] = uvs[2 * (size_t)i + 1]; }
+    }
+    Mesh m;
+    m.lib = true;
+    m.n_verts = n_verts;
+    m.n_tris = (int32_t)n_tris;
+    // model-space bounds (PassShadowMap's mesh_bounds_cache, pass_shadow_map.hpp:90-102)
+    for (int k = 0; k < 3; ++k) { m.bmin[k] = 3.402823466e38f; m.bmax[k] = -3.402823466e38f; }
+    for (int32_t i = 0; i < n_verts; ++i)
+        for (int k = 0; k < 3; ++k) {
+            const float p = positions[3 * (size_t)i + k];
+            m.bmin[k] = (p < m.bmin[k]) ? p : m.bmin[k];   // glm::min(bmin, p)
+            m.bmax[k] = (m.bmax[k] < p) ? p : m.bmax[k];   // glm::max(bmax, p)
+        }
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.pos), (size_t)n_verts * 3 * sizeof(float)));
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.nrm), (size_t)n_verts * 3 * sizeof(float)));
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.uv), (size_t)n_verts * 2 * sizeof(float)));
+    HIP_TRY(ctx, hipMemcpy(m.pos, positions, (size_t)n_verts * 3 * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(m.nrm, nrm.data(), nrm.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(m.uv, uv.data(), uv.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (indices && n_indices >= 3) {
+        HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.idx), (size_t)n_tris * 3 * sizeof(uint32_t)));
+        HIP_TRY(ctx, hipMemcpy(m.idx, indices, (size_t)n_tris * 3 * sizeof(uint32_t), hipMemcpyHostToDevice));
+    } else if (indices) {
+        m.n_tris = 0;
+    }
+    m.live = true;
+    ctx->meshes.push_back(m);
+    *mesh_id = (int32_t)ctx->meshes.size() - 1;
+    return SHS_OK;
+}
+
+int shs_render_shadow_map(shs_ctx *ctx, int32_t w, int32_t h, const float sun_dir[3], const shs_shadow_caster *casters,
+                          int32_t n_casters, float light_viewproj_out[16]) {
+    if (!ctx || !sun_dir || w <= 0 || h <= 0 || w > 16384 || h > 16384 || n_casters < 0 || (n_casters > 0 && !casters))
+        return SHS_ERR_INVALID;
+    for (int i = 0; i < n_casters; ++i)
+        if (check_lib_mesh(ctx, casters[i].mesh_id)) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    if (!ctx->h_lib_counters && hipHostMalloc(reinterpret_cast<void **>(&ctx->h_lib_counters), shs_dev::LC_N * sizeof(uint32_t)) != hipSuccess)
+        return SHS_ERR_HIP;
+    using namespace shs_host;
+    // scene AABB of the casters (pass_shadow_map.hpp:80-131)
+    vec3 mn = {1e30f, 1e30f, 1e30f}, mx = {-1e30f, -1e30f, -1e30f};
+    auto expand = [&](vec3 p) {
+        mn = {(p.x < mn.x) ? p.x : mn.x, (p.y < mn.y) ? p.y : mn.y, (p.z < mn.z) ? p.z : mn.z};
+        mx = {(mx.x < p.x) ? p.x : mx.x, (mx.y < p.y) ? p.y : mx.y, (mx.z < p.z) ? p.z : mx.z};
+    };
+    bool any = false;
+    for (int i = 0; i < n_casters; ++i) {
+        const Mesh &m = ctx->meshes[casters[i].mesh_id];
+        const float *b0 = m.bmin, *b1 = m.bmax, *M = casters[i].model;
+        const vec3 c[8] = {{b0[0], b0[1], b0[2]}, {b1[0], b0[1], b0[2]}, {b0[0], b1[1], b0[2]}, {b1[0], b1[1], b0[2]},
+                           {b0[0], b0[1], b1[2]}, {b1[0], b0[1], b1[2]}, {b0[0], b1[1], b1[2]}, {b1[0], b1[1], b1[2]}};
+        for (const vec3 &p : c)
+            expand(vec3{(M[0] * p.x + M[4] * p.y) + (M[8] * p.z + M[12] * 1.0f), (M[1] * p.x + M[5] * p.y) + (M[9] * p.z + M[13] * 1.0f),
+                        (M[2] * p.x + M[6] * p.y) + (M[10] * p.z + M[14] * 1.0f)});
+        any = true;
+    }
+    if (!any) { expand(vec3{-1.0f, -1.0f, -1.0f}); expand(vec3{1.0f, 1.0f, 1.0f}); }
+    float view[16], proj[16];
+    dir_light_camera_aabb(vec3{sun_dir[0], sun_dir[1], sun_dir[2]}, mn, mx, 10.0f, (uint32_t)std::max(w, 1), view, proj,
+                          ctx->shadow_vp);
+    if (light_viewproj_out) std::memcpy(light_viewproj_out, ctx->shadow_vp, sizeof ctx->shadow_vp);
+
+    if (ensure(ctx, ctx->shadow_map, (size_t)w * h)) return SHS_ERR_HIP;
+    Work &wk = ctx->lib_shadow;
+    wk.last_draws.clear();
+    int32_t base = 0;
+    for (int i = 0; i < n_casters; ++i) {
+        const Mesh &m = ctx->meshes[casters[i].mesh_id];
+        LibDrawGPU d;
+        std::memset(&d, 0, sizeof d);
+        d.pos = m.pos; d.nrm = m.nrm; d.uv = m.uv; d.idx = m.idx;
+        d.n_verts = m.n_verts; d.tri_base = base; d.n_tris = m.n_tris;
+        std::memcpy(d.model, casters[i].model, sizeof d.model);
+        std::memcpy(d.viewproj, ctx->shadow_vp, sizeof d.viewproj);
+        wk.last_draws.push_back(d);
+        base += m.n_tris;
+    }
+    LibFrameParams fp;
+    std::memset(&fp, 0, sizeof fp);
+    fp.W = w; fp.H = h;
+    fp.rank = 0; fp.count = 1;   // every device renders the whole shadow map (sampled anywhere)
+    wk.last_fp = fp;
+    ctx->shadow_w = w;
+    ctx->shadow_h = h;
+    ctx->cam_after_shadow = false;
+    const int rc = enqueue_pass(ctx, wk, true);
+    if (rc) return rc;
+    ctx->have_shadow = true;
+    return SHS_OK;
+}
+
+int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_lib_draw *draws, int32_t n_draws) {
+    if (!ctx || !frame || n_draws < 0 || (n_draws > 0 && !draws)) return SHS_ERR_INVALID;
+    const shs_lib_frame &f = *frame;
+    if (f.width <= 0 || f.height <= 0 || f.width > 16384 || f.height > 16384) { ctx->err = "bad frame size"; return SHS_ERR_INVALID; }
+    if (f.shard_count <= 0 || f.shard_rank < 0 || f.shard_rank >= f.shard_count) { ctx->err = "bad shard"; return SHS_ERR_INVALID; }
+    for (int i = 0; i < n_draws; ++i) {
+        if (check_lib_mesh(ctx, draws[i].mesh_id)) return SHS_ERR_INVALID;
+        if (draws[i].program < SHS_PROGRAM_PBR_MR || draws[i].program > SHS_PROGRAM_DEBUG_DEPTH) { ctx->err = "bad program"; return SHS_ERR_INVALID; }
+        if (draws[i].cull_mode < SHS_CULL_NONE || draws[i].cull_mode > SHS_CULL_FRONT) { ctx->err = "bad cull mode"; return SHS_ERR_INVALID; }
+        if (draws[i].shadow && !ctx->have_shadow) { ctx->err = "draw samples a shadow map but none was rendered"; return SHS_ERR_INVALID; }
+    }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    if (!ctx->h_lib_counters && hipHostMalloc(reinterpret_cast<void **>(&ctx->h_lib_counters), shs_dev::LC_N * sizeof(uint32_t)) != hipSuccess)
+        return SHS_ERR_HIP;
+    const size_t npx = (size_t)f.width * f.height;
+    if (ensure(ctx, ctx->lib_hdr, npx)) return SHS_ERR_HIP;
+    const bool dm = (f.flags & SHS_LIB_DEPTH_MOTION) != 0;
+    if (dm && (ensure(ctx, ctx->lib_depth, npx) || ensure(ctx, ctx->lib_motion, npx))) return SHS_ERR_HIP;
+
+    Work &wk = ctx->lib_cam;
+    wk.last_draws.resize(n_draws);
+    int32_t base = 0;
+    for (int i = 0; i < n_draws; ++i) {
+        const Mesh &m = ctx->meshes[draws[i].mesh_id];
+        build_lib_draw(draws[i], m, base, wk.last_draws[i]);
+        base += m.n_tris;
+    }
+    LibFrameParams fp;
+    std::memset(&fp, 0, sizeof fp);
+    fp.W = f.width; fp.H = f.height;
+    fp.rank = f.shard_rank; fp.count = f.shard_count;
+    fp.flags = (f.flags & SHS_LIB_BG_GRADIENT) ? shs_dev::LF_GRADIENT : 0u;
+    if (dm) {
+        fp.flags |= shs_dev::LF_DEPTH | shs_dev::LF_MOTION;
+        if (f.zf > f.zn + 1e-6f) fp.flags |= shs_dev::LF_LINZ;   // rasterizer.hpp:354
+    }
+    fp.zn = f.zn; fp.zf = f.zf; fp.zspan = f.zf - f.zn;
+    for (int i = 0; i < 4; ++i) fp.clear[i] = f.clear_hdr[i];
+    fp.sm_w = ctx->shadow_w; fp.sm_h = ctx->shadow_h;
+    wk.last_fp = fp;
+    ctx->lib_frame = f;
+    ctx->cam_after_shadow = ctx->have_shadow;
+    const int rc = enqueue_pass(ctx, wk, false);
+    if (rc) return rc;
+    ctx->have_lib_frame = true;
+    return SHS_OK;
+}
+
+int shs_resolve_lib(shs_ctx *ctx, float *hdr, float *depth, float *motion) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (!ctx->have_lib_frame) { ctx->err = "no library frame rendered"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = lib_finish(ctx);
+    if (rc) return rc;
+    const size_t npx = (size_t)ctx->lib_frame.width * ctx->lib_frame.height;
+    const bool dm = (ctx->lib_frame.flags & SHS_LIB_DEPTH_MOTION) != 0;
+    if ((depth || motion) && !dm) { ctx->err = "frame has no depth_motion target"; return SHS_ERR_INVALID; }
+    if (hdr) HIP_TRY(ctx, hipMemcpy(hdr, ctx->lib_hdr.p, npx * sizeof(float4), hipMemcpyDeviceToHost));
+    if (depth) HIP_TRY(ctx, hipMemcpy(depth, ctx->lib_depth.p, npx * sizeof(float), hipMemcpyDeviceToHost));
+    if (motion) HIP_TRY(ctx, hipMemcpy(motion, ctx->lib_motion.p, npx * sizeof(float2), hipMemcpyDeviceToHost));
+    return SHS_OK;
+}
+
+int shs_resolve_shadow_map(shs_ctx *ctx, float *depth) {
+    if (!ctx || !depth) return SHS_ERR_INVALID;
+    if (!ctx->have_shadow) { ctx->err = "no shadow map rendered"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = lib_finish(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(depth, ctx->shadow_map.p, (size_t)ctx->shadow_w * ctx->shadow_h * sizeof(float), hipMemcpyDeviceToHost));
+    return SHS_OK;
+}
+
+int shs_get_lib_stats(shs_ctx *ctx, shs_lib_stats *st) {
+    if (!ctx || !st || !ctx->have_lib_frame) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = lib_finish(ctx);
+    if (rc) return rc;
+    const Work &w = ctx->lib_cam;
+    st->tri_input = (uint64_t)w.last_n_tris;
+    st->tri_after_clip = w.st_clip;
+    st->tri_raster = w.st_raster;
+    st->covered_pixels = w.st_covered;
+    st->max_tile_bin = w.st_maxbin;
+    st->spilled = w.st_spill;
+    st->clipped_extra = w.st_extra;
+    return SHS_OK;
+}
+
+int shs_lib_device_targets(shs_ctx *ctx, void **hdr_dev, void **depth_dev, void **motion_dev) {
+    if (!ctx || !ctx->have_lib_frame) return SHS_ERR_INVALID;
+    if (hdr_dev) *hdr_dev = ctx->lib_hdr.p;
+    if (depth_dev) *depth_dev = ctx->lib_depth.p;
+    if (motion_dev) *motion_dev = ctx->lib_motion.p;
+    return SHS_OK;
+}
+
+int shs_look_at_lh(const float eye[3], const float center[3], const float up[3], float out16[16]) {
+    if (!eye || !center || !up || !out16) return SHS_ERR_INVALID;
+    shs_host::look_at_lh({eye[0], eye[1], eye[2]}, {center[0], center[1], center[2]}, {up[0], up[1], up[2]}, out16);
+    return SHS_OK;
+}
+
+int shs_perspective_lh_no(float fovy, float aspect, float zn, float zf, float out16[16]) {
+    if (!out16) return SHS_ERR_INVALID;
+    shs_host::perspective_lh_no(fovy, aspect, zn, zf, out16);
+    return SHS_OK;
+}
+
+int shs_model_euler(const float pos[3], const float rot[3], const float scl[3], float out16[16]) {
+    if (!pos || !rot || !scl || !out16) return SHS_ERR_INVALID;
+    shs_host::model_euler({pos[0], pos[1], pos[2]}, {rot[0], rot[1], rot[2]}, {scl[0], scl[1], scl[2]}, out16);
+    return SHS_OK;
+}
+
+int shs_dir_light_camera_aabb(const float sun_dir[3], const float mn[3], const float mx[3], float margin, uint32_t res,
+                              float view16[16], float proj16[16], float viewproj16[16]) {
+    if (!sun_dir || !mn || !mx || !view16 || !proj16 || !viewproj16) return SHS_ERR_INVALID;
+    shs_host::dir_light_camera_aabb({sun_dir[0], sun_dir[1], sun_dir[2]}, {mn[0], mn[1], mn[2]}, {mx[0], mx[1], mx[2]}, margin,
+                                    res, view16, proj16, viewproj16);
+    return SHS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,170 @@
+// shs_ctx.hpp -- the libshs_gpu context (struct shs_ctx) shared by the ABI translation units
+// (shs_abi.cpp: legacy path; shs_abi_lib.cpp: library path).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/shs_gpu.h"
+#include "shs_device.hpp"
+#include "shs_lib_device.hpp"
+
+namespace shs_host_detail {
+struct Mesh {
+    float *pos = nullptr;            // legacy soup: 9 floats per triangle; library mesh: 3 per vertex
+    float *nrm = nullptr;
+    int32_t n_tris = 0;
+    bool live = false;
+    // library MeshData (resources/mesh.hpp:23-43): uvs, indices (nullptr: soup), model-space bounds
+    bool lib = false;
+    float *uv = nullptr;
+    uint32_t *idx = nullptr;
+    int32_t n_verts = 0;
+    float bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
+};
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;  // elements
+};
+}  // namespace shs_host_detail
+using shs_host_detail::Mesh;
+using shs_host_detail::DevBuf;
+
+struct shs_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::vector<Mesh> meshes;
+
+    DevBuf<shs_dev::DrawGPU> draws;
+    DevBuf<shs_dev::TriRec> recs;
+    DevBuf<shs_dev::ShadeRec> shade;
+    DevBuf<uint32_t> tile_count;     // 2 parity sets of per-bin-tile counts
+    DevBuf<uint32_t> bins;           // n_tiles * bin_cap
+    DevBuf<uint2> spill;
+    DevBuf<shs_dev::GhostFrag> frags; // ghost fragments
+    DevBuf<uint2> boxes;             // per-triangle bin boxes
+    DevBuf<uint32_t> counters;       // 2 parity sets
+    DevBuf<uint32_t> busy;           // per raster tile
+    DevBuf<uint4> blk_stat;          // per setup block
+    DevBuf<uint2> rstat;             // per raster block
+    DevBuf<uint64_t> timeline;       // SHS_OPT_TIMELINE
+    bool want_timeline = false;
+    int last_setup_grid = 0, last_ghost_blocks = 0, last_clear_blocks = 0;
+    std::vector<uint4> h_blk_stat;
+    std::vector<uint2> h_rstat;
+    uint64_t geom_key = ~0ull;       // (tiles, shard) of the last frame: a change resets the counts
+    int last_setup_blocks = 0, last_raster_grid = 0;
+    uint64_t last_covered = 0, last_bins = 0, last_maxbin = 0, last_setup = 0, last_ghost = 0, last_unb = 0;
+    uint32_t bin_cap = 256;
+    int force_mode = 0;              // 0 auto, 1 scan, 2 bin (SHS_OPT_RASTER_MODE)
+    uint32_t frame_index = 0;        // parity of the counter set
+    uint32_t last_parity = 0;
+    DevBuf<uint8_t> color;
+    DevBuf<float> depth;
+    DevBuf<float4> prequant;
+
+    // pinned staging for the per-frame draw table (2 slots, guarded by events)
+    shs_dev::DrawGPU *h_draws[2] = {nullptr, nullptr};
+    size_t h_cap = 0;
+    hipEvent_t slot_ev[2] = {nullptr, nullptr};
+    bool slot_used[2] = {false, false};
+    int slot = 0;
+    uint32_t *h_counters = nullptr;  // pinned, C_NCOUNTERS
+
+    // last frame (re-issued if a bin capacity overflowed)
+    shs_frame_desc frame{};
+    std::vector<shs_legacy_draw> last_draws;
+    bool have_frame = false;
+    bool need_check = false;
+    int last_n_tris = 0;
+    int last_n_tiles = 0;
+
+    bool timing = false;
+    hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    float last_ms[4] = {0, 0, 0, 0};
+    // ring of per-frame kernel events, harvested lazily: sums of kernel durations over many frames
+    static constexpr int RING = 64;
+    hipEvent_t ring_ev[RING][5] = {};
+    bool ring_pending[RING] = {};
+    int ring_next = 0;
+    double acc_ms[4] = {0, 0, 0, 0};
+    int64_t acc_frames = 0;
+
+    // ---- library path (shs_abi_lib.cpp): one workspace per pass ----
+    struct LibWork {
+        DevBuf<shs_dev::LibDrawGPU> draws;
+        DevBuf<shs_dev::LibRec> recs;
+        DevBuf<shs_dev::LibShade> shade;
+        DevBuf<uint2> boxes;
+        DevBuf<uint32_t> xbase, tile_count, bins, counters, busy;
+        DevBuf<uint2> spill, blk_stat, rstat;
+        shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots
+        size_t h_cap = 0;
+        hipEvent_t slot_ev[2] = {nullptr, nullptr};
+        bool slot_used[2] = {false, false};
+        int slot = 0;
+        uint64_t geom_key = ~0ull;
+        uint32_t bin_cap = 256, extra_cap = 0, frame_index = 0, last_parity = 0;
+        int last_setup_blocks = 0, last_raster_grid = 0, last_n_tris = 0;
+        bool need_check = false, done = false;
+        uint64_t st_clip = 0, st_raster = 0, st_covered = 0, st_maxbin = 0, st_spill = 0, st_extra = 0;
+        std::vector<shs_dev::LibDrawGPU> last_draws;   // host copies (re-issue on overflow)
+        shs_dev::LibFrameParams last_fp{};
+    };
+    LibWork lib_cam, lib_shadow;
+    DevBuf<float4> lib_hdr;
+    DevBuf<float> lib_depth;
+    DevBuf<float2> lib_motion;
+    DevBuf<float> shadow_map;
+    int shadow_w = 0, shadow_h = 0;
+    float shadow_vp[16] = {};
+    shs_lib_frame lib_frame{};
+    bool have_lib_frame = false, have_shadow = false, cam_after_shadow = false;
+    uint32_t *h_lib_counters = nullptr;   // pinned, LC_N
+};
+
+#define HIP_TRY(ctx, expr)                                                                       \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) {                                                                  \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                      \
+            return SHS_ERR_HIP;                                                                  \
+        }                                                                                        \
+    } while (0)
+
+template <typename T>
+inline int ensure(shs_ctx *ctx, DevBuf<T> &b, size_t n) {
+    if (n <= b.cap && b.p) return SHS_OK;
+    size_t want = std::max<size_t>(n, 16);
+    if (b.p) {
+        // the old buffer may still be read by queued work on the stream
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&b.p), want * sizeof(T)));
+    b.cap = want;
+    return SHS_OK;
+}
+
+template <typename T>
+inline void release(DevBuf<T> &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+}
+
+inline int set_dev(shs_ctx *ctx) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return SHS_OK;
+}
+
+// Frees the library-path workspaces (shs_abi_lib.cpp); called by shs_destroy.
+void shs_lib_release(shs_ctx *ctx);

@@ -7,6 +7,7 @@
 // Matrices are column-major float[16]: m[c*4 + r] == glm::mat4[c][r].
 #pragma once
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 
 namespace shs_host {
@@ -172,6 +173,124 @@ inline void camera3d(vec3 position, float horizontal_angle, float vertical_angle
     const vec3 up = gnormalize(gcross(dir, right));
     perspective_lh_no(gradians(fov), 4.0f / 3.0f, zn, zf, proj);
     look_at_lh(position, gadd(position, dir), up, view);
+}
+
+// ---- library-path helpers (shs-renderer-lib) ---------------------------------------------
+// glm::determinant(mat3) (func_matrix.inl compute_determinant<3,3>), m column-major [9]
+inline float det3(const float *m) {
+    auto M = [&](int c, int r) { return m[c * 3 + r]; };
+    return (M(0, 0) * (M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2)) - M(1, 0) * (M(0, 1) * M(2, 2) - M(2, 1) * M(0, 2))) +
+           M(2, 0) * (M(0, 1) * M(1, 2) - M(1, 1) * M(0, 2));
+}
+
+// glm::inverse(mat3) (func_matrix.inl compute_inverse<3,3>)
+inline void inverse3(const float *m, float *o) {
+    auto M = [&](int c, int r) { return m[c * 3 + r]; };
+    const float one_over = 1.0f / det3(m);
+    o[0] = +(M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2)) * one_over;
+    o[3] = -(M(1, 0) * M(2, 2) - M(2, 0) * M(1, 2)) * one_over;
+    o[6] = +(M(1, 0) * M(2, 1) - M(2, 0) * M(1, 1)) * one_over;
+    o[1] = -(M(0, 1) * M(2, 2) - M(2, 1) * M(0, 2)) * one_over;
+    o[4] = +(M(0, 0) * M(2, 2) - M(2, 0) * M(0, 2)) * one_over;
+    o[7] = -(M(0, 0) * M(2, 1) - M(2, 0) * M(0, 1)) * one_over;
+    o[2] = +(M(0, 1) * M(1, 2) - M(1, 1) * M(0, 2)) * one_over;
+    o[5] = -(M(0, 0) * M(1, 2) - M(1, 0) * M(0, 2)) * one_over;
+    o[8] = +(M(0, 0) * M(1, 1) - M(1, 0) * M(0, 1)) * one_over;
+}
+
+// glm::determinant(mat4) (func_matrix.inl compute_determinant<4,4>)
+inline float det4(const float *mm) {
+    auto M = [&](int c, int r) { return mm[c * 4 + r]; };
+    const float s00 = M(2, 2) * M(3, 3) - M(3, 2) * M(2, 3);
+    const float s01 = M(2, 1) * M(3, 3) - M(3, 1) * M(2, 3);
+    const float s02 = M(2, 1) * M(3, 2) - M(3, 1) * M(2, 2);
+    const float s03 = M(2, 0) * M(3, 3) - M(3, 0) * M(2, 3);
+    const float s04 = M(2, 0) * M(3, 2) - M(3, 0) * M(2, 2);
+    const float s05 = M(2, 0) * M(3, 1) - M(3, 0) * M(2, 1);
+    const float c0 = +((M(1, 1) * s00 - M(1, 2) * s01) + M(1, 3) * s02);
+    const float c1 = -((M(1, 0) * s00 - M(1, 2) * s03) + M(1, 3) * s04);
+    const float c2 = +((M(1, 0) * s01 - M(1, 1) * s03) + M(1, 3) * s05);
+    const float c3 = -((M(1, 0) * s02 - M(1, 1) * s04) + M(1, 2) * s05);
+    return ((M(0, 0) * c0 + M(0, 1) * c1) + M(0, 2) * c2) + M(0, 3) * c3;
+}
+
+// make_default_vertex_out's normal matrix (builtin_shaders.hpp:93-95): mat3(model), replaced by
+// transpose(inverse(.)) when |det| > 1e-8; n3 column-major [9]
+inline void lib_normal_matrix(const float *model, float *n3) {
+    float m3[9];
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) m3[c * 3 + r] = model[c * 4 + r];
+    if (std::fabs(det3(m3)) > 1e-8f) {
+        float inv[9];
+        inverse3(m3, inv);
+        for (int c = 0; c < 3; ++c)
+            for (int r = 0; r < 3; ++r) n3[c * 3 + r] = inv[r * 3 + c];
+    } else {
+        std::memcpy(n3, m3, sizeof m3);
+    }
+}
+
+// glm::orthoLH_NO (matrix_clip_space.inl)
+inline void ortho_lh_no(float l, float r, float b, float t, float zn, float zf, float *m) {
+    identity(m);
+    m[0] = 2.0f / (r - l);
+    m[5] = 2.0f / (t - b);
+    m[12] = -(r + l) / (r - l);
+    m[13] = -(t + b) / (t - b);
+    m[10] = 2.0f / (zf - zn);
+    m[14] = -(zf + zn) / (zf - zn);
+}
+
+// RenderItem model matrix (pass_pbr_forward.hpp:136-141, pass_shadow_map.hpp:56-64):
+// translate * rotate(x) * rotate(y) * rotate(z) * scale, each applied to the running matrix
+inline void model_euler(vec3 pos, vec3 rot, vec3 scl, float *out) {
+    float m[16], t[16];
+    identity(m);
+    translate(m, pos, t); std::memcpy(m, t, sizeof m);
+    rotate(m, rot.x, vec3{1.0f, 0.0f, 0.0f}, t); std::memcpy(m, t, sizeof m);
+    rotate(m, rot.y, vec3{0.0f, 1.0f, 0.0f}, t); std::memcpy(m, t, sizeof m);
+    rotate(m, rot.z, vec3{0.0f, 0.0f, 1.0f}, t); std::memcpy(m, t, sizeof m);
+    scale(m, scl, out);
+}
+
+// build_dir_light_camera_aabb (camera/light_camera.hpp:33-98)
+inline void dir_light_camera_aabb(vec3 sun_dir, vec3 mn, vec3 mx, float margin, uint32_t res, float *view, float *proj,
+                                  float *viewproj) {
+    auto smin = [](float a, float b) { return (b < a) ? b : a; };   // std::min
+    auto smax = [](float a, float b) { return (a < b) ? b : a; };   // std::max
+    const vec3 dir = gnormalize(sun_dir);
+    const vec3 up = (std::fabs(dir.y) > 0.95f) ? vec3{0.0f, 0.0f, 1.0f} : vec3{0.0f, 1.0f, 0.0f};
+    const vec3 c = gscale(gadd(mn, mx), 0.5f);
+    const vec3 ext = gscale(gsub(mx, mn), 0.5f);
+    const float scene_radius = std::sqrt(gdot(ext, ext)) + margin;
+    const vec3 pos = gsub(c, gscale(dir, scene_radius * 2.0f));
+    look_at_lh(pos, c, up, view);
+    const vec3 corners[8] = {{mn.x, mn.y, mn.z}, {mx.x, mn.y, mn.z}, {mn.x, mx.y, mn.z}, {mx.x, mx.y, mn.z},
+                             {mn.x, mn.y, mx.z}, {mx.x, mn.y, mx.z}, {mn.x, mx.y, mx.z}, {mx.x, mx.y, mx.z}};
+    float l = 1e30f, r = -1e30f, b = 1e30f, t = -1e30f, n = 1e30f, f = -1e30f;
+    for (const vec3 &p : corners) {
+        // view * vec4(p, 1): (m0*x + m1*y) + (m2*z + m3*1)
+        const float px = (view[0] * p.x + view[4] * p.y) + (view[8] * p.z + view[12] * 1.0f);
+        const float py = (view[1] * p.x + view[5] * p.y) + (view[9] * p.z + view[13] * 1.0f);
+        const float pz = (view[2] * p.x + view[6] * p.y) + (view[10] * p.z + view[14] * 1.0f);
+        l = smin(l, px); r = smax(r, px);
+        b = smin(b, py); t = smax(t, py);
+        n = smin(n, pz); f = smax(f, pz);
+    }
+    l -= margin; r += margin; b -= margin; t += margin;
+    n -= margin; f += margin;
+    if (res > 0u) {
+        const float span_x = smax(r - l, 1e-5f), span_y = smax(t - b, 1e-5f);
+        const float inv_res = 1.0f / static_cast<float>(res);
+        const float texel_x = span_x * inv_res, texel_y = span_y * inv_res;
+        float cx = 0.5f * (l + r), cy = 0.5f * (b + t);
+        if (texel_x > 1e-6f) cx = std::floor(cx / texel_x + 0.5f) * texel_x;
+        if (texel_y > 1e-6f) cy = std::floor(cy / texel_y + 0.5f) * texel_y;
+        const float hx = 0.5f * span_x, hy = 0.5f * span_y;
+        l = cx - hx; r = cx + hx; b = cy - hy; t = cy + hy;
+    }
+    ortho_lh_no(l, r, b, t, n, f, proj);
+    mul(proj, view, viewproj);
 }
 
 // MonkeyObject::get_world_matrix (blinn_phong_shading.cpp:122-128): T * R * S

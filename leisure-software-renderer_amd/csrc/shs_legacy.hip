@@ -34,6 +34,7 @@
 
 #include "shs_device.hpp"
 #include "shs_internal.hpp"
+#include "shs_wave.hpp"
 
 namespace shs_dev {
 
@@ -234,54 +235,6 @@ __device__ __forceinline__ TriRec quad_make_rec(const FrameParams &fp, const Dra
 #pragma unroll
     for (int k = 0; k < 3; ++k) { sx[k] = quad_bcast(vx, k); sy[k] = quad_bcast(vy, k); sz[k] = quad_bcast(vz, k); }
     return rec_from_screen(fp, draw, local, sx, sy, sz);
-}
-
-// ---- wave helpers -----------------------------------------------------------------------------
-// LDS hand-off between lanes of ONE wave: the wave's LDS operations execute in order, so only the
-// compiler must be kept from reordering (no s_barrier: waves of a ghost block diverge).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_wave_barrier();
-    __asm__ volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-    return (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
-}
-
-// Wave-aggregated appends to NK per-key counters (call with the whole wave converged).  Lanes with
-// key[k] >= 0 get a unique slot of counter[key[k]]; each distinct key costs ONE returning atomic, and
-// all of them are issued before any return value is consumed (one memory round trip in total).
-template <int NK>
-__device__ __forceinline__ void wave_append(uint32_t *counter, const int (&key)[NK], uint32_t (&slot)[NK]) {
-    const int lane = __lane_id();
-    uint32_t add[NK], rank[NK], leader[NK], ret[NK];
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-        add[k] = 0u; rank[k] = 0u; leader[k] = 0u;
-        uint64_t pending = __ballot(key[k] >= 0);
-        while (pending) {
-            const int first = __ffsll((unsigned long long)pending) - 1;
-            const int lk = __shfl(key[k], first);
-            const uint64_t peers = __ballot(key[k] == lk) & pending;
-            if (lane == first) add[k] = (uint32_t)__popcll(peers);
-            if ((peers >> lane) & 1ull) { leader[k] = (uint32_t)first; rank[k] = lanes_below(peers); }
-            pending &= ~peers;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < NK; ++k) ret[k] = add[k] ? atomicAdd(&counter[key[k]], add[k]) : 0u;
-#pragma unroll
-    for (int k = 0; k < NK; ++k) slot[k] = __shfl(ret[k], (int)leader[k]) + rank[k];
-}
-
-// Single-counter wave append (converged wave): slot for lanes with want.
-__device__ __forceinline__ uint32_t wave_append1(uint32_t *counter, bool want) {
-    const uint64_t m = __ballot(want);
-    if (!m) return 0u;
-    const int first = __ffsll((unsigned long long)m) - 1;
-    uint32_t base = 0u;
-    if (__lane_id() == first) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    return __shfl(base, first) + lanes_below(m);
 }
 
 // Index of the draw owning triangle gid, and whether the whole wave shares it (then the draw's
@@ -766,19 +719,8 @@ __device__ __forceinline__ void shade_winner(const float4 *du, const ShadeRec &s
     pre[2] = g_clamp01(s * oc.z) * 255.0f;
 }
 
-// Order-preserving key of the z test: the reference's in-order strict-less test keeps, per pixel, the
-// lexicographic minimum of (z, submission index) (the first triangle with the minimal z wins), so
-// a 64-bit key (orderable z bits << 32 | index) resolved by atomic min in LDS is exact and
-// independent of the order candidates are processed in.  -0 and +0 compare equal in the
-// reference, so -0 maps to +0's key; NaN and z >= FLT_MAX never pass (never written).
-constexpr unsigned long long KEY_EMPTY = ~0ull;
-
-__device__ __forceinline__ unsigned long long z_key(float z, uint32_t id) {
-    uint32_t b = __float_as_uint(z);
-    b = (b << 1) == 0u ? 0u : b;                                 // -0 -> +0
-    const uint32_t ord = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-    return ((unsigned long long)ord << 32) | id;
-}
+// The z test (ZBuffer::test_and_set_depth, strict '<' in submission order) resolves through z_key
+// (shs_wave.hpp); NaN and z >= FLT_MAX never pass (never written).
 
 // One (triangle, pixel) test: the pixel is in the reference's visited set for this triangle
 // (inside the ibox, or for a bounded ghost where its tile job's clamped rectangle covers it) and

@@ -1,0 +1,810 @@
+// shs_lib.hip -- gfx950 kernels for the shs-renderer-lib software raster path.
+//
+// Replaces rasterize_mesh (sw_render/rasterizer.hpp:181-442) with the builtin PBR / Blinn-Phong /
+// debug programs (shader/builtin_shaders.hpp:25-245) as PassPBRForward runs it
+// (passes/pass_pbr_forward.hpp:49-214), and the depth pass of PassShadowMap
+// (passes/pass_shadow_map.hpp:144-204).  Paths are relative to
+// /root/reference/cpp-folders/src/shs-renderer-lib/include/shs/.
+//
+// Two launches per pass on one HIP stream:
+//   k_lib_setup   one thread per input triangle: VS x3, trivial accept or Sutherland-Hodgman against
+//                 the six clip planes, fan triangulation, NDC -> screen (rows y-up), area / cull /
+//                 bbox rejects, the per-primitive half of barycentric_2d and the 1/w terms (a 64-B
+//                 record + 112-B premultiplied varyings per primitive), "busy" marks on the 32x8
+//                 raster tiles of its bbox and, for large scenes, per-32x32-tile bin appends.
+//   k_lib_raster  persistent over the owned raster tiles: busy tiles stage their candidates'
+//                 records in LDS and deal every (primitive, pixel) pair to one lane; each passing
+//                 pair atomic-mins a 64-bit key (z01 bits, submission order) into LDS -- identical
+//                 to the reference's in-order strict-less test on a cleared buffer; the winner of
+//                 every pixel is shaded once and the tile's HDR colour, depth and motion are written
+//                 as whole row segments.  Idle tiles are written with the pass's clear values, so
+//                 every output byte is written exactly once per pass.
+// Primitive order: input triangle t's fan triangle k has submission index t*16 + k (a clipped
+// triangle yields at most 7 fans in exact arithmetic, MAX_POLY - 2 with rounding); fan 0 lives in
+// slot t, fans >= 1 in extra slots from xbase[t].
+#include <float.h>
+
+#include <algorithm>
+
+#include "shs_device.hpp"
+#include "shs_lib_device.hpp"
+#include "shs_lib_internal.hpp"
+#include "shs_wave.hpp"
+
+namespace shs_dev {
+
+constexpr float PI_F = 3.14159265358979323846264338327950288f;   // glm::pi<float>()
+
+// ---- std:: scalar semantics used by the builtin programs -------------------------------------
+__device__ __forceinline__ float s_max(float a, float b) { return (a < b) ? b : a; }        // std::max
+__device__ __forceinline__ float s_min(float a, float b) { return (b < a) ? b : a; }        // std::min
+__device__ __forceinline__ float s_clamp(float v, float lo, float hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
+__device__ __forceinline__ int s_clampi(int v, int lo, int hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
+__device__ __forceinline__ float g_clamp(float x, float lo, float hi) { return g_min(g_max(x, lo), hi); }  // glm::clamp
+__device__ __forceinline__ float g_mix(float x, float y, float a) { return x * (1.0f - a) + y * a; }      // glm::mix
+__device__ __forceinline__ f3 mix3(f3 a, f3 b, float t) { return {g_mix(a.x, b.x, t), g_mix(a.y, b.y, t), g_mix(a.z, b.z, t)}; }
+__device__ __forceinline__ f3 mul3(f3 a, f3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ f3 gmax3(f3 a, f3 b) { return {g_max(a.x, b.x), g_max(a.y, b.y), g_max(a.z, b.z)}; }
+__device__ __forceinline__ f3 neg3(f3 a) { return {-a.x, -a.y, -a.z}; }
+
+struct f4 { float x, y, z, w; };
+// glm mat4 * vec4: (m0*x + m1*y) + (m2*z + m3*w)
+__device__ __forceinline__ f4 m4v(const float *m, f4 v) {
+    return {(m[0] * v.x + m[4] * v.y) + (m[8] * v.z + m[12] * v.w), (m[1] * v.x + m[5] * v.y) + (m[9] * v.z + m[13] * v.w),
+            (m[2] * v.x + m[6] * v.y) + (m[10] * v.z + m[14] * v.w), (m[3] * v.x + m[7] * v.y) + (m[11] * v.z + m[15] * v.w)};
+}
+
+constexpr int LIB_RTW = 32, LIB_RTH = 8;   // raster tile (one 256-thread workgroup, one pixel per lane)
+constexpr int LIB_CAND = 1024;             // candidate ids gathered per round
+constexpr int LIB_CHUNK = 128;             // records staged in LDS per pass
+constexpr int MAX_POLY = 16;               // clipped polygon capacity (3 + 6 planes x up to 2 crossings)
+
+__device__ __forceinline__ bool lib_owned(const LibFrameParams &fp, int bx, int by) {
+    return ((by * fp.tiles_x + bx) % fp.count) == fp.rank;
+}
+
+// ---- k_lib_setup ------------------------------------------------------------------------------
+
+// A clip-space vertex with the varyings the builtin VS sets (make_default_vertex_out,
+// builtin_shaders.hpp:87-103): WorldPos, NormalWS, UV0 (Color0 is never read by the programs).
+struct LVert {
+    float cx, cy, cz, cw;
+    float wx, wy, wz;
+    float nx, ny, nz;
+    float u, v;
+};
+
+__device__ __forceinline__ LVert vertex_out(const LibDrawGPU &dr, uint32_t id) {
+    const float *P = dr.pos + 3 * (size_t)id, *N = dr.nrm + 3 * (size_t)id, *U = dr.uv + 2 * (size_t)id;
+    LVert o;
+    const f4 wp = m4v(dr.model, f4{P[0], P[1], P[2], 1.0f});
+    const f4 c = m4v(dr.viewproj, wp);
+    const f3 n = normalize3(m3v(dr.nmat, f3{N[0], N[1], N[2]}));
+    o.cx = c.x; o.cy = c.y; o.cz = c.z; o.cw = c.w;
+    o.wx = wp.x; o.wy = wp.y; o.wz = wp.z;
+    o.nx = n.x; o.ny = n.y; o.nz = n.z;
+    o.u = U[0]; o.v = U[1];
+    return o;
+}
+
+__device__ __forceinline__ bool fully_inside(const LVert &v) {   // rasterizer.hpp:232-240
+    if (!(v.cw > 0.0f)) return false;
+    return (v.cx >= -v.cw && v.cx <= v.cw) && (v.cy >= -v.cw && v.cy <= v.cw) && (v.cz >= -v.cw && v.cz <= v.cw);
+}
+
+// detail::lerp_rv on the varyings the FS reads (rasterizer.hpp:69-79): every component glm::mix'ed
+// (the NormalWS varying is NOT renormalised -- only the unused RasterVertex::normal_ws is).
+__device__ __forceinline__ LVert lerp_v(const LVert &a, const LVert &b, float t) {
+    LVert o;
+    const float *pa = &a.cx, *pb = &b.cx;
+    float *po = &o.cx;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) po[i] = g_mix(pa[i], pb[i], t);
+    return o;
+}
+
+__device__ __forceinline__ float plane_dist(const LVert &v, int p) {   // plane_dist_left .. far (:81-109)
+    switch (p) {
+        case 0: return v.cx + v.cw;
+        case 1: return v.cw - v.cx;
+        case 2: return v.cy + v.cw;
+        case 3: return v.cw - v.cy;
+        case 4: return v.cz + v.cw;
+        default: return v.cw - v.cz;
+    }
+}
+
+// detail::clip_polygon_frustum (:111-164) for the rare triangles that are not trivially inside.
+// Returns the polygon size (<= MAX_POLY); out holds the result.
+__device__ __noinline__ int clip_frustum(const LVert (&tri)[3], LVert (&out)[MAX_POLY]) {
+    LVert buf[2][MAX_POLY];
+    int n = 3;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) buf[0][k] = tri[k];
+    int cur = 0;
+    for (int p = 0; p < 6 && n > 0; ++p) {
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            const LVert &c = buf[cur][i], &x = buf[cur][(i + 1) % n];
+            const float da = plane_dist(c, p), db = plane_dist(x, p);
+            const bool cin = da >= 0.0f, xin = db >= 0.0f;
+            if (m > MAX_POLY - 2) break;   // unreachable for a convex polygon (<= 1 vertex added per plane)
+            if (cin && xin) {
+                buf[cur ^ 1][m++] = x;
+            } else if (cin && !xin) {
+                const float denom = da - db;
+                if (fabsf(denom) > 1e-8f) buf[cur ^ 1][m++] = lerp_v(c, x, da / denom);
+            } else if (!cin && xin) {
+                const float denom = da - db;
+                if (fabsf(denom) > 1e-8f) buf[cur ^ 1][m++] = lerp_v(c, x, da / denom);
+                buf[cur ^ 1][m++] = x;
+            }
+        }
+        n = m;
+        cur ^= 1;
+    }
+    for (int i = 0; i < n; ++i) out[i] = buf[cur][i];
+    return n;
+}
+
+__device__ __forceinline__ void lib_append_bin(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int t,
+                                               uint32_t pos, uint32_t id) {
+    if (pos < fp.bin_cap) {
+        fb.bins[(size_t)t * fp.bin_cap + pos] = id;
+    } else {
+        const uint32_t sp = atomicAdd(&cnt[LC_SPILL], 1u);
+        if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t, id);
+        else atomicOr(&cnt[LC_OVERFLOW], LOV_SPILL);
+    }
+}
+
+// Busy marks on the owned raster tiles of [x0,x1] x [y0,y1] and (bin mode) per-bin-tile appends.
+__device__ void lib_mark(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
+                         uint32_t slot) {
+    const bool sharded = fp.count > 1;
+    for (int ry = y0 / LIB_RTH; ry <= y1 / LIB_RTH; ++ry)
+        for (int rx = x0 / LIB_RTW; rx <= x1 / LIB_RTW; ++rx)
+            if (!sharded || lib_owned(fp, rx, ry / (TILE / LIB_RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+    if (fp.scan_mode) return;
+    uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
+    for (int by = y0 / TILE; by <= y1 / TILE; ++by)
+        for (int bx = x0 / TILE; bx <= x1 / TILE; ++bx) {
+            if (sharded && !lib_owned(fp, bx, by)) continue;
+            const int t = by * fp.tiles_x + bx;
+            lib_append_bin(fp, fb, cnt, t, atomicAdd(&tcount[t], 1u), slot);
+        }
+}
+
+__device__ __forceinline__ void store_box(const LibBuffers &fb, uint32_t slot, int x0, int x1, int y0, int y1) {
+    fb.boxes[slot] = make_uint2(pack16(x0, x1), pack16(y0, y1));
+}
+
+// One fan triangle of rasterize_mesh (rasterizer.hpp:255-328): NDC, screen (y-up), the area /
+// cull / bbox rejects; writes the primitive's record, varyings and box into slot.  Counts
+// tri_after_clip / tri_raster like the reference.
+__device__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, const LibDrawGPU &dr, int d,
+                         uint32_t seq, uint32_t slot, const LVert &a, const LVert &b, const LVert &c, uint32_t &n_clip,
+                         uint32_t &n_rast) {
+    ++n_clip;
+    const LVert *v[3] = {&a, &b, &c};
+    float sx[3], sy[3];
+    bool finite = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float nx = v[k]->cx / v[k]->cw, ny = v[k]->cy / v[k]->cw, nz = v[k]->cz / v[k]->cw;
+        finite = finite && isfinite(nx) && isfinite(ny) && isfinite(nz);
+        sx[k] = (nx * 0.5f + 0.5f) * (float)(fp.W - 1);
+        sy[k] = (ny * 0.5f + 0.5f) * (float)(fp.H - 1);
+    }
+    int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+    bool live = false;
+    float den = 0.0f;
+    if (finite) {
+        const float e0x = sx[1] - sx[0], e0y = sy[1] - sy[0], e1x = sx[2] - sx[0], e1y = sy[2] - sy[0];
+        const float area2 = e0x * e1y - e0y * e1x;
+        const bool is_front = (area2 > 0.0f) == (dr.front_ccw != 0);
+        const bool culled = (dr.cull_mode == 1 && !is_front) || (dr.cull_mode == 2 && is_front);
+        if (!(fabsf(area2) < 1e-10f) && !culled) {
+            x0 = max(0, (int)floorf(s_min(s_min(sx[0], sx[1]), sx[2])));
+            x1 = min(fp.W - 1, (int)ceilf(s_max(s_max(sx[0], sx[1]), sx[2])));
+            y0 = max(0, (int)floorf(s_min(s_min(sy[0], sy[1]), sy[2])));
+            y1 = min(fp.H - 1, (int)ceilf(s_max(s_max(sy[0], sy[1]), sy[2])));
+            if (x0 <= x1 && y0 <= y1) {
+                ++n_rast;
+                // barycentric_2d's den (== area2) returns bc = -1 at every pixel below 1e-8
+                den = e0x * e1y - e1x * e0y;
+                live = !(fabsf(den) < 1e-8f);
+            }
+        }
+    }
+    if (!live) {
+        store_box(fb, slot, 0, -1, 0, -1);
+        return;
+    }
+    LibRec r;
+    r.ax = sx[0]; r.ay = sy[0];
+    r.v0x = sx[1] - sx[0]; r.v0y = sy[1] - sy[0];
+    r.v1x = sx[2] - sx[0]; r.v1y = sy[2] - sy[0];
+    r.inv_den = 1.0f / den;
+    const float iw0 = 1.0f / a.cw, iw1 = 1.0f / b.cw, iw2 = 1.0f / c.cw;
+    r.iw0 = iw0; r.iw1 = iw1; r.iw2 = iw2;
+    r.z0 = a.cz * iw0; r.z1 = b.cz * iw1; r.z2 = c.cz * iw2;
+    r.seq = seq;
+    r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
+    fb.recs[slot] = r;
+    LibShade s;
+    const float iw[3] = {iw0, iw1, iw2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        s.wp[3 * k] = v[k]->wx * iw[k]; s.wp[3 * k + 1] = v[k]->wy * iw[k]; s.wp[3 * k + 2] = v[k]->wz * iw[k];
+        s.n[3 * k] = v[k]->nx * iw[k]; s.n[3 * k + 1] = v[k]->ny * iw[k]; s.n[3 * k + 2] = v[k]->nz * iw[k];
+        s.uv[2 * k] = v[k]->u * iw[k]; s.uv[2 * k + 1] = v[k]->v * iw[k];
+    }
+    s.draw = d;
+    s.pad[0] = s.pad[1] = s.pad[2] = 0;
+    fb.shade[slot] = s;
+    store_box(fb, slot, x0, x1, y0, y1);
+    lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot);
+}
+
+__device__ __forceinline__ int lib_find_draw(const LibDrawGPU *draws, int n_draws, int gid) {
+    int lo = 0, hi = n_draws - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (draws[mid].tri_base <= gid) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ bool read_tri(const LibDrawGPU &dr, int local, uint32_t (&id)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) id[k] = dr.idx ? dr.idx[3 * (size_t)local + k] : (uint32_t)(3 * local + k);
+    return id[0] < (uint32_t)dr.n_verts && id[1] < (uint32_t)dr.n_verts && id[2] < (uint32_t)dr.n_verts;
+}
+
+// Camera pass: one input triangle of rasterize_mesh.
+__device__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_clip,
+                                 uint32_t &n_rast) {
+    const int d = lib_find_draw(fb.draws, fp.n_draws, tri);
+    const LibDrawGPU &dr = fb.draws[d];
+    const int local = tri - dr.tri_base;
+    uint32_t id[3];
+    if (!read_tri(dr, local, id)) {
+        store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+        return;
+    }
+    LVert t[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = vertex_out(dr, id[k]);
+    const uint32_t seq0 = (uint32_t)tri * 16u;
+    if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
+        emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast);
+        return;
+    }
+    LVert poly[MAX_POLY];
+    const int n = clip_frustum(t, poly);
+    if (n < 3) {
+        store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+        return;
+    }
+    uint32_t xb = 0;
+    if (n > 3) {   // fans 1 .. n-3 take consecutive extra slots
+        const uint32_t e = atomicAdd(&cnt[LC_EXTRA], (uint32_t)(n - 3));
+        if (e + (uint32_t)(n - 3) > fp.extra_cap) {
+            atomicOr(&cnt[LC_OVERFLOW], LOV_EXTRA);
+            store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+            return;
+        }
+        xb = (uint32_t)fp.n_tris + e;
+        fb.xbase[tri] = xb;
+    }
+    for (int k = 1; k + 1 < n; ++k) {
+        const uint32_t slot = k == 1 ? (uint32_t)tri : xb + (uint32_t)(k - 2);
+        emit_fan(fp, fb, cnt, dr, d, seq0 + (uint32_t)(k - 1), slot, poly[0], poly[k], poly[k + 1], n_clip, n_rast);
+    }
+}
+
+// Shadow pass: one caster triangle of PassShadowMap (pass_shadow_map.hpp:155-203), draws[d].viewproj
+// holding the light camera's viewproj.  n_rast counts the triangles with a non-empty bbox.
+__device__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_rast) {
+    const int d = lib_find_draw(fb.draws, fp.n_draws, tri);
+    const LibDrawGPU &dr = fb.draws[d];
+    const int local = tri - dr.tri_base;
+    uint32_t id[3];
+    float nx[3], ny[3], nz[3];
+    bool ok = read_tri(dr, local, id);
+    if (ok) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float *P = dr.pos + 3 * (size_t)id[k];
+            const f4 w = m4v(dr.model, f4{P[0], P[1], P[2], 1.0f});
+            const f4 c = m4v(dr.viewproj, f4{w.x, w.y, w.z, 1.0f});
+            ok = ok && !(fabsf(c.w) < 1e-8f);
+            nx[k] = c.x / c.w; ny[k] = c.y / c.w; nz[k] = c.z / c.w;
+        }
+    }
+    if (ok) {   // all corners beyond one side of the NDC cube: early reject (:174-177)
+        ok = !((nx[0] < -1.0f && nx[1] < -1.0f && nx[2] < -1.0f) || (nx[0] > 1.0f && nx[1] > 1.0f && nx[2] > 1.0f)) &&
+             !((ny[0] < -1.0f && ny[1] < -1.0f && ny[2] < -1.0f) || (ny[0] > 1.0f && ny[1] > 1.0f && ny[2] > 1.0f)) &&
+             !((nz[0] < -1.0f && nz[1] < -1.0f && nz[2] < -1.0f) || (nz[0] > 1.0f && nz[1] > 1.0f && nz[2] > 1.0f));
+    }
+    int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+    float sx[3], sy[3], den = 0.0f;
+    if (ok) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            sx[k] = (nx[k] * 0.5f + 0.5f) * (float)(fp.W - 1);
+            sy[k] = (ny[k] * 0.5f + 0.5f) * (float)(fp.H - 1);
+        }
+        x0 = max(0, (int)floorf(s_min(s_min(sx[0], sx[1]), sx[2])));
+        x1 = min(fp.W - 1, (int)ceilf(s_max(s_max(sx[0], sx[1]), sx[2])));
+        y0 = max(0, (int)floorf(s_min(s_min(sy[0], sy[1]), sy[2])));
+        y1 = min(fp.H - 1, (int)ceilf(s_max(s_max(sy[0], sy[1]), sy[2])));
+        ok = x0 <= x1 && y0 <= y1;
+        if (ok) {
+            ++n_rast;
+            den = (sx[1] - sx[0]) * (sy[2] - sy[0]) - (sx[2] - sx[0]) * (sy[1] - sy[0]);
+            ok = !(fabsf(den) < 1e-8f);
+        }
+    }
+    if (!ok) {
+        store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+        return;
+    }
+    LibRec r;
+    r.ax = sx[0]; r.ay = sy[0];
+    r.v0x = sx[1] - sx[0]; r.v0y = sy[1] - sy[0];
+    r.v1x = sx[2] - sx[0]; r.v1y = sy[2] - sy[0];
+    r.inv_den = 1.0f / den;
+    r.z0 = nz[0]; r.z1 = nz[1]; r.z2 = nz[2];
+    r.iw0 = r.iw1 = r.iw2 = 0.0f;
+    r.seq = (uint32_t)tri * 16u;
+    r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
+    fb.recs[tri] = r;
+    store_box(fb, (uint32_t)tri, x0, x1, y0, y1);
+    lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri);
+}
+
+template <bool SHADOW>
+__global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
+    __shared__ uint32_t s_stat[2];
+    const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
+    uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    if (tid < 2) s_stat[tid] = 0u;
+    // zero the other counter set and bin counts for the next frame
+    if (b == 0 && tid < LC_N) fb.counters[(fp.parity ^ 1u) * LC_N + tid] = 0u;
+    {
+        const int n_bt = fp.tiles_x * fp.tiles_y;
+        uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
+        for (int t = b * 256 + tid; t < n_bt; t += (int)gridDim.x * 256) next_count[t] = 0u;
+    }
+    __syncthreads();
+    const int tri = b * 256 + tid;
+    uint32_t n_clip = 0, n_rast = 0;
+    if (tri < fp.n_tris) {
+        if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast);
+        else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        n_clip += __shfl_down(n_clip, o);
+        n_rast += __shfl_down(n_rast, o);
+    }
+    if (__lane_id() == 0) {
+        atomicAdd(&s_stat[0], n_clip);
+        atomicAdd(&s_stat[1], n_rast);
+    }
+    __syncthreads();
+    if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(s_stat[0], s_stat[1]);
+}
+
+// ---- k_lib_raster -----------------------------------------------------------------------------
+
+// One (primitive, pixel) test: barycentric_2d (rasterizer.hpp:167-179), the inside test (:338),
+// then the camera pass's 1/w depth (:341-361) or the shadow pass's NDC depth (pass_shadow_map.hpp
+// :193-200).  Returns whether the fragment passes the depth test against the clear value.
+template <bool SHADOW>
+__device__ __forceinline__ bool lib_test(const LibFrameParams &fp, const LibRec &r, int px, int py, float &z01, float &u,
+                                         float &v, float &w, float &inv_denom) {
+    const float vpx = ((float)px + 0.5f) - r.ax, vpy = ((float)py + 0.5f) - r.ay;
+    v = (vpx * r.v1y - r.v1x * vpy) * r.inv_den;
+    w = (r.v0x * vpy - vpx * r.v0y) * r.inv_den;
+    u = (1.0f - v) - w;
+    if (u < 0.0f || v < 0.0f || w < 0.0f) return false;
+    if (SHADOW) {
+        const float z_ndc = (u * r.z0 + v * r.z1) + w * r.z2;
+        z01 = s_clamp(z_ndc * 0.5f + 0.5f, 0.0f, 1.0f);
+        return z01 < 1.0f;   // RT_ShadowDepth cleared to 1, `if (z01 < zbuf)`
+    }
+    const float denom = (u * r.iw0 + v * r.iw1) + w * r.iw2;
+    if (denom <= 1e-10f) return false;
+    inv_denom = 1.0f / denom;
+    const float z_clip = (u * r.z0 + v * r.z1) + w * r.z2;
+    z01 = g_clamp((z_clip * inv_denom) * 0.5f + 0.5f, 0.0f, 1.0f);
+    if (!(fp.flags & LF_DEPTH)) return true;   // no depth_motion target: every fragment writes
+    if (fp.flags & LF_LINZ) z01 = g_clamp((1.0f / denom - fp.zn) / fp.zspan, 0.0f, 1.0f);
+    return z01 < 1.0f;                         // depth cleared to 1, `if (z01 >= zbuf) continue`
+}
+
+// Without a depth target the last fragment in submission order wins: its key is the smallest.
+__device__ __forceinline__ unsigned long long lib_key(const LibFrameParams &fp, float z01, uint32_t seq, bool shadow) {
+    return (shadow || (fp.flags & LF_DEPTH)) ? z_key(z01, seq) : (unsigned long long)(0xffffffffu - seq);
+}
+
+// shadow_visibility_dir (lighting/shadow_sample.hpp:65-104) with the FS's ShadowParams.
+__device__ float shadow_visibility(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 pos, float ndotl) {
+    const f4 p = m4v(dr.light_vp, f4{pos.x, pos.y, pos.z, 1.0f});
+    if (fabsf(p.w) < 1e-8f) return 1.0f;
+    const float su = (p.x / p.w) * 0.5f + 0.5f, sv = (p.y / p.w) * 0.5f + 0.5f, sz = (p.z / p.w) * 0.5f + 0.5f;
+    if (su < 0.0f || su > 1.0f || sv < 0.0f || sv > 1.0f) return 1.0f;
+    const float slope = 1.0f - s_clamp(ndotl, 0.0f, 1.0f);
+    const float z_test = sz - (dr.shp[0] + dr.shp[1] * slope);
+    const int cx = (int)roundf(su * (float)(fp.sm_w - 1)), cy = (int)roundf(sv * (float)(fp.sm_h - 1));
+    const int rad = __float_as_int(dr.shp[2]);
+    if (rad == 0) {
+        const float z_ref = fb.shadow_map[(size_t)s_clampi(cy, 0, fp.sm_h - 1) * fp.sm_w + s_clampi(cx, 0, fp.sm_w - 1)];
+        return (z_test <= z_ref) ? 1.0f : 0.0f;
+    }
+    const int step = max(1, (int)roundf(dr.shp[3]));
+    int count = 0, lit = 0;
+    for (int oy = -rad; oy <= rad; oy++) {
+        const size_t row = (size_t)s_clampi(cy + oy * step, 0, fp.sm_h - 1) * fp.sm_w;
+        for (int ox = -rad; ox <= rad; ox++) {
+            lit += (z_test <= fb.shadow_map[row + s_clampi(cx + ox * step, 0, fp.sm_w - 1)]) ? 1 : 0;
+            count++;
+        }
+    }
+    return (float)lit / (float)count;
+}
+
+// eval_fake_ibl (builtin_shaders.hpp:57-85)
+__device__ f3 fake_ibl(f3 N, f3 V, f3 base, float metallic, float roughness, float ao) {
+    const f3 n = normalize3(N), v = normalize3(V);
+    const f3 I = neg3(v);
+    const f3 r = sub3(I, sc3(sc3(n, dot3(n, I)), 2.0f));
+    const f3 zen = {0.32f, 0.46f, 0.72f}, hor = {0.62f, 0.66f, 0.72f}, gnd = {0.16f, 0.15f, 0.14f};
+    const float up_n = s_clamp(n.y * 0.5f + 0.5f, 0.0f, 1.0f);
+    const float up_r = s_clamp(r.y * 0.5f + 0.5f, 0.0f, 1.0f);
+    const f3 env_n = mix3(gnd, mix3(hor, zen, up_n), up_n);
+    const f3 env_r = mix3(gnd, mix3(hor, zen, up_r), up_r);
+    const float m = s_clamp(metallic, 0.0f, 1.0f), rgh = s_clamp(roughness, 0.0f, 1.0f);
+    const f3 F0 = mix3(f3{0.04f, 0.04f, 0.04f}, gmax3(base, f3{0.0f, 0.0f, 0.0f}), m);
+    const float fres = powf(1.0f - s_max(0.0f, dot3(n, v)), 5.0f);
+    const f3 F = add3(F0, sc3(sub3(f3{1.0f, 1.0f, 1.0f}, F0), fres));
+    const f3 kd = sc3(sub3(f3{1.0f, 1.0f, 1.0f}, F), 1.0f - m);
+    const f3 diffuse_ibl = sc3(mul3(mul3(kd, base), env_n), 0.12f);
+    const float spec_strength = 0.02f + (1.0f - rgh) * 0.18f;
+    const f3 spec_ibl = sc3(mul3(env_r, F), spec_strength);
+    return sc3(add3(diffuse_ibl, spec_ibl), s_clamp(ao, 0.0f, 1.0f));
+}
+
+// The builtin fragment programs (builtin_shaders.hpp:105-245); no base_color_tex -> albedo_tex = 1.
+__device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, float depth01) {
+    const f3 bc = {dr.base[0], dr.base[1], dr.base[2]};
+    if (dr.program == 2) return bc;                                                   // debug albedo
+    if (dr.program == 3) return add3(sc3(normalize3(nrm), 0.5f), f3{0.5f, 0.5f, 0.5f});  // debug normal
+    if (dr.program == 4) {                                                            // debug depth
+        const float dd = s_clamp(depth01, 0.0f, 1.0f);
+        return f3{dd, dd, dd};
+    }
+    const f3 L = {dr.L[0], dr.L[1], dr.L[2]};
+    const f3 cam = {dr.cam[0], dr.cam[1], dr.cam[2]};
+    const f3 lcol = {dr.lcol[0], dr.lcol[1], dr.lcol[2]};
+    const f3 albedo = gmax3(bc, f3{0.0f, 0.0f, 0.0f});   // base_color * vec3(1)
+    const f3 N = normalize3(nrm);
+    const f3 V = normalize3(sub3(cam, world));
+    if (dr.program == 1) {   // make_blinn_phong_program (:111-150)
+        const f3 H = normalize3(add3(L, V));
+        const float NdotL = s_max(0.0f, dot3(N, L));
+        const float NdotH = s_max(0.0f, dot3(N, H));
+        const float rough = s_clamp(dr.mat[0], 0.0f, 1.0f);
+        const float metal = s_clamp(dr.base[3], 0.0f, 1.0f);
+        const float spec_pow = s_max(4.0f, 8.0f + (1.0f - rough) * 120.0f);
+        const float spec_norm = (spec_pow + 2.0f) / (2.0f * PI_F);
+        const float spec_f0 = 0.04f + 0.96f * metal;
+        const float spec = ((powf(NdotH, spec_pow) * spec_norm) * spec_f0) * NdotL;
+        const float kd = 1.0f - metal;
+        const f3 diffuse = sc3(mul3(f3{kd, kd, kd}, albedo), NdotL / PI_F);
+        float vis = 1.0f;
+        if (dr.shadow && NdotL > 0.0f) vis = g_mix(1.0f, shadow_visibility(fp, fb, dr, world, NdotL), s_clamp(dr.mat[2], 0.0f, 1.0f));
+        const f3 direct = sc3(sc3(mul3(add3(diffuse, f3{spec, spec, spec}), lcol), dr.lcol[3]), vis);
+        return add3(direct, fake_ibl(N, V, albedo, dr.base[3], dr.mat[0], dr.mat[1]));
+    }
+    // make_pbr_mr_program (:160-212)
+    const f3 H = normalize3(add3(V, L));
+    const float NdotL = s_max(0.0f, dot3(N, L));
+    const float NdotV = s_max(0.0f, dot3(N, V));
+    const float NdotH = s_max(0.0f, dot3(N, H));
+    const float VdotH = s_max(0.0f, dot3(V, H));
+    const float rough = s_clamp(dr.mat[0], 0.04f, 1.0f);
+    const float metal = s_clamp(dr.base[3], 0.0f, 1.0f);
+    const f3 F0 = mix3(f3{0.04f, 0.04f, 0.04f}, albedo, metal);
+    const float a = rough * rough;
+    const float a2 = a * a;
+    const float denomD = (NdotH * NdotH) * (a2 - 1.0f) + 1.0f;
+    const float D = a2 / ((PI_F * denomD) * denomD + 1e-7f);
+    const float k = ((a + 1.0f) * (a + 1.0f)) * 0.125f;
+    const float G = (NdotV / ((NdotV * (1.0f - k) + k) + 1e-7f)) * (NdotL / ((NdotL * (1.0f - k) + k) + 1e-7f));
+    const f3 F = add3(F0, sc3(sub3(f3{1.0f, 1.0f, 1.0f}, F0), powf(1.0f - VdotH, 5.0f)));
+    const float sden = s_max((4.0f * NdotL) * NdotV, 1e-6f);
+    const f3 dgf = sc3(F, D * G);
+    const f3 spec = {dgf.x / sden, dgf.y / sden, dgf.z / sden};
+    const f3 kd = sc3(sub3(f3{1.0f, 1.0f, 1.0f}, F), 1.0f - metal);
+    const f3 diff = sc3(mul3(kd, albedo), 1.0f / PI_F);
+    const f3 radiance = sc3(lcol, dr.lcol[3]);
+    float vis = 1.0f;
+    if (dr.shadow && NdotL > 0.0f) vis = g_mix(1.0f, shadow_visibility(fp, fb, dr, world, NdotL), s_clamp(dr.mat[2], 0.0f, 1.0f));
+    const f3 direct = (NdotL > 0.0f && NdotV > 0.0f) ? sc3(sc3(mul3(add3(diff, spec), radiance), NdotL), vis) : f3{0.0f, 0.0f, 0.0f};
+    return add3(direct, fake_ibl(N, V, albedo, metal, rough, dr.mat[1]));
+}
+
+__device__ __forceinline__ float4 bg_color(const LibFrameParams &fp, int y) {
+    if (!(fp.flags & LF_GRADIENT)) return make_float4(fp.clear[0], fp.clear[1], fp.clear[2], fp.clear[3]);
+    const float t = (float)y / (float)max(1, fp.H - 1);   // pass_pbr_forward.hpp:75-81
+    return make_float4(0.06f + 0.08f * t, 0.08f + 0.10f * t, 0.12f + 0.12f * t, 1.0f);
+}
+
+struct LibShared {
+    float4 rec[LIB_CHUNK * 4];            // staged records (8 KB)
+    unsigned long long key[LIB_RTH * LIB_RTW];
+    uint32_t cand[LIB_CAND];
+    unsigned long long wmask[4];
+    int busy[256];
+    uint32_t nc, nbusy, cov, maxbin;
+};
+
+__device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
+    LibRec r;
+    float4 *d = reinterpret_cast<float4 *>(&r);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = s[j];
+    return r;
+}
+
+// Resolve one pixel of a tile (one thread): the winner of the key array is re-evaluated with the
+// identical arithmetic, shaded and written; pixels without a winner get the clear values.
+template <bool SHADOW>
+__device__ __forceinline__ void lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, unsigned long long key, int px,
+                                            int py, bool &covered) {
+    covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
+    if (px >= fp.W || py >= fp.H) return;
+    const size_t o = (size_t)py * fp.W + px;
+    if (SHADOW) {
+        fb.depth[o] = covered ? __uint_as_float((uint32_t)(key >> 32) & 0x7fffffffu) : 1.0f;
+        return;
+    }
+    float4 color = bg_color(fp, py);
+    float depth = 1.0f;
+    float2 mv = make_float2(0.0f, 0.0f);
+    if (covered) {
+        const uint32_t seq = (fp.flags & LF_DEPTH) ? (uint32_t)key : 0xffffffffu - (uint32_t)key;
+        const uint32_t tri = seq >> 4, k = seq & 15u;
+        const uint32_t slot = k == 0 ? tri : fb.xbase[tri] + k - 1u;
+        const LibRec r = fb.recs[slot];
+        const LibShade s = fb.shade[slot];
+        const LibDrawGPU &dr = fb.draws[s.draw];
+        float z01, u, v, w, idn;
+        lib_test<false>(fp, r, px, py, z01, u, v, w, idn);
+        depth = z01;
+        // FragmentIn from the varyings (rasterizer.hpp:365-387): (bc.x*varw0 + bc.y*varw1 + bc.z*varw2) * inv_denom
+        const f3 world = {((u * s.wp[0] + v * s.wp[3]) + w * s.wp[6]) * idn, ((u * s.wp[1] + v * s.wp[4]) + w * s.wp[7]) * idn,
+                          ((u * s.wp[2] + v * s.wp[5]) + w * s.wp[8]) * idn};
+        const f3 nv = {((u * s.n[0] + v * s.n[3]) + w * s.n[6]) * idn, ((u * s.n[1] + v * s.n[4]) + w * s.n[7]) * idn,
+                       ((u * s.n[2] + v * s.n[5]) + w * s.n[8]) * idn};
+        const f3 nrm = normalize3(nv);
+        if ((fp.flags & LF_MOTION) && dr.motion) {   // rasterizer.hpp:388-411
+            const f4 cw = {world.x, world.y, world.z, 1.0f};
+            const f4 pw = m4v(dr.c2p, cw);
+            const f4 cc = m4v(dr.viewproj, cw);
+            const f4 pc = m4v(dr.prev_vp, pw);
+            if (fabsf(cc.w) > 1e-8f && fabsf(pc.w) > 1e-8f) {
+                float vx = ((cc.x / cc.w - pc.x / pc.w) * 0.5f) * (float)fp.W;
+                float vy = ((cc.y / cc.w - pc.y / pc.w) * 0.5f) * (float)fp.H;
+                const float len = sqrtf(vx * vx + vy * vy);
+                if (len > 96.0f && len > 1e-6f) {
+                    const float sc = 96.0f / len;
+                    vx *= sc; vy *= sc;
+                }
+                mv = make_float2(vx, vy);
+            }
+        }
+        const f3 c = lib_fragment(fp, fb, dr, world, nrm, z01);
+        color = make_float4(c.x, c.y, c.z, 1.0f);
+    }
+    fb.hdr[o] = color;
+    if (fp.flags & LF_DEPTH) {
+        fb.depth[o] = depth;
+        fb.motion[o] = mv;
+    }
+}
+
+template <bool SHADOW>
+__device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared &sh) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
+    const int X0 = col * LIB_RTW, Y0 = row * LIB_RTH;
+    const int X1 = X0 + LIB_RTW - 1, Y1 = Y0 + LIB_RTH - 1;
+    const int bt = (row / (TILE / LIB_RTH)) * fp.tiles_x + col;
+    __syncthreads();   // the previous tile's key resets are done
+
+    uint32_t n_bin = 0, n_spill = 0, n_items;
+    if (fp.scan_mode) {
+        n_items = (uint32_t)fp.n_tris + (SHADOW ? 0u : min(cnt[LC_EXTRA], fp.extra_cap));
+    } else {
+        const uint32_t n_bin_total = fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + bt];
+        n_bin = min(n_bin_total, fp.bin_cap);
+        if (n_bin_total > fp.bin_cap) n_spill = min(cnt[LC_SPILL], fp.spill_cap);
+        n_items = n_bin + n_spill;
+        if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
+    }
+    const uint32_t *bin = fb.bins + (size_t)bt * fp.bin_cap;
+
+    for (uint32_t base = 0; base < n_items; base += LIB_CAND) {
+        __syncthreads();
+        if (tid == 0) sh.nc = 0;
+        __syncthreads();
+        uint32_t ids[LIB_CAND / 256];
+        uint2 bx[LIB_CAND / 256];
+#pragma unroll
+        for (int k = 0; k < LIB_CAND / 256; ++k) {
+            const uint32_t item = base + tid + 256u * k;
+            uint32_t id = 0xffffffffu;
+            if (item < n_items) {
+                if (fp.scan_mode) {
+                    id = item;
+                } else if (item < n_bin) {
+                    id = bin[item];
+                } else {
+                    const uint2 e = fb.spill[item - n_bin];
+                    if ((int)e.x == bt) id = e.y;
+                }
+            }
+            ids[k] = id;
+        }
+#pragma unroll
+        for (int k = 0; k < LIB_CAND / 256; ++k) bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
+#pragma unroll
+        for (int k = 0; k < LIB_CAND / 256; ++k) {
+            const int gx0 = lo16(bx[k].x), gx1 = hi16(bx[k].x), gy0 = lo16(bx[k].y), gy1 = hi16(bx[k].y);
+            const bool hit = ids[k] != 0xffffffffu && gx0 <= gx1 && gy0 <= gy1 && gx1 >= X0 && gx0 <= X1 && gy1 >= Y0 && gy0 <= Y1;
+            const uint64_t m = __ballot(hit);
+            uint32_t basew = 0;
+            if (lane == 0 && m) basew = atomicAdd(&sh.nc, (uint32_t)__popcll(m));
+            basew = __shfl(basew, 0);
+            if (hit) sh.cand[basew + lanes_below(m)] = ids[k];
+        }
+        __syncthreads();
+        const uint32_t nc = sh.nc;
+        for (uint32_t c = 0; c < nc; c += LIB_CHUNK) {
+            const int m = (int)min((uint32_t)LIB_CHUNK, nc - c);
+            if (c > 0) __syncthreads();
+            {   // stage records: consecutive lanes load consecutive float4s of one record
+                constexpr int NQ = LIB_CHUNK * 4 / 256;
+                float4 q[NQ];
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) {
+                    const int f = tid + 256 * k;
+                    const int ci = f >> 2;
+                    q[k] = f < 4 * m ? reinterpret_cast<const float4 *>(&fb.recs[sh.cand[c + min(ci, m - 1)]])[f & 3]
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) {
+                    const int f = tid + 256 * k;
+                    if (f < 4 * m) sh.rec[f] = q[k];
+                }
+            }
+            __syncthreads();
+            // (primitive, pixel) pair tasks: wave w takes staged candidates w + 4l; their clipped
+            // boxes' areas are prefix-summed and walked 64 pairs at a time (see shs_legacy.hip).
+            {
+                const int cidx = wave + 4 * lane;
+                int area = 0, bx0 = 0, by0 = 0, bw = 1;
+                if (cidx < m) {
+                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[cidx * 4])[3];   // iw2 seq bx by
+                    const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
+                    const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
+                    if (x0 <= x1 && y0 <= y1) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
+                }
+                int incl = area;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int vv = __shfl_up(incl, o);
+                    if (lane >= o) incl += vv;
+                }
+                const int start = incl - area;
+                const int total = __shfl(incl, 63);
+                for (int k0 = 0; k0 < total; k0 += 64) {
+                    const bool in_win = area > 0 && start >= k0 && start < k0 + 64;
+                    if (lane == 0) sh.wmask[wave] = 0ull;
+                    wave_lds_sync();
+                    if (in_win) atomicOr(&sh.wmask[wave], 1ull << (start - k0));
+                    wave_lds_sync();
+                    const unsigned long long M = sh.wmask[wave];
+                    const int before = __popcll(__ballot(area > 0 && start < k0));
+                    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                    const int o = before + __popcll(M & upto) - 1;
+                    const int k = k0 + lane;
+                    const int ostart = __shfl(start, o), ox0 = __shfl(bx0, o), oy0 = __shfl(by0, o), ow = __shfl(bw, o);
+                    if (k < total) {
+                        const int local = k - ostart;
+                        const int ly = local / ow, lx = local - ly * ow;
+                        const LibRec r = lib_rec_from(&sh.rec[(wave + 4 * o) * 4]);
+                        float z01, u, v, w, idn;
+                        if (lib_test<SHADOW>(fp, r, ox0 + lx, oy0 + ly, z01, u, v, w, idn))
+                            atomicMin(&sh.key[(oy0 + ly - Y0) * LIB_RTW + (ox0 + lx - X0)], lib_key(fp, z01, r.seq, SHADOW));
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int px = X0 + (tid & 31), py = Y0 + (tid >> 5);
+    const unsigned long long key = sh.key[tid];
+    sh.key[tid] = KEY_EMPTY;
+    bool covered;
+    lib_resolve<SHADOW>(fp, fb, key, px, py, covered);
+    const uint64_t cm = __ballot(covered);
+    if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
+    if (tid == 0) fb.busy[rt] = 0u;
+}
+
+template <bool SHADOW>
+__device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const LibBuffers &fb, int rt) {
+    const int tid = threadIdx.x;
+    const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
+    const int px = col * LIB_RTW + (tid & 31), py = row * LIB_RTH + (tid >> 5);
+    bool covered;
+    lib_resolve<SHADOW>(fp, fb, KEY_EMPTY, px, py, covered);
+}
+
+template <bool SHADOW>
+__global__ __launch_bounds__(256) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
+    __shared__ LibShared sh;
+    const int tid = threadIdx.x;
+    const uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const int G = (int)gridDim.x;
+    if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
+    sh.key[tid] = KEY_EMPTY;
+    for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
+        __syncthreads();
+        if (tid == 0) sh.nbusy = 0;
+        __syncthreads();
+        const int j = j0 + tid * G;
+        if (j < fp.n_owned_rt) {
+            // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it
+            const int t = fp.rank + (j >> 2) * fp.count;
+            const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / LIB_RTH) + (j & 3);
+            if (row < fp.rtiles_y) {
+                const int rt = row * fp.tiles_x + col;
+                if (fb.busy[rt]) sh.busy[atomicAdd(&sh.nbusy, 1u) & 0xffffu] = rt;
+                else sh.busy[255 - atomicAdd(&sh.nbusy, 0x10000u) / 0x10000u] = rt;
+            }
+        }
+        __syncthreads();
+        const int nb = (int)(sh.nbusy & 0xffffu), ne = (int)(sh.nbusy >> 16);
+        for (int i = 0; i < nb; ++i) lib_raster_tile<SHADOW>(fp, fb, cnt, sh.busy[i], sh);
+        for (int i = 0; i < ne; ++i) lib_clear_tile<SHADOW>(fp, fb, sh.busy[255 - i]);
+    }
+    __syncthreads();
+    if (tid == 0) fb.rstat[blockIdx.x] = make_uint2(sh.cov, sh.maxbin);
+}
+
+}  // namespace shs_dev
+
+namespace shs_internal {
+using namespace shs_dev;
+
+hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, hipStream_t s) {
+    const int grid = std::max(1, (fp.n_tris + 255) / 256);
+    if (shadow) hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
+    else hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
+    return hipGetLastError();
+}
+
+hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, int grid, hipStream_t s) {
+    if (shadow) hipLaunchKernelGGL(k_lib_raster<true>, dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
+    else hipLaunchKernelGGL(k_lib_raster<false>, dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
+    return hipGetLastError();
+}
+
+}  // namespace shs_internal

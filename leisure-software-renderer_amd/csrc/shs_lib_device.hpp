@@ -1,0 +1,99 @@
+// shs_lib_device.hpp -- HBM layouts of the shs-renderer-lib software raster path on gfx950
+// (rasterize_mesh + builtin programs, PassShadowMap), shared by shs_lib.hip and shs_abi.cpp.
+// Paths are relative to /root/reference/cpp-folders/src/shs-renderer-lib/include/shs/.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace shs_dev {
+
+// Per-draw block of one rasterize_mesh call (ShaderUniforms, shader/types.hpp:87-116, reduced to
+// what the builtin programs read; uniform-only products are computed once on the host with the
+// same float operations the reference runs per vertex / per fragment).
+struct alignas(16) LibDrawGPU {
+    const float *pos;        // MeshData positions, 3 floats per vertex
+    const float *nrm;        // normals (missing entries filled with (0,1,0) at upload)
+    const float *uv;         // uvs (missing entries (0,0))
+    const uint32_t *idx;     // indices, nullptr for a non-indexed soup
+    int32_t n_verts, tri_base, n_tris, program;
+    int32_t cull_mode, front_ccw, shadow, motion;   // motion: u.enable_motion_vectors
+    float model[16];         // u.model
+    float viewproj[16];      // u.viewproj
+    float nmat[12];          // transpose(inverse(mat3(model))) if |det| > 1e-8 else mat3(model) (9 used)
+    float c2p[16];           // curr_to_prev_model (rasterizer.hpp:296-308)
+    float prev_vp[16];       // u.prev_viewproj
+    float light_vp[16];      // u.light_viewproj
+    float L[4];              // normalize(-u.light_dir_ws)
+    float cam[4];            // u.camera_pos
+    float lcol[4];           // u.light_color, u.light_intensity
+    float base[4];           // u.base_color, u.metallic
+    float mat[4];            // u.roughness, u.ao, u.shadow_strength, 0
+    float shp[4];            // bias_const, bias_slope, pcf radius (int bits), pcf_step
+};
+
+// Raster record of one primitive (a fan triangle of a clipped input triangle, or a shadow-pass
+// triangle), 64 B: the per-triangle part of barycentric_2d (rasterizer.hpp:167-179), the 1/w
+// terms and the corner depths.
+struct alignas(16) LibRec {
+    float ax, ay, v0x, v0y;      // s0, v0 = s1 - s0
+    float v1x, v1y, inv_den, z0; // v1 = s2 - s0, 1/den; z_k = clip.z * (1/w) (shadow pass: NDC z)
+    float z1, z2, iw0, iw1;      // 1/clip.w per corner
+    float iw2;
+    uint32_t seq;                // submission order: input triangle * 16 + fan index
+    uint32_t bx, by;             // pixel bbox [min, max], packed int16 (lo | hi << 16)
+};
+static_assert(sizeof(LibRec) == 64, "LibRec must stay 64 B");
+
+// Perspective-premultiplied varyings of the primitive's corners (varw, rasterizer.hpp:309-328).
+struct alignas(16) LibShade {
+    float wp[9];                 // WorldPos varying * 1/w
+    float n[9];                  // NormalWS varying * 1/w
+    float uv[6];                 // UV0 varying * 1/w
+    int32_t draw;
+    int32_t pad[3];
+};
+static_assert(sizeof(LibShade) == 112, "LibShade must stay 112 B");
+
+constexpr uint32_t LF_DEPTH = 1u;       // target.depth_motion present: strict-less z test, depth written
+constexpr uint32_t LF_LINZ = 2u;        // ... with zf > zn + 1e-6: linear view depth
+constexpr uint32_t LF_MOTION = 4u;      // motion buffer written (per draw: enable_motion_vectors)
+constexpr uint32_t LF_GRADIENT = 8u;    // PassPBRForward's no-sky background gradient, else clear[]
+
+// counters[] (two parity sets, frame f uses set f & 1, k_lib_setup zeroes the other)
+constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_N = 4;
+constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
+
+struct LibFrameParams {
+    int32_t W, H;
+    int32_t rank, count;             // shard ownership of 32x32 bin tiles (tile % count == rank)
+    int32_t tiles_x, tiles_y, rtiles_y;
+    int32_t n_tris, n_draws;
+    uint32_t flags;                  // LF_*
+    float zn, zf, zspan;             // RT_ColorDepthMotion zn / zf, zspan = zf - zn
+    float clear[4];
+    uint32_t bin_cap, spill_cap, extra_cap;
+    uint32_t parity, scan_mode;
+    int32_t setup_blocks, n_owned_rt;
+    int32_t sm_w, sm_h;              // shadow map sampled by the programs
+};
+
+struct LibBuffers {
+    const LibDrawGPU *draws;
+    LibRec *recs;                    // n_tris primaries (fan 0) then extra_cap extras (fans 1..6)
+    LibShade *shade;
+    uint2 *boxes;                    // per slot: packed pixel bbox, empty (0,-1) when not rasterised
+    uint32_t *xbase;                 // per input triangle: slot of its fan triangle 1
+    uint32_t *tile_count, *bins;
+    uint2 *spill;
+    uint32_t *counters;
+    uint32_t *busy;                  // per 32x8 raster tile
+    uint2 *blk_stat;                 // per setup block: (tri_after_clip, tri_raster)
+    uint2 *rstat;                    // per raster block: (covered pixels, fullest bin)
+    float4 *hdr;                     // W*H, rows y-up (RT_ColorHDR)
+    float *depth;                    // W*H (RT_ColorDepthMotion depth / RT_ShadowDepth)
+    float2 *motion;                  // W*H
+    const float *shadow_map;         // sampled by the camera pass (sm_w * sm_h)
+};
+
+}  // namespace shs_dev

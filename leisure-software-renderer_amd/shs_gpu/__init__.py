@@ -80,6 +80,8 @@ class Context:
         self._h = h
         self._meshes = {}
         self._frame = None
+        self._lib_frame = None
+        self._shadow_size = None
 
     def _check(self, rc):
         if rc != 0:
@@ -228,6 +230,81 @@ class Context:
 
     def set_stream(self, hip_stream):
         self._check(self._lib.shs_set_stream(self._h, ctypes.c_void_p(hip_stream)))
+
+    # -- library path (rasterize_mesh / PassShadowMap / PassPBRForward) ---------------------------
+    def upload_lib_mesh(self, mesh) -> int:
+        key = ("lib", id(mesh))
+        if key in self._meshes:
+            return self._meshes[key][0]
+        pos = np.ascontiguousarray(mesh.positions, dtype=np.float32).reshape(-1, 3)
+        nrm = None if mesh.normals is None else np.ascontiguousarray(mesh.normals, dtype=np.float32).reshape(-1, 3)
+        uv = None if mesh.uvs is None else np.ascontiguousarray(mesh.uvs, dtype=np.float32).reshape(-1, 2)
+        idx = None if mesh.indices is None else np.ascontiguousarray(mesh.indices, dtype=np.uint32).reshape(-1)
+        mid = ctypes.c_int32()
+        self._check(self._lib.shs_mesh_upload(
+            self._h, _fptr(pos), pos.shape[0],
+            _fptr(nrm) if nrm is not None else None, 0 if nrm is None else nrm.shape[0],
+            _fptr(uv) if uv is not None else None, 0 if uv is None else uv.shape[0],
+            idx.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) if idx is not None else None,
+            0 if idx is None else idx.size, ctypes.byref(mid)))
+        self._meshes[key] = (mid.value, mesh)
+        return mid.value
+
+    def render_shadow_map(self, size, sun_dir, casters):
+        """PassShadowMap::execute -> the light camera's viewproj (float32[16])."""
+        from ._abi import ShadowCasterC
+        w, h = (size, size) if isinstance(size, int) else size
+        arr = (ShadowCasterC * max(len(casters), 1))()
+        for i, c in enumerate(casters):
+            arr[i].mesh_id = c.mesh if isinstance(c.mesh, int) else self.upload_lib_mesh(c.mesh)
+            for k in range(16):
+                arr[i].model[k] = float(c.model[k])
+        sd = np.ascontiguousarray(sun_dir, dtype=np.float32).reshape(3)
+        vp = np.zeros(16, np.float32)
+        self._check(self._lib.shs_render_shadow_map(self._h, w, h, _fptr(sd), arr, len(casters), _fptr(vp)))
+        self._shadow_size = (w, h)
+        return vp
+
+    def resolve_shadow_map(self):
+        w, h = self._shadow_size
+        out = np.empty((h, w), np.float32)
+        self._check(self._lib.shs_resolve_shadow_map(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out
+
+    def prepare_lib(self, frame, draws):
+        from ._abi import LibDrawC
+        from .lib import fill_draw_struct
+        arr = (LibDrawC * max(len(draws), 1))()
+        for i, d in enumerate(draws):
+            fill_draw_struct(arr[i], d, d.mesh if isinstance(d.mesh, int) else self.upload_lib_mesh(d.mesh))
+        return frame, frame.desc(), arr, len(draws)
+
+    def render_pbr_forward_prepared(self, prepared):
+        frame, desc, arr, n = prepared
+        self._check(self._lib.shs_render_pbr_forward(self._h, ctypes.byref(desc), arr, n))
+        self._lib_frame = frame
+
+    def render_pbr_forward(self, frame, draws):
+        """PassPBRForward::execute: clears + one rasterize_mesh per draw (asynchronous)."""
+        self.render_pbr_forward_prepared(self.prepare_lib(frame, draws))
+
+    def resolve_lib(self):
+        """-> (hdr float32[H,W,4], depth float32[H,W] or None, motion float32[H,W,2] or None), rows y-up."""
+        f = self._lib_frame
+        hdr = np.empty((f.height, f.width, 4), np.float32)
+        depth = np.empty((f.height, f.width), np.float32) if f.depth_motion else None
+        motion = np.empty((f.height, f.width, 2), np.float32) if f.depth_motion else None
+        vp = ctypes.c_void_p
+        self._check(self._lib.shs_resolve_lib(self._h, hdr.ctypes.data_as(vp),
+                                              depth.ctypes.data_as(vp) if depth is not None else None,
+                                              motion.ctypes.data_as(vp) if motion is not None else None))
+        return hdr, depth, motion
+
+    def lib_stats(self) -> dict:
+        from ._abi import LibStats
+        s = LibStats()
+        self._check(self._lib.shs_get_lib_stats(self._h, ctypes.byref(s)))
+        return {k: int(getattr(s, k)) for k, _ in LibStats._fields_}
 
     @property
     def stream(self):

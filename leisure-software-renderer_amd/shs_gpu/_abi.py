@@ -66,6 +66,60 @@ class RasterStats(ctypes.Structure):
     ]
 
 
+# ---- library path (rasterize_mesh / PassShadowMap / PassPBRForward) ----
+PROGRAM_PBR_MR = 0
+PROGRAM_BLINN_PHONG = 1
+PROGRAM_DEBUG_ALBEDO = 2
+PROGRAM_DEBUG_NORMAL = 3
+PROGRAM_DEBUG_DEPTH = 4
+CULL_NONE, CULL_BACK, CULL_FRONT = 0, 1, 2
+LIB_DEPTH_MOTION = 1
+LIB_BG_GRADIENT = 2
+
+_F16 = ctypes.c_float * 16
+_F3 = ctypes.c_float * 3
+
+
+class LibDrawC(ctypes.Structure):
+    _fields_ = [
+        ("mesh_id", ctypes.c_int32),
+        ("program", ctypes.c_int32),
+        ("cull_mode", ctypes.c_int32),
+        ("front_face_ccw", ctypes.c_int32),
+        ("model", _F16), ("viewproj", _F16), ("prev_model", _F16), ("prev_viewproj", _F16),
+        ("light_dir_ws", _F3), ("light_color", _F3), ("light_intensity", ctypes.c_float), ("camera_pos", _F3),
+        ("base_color", _F3), ("metallic", ctypes.c_float), ("roughness", ctypes.c_float), ("ao", ctypes.c_float),
+        ("shadow", ctypes.c_int32),
+        ("light_viewproj", _F16),
+        ("shadow_bias_const", ctypes.c_float), ("shadow_bias_slope", ctypes.c_float),
+        ("shadow_pcf_radius", ctypes.c_int32),
+        ("shadow_pcf_step", ctypes.c_float), ("shadow_strength", ctypes.c_float),
+        ("enable_motion_vectors", ctypes.c_int32),
+    ]
+
+
+class LibFrameC(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("zn", ctypes.c_float), ("zf", ctypes.c_float),
+        ("clear_hdr", ctypes.c_float * 4),
+    ]
+
+
+class LibStats(ctypes.Structure):
+    _fields_ = [
+        ("tri_input", ctypes.c_uint64), ("tri_after_clip", ctypes.c_uint64), ("tri_raster", ctypes.c_uint64),
+        ("covered_pixels", ctypes.c_uint64), ("max_tile_bin", ctypes.c_uint64), ("spilled", ctypes.c_uint64),
+        ("clipped_extra", ctypes.c_uint64),
+    ]
+
+
+class ShadowCasterC(ctypes.Structure):
+    _fields_ = [("mesh_id", ctypes.c_int32), ("model", _F16)]
+
+
 # (name, restype, argtypes) for every symbol include/shs_gpu.h declares.
 _P = ctypes.c_void_p
 _F = ctypes.POINTER(ctypes.c_float)
@@ -96,6 +150,19 @@ SIGNATURES = [
     ("shs_model_trs", ctypes.c_int, [_F, ctypes.c_float, _F, _F]),
     ("shs_mat4_mul", ctypes.c_int, [_F, _F, _F]),
     ("shs_mat4_inverse", ctypes.c_int, [_F, _F]),
+    ("shs_mesh_upload", ctypes.c_int, [_P, _F, ctypes.c_int32, _F, ctypes.c_int32, _F, ctypes.c_int32,
+                                       ctypes.POINTER(ctypes.c_uint32), ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)]),
+    ("shs_render_pbr_forward", ctypes.c_int, [_P, ctypes.POINTER(LibFrameC), ctypes.POINTER(LibDrawC), ctypes.c_int32]),
+    ("shs_resolve_lib", ctypes.c_int, [_P, _P, _P, _P]),
+    ("shs_get_lib_stats", ctypes.c_int, [_P, ctypes.POINTER(LibStats)]),
+    ("shs_lib_device_targets", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    ("shs_render_shadow_map", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _F, ctypes.POINTER(ShadowCasterC),
+                                             ctypes.c_int32, _F]),
+    ("shs_resolve_shadow_map", ctypes.c_int, [_P, _P]),
+    ("shs_look_at_lh", ctypes.c_int, [_F, _F, _F, _F]),
+    ("shs_perspective_lh_no", ctypes.c_int, [ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F]),
+    ("shs_model_euler", ctypes.c_int, [_F, _F, _F, _F]),
+    ("shs_dir_light_camera_aabb", ctypes.c_int, [_F, _F, _F, ctypes.c_float, ctypes.c_uint32, _F, _F, _F]),
 ]
 
 

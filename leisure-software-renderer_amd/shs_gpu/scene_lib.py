@@ -1,0 +1,114 @@
+"""Synthetic library-path scenes (BASELINE.json configs[4], "C5": PBR Cook-Torrance + shadow-map pass).
+
+C5: Suzanne + a floor plane, PassShadowMap (2048^2, sun normalize(0.4668,-0.3487,0.8127),
+hello_pbr.cpp:110) then PassPBRForward with make_pbr_mr_program at 3840x2160.  Reference defaults are used
+where the scene does not say otherwise: DirectionalLight colour 1 / intensity 5 (scene/scene_types.hpp:65-73),
+ShadowPassParams bias 0.0008 / 0.0015, PCF radius 2 (frame/frame_params.hpp:25-33), Camera fov 60,
+zn 0.1, zf 200 (scene_types.hpp:43-60), the no-material fallback (0.8,0.5,0.2) metallic 0.1 roughness 0.5
+(pass_pbr_forward.hpp:178-184) for Suzanne and a grey plastic floor.
+"""
+import numpy as np
+
+from .lib import (CULL_BACK, CULL_NONE, PROGRAM_PBR_MR, LibDraw, LibFrame, LibMesh, ShadowCaster, look_at_lh, mat_mul,
+                  model_euler, perspective_lh_no)
+from .scene import monkey
+
+f32 = np.float32
+SUN_DIR = (0.4668, -0.3487, 0.8127)   # normalised by build_dir_light_camera_aabb and the FS
+
+
+def _glm_normalize(v):
+    v = np.asarray(v, dtype=np.float32)
+    d = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]
+    return (v * (f32(1.0) / np.sqrt(d, dtype=np.float32))).astype(np.float32)
+
+
+_MONKEY_LIB = None
+
+
+def monkey_lib() -> LibMesh:
+    """Suzanne as an indexed MeshData: identical (position, normal) corners of the soup joined
+    (the assimp JoinIdenticalVertices step of the reference's loader), first-seen order."""
+    global _MONKEY_LIB
+    if _MONKEY_LIB is None:
+        soup = monkey()
+        corners = np.concatenate([soup.positions.reshape(-1, 3), soup.normals.reshape(-1, 3)], axis=1)
+        _, first, inv = np.unique(corners.view(np.uint32), axis=0, return_index=True, return_inverse=True)
+        order = np.argsort(first)
+        remap = np.empty_like(order)
+        remap[order] = np.arange(order.size)
+        verts = corners[first[order]]
+        _MONKEY_LIB = LibMesh(positions=np.ascontiguousarray(verts[:, :3]), normals=np.ascontiguousarray(verts[:, 3:]),
+                              uvs=None, indices=remap[inv.reshape(-1)].astype(np.uint32))
+    return _MONKEY_LIB
+
+
+def make_plane(width=10.0, depth=10.0, seg_x=10, seg_z=10) -> LibMesh:
+    """make_plane(PlaneDesc) (geometry/primitives_builders.hpp:56-114) in float32, including
+    add_triangle_match_normals' winding fix-up."""
+    sx, sz = max(1, seg_x), max(1, seg_z)
+    hw, hz = f32(width) * f32(0.5), f32(depth) * f32(0.5)
+    origin = np.array([-hw, 0.0, -hz], np.float32)
+    au = np.array([width, 0.0, 0.0], np.float32)
+    av = np.array([0.0, 0.0, depth], np.float32)
+    n = np.array([0.0, 1.0, 0.0], np.float32)
+    pos, uv = [], []
+    for y in range(sz + 1):
+        fv = f32(y) / f32(sz)
+        for x in range(sx + 1):
+            fu = f32(x) / f32(sx)
+            pos.append((origin + au * fu) + av * fv)
+            uv.append((fu, fv))
+    pos = np.asarray(pos, np.float32)
+    idx = []
+    stride = sx + 1
+
+    def add(a, b, c):
+        fn = np.cross(pos[b] - pos[a], pos[c] - pos[a])
+        if float(np.dot(fn, n + n + n)) < 0.0:
+            b, c = c, b
+        idx.extend((a, b, c))
+
+    for y in range(sz):
+        for x in range(sx):
+            i00 = y * stride + x
+            i10, i01 = i00 + 1, i00 + stride
+            add(i00, i01, i10)
+            add(i10, i01, i00 + stride + 1)
+    return LibMesh(positions=pos, normals=np.tile(n, (pos.shape[0], 1)), uvs=np.asarray(uv, np.float32),
+                   indices=np.asarray(idx, np.uint32))
+
+
+def c5_scene(width=3840, height=2160, shadow_size=2048, program=PROGRAM_PBR_MR, motion=True, yaw=0.0, floor_seg=16):
+    """-> (frame, draws without shadow wiring, casters, sun_dir, shadow_size).  Call
+    `wire_shadow(draws, light_viewproj)` after the shadow pass."""
+    zn, zf = 0.1, 200.0
+    ang = np.deg2rad(yaw)
+    eye = (f32(16.0 * np.sin(ang)), f32(7.0), f32(-16.0 * np.cos(ang)))
+    view = look_at_lh(eye, (0.0, 1.5, 0.0))
+    proj = perspective_lh_no(f32(np.deg2rad(60.0)), f32(width) / f32(height), zn, zf)
+    vp = mat_mul(proj, view)
+    eye_p = (f32(16.0 * np.sin(ang - 0.02)), f32(7.0), f32(-16.0 * np.cos(ang - 0.02)))
+    prev_vp = mat_mul(proj, look_at_lh(eye_p, (0.0, 1.5, 0.0)))
+    m_monkey = model_euler((0.0, 2.2, 0.0), (0.0, 0.0, 0.0), (2.0, 2.0, 2.0))
+    pm_monkey = model_euler((0.0, 2.2, 0.0), (0.0, -0.05, 0.0), (2.0, 2.0, 2.0))
+    m_floor = model_euler((0.0, 0.0, 0.0))
+    floor = make_plane(55.0, 140.0, floor_seg, floor_seg)
+    common = dict(viewproj=vp, prev_viewproj=prev_vp, light_dir_ws=SUN_DIR, light_color=(1.0, 1.0, 1.0),
+                  light_intensity=5.0, camera_pos=eye, program=program, enable_motion_vectors=motion)
+    draws = [
+        LibDraw(mesh=floor, model=m_floor, base_color=(0.6, 0.6, 0.6), metallic=0.0, roughness=0.8, ao=1.0,
+                cull_mode=CULL_NONE, **common),
+        LibDraw(mesh=monkey_lib(), model=m_monkey, prev_model=pm_monkey, base_color=(0.8, 0.5, 0.2), metallic=0.1,
+                roughness=0.5, ao=1.0, cull_mode=CULL_NONE, **common),
+    ]
+    casters = [ShadowCaster(floor, m_floor), ShadowCaster(monkey_lib(), m_monkey)]
+    frame = LibFrame(width, height, depth_motion=True, zn=zn, zf=zf, bg_gradient=True)
+    return frame, draws, casters, SUN_DIR, shadow_size
+
+
+def wire_shadow(draws, light_viewproj):
+    for d in draws:
+        d.shadow = True
+        d.light_viewproj = np.asarray(light_viewproj, np.float32)
+    return draws

@@ -110,3 +110,172 @@ def barycentric(tri6, px, py):
 def fnv1a64(arr):
     a = np.ascontiguousarray(arr)
     return int(lib().ora_fnv1a64(a.ctypes.data, a.nbytes))
+
+
+# ===== library path (shs_oracle_lib.c) ====================================================
+_F16 = ctypes.c_float * 16
+_F3 = ctypes.c_float * 3
+
+
+class OraMesh(ctypes.Structure):
+    _fields_ = [
+        ("positions", ctypes.POINTER(ctypes.c_float)),
+        ("normals", ctypes.POINTER(ctypes.c_float)),
+        ("uvs", ctypes.POINTER(ctypes.c_float)),
+        ("n_verts", ctypes.c_int32), ("n_normals", ctypes.c_int32), ("n_uvs", ctypes.c_int32),
+        ("indices", ctypes.POINTER(ctypes.c_uint32)),
+        ("n_indices", ctypes.c_int64),
+    ]
+
+
+class OraLibDraw(ctypes.Structure):
+    _fields_ = [
+        ("mesh", OraMesh),
+        ("program", ctypes.c_int32), ("cull_mode", ctypes.c_int32), ("front_face_ccw", ctypes.c_int32),
+        ("shadow", ctypes.c_int32),
+        ("model", _F16), ("viewproj", _F16), ("prev_model", _F16), ("prev_viewproj", _F16),
+        ("light_dir_ws", _F3), ("light_color", _F3), ("light_intensity", ctypes.c_float), ("camera_pos", _F3),
+        ("base_color", _F3), ("metallic", ctypes.c_float), ("roughness", ctypes.c_float), ("ao", ctypes.c_float),
+        ("light_viewproj", _F16),
+        ("shadow_bias_const", ctypes.c_float), ("shadow_bias_slope", ctypes.c_float),
+        ("shadow_pcf_radius", ctypes.c_int32),
+        ("shadow_pcf_step", ctypes.c_float), ("shadow_strength", ctypes.c_float),
+        ("enable_motion_vectors", ctypes.c_int32),
+    ]
+
+
+class OraLibTarget(ctypes.Structure):
+    _fields_ = [
+        ("W", ctypes.c_int32), ("H", ctypes.c_int32),
+        ("zn", ctypes.c_float), ("zf", ctypes.c_float),
+        ("bg_gradient", ctypes.c_int32),
+        ("clear_hdr", ctypes.c_float * 4),
+        ("hdr", ctypes.POINTER(ctypes.c_float)), ("depth", ctypes.POINTER(ctypes.c_float)),
+        ("motion", ctypes.POINTER(ctypes.c_float)),
+        ("shadow", ctypes.POINTER(ctypes.c_float)),
+        ("shadow_w", ctypes.c_int32), ("shadow_h", ctypes.c_int32),
+    ]
+
+
+class OraShadowCaster(ctypes.Structure):
+    _fields_ = [("mesh", OraMesh), ("model", _F16)]
+
+
+def _lib_lib():
+    L = lib()
+    if not getattr(L, "_lib_path_ready", False):
+        P = ctypes.c_void_p
+        L.ora_pbr_forward.restype = ctypes.c_int
+        L.ora_pbr_forward.argtypes = [ctypes.POINTER(OraLibTarget), ctypes.POINTER(OraLibDraw), ctypes.c_int, P]
+        L.ora_shadow_map.restype = ctypes.c_int
+        L.ora_shadow_map.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.POINTER(OraShadowCaster), ctypes.c_int, P, P]
+        L.ora_dir_light_camera_aabb.restype = None
+        L.ora_dir_light_camera_aabb.argtypes = [P, P, P, ctypes.c_float, ctypes.c_uint32, P, P, P]
+        L.ora_mat4_determinant.restype = ctypes.c_float
+        L.ora_mat4_determinant.argtypes = [P]
+        L._lib_path_ready = True
+    return L
+
+
+def _fill_mesh(om, mesh, keep):
+    pos = np.ascontiguousarray(mesh.positions, dtype=np.float32).reshape(-1, 3)
+    keep.append(pos)
+    om.positions = pos.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    om.n_verts = pos.shape[0]
+    if mesh.normals is not None:
+        n = np.ascontiguousarray(mesh.normals, dtype=np.float32).reshape(-1, 3)
+        keep.append(n)
+        om.normals = n.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        om.n_normals = n.shape[0]
+    if mesh.uvs is not None:
+        u = np.ascontiguousarray(mesh.uvs, dtype=np.float32).reshape(-1, 2)
+        keep.append(u)
+        om.uvs = u.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        om.n_uvs = u.shape[0]
+    if mesh.indices is not None:
+        i = np.ascontiguousarray(mesh.indices, dtype=np.uint32).reshape(-1)
+        keep.append(i)
+        om.indices = i.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        om.n_indices = i.size
+
+
+def _lib_draws(draws, keep):
+    arr = (OraLibDraw * max(len(draws), 1))()
+    for i, d in enumerate(draws):
+        a = arr[i]
+        _fill_mesh(a.mesh, d.mesh, keep)
+        a.program, a.cull_mode, a.front_face_ccw = int(d.program), int(d.cull_mode), 1 if d.front_face_ccw else 0
+        a.shadow = 1 if d.shadow else 0
+        pm = d.model if d.prev_model is None else d.prev_model
+        pv = d.viewproj if d.prev_viewproj is None else d.prev_viewproj
+        for k in range(16):
+            a.model[k], a.viewproj[k] = float(d.model[k]), float(d.viewproj[k])
+            a.prev_model[k], a.prev_viewproj[k] = float(pm[k]), float(pv[k])
+            a.light_viewproj[k] = float(d.light_viewproj[k])
+        for k in range(3):
+            a.light_dir_ws[k], a.light_color[k] = float(d.light_dir_ws[k]), float(d.light_color[k])
+            a.camera_pos[k], a.base_color[k] = float(d.camera_pos[k]), float(d.base_color[k])
+        a.light_intensity = float(d.light_intensity)
+        a.metallic, a.roughness, a.ao = float(d.metallic), float(d.roughness), float(d.ao)
+        a.shadow_bias_const, a.shadow_bias_slope = float(d.shadow_bias_const), float(d.shadow_bias_slope)
+        a.shadow_pcf_radius = int(d.shadow_pcf_radius)
+        a.shadow_pcf_step, a.shadow_strength = float(d.shadow_pcf_step), float(d.shadow_strength)
+        a.enable_motion_vectors = 1 if d.enable_motion_vectors else 0
+    return arr
+
+
+def pbr_forward(frame, draws, shadow_map=None):
+    """PassPBRForward::execute (one rasterize_mesh per draw) -> (hdr [H,W,4], depth [H,W] | None,
+    motion [H,W,2] | None, stats {tri_input, tri_after_clip, tri_raster}).  frame: shs_gpu.lib.LibFrame;
+    draws: shs_gpu.lib.LibDraw with host meshes; shadow_map: float32 [h, w] sampled by draws with shadow."""
+    keep = []
+    arr = _lib_draws(draws, keep)
+    W, H = frame.width, frame.height
+    hdr = np.empty((H, W, 4), np.float32)
+    depth = np.empty((H, W), np.float32) if frame.depth_motion else None
+    motion = np.empty((H, W, 2), np.float32) if frame.depth_motion else None
+    t = OraLibTarget()
+    t.W, t.H, t.zn, t.zf = W, H, frame.zn, frame.zf
+    t.bg_gradient = 1 if frame.bg_gradient else 0
+    for i in range(4):
+        t.clear_hdr[i] = frame.clear_hdr[i]
+    fp = ctypes.POINTER(ctypes.c_float)
+    t.hdr = hdr.ctypes.data_as(fp)
+    if depth is not None:
+        t.depth, t.motion = depth.ctypes.data_as(fp), motion.ctypes.data_as(fp)
+    if shadow_map is not None:
+        sm = np.ascontiguousarray(shadow_map, dtype=np.float32)
+        keep.append(sm)
+        t.shadow = sm.ctypes.data_as(fp)
+        t.shadow_h, t.shadow_w = sm.shape
+    st = np.zeros(3, np.uint64)
+    rc = _lib_lib().ora_pbr_forward(ctypes.byref(t), arr, len(draws), st.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"ora_pbr_forward failed: {rc}")
+    return hdr, depth, motion, {"tri_input": int(st[0]), "tri_after_clip": int(st[1]), "tri_raster": int(st[2])}
+
+
+def shadow_map(size, sun_dir, casters):
+    """PassShadowMap::execute -> (shadow map float32 [h, w], light viewproj float32[16])."""
+    w, h = (size, size) if isinstance(size, int) else size
+    keep = []
+    arr = (OraShadowCaster * max(len(casters), 1))()
+    for i, c in enumerate(casters):
+        _fill_mesh(arr[i].mesh, c.mesh, keep)
+        for k in range(16):
+            arr[i].model[k] = float(c.model[k])
+    sm = np.empty((h, w), np.float32)
+    vp = np.zeros(16, np.float32)
+    sd = np.ascontiguousarray(sun_dir, dtype=np.float32)
+    rc = _lib_lib().ora_shadow_map(w, h, sd.ctypes.data, arr, len(casters), sm.ctypes.data, vp.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"ora_shadow_map failed: {rc}")
+    return sm, vp
+
+
+def dir_light_camera_aabb(sun_dir, mn, mx, margin=10.0, res=2048):
+    v, p, vp = (np.zeros(16, np.float32) for _ in range(3))
+    a = [np.ascontiguousarray(x, dtype=np.float32) for x in (sun_dir, mn, mx)]
+    _lib_lib().ora_dir_light_camera_aabb(a[0].ctypes.data, a[1].ctypes.data, a[2].ctypes.data, margin, res,
+                                         v.ctypes.data, p.ctypes.data, vp.ctypes.data)
+    return v, p, vp

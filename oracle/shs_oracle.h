@@ -68,6 +68,76 @@ void ora_mat4_mul(const float *a, const float *b, float *out);
 /* 64-bit FNV-1a (demo_forward_classic_renderpath.cpp:1102-1116 pattern). */
 uint64_t ora_fnv1a64(const void *data, uint64_t nbytes);
 
+/* ===== Library path (shs_oracle_lib.c): shs-renderer-lib/include/shs/ ======================== */
+
+enum ora_program {                 /* the ShaderProgram the pass binds (pass_pbr_forward.hpp:100-108) */
+    ORA_PROGRAM_PBR_MR = 0,        /* make_pbr_mr_program       shader/builtin_shaders.hpp:154-214 */
+    ORA_PROGRAM_BLINN_PHONG = 1,   /* make_blinn_phong_program  :105-152                          */
+    ORA_PROGRAM_DEBUG_ALBEDO = 2,  /* make_debug_view_shader_program(Albedo|Normal|Depth) :221-245 */
+    ORA_PROGRAM_DEBUG_NORMAL = 3,
+    ORA_PROGRAM_DEBUG_DEPTH = 4
+};
+enum ora_cull { ORA_CULL_NONE = 0, ORA_CULL_BACK = 1, ORA_CULL_FRONT = 2 };  /* RasterizerCullMode */
+
+/* MeshData (resources/mesh.hpp:23-43): vec3 positions / normals, vec2 uvs, u32 indices (NULL:
+ * non-indexed soup, 3 consecutive positions per triangle).  Normals / uvs may be shorter than
+ * positions: missing entries read as (0,1,0) / (0,0) (rasterizer.hpp:196-202). */
+typedef struct ora_mesh {
+    const float *positions;
+    const float *normals;
+    const float *uvs;
+    int32_t n_verts, n_normals, n_uvs;
+    const uint32_t *indices;
+    int64_t n_indices;
+} ora_mesh;
+
+/* One rasterize_mesh call: mesh + the ShaderUniforms fields the builtin programs read
+ * (shader/types.hpp:87-116) + RasterizerConfig's cull mode / front face (rasterizer.hpp:33-40). */
+typedef struct ora_lib_draw {
+    ora_mesh mesh;
+    int32_t program, cull_mode, front_face_ccw, shadow;  /* shadow: u.shadow_map != nullptr */
+    float model[16], viewproj[16], prev_model[16], prev_viewproj[16];
+    float light_dir_ws[3], light_color[3], light_intensity, camera_pos[3];
+    float base_color[3], metallic, roughness, ao;
+    float light_viewproj[16];
+    float shadow_bias_const, shadow_bias_slope;
+    int32_t shadow_pcf_radius;
+    float shadow_pcf_step, shadow_strength;
+    int32_t enable_motion_vectors;
+} ora_lib_draw;
+
+/* RasterizerTarget: hdr (RT_ColorHDR, W*H*4 floats, rows y-up) and optionally depth_motion
+ * (RT_ColorDepthMotion depth W*H + motion W*H*2; NULL depth = no depth test).  The shadow map the
+ * programs sample (RT_ShadowDepth, shadow_w*shadow_h).  bg_gradient: PassPBRForward's no-sky
+ * background (pass_pbr_forward.hpp:71-84), else clear_hdr. */
+typedef struct ora_lib_target {
+    int32_t W, H;
+    float zn, zf;
+    int32_t bg_gradient;
+    float clear_hdr[4];
+    float *hdr, *depth, *motion;
+    const float *shadow;
+    int32_t shadow_w, shadow_h;
+} ora_lib_target;
+
+typedef struct ora_shadow_caster {   /* RenderItem with casts_shadow (scene/scene_types.hpp:78-87) */
+    ora_mesh mesh;
+    float model[16];
+} ora_shadow_caster;
+
+/* rasterize_mesh (sw_render/rasterizer.hpp:181-442); stats3 += {tri_input, tri_after_clip, tri_raster} */
+void ora_rasterize_mesh(const ora_lib_target *t, const ora_lib_draw *d, uint64_t *stats3);
+/* PassPBRForward::execute (passes/pass_pbr_forward.hpp:49-214): clears + one rasterize_mesh per draw */
+int ora_pbr_forward(const ora_lib_target *t, const ora_lib_draw *draws, int n_draws, uint64_t *stats3);
+/* PassShadowMap::execute (passes/pass_shadow_map.hpp:44-206) into sm[SW*SH]; returns the light viewproj */
+int ora_shadow_map(int SW, int SH, const float *sun_dir3, const ora_shadow_caster *casters, int n_casters, float *sm,
+                   float *light_viewproj_out);
+/* build_dir_light_camera_aabb (camera/light_camera.hpp:33-98) */
+void ora_dir_light_camera_aabb(const float *sun_dir3, const float *mn3, const float *mx3, float extra_margin,
+                               uint32_t res, float *view, float *proj, float *viewproj);
+void ora_look_at_lh(const float *eye3, const float *center3, const float *up3, float *out16);
+float ora_mat4_determinant(const float *m);
+
 #ifdef __cplusplus
 }
 #endif

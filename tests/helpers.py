@@ -28,3 +28,17 @@ def assert_color_parity(gpu_c, ref_c, gpu_pq=None, ref_pq=None):
     dp = np.abs(gpu_pq[..., :3] - ref_pq[..., :3])[diff[..., :3]] if diff[..., :3].any() else np.zeros(0)
     assert (dp <= TOL * 255.0).all(), f"pre-truncation floats differ by {dp.max()} (> {TOL * 255})"
     return n
+
+
+def assert_float_close(gpu, ref, tol=TOL, what="hdr"):
+    """Shaded floats (library path: HDR colour, motion): |gpu - ref| <= tol * max(1, |ref|) per
+    channel (north_star: within 1e-5 per channel; relative above 1 for HDR values).  Returns the
+    number of channels that are not bit-identical (libm powf ulp differences)."""
+    assert gpu.shape == ref.shape
+    assert np.isfinite(gpu).all() == np.isfinite(ref).all(), f"{what}: non-finite values differ"
+    err = np.abs(gpu.astype(np.float64) - ref.astype(np.float64))
+    lim = tol * np.maximum(1.0, np.abs(ref.astype(np.float64)))
+    bad = np.argwhere(err > lim)
+    assert bad.size == 0, (f"{what}: {len(bad)} channels off by > {tol} (max {err.max():.3g}), first at "
+                           f"{bad[:3].tolist()}: gpu={gpu[tuple(bad[0])]!r} ref={ref[tuple(bad[0])]!r}")
+    return int((gpu.view(np.uint32) != ref.view(np.uint32)).sum())
