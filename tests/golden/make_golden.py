@@ -4,7 +4,8 @@ pixel count) for fixed scenes, with every draw's uniforms stored as float32 bit 
 fixture is self-contained.  The oracle is the CPU restatement of the reference (parity unpinned:
 the reference cannot be built here and ships no fixtures for this path).
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py          (legacy_golden.json)
+       python tests/golden/make_golden.py --lib    (lib_golden.json: library path, C5-small scene)
 """
 import json
 import os
@@ -54,5 +55,22 @@ def main():
                    "frames": frames}, fh, indent=1)
 
 
+def main_lib():
+    """C5-small through the library-path oracle (PassShadowMap 128^2 + PassPBRForward 320x180)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_lib_oracle import _c5_small_outputs
+    sm, hdr, d, m, st = _c5_small_outputs(oracle)
+    rng = np.random.default_rng(0)
+    cov = np.argwhere(d < 1.0)
+    probes = cov[rng.choice(len(cov), 24, replace=False)].tolist() + [[0, 0], [179, 319]]
+    out = {"generator": "tests/golden/make_golden.py --lib", "oracle": "oracle/shs_oracle_lib.c",
+           "scene": "shs_gpu.scene_lib.c5_scene(320, 180), shadow 128", "stats": st,
+           "shadow_fnv": hex(oracle.fnv1a64(sm)), "depth_fnv": hex(oracle.fnv1a64(d)), "covered": int(len(cov)),
+           "probe_px": probes, "probe_hdr": [hdr[y, x].tolist() for y, x in probes]}
+    with open(os.path.join(HERE, "lib_golden.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("lib", st, out["covered"], out["depth_fnv"])
+
+
 if __name__ == "__main__":
-    main()
+    main_lib() if "--lib" in sys.argv else main()
