@@ -45,7 +45,10 @@ WORKLOADS = {
     "c2": "C2: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 1920x1080, 1 frame per step",
     "c1": "C1: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 800x600, 1 frame per step",
     "c3": "C3: 64-instance Suzanne grid, Phong, 1920x1080, 1 frame per step",
+    "c5": "C5: Suzanne + floor, PassShadowMap 2048^2 + PassPBRForward (PBR Cook-Torrance, PCF 5x5, motion) "
+          "3840x2160, 1 frame (both passes) per step",
 }
+LIB_CONFIGS = {"c5"}
 
 
 def algorithmic_bytes(frame, draws):
@@ -93,6 +96,72 @@ def run_gpu(args, rank, local_rank, world, dist):
     return frame, draws, stats, elapsed, n_frames, kms
 
 
+def lib_workload(args, rank=0):
+    from shs_gpu import scene_lib
+    return scene_lib.c5_scene(3840, 2160, 2048, yaw=3.0 * rank)
+
+
+def lib_mesh_bytes(mesh, with_attrs=True):
+    """Indexed MeshData bytes read once: 12 B of indices per triangle + per vertex 12 B position
+    (+ 12 B normal + 8 B uv for the camera pass)."""
+    n_v = mesh.positions.shape[0]
+    return mesh.n_tris * 12 + n_v * (32 if with_attrs else 12)
+
+
+def run_gpu_lib(args, rank, local_rank, world, dist):
+    """C5 frame = PassShadowMap + PassPBRForward (shs_render_shadow_map + shs_render_pbr_forward)."""
+    import shs_gpu
+    from shs_gpu import scene_lib
+    frame, draws, casters, sun, S = lib_workload(args, rank)
+    ctx = shs_gpu.Context(local_rank)
+    lvp = ctx.render_shadow_map(S, sun, casters)
+    scene_lib.wire_shadow(draws, lvp)
+    prepared = ctx.prepare_lib(frame, draws)
+    from shs_gpu import _abi
+    ShadowArr = _abi.ShadowCasterC * len(casters)
+    carr = ShadowArr()
+    for i, c in enumerate(casters):
+        carr[i].mesh_id = ctx.upload_lib_mesh(c.mesh)
+        for k in range(16):
+            carr[i].model[k] = float(c.model[k])
+    import ctypes
+    sd = (ctypes.c_float * 3)(*[float(x) for x in sun])
+    L = ctx._lib
+
+    def one_frame():
+        ctx._check(L.shs_render_shadow_map(ctx._h, S, S, sd, carr, len(casters), None))
+        ctx.render_pbr_forward_prepared(prepared)
+
+    for _ in range(max(args.warmup, 1)):
+        one_frame()
+    ctx.synchronize_lib()
+    stats = ctx.lib_stats()
+
+    def barrier_sync():
+        ctx.synchronize_lib()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    ctx.enable_timing(True)
+    ctx.lib_timing_reset()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_frame()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    n_passes, kms = ctx.lib_timing_read()
+    ctx.enable_timing(False)
+    ctx.close()
+    B_cam_raster = frame.width * frame.height * 28 + S * S * 4
+    B_frame = (sum(lib_mesh_bytes(d.mesh) for d in draws) + sum(lib_mesh_bytes(c.mesh, False) for c in casters)
+               + 2 * S * S * 4 + frame.width * frame.height * 28)
+    n_tri = sum(d.mesh.n_tris for d in draws)
+    return frame, stats, elapsed, n_passes["camera"], kms, B_cam_raster, B_frame, n_tri, S
+
+
 def collect_pmc(args):
     """rocprofv3 --pmc child passes (one counter per pass: FETCH_SIZE costs 3 TCC slots and
     WRITE_SIZE 2, they do not fit together).  Returns bytes per k_raster dispatch or None."""
@@ -100,6 +169,7 @@ def collect_pmc(args):
     if exe is None:
         return None, "rocprofv3 not found"
     out = {}
+    kmatch = "k_lib_raster<false>" if args.config in LIB_CONFIGS else "k_raster<"
     tmp = tempfile.mkdtemp(prefix="shs_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -117,7 +187,7 @@ def collect_pmc(args):
             for f in files:
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if "k_raster" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                        if kmatch in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                             vals.append(float(row["Counter_Value"]))
             if not vals:
                 return None, f"no k_raster rows for {counter}"
@@ -133,8 +203,32 @@ def collect_pmc(args):
     return {"fetch_kib": out["FETCH_SIZE"], "write_kib": out["WRITE_SIZE"], "bytes": traffic}, None
 
 
+def cpu_baseline_lib(args):
+    """The library-path oracle (PassShadowMap + PassPBRForward restated, sequential like the
+    reference's pass loop for these triangle sizes) on one host core, bounded sample."""
+    from oracle import oracle
+    from shs_gpu import scene_lib
+    frame, draws, casters, sun, S = lib_workload(args, 0)
+    n_tri = sum(d.mesh.n_tris for d in draws)
+    frames = 0
+    t0 = time.perf_counter()
+    while True:
+        sm, lvp = oracle.shadow_map(S, sun, casters)
+        scene_lib.wire_shadow(draws, lvp)
+        oracle.pbr_forward(frame, draws, sm)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    return {"value": round(n_tri * frames / el / 1e6, 5), "unit": "Mtri/s", "cores": 1, "kind": "port",
+            "sample": f"{frames} frames of the same workload (shadow {S}^2 + {frame.width}x{frame.height} PBR, "
+                      f"{n_tri} tris), {el:.1f} s wall, 1 thread (oracle/shs_oracle_lib.c, gcc -O3)"}
+
+
 def cpu_baseline(args):
     """The oracle (CPU restatement of the reference tile-job path) on this host, bounded sample."""
+    if args.config in LIB_CONFIGS:
+        return cpu_baseline_lib(args)
     from oracle import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     frame, draws = build_workload(args.config, 0)
@@ -171,7 +265,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     if args.child:  # profiled child: just render
-        run_gpu(args, 0, 0, 1, None)
+        (run_gpu_lib if args.config in LIB_CONFIGS else run_gpu)(args, 0, 0, 1, None)
         return
 
     pmc, pmc_err = (None, "skipped")
@@ -186,6 +280,8 @@ def main():
         dist_mod.init_process_group("nccl")
         dist = dist_mod
 
+    if args.config in LIB_CONFIGS:
+        return main_lib(args, world, rank, local_rank, dist, pmc, pmc_err)
     frame, draws, stats, elapsed, n_frames, kms = run_gpu(args, rank, local_rank, world, dist)
     B, n_tri = algorithmic_bytes(frame, draws)
 
@@ -253,6 +349,57 @@ def main():
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
         "timed_frames_with_events": n_frames,
         "roofline": roofline,
+    }
+    if world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
+    frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, S = run_gpu_lib(args, rank, local_rank, world, dist)
+    el_max = elapsed
+    covered_total = float(stats["covered_pixels"])
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t.item())
+        c = torch.tensor([covered_total], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        covered_total = float(c.item())
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    steps = args.steps
+    t_k = kms["raster"]
+    achieved = B_k / (t_k * 1e-3) / 1e9 if t_k > 0 else None
+    t_frame = sum(kms.values())
+    roofline = {"kernel": "k_lib_raster<false> (camera pass)", "bound": "hbm",
+                "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": round(pmc["bytes"]) if pmc else None, "algorithmic_bytes": B_k,
+                "kernel_ms": round(t_k, 5), "frame_kernels_ms": round(t_frame, 5),
+                "frame_algorithmic_bytes": B_frame,
+                "frame_frac": round(B_frame / (t_frame * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if t_frame > 0 else None}
+    if pmc is None:
+        roofline["traffic_note"] = pmc_err
+    line = {
+        "metric": METRIC, "value": round(world * n_tri * steps / el_max / 1e6, 3), "unit": "Mtri/s", "n_gpus": world,
+        "steps": steps, "warmup": args.warmup, "ms_per_step": round(el_max / steps * 1e3, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: Suzanne (indexed from the reference's monkey.rawobj) + make_plane floor, reference "
+                "defaults (sun normalize(0.4668,-0.3487,0.8127), intensity 5, PCF 2, bias 0.0008/0.0015)",
+        "config": {"workload": WORKLOADS[args.config], "width": frame.width, "height": frame.height,
+                   "shadow_map": S, "tris_per_frame": n_tri, "frames_per_step_per_gpu": 1,
+                   "parallelism": f"frame-parallel x{world}" if world > 1 else "single GPU"},
+        "shaded_mpix_s": round(covered_total * steps / el_max / 1e6, 3),
+        "frame_stats": stats, "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
+        "timed_frames_with_events": n_frames, "roofline": roofline,
     }
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)

@@ -230,6 +230,11 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
 int shs_resolve_lib(shs_ctx *ctx, float *hdr, float *depth, float *motion);
 int shs_get_lib_stats(shs_ctx *ctx, shs_lib_stats *stats);
 int shs_lib_device_targets(shs_ctx *ctx, void **hdr_dev, void **depth_dev, void **motion_dev);
+/* Kernel durations of the library passes enqueued since shs_lib_timing_reset while
+ * shs_enable_timing(ctx, 1) is on (HIP events on the context stream): sum_ms4 = {shadow k_lib_setup,
+ * shadow k_lib_raster, camera k_lib_setup, camera k_lib_raster}; n_passes2 = {shadow, camera} passes. */
+int shs_lib_timing_reset(shs_ctx *ctx);
+int shs_lib_timing_read(shs_ctx *ctx, double sum_ms4[4], int64_t n_passes2[2]);
 
 /* A shadow caster (RenderItem with casts_shadow): mesh + model matrix. */
 typedef struct shs_shadow_caster {

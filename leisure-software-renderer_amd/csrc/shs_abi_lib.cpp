@@ -23,7 +23,29 @@ namespace {
 
 constexpr int SCAN_MAX_PRIMS = 4096;   // smaller passes scan every primitive's box per busy tile
 
+int harvest(shs_ctx *ctx, Work &w, int k) {
+    if (!w.ring_pending[k]) return SHS_OK;
+    HIP_TRY(ctx, hipEventSynchronize(w.ring_ev[k][2]));
+    float a = 0.0f, b = 0.0f;
+    HIP_TRY(ctx, hipEventElapsedTime(&a, w.ring_ev[k][0], w.ring_ev[k][1]));
+    HIP_TRY(ctx, hipEventElapsedTime(&b, w.ring_ev[k][1], w.ring_ev[k][2]));
+    w.acc_ms[0] += a;
+    w.acc_ms[1] += b;
+    w.acc_n++;
+    w.ring_pending[k] = false;
+    return SHS_OK;
+}
+
+int harvest_all(shs_ctx *ctx, Work &w) {
+    for (int j = 0; j < Work::RING; ++j)
+        if (harvest(ctx, w, (w.ring_next + j) % Work::RING)) return SHS_ERR_HIP;
+    return SHS_OK;
+}
+
 void release_work(Work &w) {
+    for (auto &ev : w.ring_ev)
+        for (auto &e : ev)
+            if (e) { (void)hipEventDestroy(e); e = nullptr; }
     release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase);
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
     release(w.spill); release(w.blk_stat); release(w.rstat);
@@ -177,8 +199,21 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         fb.hdr = ctx->lib_hdr.p; fb.depth = ctx->lib_depth.p; fb.motion = ctx->lib_motion.p;
         fb.shadow_map = ctx->have_shadow ? ctx->shadow_map.p : nullptr;
     }
+    hipEvent_t *ev = nullptr;
+    if (ctx->timing) {
+        const int k = w.ring_next;
+        w.ring_next = (k + 1) % Work::RING;
+        if (harvest(ctx, w, k)) return SHS_ERR_HIP;
+        if (!w.ring_ev[k][0])
+            for (int i = 0; i < 3; ++i) HIP_TRY(ctx, hipEventCreateWithFlags(&w.ring_ev[k][i], hipEventDisableSystemFence));
+        ev = w.ring_ev[k];
+        w.ring_pending[k] = true;
+    }
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], ctx->stream));
     HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, ctx->stream));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], ctx->stream));
     HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, raster_grid, ctx->stream));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], ctx->stream));
     w.last_parity = fp.parity;
     w.frame_index++;
     w.last_setup_blocks = setup_blocks;
@@ -466,6 +501,30 @@ int shs_lib_device_targets(shs_ctx *ctx, void **hdr_dev, void **depth_dev, void 
     if (hdr_dev) *hdr_dev = ctx->lib_hdr.p;
     if (depth_dev) *depth_dev = ctx->lib_depth.p;
     if (motion_dev) *motion_dev = ctx->lib_motion.p;
+    return SHS_OK;
+}
+
+int shs_lib_timing_reset(shs_ctx *ctx) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (Work *w : {&ctx->lib_shadow, &ctx->lib_cam}) {
+        if (harvest_all(ctx, *w)) return SHS_ERR_HIP;
+        w->acc_ms[0] = w->acc_ms[1] = 0.0;
+        w->acc_n = 0;
+    }
+    return SHS_OK;
+}
+
+int shs_lib_timing_read(shs_ctx *ctx, double sum_ms4[4], int64_t n_passes2[2]) {
+    if (!ctx || !sum_ms4 || !n_passes2) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (harvest_all(ctx, ctx->lib_shadow) || harvest_all(ctx, ctx->lib_cam)) return SHS_ERR_HIP;
+    sum_ms4[0] = ctx->lib_shadow.acc_ms[0]; sum_ms4[1] = ctx->lib_shadow.acc_ms[1];
+    sum_ms4[2] = ctx->lib_cam.acc_ms[0]; sum_ms4[3] = ctx->lib_cam.acc_ms[1];
+    n_passes2[0] = ctx->lib_shadow.acc_n;
+    n_passes2[1] = ctx->lib_cam.acc_n;
     return SHS_OK;
 }
 

@@ -116,6 +116,13 @@ struct shs_ctx {
         uint64_t st_clip = 0, st_raster = 0, st_covered = 0, st_maxbin = 0, st_spill = 0, st_extra = 0;
         std::vector<shs_dev::LibDrawGPU> last_draws;   // host copies (re-issue on overflow)
         shs_dev::LibFrameParams last_fp{};
+        // kernel timing (ctx->timing): events before k_lib_setup, between, after k_lib_raster
+        static constexpr int RING = 64;
+        hipEvent_t ring_ev[RING][3] = {};
+        bool ring_pending[RING] = {};
+        int ring_next = 0;
+        double acc_ms[2] = {0, 0};
+        int64_t acc_n = 0;
     };
     LibWork lib_cam, lib_shadow;
     DevBuf<float4> lib_hdr;

@@ -300,6 +300,26 @@ class Context:
                                               motion.ctypes.data_as(vp) if motion is not None else None))
         return hdr, depth, motion
 
+    def synchronize_lib(self):
+        """Wait for the enqueued library passes (re-issues a pass whose capacity overflowed)."""
+        from ._abi import LibStats
+        if self._lib_frame is not None:
+            self._check(self._lib.shs_get_lib_stats(self._h, ctypes.byref(LibStats())))
+        elif self._shadow_size is not None:
+            self.resolve_shadow_map()
+
+    def lib_timing_reset(self):
+        self._check(self._lib.shs_lib_timing_reset(self._h))
+
+    def lib_timing_read(self):
+        """-> ({shadow, camera} pass counts, {kernel: mean ms}) since lib_timing_reset()."""
+        s = (ctypes.c_double * 4)()
+        n = (ctypes.c_int64 * 2)()
+        self._check(self._lib.shs_lib_timing_read(self._h, s, n))
+        ns, nc = max(n[0], 1), max(n[1], 1)
+        return {"shadow": n[0], "camera": n[1]}, {"shadow_setup": s[0] / ns, "shadow_raster": s[1] / ns,
+                                                    "setup": s[2] / nc, "raster": s[3] / nc}
+
     def lib_stats(self) -> dict:
         from ._abi import LibStats
         s = LibStats()

@@ -156,6 +156,8 @@ SIGNATURES = [
     ("shs_resolve_lib", ctypes.c_int, [_P, _P, _P, _P]),
     ("shs_get_lib_stats", ctypes.c_int, [_P, ctypes.POINTER(LibStats)]),
     ("shs_lib_device_targets", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    ("shs_lib_timing_reset", ctypes.c_int, [_P]),
+    ("shs_lib_timing_read", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     ("shs_render_shadow_map", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _F, ctypes.POINTER(ShadowCasterC),
                                              ctypes.c_int32, _F]),
     ("shs_resolve_shadow_map", ctypes.c_int, [_P, _P]),
