@@ -273,7 +273,7 @@ class Context:
 
     def prepare_lib(self, frame, draws):
         from ._abi import LibDrawC
-        from .lib import fill_draw_struct
+        from .lib_path import fill_draw_struct
         arr = (LibDrawC * max(len(draws), 1))()
         for i, d in enumerate(draws):
             fill_draw_struct(arr[i], d, d.mesh if isinstance(d.mesh, int) else self.upload_lib_mesh(d.mesh))

@@ -9,7 +9,7 @@ zn 0.1, zf 200 (scene_types.hpp:43-60), the no-material fallback (0.8,0.5,0.2) m
 """
 import numpy as np
 
-from .lib import (CULL_BACK, CULL_NONE, PROGRAM_PBR_MR, LibDraw, LibFrame, LibMesh, ShadowCaster, look_at_lh, mat_mul,
+from .lib_path import (CULL_BACK, CULL_NONE, PROGRAM_PBR_MR, LibDraw, LibFrame, LibMesh, ShadowCaster, look_at_lh, mat_mul,
                   model_euler, perspective_lh_no)
 from .scene import monkey
 

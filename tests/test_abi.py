@@ -104,3 +104,10 @@ def test_model_trs_reference_monkey():
     expect = np.diag([4.0, 4.0, 4.0, 1.0]).astype(np.float32)
     expect[3, 2] = 10.0
     assert np.array_equal(m, expect)
+
+
+def test_submodules_do_not_shadow_lib():
+    """Importing the scene / library-path helpers keeps shs_gpu.lib the loader function."""
+    import shs_gpu
+    from shs_gpu import lib_path, scene, scene_lib  # noqa: F401
+    assert callable(shs_gpu.lib) and shs_gpu.lib().shs_abi_version() == 1

@@ -14,13 +14,13 @@ f32 = np.float32
 
 
 def _tri_mesh(ndc_tris):
-    from shs_gpu.lib import LibMesh
+    from shs_gpu.lib_path import LibMesh
     pos = np.asarray(ndc_tris, np.float32).reshape(-1, 3)
     return LibMesh(pos, np.tile(np.array([0, 0, -1], np.float32), (pos.shape[0], 1)))
 
 
 def _draw(mesh, **kw):
-    from shs_gpu.lib import LibDraw
+    from shs_gpu.lib_path import LibDraw
     kw.setdefault("cull_mode", 0)
     kw.setdefault("program", 2)
     return LibDraw(mesh=mesh, **kw)
@@ -29,7 +29,7 @@ def _draw(mesh, **kw):
 def test_identity_triangle_coverage_and_ndc_depth(oracle_mod):
     """Identity viewproj: clip = world, w = 1.  No depth target -> z01 is NDC-based but unused; with a
     target and zf <= zn + 1e-6 the NDC depth z*0.5+0.5 is stored (rasterizer.hpp:347-356)."""
-    from shs_gpu.lib import LibFrame
+    from shs_gpu.lib_path import LibFrame
     tri = [(-0.5, -0.5, 0.2), (0.5, -0.5, 0.2), (0.0, 0.5, 0.2)]
     W, H = 65, 49
     hdr, d, m, st = oracle_mod.pbr_forward(LibFrame(W, H, zn=1.0, zf=1.0), [_draw(_tri_mesh(tri))])
@@ -48,7 +48,7 @@ def test_identity_triangle_coverage_and_ndc_depth(oracle_mod):
 def test_linear_view_depth():
     """w = 4 everywhere -> view_z = 1/denom = 4 (up to the rounding of u + v + w), z01 = (4 - zn) / (zf - zn)."""
     from oracle import oracle
-    from shs_gpu.lib import LibFrame
+    from shs_gpu.lib_path import LibFrame
     w = 4.0
     tri = [(-0.5 * w, -0.5 * w, 0.0), (0.5 * w, -0.5 * w, 0.0), (0.0, 0.5 * w, 0.0)]
     P = np.zeros(16, np.float32)   # x, y, z passthrough, w = 4 (constant)
@@ -65,7 +65,7 @@ def test_linear_view_depth():
 def test_cull_modes(oracle_mod, cull, ccw, flip, visible):
     """RasterizerCullMode + front_face_ccw on the screen-space signed area (rasterizer.hpp:271-278);
     screen rows are y-up, so NDC winding is screen winding."""
-    from shs_gpu.lib import LibFrame
+    from shs_gpu.lib_path import LibFrame
     tri = [(-0.5, -0.5, 0.0), (0.5, -0.5, 0.0), (0.0, 0.5, 0.0)]   # CCW
     if flip:
         tri = [tri[0], tri[2], tri[1]]
@@ -76,7 +76,7 @@ def test_cull_modes(oracle_mod, cull, ccw, flip, visible):
 
 def test_near_plane_clip_fans(oracle_mod):
     """One corner behind the near plane (z < -w): Sutherland-Hodgman yields a quad -> 2 fan triangles."""
-    from shs_gpu.lib import LibFrame
+    from shs_gpu.lib_path import LibFrame
     tri = [(-0.5, -0.5, 0.0), (0.5, -0.5, 0.0), (0.0, 0.5, -3.0)]
     _, d, _, st = oracle_mod.pbr_forward(LibFrame(48, 48, zn=1.0, zf=1.0), [_draw(_tri_mesh(tri))])
     assert st["tri_after_clip"] == 2 and st["tri_raster"] == 2
@@ -85,7 +85,7 @@ def test_near_plane_clip_fans(oracle_mod):
 
 
 def test_fully_outside_is_dropped(oracle_mod):
-    from shs_gpu.lib import LibFrame
+    from shs_gpu.lib_path import LibFrame
     tri = [(2.0, 2.0, 0.0), (3.0, 2.0, 0.0), (2.5, 3.0, 0.0)]
     _, d, _, st = oracle_mod.pbr_forward(LibFrame(16, 16), [_draw(_tri_mesh(tri))])
     assert st == {"tri_input": 1, "tri_after_clip": 0, "tri_raster": 0}
@@ -94,7 +94,7 @@ def test_fully_outside_is_dropped(oracle_mod):
 
 def test_depth_first_wins_and_painter_last_wins(oracle_mod):
     """Equal depth: strict '<' keeps the first triangle; without a depth target the last one is painted."""
-    from shs_gpu.lib import LibFrame
+    from shs_gpu.lib_path import LibFrame
     tri = [(-0.8, -0.8, 0.1), (0.8, -0.8, 0.1), (0.0, 0.8, 0.1)]
     a = _draw(_tri_mesh(tri), base_color=(1.0, 0.0, 0.0))
     b = _draw(_tri_mesh(tri), base_color=(0.0, 1.0, 0.0))
@@ -107,7 +107,7 @@ def test_depth_first_wins_and_painter_last_wins(oracle_mod):
 
 def test_background_gradient(oracle_mod):
     """PassPBRForward's no-sky background (pass_pbr_forward.hpp:71-84), row y = bottom-up index."""
-    from shs_gpu.lib import LibFrame
+    from shs_gpu.lib_path import LibFrame
     hdr, _, _, _ = oracle_mod.pbr_forward(LibFrame(8, 5), [])
     for y in range(5):
         t = f32(y) / f32(4)
@@ -117,7 +117,7 @@ def test_background_gradient(oracle_mod):
 def test_shadow_map_flat_quad(oracle_mod):
     """Sun straight down (|dir.y| > 0.95 -> up = +z): an orthographic light camera sees the quad at one
     constant depth; everything else stays at the clear value 1."""
-    from shs_gpu.lib import LibMesh, ShadowCaster
+    from shs_gpu.lib_path import LibMesh, ShadowCaster
     pos = np.array([[-1, 0, -1], [1, 0, -1], [1, 0, 1], [-1, 0, -1], [1, 0, 1], [-1, 0, 1]], np.float32)
     caster = ShadowCaster(LibMesh(pos), np.eye(4, dtype=np.float32).reshape(16))
     sm, vp = oracle_mod.shadow_map(64, (0.0, -1.0, 0.0), [caster])
@@ -129,7 +129,7 @@ def test_shadow_map_flat_quad(oracle_mod):
 def test_light_camera_host_matches_oracle(oracle_mod):
     """build_dir_light_camera_aabb: the C-ABI host helper (product) and the oracle's independent
     restatement agree bit-for-bit."""
-    from shs_gpu.lib import dir_light_camera_aabb
+    from shs_gpu.lib_path import dir_light_camera_aabb
     rng = np.random.default_rng(4)
     for _ in range(50):
         sun = rng.normal(size=3).astype(np.float32)

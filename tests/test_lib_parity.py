@@ -85,7 +85,7 @@ def _clip_soup(rng, n):
 
 
 def _camera(width, height, zn=0.5, zf=30.0):
-    from shs_gpu.lib import look_at_lh, mat_mul, perspective_lh_no
+    from shs_gpu.lib_path import look_at_lh, mat_mul, perspective_lh_no
     view = look_at_lh((0.3, 0.7, -3.0), (0.0, 0.0, 10.0))
     proj = perspective_lh_no(np.float32(np.deg2rad(60.0)), np.float32(width) / np.float32(height), zn, zf)
     return mat_mul(proj, view)
@@ -94,7 +94,7 @@ def _camera(width, height, zn=0.5, zf=30.0):
 @pytest.mark.parametrize("seed", [1, 2])
 @pytest.mark.parametrize("cull", [0, 1, 2])
 def test_clip_soup_exact(gpu_ctx, oracle_mod, seed, cull):
-    from shs_gpu.lib import LibDraw, LibFrame, LibMesh, model_euler
+    from shs_gpu.lib_path import LibDraw, LibFrame, LibMesh, model_euler
     rng = np.random.default_rng(seed)
     W, H = 331, 227
     pos, nrm, uv = _clip_soup(rng, 1200)
@@ -109,7 +109,7 @@ def test_clip_soup_exact(gpu_ctx, oracle_mod, seed, cull):
 
 def test_painter_mode_without_depth_target(gpu_ctx, oracle_mod):
     """No RT_ColorDepthMotion: every fragment writes colour, the last in submission order wins."""
-    from shs_gpu.lib import LibDraw, LibFrame, LibMesh
+    from shs_gpu.lib_path import LibDraw, LibFrame, LibMesh
     rng = np.random.default_rng(5)
     W, H = 200, 150
     pos, nrm, uv = _clip_soup(rng, 600)
@@ -123,7 +123,7 @@ def test_painter_mode_without_depth_target(gpu_ctx, oracle_mod):
 
 def test_linear_depth_off(gpu_ctx, oracle_mod):
     """zf <= zn + 1e-6: the NDC depth (z_ndc * 0.5 + 0.5) is kept (rasterizer.hpp:354)."""
-    from shs_gpu.lib import LibDraw, LibFrame, LibMesh
+    from shs_gpu.lib_path import LibDraw, LibFrame, LibMesh
     rng = np.random.default_rng(9)
     pos, nrm, uv = _clip_soup(rng, 500)
     vp = _camera(160, 120)
@@ -133,7 +133,7 @@ def test_linear_depth_off(gpu_ctx, oracle_mod):
 def test_indexed_grid_bins_mode(gpu_ctx, oracle_mod):
     """> 4096 primitives (per-tile bins), 16 indexed monkeys + floor, several draws, 2 programs."""
     from shs_gpu import scene_lib
-    from shs_gpu.lib import LibDraw, model_euler
+    from shs_gpu.lib_path import LibDraw, model_euler
     frame, draws, casters, sun, _ = scene_lib.c5_scene(512, 288)
     base = draws[1]
     for i in range(16):
