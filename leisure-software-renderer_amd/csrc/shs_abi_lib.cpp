@@ -181,6 +181,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fp.spill_cap = (uint32_t)std::min<size_t>(w.spill.cap, 0xffffffffu);
     fp.extra_cap = shadow ? 0u : w.extra_cap;
     fp.parity = w.frame_index & 1u;
+    // scan mode (every busy tile tests every primitive's box) for small passes, per-tile bins above
     fp.scan_mode = n_tris <= SCAN_MAX_PRIMS ? 1u : 0u;
     fp.setup_blocks = setup_blocks;
     const int owned_bt = (n_tiles - fp.rank + fp.count - 1) / fp.count;

@@ -158,21 +158,50 @@ __device__ __forceinline__ void lib_append_bin(const LibFrameParams &fp, const L
     }
 }
 
-// Busy marks on the owned raster tiles of [x0,x1] x [y0,y1] and (bin mode) per-bin-tile appends.
-__device__ void lib_mark(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
-                         uint32_t slot) {
+// Busy marks on the owned raster tiles of [x0,x1] x [y0,y1] and (bin mode) per-bin-tile appends,
+// tiles k0, k0 + dk, ... of the box (one thread: k0 = 0, dk = 1; a whole block: k0 = tid, dk = 256).
+__device__ void lib_mark_range(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
+                               uint32_t slot, int k0, int dk) {
     const bool sharded = fp.count > 1;
-    for (int ry = y0 / LIB_RTH; ry <= y1 / LIB_RTH; ++ry)
-        for (int rx = x0 / LIB_RTW; rx <= x1 / LIB_RTW; ++rx)
+    {
+        const int rx0 = x0 / LIB_RTW, ry0 = y0 / LIB_RTH, nx = x1 / LIB_RTW - rx0 + 1, n = nx * (y1 / LIB_RTH - ry0 + 1);
+        for (int k = k0; k < n; k += dk) {
+            const int rx = rx0 + k % nx, ry = ry0 + k / nx;
             if (!sharded || lib_owned(fp, rx, ry / (TILE / LIB_RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+        }
+    }
     if (fp.scan_mode) return;
     uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
-    for (int by = y0 / TILE; by <= y1 / TILE; ++by)
-        for (int bx = x0 / TILE; bx <= x1 / TILE; ++bx) {
-            if (sharded && !lib_owned(fp, bx, by)) continue;
-            const int t = by * fp.tiles_x + bx;
-            lib_append_bin(fp, fb, cnt, t, atomicAdd(&tcount[t], 1u), slot);
+    const int bx0 = x0 / TILE, by0 = y0 / TILE, nx = x1 / TILE - bx0 + 1, n = nx * (y1 / TILE - by0 + 1);
+    for (int k = k0; k < n; k += dk) {
+        const int bx = bx0 + k % nx, by = by0 + k / nx;
+        if (sharded && !lib_owned(fp, bx, by)) continue;
+        const int t = by * fp.tiles_x + bx;
+        lib_append_bin(fp, fb, cnt, t, atomicAdd(&tcount[t], 1u), slot);
+    }
+}
+
+// Primitives covering more than SMALL_MARK raster tiles are queued in LDS and marked by the whole
+// setup block after its triangles are done (a floor triangle at 4K spans thousands of tiles).
+constexpr int SMALL_MARK = 8;
+constexpr int BIG_CAP = 512;
+struct SetupShared {
+    uint4 big[BIG_CAP];       // (slot, bx, by, 0)
+    uint32_t nbig;
+    uint32_t stat[2];
+};
+
+__device__ void lib_mark(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
+                         uint32_t slot, SetupShared &ss) {
+    const int n_rt = (x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1);
+    if (n_rt > SMALL_MARK) {
+        const uint32_t q = atomicAdd(&ss.nbig, 1u);
+        if (q < BIG_CAP) {
+            ss.big[q] = make_uint4(slot, pack16(x0, x1), pack16(y0, y1), 0u);
+            return;
         }
+    }
+    lib_mark_range(fp, fb, cnt, x0, x1, y0, y1, slot, 0, 1);   // small, or the queue is full
 }
 
 __device__ __forceinline__ void store_box(const LibBuffers &fb, uint32_t slot, int x0, int x1, int y0, int y1) {
@@ -184,7 +213,7 @@ __device__ __forceinline__ void store_box(const LibBuffers &fb, uint32_t slot, i
 // tri_after_clip / tri_raster like the reference.
 __device__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, const LibDrawGPU &dr, int d,
                          uint32_t seq, uint32_t slot, const LVert &a, const LVert &b, const LVert &c, uint32_t &n_clip,
-                         uint32_t &n_rast) {
+                         uint32_t &n_rast, SetupShared &ss) {
     ++n_clip;
     const LVert *v[3] = {&a, &b, &c};
     float sx[3], sy[3];
@@ -244,7 +273,7 @@ __device__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_
     s.pad[0] = s.pad[1] = s.pad[2] = 0;
     fb.shade[slot] = s;
     store_box(fb, slot, x0, x1, y0, y1);
-    lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot);
+    lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot, ss);
 }
 
 __device__ __forceinline__ int lib_find_draw(const LibDrawGPU *draws, int n_draws, int gid) {
@@ -264,7 +293,7 @@ __device__ __forceinline__ bool read_tri(const LibDrawGPU &dr, int local, uint32
 
 // Camera pass: one input triangle of rasterize_mesh.
 __device__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_clip,
-                                 uint32_t &n_rast) {
+                                 uint32_t &n_rast, SetupShared &ss) {
     const int d = lib_find_draw(fb.draws, fp.n_draws, tri);
     const LibDrawGPU &dr = fb.draws[d];
     const int local = tri - dr.tri_base;
@@ -278,7 +307,7 @@ __device__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb,
     for (int k = 0; k < 3; ++k) t[k] = vertex_out(dr, id[k]);
     const uint32_t seq0 = (uint32_t)tri * 16u;
     if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
-        emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast);
+        emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast, ss);
         return;
     }
     LVert poly[MAX_POLY];
@@ -300,13 +329,14 @@ __device__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb,
     }
     for (int k = 1; k + 1 < n; ++k) {
         const uint32_t slot = k == 1 ? (uint32_t)tri : xb + (uint32_t)(k - 2);
-        emit_fan(fp, fb, cnt, dr, d, seq0 + (uint32_t)(k - 1), slot, poly[0], poly[k], poly[k + 1], n_clip, n_rast);
+        emit_fan(fp, fb, cnt, dr, d, seq0 + (uint32_t)(k - 1), slot, poly[0], poly[k], poly[k + 1], n_clip, n_rast, ss);
     }
 }
 
 // Shadow pass: one caster triangle of PassShadowMap (pass_shadow_map.hpp:155-203), draws[d].viewproj
 // holding the light camera's viewproj.  n_rast counts the triangles with a non-empty bbox.
-__device__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_rast) {
+__device__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_rast,
+                                 SetupShared &ss) {
     const int d = lib_find_draw(fb.draws, fp.n_draws, tri);
     const LibDrawGPU &dr = fb.draws[d];
     const int local = tri - dr.tri_base;
@@ -362,15 +392,16 @@ __device__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb,
     r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
     fb.recs[tri] = r;
     store_box(fb, (uint32_t)tri, x0, x1, y0, y1);
-    lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri);
+    lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri, ss);
 }
 
 template <bool SHADOW>
 __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
-    __shared__ uint32_t s_stat[2];
+    __shared__ SetupShared ss;
     const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    if (tid < 2) s_stat[tid] = 0u;
+    if (tid < 2) ss.stat[tid] = 0u;
+    if (tid == 0) ss.nbig = 0u;
     // zero the other counter set and bin counts for the next frame
     if (b == 0 && tid < LC_N) fb.counters[(fp.parity ^ 1u) * LC_N + tid] = 0u;
     {
@@ -382,19 +413,25 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
     const int tri = b * 256 + tid;
     uint32_t n_clip = 0, n_rast = 0;
     if (tri < fp.n_tris) {
-        if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast);
-        else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast);
+        if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss);
+        else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss);
     }
     for (int o = 32; o > 0; o >>= 1) {
         n_clip += __shfl_down(n_clip, o);
         n_rast += __shfl_down(n_rast, o);
     }
     if (__lane_id() == 0) {
-        atomicAdd(&s_stat[0], n_clip);
-        atomicAdd(&s_stat[1], n_rast);
+        atomicAdd(&ss.stat[0], n_clip);
+        atomicAdd(&ss.stat[1], n_rast);
     }
     __syncthreads();
-    if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(s_stat[0], s_stat[1]);
+    // the block's large primitives: every thread takes every 256th of their tiles
+    const uint32_t nbig = min(ss.nbig, (uint32_t)BIG_CAP);
+    for (uint32_t i = 0; i < nbig; ++i) {
+        const uint4 e = ss.big[i];
+        lib_mark_range(fp, fb, cnt, lo16(e.y), hi16(e.y), lo16(e.z), hi16(e.z), e.x, tid, 256);
+    }
+    if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(ss.stat[0], ss.stat[1]);
 }
 
 // ---- k_lib_raster -----------------------------------------------------------------------------
@@ -560,6 +597,9 @@ __device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
     return r;
 }
 
+__device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
+                                         const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv);
+
 // Resolve one pixel of a tile (one thread): the winner of the key array is re-evaluated with the
 // identical arithmetic, shaded and written; pixels without a winner get the clear values.
 template <bool SHADOW>
@@ -581,7 +621,23 @@ __device__ __forceinline__ void lib_resolve(const LibFrameParams &fp, const LibB
         const uint32_t slot = k == 0 ? tri : fb.xbase[tri] + k - 1u;
         const LibRec r = fb.recs[slot];
         const LibShade s = fb.shade[slot];
-        const LibDrawGPU &dr = fb.draws[s.draw];
+        // a wave whose covered pixels share one draw reads its uniforms with scalar loads
+        const int d0 = __builtin_amdgcn_readfirstlane(s.draw);
+        if (__ballot(s.draw != d0) == 0) shade_px(fp, fb, fb.draws[d0], r, s, px, py, color, depth, mv);
+        else shade_px(fp, fb, fb.draws[s.draw], r, s, px, py, color, depth, mv);
+    }
+    fb.hdr[o] = color;
+    if (fp.flags & LF_DEPTH) {
+        fb.depth[o] = depth;
+        fb.motion[o] = mv;
+    }
+}
+
+// The winner of one pixel: identical re-evaluation of the pixel test, the varyings, motion and the
+// fragment program (rasterizer.hpp:341-419).
+__device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
+                                         const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv) {
+    {
         float z01, u, v, w, idn;
         lib_test<false>(fp, r, px, py, z01, u, v, w, idn);
         depth = z01;
@@ -609,11 +665,6 @@ __device__ __forceinline__ void lib_resolve(const LibFrameParams &fp, const LibB
         }
         const f3 c = lib_fragment(fp, fb, dr, world, nrm, z01);
         color = make_float4(c.x, c.y, c.z, 1.0f);
-    }
-    fb.hdr[o] = color;
-    if (fp.flags & LF_DEPTH) {
-        fb.depth[o] = depth;
-        fb.motion[o] = mv;
     }
 }
 
