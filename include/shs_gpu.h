@@ -249,6 +249,51 @@ int shs_render_shadow_map(shs_ctx *ctx, int32_t w, int32_t h, const float sun_di
                           int32_t n_casters, float light_viewproj_out[16]);
 int shs_resolve_shadow_map(shs_ctx *ctx, float *depth);
 
+/* ---- Forward+ light-list binning ---------------------------------------
+ * CullingLightGPU (lighting/light_types.hpp:141-166), the std430 record the reference uploads for
+ * its GPU light culling; 160 B. */
+typedef struct shs_culling_light {
+    float position_range[4];      /* xyz position, w range                                       */
+    float color_intensity[4];
+    float direction_spot[4];
+    float axis_spot_outer[4];
+    float up_shape_x[4];
+    float shape_attenuation[4];   /* x shape, y attenuation power, z bias, w cutoff              */
+    uint32_t type_shape_flags[4]; /* x LightType, y culling shape, z flags, w attenuation model   */
+    float cull_sphere[4];
+    float cull_aabb_min[4];
+    float cull_aabb_max[4];
+} shs_culling_light;
+
+#define SHS_LIGHT_CULL_NONE 0         /* culling_mode of fp_stress_light_cull.comp             */
+#define SHS_LIGHT_CULL_TILED 1
+#define SHS_LIGHT_CULL_TILED_DEPTH 2  /* tiles + per-tile depth range (fp_stress_depth_reduce) */
+#define SHS_LIGHT_CULL_CLUSTERED 3
+
+/* The CameraUBO fields the culling reads.  depth_linear: the depth range of mode 2 is reduced from
+ * the context's library depth buffer (linear view depth, rasterizer.hpp:354-357); 0 = perspective
+ * LH_NO depth as the Vulkan depth_reduce shader assumes.  shard_rank / shard_count: only the lists of
+ * owned 32x32 tiles are built (others get count 0). */
+typedef struct shs_light_cull_desc {
+    int32_t width, height;
+    uint32_t tile_size, max_per_tile, mode, z_slices;
+    float view[16], proj[16];
+    float zn, zf;
+    int32_t depth_linear;
+    int32_t shard_rank, shard_count;
+} shs_light_cull_desc;
+
+/* Upload the frame's local light set (replaces the LightBuffer SSBO). */
+int shs_lights_upload(shs_ctx *ctx, const shs_culling_light *lights, int32_t n_lights);
+/* fp_stress_light_cull.comp (+ fp_stress_depth_reduce.comp for mode 2, over the last library depth)
+ * into device tile lists: counts[n_lists], indices[n_lists * max_per_tile], ascending light index.
+ * Draws with SHS_PROGRAM_FORWARD_PLUS read these lists. */
+int shs_light_cull(shs_ctx *ctx, const shs_light_cull_desc *desc);
+/* counts: n_lists; indices: n_lists * max_per_tile (entries past the count are undefined); ranges:
+ * tiles * 2 floats (mode 2).  Any pointer may be NULL. */
+int shs_resolve_light_lists(shs_ctx *ctx, uint32_t *counts, uint32_t *indices, float *ranges);
+#define SHS_PROGRAM_FORWARD_PLUS 5  /* per-pixel point lights from the tile lists (light_runtime.hpp:321-333) */
+
 /* Host GLM restatements for non-C++ callers (camera/convention.hpp; pass_pbr_forward.hpp:136-141). */
 int shs_look_at_lh(const float eye[3], const float center[3], const float up[3], float out16[16]);
 int shs_perspective_lh_no(float fovy_radians, float aspect, float zn, float zf, float out16[16]);

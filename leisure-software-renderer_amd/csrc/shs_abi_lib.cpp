@@ -13,6 +13,7 @@
 #include "shs_glm.hpp"
 #include "shs_lib_device.hpp"
 #include "shs_lib_internal.hpp"
+#include "shs_light_internal.hpp"
 
 using shs_dev::LibBuffers;
 using shs_dev::LibDrawGPU;
@@ -199,6 +200,9 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     } else {
         fb.hdr = ctx->lib_hdr.p; fb.depth = ctx->lib_depth.p; fb.motion = ctx->lib_motion.p;
         fb.shadow_map = ctx->have_shadow ? ctx->shadow_map.p : nullptr;
+        fb.lights = ctx->lights.p;
+        fb.tile_counts = ctx->list_counts.p;
+        fb.tile_indices = ctx->list_indices.p;
     }
     hipEvent_t *ev = nullptr;
     if (ctx->timing) {
@@ -293,6 +297,8 @@ void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_cam);
     release_work(ctx->lib_shadow);
     release(ctx->lib_hdr); release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
+    release(ctx->lights); release(ctx->light_proj); release(ctx->depth_ranges);
+    release(ctx->list_counts); release(ctx->list_indices);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
 }
@@ -415,7 +421,12 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     if (f.shard_count <= 0 || f.shard_rank < 0 || f.shard_rank >= f.shard_count) { ctx->err = "bad shard"; return SHS_ERR_INVALID; }
     for (int i = 0; i < n_draws; ++i) {
         if (check_lib_mesh(ctx, draws[i].mesh_id)) return SHS_ERR_INVALID;
-        if (draws[i].program < SHS_PROGRAM_PBR_MR || draws[i].program > SHS_PROGRAM_DEBUG_DEPTH) { ctx->err = "bad program"; return SHS_ERR_INVALID; }
+        if (draws[i].program < SHS_PROGRAM_PBR_MR || draws[i].program > SHS_PROGRAM_FORWARD_PLUS) { ctx->err = "bad program"; return SHS_ERR_INVALID; }
+        if (draws[i].program == SHS_PROGRAM_FORWARD_PLUS &&
+            (!ctx->have_cull || ctx->cull.W != f.width || ctx->cull.H != f.height)) {
+            ctx->err = "Forward+ draw needs shs_light_cull for this frame size";
+            return SHS_ERR_INVALID;
+        }
         if (draws[i].cull_mode < SHS_CULL_NONE || draws[i].cull_mode > SHS_CULL_FRONT) { ctx->err = "bad cull mode"; return SHS_ERR_INVALID; }
         if (draws[i].shadow && !ctx->have_shadow) { ctx->err = "draw samples a shadow map but none was rendered"; return SHS_ERR_INVALID; }
     }
@@ -447,6 +458,13 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     fp.zn = f.zn; fp.zf = f.zf; fp.zspan = f.zf - f.zn;
     for (int i = 0; i < 4; ++i) fp.clear[i] = f.clear_hdr[i];
     fp.sm_w = ctx->shadow_w; fp.sm_h = ctx->shadow_h;
+    if (ctx->have_cull) {
+        const shs_dev::LightCullParams &c = ctx->cull;
+        fp.lt_size = c.tile_size; fp.lt_tx = c.tiles_x; fp.lt_ty = c.tiles_y; fp.lt_maxp = c.max_per_tile;
+        fp.lt_mode = c.mode; fp.lt_zs = c.z_slices; fp.n_lights = c.n_lights;
+        fp.lt_view_z[0] = c.view[2]; fp.lt_view_z[1] = c.view[6]; fp.lt_view_z[2] = c.view[10]; fp.lt_view_z[3] = c.view[14];
+        fp.lt_zn = c.zn; fp.lt_zf = c.zf;
+    }
     wk.last_fp = fp;
     ctx->lib_frame = f;
     ctx->cam_after_shadow = ctx->have_shadow;
@@ -502,6 +520,69 @@ int shs_lib_device_targets(shs_ctx *ctx, void **hdr_dev, void **depth_dev, void 
     if (hdr_dev) *hdr_dev = ctx->lib_hdr.p;
     if (depth_dev) *depth_dev = ctx->lib_depth.p;
     if (motion_dev) *motion_dev = ctx->lib_motion.p;
+    return SHS_OK;
+}
+
+int shs_lights_upload(shs_ctx *ctx, const shs_culling_light *lights, int32_t n) {
+    static_assert(sizeof(shs_culling_light) == sizeof(shs_dev::CullLight), "CullingLightGPU layout");
+    if (!ctx || n < 0 || (n > 0 && !lights)) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    if (ensure(ctx, ctx->lights, (size_t)std::max(n, 1))) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // the previous set may still be read
+    if (n > 0) HIP_TRY(ctx, hipMemcpy(ctx->lights.p, lights, (size_t)n * sizeof(shs_dev::CullLight), hipMemcpyHostToDevice));
+    ctx->n_lights = n;
+    return SHS_OK;
+}
+
+int shs_light_cull(shs_ctx *ctx, const shs_light_cull_desc *d) {
+    if (!ctx || !d) return SHS_ERR_INVALID;
+    if (d->width <= 0 || d->height <= 0 || d->tile_size == 0 || d->max_per_tile == 0 || d->mode > 3u ||
+        (d->mode == 3u && d->z_slices == 0) || d->shard_count <= 0 || d->shard_rank < 0 || d->shard_rank >= d->shard_count) {
+        ctx->err = "bad light cull description";
+        return SHS_ERR_INVALID;
+    }
+    if (d->mode == 2u && (!ctx->have_lib_frame || !(ctx->lib_frame.flags & SHS_LIB_DEPTH_MOTION) ||
+                          ctx->lib_frame.width != d->width || ctx->lib_frame.height != d->height)) {
+        ctx->err = "tiled-depth culling needs a library frame with a depth target of the same size";
+        return SHS_ERR_INVALID;
+    }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    shs_dev::LightCullParams p;
+    std::memset(&p, 0, sizeof p);
+    p.W = d->width; p.H = d->height;
+    p.tile_size = d->tile_size; p.max_per_tile = d->max_per_tile; p.mode = d->mode;
+    p.z_slices = std::max(d->z_slices, 1u);
+    p.tiles_x = (d->width + d->tile_size - 1) / d->tile_size;
+    p.tiles_y = (d->height + d->tile_size - 1) / d->tile_size;
+    p.n_lists = p.tiles_x * p.tiles_y * (d->mode == 3u ? p.z_slices : 1u);
+    p.n_lights = (uint32_t)ctx->n_lights;
+    p.zn = d->zn; p.zf = d->zf;
+    p.depth_linear = d->depth_linear;
+    p.rank = d->shard_rank; p.count = d->shard_count;
+    std::memcpy(p.view, d->view, sizeof p.view);
+    std::memcpy(p.proj, d->proj, sizeof p.proj);
+    if (ensure(ctx, ctx->light_proj, 2 * (size_t)std::max(ctx->n_lights, 1)) ||
+        ensure(ctx, ctx->depth_ranges, (size_t)p.tiles_x * p.tiles_y) || ensure(ctx, ctx->list_counts, p.n_lists) ||
+        ensure(ctx, ctx->list_indices, (size_t)p.n_lists * p.max_per_tile) || ensure(ctx, ctx->lights, 1))
+        return SHS_ERR_HIP;
+    HIP_TRY(ctx, shs_internal::launch_light_cull(p, ctx->lights.p, ctx->light_proj.p, ctx->lib_depth.p, ctx->depth_ranges.p,
+                                                 ctx->list_counts.p, ctx->list_indices.p, ctx->stream));
+    ctx->cull = p;
+    ctx->have_cull = true;
+    return SHS_OK;
+}
+
+int shs_resolve_light_lists(shs_ctx *ctx, uint32_t *counts, uint32_t *indices, float *ranges) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (!ctx->have_cull) { ctx->err = "no light cull run"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const shs_dev::LightCullParams &p = ctx->cull;
+    if (counts) HIP_TRY(ctx, hipMemcpy(counts, ctx->list_counts.p, p.n_lists * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (indices)
+        HIP_TRY(ctx, hipMemcpy(indices, ctx->list_indices.p, (size_t)p.n_lists * p.max_per_tile * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (ranges)
+        HIP_TRY(ctx, hipMemcpy(ranges, ctx->depth_ranges.p, (size_t)p.tiles_x * p.tiles_y * sizeof(float2), hipMemcpyDeviceToHost));
     return SHS_OK;
 }
 

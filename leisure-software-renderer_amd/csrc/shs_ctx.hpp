@@ -134,6 +134,14 @@ struct shs_ctx {
     shs_lib_frame lib_frame{};
     bool have_lib_frame = false, have_shadow = false, cam_after_shadow = false;
     uint32_t *h_lib_counters = nullptr;   // pinned, LC_N
+    // Forward+ light lists (shs_light.hip)
+    DevBuf<shs_dev::CullLight> lights;
+    int32_t n_lights = 0;
+    DevBuf<float4> light_proj;
+    DevBuf<float2> depth_ranges;
+    DevBuf<uint32_t> list_counts, list_indices;
+    shs_dev::LightCullParams cull{};
+    bool have_cull = false;
 };
 
 #define HIP_TRY(ctx, expr)                                                                       \

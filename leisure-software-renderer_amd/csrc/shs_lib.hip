@@ -514,9 +514,88 @@ __device__ f3 fake_ibl(f3 N, f3 V, f3 base, float metallic, float roughness, flo
     return sc3(add3(diffuse_ibl, spec_ibl), s_clamp(ao, 0.0f, 1.0f));
 }
 
+// eval_distance_attenuation (lighting/light_runtime.hpp:182-210) on a CullingLightGPU
+__device__ __forceinline__ float distance_attenuation(const CullLight &L, float distance) {
+    const float range = s_max(L.position_range[3], 0.001f);
+    if (distance >= range) return 0.0f;
+    const float norm = s_clamp(1.0f - distance / range, 0.0f, 1.0f);
+    float falloff = 0.0f;
+    const uint32_t model = L.type_shape_flags[3];
+    if (model == 0u) {
+        falloff = norm;
+    } else if (model == 1u) {
+        falloff = (norm * norm) * (3.0f - 2.0f * norm);
+    } else if (model == 2u) {
+        const float inv = 1.0f / s_max(distance * distance, L.shape_attenuation[2]);
+        falloff = s_min(1.0f, inv * (range * range)) * (norm * norm);
+    }
+    falloff = powf(s_max(falloff, 0.0f), s_max(L.shape_attenuation[1], 0.001f));
+    if (L.shape_attenuation[3] > 0.0f && falloff < L.shape_attenuation[3]) return 0.0f;
+    return s_max(falloff, 0.0f);
+}
+
+// PointLightModel::sample + eval_local_light_brdf (light_runtime.hpp:212-237, 321-333), accumulated
+// as lit += base * diffuse + specular (exp-plumbing/hello_light_types_culling_sw.cpp:414).
+__device__ __forceinline__ void point_light(const CullLight &L, f3 world, f3 N, f3 V, f3 base, f3 &lit) {
+    const f3 tl = {L.position_range[0] - world.x, L.position_range[1] - world.y, L.position_range[2] - world.z};
+    const float dist = sqrtf(dot3(tl, tl));
+    if (dist <= 1e-4f || dist > L.position_range[3]) return;
+    const f3 Ld = {tl.x / dist, tl.y / dist, tl.z / dist};
+    const float ndotl = s_max(dot3(N, Ld), 0.0f);
+    if (ndotl <= 0.0f) return;
+    const float att = distance_attenuation(L, dist) * s_max(1.0f, 0.0f);
+    if (att <= 0.0f) return;
+    const float ci = s_max(L.color_intensity[3], 0.0f);
+    const f3 rad = {(s_max(L.color_intensity[0], 0.0f) * ci) * att, (s_max(L.color_intensity[1], 0.0f) * ci) * att,
+                    (s_max(L.color_intensity[2], 0.0f) * ci) * att};
+    f3 h = add3(Ld, V);
+    const float len2 = dot3(h, h);
+    h = len2 <= 1e-10f ? Ld : sc3(h, 1.0f / sqrtf(len2));                     // normalize_or(L + V, L)
+    const float spec = 0.30f * powf(s_max(dot3(N, h), 0.0f), 36.0f);
+    lit = add3(lit, add3(mul3(base, sc3(rad, ndotl)), sc3(rad, spec)));
+}
+
+// Forward+ program: the pixel's light list (fp_stress_scene.frag:644-685 selection: a saturated list
+// falls back to every light) through PointLightModel::sample, combined as the software light-culling
+// demo does (hello_light_types_culling_sw.cpp:404-416): ambient hemisphere + sum, clamped to [0,1].
+__device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, int px, int py) {
+    const f3 N = normalize3(nrm);
+    f3 V = sub3(f3{dr.cam[0], dr.cam[1], dr.cam[2]}, world);
+    const float vl2 = dot3(V, V);
+    V = vl2 <= 1e-10f ? f3{0.0f, 0.0f, 1.0f} : sc3(V, 1.0f / sqrtf(vl2));        // normalize_or
+    const float hemi = 0.5f + 0.5f * s_clamp(N.y, -1.0f, 1.0f);
+    const float amb = 0.22f + 0.12f * hemi;                                     // kAmbientBase / kAmbientHemi
+    const f3 base = {dr.base[0], dr.base[1], dr.base[2]};
+    f3 lit = sc3(base, amb);
+    const uint32_t ts = fp.lt_size, maxp = fp.lt_maxp;
+    const uint32_t tx = min((uint32_t)px / ts, fp.lt_tx - 1u), ty = min((uint32_t)(fp.H - 1 - py) / ts, fp.lt_ty - 1u);
+    uint32_t list = ty * fp.lt_tx + tx;
+    if (fp.lt_mode == 3u) {   // cluster_slice_from_view_depth (fp_stress_scene.frag:525-533)
+        const float vz = (fp.lt_view_z[0] * world.x + fp.lt_view_z[1] * world.y) + (fp.lt_view_z[2] * world.z + fp.lt_view_z[3] * 1.0f);
+        const float near_z = s_max(fp.lt_zn, 0.001f), far_z = s_max(fp.lt_zf, near_z + 0.01f);
+        const float d = g_clamp(s_max(0.001f, vz), near_z, far_z);
+        const float t = logf(d / near_z) / s_max(logf(far_z / near_z), 1e-6f);
+        const float zi = g_clamp(floorf(t * (float)fp.lt_zs), 0.0f, (float)(fp.lt_zs - 1u));
+        list = ((uint32_t)zi * fp.lt_ty + ty) * fp.lt_tx + tx;
+    }
+    const uint32_t count = fp.lt_mode == 0u ? maxp : min(fb.tile_counts[list], maxp);
+    if (count >= maxp) {
+        for (uint32_t i = 0; i < fp.n_lights; ++i) point_light(fb.lights[i], world, N, V, base, lit);
+    } else {
+        const uint32_t *ids = fb.tile_indices + (size_t)list * maxp;
+        for (uint32_t i = 0; i < count; ++i) {
+            const uint32_t idx = ids[i];
+            if (idx < fp.n_lights) point_light(fb.lights[idx], world, N, V, base, lit);
+        }
+    }
+    return f3{g_clamp(lit.x, 0.0f, 1.0f), g_clamp(lit.y, 0.0f, 1.0f), g_clamp(lit.z, 0.0f, 1.0f)};
+}
+
 // The builtin fragment programs (builtin_shaders.hpp:105-245); no base_color_tex -> albedo_tex = 1.
-__device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, float depth01) {
+__device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, float depth01,
+                           int px, int py) {
     const f3 bc = {dr.base[0], dr.base[1], dr.base[2]};
+    if (dr.program == 5) return forward_plus(fp, fb, dr, world, nrm, px, py);
     if (dr.program == 2) return bc;                                                   // debug albedo
     if (dr.program == 3) return add3(sc3(normalize3(nrm), 0.5f), f3{0.5f, 0.5f, 0.5f});  // debug normal
     if (dr.program == 4) {                                                            // debug depth
@@ -663,7 +742,7 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
                 mv = make_float2(vx, vy);
             }
         }
-        const f3 c = lib_fragment(fp, fb, dr, world, nrm, z01);
+        const f3 c = lib_fragment(fp, fb, dr, world, nrm, z01, px, py);
         color = make_float4(c.x, c.y, c.z, 1.0f);
     }
 }

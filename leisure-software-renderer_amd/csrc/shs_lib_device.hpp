@@ -55,6 +55,27 @@ struct alignas(16) LibShade {
 };
 static_assert(sizeof(LibShade) == 112, "LibShade must stay 112 B");
 
+// CullingLightGPU (lighting/light_types.hpp:141-166), 160 B, as the caller uploads it.
+struct alignas(16) CullLight {
+    float position_range[4], color_intensity[4], direction_spot[4], axis_spot_outer[4], up_shape_x[4];
+    float shape_attenuation[4];
+    uint32_t type_shape_flags[4];
+    float cull_sphere[4], cull_aabb_min[4], cull_aabb_max[4];
+};
+static_assert(sizeof(CullLight) == 160, "CullingLightGPU is 160 B");
+
+// The light-list binning's view of the frame (CameraUBO fields of fp_stress_light_cull.comp).
+struct LightCullParams {
+    int32_t W, H;
+    uint32_t tile_size, max_per_tile, mode, z_slices;   // mode 0 none, 1 tiled, 2 tiled depth range, 3 clustered
+    uint32_t tiles_x, tiles_y, n_lists, n_lights;
+    float zn, zf;
+    int32_t depth_linear;                               // depth input: library linear view depth
+    int32_t rank, count;                                // lists of owned 32x32 bin tiles only (tile sharding)
+    int32_t pad;
+    float view[16], proj[16];
+};
+
 constexpr uint32_t LF_DEPTH = 1u;       // target.depth_motion present: strict-less z test, depth written
 constexpr uint32_t LF_LINZ = 2u;        // ... with zf > zn + 1e-6: linear view depth
 constexpr uint32_t LF_MOTION = 4u;      // motion buffer written (per draw: enable_motion_vectors)
@@ -76,6 +97,10 @@ struct LibFrameParams {
     uint32_t parity, scan_mode;
     int32_t setup_blocks, n_owned_rt;
     int32_t sm_w, sm_h;              // shadow map sampled by the programs
+    // Forward+ program: the light lists of the last shs_light_cull
+    uint32_t lt_size, lt_tx, lt_ty, lt_maxp, lt_mode, lt_zs, n_lights;
+    float lt_view_z[4];              // view matrix row 2 (view-space z, cluster slice)
+    float lt_zn, lt_zf;              // the light cull's depth_params
 };
 
 struct LibBuffers {
@@ -94,6 +119,8 @@ struct LibBuffers {
     float *depth;                    // W*H (RT_ColorDepthMotion depth / RT_ShadowDepth)
     float2 *motion;                  // W*H
     const float *shadow_map;         // sampled by the camera pass (sm_w * sm_h)
+    const CullLight *lights;         // Forward+ program
+    const uint32_t *tile_counts, *tile_indices;
 };
 
 }  // namespace shs_dev

@@ -308,6 +308,30 @@ class Context:
         elif self._shadow_size is not None:
             self.resolve_shadow_map()
 
+    def upload_lights(self, lights):
+        """lights: numpy LIGHT_DTYPE array (CullingLightGPU records)."""
+        from ._abi import CullingLightC
+        arr = np.ascontiguousarray(lights)
+        self._check(self._lib.shs_lights_upload(self._h, arr.ctypes.data_as(ctypes.POINTER(CullingLightC)), arr.shape[0]))
+        self._n_lights = arr.shape[0]
+
+    def light_cull(self, cull):
+        """fp_stress_light_cull.comp (+ depth reduce for mode 2) into the context's tile lists."""
+        self._cull = cull
+        self._check(self._lib.shs_light_cull(self._h, ctypes.byref(cull.desc())))
+
+    def resolve_light_lists(self):
+        """-> (counts uint32[n_lists], indices uint32[n_lists, max_per_tile], ranges float32[tiles, 2])."""
+        c = self._cull
+        counts = np.empty(c.n_lists, np.uint32)
+        idx = np.empty((c.n_lists, c.max_per_tile), np.uint32)
+        tx, ty = c.tiles
+        ranges = np.empty((ty * tx, 2), np.float32)
+        vp = ctypes.c_void_p
+        self._check(self._lib.shs_resolve_light_lists(self._h, counts.ctypes.data_as(vp), idx.ctypes.data_as(vp),
+                                                      ranges.ctypes.data_as(vp)))
+        return counts, idx, ranges
+
     def lib_timing_reset(self):
         self._check(self._lib.shs_lib_timing_reset(self._h))
 

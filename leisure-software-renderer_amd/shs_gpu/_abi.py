@@ -120,6 +120,25 @@ class ShadowCasterC(ctypes.Structure):
     _fields_ = [("mesh_id", ctypes.c_int32), ("model", _F16)]
 
 
+PROGRAM_FORWARD_PLUS = 5
+LIGHT_CULL_NONE, LIGHT_CULL_TILED, LIGHT_CULL_TILED_DEPTH, LIGHT_CULL_CLUSTERED = 0, 1, 2, 3
+_F4 = ctypes.c_float * 4
+
+
+class CullingLightC(ctypes.Structure):
+    """CullingLightGPU (lighting/light_types.hpp:141-166), 160 B."""
+    _fields_ = [("position_range", _F4), ("color_intensity", _F4), ("direction_spot", _F4), ("axis_spot_outer", _F4),
+                ("up_shape_x", _F4), ("shape_attenuation", _F4), ("type_shape_flags", ctypes.c_uint32 * 4),
+                ("cull_sphere", _F4), ("cull_aabb_min", _F4), ("cull_aabb_max", _F4)]
+
+
+class LightCullDescC(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("tile_size", ctypes.c_uint32),
+                ("max_per_tile", ctypes.c_uint32), ("mode", ctypes.c_uint32), ("z_slices", ctypes.c_uint32),
+                ("view", _F16), ("proj", _F16), ("zn", ctypes.c_float), ("zf", ctypes.c_float),
+                ("depth_linear", ctypes.c_int32), ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32)]
+
+
 # (name, restype, argtypes) for every symbol include/shs_gpu.h declares.
 _P = ctypes.c_void_p
 _F = ctypes.POINTER(ctypes.c_float)
@@ -161,6 +180,9 @@ SIGNATURES = [
     ("shs_render_shadow_map", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _F, ctypes.POINTER(ShadowCasterC),
                                              ctypes.c_int32, _F]),
     ("shs_resolve_shadow_map", ctypes.c_int, [_P, _P]),
+    ("shs_lights_upload", ctypes.c_int, [_P, ctypes.POINTER(CullingLightC), ctypes.c_int32]),
+    ("shs_light_cull", ctypes.c_int, [_P, ctypes.POINTER(LightCullDescC)]),
+    ("shs_resolve_light_lists", ctypes.c_int, [_P, _P, _P, _P]),
     ("shs_look_at_lh", ctypes.c_int, [_F, _F, _F, _F]),
     ("shs_perspective_lh_no", ctypes.c_int, [ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F]),
     ("shs_model_euler", ctypes.c_int, [_F, _F, _F, _F]),

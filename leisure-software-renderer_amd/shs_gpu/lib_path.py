@@ -12,8 +12,9 @@ from typing import Optional
 import numpy as np
 
 from . import _abi
-from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, LIB_BG_GRADIENT, LIB_DEPTH_MOTION, PROGRAM_BLINN_PHONG,
-                   PROGRAM_DEBUG_ALBEDO, PROGRAM_DEBUG_DEPTH, PROGRAM_DEBUG_NORMAL, PROGRAM_PBR_MR)
+from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, LIB_BG_GRADIENT, LIB_DEPTH_MOTION, LIGHT_CULL_CLUSTERED,
+                   LIGHT_CULL_NONE, LIGHT_CULL_TILED, LIGHT_CULL_TILED_DEPTH, PROGRAM_BLINN_PHONG, PROGRAM_DEBUG_ALBEDO,
+                   PROGRAM_DEBUG_DEPTH, PROGRAM_DEBUG_NORMAL, PROGRAM_FORWARD_PLUS, PROGRAM_PBR_MR)
 
 __all__ = [
     "LibMesh", "LibDraw", "LibFrame", "ShadowCaster", "PROGRAM_PBR_MR", "PROGRAM_BLINN_PHONG", "PROGRAM_DEBUG_ALBEDO",
@@ -94,6 +95,87 @@ class LibFrame:
 class ShadowCaster:
     mesh: object
     model: np.ndarray
+
+
+# CullingLightGPU (lighting/light_types.hpp:141-166) as a numpy record (160 B, the C-ABI layout)
+LIGHT_DTYPE = np.dtype([("position_range", "<f4", 4), ("color_intensity", "<f4", 4), ("direction_spot", "<f4", 4),
+                        ("axis_spot_outer", "<f4", 4), ("up_shape_x", "<f4", 4), ("shape_attenuation", "<f4", 4),
+                        ("type_shape_flags", "<u4", 4), ("cull_sphere", "<f4", 4), ("cull_aabb_min", "<f4", 4),
+                        ("cull_aabb_max", "<f4", 4)])
+assert LIGHT_DTYPE.itemsize == 160
+
+LIGHT_FLAGS_DEFAULT = 1 | 2 | 4      # LightFlagsDefault (light_types.hpp:56-63)
+ATTEN_LINEAR, ATTEN_SMOOTH, ATTEN_INVERSE_SQUARE = 0, 1, 2
+
+
+def make_point_lights(pos, rng_range, color, intensity, attenuation_model=ATTEN_SMOOTH, power=1.0, bias=0.05,
+                      cutoff=0.0, flags=LIGHT_FLAGS_DEFAULT):
+    """make_point_culling_light (light_types.hpp:327-349) over arrays: pos [n,3], range [n], color [n,3],
+    intensity [n] -> LIGHT_DTYPE [n] (make_light_common's clamps included, light_runtime.hpp:167-180)."""
+    f = np.float32
+    pos = np.asarray(pos, f).reshape(-1, 3)
+    n = pos.shape[0]
+    rng_range = np.maximum(np.asarray(rng_range, f).reshape(n), f(0.001))           # make_light_common
+    color = np.maximum(np.asarray(color, f).reshape(n, 3), f(0.0))
+    intensity = np.maximum(np.asarray(intensity, f).reshape(n), f(0.0))
+    out = np.zeros(n, LIGHT_DTYPE)
+    out["position_range"][:, :3] = pos
+    out["position_range"][:, 3] = np.maximum(rng_range, f(0.0))
+    out["color_intensity"][:, :3] = color
+    out["color_intensity"][:, 3] = intensity
+    out["direction_spot"] = (0.0, -1.0, 0.0, 1.0)
+    out["axis_spot_outer"] = (1.0, 0.0, 0.0, 0.0)
+    out["up_shape_x"] = (0.0, 1.0, 0.0, 0.0)
+    out["shape_attenuation"] = (0.0, max(power, 0.001), max(bias, 1e-5), max(cutoff, 0.0))
+    out["type_shape_flags"] = (1, 0, flags, attenuation_model)     # Point, Sphere
+    r = np.maximum(rng_range, f(0.0))                               # point_light_culling_sphere
+    out["cull_sphere"][:, :3] = pos
+    out["cull_sphere"][:, 3] = r
+    out["cull_aabb_min"][:, :3] = pos - r[:, None]                  # aabb_from_sphere
+    out["cull_aabb_max"][:, :3] = pos + r[:, None]
+    out["cull_aabb_min"][:, 3] = 1.0
+    out["cull_aabb_max"][:, 3] = 1.0
+    return out
+
+
+@dataclass
+class LightCull:
+    """The CameraUBO fields fp_stress_light_cull.comp reads (shs_light_cull_desc)."""
+    width: int
+    height: int
+    view: np.ndarray
+    proj: np.ndarray
+    zn: float = 0.1
+    zf: float = 200.0
+    tile_size: int = 16               # frame/frame_params.hpp:83-84
+    max_per_tile: int = 128
+    mode: int = 1
+    z_slices: int = 16
+    depth_linear: bool = True
+    shard_rank: int = 0
+    shard_count: int = 1
+
+    def desc(self):
+        d = _abi.LightCullDescC()
+        d.width, d.height = self.width, self.height
+        d.tile_size, d.max_per_tile, d.mode, d.z_slices = self.tile_size, self.max_per_tile, self.mode, self.z_slices
+        for k in range(16):
+            d.view[k] = float(self.view[k])
+            d.proj[k] = float(self.proj[k])
+        d.zn, d.zf = self.zn, self.zf
+        d.depth_linear = 1 if self.depth_linear else 0
+        d.shard_rank, d.shard_count = self.shard_rank, self.shard_count
+        return d
+
+    @property
+    def tiles(self):
+        ts = self.tile_size
+        return (self.width + ts - 1) // ts, (self.height + ts - 1) // ts
+
+    @property
+    def n_lists(self):
+        tx, ty = self.tiles
+        return tx * ty * (self.z_slices if self.mode == 3 else 1)
 
 
 def fill_draw_struct(a, d: LibDraw, mesh_id: int):

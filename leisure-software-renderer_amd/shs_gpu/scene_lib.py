@@ -112,3 +112,61 @@ def wire_shadow(draws, light_viewproj):
         d.shadow = True
         d.light_viewproj = np.asarray(light_viewproj, np.float32)
     return draws
+
+
+# ---- C4: Forward+ tiled (BASELINE.json configs[3]) ---------------------------------------------
+C4_BOX_MIN = (-30.0, 0.0, 8.0)
+C4_BOX_MAX = (30.0, 12.0, 90.0)
+
+
+def c4_geometry(n_objects=1000, tris_per_object=1000, n_draws=16, seed=0x5EED):
+    """`n_objects` seeded objects of `tris_per_object` small triangles (soup, fp32
+    position + face normal), all in front of the near plane, grouped into `n_draws` draws (materials).
+    numpy PCG64 with the survey's seed stands in for its mt19937 (synthetic data either way)."""
+    rng = np.random.default_rng(seed)
+    lo, hi = np.array(C4_BOX_MIN, np.float32), np.array(C4_BOX_MAX, np.float32)
+    centers = rng.uniform(lo, hi, size=(n_objects, 3)).astype(np.float32)
+    radius = rng.uniform(0.6, 2.0, size=(n_objects, 1, 1)).astype(np.float32)
+    # per triangle: a point in the object's ball + three corners within 0.35 world units
+    p = centers[:, None, :] + radius * rng.normal(size=(n_objects, tris_per_object, 3)).astype(np.float32) * f32(0.45)
+    corners = p[:, :, None, :] + rng.uniform(-0.35, 0.35, size=(n_objects, tris_per_object, 3, 3)).astype(np.float32)
+    e1 = corners[:, :, 1] - corners[:, :, 0]
+    e2 = corners[:, :, 2] - corners[:, :, 0]
+    nrm = np.cross(e1, e2)
+    nrm /= np.maximum(np.linalg.norm(nrm, axis=-1, keepdims=True), 1e-12)
+    nrm = np.repeat(nrm[:, :, None, :], 3, axis=2).astype(np.float32)
+    groups = np.array_split(np.arange(n_objects), n_draws)
+    meshes = []
+    for g in groups:
+        pos = corners[g].reshape(-1, 3)
+        meshes.append(LibMesh(positions=np.ascontiguousarray(pos), normals=np.ascontiguousarray(nrm[g].reshape(-1, 3))))
+    colors = rng.uniform(0.25, 0.95, size=(n_draws, 3)).astype(np.float32)
+    return meshes, colors
+
+
+def c4_lights(n_lights=256, seed=0x11A7):
+    """256 point lights: position in the scene box, range U[2,8], colour U[0.2,1]^3, intensity
+    U[0.5,2], Smooth attenuation with the reference defaults (light_types.hpp:95-106)."""
+    from .lib_path import make_point_lights
+    rng = np.random.default_rng(seed)
+    pos = rng.uniform(C4_BOX_MIN, C4_BOX_MAX, size=(n_lights, 3))
+    return make_point_lights(pos, rng.uniform(2.0, 8.0, n_lights), rng.uniform(0.2, 1.0, (n_lights, 3)),
+                             rng.uniform(0.5, 2.0, n_lights))
+
+
+def c4_scene(width=3840, height=2160, n_objects=1000, tris_per_object=1000, n_draws=16, n_lights=256, mode=1,
+             tile_size=16, max_per_tile=128, yaw=0.0):
+    """-> (frame, draws, lights, cull).  Forward+ program (SHS_PROGRAM_FORWARD_PLUS), no culling."""
+    from .lib_path import PROGRAM_FORWARD_PLUS, LightCull
+    zn, zf = 0.1, 200.0
+    meshes, colors = c4_geometry(n_objects, tris_per_object, n_draws)
+    ang = np.deg2rad(yaw)
+    eye = (f32(12.0 * np.sin(ang)), f32(8.0), f32(-12.0 * np.cos(ang)))
+    view = look_at_lh(eye, (0.0, 4.0, 40.0))
+    proj = perspective_lh_no(f32(np.deg2rad(60.0)), f32(width) / f32(height), zn, zf)
+    vp = mat_mul(proj, view)
+    draws = [LibDraw(mesh=m, program=PROGRAM_FORWARD_PLUS, viewproj=vp, camera_pos=eye, base_color=tuple(c),
+                     cull_mode=CULL_NONE) for m, c in zip(meshes, colors)]
+    frame = LibFrame(width, height, depth_motion=True, zn=zn, zf=zf, bg_gradient=True)
+    cull = LightCull(width, height, view, proj, zn=zn, zf=zf, tile_size=tile_size, max_per_tile=max_per_tile, mode=mode)
+    return frame, draws, c4_lights(n_lights), cull

@@ -154,6 +154,9 @@ class OraLibTarget(ctypes.Structure):
         ("motion", ctypes.POINTER(ctypes.c_float)),
         ("shadow", ctypes.POINTER(ctypes.c_float)),
         ("shadow_w", ctypes.c_int32), ("shadow_h", ctypes.c_int32),
+        ("lights", ctypes.c_void_p), ("n_lights", ctypes.c_int32),
+        ("tile_counts", ctypes.c_void_p), ("tile_indices", ctypes.c_void_p),
+        ("cull", ctypes.c_void_p),
     ]
 
 
@@ -248,6 +251,12 @@ def pbr_forward(frame, draws, shadow_map=None):
         keep.append(sm)
         t.shadow = sm.ctypes.data_as(fp)
         t.shadow_h, t.shadow_w = sm.shape
+    if _FWD_CTX is not None:
+        lights, cdesc, counts, idx = _FWD_CTX
+        keep += [lights, cdesc, counts, idx]
+        t.lights, t.n_lights = lights.ctypes.data, lights.shape[0]
+        t.tile_counts, t.tile_indices = counts.ctypes.data, idx.ctypes.data
+        t.cull = ctypes.addressof(cdesc)
     st = np.zeros(3, np.uint64)
     rc = _lib_lib().ora_pbr_forward(ctypes.byref(t), arr, len(draws), st.ctypes.data)
     if rc != 0:
@@ -279,3 +288,77 @@ def dir_light_camera_aabb(sun_dir, mn, mx, margin=10.0, res=2048):
     _lib_lib().ora_dir_light_camera_aabb(a[0].ctypes.data, a[1].ctypes.data, a[2].ctypes.data, margin, res,
                                          v.ctypes.data, p.ctypes.data, vp.ctypes.data)
     return v, p, vp
+
+
+# ===== Forward+ light lists (shs_oracle_light.c) ===========================================
+class OraLightCullDesc(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("tile_size", ctypes.c_uint32),
+                ("max_per_tile", ctypes.c_uint32), ("mode", ctypes.c_uint32), ("z_slices", ctypes.c_uint32),
+                ("view", _F16), ("proj", _F16), ("zn", ctypes.c_float), ("zf", ctypes.c_float),
+                ("depth_linear", ctypes.c_int32)]
+
+
+def _cull_desc(c):
+    d = OraLightCullDesc()
+    d.width, d.height = c.width, c.height
+    d.tile_size, d.max_per_tile, d.mode, d.z_slices = c.tile_size, c.max_per_tile, c.mode, c.z_slices
+    for k in range(16):
+        d.view[k], d.proj[k] = float(c.view[k]), float(c.proj[k])
+    d.zn, d.zf = c.zn, c.zf
+    d.depth_linear = 1 if c.depth_linear else 0
+    return d
+
+
+def _light_lib():
+    L = _lib_lib()
+    if not getattr(L, "_light_ready", False):
+        P = ctypes.c_void_p
+        L.ora_light_cull.restype = None
+        L.ora_light_cull.argtypes = [ctypes.POINTER(OraLightCullDesc), P, ctypes.c_int, P, P, P]
+        L.ora_depth_reduce.restype = None
+        L.ora_depth_reduce.argtypes = [ctypes.POINTER(OraLightCullDesc), P, P]
+        L.ora_light_project.restype = None
+        L.ora_light_project.argtypes = [ctypes.POINTER(OraLightCullDesc), P, ctypes.c_int, P]
+        L._light_ready = True
+    return L
+
+
+def light_cull(cull, lights, depth=None):
+    """fp_stress_light_cull.comp (+ fp_stress_depth_reduce.comp over `depth` for mode 2).  cull:
+    shs_gpu.lib_path.LightCull; lights: LIGHT_DTYPE array -> (counts, indices [n_lists, maxp], ranges)."""
+    L = _light_lib()
+    d = _cull_desc(cull)
+    lights = np.ascontiguousarray(lights)
+    tx, ty = cull.tiles
+    ranges = np.zeros((tx * ty, 2), np.float32)
+    if cull.mode == 2:
+        dep = np.ascontiguousarray(depth, dtype=np.float32)
+        L.ora_depth_reduce(ctypes.byref(d), dep.ctypes.data, ranges.ctypes.data)
+    counts = np.zeros(cull.n_lists, np.uint32)
+    idx = np.zeros((cull.n_lists, cull.max_per_tile), np.uint32)
+    L.ora_light_cull(ctypes.byref(d), lights.ctypes.data, lights.shape[0], ranges.ctypes.data, counts.ctypes.data,
+                     idx.ctypes.data)
+    return counts, idx, ranges
+
+
+def light_project(cull, lights):
+    L = _light_lib()
+    d = _cull_desc(cull)
+    lights = np.ascontiguousarray(lights)
+    out = np.zeros((lights.shape[0], 8), np.float32)
+    L.ora_light_project(ctypes.byref(d), lights.ctypes.data, lights.shape[0], out.ctypes.data)
+    return out
+
+
+def forward_plus(frame, draws, lights, cull, lists, shadow_map=None):
+    """pbr_forward with the Forward+ program's light data: lists = (counts, indices) of light_cull."""
+    global _FWD_CTX
+    _FWD_CTX = (np.ascontiguousarray(lights), _cull_desc(cull), np.ascontiguousarray(lists[0], dtype=np.uint32),
+                np.ascontiguousarray(lists[1], dtype=np.uint32))
+    try:
+        return pbr_forward(frame, draws, shadow_map)
+    finally:
+        _FWD_CTX = None
+
+
+_FWD_CTX = None

@@ -75,8 +75,26 @@ enum ora_program {                 /* the ShaderProgram the pass binds (pass_pbr
     ORA_PROGRAM_BLINN_PHONG = 1,   /* make_blinn_phong_program  :105-152                          */
     ORA_PROGRAM_DEBUG_ALBEDO = 2,  /* make_debug_view_shader_program(Albedo|Normal|Depth) :221-245 */
     ORA_PROGRAM_DEBUG_NORMAL = 3,
-    ORA_PROGRAM_DEBUG_DEPTH = 4
+    ORA_PROGRAM_DEBUG_DEPTH = 4,
+    ORA_PROGRAM_FORWARD_PLUS = 5   /* per-pixel point lights from the tile lists (shs_oracle_light.c) */
 };
+
+/* CullingLightGPU (include/shs/lighting/light_types.hpp:141-166), 160 B */
+typedef struct ora_culling_light {
+    float position_range[4], color_intensity[4], direction_spot[4], axis_spot_outer[4], up_shape_x[4];
+    float shape_attenuation[4];
+    uint32_t type_shape_flags[4];
+    float cull_sphere[4], cull_aabb_min[4], cull_aabb_max[4];
+} ora_culling_light;
+
+/* The CameraUBO fields fp_stress_light_cull.comp / fp_stress_depth_reduce.comp read. */
+typedef struct ora_light_cull_desc {
+    int32_t width, height;
+    uint32_t tile_size, max_per_tile, mode, z_slices;   /* mode: 0 none, 1 tiled, 2 tiled depth range, 3 clustered */
+    float view[16], proj[16];
+    float zn, zf;
+    int32_t depth_linear;                               /* depth input holds linear view depth (library RT) */
+} ora_light_cull_desc;
 enum ora_cull { ORA_CULL_NONE = 0, ORA_CULL_BACK = 1, ORA_CULL_FRONT = 2 };  /* RasterizerCullMode */
 
 /* MeshData (resources/mesh.hpp:23-43): vec3 positions / normals, vec2 uvs, u32 indices (NULL:
@@ -118,6 +136,11 @@ typedef struct ora_lib_target {
     float *hdr, *depth, *motion;
     const float *shadow;
     int32_t shadow_w, shadow_h;
+    /* ORA_PROGRAM_FORWARD_PLUS: the light set and the lists of ora_light_cull with this desc */
+    const ora_culling_light *lights;
+    int32_t n_lights;
+    const uint32_t *tile_counts, *tile_indices;
+    const ora_light_cull_desc *cull;
 } ora_lib_target;
 
 typedef struct ora_shadow_caster {   /* RenderItem with casts_shadow (scene/scene_types.hpp:78-87) */
@@ -136,6 +159,17 @@ int ora_shadow_map(int SW, int SH, const float *sun_dir3, const ora_shadow_caste
 void ora_dir_light_camera_aabb(const float *sun_dir3, const float *mn3, const float *mx3, float extra_margin,
                                uint32_t res, float *view, float *proj, float *viewproj);
 void ora_look_at_lh(const float *eye3, const float *center3, const float *up3, float *out16);
+
+/* Light lists (shs_oracle_light.c).  ora_light_project: per light {cx, cy, radius_px, view_depth,
+ * cull radius, 0, 0, valid} (project_light_screen, tile independent).  ora_depth_reduce: per tile
+ * (min, max) linear view depth of depth[W*H] (rows y-up), (0,0) when empty.  ora_light_cull: counts
+ * per list and max_per_tile indices per list (ranges2 used by mode 2). */
+void ora_light_project(const ora_light_cull_desc *d, const ora_culling_light *lights, int n, float *out8);
+void ora_depth_reduce(const ora_light_cull_desc *d, const float *depth, float *ranges2);
+void ora_light_cull(const ora_light_cull_desc *d, const ora_culling_light *lights, int n, const float *ranges2,
+                    uint32_t *counts, uint32_t *indices);
+void ora_point_light_accumulate(const ora_culling_light *L, const float *world, const float *N, const float *V,
+                                const float *base, float *lit);
 float ora_mat4_determinant(const float *m);
 
 #ifdef __cplusplus

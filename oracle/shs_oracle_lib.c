@@ -234,7 +234,51 @@ typedef struct {
     v3 world_pos, normal_ws;
     v2 uv;
     float depth01;
+    int px, py;
 } frag_in;
+
+/* Forward+ per-pixel lighting (shs_oracle_light.c): the tile list of the pixel as fp_stress_scene.frag
+ * :644-685 selects it (saturated list -> every light), each light through PointLightModel::sample,
+ * combined like hello_light_types_culling_sw.cpp:404-416 (ambient hemisphere + sum, clamped). */
+static v3 forward_plus(const ora_lib_target *t, const ora_lib_draw *u, const frag_in *fin) {
+    const ora_light_cull_desc *d = t->cull;
+    const v3 N = normalize3(fin->normal_ws);
+    const v3 cam = V3(u->camera_pos[0], u->camera_pos[1], u->camera_pos[2]);
+    v3 V = v3sub(cam, fin->world_pos);
+    const float len2 = dot3(V, V);
+    V = len2 <= 1e-10f ? V3(0.0f, 0.0f, 1.0f) : v3s(V, 1.0f / sqrtf(len2));        /* normalize_or */
+    const float hemi = 0.5f + 0.5f * s_clamp(N.y, -1.0f, 1.0f);
+    const float amb = 0.22f + 0.12f * hemi;                                         /* kAmbientBase / Hemi */
+    float lit[3] = {u->base_color[0] * amb, u->base_color[1] * amb, u->base_color[2] * amb};
+    const float w[3] = {fin->world_pos.x, fin->world_pos.y, fin->world_pos.z}, n[3] = {N.x, N.y, N.z}, vv[3] = {V.x, V.y, V.z};
+    const uint32_t ts = d->tile_size > 0 ? d->tile_size : 1u, maxp = d->max_per_tile > 0 ? d->max_per_tile : 1u;
+    const uint32_t tx_n = ((uint32_t)t->W + ts - 1) / ts, ty_n = ((uint32_t)t->H + ts - 1) / ts;
+    uint32_t tx = (uint32_t)fin->px / ts, ty = (uint32_t)(t->H - 1 - fin->py) / ts;   /* gl_FragCoord rows y-down */
+    if (tx > tx_n - 1) tx = tx_n - 1;
+    if (ty > ty_n - 1) ty = ty_n - 1;
+    uint32_t list = ty * tx_n + tx;
+    if (d->mode == 3u) {
+        const uint32_t zs = d->z_slices > 0 ? d->z_slices : 1u;
+        const v4 vw = m4v4(d->view, (v4){w[0], w[1], w[2], 1.0f});
+        const float view_depth = s_max(0.001f, vw.z);
+        const float near_z = s_max(d->zn, 0.001f), far_z = s_max(d->zf, near_z + 0.01f);
+        const float dd = g_clamp(view_depth, near_z, far_z);
+        const float tt = logf(dd / near_z) / s_max(logf(far_z / near_z), 1e-6f);
+        const float zi = g_clamp(floorf(tt * (float)zs), 0.0f, (float)(zs - 1u));
+        list = ((uint32_t)zi * ty_n + ty) * tx_n + tx;
+    }
+    const uint32_t count = d->mode == 0u ? maxp : (t->tile_counts[list] < maxp ? t->tile_counts[list] : maxp);
+    const float base[3] = {u->base_color[0], u->base_color[1], u->base_color[2]};
+    if (count >= maxp) {
+        for (int i = 0; i < t->n_lights; ++i) ora_point_light_accumulate(&t->lights[i], w, n, vv, base, lit);
+    } else {
+        for (uint32_t i = 0; i < count; ++i) {
+            const uint32_t idx = t->tile_indices[(size_t)list * maxp + i];
+            if ((int)idx < t->n_lights) ora_point_light_accumulate(&t->lights[idx], w, n, vv, base, lit);
+        }
+    }
+    return V3(g_clamp(lit[0], 0.0f, 1.0f), g_clamp(lit[1], 0.0f, 1.0f), g_clamp(lit[2], 0.0f, 1.0f));
+}
 
 /* The builtin fragment programs.  Texture sampling: no base_color_tex -> vec3(1) (:35). */
 static v4 fragment(const ora_lib_target *t, const ora_lib_draw *u, const frag_in *fin) {
@@ -252,6 +296,11 @@ static v4 fragment(const ora_lib_target *t, const ora_lib_draw *u, const frag_in
     if (u->program == ORA_PROGRAM_DEBUG_NORMAL) {          /* :232-237 */
         const v3 n = v3add(v3s(normalize3(fin->normal_ws), 0.5f), V3(0.5f, 0.5f, 0.5f));
         o.x = n.x; o.y = n.y; o.z = n.z;
+        return o;
+    }
+    if (u->program == ORA_PROGRAM_FORWARD_PLUS) {
+        const v3 c = forward_plus(t, u, fin);
+        o.x = c.x; o.y = c.y; o.z = c.z;
         return o;
     }
     if (u->program == ORA_PROGRAM_DEBUG_DEPTH) {           /* :238-241 */
@@ -490,6 +539,8 @@ void ora_rasterize_mesh(const ora_lib_target *t, const ora_lib_draw *u, uint64_t
                         t->motion[2 * o] = mx; t->motion[2 * o + 1] = my;
                     }
                     fin.depth01 = z01;
+                    fin.px = x;
+                    fin.py = y;
                     const v4 c = fragment(t, u, &fin);
                     t->hdr[4 * o] = c.x; t->hdr[4 * o + 1] = c.y; t->hdr[4 * o + 2] = c.z; t->hdr[4 * o + 3] = c.w;
                 }
