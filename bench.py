@@ -47,8 +47,10 @@ WORKLOADS = {
     "c3": "C3: 64-instance Suzanne grid, Phong, 1920x1080, 1 frame per step",
     "c5": "C5: Suzanne + floor, PassShadowMap 2048^2 + PassPBRForward (PBR Cook-Torrance, PCF 5x5, motion) "
           "3840x2160, 1 frame (both passes) per step",
+    "c4": "C4: Forward+ tiled, 1M synthetic triangles, 256 point lights, 3840x2160 (light cull + lit forward pass), "
+          "1 frame per step",
 }
-LIB_CONFIGS = {"c5"}
+LIB_CONFIGS = {"c5", "c4"}
 
 
 def algorithmic_bytes(frame, draws):
@@ -98,7 +100,63 @@ def run_gpu(args, rank, local_rank, world, dist):
 
 def lib_workload(args, rank=0):
     from shs_gpu import scene_lib
+    if args.config == "c4":
+        return scene_lib.c4_scene(3840, 2160)
     return scene_lib.c5_scene(3840, 2160, 2048, yaw=3.0 * rank)
+
+
+def run_gpu_c4(args, rank, local_rank, world, dist):
+    """C4 frame = Forward+ light-list binning (shs_light_cull) + PassPBRForward with the per-pixel
+    point-light program over 1M triangles at 3840x2160.  N > 1: the frame's 32x32 tiles are sharded
+    (tile % N == rank) and the owned tiles are gathered into rank 0 over RCCL every frame
+    (strong scaling: the total work per step is one frame)."""
+    import shs_gpu
+    from shs_gpu import shard
+    frame, draws, lights, cull = lib_workload(args, rank)
+    ctx = shs_gpu.Context(local_rank)
+    if dist is not None:
+        import torch
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        frame.shard_rank, frame.shard_count = rank, world
+        cull.shard_rank, cull.shard_count = rank, world
+    ctx.upload_lights(lights)
+    ctx.light_cull(cull)
+    prepared = ctx.prepare_lib(frame, draws)
+
+    def one_frame():
+        ctx.light_cull(cull)
+        ctx.render_pbr_forward_prepared(prepared)
+        if dist is not None:
+            shard.gather_frame_device(dist, ctx, ctx.TARGET_LIB)
+
+    for _ in range(max(args.warmup, 1)):
+        one_frame()
+    ctx.synchronize_lib()
+    stats = ctx.lib_stats()
+
+    def barrier_sync():
+        ctx.synchronize_lib()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    ctx.enable_timing(True)
+    ctx.lib_timing_reset()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_frame()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    n_passes, kms = ctx.lib_timing_read()
+    kms = {"setup": kms["setup"], "raster": kms["raster"]}
+    ctx.enable_timing(False)
+    ctx.close()
+    n_tri = sum(d.mesh.n_tris for d in draws)
+    B_cam_raster = frame.width * frame.height * 28
+    B_frame = n_tri * 72 + frame.width * frame.height * 28 + len(lights) * 160 + cull.n_lists * 4
+    return frame, stats, elapsed, n_passes["camera"], kms, B_cam_raster, B_frame, n_tri, None
 
 
 def lib_mesh_bytes(mesh, with_attrs=True):
@@ -208,6 +266,22 @@ def cpu_baseline_lib(args):
     reference's pass loop for these triangle sizes) on one host core, bounded sample."""
     from oracle import oracle
     from shs_gpu import scene_lib
+    if args.config == "c4":
+        frame, draws, lights, cull = lib_workload(args, 0)
+        n_tri = sum(d.mesh.n_tris for d in draws)
+        frames = 0
+        t0 = time.perf_counter()
+        while True:
+            lists = oracle.light_cull(cull, lights)
+            oracle.forward_plus(frame, draws, lights, cull, lists[:2])
+            frames += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds:
+                break
+        return {"value": round(n_tri * frames / el / 1e6, 5), "unit": "Mtri/s", "cores": 1, "kind": "port",
+                "sample": f"{frames} full frame(s) of the same workload (light cull + Forward+ pass, "
+                          f"{frame.width}x{frame.height}, {n_tri} tris, {len(lights)} lights), {el:.1f} s wall, "
+                          "1 thread (oracle/shs_oracle_lib.c + shs_oracle_light.c, gcc -O3)"}
     frame, draws, casters, sun, S = lib_workload(args, 0)
     n_tri = sum(d.mesh.n_tris for d in draws)
     frames = 0
@@ -359,7 +433,12 @@ def main():
 
 
 def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
-    frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, S = run_gpu_lib(args, rank, local_rank, world, dist)
+    runner = run_gpu_c4 if args.config == "c4" else run_gpu_lib
+    frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, S = runner(args, rank, local_rank, world, dist)
+    if args.config == "c4" and dist is not None:
+        world_tri = n_tri          # one frame split over the ranks (strong scaling)
+    else:
+        world_tri = world * n_tri
     el_max = elapsed
     covered_total = float(stats["covered_pixels"])
     if dist is not None:
@@ -388,15 +467,22 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
                 "frame_frac": round(B_frame / (t_frame * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if t_frame > 0 else None}
     if pmc is None:
         roofline["traffic_note"] = pmc_err
+    c4 = args.config == "c4"
+    if c4:
+        data = ("synthetic: 1000 seeded objects x 1000 small triangles (seed 0x5EED), 256 point lights (seed 0x11A7, "
+                "range U[2,8], Smooth attenuation), 16-px tiles, max 128 lights per tile")
+        parallelism = f"tile-sharded x{world} + RCCL gather to rank 0" if world > 1 else "single GPU"
+    else:
+        data = ("synthetic: Suzanne (indexed from the reference's monkey.rawobj) + make_plane floor, reference "
+                "defaults (sun normalize(0.4668,-0.3487,0.8127), intensity 5, PCF 2, bias 0.0008/0.0015)")
+        parallelism = f"frame-parallel x{world}" if world > 1 else "single GPU"
     line = {
-        "metric": METRIC, "value": round(world * n_tri * steps / el_max / 1e6, 3), "unit": "Mtri/s", "n_gpus": world,
+        "metric": METRIC, "value": round(world_tri * steps / el_max / 1e6, 3), "unit": "Mtri/s", "n_gpus": world,
         "steps": steps, "warmup": args.warmup, "ms_per_step": round(el_max / steps * 1e3, 5), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: Suzanne (indexed from the reference's monkey.rawobj) + make_plane floor, reference "
-                "defaults (sun normalize(0.4668,-0.3487,0.8127), intensity 5, PCF 2, bias 0.0008/0.0015)",
+        "scaling": "strong" if (c4 and world > 1) else "weak", "vs_baseline": None, "dtype": "f32", "data": data,
         "config": {"workload": WORKLOADS[args.config], "width": frame.width, "height": frame.height,
                    "shadow_map": S, "tris_per_frame": n_tri, "frames_per_step_per_gpu": 1,
-                   "parallelism": f"frame-parallel x{world}" if world > 1 else "single GPU"},
+                   "parallelism": parallelism},
         "shaded_mpix_s": round(covered_total * steps / el_max / 1e6, 3),
         "frame_stats": stats, "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
         "timed_frames_with_events": n_frames, "roofline": roofline,

@@ -294,6 +294,18 @@ int shs_light_cull(shs_ctx *ctx, const shs_light_cull_desc *desc);
 int shs_resolve_light_lists(shs_ctx *ctx, uint32_t *counts, uint32_t *indices, float *ranges);
 #define SHS_PROGRAM_FORWARD_PLUS 5  /* per-pixel point lights from the tile lists (light_runtime.hpp:321-333) */
 
+/* ---- multi-GPU tile shards -------------------------------------------------------
+ * A frame rendered with shard_rank / shard_count holds only its own 32x32 tiles (tile % count ==
+ * rank).  shs_tiles_pack writes them into a caller-owned DEVICE buffer (e.g. a torch tensor on the
+ * context's device) -- one 32x32-padded block per owned tile, planes colour / depth / motion --
+ * for an RCCL gather; rank 0 calls shs_tiles_unpack once per peer to compose the full frame.  Both
+ * are enqueued on the context stream (see shs_set_stream). */
+#define SHS_TARGET_LEGACY 0   /* shs_render_legacy frame: RGBA8 canvas rows + f32 depth  */
+#define SHS_TARGET_LIB 1      /* library frame: RGBA32F HDR (+ depth + motion)           */
+int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t shard_count, int64_t *words_per_rank);
+int shs_tiles_pack(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, void *dst_dev);
+int shs_tiles_unpack(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, const void *src_dev);
+
 /* Host GLM restatements for non-C++ callers (camera/convention.hpp; pass_pbr_forward.hpp:136-141). */
 int shs_look_at_lh(const float eye[3], const float center[3], const float up[3], float out16[16]);
 int shs_perspective_lh_no(float fovy_radians, float aspect, float zn, float zf, float out16[16]);

@@ -14,6 +14,7 @@
 #include "shs_lib_device.hpp"
 #include "shs_lib_internal.hpp"
 #include "shs_light_internal.hpp"
+#include "shs_tiles_internal.hpp"
 
 using shs_dev::LibBuffers;
 using shs_dev::LibDrawGPU;
@@ -583,6 +584,61 @@ int shs_resolve_light_lists(shs_ctx *ctx, uint32_t *counts, uint32_t *indices, f
         HIP_TRY(ctx, hipMemcpy(indices, ctx->list_indices.p, (size_t)p.n_lists * p.max_per_tile * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (ranges)
         HIP_TRY(ctx, hipMemcpy(ranges, ctx->depth_ranges.p, (size_t)p.tiles_x * p.tiles_y * sizeof(float2), hipMemcpyDeviceToHost));
+    return SHS_OK;
+}
+
+static int tile_params(shs_ctx *ctx, int target, int32_t rank, int32_t count, shs_dev::TileCopyParams &p) {
+    std::memset(&p, 0, sizeof p);
+    if (count <= 0 || rank < 0 || rank >= count) { ctx->err = "bad shard"; return SHS_ERR_INVALID; }
+    p.rank = rank;
+    p.count = count;
+    if (target == SHS_TARGET_LEGACY) {
+        if (!ctx->have_frame) { ctx->err = "no legacy frame rendered"; return SHS_ERR_INVALID; }
+        p.W = ctx->frame.width; p.H = ctx->frame.height;
+        p.color_words = 1; p.color_flip = 1;
+        p.color = reinterpret_cast<uint32_t *>(ctx->color.p);
+        p.depth = reinterpret_cast<uint32_t *>(ctx->depth.p);
+    } else if (target == SHS_TARGET_LIB) {
+        if (!ctx->have_lib_frame) { ctx->err = "no library frame rendered"; return SHS_ERR_INVALID; }
+        p.W = ctx->lib_frame.width; p.H = ctx->lib_frame.height;
+        p.color_words = 4; p.color_flip = 0;
+        p.color = reinterpret_cast<uint32_t *>(ctx->lib_hdr.p);
+        if (ctx->lib_frame.flags & SHS_LIB_DEPTH_MOTION) {
+            p.depth = reinterpret_cast<uint32_t *>(ctx->lib_depth.p);
+            p.motion = reinterpret_cast<uint32_t *>(ctx->lib_motion.p);
+        }
+    } else {
+        ctx->err = "bad target";
+        return SHS_ERR_INVALID;
+    }
+    p.words = p.color_words + (p.depth ? 1 : 0) + (p.motion ? 2 : 0);
+    return SHS_OK;
+}
+
+int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t count, int64_t *words_out) {
+    if (!ctx || !words_out) return SHS_ERR_INVALID;
+    shs_dev::TileCopyParams p;
+    if (tile_params(ctx, target, 0, count, p)) return SHS_ERR_INVALID;
+    const int64_t n_tiles = (int64_t)((p.W + 31) / 32) * ((p.H + 31) / 32);
+    *words_out = ((n_tiles + count - 1) / count) * 32 * 32 * p.words;
+    return SHS_OK;
+}
+
+int shs_tiles_pack(shs_ctx *ctx, int target, int32_t rank, int32_t count, void *dst_dev) {
+    if (!ctx || !dst_dev) return SHS_ERR_INVALID;
+    shs_dev::TileCopyParams p;
+    if (tile_params(ctx, target, rank, count, p)) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, shs_internal::launch_tiles_copy(p, true, dst_dev, ctx->stream));
+    return SHS_OK;
+}
+
+int shs_tiles_unpack(shs_ctx *ctx, int target, int32_t rank, int32_t count, const void *src_dev) {
+    if (!ctx || !src_dev) return SHS_ERR_INVALID;
+    shs_dev::TileCopyParams p;
+    if (tile_params(ctx, target, rank, count, p)) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, shs_internal::launch_tiles_copy(p, false, const_cast<void *>(src_dev), ctx->stream));
     return SHS_OK;
 }
 

@@ -308,6 +308,21 @@ class Context:
         elif self._shadow_size is not None:
             self.resolve_shadow_map()
 
+    # -- tile shards (multi-GPU gather) ----------------------------------------------------------
+    TARGET_LEGACY, TARGET_LIB = 0, 1
+
+    def tiles_packed_words(self, target, count):
+        n = ctypes.c_int64()
+        self._check(self._lib.shs_tiles_packed_words(self._h, target, count, ctypes.byref(n)))
+        return n.value
+
+    def tiles_pack(self, target, rank, count, dst_ptr):
+        """Pack rank's owned tiles into the device buffer at dst_ptr (e.g. tensor.data_ptr())."""
+        self._check(self._lib.shs_tiles_pack(self._h, target, rank, count, ctypes.c_void_p(dst_ptr)))
+
+    def tiles_unpack(self, target, rank, count, src_ptr):
+        self._check(self._lib.shs_tiles_unpack(self._h, target, rank, count, ctypes.c_void_p(src_ptr)))
+
     def upload_lights(self, lights):
         """lights: numpy LIGHT_DTYPE array (CullingLightGPU records)."""
         from ._abi import CullingLightC

@@ -180,6 +180,9 @@ SIGNATURES = [
     ("shs_render_shadow_map", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _F, ctypes.POINTER(ShadowCasterC),
                                              ctypes.c_int32, _F]),
     ("shs_resolve_shadow_map", ctypes.c_int, [_P, _P]),
+    ("shs_tiles_packed_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
+    ("shs_tiles_pack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
+    ("shs_tiles_unpack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
     ("shs_lights_upload", ctypes.c_int, [_P, ctypes.POINTER(CullingLightC), ctypes.c_int32]),
     ("shs_light_cull", ctypes.c_int, [_P, ctypes.POINTER(LightCullDescC)]),
     ("shs_resolve_light_lists", ctypes.c_int, [_P, _P, _P, _P]),

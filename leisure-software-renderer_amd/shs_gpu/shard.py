@@ -72,6 +72,67 @@ def packed_len(width, height, tile, rank, count):
     return n
 
 
+# ---- device-resident gather (libshs_gpu shs_tiles_pack / shs_tiles_unpack) -----------------------
+# Layout of one rank's packed buffer (shs_tiles.hip): owned tile i = rank + i*count occupies
+# TILE*TILE*words int32 words at i*TILE*TILE*words; inside it, plane c (colour words, depth, motion)
+# holds the tile's pixels row-major in screen rows, padded to 32x32.
+
+def planes_of(frame_planes):
+    """frame_planes: list of (array [H,W,k] or [H,W] of 4-byte words, flip_rows) -> list of
+    per-plane uint32 views [H, W] in SCREEN row order."""
+    out = []
+    for a, flip in frame_planes:
+        a = np.ascontiguousarray(a)
+        words = a.view(np.uint32)
+        words = words.reshape(a.shape[0], a.shape[1], -1)
+        for k in range(words.shape[2]):
+            p = words[:, :, k]
+            out.append(p[::-1] if flip else p)
+    return out
+
+
+def pack_padded(planes, width, height, rank, count, tile=32):
+    """CPU restatement of shs_tiles_pack for screen-row planes (list of uint32 [H, W])."""
+    owned = owned_tiles(width, height, tile, rank, count)
+    nw = len(planes)
+    out = np.zeros((len(owned), nw, tile, tile), np.uint32)
+    for i, t in enumerate(owned):
+        y0, y1, x0, x1 = _tile_slices(t, width, height, tile)
+        for c, p in enumerate(planes):
+            out[i, c, :y1 - y0, :x1 - x0] = p[y0:y1, x0:x1]
+    return out.reshape(-1)
+
+
+def unpack_padded(planes, packed, width, height, rank, count, tile=32):
+    owned = owned_tiles(width, height, tile, rank, count)
+    blk = np.asarray(packed).view(np.uint32).reshape(-1, len(planes), tile, tile)
+    for i, t in enumerate(owned):
+        y0, y1, x0, x1 = _tile_slices(t, width, height, tile)
+        for c, p in enumerate(planes):
+            p[y0:y1, x0:x1] = blk[i, c, :y1 - y0, :x1 - x0]
+
+
+def gather_frame_device(dist, ctx, target, stream=None):
+    """RCCL gather of a tile-sharded frame into rank 0's context framebuffers (device to device).
+    Every rank packs its owned tiles on the GPU (shs_tiles_pack), rank 0 receives the peers' buffers
+    with dist.gather (ncclSend/Recv over xGMI) and unpacks them in place (shs_tiles_unpack).  The
+    context runs on torch's current stream so RCCL and the kernels are ordered."""
+    rank, count = dist.get_rank(), dist.get_world_size()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    ctx.set_stream(s.cuda_stream)
+    words = ctx.tiles_packed_words(target, count)
+    buf = torch.empty(words, dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+    ctx.tiles_pack(target, rank, count, buf.data_ptr())
+    if rank == 0:
+        bufs = [torch.empty_like(buf) for _ in range(count)]
+        dist.gather(buf, gather_list=bufs, dst=0)
+        for r in range(1, count):
+            ctx.tiles_unpack(target, r, count, bufs[r].data_ptr())
+    else:
+        dist.gather(buf, dst=0)
+    return rank == 0
+
+
 def gather_frame(dist, color, depth, tile, device=None):
     """Collective: every rank passes its shard-rendered (color, depth) host buffers (only its own
     tiles meaningful); rank 0 returns the composed full frame, other ranks return None.

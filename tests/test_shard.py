@@ -86,3 +86,68 @@ def test_gloo_gather_composes_full_frame(world):
     assert all(p.exitcode == 0 for p in procs)
     results = [q.get(timeout=5) for _ in range(world)]
     assert all(results)
+
+
+@pytest.mark.parametrize("w,h,count", [(333, 241, 3), (3840, 2160, 8), (100, 40, 1)])
+def test_padded_layout_roundtrip(w, h, count):
+    """The device gather's packed layout (shs_tiles.hip), restated on the host: every rank's padded
+    tile blocks unpack into exactly the full frame; buffer sizes match shs_tiles_packed_words."""
+    rng = np.random.default_rng(4)
+    hdr = rng.normal(size=(h, w, 4)).astype(np.float32)
+    depth = rng.random((h, w)).astype(np.float32)
+    src = shard.planes_of([(hdr, False), (depth, False)])
+    dst_hdr, dst_depth = np.zeros_like(hdr), np.zeros_like(depth)
+    dst = shard.planes_of([(dst_hdr, False), (dst_depth, False)])
+    n_tiles = ((w + 31) // 32) * ((h + 31) // 32)
+    for r in range(count):
+        p = shard.pack_padded(src, w, h, r, count)
+        assert p.size <= ((n_tiles + count - 1) // count) * 1024 * 5
+        shard.unpack_padded(dst, p, w, h, r, count)
+    assert np.array_equal(dst_hdr.view(np.uint32), hdr.view(np.uint32))
+    assert np.array_equal(dst_depth.view(np.uint32), depth.view(np.uint32))
+
+
+def _gloo_padded_worker(rank, world, port, q):
+    """The device gather's protocol over gloo: pack (host restatement), gather to rank 0, unpack."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w, h = 333, 241
+        rng = np.random.default_rng(12)
+        color = rng.integers(0, 2**31, size=(h, w), dtype=np.int64).astype(np.uint32)
+        n_tiles = ((w + 31) // 32) * ((h + 31) // 32)
+        words = ((n_tiles + world - 1) // world) * 1024
+        buf = np.zeros(words, np.uint32)
+        mine = shard.pack_padded([color], w, h, rank, world)
+        buf[:mine.size] = mine
+        t = torch.from_numpy(buf.view(np.int32))
+        if rank == 0:
+            bufs = [torch.empty_like(t) for _ in range(world)]
+            dist.gather(t, gather_list=bufs, dst=0)
+            out = np.zeros_like(color)
+            for r in range(world):
+                shard.unpack_padded([out], bufs[r].numpy().view(np.uint32), w, h, r, world)
+            q.put(bool(np.array_equal(out, color)))
+        else:
+            dist.gather(t, dst=0)
+            q.put(True)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_device_protocol_gather():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_padded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(q.get(timeout=5) for _ in range(world))
