@@ -339,7 +339,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     if args.child:  # profiled child: just render
-        (run_gpu_lib if args.config in LIB_CONFIGS else run_gpu)(args, 0, 0, 1, None)
+        {"c4": run_gpu_c4, "c5": run_gpu_lib}.get(args.config, run_gpu)(args, 0, 0, 1, None)
         return
 
     pmc, pmc_err = (None, "skipped")
