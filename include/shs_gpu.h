@@ -11,7 +11,8 @@
  *     Gouraud :186-236, Flat :194-247 copies).  Replaced by shs_render_legacy(): the std::function
  *     shaders become the shading-model enum + POD uniform block of shs_legacy_draw, the per-tile job
  *     loop becomes one enqueue on the context's HIP stream.
- *   Seam 2 (library rasterize_mesh) and Seam 3 (IRenderPass plugin) are later rows.
+ *   Seam 2 (library rasterize_mesh) and Seam 3 (the PassShadowMap / PassPBRForward IRenderPass
+ *     bodies, Forward+ light culling): the "Library path" section below.
  *
  * Conventions: every function returns int status (0 = SHS_OK), never throws; a
  * context is used by one host thread at a time; host buffers are caller-owned and use the exact
