@@ -71,6 +71,10 @@ def run_gpu(args, rank, local_rank, world, dist):
     frame, draws = build_workload(args.config, rank)
     frame.debug_flags = args.debug_flags   # timing experiments only (wrong images)
     ctx = shs_gpu.Context(local_rank)
+    if args.raster_mode:
+        ctx.set_raster_mode(args.raster_mode)
+    if args.raster_loop >= 0:
+        ctx.set_raster_loop(args.raster_loop)
     prepared = ctx.prepare(frame, draws)
     for _ in range(max(args.warmup, 1)):
         ctx.render_prepared(prepared)
@@ -332,6 +336,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--debug-flags", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--raster-mode", type=int, default=0, help="legacy path: 0 auto, 1 scan, 2 bins")
+    ap.add_argument("--raster-loop", type=int, default=-1, help="legacy path: 0 per-pixel, 1 pair tasks (default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

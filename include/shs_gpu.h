@@ -146,6 +146,9 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
 /* SHS_OPT_TIMELINE: 1 = record every workgroup's start / end time (s_memrealtime, 100 MHz) of the
  * frames that follow (profiling aid; read with shs_debug_timeline), 0 = off. */
 #define SHS_OPT_TIMELINE 3
+/* SHS_OPT_RASTER_LOOP: 1 = (candidate, pixel) pair tasks dealt over the waves (default), 0 = each
+ * thread loops over the tile's candidates for its own pixel.  Results are identical in both. */
+#define SHS_OPT_RASTER_LOOP 4
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 
 /* Debug / profiling hook: the last frame's workgroup timeline.  out[0..7] = {k_setup grid, k_raster

@@ -282,7 +282,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.n_tris = n_tris; fp.n_draws = n_draws;
     fp.clear_rgba = (uint32_t)f.clear_color[0] | ((uint32_t)f.clear_color[1] << 8) | ((uint32_t)f.clear_color[2] << 16) |
                     ((uint32_t)f.clear_color[3] << 24);
-    fp.flags = f.flags;
+    fp.flags = (f.flags & ~shs_dev::RF_PER_PIXEL) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ctx->spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ctx->frags.cap, 0xffffffffu);
@@ -555,6 +555,11 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
     if (option == SHS_OPT_RASTER_MODE) {
         if (value < 0 || value > 2) return SHS_ERR_INVALID;
         ctx->force_mode = (int)value;
+        return SHS_OK;
+    }
+    if (option == SHS_OPT_RASTER_LOOP) {
+        if (value < 0 || value > 1) return SHS_ERR_INVALID;
+        ctx->pair_loop = value == 1;
         return SHS_OK;
     }
     if (option == SHS_OPT_TIMELINE) {

@@ -63,6 +63,7 @@ struct shs_ctx {
     uint64_t last_covered = 0, last_bins = 0, last_maxbin = 0, last_setup = 0, last_ghost = 0, last_unb = 0;
     uint32_t bin_cap = 256;
     int force_mode = 0;              // 0 auto, 1 scan, 2 bin (SHS_OPT_RASTER_MODE)
+    bool pair_loop = true;           // SHS_OPT_RASTER_LOOP: (candidate, pixel) pair tasks (default)
     uint32_t frame_index = 0;        // parity of the counter set
     uint32_t last_parity = 0;
     DevBuf<uint8_t> color;

@@ -791,6 +791,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     const uint32_t *bin = fb.bins + (size_t)bt * fp.bin_cap;
     uint32_t seq = 0;   // candidates processed (profiling)
     int pairs = 0;      // (candidate, pixel) tasks (profiling)
+    unsigned long long kmin = KEY_EMPTY;   // per-pixel loop: this thread's pixel key
 
     for (uint32_t base = 0; base < n_items; base += CAND) {
         __syncthreads();
@@ -861,6 +862,27 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             }
             __syncthreads();
             tl_mark(tl, tls, 2);
+            if (fp.flags & RF_PER_PIXEL) {
+                // Per-pixel loop: every thread tests its own pixel against the staged candidates in
+                // order (LDS broadcast reads, the key min kept in a register).  A wave owns two tile
+                // rows and skips a candidate whose box misses them as a whole.
+                const int px = X0 + (tid & 31), py = Y0 + (tid >> 5);
+                const int wy0 = Y0 + 2 * wave, wy1 = wy0 + 1;
+                for (int cc = 0; cc < m; ++cc) {
+                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[cc * 6])[4];   // ibx iby gbx gby
+                    const int x0 = lo16(bb.z), x1 = hi16(bb.z), y0 = lo16(bb.w), y1 = hi16(bb.w);
+                    if (y1 < wy0 || y0 > wy1) continue;                                     // wave-uniform
+                    if (px < x0 || px > x1 || py < y0 || py > y1) continue;
+                    const TriRec r = rec_from(&sh.rec[cc * 6]);
+                    float z;
+                    if (pixel_test(fp, r, px, py, z)) {
+                        const unsigned long long k = z_key(z, sh.id[cc]);
+                        kmin = k < kmin ? k : kmin;
+                    }
+                }
+                seq += (uint32_t)m;
+                continue;
+            }
             // Pair tasks.  Wave w takes the staged candidates c = w + 4l (lane l holds candidate l of
             // its list): clipped bin box in the tile, area, and the wave-inclusive prefix of the areas.
             // The wave then walks its (candidate, pixel) pairs 64 at a time; a pair's owner is found
@@ -924,7 +946,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
 
     // one pixel per thread: resolve, shade the winner, write (rows of 32 px: 128-B segments)
     const int px = X0 + (tid & 31), py = Y0 + (tid >> 5);
-    const unsigned long long key = sh.key[tid];
+    const unsigned long long lkey = sh.key[tid];
+    const unsigned long long key = lkey < kmin ? lkey : kmin;
     sh.key[tid] = KEY_EMPTY;   // clean for the next tile (read above, by this thread only)
     uint32_t rgba = fp.clear_rgba;
     float depth = FLT_MAX;

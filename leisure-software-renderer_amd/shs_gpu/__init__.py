@@ -210,6 +210,10 @@ class Context:
         """0 auto, 1 scan (no bins), 2 bins."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_RASTER_MODE, int(mode)))
 
+    def set_raster_loop(self, loop: int):
+        """Legacy raster inner loop: 1 (candidate, pixel) pair tasks (default), 0 per-pixel candidate loop."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_RASTER_LOOP, int(loop)))
+
     def set_timeline(self, enable: bool):
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_TIMELINE, 1 if enable else 0))
 

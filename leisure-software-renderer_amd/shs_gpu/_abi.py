@@ -25,6 +25,7 @@ FRAME_PREQUANT = 1
 OPT_BIN_CAPACITY = 1
 OPT_RASTER_MODE = 2
 OPT_TIMELINE = 3
+OPT_RASTER_LOOP = 4
 
 
 class LegacyDraw(ctypes.Structure):

@@ -260,11 +260,13 @@ def test_hair_slivers_tile_clamp_ghosts(gpu_ctx, oracle_mod):
     _check(gpu_ctx, oracle_mod, shs_gpu.Frame(W, H, ref_tile=(W, H)), [draw])
 
 
-@pytest.fixture(scope="module", params=[1, 2], ids=["scan", "bins"])
+@pytest.fixture(scope="module", params=[(1, 0), (2, 0), (1, 1), (2, 1)],
+                ids=["scan-pixel", "bins-pixel", "scan-pairs", "bins-pairs"])
 def mode_ctx(request):
     import shs_gpu
     ctx = shs_gpu.Context(0)
-    ctx.set_raster_mode(request.param)
+    ctx.set_raster_mode(request.param[0])
+    ctx.set_raster_loop(request.param[1])
     yield ctx
     ctx.close()
 
