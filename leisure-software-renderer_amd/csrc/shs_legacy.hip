@@ -746,18 +746,30 @@ __device__ __forceinline__ bool pixel_test(const FrameParams &fp, const TriRec &
     return z < FLT_MAX;   // NaN and FLT_MAX never beat the FLT_MAX clear
 }
 
-constexpr int RCHUNK = 128;        // candidate records staged per pass
+constexpr int RCHUNK = 64;         // candidate records staged per pass (one wave scans their areas)
 constexpr int LDS_DRAWS = 64;      // draws whose shading uniforms are kept in LDS
+constexpr int PAIR_WORDS = RCHUNK * RTW * RTH / 64;   // pair-start bitmap words (a box is <= 256 px)
+constexpr uint32_t SLOT_NONE = 127u;                  // key slot field: winner not staged in LDS
+
+// Candidate key: z_key with the low word (id << 7 | staging slot) when ids fit in 25 bits.  The order
+// is still (z, id) -- a triangle has one slot per tile -- and the slot lets the resolve read the
+// winner's records from LDS instead of HBM.  SLOT_NONE (multi-pass tiles, ghost fragments): HBM.
+__device__ __forceinline__ unsigned long long cand_key(float z, uint32_t id, bool slot_keys, uint32_t slot) {
+    return z_key(z, slot_keys ? (id << 7) | slot : id);
+}
 
 struct RasterShared {
-    float4 rec[RCHUNK * 6];           // staged triangle records (12 KB)
+    float4 rec[RCHUNK * 6];           // staged triangle records (6 KB)
+    float4 srec[RCHUNK * 5];          // staged shading records (single-pass tiles, 5 KB)
     unsigned long long key[RTH * RTW];// per-pixel (z, index) keys (2 KB)
+    unsigned long long bits[PAIR_WORDS]; // bit k: a staged candidate's pairs start at pair k (2 KB)
+    uint4 pinfo[RCHUNK];              // per staged candidate: first pair, x0 | y0 << 16, box width, 2^16/width
     uint32_t id[RCHUNK];
     uint32_t cand[CAND];
-    unsigned long long wmask[4];      // per-wave candidate-start masks (pair windows)
     float4 du[LDS_DRAWS * 4];         // per-draw {light, cam, ocol, colf} (4 KB)
     int busy[256];                    // this workgroup's busy tiles
-    uint32_t nc, nbusy, cov, maxbin;
+    uint32_t nc, nbusy, cov, maxbin, npairs;
+    uint8_t wown[PAIR_WORDS];         // staged candidate owning each bitmap word's first pair
 };
 
 // One busy raster tile.  Candidates (bin box overlaps the tile) are staged in LDS; every (candidate,
@@ -766,8 +778,8 @@ struct RasterShared {
 // each thread owns one pixel: the winner's record and varyings are fetched by index, (u, v, w)
 // recomputed with the identical arithmetic, the pixel shaded and written.
 __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
-                                            const uint32_t *cnt, int rt, const uint2 (&pbx)[CAND / 256], bool prefetched,
-                                            RasterShared &sh, uint64_t *tl) {
+                                            const uint32_t *cnt, uint32_t n_frag, int rt, const uint2 (&pbx)[CAND / 256],
+                                            bool prefetched, RasterShared &sh, uint64_t *tl) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tls = fp.setup_grid + (int)blockIdx.x;
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
@@ -792,6 +804,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     uint32_t seq = 0;   // candidates processed (profiling)
     int pairs = 0;      // (candidate, pixel) tasks (profiling)
     unsigned long long kmin = KEY_EMPTY;   // per-pixel loop: this thread's pixel key
+    const bool slot_keys = fp.n_tris < (1 << 25);
+    bool single = n_items <= (uint32_t)CAND;   // one gather round and one staging pass: winners in LDS
 
     for (uint32_t base = 0; base < n_items; base += CAND) {
         __syncthreads();
@@ -839,14 +853,17 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
         __syncthreads();
         tl_mark(tl, tls, 1);
         const uint32_t nc = sh.nc;
+        single = single && nc <= (uint32_t)RCHUNK;
         for (uint32_t c = 0; c < nc; c += RCHUNK) {
             const int m = (int)min((uint32_t)RCHUNK, nc - c);
             if (c > 0) __syncthreads();
-            // stage records: consecutive lanes load consecutive float4s of one record
+            // stage records (single-pass tiles: the shading records too, so the resolve reads no HBM):
+            // consecutive lanes load consecutive float4s of one record; all loads in one round trip
             if (tid < m) sh.id[tid] = sh.cand[c + tid];
+            for (int i = tid; i < m * (RTW * RTH / 64); i += 256) sh.bits[i] = 0ull;
             {
-                constexpr int NQ = RCHUNK * 6 / 256;
-                float4 q[NQ];
+                constexpr int NQ = (RCHUNK * 6 + 255) / 256, NS = (RCHUNK * 5 + 255) / 256;
+                float4 q[NQ], s[NS];
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) {
                     const int f = tid + 256 * k;
@@ -855,9 +872,21 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
 #pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    const int f = tid + 256 * k;
+                    const int ci = f / 5;
+                    s[k] = single && f < 5 * m ? reinterpret_cast<const float4 *>(&fb.shade[sh.cand[min(ci, m - 1)]])[f - 5 * ci]
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
                 for (int k = 0; k < NQ; ++k) {
                     const int f = tid + 256 * k;
                     if (f < 6 * m) sh.rec[f] = q[k];
+                }
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    const int f = tid + 256 * k;
+                    if (single && f < 5 * m) sh.srec[f] = s[k];
                 }
             }
             __syncthreads();
@@ -876,22 +905,22 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                     const TriRec r = rec_from(&sh.rec[cc * 6]);
                     float z;
                     if (pixel_test(fp, r, px, py, z)) {
-                        const unsigned long long k = z_key(z, sh.id[cc]);
+                        const unsigned long long k = cand_key(z, sh.id[cc], slot_keys, single ? (uint32_t)cc : SLOT_NONE);
                         kmin = k < kmin ? k : kmin;
                     }
                 }
                 seq += (uint32_t)m;
                 continue;
             }
-            // Pair tasks.  Wave w takes the staged candidates c = w + 4l (lane l holds candidate l of
-            // its list): clipped bin box in the tile, area, and the wave-inclusive prefix of the areas.
-            // The wave then walks its (candidate, pixel) pairs 64 at a time; a pair's owner is found
-            // by counting the candidate starts at or before it (ballot + 64-bit start mask), no search.
-            {
-                const int c = wave + 4 * lane;
+            // Pair tasks, dealt evenly over the workgroup.  Wave 0 lays the staged candidates' clipped
+            // bin boxes end to end (prefix of the areas; every staged box holds >= 1 pixel of the tile,
+            // so the starts are distinct) and marks each start in a bitmap over the pairs, plus the
+            // owner of every bitmap word's first pair.  Wave w then takes the 64-pair windows w, w + 4,
+            // ...: a pair's owner = that word's first owner + the starts in the word up to it.
+            if (wave == 0) {
                 int area = 0, bx0 = 0, by0 = 0, bw = 1;
-                if (c < m) {
-                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[c * 6])[4];   // ibx iby gbx gby
+                if (lane < m) {
+                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[lane * 6])[4];   // ibx iby gbx gby
                     const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
                     const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
                     if (x0 <= x1 && y0 <= y1) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
@@ -903,30 +932,33 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                     if (lane >= o) incl += v;
                 }
                 const int start = incl - area;
-                const int total = __shfl(incl, 63);
-                pairs += total;
-                for (int k0 = 0; k0 < total; k0 += 64) {
-                    // candidates starting inside [k0, k0 + 64): one bit each (areas >= 1: distinct starts)
-                    const bool in_win = area > 0 && start >= k0 && start < k0 + 64;
-                    if (lane == 0) sh.wmask[wave] = 0ull;
-                    wave_lds_sync();
-                    if (in_win) atomicOr(&sh.wmask[wave], 1ull << (start - k0));
-                    wave_lds_sync();
-                    const unsigned long long M = sh.wmask[wave];
-                    const int before = __popcll(__ballot(area > 0 && start < k0));
-                    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-                    const int o = before + __popcll(M & upto) - 1;            // owner (wave list index)
-                    const int k = k0 + lane;
-                    const int ostart = __shfl(start, o), ox0 = __shfl(bx0, o), oy0 = __shfl(by0, o), ow = __shfl(bw, o);
-                    if (k < total) {
-                        const int local = k - ostart;
-                        const int ly = local / ow, lx = local - ly * ow;
-                        const int oc = wave + 4 * o;
-                        const TriRec r = rec_from(&sh.rec[oc * 6]);
-                        float z;
-                        if (pixel_test(fp, r, ox0 + lx, oy0 + ly, z))
-                            atomicMin(&sh.key[(oy0 + ly - Y0) * RTW + (ox0 + lx - X0)], z_key(z, sh.id[oc]));
-                    }
+                if (area > 0) {
+                    // 2^16 / width rounded up: (local * magic) >> 16 == local / width for local < 256
+                    sh.pinfo[lane] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16), (uint32_t)bw,
+                                                (65536u + (uint32_t)bw - 1u) / (uint32_t)bw);
+                    atomicOr(&sh.bits[start >> 6], 1ull << (start & 63));
+                    for (int wd = (start + 63) >> 6; wd * 64 < incl; ++wd) sh.wown[wd] = (uint8_t)lane;
+                }
+                if (lane == 63) sh.npairs = (uint32_t)incl;
+            }
+            __syncthreads();
+            const int total = (int)sh.npairs;
+            pairs += total;
+            for (int k0 = 64 * wave; k0 < total; k0 += 256) {
+                const int k = k0 + lane;
+                if (k < total) {
+                    const unsigned long long wb = sh.bits[k0 >> 6];
+                    const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
+                    const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
+                    const uint4 pi = sh.pinfo[o];
+                    const int local = k - (int)pi.x;
+                    const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * (int)pi.z;
+                    const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
+                    const TriRec r = rec_from(&sh.rec[o * 6]);
+                    float z;
+                    if (pixel_test(fp, r, px, py, z))
+                        atomicMin(&sh.key[(py - Y0) * RTW + (px - X0)],
+                                  cand_key(z, sh.id[o], slot_keys, single ? (uint32_t)o : SLOT_NONE));
                 }
             }
             seq += (uint32_t)m;
@@ -935,11 +967,11 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     tl_mark(tl, tls, 3);
     // tile-clamp pixels of unbounded slivers outside their bbox that passed (k_setup ghost waves)
     {
-        const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
         for (uint32_t f = tid; f < n_frag; f += 256) {
             const GhostFrag g = fb.frags[f];
             const int gx = (int)(g.xy & 0xffffu), gy = (int)(g.xy >> 16);
-            if (gx >= X0 && gx <= X1 && gy >= Y0 && gy <= Y1) atomicMin(&sh.key[(gy - Y0) * RTW + (gx - X0)], z_key(g.z, g.id));
+            if (gx >= X0 && gx <= X1 && gy >= Y0 && gy <= Y1)
+                atomicMin(&sh.key[(gy - Y0) * RTW + (gx - X0)], cand_key(g.z, g.id, slot_keys, SLOT_NONE));
         }
     }
     __syncthreads();
@@ -954,18 +986,26 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
     const bool covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
     if (covered) {
-        const uint32_t id = (uint32_t)key;
+        const uint32_t lo = (uint32_t)key;
+        const uint32_t id = slot_keys ? lo >> 7 : lo, slot = slot_keys ? lo & SLOT_NONE : SLOT_NONE;
         TriRec r;
         ShadeRec sr;
         {
-            const float4 *s4 = reinterpret_cast<const float4 *>(&fb.recs[id]);
-            const float4 *h4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
             float4 *d4 = reinterpret_cast<float4 *>(&r);
             float4 *e4 = reinterpret_cast<float4 *>(&sr);
+            if (slot != SLOT_NONE) {   // only single-pass tiles encode a slot: the staged copies
 #pragma unroll
-            for (int k = 0; k < 6; ++k) d4[k] = s4[k];
+                for (int k = 0; k < 6; ++k) d4[k] = sh.rec[slot * 6 + k];
 #pragma unroll
-            for (int k = 0; k < 5; ++k) e4[k] = h4[k];
+                for (int k = 0; k < 5; ++k) e4[k] = sh.srec[slot * 5 + k];
+            } else {
+                const float4 *s4 = reinterpret_cast<const float4 *>(&fb.recs[id]);
+                const float4 *h4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) d4[k] = s4[k];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) e4[k] = h4[k];
+            }
         }
         float u, v, w;
         bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
@@ -1008,7 +1048,7 @@ __device__ __forceinline__ void clear_tile(const FrameParams &fp, const FrameBuf
 // Persistent raster: workgroup b takes owned raster tiles j = b, b + G, b + 2G, ...: the busy ones
 // are rasterized, the others cleared -- every pixel of the frame is written exactly once.
 template <bool KARG>
-__global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
+__global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
     const int tid = threadIdx.x;
     const uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
@@ -1018,9 +1058,22 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
     sh.key[tid] = KEY_EMPTY;
-    // per-draw shading uniforms into LDS; small scan-mode scenes: every bin box into registers
-    for (int i = tid; i < min(fp.n_draws, LDS_DRAWS) * 4; i += 256)
-        sh.du[i] = reinterpret_cast<const float4 *>(draws[i >> 2].light)[i & 3];
+    // Every independent first-touch load is issued up front so their HBM/MALL round trips overlap
+    // (each costs ~1-2 us at kernel start): the first round's busy flags, the ghost-fragment count,
+    // and for small scan-mode scenes every bin box (into registers).
+    auto owned_tile = [&](int j) -> int {
+        // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it; -1 past the frame
+        if (j >= fp.n_owned_rt) return -1;
+        const int t = fp.rank + (j >> 2) * fp.count;
+        const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / RTH) + (j & 3);
+        return row < fp.rtiles_y ? row * fp.tiles_x + col : -1;
+    };
+    const int rt_first = owned_tile((int)blockIdx.x + tid * G);
+    const uint32_t busy_first = rt_first >= 0 ? fb.busy[rt_first] : 0u;
+    const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
+    static_assert(LDS_DRAWS * 4 == 256, "one per-draw uniform float4 per thread");
+    const float4 du_first = tid < min(fp.n_draws, LDS_DRAWS) * 4 ? reinterpret_cast<const float4 *>(draws[tid >> 2].light)[tid & 3]
+                                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
     const bool prefetched = fp.scan_mode && fp.n_tris <= CAND;
     uint2 pbx[CAND / 256];
 #pragma unroll
@@ -1028,22 +1081,22 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
         const int i = tid + 256 * k;
         pbx[k] = (prefetched && i < fp.n_tris) ? fb.boxes[i] : make_uint2(0u, 0u);
     }
+    // pin the box loads here (the compiler would otherwise sink them to their first use, a second
+    // round trip after the busy flags)
+#pragma unroll
+    for (int k = 0; k < CAND / 256; ++k) asm volatile("" : "+v"(pbx[k].x), "+v"(pbx[k].y));
+    if (tid < min(fp.n_draws, LDS_DRAWS) * 4) sh.du[tid] = du_first;
     bool first = true;
     for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
         __syncthreads();
         if (tid == 0) sh.nbusy = 0;
         __syncthreads();
         // thread t checks owned raster tile j0 + t*G: busy ones are queued, the others cleared
-        const int j = j0 + tid * G;
-        if (j < fp.n_owned_rt) {
-            // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it
-            const int t = fp.rank + (j >> 2) * fp.count;
-            const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / RTH) + (j & 3);
-            if (row < fp.rtiles_y) {
-                const int rt = row * fp.tiles_x + col;
-                if (fb.busy[rt]) sh.busy[atomicAdd(&sh.nbusy, 1u) & 0xffffu] = rt;
-                else sh.busy[255 - atomicAdd(&sh.nbusy, 0x10000u) / 0x10000u] = rt;   // clear list from the top
-            }
+        const int rt = j0 == (int)blockIdx.x ? rt_first : owned_tile(j0 + tid * G);
+        if (rt >= 0) {
+            const uint32_t b = j0 == (int)blockIdx.x ? busy_first : fb.busy[rt];
+            if (b) sh.busy[atomicAdd(&sh.nbusy, 1u) & 0xffffu] = rt;
+            else sh.busy[255 - atomicAdd(&sh.nbusy, 0x10000u) / 0x10000u] = rt;   // clear list from the top
         }
         __syncthreads();
         tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
@@ -1058,8 +1111,8 @@ __global__ __launch_bounds__(256) void k_raster(FrameParams fp, FrameBuffers fb,
                 if (tid == 0) fb.busy[rt] = 0u;
                 continue;
             }
-            if (fp.flags & DBG_TWICE) raster_tile(fp, fb, draws, cnt, rt, pbx, prefetched, sh, nullptr);   // warm run
-            raster_tile(fp, fb, draws, cnt, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
+            if (fp.flags & DBG_TWICE) raster_tile(fp, fb, draws, cnt, n_frag, rt, pbx, prefetched, sh, nullptr);   // warm run
+            raster_tile(fp, fb, draws, cnt, n_frag, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
             first = false;
         }
         for (int i = 0; i < ne; ++i) clear_tile(fp, fb, sh.busy[255 - i]);
