@@ -188,7 +188,9 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fp.setup_blocks = setup_blocks;
     const int owned_bt = (n_tiles - fp.rank + fp.count - 1) / fp.count;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / 8);
-    const int raster_grid = std::max(1, std::min(fp.n_owned_rt, 256 * 4));
+    int &resident = ctx->lib_resident[shadow ? 1 : 0];
+    if (resident <= 0) resident = shs_internal::lib_raster_resident_blocks(ctx->device, shadow);
+    const int raster_grid = std::max(1, std::min(fp.n_owned_rt, resident));
     if (ensure(ctx, w.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
 
     LibBuffers fb;

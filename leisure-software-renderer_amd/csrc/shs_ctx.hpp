@@ -126,6 +126,7 @@ struct shs_ctx {
         int64_t acc_n = 0;
     };
     LibWork lib_cam, lib_shadow;
+    int lib_resident[2] = {0, 0};         // resident k_lib_raster workgroups (camera, shadow)
     DevBuf<float4> lib_hdr;
     DevBuf<float> lib_depth;
     DevBuf<float2> lib_motion;

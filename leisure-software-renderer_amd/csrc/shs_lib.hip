@@ -25,6 +25,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <climits>
 
 #include "shs_device.hpp"
 #include "shs_lib_device.hpp"
@@ -116,7 +117,7 @@ __device__ __forceinline__ float plane_dist(const LVert &v, int p) {   // plane_
 
 // detail::clip_polygon_frustum (:111-164) for the rare triangles that are not trivially inside.
 // Returns the polygon size (<= MAX_POLY); out holds the result.
-__device__ __noinline__ int clip_frustum(const LVert (&tri)[3], LVert (&out)[MAX_POLY]) {
+__device__ __forceinline__ int clip_frustum(const LVert (&tri)[3], LVert (&out)[MAX_POLY]) {
     LVert buf[2][MAX_POLY];
     int n = 3;
 #pragma unroll
@@ -160,7 +161,7 @@ __device__ __forceinline__ void lib_append_bin(const LibFrameParams &fp, const L
 
 // Busy marks on the owned raster tiles of [x0,x1] x [y0,y1] and (bin mode) per-bin-tile appends,
 // tiles k0, k0 + dk, ... of the box (one thread: k0 = 0, dk = 1; a whole block: k0 = tid, dk = 256).
-__device__ void lib_mark_range(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
+__device__ __forceinline__ void lib_mark_range(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
                                uint32_t slot, int k0, int dk) {
     const bool sharded = fp.count > 1;
     {
@@ -185,14 +186,32 @@ __device__ void lib_mark_range(const LibFrameParams &fp, const LibBuffers &fb, u
 // setup block after its triangles are done (a floor triangle at 4K spans thousands of tiles).
 constexpr int SMALL_MARK = 8;
 constexpr int BIG_CAP = 512;
+// Block-aggregated marks: every thread may defer one primitive of <= 2x2 bin tiles; the block then
+// counts its appends per bin tile in LDS over the union of the deferred boxes and takes one global
+// atomicAdd per touched bin tile (a block's triangles are neighbours in the mesh, so the union is
+// small; C4's 1M triangles otherwise hit each bin counter ~120 times).  List order inside a bin does
+// not matter: the raster resolves by (z, submission index) keys.
+constexpr int AGG_BINS = 256;             // union capacity in bin tiles (else the per-primitive path)
+struct Pend {
+    uint32_t slot = 0;
+    int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+    bool valid = false;
+};
 struct SetupShared {
     uint4 big[BIG_CAP];       // (slot, bx, by, 0)
     uint32_t nbig;
     uint32_t stat[2];
+    int ub[4];                // union of deferred bin rects: bx0, by0, bx1, by1
+    uint32_t bcnt[AGG_BINS];  // per union bin tile: deferred appends, then their base in the bin list
+    uint32_t rbusy[AGG_BINS]; // per union bin tile: bit r = raster row r of it is busy
 };
 
-__device__ void lib_mark(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
-                         uint32_t slot, SetupShared &ss) {
+__device__ __forceinline__ void lib_mark(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
+                         uint32_t slot, SetupShared &ss, Pend &pend) {
+    if (!pend.valid && (x1 / TILE - x0 / TILE) < 2 && (y1 / TILE - y0 / TILE) < 2) {
+        pend.slot = slot; pend.x0 = x0; pend.x1 = x1; pend.y0 = y0; pend.y1 = y1; pend.valid = true;
+        return;
+    }
     const int n_rt = (x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1);
     if (n_rt > SMALL_MARK) {
         const uint32_t q = atomicAdd(&ss.nbig, 1u);
@@ -211,9 +230,9 @@ __device__ __forceinline__ void store_box(const LibBuffers &fb, uint32_t slot, i
 // One fan triangle of rasterize_mesh (rasterizer.hpp:255-328): NDC, screen (y-up), the area /
 // cull / bbox rejects; writes the primitive's record, varyings and box into slot.  Counts
 // tri_after_clip / tri_raster like the reference.
-__device__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, const LibDrawGPU &dr, int d,
+__device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, const LibDrawGPU &dr, int d,
                          uint32_t seq, uint32_t slot, const LVert &a, const LVert &b, const LVert &c, uint32_t &n_clip,
-                         uint32_t &n_rast, SetupShared &ss) {
+                         uint32_t &n_rast, SetupShared &ss, Pend &pend) {
     ++n_clip;
     const LVert *v[3] = {&a, &b, &c};
     float sx[3], sy[3];
@@ -273,7 +292,7 @@ __device__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_
     s.pad[0] = s.pad[1] = s.pad[2] = 0;
     fb.shade[slot] = s;
     store_box(fb, slot, x0, x1, y0, y1);
-    lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot, ss);
+    lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot, ss, pend);
 }
 
 __device__ __forceinline__ int lib_find_draw(const LibDrawGPU *draws, int n_draws, int gid) {
@@ -291,9 +310,12 @@ __device__ __forceinline__ bool read_tri(const LibDrawGPU &dr, int local, uint32
     return id[0] < (uint32_t)dr.n_verts && id[1] < (uint32_t)dr.n_verts && id[2] < (uint32_t)dr.n_verts;
 }
 
+__device__ uint2 setup_clipped_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int d, int tri, uint32_t i0,
+                                   uint32_t i1, uint32_t i2, SetupShared &ss, Pend &pend);
+
 // Camera pass: one input triangle of rasterize_mesh.
-__device__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_clip,
-                                 uint32_t &n_rast, SetupShared &ss) {
+__device__ __forceinline__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_clip,
+                                 uint32_t &n_rast, SetupShared &ss, Pend &pend) {
     const int d = lib_find_draw(fb.draws, fp.n_draws, tri);
     const LibDrawGPU &dr = fb.draws[d];
     const int local = tri - dr.tri_base;
@@ -307,14 +329,29 @@ __device__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb,
     for (int k = 0; k < 3; ++k) t[k] = vertex_out(dr, id[k]);
     const uint32_t seq0 = (uint32_t)tri * 16u;
     if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
-        emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast, ss);
+        emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast, ss, pend);
         return;
     }
+    const uint2 nc = setup_clipped_tri(fp, fb, cnt, d, tri, id[0], id[1], id[2], ss, pend);
+    n_clip += nc.x;
+    n_rast += nc.y;
+}
+
+// The clipping half of setup_camera_tri (inlined; only this branch touches the scratch-resident
+// polygon buffers, so the trivially-inside path keeps its vertices in registers).  The corners are
+// recomputed from their ids with the identical arithmetic.  Returns the (tri_after_clip,
+// tri_raster) increments.
+__device__ __forceinline__ uint2 setup_clipped_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int d, int tri,
+                                                   uint32_t i0, uint32_t i1, uint32_t i2, SetupShared &ss, Pend &pend) {
+    uint32_t n_clip = 0, n_rast = 0;
+    const LibDrawGPU &dr = fb.draws[d];
+    const LVert t[3] = {vertex_out(dr, i0), vertex_out(dr, i1), vertex_out(dr, i2)};
+    const uint32_t seq0 = (uint32_t)tri * 16u;
     LVert poly[MAX_POLY];
     const int n = clip_frustum(t, poly);
     if (n < 3) {
         store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
-        return;
+        return make_uint2(0u, 0u);
     }
     uint32_t xb = 0;
     if (n > 3) {   // fans 1 .. n-3 take consecutive extra slots
@@ -322,21 +359,22 @@ __device__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb,
         if (e + (uint32_t)(n - 3) > fp.extra_cap) {
             atomicOr(&cnt[LC_OVERFLOW], LOV_EXTRA);
             store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
-            return;
+            return make_uint2(0u, 0u);
         }
         xb = (uint32_t)fp.n_tris + e;
         fb.xbase[tri] = xb;
     }
     for (int k = 1; k + 1 < n; ++k) {
         const uint32_t slot = k == 1 ? (uint32_t)tri : xb + (uint32_t)(k - 2);
-        emit_fan(fp, fb, cnt, dr, d, seq0 + (uint32_t)(k - 1), slot, poly[0], poly[k], poly[k + 1], n_clip, n_rast, ss);
+        emit_fan(fp, fb, cnt, dr, d, seq0 + (uint32_t)(k - 1), slot, poly[0], poly[k], poly[k + 1], n_clip, n_rast, ss, pend);
     }
+    return make_uint2(n_clip, n_rast);
 }
 
 // Shadow pass: one caster triangle of PassShadowMap (pass_shadow_map.hpp:155-203), draws[d].viewproj
 // holding the light camera's viewproj.  n_rast counts the triangles with a non-empty bbox.
-__device__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_rast,
-                                 SetupShared &ss) {
+__device__ __forceinline__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_rast,
+                                 SetupShared &ss, Pend &pend) {
     const int d = lib_find_draw(fb.draws, fp.n_draws, tri);
     const LibDrawGPU &dr = fb.draws[d];
     const int local = tri - dr.tri_base;
@@ -392,7 +430,7 @@ __device__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb,
     r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
     fb.recs[tri] = r;
     store_box(fb, (uint32_t)tri, x0, x1, y0, y1);
-    lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri, ss);
+    lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri, ss, pend);
 }
 
 template <bool SHADOW>
@@ -402,6 +440,10 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
     if (tid < 2) ss.stat[tid] = 0u;
     if (tid == 0) ss.nbig = 0u;
+    if (tid < 4) ss.ub[tid] = tid < 2 ? INT_MAX : -1;
+    static_assert(AGG_BINS == 256, "one union bin tile per thread");
+    ss.bcnt[tid] = 0u;
+    ss.rbusy[tid] = 0u;
     // zero the other counter set and bin counts for the next frame
     if (b == 0 && tid < LC_N) fb.counters[(fp.parity ^ 1u) * LC_N + tid] = 0u;
     {
@@ -412,9 +454,16 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
     __syncthreads();
     const int tri = b * 256 + tid;
     uint32_t n_clip = 0, n_rast = 0;
+    Pend pend;
     if (tri < fp.n_tris) {
-        if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss);
-        else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss);
+        if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend);
+        else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend);
+    }
+    if (pend.valid) {
+        atomicMin(&ss.ub[0], pend.x0 / TILE);
+        atomicMin(&ss.ub[1], pend.y0 / TILE);
+        atomicMax(&ss.ub[2], pend.x1 / TILE);
+        atomicMax(&ss.ub[3], pend.y1 / TILE);
     }
     for (int o = 32; o > 0; o >>= 1) {
         n_clip += __shfl_down(n_clip, o);
@@ -425,6 +474,60 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
         atomicAdd(&ss.stat[1], n_rast);
     }
     __syncthreads();
+    // the deferred primitives (<= 2x2 bin tiles each): busy rows and bin appends through LDS
+    {
+        const int ubx0 = ss.ub[0], uby0 = ss.ub[1], uw = ss.ub[2] - ubx0 + 1, uh = ss.ub[3] - uby0 + 1;
+        const bool agg = uw > 0 && uh > 0 && uw * uh <= AGG_BINS;   // block-uniform
+        const bool sharded = fp.count > 1;
+        constexpr int RPB = TILE / LIB_RTH;                        // raster rows per bin tile
+        const int bx0 = pend.x0 / TILE, by0 = pend.y0 / TILE, bx1 = pend.x1 / TILE, by1 = pend.y1 / TILE;
+        uint32_t pos[2][2] = {{0u, 0u}, {0u, 0u}};
+        if (pend.valid) {
+            if (!agg) {
+                lib_mark_range(fp, fb, cnt, pend.x0, pend.x1, pend.y0, pend.y1, pend.slot, 0, 1);
+            } else {
+                for (int ry = pend.y0 / LIB_RTH; ry <= pend.y1 / LIB_RTH; ++ry) {
+                    const int by = ry / RPB;
+                    for (int rx = pend.x0 / LIB_RTW; rx <= pend.x1 / LIB_RTW; ++rx)
+                        if (!sharded || lib_owned(fp, rx, by))
+                            atomicOr(&ss.rbusy[(by - uby0) * uw + (rx - ubx0)], 1u << (ry % RPB));
+                }
+                if (!fp.scan_mode) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int i = 0; i < 2; ++i)
+                            if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j)))
+                                pos[j][i] = atomicAdd(&ss.bcnt[(by0 + j - uby0) * uw + (bx0 + i - ubx0)], 1u);
+                }
+            }
+        }
+        if (agg) {
+            __syncthreads();
+            if (tid < uw * uh) {
+                const int bx = ubx0 + tid % uw, by = uby0 + tid / uw;
+                const uint32_t rb = ss.rbusy[tid];
+                for (int r = 0; r < RPB; ++r)
+                    if ((rb >> r) & 1u) fb.busy[(by * RPB + r) * fp.tiles_x + bx] = 1u;
+                const uint32_t n = ss.bcnt[tid];
+                if (!fp.scan_mode && n) {
+                    uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
+                    ss.bcnt[tid] = atomicAdd(&tcount[by * fp.tiles_x + bx], n);
+                }
+            }
+            __syncthreads();
+            if (pend.valid && !fp.scan_mode) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j))) {
+                            const int u = (by0 + j - uby0) * uw + (bx0 + i - ubx0);
+                            lib_append_bin(fp, fb, cnt, (by0 + j) * fp.tiles_x + bx0 + i, ss.bcnt[u] + pos[j][i], pend.slot);
+                        }
+            }
+        }
+    }
     // the block's large primitives: every thread takes every 256th of their tiles
     const uint32_t nbig = min(ss.nbig, (uint32_t)BIG_CAP);
     for (uint32_t i = 0; i < nbig; ++i) {
@@ -659,13 +762,19 @@ __device__ __forceinline__ float4 bg_color(const LibFrameParams &fp, int y) {
     return make_float4(0.06f + 0.08f * t, 0.08f + 0.10f * t, 0.12f + 0.12f * t, 1.0f);
 }
 
+constexpr int LIB_PAIR_WORDS = LIB_CHUNK * LIB_RTW * LIB_RTH / 64;   // pair-start bitmap words
+
 struct LibShared {
     float4 rec[LIB_CHUNK * 4];            // staged records (8 KB)
     unsigned long long key[LIB_RTH * LIB_RTW];
+    unsigned long long bits[LIB_PAIR_WORDS]; // bit k: a surviving candidate's pairs start at pair k (4 KB)
+    uint4 pinfo[LIB_CHUNK];               // per surviving candidate: first pair, x0 | y0 << 16, width | slot << 16, 2^16/width
     uint32_t cand[LIB_CAND];
-    unsigned long long wmask[4];
     int busy[256];
-    uint32_t nc, nbusy, cov, maxbin;
+    uint32_t wtot[4][2];                  // per wave: surviving candidates, pairs
+    uint32_t ordmax[2];                   // tile's max per-pixel key z (orderable bits), by chunk parity
+    uint32_t nc, nbusy, cov, maxbin, npairs;
+    uint8_t wown[LIB_PAIR_WORDS];         // surviving candidate owning each bitmap word's first pair
 };
 
 __device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
@@ -747,9 +856,42 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
     }
 }
 
+// Orderable key bits (z_key's high word) of a conservative lower bound of the depth lib_test can
+// produce anywhere on the primitive.  The camera pass's 1/w depth is a weighted mean of the corners'
+// clip z (weights bc_k / w_k >= 0) or, linear, 1 / sum(bc_k / w_k) with sum(bc) = 1 +- 2 ulp -- both
+// bounded below by the corner minimum; the shadow pass's affine NDC z likewise.  The margin (1e-5
+// of the magnitudes, ~170 ulp) covers every rounding on the way.  Non-finite inputs never cull (0).
 template <bool SHADOW>
-__device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared &sh) {
+__device__ __forceinline__ uint32_t lib_zmin_ord(const LibFrameParams &fp, const LibRec &r) {
+    float z01;
+    if (SHADOW) {
+        if (!(isfinite(r.z0) && isfinite(r.z1) && isfinite(r.z2))) return 0u;
+        const float lo = fminf(fminf(r.z0, r.z1), r.z2);
+        const float mag = fmaxf(fmaxf(fabsf(r.z0), fabsf(r.z1)), fabsf(r.z2));
+        z01 = s_clamp((lo - 1e-5f * (1.0f + mag)) * 0.5f + 0.5f, 0.0f, 1.0f);
+    } else {
+        if (!(r.iw0 > 0.0f && r.iw1 > 0.0f && r.iw2 > 0.0f && isfinite(r.iw0) && isfinite(r.iw1) && isfinite(r.iw2)))
+            return 0u;
+        if (fp.flags & LF_LINZ) {
+            const float lo = fminf(fminf(1.0f / r.iw0, 1.0f / r.iw1), 1.0f / r.iw2);
+            z01 = g_clamp((lo * (1.0f - 1e-5f) - fp.zn) / fp.zspan, 0.0f, 1.0f);
+        } else {
+            const float c0 = r.z0 / r.iw0, c1 = r.z1 / r.iw1, c2 = r.z2 / r.iw2;
+            if (!(isfinite(c0) && isfinite(c1) && isfinite(c2))) return 0u;
+            const float lo = fminf(fminf(c0, c1), c2);
+            const float mag = fmaxf(fmaxf(fabsf(c0), fabsf(c1)), fabsf(c2));
+            z01 = g_clamp((lo - 1e-5f * (1.0f + mag)) * 0.5f + 0.5f, 0.0f, 1.0f);
+        }
+    }
+    if (!isfinite(z01)) return 0u;
+    return (uint32_t)(z_key(z01, 0u) >> 32);
+}
+
+template <bool SHADOW>
+__device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared &sh,
+                                uint32_t &chunk) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool hiz = SHADOW || (fp.flags & LF_DEPTH);   // painter's order (no depth target): never
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
     const int X0 = col * LIB_RTW, Y0 = row * LIB_RTH;
     const int X1 = X0 + LIB_RTW - 1, Y1 = Y0 + LIB_RTH - 1;
@@ -807,6 +949,13 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         for (uint32_t c = 0; c < nc; c += LIB_CHUNK) {
             const int m = (int)min((uint32_t)LIB_CHUNK, nc - c);
             if (c > 0) __syncthreads();
+            if (hiz) {   // the tile's largest per-pixel key z so far (all earlier pairs are resolved)
+                uint32_t o = (uint32_t)(sh.key[tid] >> 32);
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) o = max(o, (uint32_t)__shfl_xor((int)o, off));
+                if (lane == 0) atomicMax(&sh.ordmax[chunk & 1u], o);
+            }
+            for (int i = tid; i < m * (LIB_RTW * LIB_RTH / 64); i += 256) sh.bits[i] = 0ull;
             {   // stage records: consecutive lanes load consecutive float4s of one record
                 constexpr int NQ = LIB_CHUNK * 4 / 256;
                 float4 q[NQ];
@@ -824,47 +973,70 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 }
             }
             __syncthreads();
-            // (primitive, pixel) pair tasks: wave w takes staged candidates w + 4l; their clipped
-            // boxes' areas are prefix-summed and walked 64 pairs at a time (see shs_legacy.hip).
+            // Candidates that cannot win any pixel are dropped before pair expansion (hierarchical z):
+            // a conservative lower bound of the primitive's depth over its whole extent (lib_zmin_ord)
+            // above the tile's largest current per-pixel key z.  The survivors' clipped boxes are laid
+            // end to end (block prefix of the areas) and every (primitive, pixel) pair is dealt to one
+            // lane, 64-pair windows round-robin over the waves (start bitmap + word owners, as in
+            // shs_legacy.hip).
             {
-                const int cidx = wave + 4 * lane;
+                const uint32_t ordmax = sh.ordmax[chunk & 1u];
+                if (tid == 0) sh.ordmax[(chunk + 1u) & 1u] = 0u;   // next chunk's max starts here
                 int area = 0, bx0 = 0, by0 = 0, bw = 1;
-                if (cidx < m) {
-                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[cidx * 4])[3];   // iw2 seq bx by
+                if (tid < m) {
+                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[tid * 4])[3];   // iw2 seq bx by
                     const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
                     const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
-                    if (x0 <= x1 && y0 <= y1) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
+                    bool live = x0 <= x1 && y0 <= y1;
+                    if (live && hiz && ordmax != 0xffffffffu)
+                        live = lib_zmin_ord<SHADOW>(fp, lib_rec_from(&sh.rec[tid * 4])) <= ordmax;
+                    if (live) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
                 }
+                const uint64_t alive = __ballot(area > 0);
                 int incl = area;
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) {
                     const int vv = __shfl_up(incl, o);
                     if (lane >= o) incl += vv;
                 }
-                const int start = incl - area;
-                const int total = __shfl(incl, 63);
-                for (int k0 = 0; k0 < total; k0 += 64) {
-                    const bool in_win = area > 0 && start >= k0 && start < k0 + 64;
-                    if (lane == 0) sh.wmask[wave] = 0ull;
-                    wave_lds_sync();
-                    if (in_win) atomicOr(&sh.wmask[wave], 1ull << (start - k0));
-                    wave_lds_sync();
-                    const unsigned long long M = sh.wmask[wave];
-                    const int before = __popcll(__ballot(area > 0 && start < k0));
-                    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-                    const int o = before + __popcll(M & upto) - 1;
+                if (lane == 63) { sh.wtot[wave][0] = (uint32_t)__popcll(alive); sh.wtot[wave][1] = (uint32_t)incl; }
+                __syncthreads();
+                uint32_t cbase = 0, pbase = 0, ntot = 0, ptot = 0;
+#pragma unroll
+                for (int w2 = 0; w2 < 4; ++w2) {
+                    const uint32_t c2 = sh.wtot[w2][0], p2 = sh.wtot[w2][1];
+                    if (w2 < wave) { cbase += c2; pbase += p2; }
+                    ntot += c2; ptot += p2;
+                }
+                if (area > 0) {
+                    const int ci = (int)cbase + lanes_below(alive);
+                    const int start = (int)pbase + incl - area;
+                    sh.pinfo[ci] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16),
+                                              (uint32_t)bw | ((uint32_t)tid << 16), (65536u + (uint32_t)bw - 1u) / (uint32_t)bw);
+                    atomicOr(&sh.bits[start >> 6], 1ull << (start & 63));
+                    for (int wd = (start + 63) >> 6; wd * 64 < start + area; ++wd) sh.wown[wd] = (uint8_t)ci;
+                }
+                __syncthreads();
+                const int total = (int)ptot;
+                for (int k0 = 64 * wave; k0 < total; k0 += 256) {
                     const int k = k0 + lane;
-                    const int ostart = __shfl(start, o), ox0 = __shfl(bx0, o), oy0 = __shfl(by0, o), ow = __shfl(bw, o);
                     if (k < total) {
-                        const int local = k - ostart;
-                        const int ly = local / ow, lx = local - ly * ow;
-                        const LibRec r = lib_rec_from(&sh.rec[(wave + 4 * o) * 4]);
+                        const unsigned long long wb = sh.bits[k0 >> 6];
+                        const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
+                        const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
+                        const uint4 pi = sh.pinfo[o];
+                        const int local = k - (int)pi.x, ow = (int)(pi.z & 0xffffu);
+                        const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * ow;
+                        const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
+                        const LibRec r = lib_rec_from(&sh.rec[(pi.z >> 16) * 4]);
                         float z01, u, v, w, idn;
-                        if (lib_test<SHADOW>(fp, r, ox0 + lx, oy0 + ly, z01, u, v, w, idn))
-                            atomicMin(&sh.key[(oy0 + ly - Y0) * LIB_RTW + (ox0 + lx - X0)], lib_key(fp, z01, r.seq, SHADOW));
+                        if (lib_test<SHADOW>(fp, r, px, py, z01, u, v, w, idn))
+                            atomicMin(&sh.key[(py - Y0) * LIB_RTW + (px - X0)], lib_key(fp, z01, r.seq, SHADOW));
                     }
                 }
+                (void)ntot;
             }
+            ++chunk;
         }
     }
     __syncthreads();
@@ -888,13 +1060,14 @@ __device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const L
 }
 
 template <bool SHADOW>
-__global__ __launch_bounds__(256) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
+__global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
     __shared__ LibShared sh;
     const int tid = threadIdx.x;
     const uint32_t *cnt = fb.counters + fp.parity * LC_N;
     const int G = (int)gridDim.x;
-    if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
+    if (tid == 0) { sh.cov = 0; sh.maxbin = 0; sh.ordmax[0] = 0u; sh.ordmax[1] = 0u; }
     sh.key[tid] = KEY_EMPTY;
+    uint32_t chunk = 0;   // staging passes so far (selects the ordmax slot)
     for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
         __syncthreads();
         if (tid == 0) sh.nbusy = 0;
@@ -912,7 +1085,7 @@ __global__ __launch_bounds__(256) void k_lib_raster(LibFrameParams fp, LibBuffer
         }
         __syncthreads();
         const int nb = (int)(sh.nbusy & 0xffffu), ne = (int)(sh.nbusy >> 16);
-        for (int i = 0; i < nb; ++i) lib_raster_tile<SHADOW>(fp, fb, cnt, sh.busy[i], sh);
+        for (int i = 0; i < nb; ++i) lib_raster_tile<SHADOW>(fp, fb, cnt, sh.busy[i], sh, chunk);
         for (int i = 0; i < ne; ++i) lib_clear_tile<SHADOW>(fp, fb, sh.busy[255 - i]);
     }
     __syncthreads();
@@ -929,6 +1102,17 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
     if (shadow) hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     else hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
+}
+
+int lib_raster_resident_blocks(int device, bool shadow) {
+    // persistent grid: every workgroup resident at once (CUs x the kernel's occupancy)
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    const hipError_t e = shadow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lib_raster<true>, 256, 0)
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lib_raster<false>, 256, 0);
+    if (e != hipSuccess || per_cu <= 0) per_cu = 2;
+    (void)hipGetLastError();   // a failed query must not leave a sticky error for the host's next HIP user
+    return cus * per_cu;
 }
 
 hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, int grid, hipStream_t s) {

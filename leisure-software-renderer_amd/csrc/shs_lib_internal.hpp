@@ -7,6 +7,7 @@
 namespace shs_internal {
 // shadow = true: PassShadowMap's depth pass; false: rasterize_mesh + builtin programs.
 hipError_t launch_lib_setup(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, hipStream_t s);
+int lib_raster_resident_blocks(int device, bool shadow);   // CUs x occupancy of k_lib_raster
 hipError_t launch_lib_raster(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, int grid,
                              hipStream_t s);
 }  // namespace shs_internal

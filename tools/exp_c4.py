@@ -1,0 +1,54 @@
+"""C4 cost breakdown (GPU box): kernel times of the library path under scene variants.
+
+usage: python tools/exp_c4.py [frames]
+Each variant prints mean k_lib_setup / k_lib_raster ms over `frames` frames and the pass stats."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "leisure-software-renderer_amd"), ROOT]
+import shs_gpu  # noqa: E402
+from shs_gpu import lib_path, scene_lib  # noqa: E402
+
+
+def run(label, n_objects=1000, tpo=1000, program=None, width=3840, height=2160, frames=20):
+    frame, draws, lights, cull = scene_lib.c4_scene(width, height, n_objects=n_objects, tris_per_object=tpo)
+    if program is not None:
+        for d in draws:
+            d.program = program
+    ctx = shs_gpu.Context(0)
+    ctx.upload_lights(lights)
+    ctx.light_cull(cull)
+    prepared = ctx.prepare_lib(frame, draws)
+    for _ in range(3):
+        ctx.light_cull(cull)
+        ctx.render_pbr_forward_prepared(prepared)
+    ctx.synchronize_lib()
+    st = ctx.lib_stats()
+    ctx.enable_timing(True)
+    ctx.lib_timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        ctx.light_cull(cull)
+        ctx.render_pbr_forward_prepared(prepared)
+    ctx.synchronize_lib()
+    dt = (time.perf_counter() - t0) / frames * 1e3
+    _, kms = ctx.lib_timing_read()
+    ctx.close()
+    print(f"{label:28s} frame {dt:7.3f} ms  setup {kms['setup']:7.3f}  raster {kms['raster']:7.3f}  "
+          f"clip {st['tri_after_clip']} rast {st['tri_raster']} cov {st['covered_pixels']} maxbin {st['max_tile_bin']} "
+          f"spill {st['spilled']} extra {st['clipped_extra']}", flush=True)
+
+
+def main():
+    frames = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    run("c4", frames=frames)
+    run("c4 debug-albedo", program=lib_path.PROGRAM_DEBUG_ALBEDO, frames=frames)
+    run("c4 250k tris", n_objects=250, frames=frames)
+    run("c4 100 obj x 100", n_objects=100, tpo=100, frames=frames)
+    run("c4 1080p", width=1920, height=1080, frames=frames)
+
+
+if __name__ == "__main__":
+    main()
