@@ -156,6 +156,11 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value);
  * order), then S slots per k_setup workgroup followed by S per k_raster workgroup: start, end, and
  * phase marks of the workgroup's thread 0 (0 where a phase did not run). */
 int shs_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out);
+/* Debug / profiling hook: the last camera pass's k_lib_raster workgroup timeline (SHS_OPT_TIMELINE),
+ * 12 uint64 per workgroup: start, end, summed ticks of gather / stage + pairs / resolve + shade over
+ * its busy tiles, clear ticks, busy tiles, cleared tiles, staging passes, pairs, candidates, longest
+ * busy tile (s_memrealtime, 100 MHz).  out = NULL: *n_out = the count only. */
+int shs_lib_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out);
 
 /* Library/ABI version for integration checks; edge of the square GPU screen tile (shard unit). */
 int shs_abi_version(void);

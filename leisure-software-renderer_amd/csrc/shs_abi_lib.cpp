@@ -206,6 +206,12 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         fb.lights = ctx->lights.p;
         fb.tile_counts = ctx->list_counts.p;
         fb.tile_indices = ctx->list_indices.p;
+        if (ctx->want_timeline) {
+            const size_t n = (size_t)raster_grid * shs_dev::LTL_STRIDE;
+            if (ensure(ctx, ctx->lib_timeline, n)) return SHS_ERR_HIP;
+            HIP_TRY(ctx, hipMemsetAsync(ctx->lib_timeline.p, 0, n * sizeof(uint64_t), ctx->stream));
+            fb.timeline = ctx->lib_timeline.p;
+        }
     }
     hipEvent_t *ev = nullptr;
     if (ctx->timing) {
@@ -301,7 +307,7 @@ void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_shadow);
     release(ctx->lib_hdr); release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
     release(ctx->lights); release(ctx->light_proj); release(ctx->depth_ranges);
-    release(ctx->list_counts); release(ctx->list_indices);
+    release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
 }
@@ -499,6 +505,22 @@ int shs_resolve_shadow_map(shs_ctx *ctx, float *depth) {
     int rc = lib_finish(ctx);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(depth, ctx->shadow_map.p, (size_t)ctx->shadow_w * ctx->shadow_h * sizeof(float), hipMemcpyDeviceToHost));
+    return SHS_OK;
+}
+
+int shs_lib_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out) {
+    if (!ctx || !n_out) return SHS_ERR_INVALID;
+    if (!ctx->want_timeline || !ctx->lib_timeline.p || ctx->lib_cam.last_raster_grid <= 0) {
+        ctx->err = "timeline not enabled or no camera pass yet";
+        return SHS_ERR_INVALID;
+    }
+    const int64_t n = (int64_t)ctx->lib_cam.last_raster_grid * shs_dev::LTL_STRIDE;
+    *n_out = n;
+    if (!out) return SHS_OK;
+    if (capacity < n) { ctx->err = "capacity too small"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(out, ctx->lib_timeline.p, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return SHS_OK;
 }
 

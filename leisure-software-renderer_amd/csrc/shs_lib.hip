@@ -558,10 +558,13 @@ __device__ __forceinline__ bool lib_test(const LibFrameParams &fp, const LibRec 
     const float denom = (u * r.iw0 + v * r.iw1) + w * r.iw2;
     if (denom <= 1e-10f) return false;
     inv_denom = 1.0f / denom;
+    if ((fp.flags & (LF_DEPTH | LF_LINZ)) == (LF_DEPTH | LF_LINZ)) {   // linear view depth replaces z01
+        z01 = g_clamp((inv_denom - fp.zn) / fp.zspan, 0.0f, 1.0f);
+        return z01 < 1.0f;
+    }
     const float z_clip = (u * r.z0 + v * r.z1) + w * r.z2;
     z01 = g_clamp((z_clip * inv_denom) * 0.5f + 0.5f, 0.0f, 1.0f);
     if (!(fp.flags & LF_DEPTH)) return true;   // no depth_motion target: every fragment writes
-    if (fp.flags & LF_LINZ) z01 = g_clamp((1.0f / denom - fp.zn) / fp.zspan, 0.0f, 1.0f);
     return z01 < 1.0f;                         // depth cleared to 1, `if (z01 >= zbuf) continue`
 }
 
@@ -769,13 +772,17 @@ struct LibShared {
     unsigned long long key[LIB_RTH * LIB_RTW];
     unsigned long long bits[LIB_PAIR_WORDS]; // bit k: a surviving candidate's pairs start at pair k (4 KB)
     uint4 pinfo[LIB_CHUNK];               // per surviving candidate: first pair, x0 | y0 << 16, width | slot << 16, 2^16/width
+    uint32_t zord[LIB_CHUNK];             // per surviving candidate: lib_zmin_ord (0: never skipped)
     uint32_t cand[LIB_CAND];
     int busy[256];
     uint32_t wtot[4][2];                  // per wave: surviving candidates, pairs
     uint32_t ordmax[2];                   // tile's max per-pixel key z (orderable bits), by chunk parity
     uint32_t nc, nbusy, cov, maxbin, npairs;
+    uint64_t tl[LTL_STRIDE];              // SHS_OPT_TIMELINE accumulators (thread 0)
     uint8_t wown[LIB_PAIR_WORDS];         // surviving candidate owning each bitmap word's first pair
 };
+
+__device__ __forceinline__ uint64_t tl_now() { return __builtin_amdgcn_s_memrealtime(); }
 
 __device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
     LibRec r;
@@ -897,6 +904,10 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     const int X1 = X0 + LIB_RTW - 1, Y1 = Y0 + LIB_RTH - 1;
     const int bt = (row / (TILE / LIB_RTH)) * fp.tiles_x + col;
     __syncthreads();   // the previous tile's key resets are done
+    const bool tlon = fb.timeline != nullptr && tid == 0;
+    const uint64_t t_tile = tlon ? tl_now() : 0ull;
+    uint64_t t_gather = 0ull;
+    const uint32_t chunk0 = chunk;
 
     uint32_t n_bin = 0, n_spill = 0, n_items;
     if (fp.scan_mode) {
@@ -914,6 +925,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         __syncthreads();
         if (tid == 0) sh.nc = 0;
         __syncthreads();
+        const uint64_t t_g0 = tlon ? tl_now() : 0ull;
         uint32_t ids[LIB_CAND / 256];
         uint2 bx[LIB_CAND / 256];
 #pragma unroll
@@ -946,6 +958,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         }
         __syncthreads();
         const uint32_t nc = sh.nc;
+        if (tlon) { t_gather += tl_now() - t_g0; sh.tl[LTL_NCAND] += nc; }
         for (uint32_t c = 0; c < nc; c += LIB_CHUNK) {
             const int m = (int)min((uint32_t)LIB_CHUNK, nc - c);
             if (c > 0) __syncthreads();
@@ -983,13 +996,16 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 const uint32_t ordmax = sh.ordmax[chunk & 1u];
                 if (tid == 0) sh.ordmax[(chunk + 1u) & 1u] = 0u;   // next chunk's max starts here
                 int area = 0, bx0 = 0, by0 = 0, bw = 1;
+                uint32_t zord = 0u;
                 if (tid < m) {
                     const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[tid * 4])[3];   // iw2 seq bx by
                     const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
                     const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
                     bool live = x0 <= x1 && y0 <= y1;
-                    if (live && hiz && ordmax != 0xffffffffu)
-                        live = lib_zmin_ord<SHADOW>(fp, lib_rec_from(&sh.rec[tid * 4])) <= ordmax;
+                    if (live && hiz) {
+                        zord = lib_zmin_ord<SHADOW>(fp, lib_rec_from(&sh.rec[tid * 4]));
+                        live = zord <= ordmax;   // ordmax 0xffffffff (an empty pixel): never culled
+                    }
                     if (live) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
                 }
                 const uint64_t alive = __ballot(area > 0);
@@ -1013,11 +1029,13 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                     const int start = (int)pbase + incl - area;
                     sh.pinfo[ci] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16),
                                               (uint32_t)bw | ((uint32_t)tid << 16), (65536u + (uint32_t)bw - 1u) / (uint32_t)bw);
+                    sh.zord[ci] = zord;
                     atomicOr(&sh.bits[start >> 6], 1ull << (start & 63));
                     for (int wd = (start + 63) >> 6; wd * 64 < start + area; ++wd) sh.wown[wd] = (uint8_t)ci;
                 }
                 __syncthreads();
                 const int total = (int)ptot;
+                if (tlon) sh.tl[LTL_NPAIRS] += ptot;
                 for (int k0 = 64 * wave; k0 < total; k0 += 256) {
                     const int k = k0 + lane;
                     if (k < total) {
@@ -1028,10 +1046,14 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                         const int local = k - (int)pi.x, ow = (int)(pi.z & 0xffffu);
                         const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * ow;
                         const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
+                        const int kp = (py - Y0) * LIB_RTW + (px - X0);
+                        // per-pixel hierarchical z: the pixel's current key already beats the
+                        // primitive's depth bound (a stale, higher key only skips less)
+                        if (sh.zord[o] > reinterpret_cast<const uint32_t *>(sh.key)[2 * kp + 1]) continue;
                         const LibRec r = lib_rec_from(&sh.rec[(pi.z >> 16) * 4]);
                         float z01, u, v, w, idn;
                         if (lib_test<SHADOW>(fp, r, px, py, z01, u, v, w, idn))
-                            atomicMin(&sh.key[(py - Y0) * LIB_RTW + (px - X0)], lib_key(fp, z01, r.seq, SHADOW));
+                            atomicMin(&sh.key[kp], lib_key(fp, z01, r.seq, SHADOW));
                     }
                 }
                 (void)ntot;
@@ -1040,6 +1062,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         }
     }
     __syncthreads();
+    const uint64_t t_res = tlon ? tl_now() : 0ull;
     const int px = X0 + (tid & 31), py = Y0 + (tid >> 5);
     const unsigned long long key = sh.key[tid];
     sh.key[tid] = KEY_EMPTY;
@@ -1048,6 +1071,15 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
     if (tid == 0) fb.busy[rt] = 0u;
+    if (tlon) {
+        const uint64_t t_end = tl_now();
+        sh.tl[LTL_GATHER] += t_gather;
+        sh.tl[LTL_PAIRS] += (t_res - t_tile) - t_gather;
+        sh.tl[LTL_SHADE] += t_end - t_res;
+        sh.tl[LTL_NBUSY] += 1;
+        sh.tl[LTL_CHUNKS] += chunk - chunk0;
+        sh.tl[LTL_MAXTILE] = max(sh.tl[LTL_MAXTILE], t_end - t_tile);
+    }
 }
 
 template <bool SHADOW>
@@ -1068,6 +1100,7 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; sh.ordmax[0] = 0u; sh.ordmax[1] = 0u; }
     sh.key[tid] = KEY_EMPTY;
     uint32_t chunk = 0;   // staging passes so far (selects the ordmax slot)
+    if (fb.timeline && tid < LTL_STRIDE) sh.tl[tid] = tid == LTL_START ? tl_now() : 0ull;
     for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
         __syncthreads();
         if (tid == 0) sh.nbusy = 0;
@@ -1086,10 +1119,16 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
         __syncthreads();
         const int nb = (int)(sh.nbusy & 0xffffu), ne = (int)(sh.nbusy >> 16);
         for (int i = 0; i < nb; ++i) lib_raster_tile<SHADOW>(fp, fb, cnt, sh.busy[i], sh, chunk);
+        const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
         for (int i = 0; i < ne; ++i) lib_clear_tile<SHADOW>(fp, fb, sh.busy[255 - i]);
+        if (fb.timeline && tid == 0) { sh.tl[LTL_CLEAR] += tl_now() - t_c; sh.tl[LTL_NCLEAR] += (uint64_t)ne; }
     }
     __syncthreads();
     if (tid == 0) fb.rstat[blockIdx.x] = make_uint2(sh.cov, sh.maxbin);
+    if (fb.timeline && tid == 0) {
+        sh.tl[LTL_END] = tl_now();
+        for (int i = 0; i < LTL_STRIDE; ++i) fb.timeline[(size_t)blockIdx.x * LTL_STRIDE + i] = sh.tl[i];
+    }
 }
 
 }  // namespace shs_dev

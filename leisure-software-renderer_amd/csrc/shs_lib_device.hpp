@@ -121,6 +121,13 @@ struct LibBuffers {
     const float *shadow_map;         // sampled by the camera pass (sm_w * sm_h)
     const CullLight *lights;         // Forward+ program
     const uint32_t *tile_counts, *tile_indices;
+    uint64_t *timeline;              // SHS_OPT_TIMELINE (camera pass): LTL_STRIDE per raster workgroup
 };
+
+// Library raster timeline slots (s_memrealtime, 100 MHz ticks): per workgroup start, end, summed
+// phase ticks over its busy tiles (gather, stage + pairs, resolve + shade), clear ticks, counts.
+constexpr int LTL_STRIDE = 12;
+enum : int { LTL_START = 0, LTL_END, LTL_GATHER, LTL_PAIRS, LTL_SHADE, LTL_CLEAR, LTL_NBUSY, LTL_NCLEAR, LTL_CHUNKS,
+             LTL_NPAIRS, LTL_NCAND, LTL_MAXTILE };
 
 }  // namespace shs_dev

@@ -217,6 +217,18 @@ class Context:
     def set_timeline(self, enable: bool):
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_TIMELINE, 1 if enable else 0))
 
+    LIB_TIMELINE_FIELDS = ("start", "end", "gather", "pairs", "shade", "clear", "n_busy", "n_clear", "chunks",
+                           "n_pairs", "n_cand", "max_tile")
+
+    def lib_debug_timeline(self):
+        """Last camera pass's k_lib_raster workgroup timeline: uint64 [grid, 12] (LIB_TIMELINE_FIELDS;
+        times in 10-ns ticks)."""
+        n = ctypes.c_int64()
+        self._check(self._lib.shs_lib_debug_timeline(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        self._check(self._lib.shs_lib_debug_timeline(self._h, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)))
+        return out.reshape(-1, len(self.LIB_TIMELINE_FIELDS))
+
     def debug_timeline(self):
         """Last frame's workgroup timeline: (header dict, setup [n,2], raster [n,2]) in 10-ns ticks."""
         n = ctypes.c_int64()
