@@ -620,44 +620,79 @@ __device__ f3 fake_ibl(f3 N, f3 V, f3 base, float metallic, float roughness, flo
     return sc3(add3(diffuse_ibl, spec_ibl), s_clamp(ao, 0.0f, 1.0f));
 }
 
+// The CullingLightGPU fields the point-light program reads (64 B; staged in LDS per workgroup).
+struct PLight {
+    float4 pr;        // position_range
+    float4 ci;        // color_intensity
+    float4 sa;        // shape_attenuation
+    uint32_t model;   // type_shape_flags[3]: attenuation model
+};
+constexpr int LIB_LDS_LIGHTS = 256;                  // lights staged in LDS by the camera pass
+__shared__ float4 lib_lds_lights[LIB_LDS_LIGHTS * 4];  // per light: pr, ci, sa, (model bits, 0, 0, 0)
+
+__device__ __forceinline__ PLight plight_global(const CullLight &L) {
+    PLight p;
+    p.pr = *reinterpret_cast<const float4 *>(L.position_range);
+    p.ci = *reinterpret_cast<const float4 *>(L.color_intensity);
+    p.sa = *reinterpret_cast<const float4 *>(L.shape_attenuation);
+    p.model = L.type_shape_flags[3];
+    return p;
+}
+
+__device__ __forceinline__ PLight plight_lds(uint32_t i) {
+    PLight p;
+    p.pr = lib_lds_lights[4 * i];
+    p.ci = lib_lds_lights[4 * i + 1];
+    p.sa = lib_lds_lights[4 * i + 2];
+    p.model = __float_as_uint(lib_lds_lights[4 * i + 3].x);
+    return p;
+}
+
 // eval_distance_attenuation (lighting/light_runtime.hpp:182-210) on a CullingLightGPU
-__device__ __forceinline__ float distance_attenuation(const CullLight &L, float distance) {
-    const float range = s_max(L.position_range[3], 0.001f);
+__device__ __forceinline__ float distance_attenuation(const PLight &L, float distance) {
+    const float range = s_max(L.pr.w, 0.001f);
     if (distance >= range) return 0.0f;
     const float norm = s_clamp(1.0f - distance / range, 0.0f, 1.0f);
     float falloff = 0.0f;
-    const uint32_t model = L.type_shape_flags[3];
+    const uint32_t model = L.model;
     if (model == 0u) {
         falloff = norm;
     } else if (model == 1u) {
         falloff = (norm * norm) * (3.0f - 2.0f * norm);
     } else if (model == 2u) {
-        const float inv = 1.0f / s_max(distance * distance, L.shape_attenuation[2]);
+        const float inv = 1.0f / s_max(distance * distance, L.sa.z);
         falloff = s_min(1.0f, inv * (range * range)) * (norm * norm);
     }
-    falloff = powf(s_max(falloff, 0.0f), s_max(L.shape_attenuation[1], 0.001f));
-    if (L.shape_attenuation[3] > 0.0f && falloff < L.shape_attenuation[3]) return 0.0f;
+    const float fpow = s_max(L.sa.y, 0.001f);
+    falloff = fpow == 1.0f ? s_max(falloff, 0.0f) : powf(s_max(falloff, 0.0f), fpow);   // pow(x, 1) == x exactly
+    if (L.sa.w > 0.0f && falloff < L.sa.w) return 0.0f;
     return s_max(falloff, 0.0f);
 }
 
 // PointLightModel::sample + eval_local_light_brdf (light_runtime.hpp:212-237, 321-333), accumulated
 // as lit += base * diffuse + specular (exp-plumbing/hello_light_types_culling_sw.cpp:414).
-__device__ __forceinline__ void point_light(const CullLight &L, f3 world, f3 N, f3 V, f3 base, f3 &lit) {
-    const f3 tl = {L.position_range[0] - world.x, L.position_range[1] - world.y, L.position_range[2] - world.z};
-    const float dist = sqrtf(dot3(tl, tl));
-    if (dist <= 1e-4f || dist > L.position_range[3]) return;
+__device__ __forceinline__ void point_light(const PLight &L, f3 world, f3 N, f3 V, f3 base, f3 &lit) {
+    const f3 tl = {L.pr.x - world.x, L.pr.y - world.y, L.pr.z - world.z};
+    const float d2 = dot3(tl, tl);
+    // out of range without the square root: d2 > range^2 (1 + 2^-20) implies the correctly rounded
+    // sqrt(d2) > range (NaN / overflow fall through to the exact test)
+    if (d2 > (L.pr.w * L.pr.w) * (1.0f + 0x1p-20f)) return;
+    const float dist = sqrtf(d2);
+    if (dist <= 1e-4f || dist > L.pr.w) return;
     const f3 Ld = {tl.x / dist, tl.y / dist, tl.z / dist};
     const float ndotl = s_max(dot3(N, Ld), 0.0f);
     if (ndotl <= 0.0f) return;
     const float att = distance_attenuation(L, dist) * s_max(1.0f, 0.0f);
     if (att <= 0.0f) return;
-    const float ci = s_max(L.color_intensity[3], 0.0f);
-    const f3 rad = {(s_max(L.color_intensity[0], 0.0f) * ci) * att, (s_max(L.color_intensity[1], 0.0f) * ci) * att,
-                    (s_max(L.color_intensity[2], 0.0f) * ci) * att};
+    const float ci = s_max(L.ci.w, 0.0f);
+    const f3 rad = {(s_max(L.ci.x, 0.0f) * ci) * att, (s_max(L.ci.y, 0.0f) * ci) * att,
+                    (s_max(L.ci.z, 0.0f) * ci) * att};
     f3 h = add3(Ld, V);
     const float len2 = dot3(h, h);
     h = len2 <= 1e-10f ? Ld : sc3(h, 1.0f / sqrtf(len2));                     // normalize_or(L + V, L)
-    const float spec = 0.30f * powf(s_max(dot3(N, h), 0.0f), 36.0f);
+    // pow(x, 36) by squaring (x^32 * x^4, <= 6 ulp): well inside the shaded-float tolerance
+    const float x1 = s_max(dot3(N, h), 0.0f), x2 = x1 * x1, x4 = x2 * x2, x8 = x4 * x4, x16 = x8 * x8, x32 = x16 * x16;
+    const float spec = 0.30f * (x32 * x4);
     lit = add3(lit, add3(mul3(base, sc3(rad, ndotl)), sc3(rad, spec)));
 }
 
@@ -685,13 +720,18 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
         list = ((uint32_t)zi * fp.lt_ty + ty) * fp.lt_tx + tx;
     }
     const uint32_t count = fp.lt_mode == 0u ? maxp : min(fb.tile_counts[list], maxp);
+    const bool lds = fp.n_lights <= (uint32_t)LIB_LDS_LIGHTS;   // k_lib_raster staged them
     if (count >= maxp) {
-        for (uint32_t i = 0; i < fp.n_lights; ++i) point_light(fb.lights[i], world, N, V, base, lit);
+        for (uint32_t i = 0; i < fp.n_lights; ++i)
+            point_light(lds ? plight_lds(i) : plight_global(fb.lights[i]), world, N, V, base, lit);
     } else {
+        // the next index is loaded while the current light is evaluated
         const uint32_t *ids = fb.tile_indices + (size_t)list * maxp;
+        uint32_t next = count > 0 ? ids[0] : 0u;
         for (uint32_t i = 0; i < count; ++i) {
-            const uint32_t idx = ids[i];
-            if (idx < fp.n_lights) point_light(fb.lights[idx], world, N, V, base, lit);
+            const uint32_t idx = next;
+            if (i + 1 < count) next = ids[i + 1];
+            if (idx < fp.n_lights) point_light(lds ? plight_lds(idx) : plight_global(fb.lights[idx]), world, N, V, base, lit);
         }
     }
     return f3{g_clamp(lit.x, 0.0f, 1.0f), g_clamp(lit.y, 0.0f, 1.0f), g_clamp(lit.z, 0.0f, 1.0f)};
@@ -1099,6 +1139,15 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
     const int G = (int)gridDim.x;
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; sh.ordmax[0] = 0u; sh.ordmax[1] = 0u; }
     sh.key[tid] = KEY_EMPTY;
+    if (!SHADOW && fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights (read after the tile syncs)
+        for (int i = tid; i < fp.n_lights; i += 256) {
+            const PLight p = plight_global(fb.lights[i]);
+            lib_lds_lights[4 * i] = p.pr;
+            lib_lds_lights[4 * i + 1] = p.ci;
+            lib_lds_lights[4 * i + 2] = p.sa;
+            lib_lds_lights[4 * i + 3] = make_float4(__uint_as_float(p.model), 0.0f, 0.0f, 0.0f);
+        }
+    }
     uint32_t chunk = 0;   // staging passes so far (selects the ordmax slot)
     if (fb.timeline && tid < LTL_STRIDE) sh.tl[tid] = tid == LTL_START ? tl_now() : 0ull;
     for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
