@@ -48,7 +48,7 @@ void release_work(Work &w) {
     for (auto &ev : w.ring_ev)
         for (auto &e : ev)
             if (e) { (void)hipEventDestroy(e); e = nullptr; }
-    release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase);
+    release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase); release(w.zord);
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
     release(w.spill); release(w.blk_stat); release(w.rstat);
     for (int i = 0; i < 2; ++i) {
@@ -148,7 +148,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     const int n_tris = (int)total;
     if (w.extra_cap == 0) w.extra_cap = (uint32_t)std::max(4096, n_tris / 4);
     const size_t n_slots = (size_t)std::max(n_tris, 1) + (shadow ? 0 : w.extra_cap);
-    if (ensure(ctx, w.recs, n_slots) || ensure(ctx, w.boxes, n_slots)) return SHS_ERR_HIP;
+    if (ensure(ctx, w.recs, n_slots) || ensure(ctx, w.boxes, n_slots) || ensure(ctx, w.zord, n_slots)) return SHS_ERR_HIP;
     if (!shadow && (ensure(ctx, w.shade, n_slots) || ensure(ctx, w.xbase, (size_t)std::max(n_tris, 1)))) return SHS_ERR_HIP;
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count;
     bool reset = gkey != w.geom_key;
@@ -195,7 +195,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
 
     LibBuffers fb;
     std::memset(&fb, 0, sizeof fb);
-    fb.draws = w.draws.p; fb.recs = w.recs.p; fb.shade = w.shade.p; fb.boxes = w.boxes.p; fb.xbase = w.xbase.p;
+    fb.draws = w.draws.p; fb.recs = w.recs.p; fb.shade = w.shade.p; fb.boxes = w.boxes.p; fb.xbase = w.xbase.p; fb.zord = w.zord.p;
     fb.tile_count = w.tile_count.p; fb.bins = w.bins.p; fb.spill = w.spill.p; fb.counters = w.counters.p;
     fb.busy = w.busy.p; fb.blk_stat = w.blk_stat.p; fb.rstat = w.rstat.p;
     if (shadow) {

@@ -103,7 +103,7 @@ struct shs_ctx {
         DevBuf<shs_dev::LibRec> recs;
         DevBuf<shs_dev::LibShade> shade;
         DevBuf<uint2> boxes;
-        DevBuf<uint32_t> xbase, tile_count, bins, counters, busy;
+        DevBuf<uint32_t> xbase, zord, tile_count, bins, counters, busy;
         DevBuf<uint2> spill, blk_stat, rstat;
         shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots
         size_t h_cap = 0;

@@ -64,6 +64,37 @@ __device__ __forceinline__ bool lib_owned(const LibFrameParams &fp, int bx, int 
     return ((by * fp.tiles_x + bx) % fp.count) == fp.rank;
 }
 
+// Orderable key bits (z_key's high word) of a conservative lower bound of the depth lib_test can
+// produce anywhere on the primitive.  The camera pass's 1/w depth is a weighted mean of the corners'
+// clip z (weights bc_k / w_k >= 0) or, linear, 1 / sum(bc_k / w_k) with sum(bc) = 1 +- 2 ulp -- both
+// bounded below by the corner minimum; the shadow pass's affine NDC z likewise.  The margin (1e-5
+// of the magnitudes, ~170 ulp) covers every rounding on the way.  Non-finite inputs never cull (0).
+template <bool SHADOW>
+__device__ __forceinline__ uint32_t lib_zmin_ord(const LibFrameParams &fp, const LibRec &r) {
+    float z01;
+    if (SHADOW) {
+        if (!(isfinite(r.z0) && isfinite(r.z1) && isfinite(r.z2))) return 0u;
+        const float lo = fminf(fminf(r.z0, r.z1), r.z2);
+        const float mag = fmaxf(fmaxf(fabsf(r.z0), fabsf(r.z1)), fabsf(r.z2));
+        z01 = s_clamp((lo - 1e-5f * (1.0f + mag)) * 0.5f + 0.5f, 0.0f, 1.0f);
+    } else {
+        if (!(r.iw0 > 0.0f && r.iw1 > 0.0f && r.iw2 > 0.0f && isfinite(r.iw0) && isfinite(r.iw1) && isfinite(r.iw2)))
+            return 0u;
+        if (fp.flags & LF_LINZ) {
+            const float lo = fminf(fminf(1.0f / r.iw0, 1.0f / r.iw1), 1.0f / r.iw2);
+            z01 = g_clamp((lo * (1.0f - 1e-5f) - fp.zn) / fp.zspan, 0.0f, 1.0f);
+        } else {
+            const float c0 = r.z0 / r.iw0, c1 = r.z1 / r.iw1, c2 = r.z2 / r.iw2;
+            if (!(isfinite(c0) && isfinite(c1) && isfinite(c2))) return 0u;
+            const float lo = fminf(fminf(c0, c1), c2);
+            const float mag = fmaxf(fmaxf(fabsf(c0), fabsf(c1)), fabsf(c2));
+            z01 = g_clamp((lo - 1e-5f * (1.0f + mag)) * 0.5f + 0.5f, 0.0f, 1.0f);
+        }
+    }
+    if (!isfinite(z01)) return 0u;
+    return (uint32_t)(z_key(z01, 0u) >> 32);
+}
+
 // ---- k_lib_setup ------------------------------------------------------------------------------
 
 // A clip-space vertex with the varyings the builtin VS sets (make_default_vertex_out,
@@ -280,6 +311,7 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     r.seq = seq;
     r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
     fb.recs[slot] = r;
+    fb.zord[slot] = (fp.flags & LF_DEPTH) ? lib_zmin_ord<false>(fp, r) : 0u;
     LibShade s;
     const float iw[3] = {iw0, iw1, iw2};
 #pragma unroll
@@ -429,6 +461,7 @@ __device__ __forceinline__ void setup_shadow_tri(const LibFrameParams &fp, const
     r.seq = (uint32_t)tri * 16u;
     r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
     fb.recs[tri] = r;
+    fb.zord[tri] = lib_zmin_ord<true>(fp, r);
     store_box(fb, (uint32_t)tri, x0, x1, y0, y1);
     lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri, ss, pend);
 }
@@ -812,11 +845,16 @@ struct LibShared {
     unsigned long long key[LIB_RTH * LIB_RTW];
     unsigned long long bits[LIB_PAIR_WORDS]; // bit k: a surviving candidate's pairs start at pair k (4 KB)
     uint4 pinfo[LIB_CHUNK];               // per surviving candidate: first pair, x0 | y0 << 16, width | slot << 16, 2^16/width
-    uint32_t zord[LIB_CHUNK];             // per surviving candidate: lib_zmin_ord (0: never skipped)
-    uint32_t cand[LIB_CAND];
+    uint32_t zord[LIB_CHUNK];             // per staged candidate: its depth bound (0: never skipped)
+    uint2 lbox[LIB_CAND];                 // the tile's candidate list, front to back: boxes,
+    uint32_t lid[LIB_CAND];               //   slots
+    uint32_t lkey[LIB_CAND];              //   and depth bounds (lib_zmin_ord; 0 without a depth test)
+    uint32_t sel[LIB_CHUNK];              // list positions staged by the current pass
+    uint32_t hist[256];                   // depth buckets: counts, then first positions
+    uint32_t zlo, zhi;
     int busy[256];
     uint32_t wtot[4][2];                  // per wave: surviving candidates, pairs
-    uint32_t ordmax[2];                   // tile's max per-pixel key z (orderable bits), by chunk parity
+    uint32_t colmax[2][LIB_RTW];          // per pixel column: max key z (orderable bits) over its rows, by chunk parity
     uint32_t nc, nbusy, cov, maxbin, npairs;
     uint64_t tl[LTL_STRIDE];              // SHS_OPT_TIMELINE accumulators (thread 0)
     uint8_t wown[LIB_PAIR_WORDS];         // surviving candidate owning each bitmap word's first pair
@@ -903,37 +941,6 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
     }
 }
 
-// Orderable key bits (z_key's high word) of a conservative lower bound of the depth lib_test can
-// produce anywhere on the primitive.  The camera pass's 1/w depth is a weighted mean of the corners'
-// clip z (weights bc_k / w_k >= 0) or, linear, 1 / sum(bc_k / w_k) with sum(bc) = 1 +- 2 ulp -- both
-// bounded below by the corner minimum; the shadow pass's affine NDC z likewise.  The margin (1e-5
-// of the magnitudes, ~170 ulp) covers every rounding on the way.  Non-finite inputs never cull (0).
-template <bool SHADOW>
-__device__ __forceinline__ uint32_t lib_zmin_ord(const LibFrameParams &fp, const LibRec &r) {
-    float z01;
-    if (SHADOW) {
-        if (!(isfinite(r.z0) && isfinite(r.z1) && isfinite(r.z2))) return 0u;
-        const float lo = fminf(fminf(r.z0, r.z1), r.z2);
-        const float mag = fmaxf(fmaxf(fabsf(r.z0), fabsf(r.z1)), fabsf(r.z2));
-        z01 = s_clamp((lo - 1e-5f * (1.0f + mag)) * 0.5f + 0.5f, 0.0f, 1.0f);
-    } else {
-        if (!(r.iw0 > 0.0f && r.iw1 > 0.0f && r.iw2 > 0.0f && isfinite(r.iw0) && isfinite(r.iw1) && isfinite(r.iw2)))
-            return 0u;
-        if (fp.flags & LF_LINZ) {
-            const float lo = fminf(fminf(1.0f / r.iw0, 1.0f / r.iw1), 1.0f / r.iw2);
-            z01 = g_clamp((lo * (1.0f - 1e-5f) - fp.zn) / fp.zspan, 0.0f, 1.0f);
-        } else {
-            const float c0 = r.z0 / r.iw0, c1 = r.z1 / r.iw1, c2 = r.z2 / r.iw2;
-            if (!(isfinite(c0) && isfinite(c1) && isfinite(c2))) return 0u;
-            const float lo = fminf(fminf(c0, c1), c2);
-            const float mag = fmaxf(fmaxf(fabsf(c0), fabsf(c1)), fabsf(c2));
-            z01 = g_clamp((lo - 1e-5f * (1.0f + mag)) * 0.5f + 0.5f, 0.0f, 1.0f);
-        }
-    }
-    if (!isfinite(z01)) return 0u;
-    return (uint32_t)(z_key(z01, 0u) >> 32);
-}
-
 template <bool SHADOW>
 __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared &sh,
                                 uint32_t &chunk) {
@@ -963,13 +970,18 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
 
     for (uint32_t base = 0; base < n_items; base += LIB_CAND) {
         __syncthreads();
-        if (tid == 0) sh.nc = 0;
+        if (tid == 0) { sh.nc = 0; sh.zlo = 0xffffffffu; sh.zhi = 0u; }
+        sh.hist[tid] = 0u;
         __syncthreads();
         const uint64_t t_g0 = tlon ? tl_now() : 0ull;
-        uint32_t ids[LIB_CAND / 256];
-        uint2 bx[LIB_CAND / 256];
+        // (1) gather up to LIB_CAND candidates (bin list or every primitive), their boxes and depth
+        //     bounds in one round trip; a candidate's box overlaps the tile
+        constexpr int NG = LIB_CAND / 256;
+        uint32_t ids[NG], zk[NG];
+        uint2 bx[NG];
+        bool hit[NG];
 #pragma unroll
-        for (int k = 0; k < LIB_CAND / 256; ++k) {
+        for (int k = 0; k < NG; ++k) {
             const uint32_t item = base + tid + 256u * k;
             uint32_t id = 0xffffffffu;
             if (item < n_items) {
@@ -985,120 +997,202 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
             ids[k] = id;
         }
 #pragma unroll
-        for (int k = 0; k < LIB_CAND / 256; ++k) bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
-#pragma unroll
-        for (int k = 0; k < LIB_CAND / 256; ++k) {
-            const int gx0 = lo16(bx[k].x), gx1 = hi16(bx[k].x), gy0 = lo16(bx[k].y), gy1 = hi16(bx[k].y);
-            const bool hit = ids[k] != 0xffffffffu && gx0 <= gx1 && gy0 <= gy1 && gx1 >= X0 && gx0 <= X1 && gy1 >= Y0 && gy0 <= Y1;
-            const uint64_t m = __ballot(hit);
-            uint32_t basew = 0;
-            if (lane == 0 && m) basew = atomicAdd(&sh.nc, (uint32_t)__popcll(m));
-            basew = __shfl(basew, 0);
-            if (hit) sh.cand[basew + lanes_below(m)] = ids[k];
+        for (int k = 0; k < NG; ++k) {
+            bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
+            zk[k] = hiz && ids[k] != 0xffffffffu ? fb.zord[ids[k]] : 0u;
         }
+        uint32_t zlo = 0xffffffffu, zhi = 0u, nhit = 0u;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const int gx0 = lo16(bx[k].x), gx1 = hi16(bx[k].x), gy0 = lo16(bx[k].y), gy1 = hi16(bx[k].y);
+            hit[k] = ids[k] != 0xffffffffu && gx0 <= gx1 && gy0 <= gy1 && gx1 >= X0 && gx0 <= X1 && gy1 >= Y0 && gy0 <= Y1;
+            if (hit[k]) { zlo = min(zlo, zk[k]); zhi = max(zhi, zk[k]); }
+            nhit += (uint32_t)__popcll(__ballot(hit[k]));
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            zlo = min(zlo, (uint32_t)__shfl_xor((int)zlo, off));
+            zhi = max(zhi, (uint32_t)__shfl_xor((int)zhi, off));
+        }
+        if (lane == 0 && nhit) { atomicAdd(&sh.nc, nhit); atomicMin(&sh.zlo, zlo); atomicMax(&sh.zhi, zhi); }
         __syncthreads();
         const uint32_t nc = sh.nc;
-        if (tlon) { t_gather += tl_now() - t_g0; sh.tl[LTL_NCAND] += nc; }
-        for (uint32_t c = 0; c < nc; c += LIB_CHUNK) {
-            const int m = (int)min((uint32_t)LIB_CHUNK, nc - c);
-            if (c > 0) __syncthreads();
-            if (hiz) {   // the tile's largest per-pixel key z so far (all earlier pairs are resolved)
-                uint32_t o = (uint32_t)(sh.key[tid] >> 32);
+        // (2) the list, front to back: a 256-bucket counting sort by depth bound.  bucket(z) is
+        //     monotone in z, so the entries from position p on lie in buckets >= bucket(lkey[p]).
+        //     Order inside a tile is otherwise free -- the resolve is by (z, submission index) keys.
+        const uint32_t s_lo = sh.zlo, s_span = sh.zhi - sh.zlo;
+        const float s_scale = (hiz && s_span) ? 255.0f / (float)s_span : 0.0f;
+        auto bucket = [&](uint32_t z) { return min(255u, (uint32_t)((float)(z - s_lo) * s_scale)); };
+        uint32_t bk[NG], rk[NG];
 #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) o = max(o, (uint32_t)__shfl_xor((int)o, off));
-                if (lane == 0) atomicMax(&sh.ordmax[chunk & 1u], o);
+        for (int k = 0; k < NG; ++k) {
+            bk[k] = 0u; rk[k] = 0u;
+            if (hit[k]) { bk[k] = bucket(zk[k]); rk[k] = atomicAdd(&sh.hist[bk[k]], 1u); }
+        }
+        __syncthreads();
+        {
+            const uint32_t cntb = sh.hist[tid];
+            uint32_t incl = cntb;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t vv = (uint32_t)__shfl_up((int)incl, o);
+                if (lane >= o) incl += vv;
             }
-            for (int i = tid; i < m * (LIB_RTW * LIB_RTH / 64); i += 256) sh.bits[i] = 0ull;
-            {   // stage records: consecutive lanes load consecutive float4s of one record
+            if (lane == 63) sh.wtot[wave][0] = incl;
+            __syncthreads();
+            uint32_t wbase = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < 4; ++w2) wbase += w2 < wave ? sh.wtot[w2][0] : 0u;
+            sh.hist[tid] = wbase + incl - cntb;   // first position of bucket tid
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NG; ++k)
+            if (hit[k]) {
+                const uint32_t pos = sh.hist[bk[k]] + rk[k];
+                sh.lid[pos] = ids[k];
+                sh.lkey[pos] = zk[k];
+                sh.lbox[pos] = bx[k];
+            }
+        __syncthreads();
+        if (tlon) { t_gather += tl_now() - t_g0; sh.tl[LTL_NCAND] += nc; }
+
+        // (3) staging passes.  Each selects, in list order, the entries that can still win a pixel
+        //     -- depth bound <= the largest current key z over the pixel columns their box covers
+        //     (hierarchical z; 0xffffffff = an uncovered pixel) -- stages up to LIB_CHUNK of them and
+        //     expands their (primitive, pixel) pairs.  Once the whole tile's largest key z sorts into
+        //     a lower bucket than the next entry, the rest of the list is skipped.
+        uint32_t p = 0;
+        while (p < nc) {
+            if (p > 0) __syncthreads();   // the previous pass's pairs are resolved
+            if (hiz) {   // per pixel column, the largest key z so far
+                uint32_t o = (uint32_t)(sh.key[tid] >> 32);
+                o = max(o, (uint32_t)__shfl_xor((int)o, 32));   // a wave holds two rows of the column
+                if (lane < LIB_RTW) atomicMax(&sh.colmax[chunk & 1u][lane], o);
+            }
+            __syncthreads();
+            const uint32_t *colmax = sh.colmax[chunk & 1u];
+            uint32_t ordmax = colmax[lane & (LIB_RTW - 1)];   // the whole tile's max (every wave alike)
+#pragma unroll
+            for (int off = LIB_RTW / 2; off > 0; off >>= 1) ordmax = max(ordmax, (uint32_t)__shfl_xor((int)ordmax, off));
+            if (tid < LIB_RTW) sh.colmax[(chunk + 1u) & 1u][tid] = 0u;   // next pass's maxima start here
+            ++chunk;
+            auto done_after = [&](uint32_t q) {   // nothing from list position q on can win (uniform)
+                return hiz && ordmax != 0xffffffffu && (ordmax < s_lo || bucket(ordmax) < bucket(sh.lkey[q]));
+            };
+            if (done_after(p)) break;
+            // select the next survivors (at most LIB_CHUNK), skipping rejected runs
+            uint32_t m = 0;
+            while (p < nc) {
+                const uint32_t q = p + (uint32_t)tid;
+                bool alive = false;
+                if (tid < LIB_CHUNK && q < nc) {
+                    alive = true;
+                    if (hiz) {
+                        const uint2 b = sh.lbox[q];
+                        const int x0 = max(lo16(b.x), X0) - X0, x1 = min(hi16(b.x), X1) - X0;
+                        uint32_t cm = 0u;
+                        for (int x = x0; x <= x1; ++x) cm = max(cm, colmax[x]);
+                        alive = sh.lkey[q] <= cm;
+                    }
+                }
+                const uint64_t am = __ballot(alive);
+                if (lane == 0) sh.wtot[wave][0] = (uint32_t)__popcll(am);
+                __syncthreads();
+                uint32_t wb = 0;
+#pragma unroll
+                for (int w2 = 0; w2 < 4; ++w2) {
+                    const uint32_t c2 = sh.wtot[w2][0];
+                    wb += w2 < wave ? c2 : 0u;
+                    m += c2;
+                }
+                if (alive) sh.sel[wb + lanes_below(am)] = q;
+                p += LIB_CHUNK;
+                __syncthreads();   // sel complete; wtot reusable
+                if (m > 0 || p >= nc || done_after(p)) break;
+            }
+            if (m == 0) break;
+            // stage the survivors' records (consecutive lanes: consecutive float4s of one record)
+            for (int i = tid; i < (int)m * (LIB_RTW * LIB_RTH / 64); i += 256) sh.bits[i] = 0ull;
+            {
                 constexpr int NQ = LIB_CHUNK * 4 / 256;
-                float4 q[NQ];
+                float4 q4[NQ];
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) {
                     const int f = tid + 256 * k;
                     const int ci = f >> 2;
-                    q[k] = f < 4 * m ? reinterpret_cast<const float4 *>(&fb.recs[sh.cand[c + min(ci, m - 1)]])[f & 3]
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                    q4[k] = f < 4 * (int)m ? reinterpret_cast<const float4 *>(&fb.recs[sh.lid[sh.sel[min(ci, (int)m - 1)]]])[f & 3]
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) {
                     const int f = tid + 256 * k;
-                    if (f < 4 * m) sh.rec[f] = q[k];
+                    if (f < 4 * (int)m) sh.rec[f] = q4[k];
                 }
             }
             __syncthreads();
-            // Candidates that cannot win any pixel are dropped before pair expansion (hierarchical z):
-            // a conservative lower bound of the primitive's depth over its whole extent (lib_zmin_ord)
-            // above the tile's largest current per-pixel key z.  The survivors' clipped boxes are laid
-            // end to end (block prefix of the areas) and every (primitive, pixel) pair is dealt to one
-            // lane, 64-pair windows round-robin over the waves (start bitmap + word owners, as in
-            // shs_legacy.hip).
+            // Pair tasks: the staged boxes laid end to end (block prefix of the areas); every
+            // (primitive, pixel) pair is dealt to one lane, 64-pair windows round-robin over the
+            // waves (start bitmap + word owners, as in shs_legacy.hip).
             {
-                const uint32_t ordmax = sh.ordmax[chunk & 1u];
-                if (tid == 0) sh.ordmax[(chunk + 1u) & 1u] = 0u;   // next chunk's max starts here
                 int area = 0, bx0 = 0, by0 = 0, bw = 1;
                 uint32_t zord = 0u;
-                if (tid < m) {
-                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[tid * 4])[3];   // iw2 seq bx by
-                    const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
-                    const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
-                    bool live = x0 <= x1 && y0 <= y1;
-                    if (live && hiz) {
-                        zord = lib_zmin_ord<SHADOW>(fp, lib_rec_from(&sh.rec[tid * 4]));
-                        live = zord <= ordmax;   // ordmax 0xffffffff (an empty pixel): never culled
-                    }
-                    if (live) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
+                if (tid < (int)m) {
+                    const uint32_t q = sh.sel[tid];
+                    const uint2 b = sh.lbox[q];
+                    const int x0 = max(lo16(b.x), X0), x1 = min(hi16(b.x), X1);
+                    const int y0 = max(lo16(b.y), Y0), y1 = min(hi16(b.y), Y1);
+                    area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1;
+                    zord = sh.lkey[q];
                 }
-                const uint64_t alive = __ballot(area > 0);
                 int incl = area;
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) {
                     const int vv = __shfl_up(incl, o);
                     if (lane >= o) incl += vv;
                 }
-                if (lane == 63) { sh.wtot[wave][0] = (uint32_t)__popcll(alive); sh.wtot[wave][1] = (uint32_t)incl; }
+                if (lane == 63) sh.wtot[wave][1] = (uint32_t)incl;
                 __syncthreads();
-                uint32_t cbase = 0, pbase = 0, ntot = 0, ptot = 0;
+                uint32_t pbase = 0, ptot = 0;
 #pragma unroll
                 for (int w2 = 0; w2 < 4; ++w2) {
-                    const uint32_t c2 = sh.wtot[w2][0], p2 = sh.wtot[w2][1];
-                    if (w2 < wave) { cbase += c2; pbase += p2; }
-                    ntot += c2; ptot += p2;
+                    const uint32_t p2 = sh.wtot[w2][1];
+                    if (w2 < wave) pbase += p2;
+                    ptot += p2;
                 }
                 if (area > 0) {
-                    const int ci = (int)cbase + lanes_below(alive);
                     const int start = (int)pbase + incl - area;
-                    sh.pinfo[ci] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16),
-                                              (uint32_t)bw | ((uint32_t)tid << 16), (65536u + (uint32_t)bw - 1u) / (uint32_t)bw);
-                    sh.zord[ci] = zord;
+                    sh.pinfo[tid] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16),
+                                               (uint32_t)bw | ((uint32_t)tid << 16), (65536u + (uint32_t)bw - 1u) / (uint32_t)bw);
+                    sh.zord[tid] = zord;
                     atomicOr(&sh.bits[start >> 6], 1ull << (start & 63));
-                    for (int wd = (start + 63) >> 6; wd * 64 < start + area; ++wd) sh.wown[wd] = (uint8_t)ci;
+                    for (int wd = (start + 63) >> 6; wd * 64 < start + area; ++wd) sh.wown[wd] = (uint8_t)tid;
                 }
                 __syncthreads();
                 const int total = (int)ptot;
                 if (tlon) sh.tl[LTL_NPAIRS] += ptot;
-                for (int k0 = 64 * wave; k0 < total; k0 += 256) {
+                const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
+                // one pair: its owner (word's first owner + starts up to it), pixel, then the test
+                auto pair = [&](int k0) {
                     const int k = k0 + lane;
-                    if (k < total) {
-                        const unsigned long long wb = sh.bits[k0 >> 6];
-                        const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
-                        const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
-                        const uint4 pi = sh.pinfo[o];
-                        const int local = k - (int)pi.x, ow = (int)(pi.z & 0xffffu);
-                        const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * ow;
-                        const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
-                        const int kp = (py - Y0) * LIB_RTW + (px - X0);
-                        // per-pixel hierarchical z: the pixel's current key already beats the
-                        // primitive's depth bound (a stale, higher key only skips less)
-                        if (sh.zord[o] > reinterpret_cast<const uint32_t *>(sh.key)[2 * kp + 1]) continue;
-                        const LibRec r = lib_rec_from(&sh.rec[(pi.z >> 16) * 4]);
-                        float z01, u, v, w, idn;
-                        if (lib_test<SHADOW>(fp, r, px, py, z01, u, v, w, idn))
-                            atomicMin(&sh.key[kp], lib_key(fp, z01, r.seq, SHADOW));
-                    }
-                }
-                (void)ntot;
+                    if (k >= total) return;
+                    const unsigned long long wb = sh.bits[k0 >> 6];
+                    const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
+                    const uint4 pi = sh.pinfo[o];
+                    const int local = k - (int)pi.x, ow = (int)(pi.z & 0xffffu);
+                    const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * ow;
+                    const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
+                    const int kp = (py - Y0) * LIB_RTW + (px - X0);
+                    // per-pixel hierarchical z: the pixel's current key already beats the
+                    // primitive's depth bound (a stale, higher key only skips less)
+                    if (sh.zord[o] > reinterpret_cast<const uint32_t *>(sh.key)[2 * kp + 1]) return;
+                    const LibRec r = lib_rec_from(&sh.rec[(pi.z >> 16) * 4]);
+                    float z01, u, v, w, idn;
+                    if (lib_test<SHADOW>(fp, r, px, py, z01, u, v, w, idn))
+                        atomicMin(&sh.key[kp], lib_key(fp, z01, r.seq, SHADOW));
+                };
+                for (int k0 = 64 * wave; k0 < total; k0 += 256) pair(k0);
             }
-            ++chunk;
         }
     }
     __syncthreads();
@@ -1137,7 +1231,8 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
     const int tid = threadIdx.x;
     const uint32_t *cnt = fb.counters + fp.parity * LC_N;
     const int G = (int)gridDim.x;
-    if (tid == 0) { sh.cov = 0; sh.maxbin = 0; sh.ordmax[0] = 0u; sh.ordmax[1] = 0u; }
+    if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
+    if (tid < 2 * LIB_RTW) sh.colmax[tid / LIB_RTW][tid % LIB_RTW] = 0u;
     sh.key[tid] = KEY_EMPTY;
     if (!SHADOW && fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights (read after the tile syncs)
         for (int i = tid; i < fp.n_lights; i += 256) {
@@ -1148,7 +1243,7 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
             lib_lds_lights[4 * i + 3] = make_float4(__uint_as_float(p.model), 0.0f, 0.0f, 0.0f);
         }
     }
-    uint32_t chunk = 0;   // staging passes so far (selects the ordmax slot)
+    uint32_t chunk = 0;   // staging passes so far (selects the colmax slot)
     if (fb.timeline && tid < LTL_STRIDE) sh.tl[tid] = tid == LTL_START ? tl_now() : 0ull;
     for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
         __syncthreads();

@@ -108,6 +108,7 @@ struct LibBuffers {
     LibRec *recs;                    // n_tris primaries (fan 0) then extra_cap extras (fans 1..6)
     LibShade *shade;
     uint2 *boxes;                    // per slot: packed pixel bbox, empty (0,-1) when not rasterised
+    uint32_t *zord;                  // per slot: orderable bits of a lower bound of its depth (front-to-back sort key)
     uint32_t *xbase;                 // per input triangle: slot of its fan triangle 1
     uint32_t *tile_count, *bins;
     uint2 *spill;
