@@ -606,6 +606,23 @@ __device__ __forceinline__ unsigned long long lib_key(const LibFrameParams &fp, 
     return (shadow || (fp.flags & LF_DEPTH)) ? z_key(z01, seq) : (unsigned long long)(0xffffffffu - seq);
 }
 
+// (2R+1)^2 PCF taps with every fetch issued before the first compare (one memory round trip).
+template <int R>
+__device__ __forceinline__ float pcf_fixed(const LibFrameParams &fp, const LibBuffers &fb, int cx, int cy, int step, float z_test) {
+    constexpr int N = 2 * R + 1;
+    float ref[N * N];
+#pragma unroll
+    for (int oy = -R; oy <= R; oy++) {
+        const size_t row = (size_t)s_clampi(cy + oy * step, 0, fp.sm_h - 1) * fp.sm_w;
+#pragma unroll
+        for (int ox = -R; ox <= R; ox++) ref[(oy + R) * N + ox + R] = fb.shadow_map[row + s_clampi(cx + ox * step, 0, fp.sm_w - 1)];
+    }
+    int lit = 0;
+#pragma unroll
+    for (int i = 0; i < N * N; ++i) lit += (z_test <= ref[i]) ? 1 : 0;
+    return (float)lit / (float)(N * N);
+}
+
 // shadow_visibility_dir (lighting/shadow_sample.hpp:65-104) with the FS's ShadowParams.
 __device__ float shadow_visibility(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 pos, float ndotl) {
     const f4 p = m4v(dr.light_vp, f4{pos.x, pos.y, pos.z, 1.0f});
@@ -621,6 +638,8 @@ __device__ float shadow_visibility(const LibFrameParams &fp, const LibBuffers &f
         return (z_test <= z_ref) ? 1.0f : 0.0f;
     }
     const int step = max(1, (int)roundf(dr.shp[3]));
+    if (rad == 1) return pcf_fixed<1>(fp, fb, cx, cy, step, z_test);
+    if (rad == 2) return pcf_fixed<2>(fp, fb, cx, cy, step, z_test);   // the reference default (5x5)
     int count = 0, lit = 0;
     for (int oy = -rad; oy <= rad; oy++) {
         const size_t row = (size_t)s_clampi(cy + oy * step, 0, fp.sm_h - 1) * fp.sm_w;
@@ -1014,9 +1033,27 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
             zlo = min(zlo, (uint32_t)__shfl_xor((int)zlo, off));
             zhi = max(zhi, (uint32_t)__shfl_xor((int)zhi, off));
         }
-        if (lane == 0 && nhit) { atomicAdd(&sh.nc, nhit); atomicMin(&sh.zlo, zlo); atomicMax(&sh.zhi, zhi); }
+        uint32_t basew = 0;   // this wave's first position in gather order
+        if (lane == 0 && nhit) { basew = atomicAdd(&sh.nc, nhit); atomicMin(&sh.zlo, zlo); atomicMax(&sh.zhi, zhi); }
+        basew = (uint32_t)__shfl((int)basew, 0);
         __syncthreads();
         const uint32_t nc = sh.nc;
+        // one staging pass holds every candidate (or painter's order): gather order, no sort
+        const bool sorted = hiz && nc > (uint32_t)LIB_CHUNK;
+        if (!sorted) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                const uint64_t hm = __ballot(hit[k]);
+                if (hit[k]) {
+                    const uint32_t pos = basew + run + lanes_below(hm);
+                    sh.lid[pos] = ids[k];
+                    sh.lkey[pos] = zk[k];
+                    sh.lbox[pos] = bx[k];
+                }
+                run += (uint32_t)__popcll(hm);
+            }
+        }
         // (2) the list, front to back: a 256-bucket counting sort by depth bound.  bucket(z) is
         //     monotone in z, so the entries from position p on lie in buckets >= bucket(lkey[p]).
         //     Order inside a tile is otherwise free -- the resolve is by (z, submission index) keys.
@@ -1027,10 +1064,10 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
             bk[k] = 0u; rk[k] = 0u;
-            if (hit[k]) { bk[k] = bucket(zk[k]); rk[k] = atomicAdd(&sh.hist[bk[k]], 1u); }
+            if (sorted && hit[k]) { bk[k] = bucket(zk[k]); rk[k] = atomicAdd(&sh.hist[bk[k]], 1u); }
         }
-        __syncthreads();
-        {
+        if (sorted) {
+            __syncthreads();
             const uint32_t cntb = sh.hist[tid];
             uint32_t incl = cntb;
 #pragma unroll
@@ -1044,16 +1081,16 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
 #pragma unroll
             for (int w2 = 0; w2 < 4; ++w2) wbase += w2 < wave ? sh.wtot[w2][0] : 0u;
             sh.hist[tid] = wbase + incl - cntb;   // first position of bucket tid
-        }
-        __syncthreads();
+            __syncthreads();
 #pragma unroll
-        for (int k = 0; k < NG; ++k)
-            if (hit[k]) {
-                const uint32_t pos = sh.hist[bk[k]] + rk[k];
-                sh.lid[pos] = ids[k];
-                sh.lkey[pos] = zk[k];
-                sh.lbox[pos] = bx[k];
-            }
+            for (int k = 0; k < NG; ++k)
+                if (hit[k]) {
+                    const uint32_t pos = sh.hist[bk[k]] + rk[k];
+                    sh.lid[pos] = ids[k];
+                    sh.lkey[pos] = zk[k];
+                    sh.lbox[pos] = bx[k];
+                }
+        }
         __syncthreads();
         if (tlon) { t_gather += tl_now() - t_g0; sh.tl[LTL_NCAND] += nc; }
 
@@ -1065,53 +1102,61 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         uint32_t p = 0;
         while (p < nc) {
             if (p > 0) __syncthreads();   // the previous pass's pairs are resolved
-            if (hiz) {   // per pixel column, the largest key z so far
-                uint32_t o = (uint32_t)(sh.key[tid] >> 32);
-                o = max(o, (uint32_t)__shfl_xor((int)o, 32));   // a wave holds two rows of the column
-                if (lane < LIB_RTW) atomicMax(&sh.colmax[chunk & 1u][lane], o);
-            }
-            __syncthreads();
-            const uint32_t *colmax = sh.colmax[chunk & 1u];
-            uint32_t ordmax = colmax[lane & (LIB_RTW - 1)];   // the whole tile's max (every wave alike)
-#pragma unroll
-            for (int off = LIB_RTW / 2; off > 0; off >>= 1) ordmax = max(ordmax, (uint32_t)__shfl_xor((int)ordmax, off));
-            if (tid < LIB_RTW) sh.colmax[(chunk + 1u) & 1u][tid] = 0u;   // next pass's maxima start here
-            ++chunk;
-            auto done_after = [&](uint32_t q) {   // nothing from list position q on can win (uniform)
-                return hiz && ordmax != 0xffffffffu && (ordmax < s_lo || bucket(ordmax) < bucket(sh.lkey[q]));
-            };
-            if (done_after(p)) break;
-            // select the next survivors (at most LIB_CHUNK), skipping rejected runs
             uint32_t m = 0;
-            while (p < nc) {
-                const uint32_t q = p + (uint32_t)tid;
-                bool alive = false;
-                if (tid < LIB_CHUNK && q < nc) {
-                    alive = true;
-                    if (hiz) {
-                        const uint2 b = sh.lbox[q];
-                        const int x0 = max(lo16(b.x), X0) - X0, x1 = min(hi16(b.x), X1) - X0;
-                        uint32_t cm = 0u;
-                        for (int x = x0; x <= x1; ++x) cm = max(cm, colmax[x]);
-                        alive = sh.lkey[q] <= cm;
-                    }
-                }
-                const uint64_t am = __ballot(alive);
-                if (lane == 0) sh.wtot[wave][0] = (uint32_t)__popcll(am);
+            if (!sorted) {   // list order, LIB_CHUNK at a time (one pass unless painter's order)
+                m = min((uint32_t)LIB_CHUNK, nc - p);
+                for (int i = tid; i < (int)m; i += 256) sh.sel[i] = p + (uint32_t)i;
+                p += m;
+                ++chunk;
                 __syncthreads();
-                uint32_t wb = 0;
-#pragma unroll
-                for (int w2 = 0; w2 < 4; ++w2) {
-                    const uint32_t c2 = sh.wtot[w2][0];
-                    wb += w2 < wave ? c2 : 0u;
-                    m += c2;
+            } else {
+                if (hiz) {   // per pixel column, the largest key z so far
+                    uint32_t o = (uint32_t)(sh.key[tid] >> 32);
+                    o = max(o, (uint32_t)__shfl_xor((int)o, 32));   // a wave holds two rows of the column
+                    if (lane < LIB_RTW) atomicMax(&sh.colmax[chunk & 1u][lane], o);
                 }
-                if (alive) sh.sel[wb + lanes_below(am)] = q;
-                p += LIB_CHUNK;
-                __syncthreads();   // sel complete; wtot reusable
-                if (m > 0 || p >= nc || done_after(p)) break;
+                __syncthreads();
+                const uint32_t *colmax = sh.colmax[chunk & 1u];
+                uint32_t ordmax = colmax[lane & (LIB_RTW - 1)];   // the whole tile's max (every wave alike)
+#pragma unroll
+                for (int off = LIB_RTW / 2; off > 0; off >>= 1) ordmax = max(ordmax, (uint32_t)__shfl_xor((int)ordmax, off));
+                if (tid < LIB_RTW) sh.colmax[(chunk + 1u) & 1u][tid] = 0u;   // next pass's maxima start here
+                ++chunk;
+                auto done_after = [&](uint32_t q) {   // nothing from list position q on can win (uniform)
+                    return hiz && ordmax != 0xffffffffu && (ordmax < s_lo || bucket(ordmax) < bucket(sh.lkey[q]));
+                };
+                if (done_after(p)) break;
+                // select the next survivors (at most LIB_CHUNK), skipping rejected runs
+                while (p < nc) {
+                    const uint32_t q = p + (uint32_t)tid;
+                    bool alive = false;
+                    if (tid < LIB_CHUNK && q < nc) {
+                        alive = true;
+                        if (hiz) {
+                            const uint2 b = sh.lbox[q];
+                            const int x0 = max(lo16(b.x), X0) - X0, x1 = min(hi16(b.x), X1) - X0;
+                            uint32_t cm = 0u;
+                            for (int x = x0; x <= x1; ++x) cm = max(cm, colmax[x]);
+                            alive = sh.lkey[q] <= cm;
+                        }
+                    }
+                    const uint64_t am = __ballot(alive);
+                    if (lane == 0) sh.wtot[wave][0] = (uint32_t)__popcll(am);
+                    __syncthreads();
+                    uint32_t wb = 0;
+#pragma unroll
+                    for (int w2 = 0; w2 < 4; ++w2) {
+                        const uint32_t c2 = sh.wtot[w2][0];
+                        wb += w2 < wave ? c2 : 0u;
+                        m += c2;
+                    }
+                    if (alive) sh.sel[wb + lanes_below(am)] = q;
+                    p += LIB_CHUNK;
+                    __syncthreads();   // sel complete; wtot reusable
+                    if (m > 0 || p >= nc || done_after(p)) break;
+                }
+                if (m == 0) break;
             }
-            if (m == 0) break;
             // stage the survivors' records (consecutive lanes: consecutive float4s of one record)
             for (int i = tid; i < (int)m * (LIB_RTW * LIB_RTH / 64); i += 256) sh.bits[i] = 0ull;
             {
@@ -1197,9 +1242,12 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     }
     __syncthreads();
     const uint64_t t_res = tlon ? tl_now() : 0ull;
-    const int px = X0 + (tid & 31), py = Y0 + (tid >> 5);
-    const unsigned long long key = sh.key[tid];
-    sh.key[tid] = KEY_EMPTY;
+    // resolve: a wave takes a 16x4 block (one 16-px light tile wide, so Forward+ lanes share a list;
+    // rows are still 256-B segments of the HDR target)
+    const int lx = 16 * (wave & 1) + (lane & 15), ly = 4 * (wave >> 1) + (lane >> 4);
+    const int px = X0 + lx, py = Y0 + ly;
+    const unsigned long long key = sh.key[ly * LIB_RTW + lx];
+    sh.key[ly * LIB_RTW + lx] = KEY_EMPTY;   // this thread's pixel only: clean for the next tile
     bool covered;
     lib_resolve<SHADOW>(fp, fb, key, px, py, covered);
     const uint64_t cm = __ballot(covered);
