@@ -161,6 +161,9 @@ int shs_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n
  * its busy tiles, clear ticks, busy tiles, cleared tiles, staging passes, pairs, candidates, longest
  * busy tile (s_memrealtime, 100 MHz).  out = NULL: *n_out = the count only. */
 int shs_lib_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out);
+/* The same for the last camera pass's k_lib_setup: 6 uint64 per workgroup -- start, after its
+ * triangles, after the deferred marks, end, large primitives, deferred union width x height. */
+int shs_lib_debug_setup_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out);
 
 /* Library/ABI version for integration checks; edge of the square GPU screen tile (shard unit). */
 int shs_abi_version(void);

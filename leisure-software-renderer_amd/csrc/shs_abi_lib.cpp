@@ -211,6 +211,10 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
             if (ensure(ctx, ctx->lib_timeline, n)) return SHS_ERR_HIP;
             HIP_TRY(ctx, hipMemsetAsync(ctx->lib_timeline.p, 0, n * sizeof(uint64_t), ctx->stream));
             fb.timeline = ctx->lib_timeline.p;
+            const size_t ns = (size_t)std::max(setup_blocks, 1) * shs_dev::STL_STRIDE;
+            if (ensure(ctx, ctx->lib_stimeline, ns)) return SHS_ERR_HIP;
+            HIP_TRY(ctx, hipMemsetAsync(ctx->lib_stimeline.p, 0, ns * sizeof(uint64_t), ctx->stream));
+            fb.stimeline = ctx->lib_stimeline.p;
         }
     }
     hipEvent_t *ev = nullptr;
@@ -307,7 +311,7 @@ void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_shadow);
     release(ctx->lib_hdr); release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
     release(ctx->lights); release(ctx->light_proj); release(ctx->depth_ranges);
-    release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline);
+    release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
 }
@@ -505,6 +509,22 @@ int shs_resolve_shadow_map(shs_ctx *ctx, float *depth) {
     int rc = lib_finish(ctx);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(depth, ctx->shadow_map.p, (size_t)ctx->shadow_w * ctx->shadow_h * sizeof(float), hipMemcpyDeviceToHost));
+    return SHS_OK;
+}
+
+int shs_lib_debug_setup_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out) {
+    if (!ctx || !n_out) return SHS_ERR_INVALID;
+    if (!ctx->want_timeline || !ctx->lib_stimeline.p || ctx->lib_cam.last_setup_blocks <= 0) {
+        ctx->err = "timeline not enabled or no camera pass yet";
+        return SHS_ERR_INVALID;
+    }
+    const int64_t n = (int64_t)ctx->lib_cam.last_setup_blocks * shs_dev::STL_STRIDE;
+    *n_out = n;
+    if (!out) return SHS_OK;
+    if (capacity < n) { ctx->err = "capacity too small"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(out, ctx->lib_stimeline.p, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return SHS_OK;
 }
 

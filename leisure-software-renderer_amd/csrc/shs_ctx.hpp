@@ -127,7 +127,8 @@ struct shs_ctx {
     };
     LibWork lib_cam, lib_shadow;
     int lib_resident[2] = {0, 0};         // resident k_lib_raster workgroups (camera, shadow)
-    DevBuf<uint64_t> lib_timeline;        // SHS_OPT_TIMELINE, camera pass
+    DevBuf<uint64_t> lib_timeline;        // SHS_OPT_TIMELINE, camera pass raster
+    DevBuf<uint64_t> lib_stimeline;       // SHS_OPT_TIMELINE, camera pass setup
     DevBuf<float4> lib_hdr;
     DevBuf<float> lib_depth;
     DevBuf<float2> lib_motion;

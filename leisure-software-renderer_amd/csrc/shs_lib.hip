@@ -95,6 +95,8 @@ __device__ __forceinline__ uint32_t lib_zmin_ord(const LibFrameParams &fp, const
     return (uint32_t)(z_key(z01, 0u) >> 32);
 }
 
+__device__ __forceinline__ uint64_t tl_now() { return __builtin_amdgcn_s_memrealtime(); }
+
 // ---- k_lib_setup ------------------------------------------------------------------------------
 
 // A clip-space vertex with the varyings the builtin VS sets (make_default_vertex_out,
@@ -106,16 +108,31 @@ struct LVert {
     float u, v;
 };
 
-__device__ __forceinline__ LVert vertex_out(const LibDrawGPU &dr, uint32_t id) {
-    const float *P = dr.pos + 3 * (size_t)id, *N = dr.nrm + 3 * (size_t)id, *U = dr.uv + 2 * (size_t)id;
+// The normal and UV varyings of a vertex (the half of make_default_vertex_out that only surviving
+// primitives need).
+__device__ __forceinline__ void vertex_attrs(const LibDrawGPU &dr, uint32_t id, LVert &o) {
+    const float *N = dr.nrm + 3 * (size_t)id, *U = dr.uv + 2 * (size_t)id;
+    const f3 n = normalize3(m3v(dr.nmat, f3{N[0], N[1], N[2]}));
+    o.nx = n.x; o.ny = n.y; o.nz = n.z;
+    o.u = U[0]; o.v = U[1];
+}
+
+// Clip and world position (the varyings are left 0 until vertex_attrs).
+__device__ __forceinline__ LVert vertex_pos(const LibDrawGPU &dr, uint32_t id) {
+    const float *P = dr.pos + 3 * (size_t)id;
     LVert o;
     const f4 wp = m4v(dr.model, f4{P[0], P[1], P[2], 1.0f});
     const f4 c = m4v(dr.viewproj, wp);
-    const f3 n = normalize3(m3v(dr.nmat, f3{N[0], N[1], N[2]}));
     o.cx = c.x; o.cy = c.y; o.cz = c.z; o.cw = c.w;
     o.wx = wp.x; o.wy = wp.y; o.wz = wp.z;
-    o.nx = n.x; o.ny = n.y; o.nz = n.z;
-    o.u = U[0]; o.v = U[1];
+    o.nx = o.ny = o.nz = 0.0f;
+    o.u = o.v = 0.0f;
+    return o;
+}
+
+__device__ __forceinline__ LVert vertex_out(const LibDrawGPU &dr, uint32_t id) {
+    LVert o = vertex_pos(dr, id);
+    vertex_attrs(dr, id, o);
     return o;
 }
 
@@ -230,6 +247,7 @@ struct Pend {
 };
 struct SetupShared {
     uint4 big[BIG_CAP];       // (slot, bx, by, 0)
+    uint32_t pre[2][BIG_CAP + 1]; // large primitives: first busy-mark task, first bin-append task
     uint32_t nbig;
     uint32_t stat[2];
     int ub[4];                // union of deferred bin rects: bx0, by0, bx1, by1
@@ -261,11 +279,13 @@ __device__ __forceinline__ void store_box(const LibBuffers &fb, uint32_t slot, i
 // One fan triangle of rasterize_mesh (rasterizer.hpp:255-328): NDC, screen (y-up), the area /
 // cull / bbox rejects; writes the primitive's record, varyings and box into slot.  Counts
 // tri_after_clip / tri_raster like the reference.
+// lazy_ids (trivially inside triangles): a, b, c hold positions only; the normal / UV varyings are
+// loaded and transformed for primitives that survive the culls.
 __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, const LibDrawGPU &dr, int d,
-                         uint32_t seq, uint32_t slot, const LVert &a, const LVert &b, const LVert &c, uint32_t &n_clip,
-                         uint32_t &n_rast, SetupShared &ss, Pend &pend) {
+                         uint32_t seq, uint32_t slot, LVert a, LVert b, LVert c, uint32_t &n_clip,
+                         uint32_t &n_rast, SetupShared &ss, Pend &pend, const uint32_t *lazy_ids = nullptr) {
     ++n_clip;
-    const LVert *v[3] = {&a, &b, &c};
+    LVert *v[3] = {&a, &b, &c};
     float sx[3], sy[3];
     bool finite = true;
 #pragma unroll
@@ -296,9 +316,24 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
             }
         }
     }
+    if (live && fp.count > 1) {
+        // tile-sharded pass: a small primitive on no owned 32x32 tile is not needed on this rank
+        // (its record, varyings and marks are skipped; the frame counters still count it)
+        const int tx0 = x0 / TILE, tx1 = x1 / TILE, ty0 = y0 / TILE, ty1 = y1 / TILE;
+        if ((tx1 - tx0) < 2 && (ty1 - ty0) < 2) {
+            bool mine = false;
+            for (int ty = ty0; ty <= ty1; ++ty)
+                for (int tx = tx0; tx <= tx1; ++tx) mine = mine || lib_owned(fp, tx, ty);
+            live = mine;
+        }
+    }
     if (!live) {
         store_box(fb, slot, 0, -1, 0, -1);
         return;
+    }
+    if (lazy_ids) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) vertex_attrs(dr, lazy_ids[k], *v[k]);
     }
     LibRec r;
     r.ax = sx[0]; r.ay = sy[0];
@@ -347,8 +382,8 @@ __device__ uint2 setup_clipped_tri(const LibFrameParams &fp, const LibBuffers &f
 
 // Camera pass: one input triangle of rasterize_mesh.
 __device__ __forceinline__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_clip,
-                                 uint32_t &n_rast, SetupShared &ss, Pend &pend) {
-    const int d = lib_find_draw(fb.draws, fp.n_draws, tri);
+                                 uint32_t &n_rast, SetupShared &ss, Pend &pend, int d_uni) {
+    const int d = d_uni >= 0 ? d_uni : lib_find_draw(fb.draws, fp.n_draws, tri);
     const LibDrawGPU &dr = fb.draws[d];
     const int local = tri - dr.tri_base;
     uint32_t id[3];
@@ -358,10 +393,10 @@ __device__ __forceinline__ void setup_camera_tri(const LibFrameParams &fp, const
     }
     LVert t[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) t[k] = vertex_out(dr, id[k]);
+    for (int k = 0; k < 3; ++k) t[k] = vertex_pos(dr, id[k]);
     const uint32_t seq0 = (uint32_t)tri * 16u;
     if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
-        emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast, ss, pend);
+        emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast, ss, pend, id);
         return;
     }
     const uint2 nc = setup_clipped_tri(fp, fb, cnt, d, tri, id[0], id[1], id[2], ss, pend);
@@ -406,8 +441,8 @@ __device__ __forceinline__ uint2 setup_clipped_tri(const LibFrameParams &fp, con
 // Shadow pass: one caster triangle of PassShadowMap (pass_shadow_map.hpp:155-203), draws[d].viewproj
 // holding the light camera's viewproj.  n_rast counts the triangles with a non-empty bbox.
 __device__ __forceinline__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_rast,
-                                 SetupShared &ss, Pend &pend) {
-    const int d = lib_find_draw(fb.draws, fp.n_draws, tri);
+                                 SetupShared &ss, Pend &pend, int d_uni) {
+    const int d = d_uni >= 0 ? d_uni : lib_find_draw(fb.draws, fp.n_draws, tri);
     const LibDrawGPU &dr = fb.draws[d];
     const int local = tri - dr.tri_base;
     uint32_t id[3];
@@ -471,6 +506,8 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
     __shared__ SetupShared ss;
     const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const bool stl = fb.stimeline != nullptr && tid == 0;
+    const uint64_t st0 = stl ? tl_now() : 0ull;
     if (tid < 2) ss.stat[tid] = 0u;
     if (tid == 0) ss.nbig = 0u;
     if (tid < 4) ss.ub[tid] = tid < 2 ? INT_MAX : -1;
@@ -488,9 +525,19 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
     const int tri = b * 256 + tid;
     uint32_t n_clip = 0, n_rast = 0;
     Pend pend;
+    // the block's draw when all its triangles share one (block-uniform: its uniforms come in
+    // through scalar loads), else -1 and a per-thread search
+    const int t_first = b * 256, t_last = min(b * 256 + 255, fp.n_tris - 1);
+    const int d_first = lib_find_draw(fb.draws, fp.n_draws, t_first);
+    const int d_uni = (d_first + 1 >= fp.n_draws || fb.draws[d_first + 1].tri_base > t_last) ? d_first : -1;
     if (tri < fp.n_tris) {
-        if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend);
-        else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend);
+        if (d_uni >= 0) {   // two inlined copies: this one sees d_uni as the (scalar) draw
+            if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, d_uni);
+            else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, d_uni);
+        } else {
+            if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, -1);
+            else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, -1);
+        }
     }
     if (pend.valid) {
         atomicMin(&ss.ub[0], pend.x0 / TILE);
@@ -507,9 +554,11 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
         atomicAdd(&ss.stat[1], n_rast);
     }
     __syncthreads();
+    const uint64_t st1 = stl ? tl_now() : 0ull;
     // the deferred primitives (<= 2x2 bin tiles each): busy rows and bin appends through LDS
     {
         const int ubx0 = ss.ub[0], uby0 = ss.ub[1], uw = ss.ub[2] - ubx0 + 1, uh = ss.ub[3] - uby0 + 1;
+        if (stl) fb.stimeline[(size_t)b * STL_STRIDE + 5] = (uint64_t)max(uw, 0) * (uint64_t)max(uh, 0);
         const bool agg = uw > 0 && uh > 0 && uw * uh <= AGG_BINS;   // block-uniform
         const bool sharded = fp.count > 1;
         constexpr int RPB = TILE / LIB_RTH;                        // raster rows per bin tile
@@ -561,13 +610,82 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
             }
         }
     }
-    // the block's large primitives: every thread takes every 256th of their tiles
+    const uint64_t st2 = stl ? tl_now() : 0ull;
+    // The block's large primitives, all at once: their (primitive, raster tile) busy marks and
+    // (primitive, bin tile) appends are laid end to end (prefix sums over the queue) and dealt over
+    // the block; a task finds its primitive by binary search.
     const uint32_t nbig = min(ss.nbig, (uint32_t)BIG_CAP);
-    for (uint32_t i = 0; i < nbig; ++i) {
-        const uint4 e = ss.big[i];
-        lib_mark_range(fp, fb, cnt, lo16(e.y), hi16(e.y), lo16(e.z), hi16(e.z), e.x, tid, 256);
+    if (nbig > 0) {   // block-uniform
+        auto extent = [&](uint32_t i, int cell_w, int cell_h, int &cx0, int &cy0, int &nx) {
+            const uint4 e = ss.big[i];
+            cx0 = lo16(e.y) / cell_w;
+            cy0 = lo16(e.z) / cell_h;
+            nx = hi16(e.y) / cell_w - cx0 + 1;
+            return (uint32_t)(nx * (hi16(e.z) / cell_h - cy0 + 1));
+        };
+        // exclusive scans of the task counts (BIG_CAP = 2 x 256: two values per thread)
+        static_assert(BIG_CAP == 512, "two queue entries per thread");
+        uint32_t c[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t i = 2u * tid + h;
+            int a, b2, n;
+            c[0][h] = i < nbig ? extent(i, LIB_RTW, LIB_RTH, a, b2, n) : 0u;
+            c[1][h] = i < nbig && !fp.scan_mode ? extent(i, TILE, TILE, a, b2, n) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t pair = c[q][0] + c[q][1];
+            uint32_t incl = pair;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t vv = (uint32_t)__shfl_up((int)incl, o);
+                if ((tid & 63) >= o) incl += vv;
+            }
+            __syncthreads();
+            if ((tid & 63) == 63) ss.bcnt[tid >> 6] = incl;    // per-wave totals (bcnt is free now)
+            __syncthreads();
+            uint32_t wb = 0;
+            for (int w2 = 0; w2 < (tid >> 6); ++w2) wb += ss.bcnt[w2];
+            const uint32_t excl = wb + incl - pair;
+            ss.pre[q][2 * tid] = excl;
+            ss.pre[q][2 * tid + 1] = excl + c[q][0];
+            __syncthreads();
+            if (tid == 0) ss.pre[q][BIG_CAP] = ss.bcnt[0] + ss.bcnt[1] + ss.bcnt[2] + ss.bcnt[3];
+            __syncthreads();
+        }
+        const bool sharded = fp.count > 1;
+        uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t total = ss.pre[q][BIG_CAP];
+            uint32_t lo = 0;   // the primitive of task t: non-decreasing in t, so carried along
+            int cx0 = 0, cy0 = 0, nx = 1;
+            bool have = false;
+            for (uint32_t t = tid; t < total; t += 256) {
+                bool moved = !have;
+                while (lo + 1 < nbig && ss.pre[q][lo + 1] <= t) { ++lo; moved = true; }
+                if (moved) (void)extent(lo, q == 0 ? LIB_RTW : TILE, q == 0 ? LIB_RTH : TILE, cx0, cy0, nx);
+                have = true;
+                const int k = (int)(t - ss.pre[q][lo]);
+                const int cx = cx0 + k % nx, cy = cy0 + k / nx;
+                if (q == 0) {
+                    if (!sharded || lib_owned(fp, cx, cy / (TILE / LIB_RTH))) fb.busy[cy * fp.tiles_x + cx] = 1u;
+                } else if (!sharded || lib_owned(fp, cx, cy)) {
+                    const int bt = cy * fp.tiles_x + cx;
+                    lib_append_bin(fp, fb, cnt, bt, atomicAdd(&tcount[bt], 1u), ss.big[lo].x);
+                }
+            }
+        }
     }
     if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(ss.stat[0], ss.stat[1]);
+    if (fb.stimeline) {
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t *o = fb.stimeline + (size_t)b * STL_STRIDE;
+            o[0] = st0; o[1] = st1; o[2] = st2; o[3] = tl_now(); o[4] = nbig;
+        }
+    }
 }
 
 // ---- k_lib_raster -----------------------------------------------------------------------------
@@ -879,7 +997,6 @@ struct LibShared {
     uint8_t wown[LIB_PAIR_WORDS];         // surviving candidate owning each bitmap word's first pair
 };
 
-__device__ __forceinline__ uint64_t tl_now() { return __builtin_amdgcn_s_memrealtime(); }
 
 __device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
     LibRec r;

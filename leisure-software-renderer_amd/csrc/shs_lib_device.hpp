@@ -123,7 +123,12 @@ struct LibBuffers {
     const CullLight *lights;         // Forward+ program
     const uint32_t *tile_counts, *tile_indices;
     uint64_t *timeline;              // SHS_OPT_TIMELINE (camera pass): LTL_STRIDE per raster workgroup
+    uint64_t *stimeline;             // SHS_OPT_TIMELINE (camera pass): STL_STRIDE per setup workgroup
 };
+
+// Library setup timeline slots: start, after the per-triangle work, after the deferred marks,
+// after the large-primitive marks (= end), large primitives, deferred-union width x height.
+constexpr int STL_STRIDE = 6;
 
 // Library raster timeline slots (s_memrealtime, 100 MHz ticks): per workgroup start, end, summed
 // phase ticks over its busy tiles (gather, stage + pairs, resolve + shade), clear ticks, counts.

@@ -229,6 +229,16 @@ class Context:
         self._check(self._lib.shs_lib_debug_timeline(self._h, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)))
         return out.reshape(-1, len(self.LIB_TIMELINE_FIELDS))
 
+    def lib_debug_setup_timeline(self):
+        """Last camera pass's k_lib_setup workgroup timeline: uint64 [blocks, 6] (start, triangles done,
+        deferred marks done, end in 10-ns ticks; large primitives; deferred union w*h)."""
+        n = ctypes.c_int64()
+        self._check(self._lib.shs_lib_debug_setup_timeline(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        self._check(self._lib.shs_lib_debug_setup_timeline(self._h, out.ctypes.data_as(ctypes.c_void_p), n.value,
+                                                           ctypes.byref(n)))
+        return out.reshape(-1, 6)
+
     def debug_timeline(self):
         """Last frame's workgroup timeline: (header dict, setup [n,2], raster [n,2]) in 10-ns ticks."""
         n = ctypes.c_int64()

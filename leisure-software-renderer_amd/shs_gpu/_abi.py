@@ -167,6 +167,7 @@ SIGNATURES = [
     ("shs_set_option", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int64]),
     ("shs_debug_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_lib_debug_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    ("shs_lib_debug_setup_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),
     ("shs_model_trs", ctypes.c_int, [_F, ctypes.c_float, _F, _F]),
     ("shs_mat4_mul", ctypes.c_int, [_F, _F, _F]),

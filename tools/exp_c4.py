@@ -12,8 +12,10 @@ import shs_gpu  # noqa: E402
 from shs_gpu import lib_path, scene_lib  # noqa: E402
 
 
-def run(label, n_objects=1000, tpo=1000, program=None, width=3840, height=2160, frames=20):
+def run(label, n_objects=1000, tpo=1000, program=None, width=3840, height=2160, frames=20, shard=(0, 1)):
     frame, draws, lights, cull = scene_lib.c4_scene(width, height, n_objects=n_objects, tris_per_object=tpo)
+    frame.shard_rank, frame.shard_count = shard
+    cull.shard_rank, cull.shard_count = shard
     if program is not None:
         for d in draws:
             d.program = program
@@ -48,6 +50,8 @@ def main():
     run("c4 250k tris", n_objects=250, frames=frames)
     run("c4 100 obj x 100", n_objects=100, tpo=100, frames=frames)
     run("c4 1080p", width=1920, height=1080, frames=frames)
+    for n in (2, 4, 8):
+        run(f"c4 rank 0 of {n}", frames=frames, shard=(0, n))
 
 
 if __name__ == "__main__":

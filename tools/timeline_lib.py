@@ -59,6 +59,17 @@ def main():
             dist(n + " us", f[n] / 100.0)
         for n in ("n_busy", "n_clear", "chunks", "n_pairs", "n_cand"):
             dist(n, f[n].astype(np.float64))
+        st = ctx.lib_debug_setup_timeline().astype(np.int64)
+        s0 = st[:, 0].min()
+        sd = (st[:, 3] - st[:, 0]) / 100.0
+        ks = int(np.argmax(sd))
+        print(f"  setup: {len(st)} workgroups, span {(st[:, 3].max() - s0) / 100:.1f} us, start spread "
+              f"{(st[:, 0].max() - s0) / 100:.1f} us; wg dur med {np.median(sd):.2f} p90 {np.percentile(sd, 90):.2f} "
+              f"max {sd.max():.2f}; phases (tri/defer/big) med {np.median((st[:, 1] - st[:, 0]) / 100):.2f}/"
+              f"{np.median((st[:, 2] - st[:, 1]) / 100):.2f}/{np.median((st[:, 3] - st[:, 2]) / 100):.2f}; "
+              f"slowest wg {ks}: {(st[ks, 1] - st[ks, 0]) / 100:.2f}/{(st[ks, 2] - st[ks, 1]) / 100:.2f}/"
+              f"{(st[ks, 3] - st[ks, 2]) / 100:.2f} big={st[ks, 4]} union={st[ks, 5]}; blocks with big prims "
+              f"{int((st[:, 4] > 0).sum())}, no-agg unions {int((st[:, 5] > 256).sum())}")
         k = int(np.argmax(dur))
         print("  slowest wg %d: %s" % (k, " ".join(
             "%s=%s" % (n, ("%.1f" % (f[n][k] / 100.0)) if n in ("gather", "pairs", "shade", "clear", "max_tile")
