@@ -325,6 +325,27 @@ int shs_model_euler(const float pos[3], const float rot_euler[3], const float sc
 int shs_dir_light_camera_aabb(const float sun_dir[3], const float aabb_min[3], const float aabb_max[3], float extra_margin,
                               uint32_t resolution, float view16[16], float proj16[16], float viewproj16[16]);
 
+/* ---- after the path: PassTonemap + present staging ------------------------
+ * PassTonemap::execute (shs-renderer-lib/include/shs/passes/pass_tonemap.hpp:36-83) over the last
+ * camera pass's HDR target, and the SDL texture staging of upload_ldr_to_rgba8
+ * (exp-plumbing/hello_pass_basics.cpp:102-119), in one launch on the context stream.  The bytes are
+ * the reference's: the host derives, with its own std::pow / std::lround, the 255 thresholds in
+ * x = c / (1 + c) where the byte changes, and the kernel counts thresholds. */
+#define SHS_TONEMAP_LDR 1u      /* RT_ColorLDR: W*H RGBA8, rows y up, alpha 255 */
+#define SHS_TONEMAP_PRESENT 2u  /* RGBA8 staging for SDL_UpdateTexture: rows top-down, alpha 255 */
+typedef struct shs_tonemap_desc {
+    float exposure;             /* FrameParams::pass.tonemap.exposure (clamped to >= 0.0001 as the pass does) */
+    float gamma;                /* ...gamma (clamped to >= 0.001) */
+    uint32_t flags;             /* SHS_TONEMAP_* targets to write (at least one) */
+} shs_tonemap_desc;
+int shs_tonemap(shs_ctx *ctx, const shs_tonemap_desc *desc);
+/* Copy the tonemapped targets into caller-owned W*H*4-byte buffers (either may be NULL). */
+int shs_resolve_ldr(shs_ctx *ctx, uint8_t *ldr, uint8_t *present);
+int shs_ldr_device_targets(shs_ctx *ctx, void **ldr_dev, void **present_dev);
+/* Host-only (no device): the byte thresholds for gamma (thr[0] = 0; +inf where a byte is never
+ * reached).  Exposed for the parity tests. */
+int shs_tonemap_thresholds(float gamma, float thr[256]);
+
 #ifdef __cplusplus
 }
 #endif

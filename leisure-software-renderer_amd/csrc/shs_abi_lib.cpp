@@ -288,8 +288,10 @@ int lib_finish(shs_ctx *ctx) {
         if (check_pass(ctx, ctx->lib_shadow, g_sh) || check_pass(ctx, ctx->lib_cam, g_cam)) return SHS_ERR_HIP;
         if (!g_sh && !g_cam) return SHS_OK;
         if (g_sh && enqueue_pass(ctx, ctx->lib_shadow, true)) return SHS_ERR_HIP;
-        if ((g_cam || (g_sh && ctx->cam_after_shadow)) && ctx->lib_cam.done && enqueue_pass(ctx, ctx->lib_cam, false))
-            return SHS_ERR_HIP;
+        if ((g_cam || (g_sh && ctx->cam_after_shadow)) && ctx->lib_cam.done) {
+            if (enqueue_pass(ctx, ctx->lib_cam, false)) return SHS_ERR_HIP;
+            if (ctx->have_ldr && shs_tonemap_reissue(ctx)) return SHS_ERR_HIP;
+        }
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     ctx->err = "capacity overflow persisted";
@@ -312,6 +314,7 @@ void shs_lib_release(shs_ctx *ctx) {
     release(ctx->lib_hdr); release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
     release(ctx->lights); release(ctx->light_proj); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
+    release(ctx->lib_ldr); release(ctx->lib_present);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
 }
@@ -484,6 +487,7 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     const int rc = enqueue_pass(ctx, wk, false);
     if (rc) return rc;
     ctx->have_lib_frame = true;
+    ctx->have_ldr = false;   // a new camera pass: a tonemap must follow it again
     return SHS_OK;
 }
 

@@ -146,7 +146,16 @@ struct shs_ctx {
     DevBuf<uint32_t> list_counts, list_indices;
     shs_dev::LightCullParams cull{};
     bool have_cull = false;
+    // PassTonemap + present staging (shs_abi_post.cpp)
+    DevBuf<uint32_t> lib_ldr, lib_present;
+    shs_tonemap_desc tm_desc{};
+    float tm_gamma = -1.0f;               // gamma of tm_thr
+    float tm_thr[256] = {};
+    bool have_ldr = false;                // a tonemap follows the current camera pass
 };
+
+// Re-enqueues the tonemap after lib_finish re-issued the camera pass (shs_abi_post.cpp).
+int shs_tonemap_reissue(shs_ctx *ctx);
 
 #define HIP_TRY(ctx, expr)                                                                       \
     do {                                                                                         \

@@ -1,0 +1,54 @@
+// shs_post.hip -- gfx950 kernels for the step after the raster path:
+//   PassTonemap::execute     shs-renderer-lib/include/shs/passes/pass_tonemap.hpp:36-83
+//   upload_ldr_to_rgba8      exp-plumbing/hello_pass_basics.cpp:102-119 (the SDL texture staging)
+// (paths relative to /root/reference/cpp-folders/src/).  One launch reads the HDR target once and
+// writes the LDR target and / or the present staging once: 16 B read + 4 or 8 B written per pixel,
+// HBM-bound.
+#include <float.h>
+
+#include "shs_post_internal.hpp"
+
+namespace shs_dev {
+
+// One channel: exposure, std::max(0, c) (NaN -> 0), Reinhard, then the byte by threshold count.
+// The first guess comes from a fast pow; the two loops move it to the exact count.
+__device__ __forceinline__ uint32_t tonemap_byte(float s, float exposure, float inv_gamma, const float *thr) {
+    const float e = s * exposure;
+    const float c = (0.0f < e) ? e : 0.0f;
+    const float x = c / (1.0f + c);
+    if (!(x >= 0.0f)) return 0u;   // c = inf: inf / inf = NaN, and the reference's lround(NaN) casts to 0
+    const float g = x > 0.0f ? __builtin_amdgcn_exp2f(inv_gamma * __builtin_amdgcn_logf(x)) : 0.0f;
+    int k = (int)fminf(fmaxf(g * 255.0f + 0.5f, 0.0f), 255.0f);
+    while (k < 255 && thr[k + 1] <= x) ++k;
+    while (k > 0 && thr[k] > x) --k;
+    return (uint32_t)k;
+}
+
+// 64 x 4 pixels per workgroup: each wave reads 64 float4 of one row (1 KB) and writes 256 B rows.
+__global__ __launch_bounds__(256) void k_tonemap(TonemapParams p) {
+    __shared__ float thr[256];
+    thr[threadIdx.x] = p.thr[threadIdx.x];
+    __syncthreads();
+    const int x = (int)blockIdx.x * 64 + (int)(threadIdx.x & 63u);
+    const int y = (int)blockIdx.y * 4 + (int)(threadIdx.x >> 6);
+    if (x >= p.W || y >= p.H) return;
+    const float4 s = p.hdr[(size_t)y * p.W + x];
+    const uint32_t rgba = tonemap_byte(s.x, p.exposure, p.inv_gamma, thr) |
+                          (tonemap_byte(s.y, p.exposure, p.inv_gamma, thr) << 8) |
+                          (tonemap_byte(s.z, p.exposure, p.inv_gamma, thr) << 16) | (255u << 24);
+    if (p.ldr) __builtin_nontemporal_store(rgba, &p.ldr[(size_t)y * p.W + x]);
+    if (p.present) __builtin_nontemporal_store(rgba, &p.present[(size_t)(p.H - 1 - y) * p.W + x]);
+}
+
+}  // namespace shs_dev
+
+namespace shs_internal {
+using namespace shs_dev;
+
+hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s) {
+    const dim3 grid((unsigned)((p.W + 63) / 64), (unsigned)((p.H + 3) / 4));
+    hipLaunchKernelGGL(k_tonemap, grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace shs_internal

@@ -1,0 +1,27 @@
+// shs_post_internal.hpp -- launch interface of shs_post.hip (the passes after the raster path).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace shs_dev {
+
+// PassTonemap + the present staging.  thr[k] (k = 1..255) is the smallest x = c / (1 + c) whose
+// reference byte clamp(lround(pow(x, inv_gamma) * 255), 0, 255) is >= k (+inf when none is): the
+// byte of any x is the number of thresholds <= x (the composite is monotone in x), so the GPU
+// reproduces the host libm's pow / lround exactly without evaluating them.
+struct TonemapParams {
+    const float4 *hdr;      // W*H, rows y up (RT_ColorHDR)
+    uint32_t *ldr;          // W*H RGBA8, rows y up (RT_ColorLDR), or null
+    uint32_t *present;      // W*H RGBA8, rows top-down (upload_ldr_to_rgba8), or null
+    int W, H;
+    float exposure;         // max(0.0001, exposure)
+    float inv_gamma;        // 1 / max(0.001, gamma): only steers the first guess
+    float thr[256];         // thr[0] unused
+};
+
+}  // namespace shs_dev
+
+namespace shs_internal {
+hipError_t launch_tonemap(const shs_dev::TonemapParams &p, hipStream_t s);
+}  // namespace shs_internal

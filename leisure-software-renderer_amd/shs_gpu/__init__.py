@@ -217,6 +217,46 @@ class Context:
     def set_timeline(self, enable: bool):
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_TIMELINE, 1 if enable else 0))
 
+    # -- after the path: PassTonemap + present staging ------------------------------------------
+    def tonemap(self, exposure: float = 1.0, gamma: float = 2.2, ldr: bool = True, present: bool = True):
+        """PassTonemap (pass_tonemap.hpp:36-83) over the last camera pass's HDR target into the
+        RT_ColorLDR layout and / or the SDL staging of upload_ldr_to_rgba8 (one launch)."""
+        d = _abi.TonemapDescC()
+        d.exposure, d.gamma = float(exposure), float(gamma)
+        d.flags = (_abi.TONEMAP_LDR if ldr else 0) | (_abi.TONEMAP_PRESENT if present else 0)
+        self._check(self._lib.shs_tonemap(self._h, ctypes.byref(d)))
+        self._tonemap_flags = d.flags
+
+    def resolve_ldr(self):
+        """-> (ldr uint8 [H, W, 4] rows y up or None, present uint8 [H, W, 4] rows top-down or None)."""
+        f = self._lib_frame
+        flags = getattr(self, "_tonemap_flags", 0)
+        ldr = np.empty((f.height, f.width, 4), np.uint8) if flags & _abi.TONEMAP_LDR else None
+        pre = np.empty((f.height, f.width, 4), np.uint8) if flags & _abi.TONEMAP_PRESENT else None
+        self._check(self._lib.shs_resolve_ldr(self._h, None if ldr is None else ldr.ctypes.data_as(ctypes.c_void_p),
+                                              None if pre is None else pre.ctypes.data_as(ctypes.c_void_p)))
+        return ldr, pre
+
+    def lib_device_targets(self):
+        """Device pointers of the library targets: (hdr float4 W*H, depth W*H, motion float2 W*H)."""
+        a, b, c = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(self._lib.shs_lib_device_targets(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def ldr_device_targets(self):
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(self._lib.shs_ldr_device_targets(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    @staticmethod
+    def tonemap_thresholds(gamma: float):
+        """Host-side byte thresholds in x = c / (1 + c) (thr[0] = 0; +inf = byte never reached)."""
+        thr = np.zeros(256, np.float32)
+        rc = lib().shs_tonemap_thresholds(float(gamma), thr.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        if rc != 0:
+            raise ShsError(rc, "shs_tonemap_thresholds")
+        return thr
+
     LIB_TIMELINE_FIELDS = ("start", "end", "gather", "pairs", "shade", "clear", "n_busy", "n_clear", "chunks",
                            "n_pairs", "n_cand", "max_tile")
 

@@ -122,6 +122,11 @@ class ShadowCasterC(ctypes.Structure):
 
 
 PROGRAM_FORWARD_PLUS = 5
+TONEMAP_LDR, TONEMAP_PRESENT = 1, 2
+
+
+class TonemapDescC(ctypes.Structure):
+    _fields_ = [("exposure", ctypes.c_float), ("gamma", ctypes.c_float), ("flags", ctypes.c_uint32)]
 LIGHT_CULL_NONE, LIGHT_CULL_TILED, LIGHT_CULL_TILED_DEPTH, LIGHT_CULL_CLUSTERED = 0, 1, 2, 3
 _F4 = ctypes.c_float * 4
 
@@ -168,6 +173,10 @@ SIGNATURES = [
     ("shs_debug_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_lib_debug_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_lib_debug_setup_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    ("shs_tonemap", ctypes.c_int, [_P, ctypes.POINTER(TonemapDescC)]),
+    ("shs_resolve_ldr", ctypes.c_int, [_P, _P, _P]),
+    ("shs_ldr_device_targets", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    ("shs_tonemap_thresholds", ctypes.c_int, [ctypes.c_float, _F]),
     ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),
     ("shs_model_trs", ctypes.c_int, [_F, ctypes.c_float, _F, _F]),
     ("shs_mat4_mul", ctypes.c_int, [_F, _F, _F]),

@@ -362,3 +362,28 @@ def forward_plus(frame, draws, lights, cull, lists, shadow_map=None):
 
 
 _FWD_CTX = None
+
+
+def tonemap(hdr, exposure=1.0, gamma=2.2):
+    """PassTonemap + upload_ldr_to_rgba8 over hdr float32 [H, W, 4] (rows y up) ->
+    (ldr uint8 [H, W, 4] rows y up, present uint8 [H, W, 4] rows top-down)."""
+    L = _lib_lib()
+    if not getattr(L, "_post_ready", False):
+        P = ctypes.c_void_p
+        L.ora_tonemap.restype = None
+        L.ora_tonemap.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float, P, P]
+        L.ora_tonemap_channel.restype = ctypes.c_uint8
+        L.ora_tonemap_channel.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float]
+        L._post_ready = True
+    hdr = np.ascontiguousarray(hdr, dtype=np.float32)
+    H, W = hdr.shape[:2]
+    ldr = np.empty((H, W, 4), np.uint8)
+    present = np.empty((H, W, 4), np.uint8)
+    L.ora_tonemap(hdr.ctypes.data, W, H, float(exposure), float(gamma), ldr.ctypes.data, present.ctypes.data)
+    return ldr, present
+
+
+def tonemap_channel(s, exposure, inv_gamma):
+    """One channel byte of PassTonemap (exposure / inv_gamma already clamped as the pass does)."""
+    tonemap(np.zeros((1, 1, 4), np.float32))   # binds the signatures
+    return int(_lib_lib().ora_tonemap_channel(float(s), float(exposure), float(inv_gamma)))

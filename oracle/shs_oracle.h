@@ -172,6 +172,11 @@ void ora_point_light_accumulate(const ora_culling_light *L, const float *world, 
                                 const float *base, float *lit);
 float ora_mat4_determinant(const float *m);
 
+/* PassTonemap (passes/pass_tonemap.hpp:36-83) + upload_ldr_to_rgba8 (exp-plumbing/hello_pass_basics.cpp:102-119):
+ * hdr W*H*4 floats (rows y up) -> ldr (rows y up) and / or present (rows top-down), W*H*4 bytes. */
+uint8_t ora_tonemap_channel(float s, float exposure, float inv_gamma);
+void ora_tonemap(const float *hdr, int W, int H, float exposure, float gamma, uint8_t *ldr, uint8_t *present);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,146 @@
+"""PassTonemap + present staging: shs_tonemap against the oracle restatement of
+pass_tonemap.hpp:36-83 and hello_pass_basics.cpp:102-119 (oracle/shs_oracle_post.c).
+
+CPU: the library's host-side byte thresholds reproduce the reference expression (glibc powf / lround)
+on dense float samples around every threshold, with the kernel's decision (count of thresholds <= x)
+emulated in numpy.  GPU: bit-exact LDR and present bytes for rendered and synthetic HDR targets."""
+import numpy as np
+import pytest
+
+
+def _x_of(s, exposure):
+    """The kernel's x = c / (1 + c), c = std::max(0, s * exposure), in float32."""
+    e = np.float32(s) * np.float32(exposure)
+    c = np.where(np.float32(0) < e, e, np.float32(0)).astype(np.float32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        return (c / (np.float32(1) + c)).astype(np.float32)
+
+
+def _emulate(s, exposure, thr):
+    x = _x_of(s, exposure)
+    out = np.zeros(x.shape, np.int64)
+    ok = x >= 0   # NaN -> 0
+    out[ok] = np.searchsorted(thr[1:], x[ok], side="right")
+    return out
+
+
+@pytest.mark.parametrize("gamma", [2.2, 1.0, 1.8, 0.5])
+def test_thresholds_match_reference_bytes(oracle_mod, gamma):
+    import shs_gpu
+    thr = shs_gpu.Context.tonemap_thresholds(gamma)
+    assert np.all(np.diff(thr[1:]) >= 0)
+    inv_gamma = np.float32(1.0) / np.float32(max(0.001, gamma))
+    # s values whose x lands within +-40 ulps of each finite threshold, plus a uniform sweep
+    samples = [np.linspace(-1.0, 50.0, 4001, dtype=np.float32)]
+    for t in thr[1:]:
+        if not np.isfinite(t) or t <= 0 or t >= 1:
+            continue
+        s0 = np.float32(t / (1.0 - t))
+        samples.append(s0 + np.arange(-40, 41, dtype=np.float32) * np.spacing(s0))
+    s = np.concatenate(samples).astype(np.float32)
+    want = np.array([oracle_mod.tonemap_channel(v, 1.0, inv_gamma) for v in s])
+    got = _emulate(s, 1.0, thr)
+    bad = np.nonzero(want != got)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, e.g. s={s[bad[:5]]} want={want[bad[:5]]} got={got[bad[:5]]}"
+
+
+def test_oracle_edge_values(oracle_mod):
+    """NaN and negative inputs give 0; +inf gives 0 (inf / inf = NaN, lround(NaN) casts to 0 on x86-64);
+    a huge finite value gives 255; alpha is 255; present is the y-flip of ldr."""
+    hdr = np.array([[[np.nan, -1.0, 1e30, 1.0], [np.inf, 0.0, 1.0, 0.5]],
+                    [[0.25, 0.5, 4.0, 1.0], [-np.inf, 1e-30, 2.0, 1.0]]], np.float32)
+    ldr, pre = oracle_mod.tonemap(hdr, 1.0, 2.2)
+    assert ldr[0, 0, 0] == 0 and ldr[0, 0, 1] == 0 and ldr[0, 0, 2] == 255 and ldr[0, 1, 0] == 0
+    assert np.all(ldr[..., 3] == 255)
+    assert np.array_equal(pre, ldr[::-1])
+
+
+# ---- GPU ------------------------------------------------------------------------------------------
+
+def _c5(W, H):
+    from shs_gpu import scene_lib
+    frame, draws, casters, sun, S = scene_lib.c5_scene(W, H)
+    return frame, draws
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exposure,gamma", [(1.0, 2.2), (2.5, 2.2), (0.7, 1.0), (1.0, 1.6)])
+def test_tonemap_rendered_frame_exact(oracle_mod, exposure, gamma):
+    import shs_gpu
+    frame, draws = _c5(352, 200)
+    with shs_gpu.Context(0) as ctx:
+        ctx.render_pbr_forward(frame, draws)
+        ctx.tonemap(exposure, gamma)
+        ldr, pre = ctx.resolve_ldr()
+        hdr, _, _ = ctx.resolve_lib()
+    want_ldr, want_pre = oracle_mod.tonemap(hdr, exposure, gamma)
+    assert np.array_equal(ldr, want_ldr)
+    assert np.array_equal(pre, want_pre)
+
+
+@pytest.mark.gpu
+def test_tonemap_synthetic_hdr_exact(oracle_mod):
+    """Every byte boundary, NaN / inf / negative / denormal / huge inputs, written straight into the
+    device HDR target."""
+    import torch
+    import shs_gpu
+    W, H = 256, 64
+    frame, draws = _c5(W, H)
+    thr = shs_gpu.Context.tonemap_thresholds(2.2)
+    vals = []
+    for t in thr[1:]:
+        if np.isfinite(t) and 0 < t < 1:
+            s0 = np.float32(t / (1.0 - t))
+            vals += list(s0 + np.arange(-6, 7, dtype=np.float32) * np.spacing(s0))
+    vals += [np.nan, np.inf, -np.inf, -0.0, 0.0, 1e-45, 1e-38, 3e38, -5.0, 1e6]
+    rng = np.random.default_rng(3)
+    flat = np.array(vals, np.float32)
+    hdr = rng.uniform(-0.5, 8.0, size=(H, W, 4)).astype(np.float32)
+    n = min(flat.size, H * W * 3)
+    rgb = hdr[..., :3].reshape(-1).copy()
+    rgb[:n] = flat[:n]
+    hdr[..., :3] = rgb.reshape(H, W, 3)
+    hdr[..., 3] = 1.0
+    assert np.isnan(hdr).any() and np.isinf(hdr).any()
+    with shs_gpu.Context(0) as ctx:
+        ctx.render_pbr_forward(frame, draws)
+        ctx.synchronize_lib()
+        dev = ctx.lib_device_targets()[0]
+        src = torch.from_numpy(hdr.reshape(-1)).to("cuda:0")
+        torch.cuda.synchronize()
+        _memcpy_d2d(dev, src.data_ptr(), hdr.nbytes)
+        ctx.tonemap(1.0, 2.2)
+        ldr, pre = ctx.resolve_ldr()
+    want_ldr, want_pre = oracle_mod.tonemap(hdr, 1.0, 2.2)
+    bad = np.argwhere(ldr != want_ldr)
+    assert bad.size == 0, f"{len(bad)} mismatches, first {bad[:4]}"
+    assert np.array_equal(pre, want_pre)
+
+
+def _memcpy_d2d(dst, src, nbytes):
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    rc = hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 3)   # hipMemcpyDeviceToDevice
+    assert rc == 0, rc
+
+
+@pytest.mark.gpu
+def test_tonemap_follows_new_pass_and_validates(oracle_mod):
+    import shs_gpu
+    from shs_gpu import ShsError
+    frame, draws = _c5(160, 96)
+    with shs_gpu.Context(0) as ctx:
+        with pytest.raises(ShsError):
+            ctx.tonemap()                     # no camera pass yet
+        ctx.render_pbr_forward(frame, draws)
+        with pytest.raises(ShsError):
+            ctx.resolve_ldr()                 # no tonemap since the pass
+        with pytest.raises(ShsError):
+            ctx.tonemap(ldr=False, present=False)
+        ctx.tonemap(ldr=False, present=True)
+        ldr, pre = ctx.resolve_ldr()
+        assert ldr is None and pre is not None
+        hdr, _, _ = ctx.resolve_lib()
+        _, want_pre = oracle_mod.tonemap(hdr, 1.0, 2.2)
+        assert np.array_equal(pre, want_pre)
