@@ -342,6 +342,25 @@ int shs_tonemap(shs_ctx *ctx, const shs_tonemap_desc *desc);
 /* Copy the tonemapped targets into caller-owned W*H*4-byte buffers (either may be NULL). */
 int shs_resolve_ldr(shs_ctx *ctx, uint8_t *ldr, uint8_t *present);
 int shs_ldr_device_targets(shs_ctx *ctx, void **ldr_dev, void **present_dev);
+/* PassMotionBlur::execute (shs-renderer-lib/include/shs/passes/pass_motion_blur.hpp:38-170) on the
+ * last tonemap's RT_ColorLDR (SHS_TONEMAP_LDR) with the camera pass's depth / motion planes
+ * (SHS_LIB_DEPTH_MOTION), into a separate RT_ColorLDR (+ its present staging with
+ * SHS_MOTION_BLUR_PRESENT).  Fields are FrameParams::pass.motion_blur (frame/frame_params.hpp:49-57)
+ * and FrameParams::dt; enable = 0 copies the input, as the pass does. */
+#define SHS_MOTION_BLUR_PRESENT 1u
+typedef struct shs_motion_blur_desc {
+    int32_t enable;
+    int32_t samples;            /* default 10, clamped to [4, 32] */
+    float strength;             /* 1 */
+    float max_velocity_px;      /* 20 */
+    float min_velocity_px;      /* 0.25 */
+    float depth_reject;         /* 0.08 */
+    float dt;                   /* FrameParams::dt, seconds */
+    uint32_t flags;             /* SHS_MOTION_BLUR_* */
+} shs_motion_blur_desc;
+int shs_motion_blur(shs_ctx *ctx, const shs_motion_blur_desc *desc);
+/* Copy the blurred RT_ColorLDR (rows y up) and / or its present staging (rows top-down). */
+int shs_resolve_motion_blur(shs_ctx *ctx, uint8_t *ldr, uint8_t *present);
 /* Host-only (no device): the byte thresholds for gamma (thr[0] = 0; +inf where a byte is never
  * reached).  Exposed for the parity tests. */
 int shs_tonemap_thresholds(float gamma, float thr[256]);

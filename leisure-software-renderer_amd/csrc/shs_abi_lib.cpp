@@ -314,7 +314,7 @@ void shs_lib_release(shs_ctx *ctx) {
     release(ctx->lib_hdr); release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
     release(ctx->lights); release(ctx->light_proj); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
-    release(ctx->lib_ldr); release(ctx->lib_present);
+    release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
 }
@@ -487,7 +487,8 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     const int rc = enqueue_pass(ctx, wk, false);
     if (rc) return rc;
     ctx->have_lib_frame = true;
-    ctx->have_ldr = false;   // a new camera pass: a tonemap must follow it again
+    ctx->have_ldr = false;   // a new camera pass: a tonemap (and motion blur) must follow it again
+    ctx->have_mb = false;
     return SHS_OK;
 }
 

@@ -1,6 +1,7 @@
-// shs_abi_post.cpp -- C ABI of the passes after the raster path (include/shs_gpu.h, SURVEY.md 8f row 1):
+// shs_abi_post.cpp -- C ABI of the passes after the raster path (include/shs_gpu.h, SURVEY.md 8f rows 1, 4):
 // PassTonemap (shs-renderer-lib/include/shs/passes/pass_tonemap.hpp:36-83) and the SDL texture
-// staging upload_ldr_to_rgba8 (exp-plumbing/hello_pass_basics.cpp:102-119), paths relative to
+// staging upload_ldr_to_rgba8 (exp-plumbing/hello_pass_basics.cpp:102-119) and PassMotionBlur
+// (shs-renderer-lib/include/shs/passes/pass_motion_blur.hpp:38-170), paths relative to
 // /root/reference/cpp-folders/src/.
 #include <cmath>
 #include <cstdint>
@@ -75,9 +76,40 @@ int enqueue_tonemap(shs_ctx *ctx) {
     return SHS_OK;
 }
 
+int enqueue_motion_blur(shs_ctx *ctx) {
+    const shs_motion_blur_desc &d = ctx->mb_desc;
+    const int W = ctx->lib_frame.width, H = ctx->lib_frame.height;
+    const size_t npx = (size_t)W * H;
+    if (ensure(ctx, ctx->lib_mb, npx)) return SHS_ERR_HIP;
+    if ((d.flags & SHS_MOTION_BLUR_PRESENT) && ensure(ctx, ctx->lib_mb_present, npx)) return SHS_ERR_HIP;
+    shs_dev::MotionBlurParams p{};
+    p.src = ctx->lib_ldr.p;
+    p.depth = ctx->lib_depth.p;
+    p.motion = ctx->lib_motion.p;
+    p.dst = ctx->lib_mb.p;
+    p.present = (d.flags & SHS_MOTION_BLUR_PRESENT) ? ctx->lib_mb_present.p : nullptr;
+    p.W = W;
+    p.H = H;
+    // the pass's parameter clamps (pass_motion_blur.hpp:76-81), the same float expressions
+    p.enable = d.enable != 0;
+    p.samples = std::min(std::max(d.samples, 4), 32);
+    p.strength = std::max(0.0f, d.strength);
+    p.max_vel = std::max(1.0f, d.max_velocity_px);
+    p.min_vel = std::max(0.0f, d.min_velocity_px);
+    p.depth_eps = std::max(0.0f, d.depth_reject);
+    const float dts = std::max(d.dt, 1e-4f) * 60.0f;
+    p.dt_scale = dts < 0.5f ? 0.5f : (2.5f < dts ? 2.5f : dts);   // std::clamp
+    HIP_TRY(ctx, shs_internal::launch_motion_blur(p, ctx->stream));
+    return SHS_OK;
+}
+
 }  // namespace
 
-int shs_tonemap_reissue(shs_ctx *ctx) { return enqueue_tonemap(ctx); }
+int shs_tonemap_reissue(shs_ctx *ctx) {
+    const int rc = enqueue_tonemap(ctx);
+    if (rc || !ctx->have_mb) return rc;
+    return enqueue_motion_blur(ctx);
+}
 
 extern "C" {
 
@@ -103,6 +135,39 @@ int shs_tonemap(shs_ctx *ctx, const shs_tonemap_desc *desc) {
     const int rc = enqueue_tonemap(ctx);
     if (rc) return rc;
     ctx->have_ldr = true;
+    ctx->have_mb = false;
+    return SHS_OK;
+}
+
+int shs_motion_blur(shs_ctx *ctx, const shs_motion_blur_desc *desc) {
+    if (!ctx || !desc) return SHS_ERR_INVALID;
+    if (!ctx->have_ldr || !(ctx->tm_desc.flags & SHS_TONEMAP_LDR)) {
+        ctx->err = "motion blur needs a tonemap with SHS_TONEMAP_LDR after the camera pass";
+        return SHS_ERR_INVALID;
+    }
+    if (!(ctx->lib_frame.flags & SHS_LIB_DEPTH_MOTION)) {
+        ctx->err = "motion blur needs the depth_motion target (SHS_LIB_DEPTH_MOTION)";
+        return SHS_ERR_INVALID;
+    }
+    if (desc->flags & ~SHS_MOTION_BLUR_PRESENT) { ctx->err = "motion blur flags"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    ctx->mb_desc = *desc;
+    const int rc = enqueue_motion_blur(ctx);
+    if (rc) return rc;
+    ctx->have_mb = true;
+    return SHS_OK;
+}
+
+int shs_resolve_motion_blur(shs_ctx *ctx, uint8_t *ldr, uint8_t *present) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (!ctx->have_mb) { ctx->err = "no motion blur since the last camera pass"; return SHS_ERR_INVALID; }
+    if (present && !(ctx->mb_desc.flags & SHS_MOTION_BLUR_PRESENT)) { ctx->err = "no present staging written"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    const int rc = shs_resolve_lib(ctx, nullptr, nullptr, nullptr);   // finishes (re-issues) the pass chain
+    if (rc) return rc;
+    const size_t n = (size_t)ctx->lib_frame.width * ctx->lib_frame.height * 4;
+    if (ldr) HIP_TRY(ctx, hipMemcpy(ldr, ctx->lib_mb.p, n, hipMemcpyDeviceToHost));
+    if (present) HIP_TRY(ctx, hipMemcpy(present, ctx->lib_mb_present.p, n, hipMemcpyDeviceToHost));
     return SHS_OK;
 }
 

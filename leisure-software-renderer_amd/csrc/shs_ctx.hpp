@@ -152,6 +152,9 @@ struct shs_ctx {
     float tm_gamma = -1.0f;               // gamma of tm_thr
     float tm_thr[256] = {};
     bool have_ldr = false;                // a tonemap follows the current camera pass
+    DevBuf<uint32_t> lib_mb, lib_mb_present;
+    shs_motion_blur_desc mb_desc{};
+    bool have_mb = false;                 // a motion blur follows that tonemap
 };
 
 // Re-enqueues the tonemap after lib_finish re-issued the camera pass (shs_abi_post.cpp).

@@ -1,6 +1,7 @@
 // shs_post.hip -- gfx950 kernels for the step after the raster path:
 //   PassTonemap::execute     shs-renderer-lib/include/shs/passes/pass_tonemap.hpp:36-83
 //   upload_ldr_to_rgba8      exp-plumbing/hello_pass_basics.cpp:102-119 (the SDL texture staging)
+//   PassMotionBlur::execute  shs-renderer-lib/include/shs/passes/pass_motion_blur.hpp:38-170
 // (paths relative to /root/reference/cpp-folders/src/).  One launch reads the HDR target once and
 // writes the LDR target and / or the present staging once: 16 B read + 4 or 8 B written per pixel,
 // HBM-bound.
@@ -40,10 +41,65 @@ __global__ __launch_bounds__(256) void k_tonemap(TonemapParams p) {
     if (p.present) __builtin_nontemporal_store(rgba, &p.present[(size_t)(p.H - 1 - y) * p.W + x]);
 }
 
+// std::lround then the (int) cast of the reference: half away from zero, 64-bit, then truncated
+// (NaN and out-of-range values end up 0 or clamped exactly like x86-64's lround + cast).
+__device__ __forceinline__ int lround_int(float v) { return (int)(long long)roundf(v); }
+
+__device__ __forceinline__ int clamp_i(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// One pixel of PassMotionBlur: the velocity (scaled, clamped), `samples` taps along it at
+// lround(p + v * t), depth-rejected, averaged as floats and rounded back to bytes.
+__global__ __launch_bounds__(256) void k_motion_blur(MotionBlurParams p) {
+    const int x = (int)blockIdx.x * 64 + (int)(threadIdx.x & 63u);
+    const int y = (int)blockIdx.y * 4 + (int)(threadIdx.x >> 6);
+    if (x >= p.W || y >= p.H) return;
+    const size_t o = (size_t)y * p.W + x;
+    uint32_t out = p.src[o];
+    if (p.enable) {
+        const float2 mv = p.motion[o];
+        float vx = mv.x * p.strength * p.dt_scale;
+        float vy = mv.y * p.strength * p.dt_scale;
+        const float len = sqrtf(vx * vx + vy * vy);
+        if (!(len < p.min_vel)) {
+            if (len > p.max_vel && len > 1e-6f) {
+                const float s = p.max_vel / len;
+                vx *= s;
+                vy *= s;
+            }
+            const float cd = p.depth[o];
+            float ar = 0.0f, ag = 0.0f, ab = 0.0f, aw = 0.0f;
+            for (int i = 0; i < p.samples; ++i) {
+                const float t = ((float)i / (float)(p.samples - 1) - 0.5f);
+                const int sx = clamp_i(lround_int((float)x + vx * t), 0, p.W - 1);
+                const int sy = clamp_i(lround_int((float)y + vy * t), 0, p.H - 1);
+                const size_t so = (size_t)sy * p.W + sx;
+                if (fabsf(p.depth[so] - cd) > p.depth_eps) continue;
+                const uint32_t c = p.src[so];
+                ar += (float)(c & 255u);
+                ag += (float)((c >> 8) & 255u);
+                ab += (float)((c >> 16) & 255u);
+                aw += 1.0f;
+            }
+            if (!(aw < 1.0f)) {
+                out = (uint32_t)clamp_i(lround_int(ar / aw), 0, 255) | ((uint32_t)clamp_i(lround_int(ag / aw), 0, 255) << 8) |
+                      ((uint32_t)clamp_i(lround_int(ab / aw), 0, 255) << 16) | (255u << 24);
+            }
+        }
+    }
+    p.dst[o] = out;
+    if (p.present) p.present[(size_t)(p.H - 1 - y) * p.W + x] = out;
+}
+
 }  // namespace shs_dev
 
 namespace shs_internal {
 using namespace shs_dev;
+
+hipError_t launch_motion_blur(const MotionBlurParams &p, hipStream_t s) {
+    const dim3 grid((unsigned)((p.W + 63) / 64), (unsigned)((p.H + 3) / 4));
+    hipLaunchKernelGGL(k_motion_blur, grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
 
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s) {
     const dim3 grid((unsigned)((p.W + 63) / 64), (unsigned)((p.H + 3) / 4));

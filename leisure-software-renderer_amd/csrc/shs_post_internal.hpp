@@ -20,8 +20,22 @@ struct TonemapParams {
     float thr[256];         // thr[0] unused
 };
 
+// PassMotionBlur (passes/pass_motion_blur.hpp:38-170) with the pass's parameter clamps applied
+// on the host (identical float expressions).
+struct MotionBlurParams {
+    const uint32_t *src;    // RT_ColorLDR RGBA8, rows y up
+    const float *depth;     // RT_ColorDepthMotion depth, rows y up
+    const float2 *motion;   // RT_ColorDepthMotion motion (px), rows y up
+    uint32_t *dst;          // blurred RT_ColorLDR
+    uint32_t *present;      // its upload_ldr_to_rgba8 staging (rows top-down), or null
+    int W, H;
+    int enable, samples;    // samples clamped to [4, 32]
+    float strength, max_vel, min_vel, depth_eps, dt_scale;
+};
+
 }  // namespace shs_dev
 
 namespace shs_internal {
 hipError_t launch_tonemap(const shs_dev::TonemapParams &p, hipStream_t s);
+hipError_t launch_motion_blur(const shs_dev::MotionBlurParams &p, hipStream_t s);
 }  // namespace shs_internal

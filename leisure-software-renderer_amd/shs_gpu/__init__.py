@@ -237,6 +237,27 @@ class Context:
                                               None if pre is None else pre.ctypes.data_as(ctypes.c_void_p)))
         return ldr, pre
 
+    def motion_blur(self, enable=True, samples=10, strength=1.0, max_velocity_px=20.0, min_velocity_px=0.25,
+                    depth_reject=0.08, dt=1.0 / 60.0, present=True):
+        """PassMotionBlur (pass_motion_blur.hpp:38-170) over the last tonemap's RT_ColorLDR with the
+        camera pass's depth / motion planes (defaults: MotionBlurPassParams)."""
+        d = _abi.MotionBlurDescC()
+        d.enable, d.samples = 1 if enable else 0, int(samples)
+        d.strength, d.max_velocity_px, d.min_velocity_px = float(strength), float(max_velocity_px), float(min_velocity_px)
+        d.depth_reject, d.dt = float(depth_reject), float(dt)
+        d.flags = _abi.MOTION_BLUR_PRESENT if present else 0
+        self._check(self._lib.shs_motion_blur(self._h, ctypes.byref(d)))
+        self._mb_present = bool(present)
+
+    def resolve_motion_blur(self):
+        """-> (blurred RT_ColorLDR uint8 [H, W, 4] rows y up, present staging or None)."""
+        f = self._lib_frame
+        ldr = np.empty((f.height, f.width, 4), np.uint8)
+        pre = np.empty((f.height, f.width, 4), np.uint8) if getattr(self, "_mb_present", False) else None
+        self._check(self._lib.shs_resolve_motion_blur(self._h, ldr.ctypes.data_as(ctypes.c_void_p),
+                                                      None if pre is None else pre.ctypes.data_as(ctypes.c_void_p)))
+        return ldr, pre
+
     def lib_device_targets(self):
         """Device pointers of the library targets: (hdr float4 W*H, depth W*H, motion float2 W*H)."""
         a, b, c = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()

@@ -125,6 +125,15 @@ PROGRAM_FORWARD_PLUS = 5
 TONEMAP_LDR, TONEMAP_PRESENT = 1, 2
 
 
+MOTION_BLUR_PRESENT = 1
+
+
+class MotionBlurDescC(ctypes.Structure):
+    _fields_ = [("enable", ctypes.c_int32), ("samples", ctypes.c_int32), ("strength", ctypes.c_float),
+                ("max_velocity_px", ctypes.c_float), ("min_velocity_px", ctypes.c_float),
+                ("depth_reject", ctypes.c_float), ("dt", ctypes.c_float), ("flags", ctypes.c_uint32)]
+
+
 class TonemapDescC(ctypes.Structure):
     _fields_ = [("exposure", ctypes.c_float), ("gamma", ctypes.c_float), ("flags", ctypes.c_uint32)]
 LIGHT_CULL_NONE, LIGHT_CULL_TILED, LIGHT_CULL_TILED_DEPTH, LIGHT_CULL_CLUSTERED = 0, 1, 2, 3
@@ -177,6 +186,8 @@ SIGNATURES = [
     ("shs_resolve_ldr", ctypes.c_int, [_P, _P, _P]),
     ("shs_ldr_device_targets", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("shs_tonemap_thresholds", ctypes.c_int, [ctypes.c_float, _F]),
+    ("shs_motion_blur", ctypes.c_int, [_P, ctypes.POINTER(MotionBlurDescC)]),
+    ("shs_resolve_motion_blur", ctypes.c_int, [_P, _P, _P]),
     ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),
     ("shs_model_trs", ctypes.c_int, [_F, ctypes.c_float, _F, _F]),
     ("shs_mat4_mul", ctypes.c_int, [_F, _F, _F]),

@@ -387,3 +387,25 @@ def tonemap_channel(s, exposure, inv_gamma):
     """One channel byte of PassTonemap (exposure / inv_gamma already clamped as the pass does)."""
     tonemap(np.zeros((1, 1, 4), np.float32))   # binds the signatures
     return int(_lib_lib().ora_tonemap_channel(float(s), float(exposure), float(inv_gamma)))
+
+
+def motion_blur(src_ldr, depth, motion, enable=True, samples=10, strength=1.0, max_velocity_px=20.0,
+                min_velocity_px=0.25, depth_reject=0.08, dt=1.0 / 60.0):
+    """PassMotionBlur over an RT_ColorLDR (uint8 [H, W, 4], rows y up) with the depth [H, W] and motion
+    [H, W, 2] planes -> uint8 [H, W, 4] (defaults: MotionBlurPassParams, frame_params.hpp:49-57)."""
+    L = _lib_lib()
+    if not getattr(L, "_mb_ready", False):
+        P = ctypes.c_void_p
+        L.ora_motion_blur.restype = None
+        L.ora_motion_blur.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int] + \
+            [ctypes.c_float] * 5 + [P]
+        L._mb_ready = True
+    src = np.ascontiguousarray(src_ldr, dtype=np.uint8)
+    H, W = src.shape[:2]
+    dep = np.ascontiguousarray(depth, dtype=np.float32)
+    mot = np.ascontiguousarray(motion, dtype=np.float32)
+    out = np.empty_like(src)
+    L.ora_motion_blur(src.ctypes.data, dep.ctypes.data, mot.ctypes.data, W, H, 1 if enable else 0, int(samples),
+                      float(strength), float(max_velocity_px), float(min_velocity_px), float(depth_reject), float(dt),
+                      out.ctypes.data)
+    return out

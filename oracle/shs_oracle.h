@@ -176,6 +176,11 @@ float ora_mat4_determinant(const float *m);
  * hdr W*H*4 floats (rows y up) -> ldr (rows y up) and / or present (rows top-down), W*H*4 bytes. */
 uint8_t ora_tonemap_channel(float s, float exposure, float inv_gamma);
 void ora_tonemap(const float *hdr, int W, int H, float exposure, float gamma, uint8_t *ldr, uint8_t *present);
+/* PassMotionBlur (passes/pass_motion_blur.hpp:38-170): src / dst W*H*4 bytes, depth W*H, motion W*H*2
+ * (all rows y up). */
+void ora_motion_blur(const uint8_t *src, const float *depth, const float *motion, int W, int H, int enable,
+                     int samples, float strength, float max_velocity_px, float min_velocity_px, float depth_reject,
+                     float dt, uint8_t *dst);
 
 #ifdef __cplusplus
 }

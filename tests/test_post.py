@@ -144,3 +144,63 @@ def test_tonemap_follows_new_pass_and_validates(oracle_mod):
         hdr, _, _ = ctx.resolve_lib()
         _, want_pre = oracle_mod.tonemap(hdr, 1.0, 2.2)
         assert np.array_equal(pre, want_pre)
+
+
+# ---- PassMotionBlur ------------------------------------------------------------
+
+def test_oracle_motion_blur_identities(oracle_mod):
+    """No motion (below min_velocity) or enable = 0 leaves the image unchanged; a uniform image with
+    equal depths stays uniform whatever the motion (every tap is accepted)."""
+    rng = np.random.default_rng(5)
+    H, W = 24, 40
+    src = rng.integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+    src[..., 3] = 255
+    depth = rng.uniform(0.2, 0.9, size=(H, W)).astype(np.float32)
+    zero = np.zeros((H, W, 2), np.float32)
+    assert np.array_equal(oracle_mod.motion_blur(src, depth, zero), src)
+    mot = rng.uniform(-30, 30, size=(H, W, 2)).astype(np.float32)
+    assert np.array_equal(oracle_mod.motion_blur(src, depth, mot, enable=False), src)
+    flat = np.full_like(src, 77)
+    flat[..., 3] = 255
+    out = oracle_mod.motion_blur(flat, np.full((H, W), 0.5, np.float32), mot)
+    assert np.array_equal(out, flat)
+
+
+MB_CASES = [dict(), dict(samples=4), dict(samples=32, strength=2.5), dict(dt=1.0 / 30.0, min_velocity_px=0.0),
+            dict(depth_reject=0.002, max_velocity_px=6.0), dict(enable=False), dict(samples=100, strength=-1.0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(len(MB_CASES)))
+def test_motion_blur_exact(oracle_mod, case):
+    import shs_gpu
+    params = MB_CASES[case]
+    frame, draws = _c5(352, 200)
+    with shs_gpu.Context(0) as ctx:
+        ctx.render_pbr_forward(frame, draws)
+        ctx.tonemap(1.0, 2.2, ldr=True, present=False)
+        ctx.motion_blur(**params)
+        got, pre = ctx.resolve_motion_blur()
+        ldr, _ = ctx.resolve_ldr()
+        _, depth, motion = ctx.resolve_lib()
+    assert np.abs(motion).max() > 1.0, "scene has no motion to blur"
+    want = oracle_mod.motion_blur(ldr, depth, motion, **params)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, f"{len(bad)} byte mismatches, first {bad[:4]}"
+    assert np.array_equal(pre, want[::-1])
+    if params.get("enable", True) and params.get("strength", 1.0) > 0:
+        assert not np.array_equal(got, ldr), "blur changed nothing"
+
+
+@pytest.mark.gpu
+def test_motion_blur_requires_inputs():
+    import shs_gpu
+    from shs_gpu import ShsError
+    frame, draws = _c5(96, 64)
+    with shs_gpu.Context(0) as ctx:
+        ctx.render_pbr_forward(frame, draws)
+        with pytest.raises(ShsError):
+            ctx.motion_blur()                         # no tonemap yet
+        ctx.tonemap(ldr=False, present=True)
+        with pytest.raises(ShsError):
+            ctx.motion_blur()                         # the tonemap wrote no RT_ColorLDR

@@ -32,3 +32,26 @@ for flags in ((True, True), (True, False)):
     print(f"tonemap ldr={flags[0]} present={flags[1]}: {ms * 1e3:.1f} us/launch, {by / ms / 1e6:.0f} GB/s "
           f"({by / ms / 1e6 / 8000:.3f} of 8 TB/s), {px / ms / 1e3:.0f} Mpix/s", flush=True)
 ctx.close()
+
+# PassMotionBlur after a tonemap (RT_ColorLDR): default parameters
+ctx = shs_gpu.Context(0)
+ctx.set_stream(stream.cuda_stream)
+ctx.render_pbr_forward(frame, draws)
+ctx.tonemap(1.0, 2.2, ldr=True, present=False)
+for present in (False, True):
+    for _ in range(10):
+        ctx.motion_blur(present=present)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 200
+    a.record()
+    for _ in range(n):
+        ctx.motion_blur(present=present)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / n
+    px = frame.width * frame.height
+    by = px * (4 + 4 + 8 + 4 + 4 * int(present))   # src + depth + motion read, dst (+ present) written
+    print(f"motion blur present={present}: {ms * 1e3:.1f} us/launch, {by / ms / 1e6:.0f} GB/s algorithmic "
+          f"({by / ms / 1e6 / 8000:.3f} of 8 TB/s)", flush=True)
+ctx.close()
