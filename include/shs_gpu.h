@@ -361,6 +361,29 @@ typedef struct shs_motion_blur_desc {
 int shs_motion_blur(shs_ctx *ctx, const shs_motion_blur_desc *desc);
 /* Copy the blurred RT_ColorLDR (rows y up) and / or its present staging (rows top-down). */
 int shs_resolve_motion_blur(shs_ctx *ctx, uint8_t *ldr, uint8_t *present);
+/* ---- software occlusion pass ------------------------------------------------
+ * culling_sw::run_software_occlusion_pass (shs-renderer-lib/include/shs/geometry/culling_software.hpp
+ * :229-331) as scene_culling.hpp:187-219 drives it: the frustum-visible objects in view-depth order
+ * (view z of the world AABB centre), each tested against the occlusion depth with its screen rect
+ * (project_aabb_to_screen_rect + is_rect_occluded) and, when visible, depth-rasterized into it
+ * (rasterize_mesh_depth_transformed).  Synchronous: the visible list feeds the host's draw list. */
+typedef struct shs_occluder {
+    int32_t mesh_id;            /* indexed shs_mesh_upload mesh (DebugMesh vertices + indices) */
+    float model[16];            /* the instance transform (column-major) */
+    float aabb_min[3], aabb_max[3];   /* world AABB (SceneElement::geometry.world_aabb()) */
+} shs_occluder;
+typedef struct shs_occlusion_desc {
+    int32_t width, height;      /* occlusion buffer (OCC_W x OCC_H) */
+    float view[16], view_proj[16];
+    float depth_epsilon;        /* 1e-4 in the reference */
+    int32_t enable;             /* 0: every frustum-visible object is visible */
+} shs_occlusion_desc;
+/* occluded[n_objects] (1 = occluded; 0 for objects not frustum-visible), visible[] in visit order
+ * (capacity n_frustum_visible), *n_visible, depth W*H (y * W + x, may be NULL). */
+int shs_occlusion_pass(shs_ctx *ctx, const shs_occlusion_desc *desc, const shs_occluder *objects, int32_t n_objects,
+                       const uint32_t *frustum_visible, int32_t n_frustum_visible, uint8_t *occluded,
+                       uint32_t *visible, int32_t *n_visible, float *depth);
+
 /* Host-only (no device): the byte thresholds for gamma (thr[0] = 0; +inf where a byte is never
  * reached).  Exposed for the parity tests. */
 int shs_tonemap_thresholds(float gamma, float thr[256]);

@@ -10,6 +10,7 @@
 #include "../../include/shs_gpu.h"
 #include "shs_device.hpp"
 #include "shs_lib_device.hpp"
+#include "shs_occlusion_internal.hpp"
 
 namespace shs_host_detail {
 struct Mesh {
@@ -155,6 +156,10 @@ struct shs_ctx {
     DevBuf<uint32_t> lib_mb, lib_mb_present;
     shs_motion_blur_desc mb_desc{};
     bool have_mb = false;                 // a motion blur follows that tonemap
+    // software occlusion pass (shs_abi_occ.cpp)
+    DevBuf<uint32_t> occ_depth, occ_visible;
+    DevBuf<uint8_t> occ_flags;
+    DevBuf<shs_dev::OccObject> occ_objs;
 };
 
 // Re-enqueues the tonemap after lib_finish re-issued the camera pass (shs_abi_post.cpp).

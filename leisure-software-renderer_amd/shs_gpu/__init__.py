@@ -258,6 +258,36 @@ class Context:
                                                       None if pre is None else pre.ctypes.data_as(ctypes.c_void_p)))
         return ldr, pre
 
+    def occlusion_pass(self, width, height, view, view_proj, objects, frustum_visible, depth_epsilon=1e-4,
+                       enable=True):
+        """culling_sw::run_software_occlusion_pass (culling_software.hpp:229-331).  objects: sequence of
+        (LibMesh with indices, model float[16], aabb_min[3], aabb_max[3]) -> (occluded uint8 [n],
+        visible uint32 [k] in visit order, depth float32 [height, width])."""
+        n = len(objects)
+        arr = (_abi.OccluderC * max(n, 1))()
+        for i, (mesh, model, mn, mx) in enumerate(objects):
+            a = arr[i]
+            a.mesh_id = self.upload_lib_mesh(mesh)
+            for k in range(16):
+                a.model[k] = float(model[k])
+            for k in range(3):
+                a.aabb_min[k], a.aabb_max[k] = float(mn[k]), float(mx[k])
+        d = _abi.OcclusionDescC()
+        d.width, d.height = int(width), int(height)
+        for k in range(16):
+            d.view[k], d.view_proj[k] = float(view[k]), float(view_proj[k])
+        d.depth_epsilon, d.enable = float(depth_epsilon), 1 if enable else 0
+        fv = np.ascontiguousarray(frustum_visible, dtype=np.uint32)
+        occ = np.zeros(max(n, 1), np.uint8)
+        vis = np.zeros(max(fv.size, 1), np.uint32)
+        nv = ctypes.c_int32()
+        depth = np.zeros((height, width), np.float32)
+        self._check(self._lib.shs_occlusion_pass(self._h, ctypes.byref(d), arr, n, fv.ctypes.data_as(ctypes.c_void_p),
+                                                 fv.size, occ.ctypes.data_as(ctypes.c_void_p),
+                                                 vis.ctypes.data_as(ctypes.c_void_p), ctypes.byref(nv),
+                                                 depth.ctypes.data_as(ctypes.c_void_p)))
+        return occ[:n], vis[:nv.value], depth
+
     def lib_device_targets(self):
         """Device pointers of the library targets: (hdr float4 W*H, depth W*H, motion float2 W*H)."""
         a, b, c = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()

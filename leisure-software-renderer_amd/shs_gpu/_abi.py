@@ -134,6 +134,15 @@ class MotionBlurDescC(ctypes.Structure):
                 ("depth_reject", ctypes.c_float), ("dt", ctypes.c_float), ("flags", ctypes.c_uint32)]
 
 
+class OccluderC(ctypes.Structure):
+    _fields_ = [("mesh_id", ctypes.c_int32), ("model", _F16), ("aabb_min", _F3), ("aabb_max", _F3)]
+
+
+class OcclusionDescC(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("view", _F16), ("view_proj", _F16),
+                ("depth_epsilon", ctypes.c_float), ("enable", ctypes.c_int32)]
+
+
 class TonemapDescC(ctypes.Structure):
     _fields_ = [("exposure", ctypes.c_float), ("gamma", ctypes.c_float), ("flags", ctypes.c_uint32)]
 LIGHT_CULL_NONE, LIGHT_CULL_TILED, LIGHT_CULL_TILED_DEPTH, LIGHT_CULL_CLUSTERED = 0, 1, 2, 3
@@ -186,6 +195,8 @@ SIGNATURES = [
     ("shs_resolve_ldr", ctypes.c_int, [_P, _P, _P]),
     ("shs_ldr_device_targets", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("shs_tonemap_thresholds", ctypes.c_int, [ctypes.c_float, _F]),
+    ("shs_occlusion_pass", ctypes.c_int, [_P, ctypes.POINTER(OcclusionDescC), ctypes.POINTER(OccluderC), ctypes.c_int32,
+                                          _P, ctypes.c_int32, _P, _P, ctypes.POINTER(ctypes.c_int32), _P]),
     ("shs_motion_blur", ctypes.c_int, [_P, ctypes.POINTER(MotionBlurDescC)]),
     ("shs_resolve_motion_blur", ctypes.c_int, [_P, _P, _P]),
     ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),

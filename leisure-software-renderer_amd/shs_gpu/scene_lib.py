@@ -170,3 +170,59 @@ def c4_scene(width=3840, height=2160, n_objects=1000, tris_per_object=1000, n_dr
     frame = LibFrame(width, height, depth_motion=True, zn=zn, zf=zf, bg_gradient=True)
     cull = LightCull(width, height, view, proj, zn=zn, zf=zf, tile_size=tile_size, max_per_tile=max_per_tile, mode=mode)
     return frame, draws, c4_lights(n_lights), cull
+
+
+# ---- software occlusion scene (hello_occlusion_culling_sw.cpp lineage) --------
+
+def box_mesh(hx=0.5, hy=0.5, hz=0.5) -> LibMesh:
+    """An indexed box (8 corners, 12 triangles), a DebugMesh like the Jolt box shape's."""
+    p = np.array([[sx * hx, sy * hy, sz * hz] for sz in (-1, 1) for sy in (-1, 1) for sx in (-1, 1)], np.float32)
+    q = [(0, 1, 3, 2), (4, 6, 7, 5), (0, 4, 5, 1), (2, 3, 7, 6), (0, 2, 6, 4), (1, 5, 7, 3)]
+    idx = np.array([[a, b, c, a, c, d] for a, b, c, d in q], np.uint32).reshape(-1)
+    return LibMesh(positions=p, indices=idx)
+
+
+def sphere_mesh(r=0.5, seg=12, rings=8) -> LibMesh:
+    v = []
+    for i in range(rings + 1):
+        th = np.pi * i / rings
+        for j in range(seg):
+            ph = 2.0 * np.pi * j / seg
+            v.append((r * np.sin(th) * np.cos(ph), r * np.cos(th), r * np.sin(th) * np.sin(ph)))
+    idx = []
+    for i in range(rings):
+        for j in range(seg):
+            a, b = i * seg + j, i * seg + (j + 1) % seg
+            c, d = a + seg, b + seg
+            idx += [a, c, b, b, c, d]
+    return LibMesh(positions=np.array(v, np.float32), indices=np.array(idx, np.uint32))
+
+
+def world_aabb(mesh, model):
+    m = np.asarray(model, np.float32).reshape(4, 4).T   # column-major storage -> row-major matrix
+    p = np.c_[mesh.positions, np.ones(len(mesh.positions), np.float32)] @ m.T
+    return p[:, :3].min(0).astype(np.float32), p[:, :3].max(0).astype(np.float32)
+
+
+def occlusion_scene(n_objects=300, seed=7, width=300, height=225, walls=3):
+    """-> (objects [(mesh, model, aabb_min, aabb_max)], view, view_proj, width, height).  Random boxes
+    and spheres on a field, a few wide walls close to the camera occluding part of it, some objects
+    behind the camera (their corners fail the clip.w test)."""
+    rng = np.random.default_rng(seed)
+    box, sph = box_mesh(), sphere_mesh()
+    objs = []
+    for i in range(n_objects):
+        pos = (f32(rng.uniform(-30, 30)), f32(rng.uniform(0.0, 3.0)), f32(rng.uniform(-8, 70)))
+        rot = tuple(f32(a) for a in rng.uniform(-np.pi, np.pi, 3))
+        s = f32(rng.uniform(0.5, 3.0))
+        model = model_euler(pos, rot, (s, s, s))
+        mesh = box if i % 2 == 0 else sph
+        mn, mx = world_aabb(mesh, model)
+        objs.append((mesh, model, mn, mx))
+    for w in range(walls):
+        model = model_euler((f32(-12.0 + 12.0 * w), f32(2.0), f32(8.0 + 3.0 * w)), (0.0, 0.0, 0.0), (f32(7.0), f32(6.0), f32(0.5)))
+        mn, mx = world_aabb(box, model)
+        objs.append((box, model, mn, mx))
+    view = look_at_lh((0.0, 3.0, -4.0), (0.0, 2.0, 30.0))
+    proj = perspective_lh_no(f32(np.deg2rad(60.0)), f32(width) / f32(height), f32(0.1), f32(1000.0))
+    return objs, view, mat_mul(proj, view), width, height

@@ -409,3 +409,42 @@ def motion_blur(src_ldr, depth, motion, enable=True, samples=10, strength=1.0, m
                       float(strength), float(max_velocity_px), float(min_velocity_px), float(depth_reject), float(dt),
                       out.ctypes.data)
     return out
+
+
+class OraOccObject(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_void_p), ("n_verts", ctypes.c_int32), ("idx", ctypes.c_void_p), ("n_idx", ctypes.c_int32),
+                ("model", _F16), ("aabb_min", ctypes.c_float * 3), ("aabb_max", ctypes.c_float * 3)]
+
+
+def occlusion_pass(width, height, view, view_proj, objects, frustum_visible, depth_epsilon=1e-4, enable=True):
+    """culling_sw::run_software_occlusion_pass restated -> (occluded uint8 [n], visible uint32 [k], depth)."""
+    L = _lib_lib()
+    if not getattr(L, "_occ_ready", False):
+        P = ctypes.c_void_p
+        L.ora_occlusion_pass.restype = ctypes.c_int
+        L.ora_occlusion_pass.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                         P, P, ctypes.c_float, P, P]
+        L._occ_ready = True
+    n = len(objects)
+    arr = (OraOccObject * max(n, 1))()
+    keep = []
+    for i, (mesh, model, mn, mx) in enumerate(objects):
+        pos = np.ascontiguousarray(mesh.positions, dtype=np.float32)
+        idx = np.ascontiguousarray(mesh.indices, dtype=np.uint32)
+        keep += [pos, idx]
+        a = arr[i]
+        a.pos, a.n_verts, a.idx, a.n_idx = pos.ctypes.data, pos.shape[0], idx.ctypes.data, idx.size
+        for k in range(16):
+            a.model[k] = float(model[k])
+        for k in range(3):
+            a.aabb_min[k], a.aabb_max[k] = float(mn[k]), float(mx[k])
+    fv = np.ascontiguousarray(frustum_visible, dtype=np.uint32)
+    v16 = np.ascontiguousarray(view, dtype=np.float32)
+    vp16 = np.ascontiguousarray(view_proj, dtype=np.float32)
+    depth = np.ones((height, width), np.float32)
+    occ = np.zeros(max(n, 1), np.uint8)
+    vis = np.zeros(max(fv.size, 1), np.uint32)
+    nv = L.ora_occlusion_pass(ctypes.addressof(arr), n, fv.ctypes.data, fv.size, 1 if enable else 0, depth.ctypes.data,
+                              width, height, v16.ctypes.data, vp16.ctypes.data, float(depth_epsilon), occ.ctypes.data,
+                              vis.ctypes.data)
+    return occ[:n], vis[:nv], depth

@@ -182,6 +182,22 @@ void ora_motion_blur(const uint8_t *src, const float *depth, const float *motion
                      int samples, float strength, float max_velocity_px, float min_velocity_px, float depth_reject,
                      float dt, uint8_t *dst);
 
+/* culling_sw::run_software_occlusion_pass (geometry/culling_software.hpp:229-331) as scene_culling.hpp
+ * :187-219 drives it.  One object: an indexed DebugMesh (positions xyz, indices) + model + world AABB.
+ * Writes occluded[n_objects] (0 for objects not frustum-visible), visible_out (sorted visit order),
+ * depth W*H (rows as the reference indexes them: y * W + x); returns the visible count. */
+typedef struct ora_occ_object {
+    const float *pos;
+    int32_t n_verts;
+    const uint32_t *idx;
+    int32_t n_idx;
+    float model[16];
+    float aabb_min[3], aabb_max[3];
+} ora_occ_object;
+int ora_occlusion_pass(const ora_occ_object *objs, int n_objects, const uint32_t *frustum_visible, int n_fv, int enable,
+                       float *depth, int W, int H, const float *view16, const float *vp16, float eps,
+                       uint8_t *occluded, uint32_t *visible_out);
+
 #ifdef __cplusplus
 }
 #endif
