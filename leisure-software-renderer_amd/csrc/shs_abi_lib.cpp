@@ -315,7 +315,7 @@ void shs_lib_release(shs_ctx *ctx) {
     release(ctx->lights); release(ctx->light_proj); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
     release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
-    release(ctx->occ_depth); release(ctx->occ_visible); release(ctx->occ_flags); release(ctx->occ_objs);
+    release(ctx->occ_depth); release(ctx->occ_visible); release(ctx->occ_flags); release(ctx->occ_objs); release(ctx->occ_rects); release(ctx->occ_tris);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
 }

@@ -2,6 +2,7 @@
 // culling_sw::run_software_occlusion_pass (shs-renderer-lib/include/shs/geometry/culling_software.hpp
 // :229-331) as SceneCullingContext::run_software_occlusion drives it (scene/scene_culling.hpp:187-219).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -26,7 +27,10 @@ extern "C" int shs_occlusion_pass(shs_ctx *ctx, const shs_occlusion_desc *desc, 
     if (!ctx || !desc || (n_objects > 0 && !objects) || (n_frustum_visible > 0 && !frustum_visible) || !occluded ||
         !visible || !n_visible || n_objects < 0 || n_frustum_visible < 0)
         return SHS_ERR_INVALID;
-    if (desc->width <= 0 || desc->height <= 0) { ctx->err = "occlusion buffer size"; return SHS_ERR_INVALID; }
+    if (desc->width <= 0 || desc->height <= 0 || desc->width > 65535 || desc->height > 65535) {
+        ctx->err = "occlusion buffer size: 1 .. 65535 per side";
+        return SHS_ERR_INVALID;
+    }
     std::memset(occluded, 0, (size_t)n_objects);
     // the frustum-visible objects, sorted by view depth (std::sort's strict '<'; equal keys keep the
     // input order here), out-of-range indices dropped as the reference's comparator pushes them last
@@ -43,6 +47,7 @@ extern "C" int shs_occlusion_pass(shs_ctx *ctx, const shs_occlusion_desc *desc, 
     for (uint32_t idx : order) key[idx] = aabb_center_view_z(objects[idx], desc->view);
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
     std::vector<shs_dev::OccObject> objs(order.size());
+    size_t n_tris_total = 0;
     for (size_t s = 0; s < order.size(); ++s) {
         const shs_occluder &o = objects[order[s]];
         if (o.mesh_id < 0 || o.mesh_id >= (int)ctx->meshes.size() || !ctx->meshes[o.mesh_id].live ||
@@ -57,6 +62,8 @@ extern "C" int shs_occlusion_pass(shs_ctx *ctx, const shs_occlusion_desc *desc, 
         d.n_verts = m.n_verts;
         d.n_idx = m.n_tris * 3;
         d.index = order[s];
+        d.tri_base = (uint32_t)n_tris_total;
+        n_tris_total += (size_t)m.n_tris;
         std::memcpy(d.model, o.model, sizeof d.model);
         std::memcpy(d.aabb_min, o.aabb_min, sizeof d.aabb_min);
         std::memcpy(d.aabb_max, o.aabb_max, sizeof d.aabb_max);
@@ -65,23 +72,29 @@ extern "C" int shs_occlusion_pass(shs_ctx *ctx, const shs_occlusion_desc *desc, 
     const size_t npx = (size_t)desc->width * desc->height;
     if (ensure(ctx, ctx->occ_depth, npx) || ensure(ctx, ctx->occ_objs, std::max<size_t>(objs.size(), 1)) ||
         ensure(ctx, ctx->occ_flags, std::max<size_t>((size_t)n_objects, 1)) ||
-        ensure(ctx, ctx->occ_visible, std::max<size_t>(order.size(), 1) + 1))
+        ensure(ctx, ctx->occ_visible, std::max<size_t>(order.size(), 1) + 1) ||
+        ensure(ctx, ctx->occ_rects, objs.size() + 2) || ensure(ctx, ctx->occ_tris, std::max<size_t>(n_tris_total, 1)))
         return SHS_ERR_HIP;
     if (!objs.empty())
         HIP_TRY(ctx, hipMemcpyAsync(ctx->occ_objs.p, objs.data(), objs.size() * sizeof(shs_dev::OccObject),
                                     hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->occ_rects.p + objs.size(), 0, 2 * sizeof(shs_dev::OccRect), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->occ_flags.p, 0, std::max<size_t>((size_t)n_objects, 1), ctx->stream));
     shs_dev::OccParams p{};
     p.objs = ctx->occ_objs.p;
+    p.rects = ctx->occ_rects.p;
+    p.tris = ctx->occ_tris.p;
     p.n = (int32_t)objs.size();
     p.W = desc->width;
     p.H = desc->height;
     std::memcpy(p.vp, desc->view_proj, sizeof p.vp);
     p.eps = desc->depth_epsilon;
+    p.chunk = (int32_t)std::min<uint64_t>(1024, 0xffffffffull / npx);
     p.depth = ctx->occ_depth.p;
     p.occluded = ctx->occ_flags.p;
     p.visible = ctx->occ_visible.p + 1;
     p.n_visible = ctx->occ_visible.p;
+    p.prof = std::getenv("SHS_OCC_PROF") != nullptr;
     HIP_TRY(ctx, shs_internal::launch_occlusion(p, ctx->stream));
     std::vector<uint32_t> vis(order.size() + 1);
     HIP_TRY(ctx, hipMemcpyAsync(vis.data(), ctx->occ_visible.p, vis.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));

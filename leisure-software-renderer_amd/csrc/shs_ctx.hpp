@@ -160,6 +160,8 @@ struct shs_ctx {
     DevBuf<uint32_t> occ_depth, occ_visible;
     DevBuf<uint8_t> occ_flags;
     DevBuf<shs_dev::OccObject> occ_objs;
+    DevBuf<shs_dev::OccRect> occ_rects;
+    DevBuf<shs_dev::OccTri> occ_tris;
 };
 
 // Re-enqueues the tonemap after lib_finish re-issued the camera pass (shs_abi_post.cpp).

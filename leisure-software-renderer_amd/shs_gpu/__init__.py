@@ -264,14 +264,13 @@ class Context:
         (LibMesh with indices, model float[16], aabb_min[3], aabb_max[3]) -> (occluded uint8 [n],
         visible uint32 [k] in visit order, depth float32 [height, width])."""
         n = len(objects)
-        arr = (_abi.OccluderC * max(n, 1))()
-        for i, (mesh, model, mn, mx) in enumerate(objects):
-            a = arr[i]
-            a.mesh_id = self.upload_lib_mesh(mesh)
-            for k in range(16):
-                a.model[k] = float(model[k])
-            for k in range(3):
-                a.aabb_min[k], a.aabb_max[k] = float(mn[k]), float(mx[k])
+        # shs_occluder records (int32 mesh_id, float model[16], aabb_min[3], aabb_max[3]) built in numpy
+        arr = np.zeros((max(n, 1), ctypes.sizeof(_abi.OccluderC) // 4), np.float32)
+        if n:
+            arr[:n, 0].view(np.int32)[:] = [self.upload_lib_mesh(o[0]) for o in objects]
+            arr[:n, 1:17] = np.asarray([o[1] for o in objects], np.float32).reshape(n, 16)
+            arr[:n, 17:20] = np.asarray([o[2] for o in objects], np.float32).reshape(n, 3)
+            arr[:n, 20:23] = np.asarray([o[3] for o in objects], np.float32).reshape(n, 3)
         d = _abi.OcclusionDescC()
         d.width, d.height = int(width), int(height)
         for k in range(16):
@@ -282,7 +281,8 @@ class Context:
         vis = np.zeros(max(fv.size, 1), np.uint32)
         nv = ctypes.c_int32()
         depth = np.zeros((height, width), np.float32)
-        self._check(self._lib.shs_occlusion_pass(self._h, ctypes.byref(d), arr, n, fv.ctypes.data_as(ctypes.c_void_p),
+        self._check(self._lib.shs_occlusion_pass(self._h, ctypes.byref(d), arr.ctypes.data_as(ctypes.POINTER(_abi.OccluderC)), n,
+                                                 fv.ctypes.data_as(ctypes.c_void_p),
                                                  fv.size, occ.ctypes.data_as(ctypes.c_void_p),
                                                  vis.ctypes.data_as(ctypes.c_void_p), ctypes.byref(nv),
                                                  depth.ctypes.data_as(ctypes.c_void_p)))

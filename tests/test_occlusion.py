@@ -37,12 +37,13 @@ def test_occlusion_pass_exact(oracle_mod, seed, n, eps):
     assert np.array_equal(got[0], want[0]), f"occluded flags differ at {np.nonzero(got[0] != want[0])[0][:8]}"
     assert np.array_equal(got[1], want[1])
     assert np.array_equal(got[2].view(np.uint32), want[2].view(np.uint32))
-    assert 0 < want[0].sum() < len(objs)
+    if eps <= 1e-4:   # a coarse epsilon keeps every object visible (z_near <= depth + eps everywhere)
+        assert 0 < want[0].sum() < len(objs)
 
 
 @pytest.mark.gpu
 def test_occlusion_pass_large_buffer_and_disabled(oracle_mod):
-    """A 4x larger buffer (1200x900, beyond the reference demo's 300x225) and enable = 0."""
+    """A 4x larger buffer (1200x900, beyond the reference demo's 300x225), enable = 0, a side over 65535."""
     import shs_gpu
     objs, view, vp, _, _ = _scene(n_objects=200, seed=19, width=1200, height=900)
     fv = np.arange(len(objs), dtype=np.uint32)
@@ -53,3 +54,5 @@ def test_occlusion_pass_large_buffer_and_disabled(oracle_mod):
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
     assert np.array_equal(got[2].view(np.uint32), want[2].view(np.uint32))
     assert off[0].sum() == 0 and np.array_equal(off[1], fv)
+    with shs_gpu.Context(0) as ctx, pytest.raises(shs_gpu.ShsError):
+        ctx.occlusion_pass(65536, 2, view, vp, objs, fv)   # sides are limited to 16 bits
