@@ -77,6 +77,7 @@ int shs_destroy(shs_ctx *ctx) {
     shs_lib_release(ctx);
     release(ctx->draws); release(ctx->recs); release(ctx->shade); release(ctx->tile_count); release(ctx->bins);
     release(ctx->spill); release(ctx->frags); release(ctx->counters); release(ctx->busy); release(ctx->boxes);
+    release(ctx->slivers);
     release(ctx->blk_stat); release(ctx->rstat); release(ctx->timeline);
     release(ctx->color); release(ctx->depth); release(ctx->prequant);
     for (int i = 0; i < 2; ++i) {
@@ -203,7 +204,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     const int n_tris = (int)total;
 
     if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1)) || ensure(ctx, ctx->shade, (size_t)std::max(n_tris, 1)) ||
-        ensure(ctx, ctx->boxes, (size_t)std::max(n_tris, 1)))
+        ensure(ctx, ctx->boxes, (size_t)std::max(n_tris, 1)) || ensure(ctx, ctx->slivers, (size_t)std::max(n_tris, 1)))
         return SHS_ERR_HIP;
     // Bin counts (2 parity sets) and busy flags are kept zero by the kernels themselves (k_setup's
     // clear blocks zero the next frame's counts, k_raster resets the flags it consumed); they are
@@ -286,16 +287,22 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ctx->spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ctx->frags.cap, 0xffffffffu);
-    {   // ~4K ghost waves per frame: small scenes split each sliver group over many waves
+    {   // ~1K ghost waves per frame: small scenes split each sliver group over a few waves.  Measured
+        // at C2 (61 groups, ~17 unbounded slivers): 4K waves 8.9 us setup, 2K 7.7, 1K 7.3, 512 8.1,
+        // 256 9.3 -- past ~1K the extra workgroup launches cost more than the shorter enumerations save.
         const int n_groups = std::max(1, (n_tris + 15) / 16);
-        fp.ghost_slices = (uint32_t)std::min(64, std::max(1, 4096 / n_groups));
+        fp.ghost_slices = (uint32_t)std::min(16, std::max(1, 1024 / n_groups));
     }
     fp.parity = ctx->frame_index & 1u;
     fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;
     fp.setup_blocks = setup_blocks;
-    fp.ghost_blocks = (n_groups * (int)fp.ghost_slices + 3) / 4;
+    // Binned (large) scenes list their unbounded slivers in k_setup and enumerate them in k_ghost:
+    // ghost waves would recompute every triangle's record (C3: ~1/3 of k_setup's time).  Scan-mode
+    // scenes keep the ghost waves inside k_setup (one launch fewer on a latency-bound frame).
+    fp.ghost_list = fp.scan_mode ? 0u : 1u;
+    fp.ghost_blocks = fp.ghost_list ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
     fp.clear_blocks = 0;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / shs_dev::RTH);
     // persistent raster grid: one resident wave of workgroups (k_raster runs 4 per CU)
@@ -311,6 +318,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     FrameBuffers fb;
     fb.draws = ctx->draws.p; fb.recs = ctx->recs.p; fb.shade = ctx->shade.p; fb.tile_count = ctx->tile_count.p; fb.bins = ctx->bins.p;
     fb.spill = ctx->spill.p; fb.frags = ctx->frags.p; fb.counters = ctx->counters.p;
+    fb.slivers = ctx->slivers.p;
     fb.busy = ctx->busy.p;
     fb.blk_stat = ctx->blk_stat.p;
     fb.rstat = ctx->rstat.p;
@@ -328,9 +336,10 @@ static int enqueue_frame(shs_ctx *ctx) {
         ev = ctx->ring_ev[k];
         ctx->ring_pending[k] = true;
     }
-    // kernel durations: [0] k_setup, [1] [2] (unused), [3] k_raster
+    // kernel durations: [0] k_setup (+ k_ghost in ghost_list mode), [1] [2] (unused), [3] k_raster
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], st));
     HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, ka, st));
+    if (fp.ghost_list && !(fp.flags & shs_dev::DBG_SKIP_GHOST)) HIP_TRY(ctx, shs_internal::launch_ghost(fp, fb, st));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], st));
     HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, ka, raster_grid, st));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));

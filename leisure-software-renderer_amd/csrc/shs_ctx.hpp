@@ -49,6 +49,7 @@ struct shs_ctx {
     DevBuf<uint32_t> bins;           // n_tiles * bin_cap
     DevBuf<uint2> spill;
     DevBuf<shs_dev::GhostFrag> frags; // ghost fragments
+    DevBuf<uint32_t> slivers;        // unbounded sliver ids (ghost_list mode)
     DevBuf<uint2> boxes;             // per-triangle bin boxes
     DevBuf<uint32_t> counters;       // 2 parity sets
     DevBuf<uint32_t> busy;           // per raster tile

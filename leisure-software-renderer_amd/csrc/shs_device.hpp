@@ -83,14 +83,14 @@ constexpr double GHOST_MAX_EXPAND = 48.0;  // larger danger boxes are handled as
 
 // counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one).
 // Only the append positions and the overflow flags live here; statistics go to per-block slots.
-constexpr int C_OVERFLOW = 0, C_SPILL = 1, C_FRAG = 2, C_NCOUNTERS = 4;
+constexpr int C_OVERFLOW = 0, C_SPILL = 1, C_FRAG = 2, C_SLIVER = 3, C_NCOUNTERS = 4;
 constexpr uint32_t OV_SPILL = 1u, OV_FRAG = 2u;
 
 // Timing-experiment switches (frame flags bits 8+; results are WRONG with any of them set): they
 // let bench --debug-flags attribute kernel time to phases.  Never set by the product path.
 constexpr uint32_t DBG_SKIP_GHOST = 1u << 8, DBG_SKIP_SHADE = 1u << 9, DBG_CLEAR_ONLY = 1u << 10,
                    DBG_SKIP_BIN = 1u << 11, DBG_SKIP_CLEAR = 1u << 12,
-                   DBG_TWICE = 1u << 13;
+                   DBG_TWICE = 1u << 13, DBG_SKIP_PAIRS = 1u << 14;
 // Raster inner loop (frame flags bit 16, set by the context from SHS_OPT_RASTER_LOOP): per-pixel
 // candidate loop instead of (candidate, pixel) pair tasks.  Results are identical either way.
 constexpr uint32_t RF_PER_PIXEL = 1u << 16;
@@ -125,6 +125,8 @@ struct FrameParams {
     uint32_t ghost_slices;           // ghost waves per GHOST_GROUP triangles (k_setup)
     uint32_t parity;                 // counter / bin-count set used by this frame
     uint32_t scan_mode;              // 1: no bins, busy raster tiles scan all bin boxes (small scenes)
+    uint32_t ghost_list;             // 1: k_setup lists the unbounded slivers, k_ghost enumerates them
+                                     // (binned scenes); 0: k_setup's ghost waves (scan-mode scenes)
     int32_t setup_blocks, ghost_blocks, clear_blocks;   // k_setup block roles, in this order (no
                                                         // clear blocks: k_raster clears)
     int32_t n_owned_rt;              // raster tiles of the owned bin tiles (4 per bin tile)
@@ -139,6 +141,7 @@ struct FrameBuffers {
     uint32_t *bins;                  // n_bin_tiles * bin_cap
     uint2 *spill;                    // (bin tile, tri) pairs beyond bin_cap
     GhostFrag *frags;                // tile-clamp pixels of unbounded slivers that pass (frag_cap)
+    uint32_t *slivers;               // n_tris: unbounded slivers' ids (ghost_list mode, C_SLIVER entries)
     uint2 *boxes;                    // n_tris: packed bin box (gbx, gby); empty for culled
     uint32_t *counters;              // 2 * C_NCOUNTERS
     uint32_t *busy;                  // per raster tile: 1 = has candidates / fragments (k_raster resets)

@@ -7,6 +7,7 @@
 namespace shs_internal {
 hipError_t launch_setup(const shs_dev::FrameParams &fp, const shs_dev::FrameBuffers &fb, const shs_dev::KArgDraws &ka,
                         hipStream_t s);
+hipError_t launch_ghost(const shs_dev::FrameParams &fp, const shs_dev::FrameBuffers &fb, hipStream_t s);
 hipError_t launch_raster(const shs_dev::FrameParams &fp, const shs_dev::FrameBuffers &fb, const shs_dev::KArgDraws &ka,
                          int grid, hipStream_t s);
 }  // namespace shs_internal

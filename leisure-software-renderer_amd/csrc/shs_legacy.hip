@@ -337,6 +337,73 @@ __device__ __forceinline__ TriRec quad_record(const FrameParams &fp, const DrawG
     return r;
 }
 
+// q = n / d, r = n % d for 0 <= n < 2^24, 1 <= d < 2^24 (rd = 1.0f / d): the float quotient is
+// within 1 of the exact one, fixed up by the remainder.
+__device__ __forceinline__ void div_small(int n, int d, float rd, int &q, int &r) {
+    q = (int)((float)n * rd);
+    r = n - q * d;
+    if (r < 0) { --q; r += d; }
+    if (r >= d) { ++q; r -= d; }
+}
+
+// Every pixel sliver `tri` (record t) visits outside its ibox in the reference's tile jobs, the
+// slice-th 64-pixel batch of every `stride`: passing ones become ghost fragments.  Wave-uniform
+// arguments, converged wave.
+__device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, const TriRec &t,
+                                              uint32_t tri, int slice, int stride) {
+    const int lane = __lane_id();
+    const int ix0 = lo16(t.ibx), ix1 = hi16(t.ibx), iy0 = lo16(t.iby), iy1 = hi16(t.iby);
+    SliverSpan sp;
+    classify_axis(fp.rt_x, fp.rtw, fp.W, t.fminx, t.fmaxx, sp.cl, sp.cr, sp.xi0, sp.xi1);
+    classify_axis(fp.rt_y, fp.rth, fp.H, t.fminy, t.fmaxy, sp.ru, sp.rd, sp.yi0, sp.yi1);
+    const int nxo = sp.cl + sp.cr, nyo = sp.ru + sp.rd;
+    const int nxi = max(sp.xi1 - sp.xi0 + 1, 0), nyi = max(sp.yi1 - sp.yi0 + 1, 0);
+    const int ny = nyo + nyi;
+    // total <= W * H (< 2^24 px): 32-bit indices, divisions by reciprocal with a +-1 fix
+    const int total_a = nxo * ny, total = total_a + nxi * nyo;
+    const float rny = 1.0f / (float)max(ny, 1), rnyo = 1.0f / (float)max(nyo, 1);
+    for (int kb = slice * 64; kb < total; kb += stride) {
+        const int k = kb + lane;
+        bool pass = false;
+        int px = 0, py = 0;
+        float z = 0.f, u = 0.f, v = 0.f, w = 0.f;
+        if (k < total) {
+            if (k < total_a) {
+                int xi, yi;
+                div_small(k, ny, rny, xi, yi);
+                px = edge_coord(xi, sp.cl, fp.rt_x, sp.cr, fp.rtw, fp.W);
+                py = yi < nyo ? edge_coord(yi, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H) : sp.yi0 + (yi - nyo);
+            } else {
+                int xi, yi;
+                div_small(k - total_a, nyo, rnyo, xi, yi);
+                px = sp.xi0 + xi;
+                py = edge_coord(yi, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H);
+            }
+            const bool in_ibox = px >= ix0 && px <= ix1 && py >= iy0 && py <= iy1;   // k_raster's part
+            if (!in_ibox && (fp.count == 1 || owned_bin_tile(fp, px / TILE, py / TILE)) && bary_pass(t, (float)px + 0.5f, (float)py + 0.5f, u, v, w)) {
+                z = (u * t.z0 + v * t.z1) + w * t.z2;
+                pass = z < FLT_MAX;   // NaN / FLT_MAX never pass the strict z test
+            }
+        }
+        const uint32_t slot = wave_append1(&cnt[C_FRAG], pass);
+        if (pass) {
+            if (slot < fp.frag_cap) {
+                GhostFrag g;
+                g.xy = (uint32_t)px | ((uint32_t)py << 16);
+                g.z = z;
+                g.id = tri;
+                g.v = v;
+                g.w = w;
+                g.pad[0] = g.pad[1] = g.pad[2] = 0u;
+                fb.frags[slot] = g;
+                fb.busy[(py / RTH) * fp.tiles_x + px / RTW] = 1u;
+            } else {
+                atomicOr(&cnt[C_OVERFLOW], OV_FRAG);
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
                                            uint32_t *cnt, int group, int slice, GhostScratch &gs) {
     const int lane = __lane_id();
@@ -357,53 +424,7 @@ __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuf
         wave_lds_sync();
         const TriRec t = rec_from(gs.rec);
         wave_lds_sync();   // gs.rec is rewritten by the next sliver
-        const uint32_t tri = (uint32_t)(group * GHOST_GROUP + (src >> 2));
-        const int ix0 = lo16(t.ibx), ix1 = hi16(t.ibx), iy0 = lo16(t.iby), iy1 = hi16(t.iby);
-        SliverSpan sp;
-        classify_axis(fp.rt_x, fp.rtw, fp.W, t.fminx, t.fmaxx, sp.cl, sp.cr, sp.xi0, sp.xi1);
-        classify_axis(fp.rt_y, fp.rth, fp.H, t.fminy, t.fmaxy, sp.ru, sp.rd, sp.yi0, sp.yi1);
-        const int nxo = sp.cl + sp.cr, nyo = sp.ru + sp.rd;
-        const int nxi = max(sp.xi1 - sp.xi0 + 1, 0), nyi = max(sp.yi1 - sp.yi0 + 1, 0);
-        const int ny = nyo + nyi;
-        const int64_t total_a = (int64_t)nxo * ny, total = total_a + (int64_t)nxi * nyo;
-        for (int64_t kb = (int64_t)slice * 64; kb < total; kb += stride) {
-            const int64_t k = kb + lane;
-            bool pass = false;
-            int px = 0, py = 0;
-            float z = 0.f, u = 0.f, v = 0.f, w = 0.f;
-            if (k < total) {
-                if (k < total_a) {
-                    const int xi = (int)(k / ny), yi = (int)(k % ny);
-                    px = edge_coord(xi, sp.cl, fp.rt_x, sp.cr, fp.rtw, fp.W);
-                    py = yi < nyo ? edge_coord(yi, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H) : sp.yi0 + (yi - nyo);
-                } else {
-                    const int64_t kk = k - total_a;
-                    px = sp.xi0 + (int)(kk / nyo);
-                    py = edge_coord((int)(kk % nyo), sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H);
-                }
-                const bool in_ibox = px >= ix0 && px <= ix1 && py >= iy0 && py <= iy1;   // k_raster's part
-                if (!in_ibox && owned_bin_tile(fp, px / TILE, py / TILE) && bary_pass(t, (float)px + 0.5f, (float)py + 0.5f, u, v, w)) {
-                    z = (u * t.z0 + v * t.z1) + w * t.z2;
-                    pass = z < FLT_MAX;   // NaN / FLT_MAX never pass the strict z test
-                }
-            }
-            const uint32_t slot = wave_append1(&cnt[C_FRAG], pass);
-            if (pass) {
-                if (slot < fp.frag_cap) {
-                    GhostFrag g;
-                    g.xy = (uint32_t)px | ((uint32_t)py << 16);
-                    g.z = z;
-                    g.id = tri;
-                    g.v = v;
-                    g.w = w;
-                    g.pad[0] = g.pad[1] = g.pad[2] = 0u;
-                    fb.frags[slot] = g;
-                    fb.busy[(py / RTH) * fp.tiles_x + px / RTW] = 1u;
-                } else {
-                    atomicOr(&cnt[C_OVERFLOW], OV_FRAG);
-                }
-            }
-        }
+        sliver_pixels(fp, fb, cnt, t, (uint32_t)(group * GHOST_GROUP + (src >> 2)), slice, stride);
     }
 }
 
@@ -606,6 +627,11 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
 
     // -- per-block statistics (no same-address global atomics); one lane per quad counts
     const bool lead = qt.valid && q == 0 && !(flags & TRI_CULLED);
+    if (fp.ghost_list) {   // the unbounded slivers, listed for k_ghost (ids < n_tris: never overflows)
+        const bool unb = lead && (flags & TRI_UNBOUNDED);
+        const uint32_t slot = wave_append1(&cnt[C_SLIVER], unb);
+        if (unb) fb.slivers[slot] = (uint32_t)tri;
+    }
     const uint64_t m_setup = __ballot(lead);
     const uint64_t m_ghost = __ballot(lead && (flags & TRI_GHOST));
     const uint64_t m_unb = __ballot(lead && (flags & TRI_UNBOUNDED));
@@ -654,6 +680,25 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
             fb.timeline[TL_STRIDE * b + 10] = c_start;
             fb.timeline[TL_STRIDE * b + 11] = __builtin_amdgcn_s_memtime();
         }
+    }
+}
+
+// ---- k_ghost (ghost_list mode) -----------------------------------------------------------------
+// The listed unbounded slivers' tile-clamp pixels: wave w takes items w, w + waves, ... of
+// (sliver, slice); each sliver is cut into enough slices that the grid's waves stay busy.  The
+// records come from k_setup's stores (identical to the ghost waves' recomputation).
+constexpr int GHOST_LIST_BLOCKS = 512;
+
+__global__ __launch_bounds__(256) void k_ghost(FrameParams fp, FrameBuffers fb) {
+    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
+    const int n = (int)min(cnt[C_SLIVER], (uint32_t)fp.n_tris);
+    const int waves = (int)gridDim.x * 4, gw = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    const int slices = n > 0 ? max(1, min(16, waves / n)) : 1;
+    for (int item = gw; item < n * slices; item += waves) {
+        const int s = item / slices, slice = item - s * slices;
+        const uint32_t tri = fb.slivers[s];
+        const TriRec t = rec_from(reinterpret_cast<const float4 *>(&fb.recs[tri]));
+        sliver_pixels(fp, fb, cnt, t, tri, slice, 64 * slices);
     }
 }
 
@@ -942,7 +987,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                 if (lane == 63) sh.npairs = (uint32_t)incl;
             }
             __syncthreads();
-            const int total = (int)sh.npairs;
+            const int total = (fp.flags & DBG_SKIP_PAIRS) ? 0 : (int)sh.npairs;
             pairs += total;
             for (int k0 = 64 * wave; k0 < total; k0 += 256) {
                 const int k = k0 + lane;
@@ -1024,8 +1069,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
     if (px < fp.W && py < fp.H) {
-        reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - py) * fp.W + px] = rgba;
-        fb.depth[(size_t)py * fp.W + px] = depth;
+        __builtin_nontemporal_store(rgba, &reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - py) * fp.W + px]);
+        __builtin_nontemporal_store(depth, &fb.depth[(size_t)py * fp.W + px]);
         if (fb.prequant) fb.prequant[(size_t)(fp.H - 1 - py) * fp.W + px] = pq;
     }
     if (tid == 0) fb.busy[rt] = 0u;   // clean for the next frame
@@ -1039,8 +1084,8 @@ __device__ __forceinline__ void clear_tile(const FrameParams &fp, const FrameBuf
     const int px = col * RTW + (tid & 31), py = row * RTH + (tid >> 5);
     if (px < fp.W && py < fp.H) {
         const size_t c = (size_t)(fp.H - 1 - py) * fp.W + px;
-        reinterpret_cast<uint32_t *>(fb.color)[c] = fp.clear_rgba;
-        fb.depth[(size_t)py * fp.W + px] = FLT_MAX;
+        __builtin_nontemporal_store(fp.clear_rgba, &reinterpret_cast<uint32_t *>(fb.color)[c]);
+        __builtin_nontemporal_store(FLT_MAX, &fb.depth[(size_t)py * fp.W + px]);
         if (fb.prequant) fb.prequant[c] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
@@ -1141,6 +1186,11 @@ hipError_t launch_setup(const FrameParams &fp, const FrameBuffers &fb, const KAr
         hipLaunchKernelGGL(k_setup<true>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
     else
         hipLaunchKernelGGL(k_setup<false>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
+    return hipGetLastError();
+}
+
+hipError_t launch_ghost(const FrameParams &fp, const FrameBuffers &fb, hipStream_t s) {
+    hipLaunchKernelGGL(k_ghost, dim3(GHOST_LIST_BLOCKS), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }
 
