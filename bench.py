@@ -42,9 +42,9 @@ for p in (PKG, ROOT):
 METRIC = "Mtri/s + shaded Mpix/s at 1920×1080 Blinn-Phong; 1/2/4/8 MI355X scaling"
 HBM_PEAK_GBS = 8000.0
 WORKLOADS = {
-    "c2": "C2: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 1920x1080, 1 frame per step",
-    "c1": "C1: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 800x600, 1 frame per step",
-    "c3": "C3: 64-instance Suzanne grid, Phong, 1920x1080, 1 frame per step",
+    "c2": "C2: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 1920x1080, a batch of camera poses per step",
+    "c1": "C1: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 800x600, a batch of camera poses per step",
+    "c3": "C3: 64-instance Suzanne grid, Phong, 1920x1080, a batch of camera poses per step",
     "c5": "C5: Suzanne + floor, PassShadowMap 2048^2 + PassPBRForward (PBR Cook-Torrance, PCF 5x5, motion) "
           "3840x2160, 1 frame (both passes) per step",
     "c4": "C4: Forward+ tiled, 1M synthetic triangles, 256 point lights, 3840x2160 (light cull + lit forward pass), "
@@ -66,19 +66,48 @@ def build_workload(name, rank=0):
     return scene.config(name, yaw=3.0 * rank)
 
 
+POSE_SETS = 4   # distinct batches of camera poses the timed steps cycle through
+
+
+def batch_poses(name, n_frames, rank=0):
+    """POSE_SETS batches of n_frames camera poses of the workload's scene: frame k of set p looks from
+    yaw = 3*rank - 12 + 24 * (p * n_frames + k) / (POSE_SETS * n_frames) degrees and a small pitch
+    sweep, so every frame of every step is a different image of the same scene (nothing is cached:
+    each step re-runs the whole path for its own poses)."""
+    from shs_gpu import scene
+    total = POSE_SETS * n_frames
+    sets = []
+    for p in range(POSE_SETS):
+        fds = []
+        for k in range(n_frames):
+            i = p * n_frames + k
+            frame, draws = scene.config(name, yaw=3.0 * rank - 12.0 + 24.0 * i / total,
+                                        pitch=-3.0 + 6.0 * ((i * 7) % total) / total)
+            fds.append(draws)
+        sets.append(fds)
+    return frame, sets
+
+
 def run_gpu(args, rank, local_rank, world, dist):
+    """One step = one shs_render_legacy_batch of F frames (F = --frames-per-step): one k_setup + one
+    k_raster launch render F independent frames, each into its own colour + depth framebuffers.
+    F = 1 is the single-frame (latency) path, one shs_render_legacy per step."""
     import shs_gpu
-    frame, draws = build_workload(args.config, rank)
+    F = args.frames_per_step
+    frame, sets = batch_poses(args.config, F, rank)
     frame.debug_flags = args.debug_flags   # timing experiments only (wrong images)
     ctx = shs_gpu.Context(local_rank)
     if args.raster_mode:
         ctx.set_raster_mode(args.raster_mode)
     if args.raster_loop >= 0:
         ctx.set_raster_loop(args.raster_loop)
-    prepared = ctx.prepare(frame, draws)
-    for _ in range(max(args.warmup, 1)):
-        ctx.render_prepared(prepared)
+    prepared = [ctx.prepare_batch(frame, fds) for fds in sets]
+    render = ctx.render_batch_prepared
+    for i in range(max(args.warmup, 1)):
+        render(prepared[i % POSE_SETS])
     ctx.synchronize()
+    # the statistics of a timed-loop batch (the capacity adaptation of the warm-up has settled)
+    render(prepared[0])
     stats = ctx.stats()
 
     def barrier_sync():
@@ -92,14 +121,33 @@ def run_gpu(args, rank, local_rank, world, dist):
     ctx.timing_reset()
     barrier_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.render_prepared(prepared)
+    for i in range(args.steps):
+        render(prepared[i % POSE_SETS])
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    n_frames, kms = ctx.timing_read()
+    n_launches, kms = ctx.timing_read()
     ctx.enable_timing(False)
+    single = None
+    if F > 1 and not args.child:
+        # the single-frame latency figure beside it: one shs_render_legacy per step
+        one = ctx.prepare(frame, sets[0][0])
+        for _ in range(10):
+            ctx.render_prepared(one)
+        ctx.synchronize()
+        n1 = max(20, min(args.steps * 4, 400))
+        ctx.enable_timing(True)
+        ctx.timing_reset()
+        t1 = time.perf_counter()
+        for _ in range(n1):
+            ctx.render_prepared(one)
+        ctx.synchronize()
+        el1 = time.perf_counter() - t1
+        _, k1 = ctx.timing_read()
+        ctx.enable_timing(False)
+        single = {"ms_per_frame": round(el1 / n1 * 1e3, 5), "steps": n1,
+                  "kernels_ms": {k: round(v, 5) for k, v in k1.items()}}
     ctx.close()
-    return frame, draws, stats, elapsed, n_frames, kms
+    return frame, sets[0][0], stats, elapsed, n_launches, kms, single
 
 
 def lib_workload(args, rank=0):
@@ -238,7 +286,7 @@ def collect_pmc(args):
             d = os.path.join(tmp, counter)
             cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                    sys.executable, os.path.abspath(__file__), "--child", "--config", args.config,
-                   "--steps", "20", "--warmup", "3"]
+                   "--steps", "20", "--warmup", "3", "--frames-per-step", str(args.frames_per_step)]
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=300, text=True)
             if r.returncode != 0:
                 return None, f"rocprofv3 {counter} rc={r.returncode}: {r.stdout[-400:]}"
@@ -331,6 +379,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--frames-per-step", type=int, default=0,
+                    help="legacy configs: frames per shs_render_legacy_batch step (default 64 for c1/c2, 16 for c3)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -339,6 +389,8 @@ def main():
     ap.add_argument("--raster-mode", type=int, default=0, help="legacy path: 0 auto, 1 scan, 2 bins")
     ap.add_argument("--raster-loop", type=int, default=-1, help="legacy path: 0 per-pixel, 1 pair tasks (default)")
     args = ap.parse_args()
+    if args.frames_per_step <= 0:
+        args.frames_per_step = {"c1": 64, "c2": 64, "c3": 16}.get(args.config, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -362,11 +414,13 @@ def main():
 
     if args.config in LIB_CONFIGS:
         return main_lib(args, world, rank, local_rank, dist, pmc, pmc_err)
-    frame, draws, stats, elapsed, n_frames, kms = run_gpu(args, rank, local_rank, world, dist)
-    B, n_tri = algorithmic_bytes(frame, draws)
+    frame, draws, stats, elapsed, n_launches, kms, single = run_gpu(args, rank, local_rank, world, dist)
+    B1, n_tri1 = algorithmic_bytes(frame, draws)
+    F = args.frames_per_step
+    B, n_tri = B1 * F, n_tri1 * F          # per step (= per k_raster launch)
 
     el_max = elapsed
-    covered = stats["covered_pixels"]
+    covered = stats["covered_pixels"]       # batch total
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
@@ -385,7 +439,7 @@ def main():
         return
 
     steps = args.steps
-    value = world * n_tri * steps / el_max / 1e6
+    value = world * n_tri * steps / el_max / 1e6     # n_tri = triangles per step (F frames)
     mpix = covered_total * steps / el_max / 1e6
     t_raster_ms = kms["raster"]
     achieved = B / (t_raster_ms * 1e-3) / 1e9 if t_raster_ms > 0 else None
@@ -400,11 +454,14 @@ def main():
         "algorithmic_bytes": B,
         "kernel_ms": round(t_raster_ms, 5),
     }
-    # the whole frame's device time (k_setup + k_raster) against the same bytes, for reference
+    # the whole step's device time (k_setup + k_raster) against the same bytes, and the driver-timed
+    # step (wall clock between the barriers, host enqueue included)
     t_frame_ms = kms.get("setup", 0.0) + t_raster_ms
     if t_frame_ms > 0:
         roofline["frame_kernels_ms"] = round(t_frame_ms, 5)
         roofline["frame_frac"] = round(B / (t_frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    roofline["step_achieved"] = round(world * B * steps / el_max / 1e9, 2)
+    roofline["step_frac"] = round(world * B * steps / el_max / 1e9 / HBM_PEAK_GBS / world, 4)
     if pmc is None:
         roofline["traffic_note"] = pmc_err
     line = {
@@ -422,14 +479,17 @@ def main():
         "data": "synthetic: Suzanne soup from the reference's assets/obj/monkey/monkey.rawobj (967 tris), "
                 "reference scene constants (camera (0,5,-20) fov60, light, colour)",
         "config": {"workload": WORKLOADS[args.config], "width": frame.width, "height": frame.height,
-                   "tris_per_frame": n_tri, "frames_per_step_per_gpu": 1,
+                   "tris_per_frame": n_tri1, "frames_per_step_per_gpu": F,
+                   "pose_sets": POSE_SETS,
                    "parallelism": f"frame-parallel x{world}" if world > 1 else "single GPU"},
         "shaded_mpix_s": round(mpix, 3),
-        "frame_stats": stats,
+        "batch_stats": stats,
         "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
-        "timed_frames_with_events": n_frames,
+        "timed_launches_with_events": n_launches,
         "roofline": roofline,
     }
+    if single is not None:
+        line["single_frame"] = single
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(line), flush=True)

@@ -104,10 +104,23 @@ int shs_mesh_release(shs_ctx *ctx, int32_t mesh_id);
  * asynchronously on the context stream.  Results stay in device memory until shs_resolve. */
 int shs_render_legacy(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws);
 
+/* A batch of n_frames frames (1 <= n_frames <= SHS_MAX_BATCH_FRAMES) of one frame description, e.g.
+ * the next n_frames camera poses of a render-ahead host or the views of a multi-view capture: frame f
+ * draws draws[f * n_draws .. f * n_draws + n_draws - 1], in that order, and every frame must submit
+ * the same number of triangles.  Each frame has its own device framebuffers (frame f's colour at
+ * byte f*W*H*4 of the colour plane shs_device_framebuffers returns, its depth at float f*W*H); the
+ * frames are independent -- each equals the frame shs_render_legacy renders from its draws.  One
+ * k_setup + one k_raster launch cover the whole batch.  shs_render_legacy(ctx, frame, draws, n) is
+ * shs_render_legacy_batch(ctx, frame, draws, n, 1).  Statistics (shs_get_stats) are batch totals. */
+#define SHS_MAX_BATCH_FRAMES 1024
+int shs_render_legacy_batch(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws,
+                            int32_t n_frames);
+
 /* Copy the frame into caller-owned host buffers (blocking).  color: W*H*4 bytes, canvas rows
  * (Canvas::buffer() layout); depth: W*H floats, screen rows (ZBuffer::buffer() as the legacy
- * pipelines index it).  Either pointer may be NULL. */
+ * pipelines index it).  Either pointer may be NULL.  shs_resolve = frame 0 of the last batch. */
 int shs_resolve(shs_ctx *ctx, uint8_t *color, float *depth);
+int shs_resolve_frame(shs_ctx *ctx, int32_t frame_index, uint8_t *color, float *depth);
 /* Pre-truncation shader floats, W*H*4 (canvas rows), only when SHS_FRAME_PREQUANT was set. */
 int shs_resolve_prequant(shs_ctx *ctx, float *prequant);
 /* Device pointers of the current frame (zero-copy hand-off to torch / RCCL). */

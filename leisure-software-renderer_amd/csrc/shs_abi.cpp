@@ -190,7 +190,9 @@ static int harvest_all(shs_ctx *ctx) {
 
 static int enqueue_frame(shs_ctx *ctx) {
     const shs_frame_desc &f = ctx->frame;
-    const int n_draws = (int)ctx->last_draws.size();
+    const int n_frames = ctx->last_n_frames;
+    const int n_draws = ctx->frame_draws;                 // per frame
+    const int n_draws_all = (int)ctx->last_draws.size();  // n_frames * n_draws
     const int tiles_x = (f.width + shs_dev::TILE - 1) / shs_dev::TILE;
     const int tiles_y = (f.height + shs_dev::TILE - 1) / shs_dev::TILE;
     const int n_tiles = tiles_x * tiles_y;
@@ -199,25 +201,26 @@ static int enqueue_frame(shs_ctx *ctx) {
     const size_t npx = (size_t)f.width * f.height;
 
     int64_t total = 0;
-    for (const auto &d : ctx->last_draws) total += ctx->meshes[d.mesh_id].n_tris;
-    if (total > 0x3fffffff) { ctx->err = "too many triangles in one frame"; return SHS_ERR_INVALID; }
-    const int n_tris = (int)total;
+    for (int i = 0; i < n_draws; ++i) total += ctx->meshes[ctx->last_draws[i].mesh_id].n_tris;
+    if (total * n_frames > 0x3fffffff) { ctx->err = "too many triangles in one batch"; return SHS_ERR_INVALID; }
+    const int n_tris = (int)total;   // per frame (every frame of a batch has the same count)
+    const size_t nt_all = (size_t)std::max(n_tris, 1) * n_frames;
 
-    if (ensure(ctx, ctx->recs, (size_t)std::max(n_tris, 1)) || ensure(ctx, ctx->shade, (size_t)std::max(n_tris, 1)) ||
-        ensure(ctx, ctx->boxes, (size_t)std::max(n_tris, 1)) || ensure(ctx, ctx->slivers, (size_t)std::max(n_tris, 1)))
+    if (ensure(ctx, ctx->recs, nt_all) || ensure(ctx, ctx->shade, nt_all) || ensure(ctx, ctx->boxes, nt_all) ||
+        ensure(ctx, ctx->slivers, nt_all))
         return SHS_ERR_HIP;
     // Bin counts (2 parity sets) and busy flags are kept zero by the kernels themselves (k_setup's
     // clear blocks zero the next frame's counts, k_raster resets the flags it consumed); they are
     // reset here only when the buffers are new or the tile geometry / shard changes.
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)f.shard_rank << 16) ^
-                          (uint64_t)f.shard_count;
+                          (uint64_t)f.shard_count ^ ((uint64_t)n_frames << 24);
     bool reset = gkey != ctx->geom_key;
-    if (ctx->tile_count.cap < 2 * (size_t)n_tiles || !ctx->tile_count.p) {
-        if (ensure(ctx, ctx->tile_count, 2 * (size_t)n_tiles)) return SHS_ERR_HIP;
+    if (ctx->tile_count.cap < 2 * (size_t)n_tiles * n_frames || !ctx->tile_count.p) {
+        if (ensure(ctx, ctx->tile_count, 2 * (size_t)n_tiles * n_frames)) return SHS_ERR_HIP;
         reset = true;
     }
-    if (ctx->busy.cap < (size_t)n_rt || !ctx->busy.p) {
-        if (ensure(ctx, ctx->busy, n_rt)) return SHS_ERR_HIP;
+    if (ctx->busy.cap < (size_t)n_rt * n_frames || !ctx->busy.p) {
+        if (ensure(ctx, ctx->busy, (size_t)n_rt * n_frames)) return SHS_ERR_HIP;
         reset = true;
     }
     if (reset) {
@@ -225,48 +228,51 @@ static int enqueue_frame(shs_ctx *ctx) {
         HIP_TRY(ctx, hipMemsetAsync(ctx->busy.p, 0, ctx->busy.cap * sizeof(uint32_t), ctx->stream));
         ctx->geom_key = gkey;
     }
-    if (ensure(ctx, ctx->bins, (size_t)n_tiles * ctx->bin_cap)) return SHS_ERR_HIP;
-    const int setup_blocks = (n_tris + 63) / 64;   // a quad of lanes per triangle
-    if (ensure(ctx, ctx->blk_stat, (size_t)std::max(setup_blocks, 1))) return SHS_ERR_HIP;
+    if (ensure(ctx, ctx->bins, (size_t)n_tiles * ctx->bin_cap * n_frames)) return SHS_ERR_HIP;
+    const int setup_blocks = (n_tris + 63) / 64;   // a quad of lanes per triangle, per frame
+    if (ensure(ctx, ctx->blk_stat, (size_t)std::max(setup_blocks, 1) * n_frames)) return SHS_ERR_HIP;
     if (!ctx->spill.p && ensure(ctx, ctx->spill, 1 << 16)) return SHS_ERR_HIP;
     if (!ctx->frags.p && ensure(ctx, ctx->frags, 1 << 12)) return SHS_ERR_HIP;
-    if (ensure(ctx, ctx->color, npx * 4) || ensure(ctx, ctx->depth, npx)) return SHS_ERR_HIP;
+    if (ensure(ctx, ctx->color, npx * 4 * n_frames) || ensure(ctx, ctx->depth, npx * n_frames)) return SHS_ERR_HIP;
     const bool want_pq = (f.flags & SHS_FRAME_PREQUANT) != 0;
-    if (want_pq && ensure(ctx, ctx->prequant, npx)) return SHS_ERR_HIP;
+    if (want_pq && ensure(ctx, ctx->prequant, npx * n_frames)) return SHS_ERR_HIP;
 
     // per-draw uniform blocks: kernel arguments for small scenes, a device table otherwise
     shs_dev::KArgDraws ka;
     std::memset(&ka, 0, sizeof ka);
     hipStream_t st = ctx->stream;
     int32_t base = 0;
-    if (n_draws <= shs_dev::KARG_DRAWS) {
-        for (int i = 0; i < n_draws; ++i) {
+    // tri_base restarts at 0 in every frame (submission order is per frame)
+    if (n_draws_all <= shs_dev::KARG_DRAWS) {
+        for (int i = 0; i < n_draws_all; ++i) {
+            if (i % std::max(n_draws, 1) == 0) base = 0;
             const shs_legacy_draw &d = ctx->last_draws[i];
             build_draw(d, ctx->meshes[d.mesh_id], base, ka.d[i]);
             base += ctx->meshes[d.mesh_id].n_tris;
         }
     } else {
-        if (ensure(ctx, ctx->draws, n_draws)) return SHS_ERR_HIP;
+        if (ensure(ctx, ctx->draws, n_draws_all)) return SHS_ERR_HIP;
         const int s = ctx->slot;
         ctx->slot ^= 1;
         if (ctx->slot_used[s]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[s]));
-        if ((size_t)n_draws > ctx->h_cap) {
+        if ((size_t)n_draws_all > ctx->h_cap) {
             for (int i = 0; i < 2; ++i) {
                 if (i != s && ctx->slot_used[i]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[i]));
                 if (ctx->h_draws[i]) HIP_TRY(ctx, hipHostFree(ctx->h_draws[i]));
                 ctx->h_draws[i] = nullptr;
             }
-            const size_t cap = std::max<size_t>(n_draws, 64);
+            const size_t cap = std::max<size_t>(n_draws_all, 64);
             for (int i = 0; i < 2; ++i)
                 HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_draws[i]), cap * sizeof(DrawGPU)));
             ctx->h_cap = cap;
         }
-        for (int i = 0; i < n_draws; ++i) {
+        for (int i = 0; i < n_draws_all; ++i) {
+            if (i % std::max(n_draws, 1) == 0) base = 0;
             const shs_legacy_draw &d = ctx->last_draws[i];
             build_draw(d, ctx->meshes[d.mesh_id], base, ctx->h_draws[s][i]);
             base += ctx->meshes[d.mesh_id].n_tris;
         }
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->draws.p, ctx->h_draws[s], n_draws * sizeof(DrawGPU), hipMemcpyHostToDevice, st));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->draws.p, ctx->h_draws[s], n_draws_all * sizeof(DrawGPU), hipMemcpyHostToDevice, st));
         HIP_TRY(ctx, hipEventRecord(ctx->slot_ev[s], st));
         ctx->slot_used[s] = true;
     }
@@ -287,10 +293,11 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ctx->spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ctx->frags.cap, 0xffffffffu);
-    {   // ~1K ghost waves per frame: small scenes split each sliver group over a few waves.  Measured
+    {   // ~1K ghost waves per launch: small scenes split each sliver group over a few waves.  Measured
         // at C2 (61 groups, ~17 unbounded slivers): 4K waves 8.9 us setup, 2K 7.7, 1K 7.3, 512 8.1,
         // 256 9.3 -- past ~1K the extra workgroup launches cost more than the shorter enumerations save.
-        const int n_groups = std::max(1, (n_tris + 15) / 16);
+        // A batch of frames already brings n_frames x the groups.
+        const int n_groups = std::max(1, (n_tris + 15) / 16) * n_frames;
         fp.ghost_slices = (uint32_t)std::min(16, std::max(1, 1024 / n_groups));
     }
     fp.parity = ctx->frame_index & 1u;
@@ -305,10 +312,12 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.ghost_blocks = fp.ghost_list ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
     fp.clear_blocks = 0;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / shs_dev::RTH);
+    fp.n_frames = n_frames;
+    fp.frame_blocks = std::max(1, fp.setup_blocks + fp.ghost_blocks + fp.clear_blocks);
     // persistent raster grid: one resident wave of workgroups (k_raster runs 4 per CU)
-    const int raster_grid = std::max(1, std::min(fp.n_owned_rt, 256 * 4));
+    const int raster_grid = std::max(1, std::min(fp.n_owned_rt * n_frames, 256 * 4));
     if (ensure(ctx, ctx->rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
-    fp.setup_grid = std::max(1, fp.setup_blocks + fp.ghost_blocks + fp.clear_blocks);
+    fp.setup_grid = fp.frame_blocks * n_frames;
     if (ctx->want_timeline) {
         const size_t n = (size_t)shs_dev::TL_STRIDE * (fp.setup_grid + raster_grid);
         if (ensure(ctx, ctx->timeline, n)) return SHS_ERR_HIP;
@@ -349,7 +358,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     ctx->need_check = true;
     ctx->last_n_tris = n_tris;
     ctx->last_n_tiles = n_tiles;
-    ctx->last_setup_blocks = setup_blocks;
+    ctx->last_setup_blocks = setup_blocks * n_frames;
     ctx->last_raster_grid = raster_grid;
     ctx->last_setup_grid = fp.setup_grid;
     ctx->last_ghost_blocks = fp.ghost_blocks;
@@ -412,13 +421,17 @@ static int finish_frame(shs_ctx *ctx) {
     return SHS_OK;
 }
 
-int shs_render_legacy(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws) {
-    if (!ctx || !frame || n_draws < 0 || (n_draws > 0 && !draws)) return SHS_ERR_INVALID;
+int shs_render_legacy_batch(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws,
+                            int32_t n_frames) {
+    if (!ctx || !frame || n_draws < 0 || (n_draws > 0 && !draws) || n_frames < 1 || n_frames > SHS_MAX_BATCH_FRAMES)
+        return SHS_ERR_INVALID;
     const shs_frame_desc &f = *frame;
     if (f.width <= 0 || f.height <= 0 || f.width > 16384 || f.height > 16384) { ctx->err = "bad frame size"; return SHS_ERR_INVALID; }
     if (f.ref_tile_w <= 0 || f.ref_tile_h <= 0) { ctx->err = "bad reference tile size"; return SHS_ERR_INVALID; }
     if (f.shard_count <= 0 || f.shard_rank < 0 || f.shard_rank >= f.shard_count) { ctx->err = "bad shard"; return SHS_ERR_INVALID; }
-    for (int i = 0; i < n_draws; ++i) {
+    const int n_all = n_draws * n_frames;
+    int64_t tris0 = 0;
+    for (int i = 0; i < n_all; ++i) {
         const int id = draws[i].mesh_id;
         if (id < 0 || id >= (int)ctx->meshes.size() || !ctx->meshes[id].live || ctx->meshes[id].lib) {
             ctx->err = "bad mesh id (not a legacy soup mesh)";
@@ -429,13 +442,26 @@ int shs_render_legacy(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legac
             return SHS_ERR_INVALID;
         }
     }
+    // every frame of a batch submits the same number of triangles (one submission-order layout)
+    for (int fr = 0; fr < n_frames; ++fr) {
+        int64_t t = 0;
+        for (int i = 0; i < n_draws; ++i) t += ctx->meshes[draws[fr * n_draws + i].mesh_id].n_tris;
+        if (fr == 0) tris0 = t;
+        else if (t != tris0) { ctx->err = "frames of a batch must submit equal triangle counts"; return SHS_ERR_INVALID; }
+    }
     if (set_dev(ctx)) return SHS_ERR_HIP;
-    // No host sync here: a still-pending previous frame is superseded by this one (it rewrites every
-    // pixel); only the newest frame's overflow flags are checked (and the frame re-issued) when the
+    // No host sync here: a still-pending previous batch is superseded by this one (it rewrites every
+    // pixel); only the newest batch's overflow flags are checked (and the batch re-issued) when the
     // caller synchronises / resolves.
     ctx->frame = f;
-    ctx->last_draws.assign(draws, draws + n_draws);
+    ctx->last_draws.assign(draws, draws + n_all);
+    ctx->last_n_frames = n_frames;
+    ctx->frame_draws = n_draws;
     return enqueue_frame(ctx);
+}
+
+int shs_render_legacy(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws) {
+    return shs_render_legacy_batch(ctx, frame, draws, n_draws, 1);
 }
 
 int shs_synchronize(shs_ctx *ctx) {
@@ -444,17 +470,20 @@ int shs_synchronize(shs_ctx *ctx) {
     return finish_frame(ctx);
 }
 
-int shs_resolve(shs_ctx *ctx, uint8_t *color, float *depth) {
+int shs_resolve_frame(shs_ctx *ctx, int32_t frame_index, uint8_t *color, float *depth) {
     if (!ctx) return SHS_ERR_INVALID;
     if (!ctx->have_frame) { ctx->err = "no frame rendered"; return SHS_ERR_INVALID; }
+    if (frame_index < 0 || frame_index >= ctx->last_n_frames) { ctx->err = "frame index outside the batch"; return SHS_ERR_INVALID; }
     if (set_dev(ctx)) return SHS_ERR_HIP;
     int rc = finish_frame(ctx);
     if (rc) return rc;
     const size_t npx = (size_t)ctx->frame.width * ctx->frame.height;
-    if (color) HIP_TRY(ctx, hipMemcpy(color, ctx->color.p, npx * 4, hipMemcpyDeviceToHost));
-    if (depth) HIP_TRY(ctx, hipMemcpy(depth, ctx->depth.p, npx * sizeof(float), hipMemcpyDeviceToHost));
+    if (color) HIP_TRY(ctx, hipMemcpy(color, ctx->color.p + npx * 4 * frame_index, npx * 4, hipMemcpyDeviceToHost));
+    if (depth) HIP_TRY(ctx, hipMemcpy(depth, ctx->depth.p + npx * frame_index, npx * sizeof(float), hipMemcpyDeviceToHost));
     return SHS_OK;
 }
+
+int shs_resolve(shs_ctx *ctx, uint8_t *color, float *depth) { return shs_resolve_frame(ctx, 0, color, depth); }
 
 int shs_resolve_prequant(shs_ctx *ctx, float *pq) {
     if (!ctx || !pq) return SHS_ERR_INVALID;
@@ -479,7 +508,7 @@ int shs_get_stats(shs_ctx *ctx, shs_raster_stats *st) {
     if (set_dev(ctx)) return SHS_ERR_HIP;
     int rc = finish_frame(ctx);
     if (rc) return rc;
-    st->tri_input = (uint64_t)ctx->last_n_tris;
+    st->tri_input = (uint64_t)ctx->last_n_tris * ctx->last_n_frames;
     st->tri_setup = ctx->last_setup;
     st->tri_ghost = ctx->last_ghost;
     st->bin_entries = ctx->last_bins;

@@ -59,9 +59,12 @@ int enqueue_tonemap(shs_ctx *ctx) {
     const size_t npx = (size_t)W * H;
     if ((d.flags & SHS_TONEMAP_LDR) && ensure(ctx, ctx->lib_ldr, npx)) return SHS_ERR_HIP;
     if ((d.flags & SHS_TONEMAP_PRESENT) && ensure(ctx, ctx->lib_present, npx)) return SHS_ERR_HIP;
-    if (ctx->tm_gamma != d.gamma) {
-        tonemap_thresholds(d.gamma, ctx->tm_thr);
-        ctx->tm_gamma = d.gamma;
+    // the thresholds depend on the clamped gamma only (pass_tonemap.hpp: 1 / max(0.001, gamma))
+    const float g = std::max(0.001f, d.gamma);
+    if (!ctx->tm_thr_valid || ctx->tm_gamma != g) {
+        tonemap_thresholds(g, ctx->tm_thr);
+        ctx->tm_gamma = g;
+        ctx->tm_thr_valid = true;
     }
     shs_dev::TonemapParams p{};
     p.hdr = ctx->lib_hdr.p;

@@ -85,7 +85,9 @@ struct shs_ctx {
     std::vector<shs_legacy_draw> last_draws;
     bool have_frame = false;
     bool need_check = false;
-    int last_n_tris = 0;
+    int last_n_frames = 1;           // frames of the last batch (last_draws holds n_frames x frame_draws)
+    int frame_draws = 0;             // draws per frame of the last batch
+    int last_n_tris = 0;             // triangles per frame
     int last_n_tiles = 0;
 
     bool timing = false;
@@ -151,7 +153,8 @@ struct shs_ctx {
     // PassTonemap + present staging (shs_abi_post.cpp)
     DevBuf<uint32_t> lib_ldr, lib_present;
     shs_tonemap_desc tm_desc{};
-    float tm_gamma = -1.0f;               // gamma of tm_thr
+    float tm_gamma = 0.0f;                // clamped gamma (max(0.001, gamma)) of tm_thr
+    bool tm_thr_valid = false;            // tm_thr holds the thresholds of tm_gamma
     float tm_thr[256] = {};
     bool have_ldr = false;                // a tonemap follows the current camera pass
     DevBuf<uint32_t> lib_mb, lib_mb_present;

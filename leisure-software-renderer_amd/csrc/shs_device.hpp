@@ -106,7 +106,8 @@ struct alignas(16) GhostFrag {
     float z;
     uint32_t id;     // submission index
     float v, w;      // barycentrics for shading (u = (1 - v) - w)
-    uint32_t pad[3];
+    uint32_t frame;  // frame of the batch
+    uint32_t pad[2];
 };
 
 struct FrameParams {
@@ -129,30 +130,56 @@ struct FrameParams {
                                      // (binned scenes); 0: k_setup's ghost waves (scan-mode scenes)
     int32_t setup_blocks, ghost_blocks, clear_blocks;   // k_setup block roles, in this order (no
                                                         // clear blocks: k_raster clears)
-    int32_t n_owned_rt;              // raster tiles of the owned bin tiles (4 per bin tile)
+    int32_t n_owned_rt;              // raster tiles of the owned bin tiles (4 per bin tile), per frame
     int32_t setup_grid;              // k_setup grid (k_raster's timeline slots follow)
+    // Frame batches: n_frames frames of this size, each with its own n_draws draws (draw table entry
+    // f * n_draws + i) and its own framebuffers / workspace (FrameBuffers strides below).  k_setup runs
+    // frame_blocks (= setup_blocks + ghost_blocks) blocks per frame; k_raster's persistent grid walks
+    // the n_frames * n_owned_rt raster tiles of the whole batch.
+    int32_t n_frames;
+    int32_t frame_blocks;
 };
 
+// Device buffers.  "per frame" buffers hold n_frames consecutive copies (frame_view() offsets them);
+// the others are shared by the batch.
 struct FrameBuffers {
-    const DrawGPU *draws;            // device draw table (n_draws > KARG_DRAWS)
-    TriRec *recs;
-    ShadeRec *shade;                 // n_tris
-    uint32_t *tile_count;            // 2 parity sets x n_bin_tiles; k_setup zeroes the next frame's set
-    uint32_t *bins;                  // n_bin_tiles * bin_cap
-    uint2 *spill;                    // (bin tile, tri) pairs beyond bin_cap
+    const DrawGPU *draws;            // device draw table (n_frames * n_draws > KARG_DRAWS)
+    TriRec *recs;                    // per frame: n_tris
+    ShadeRec *shade;                 // per frame: n_tris
+    uint32_t *tile_count;            // per frame: 2 parity sets x n_bin_tiles; k_setup zeroes the next set
+    uint32_t *bins;                  // per frame: n_bin_tiles * bin_cap
+    uint2 *spill;                    // (f * n_bin_tiles + bin tile, tri) pairs beyond bin_cap
     GhostFrag *frags;                // tile-clamp pixels of unbounded slivers that pass (frag_cap)
-    uint32_t *slivers;               // n_tris: unbounded slivers' ids (ghost_list mode, C_SLIVER entries)
-    uint2 *boxes;                    // n_tris: packed bin box (gbx, gby); empty for culled
+    uint32_t *slivers;               // n_frames * n_tris: unbounded slivers, f * n_tris + tri (ghost_list)
+    uint2 *boxes;                    // per frame: n_tris packed bin boxes (gbx, gby); empty for culled
     uint32_t *counters;              // 2 * C_NCOUNTERS
-    uint32_t *busy;                  // per raster tile: 1 = has candidates / fragments (k_raster resets)
+    uint32_t *busy;                  // per frame, per raster tile: 1 = has candidates / fragments
+                                     // (k_raster resets)
     uint4 *blk_stat;                 // per setup block: (set up, ghost, unbounded, bin entries)
     uint2 *rstat;                    // per raster block: (covered pixels, fullest bin seen)
     uint64_t *timeline;              // optional: TL_STRIDE slots per workgroup, k_setup then k_raster:
                                      // start, end, then phase marks of thread 0 (first busy tile)
-    uint8_t *color;                  // W*H*4, canvas rows
-    float *depth;                    // W*H, screen rows
-    float4 *prequant;                // W*H (optional)
+    uint8_t *color;                  // per frame: W*H*4, canvas rows
+    float *depth;                    // per frame: W*H, screen rows
+    float4 *prequant;                // per frame: W*H (optional)
 };
+
+// The buffers of frame f of the batch (shared buffers unchanged).
+__device__ __forceinline__ FrameBuffers frame_view(const FrameParams &fp, const FrameBuffers &fb, int f) {
+    FrameBuffers v = fb;
+    const size_t nt = (size_t)fp.n_tris, n_bt = (size_t)fp.tiles_x * fp.tiles_y;
+    const size_t npx = (size_t)fp.W * fp.H, n_rt = (size_t)fp.tiles_x * fp.rtiles_y;
+    v.recs += f * nt;
+    v.shade += f * nt;
+    v.boxes += f * nt;
+    v.tile_count += f * 2 * n_bt;
+    v.bins += f * n_bt * fp.bin_cap;
+    v.busy += f * n_rt;
+    v.color += f * npx * 4;
+    v.depth += f * npx;
+    if (v.prequant) v.prequant += f * npx;
+    return v;
+}
 
 constexpr int TL_STRIDE = 12;
 

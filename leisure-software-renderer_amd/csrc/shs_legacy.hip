@@ -339,6 +339,8 @@ __device__ __forceinline__ TriRec quad_record(const FrameParams &fp, const DrawG
 
 // q = n / d, r = n % d for 0 <= n < 2^24, 1 <= d < 2^24 (rd = 1.0f / d): the float quotient is
 // within 1 of the exact one, fixed up by the remainder.
+// q = n / d, r = n % d for 0 <= n < 2^31, 1 <= d, provided the true quotient is < 2^22 (the
+// float product's relative error 2^-23 then moves it by less than one).
 __device__ __forceinline__ void div_small(int n, int d, float rd, int &q, int &r) {
     q = (int)((float)n * rd);
     r = n - q * d;
@@ -350,7 +352,7 @@ __device__ __forceinline__ void div_small(int n, int d, float rd, int &q, int &r
 // slice-th 64-pixel batch of every `stride`: passing ones become ghost fragments.  Wave-uniform
 // arguments, converged wave.
 __device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, const TriRec &t,
-                                              uint32_t tri, int slice, int stride) {
+                                              uint32_t tri, uint32_t frame, int slice, int stride) {
     const int lane = __lane_id();
     const int ix0 = lo16(t.ibx), ix1 = hi16(t.ibx), iy0 = lo16(t.iby), iy1 = hi16(t.iby);
     SliverSpan sp;
@@ -359,7 +361,9 @@ __device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const Frame
     const int nxo = sp.cl + sp.cr, nyo = sp.ru + sp.rd;
     const int nxi = max(sp.xi1 - sp.xi0 + 1, 0), nyi = max(sp.yi1 - sp.yi0 + 1, 0);
     const int ny = nyo + nyi;
-    // total <= W * H (< 2^24 px): 32-bit indices, divisions by reciprocal with a +-1 fix
+    // total <= W * H <= 2^28 (the ABI caps frames at 16384 x 16384): 32-bit indices.  Divisions by
+    // reciprocal with a +-1 fix: the quotients are pixel columns / rows (< 2^14 < 2^22), so the float
+    // estimate n * (1/d) is off by less than one and one correction step restores q and r exactly.
     const int total_a = nxo * ny, total = total_a + nxi * nyo;
     const float rny = 1.0f / (float)max(ny, 1), rnyo = 1.0f / (float)max(nyo, 1);
     for (int kb = slice * 64; kb < total; kb += stride) {
@@ -394,7 +398,8 @@ __device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const Frame
                 g.id = tri;
                 g.v = v;
                 g.w = w;
-                g.pad[0] = g.pad[1] = g.pad[2] = 0u;
+                g.frame = frame;
+                g.pad[0] = g.pad[1] = 0u;
                 fb.frags[slot] = g;
                 fb.busy[(py / RTH) * fp.tiles_x + px / RTW] = 1u;
             } else {
@@ -405,7 +410,7 @@ __device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const Frame
 }
 
 __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
-                                           uint32_t *cnt, int group, int slice, GhostScratch &gs) {
+                                           uint32_t *cnt, int frame, int group, int slice, GhostScratch &gs) {
     const int lane = __lane_id();
     QuadTri qt = quad_tri(draws, fp.n_draws, fp.n_tris, group * GHOST_GROUP + (lane >> 2));
     TriRec r;
@@ -424,19 +429,19 @@ __device__ __forceinline__ void ghost_wave(const FrameParams &fp, const FrameBuf
         wave_lds_sync();
         const TriRec t = rec_from(gs.rec);
         wave_lds_sync();   // gs.rec is rewritten by the next sliver
-        sliver_pixels(fp, fb, cnt, t, (uint32_t)(group * GHOST_GROUP + (src >> 2)), slice, stride);
+        sliver_pixels(fp, fb, cnt, t, (uint32_t)(group * GHOST_GROUP + (src >> 2)), (uint32_t)frame, slice, stride);
     }
 }
 
 // ---- k_setup ----------------------------------------------------------------------------------
 
-__device__ __forceinline__ void append_bin(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int t, uint32_t pos,
-                                           uint32_t id) {
+__device__ __forceinline__ void append_bin(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int frame, int t,
+                                           uint32_t pos, uint32_t id) {
     if (pos < fp.bin_cap) {
         fb.bins[(size_t)t * fp.bin_cap + pos] = id;
     } else {
         const uint32_t sp = atomicAdd(&cnt[C_SPILL], 1u);
-        if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t, id);
+        if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)(frame * fp.tiles_x * fp.tiles_y + t), id);
         else atomicOr(&cnt[C_OVERFLOW], OV_SPILL);
     }
 }
@@ -513,7 +518,7 @@ __device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, 
 
 // Record, varyings and their stores for the quad's triangle; returns the flags and the bin box.
 __device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU &dr, int d,
-                                               int tri, uint2 &gbox) {
+                                               int dbase, int tri, uint2 &gbox) {
     const int q = __lane_id() & 3, qv = q < 3 ? q : 2;
     const int local = tri - dr.tri_base;
     const float *P = dr.pos + 9 * (size_t)local + 3 * qv;
@@ -525,7 +530,7 @@ __device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const Fram
     f3 a, nr;
     corner_varyings(dr, p3, n3, a, nr);
     quad_store_rec(fb, tri, r);
-    quad_store_shade(fb, tri, d, dr.shading, a, nr);
+    quad_store_shade(fb, tri, dbase + d, dr.shading, a, nr);   // the draw-table index of the batch
     if (q == 0) fb.boxes[tri] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
     gbox = make_uint2(r.gbx, r.gby);
     return r.flags;
@@ -535,12 +540,14 @@ constexpr int SMALL_RT = 16;  // raster tiles a quad marks by itself (4 per lane
 constexpr int SMALL_BT = 8;   // bin tiles a quad appends to by itself (2 per lane)
 
 // One setup workgroup: 64 triangles, a quad of lanes each.
-__device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
-                                            uint32_t *cnt, uint32_t (&s_stat)[4]) {
+// frame / lb: the batch frame and this block's index among the frame's setup blocks; draws = the
+// frame's draw slice (table entries dbase ..).
+__device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, int dbase,
+                                            int frame, int lb, uint32_t *cnt, uint32_t (&s_stat)[4]) {
     const int tid = threadIdx.x, lane = __lane_id(), q = lane & 3;
     if (tid < 4) s_stat[tid] = 0u;
     __syncthreads();
-    QuadTri qt = quad_tri(draws, fp.n_draws, fp.n_tris, (int)blockIdx.x * 64 + (tid >> 2));
+    QuadTri qt = quad_tri(draws, fp.n_draws, fp.n_tris, lb * 64 + (tid >> 2));
     const int tri = qt.tri;
     uint32_t flags = TRI_CULLED;
     int gx0 = 0, gx1 = -1, gy0 = 0, gy1 = -1;
@@ -549,9 +556,9 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
         uint2 gb;
         if (qt.uniform) {
             const int d = __builtin_amdgcn_readfirstlane(qt.draw);
-            flags = setup_quad(fp, fb, draws[d], d, tri, gb);
+            flags = setup_quad(fp, fb, draws[d], d, dbase, tri, gb);
         } else {
-            flags = setup_quad(fp, fb, draws[qt.draw], qt.draw, tri, gb);
+            flags = setup_quad(fp, fb, draws[qt.draw], qt.draw, dbase, tri, gb);
         }
         gx0 = lo16(gb.x); gx1 = hi16(gb.x); gy0 = lo16(gb.y); gy1 = hi16(gb.y);
     }
@@ -602,7 +609,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
         wave_append<2>(tcount, key, pos);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
-            if (key[k] >= 0) { append_bin(fp, fb, cnt, key[k], pos[k], (uint32_t)tri); ++n_bin; }
+            if (key[k] >= 0) { append_bin(fp, fb, cnt, frame, key[k], pos[k], (uint32_t)tri); ++n_bin; }
         uint64_t big = __ballot(n_bt > SMALL_BT && q == 0);
         while (big) {
             const int src = __ffsll((unsigned long long)big) - 1;
@@ -615,7 +622,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
                 const int bx = cx0 + k % nx, by = cy0 + k / nx;
                 if (sharded && !owned_bin_tile(fp, bx, by)) continue;
                 const int t = by * fp.tiles_x + bx;
-                append_bin(fp, fb, cnt, t, atomicAdd(&tcount[t], 1u), id);
+                append_bin(fp, fb, cnt, frame, t, atomicAdd(&tcount[t], 1u), id);
                 ++mine;
             }
             for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o);
@@ -630,7 +637,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     if (fp.ghost_list) {   // the unbounded slivers, listed for k_ghost (ids < n_tris: never overflows)
         const bool unb = lead && (flags & TRI_UNBOUNDED);
         const uint32_t slot = wave_append1(&cnt[C_SLIVER], unb);
-        if (unb) fb.slivers[slot] = (uint32_t)tri;
+        if (unb) fb.slivers[slot] = (uint32_t)(frame * fp.n_tris + tri);
     }
     const uint64_t m_setup = __ballot(lead);
     const uint64_t m_ghost = __ballot(lead && (flags & TRI_GHOST));
@@ -643,34 +650,40 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
         atomicAdd(&s_stat[3], n_bin);
     }
     __syncthreads();
-    if (tid == 0) fb.blk_stat[blockIdx.x] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
+    if (tid == 0) fb.blk_stat[frame * fp.setup_blocks + lb] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
 }
 
 template <bool KARG>
-__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
+__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
-    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
-    const DrawGPU *draws = draw_table<KARG>(fb, ka);
+    uint32_t *cnt = fb_all.counters + fp.parity * C_NCOUNTERS;
     const int b = (int)blockIdx.x;
+    // frame of the batch and the block's role inside it
+    const int frame = b / fp.frame_blocks, lb = b - frame * fp.frame_blocks;
+    const FrameBuffers fb = frame_view(fp, fb_all, frame);
+    const int dbase = frame * fp.n_draws;
+    const DrawGPU *draws = draw_table<KARG>(fb_all, ka) + dbase;
     const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
-    // zero the other counter set and bin counts for the next frame (block 0 exists even for an
-    // empty frame)
-    if (b == 0 && threadIdx.x < C_NCOUNTERS) fb.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
+    // zero the other counter set and every frame's other bin-count set for the next batch (block 0
+    // exists even for an empty frame)
+    if (b == 0 && threadIdx.x < C_NCOUNTERS) fb_all.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
     {
         const int n_bt = fp.tiles_x * fp.tiles_y;
-        uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
-        for (int t = b * 256 + (int)threadIdx.x; t < n_bt; t += (int)gridDim.x * 256) next_count[t] = 0u;
+        for (int i = b * 256 + (int)threadIdx.x; i < n_bt * fp.n_frames; i += (int)gridDim.x * 256) {
+            const int f = i / n_bt, t = i - f * n_bt;
+            fb_all.tile_count[((size_t)f * 2 + (fp.parity ^ 1u)) * n_bt + t] = 0u;
+        }
     }
-    if (b < fp.setup_blocks) {
-        setup_block(fp, fb, draws, cnt, s_stat);
-    } else if (b < fp.setup_blocks + fp.ghost_blocks) {
+    if (lb < fp.setup_blocks) {
+        setup_block(fp, fb, draws, dbase, frame, lb, cnt, s_stat);
+    } else if (lb < fp.setup_blocks + fp.ghost_blocks) {
         const int wave = threadIdx.x >> 6;
-        const int gw = (b - fp.setup_blocks) * 4 + wave;
+        const int gw = (lb - fp.setup_blocks) * 4 + wave;
         const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
         if (gw < n_groups * (int)fp.ghost_slices && !(fp.flags & DBG_SKIP_GHOST))
-            ghost_wave(fp, fb, draws, cnt, gw / (int)fp.ghost_slices, gw % (int)fp.ghost_slices, s_ghost[wave]);
+            ghost_wave(fp, fb, draws, cnt, frame, gw / (int)fp.ghost_slices, gw % (int)fp.ghost_slices, s_ghost[wave]);
     }
     if (fb.timeline) {
         __syncthreads();
@@ -689,16 +702,18 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb, 
 // records come from k_setup's stores (identical to the ghost waves' recomputation).
 constexpr int GHOST_LIST_BLOCKS = 512;
 
-__global__ __launch_bounds__(256) void k_ghost(FrameParams fp, FrameBuffers fb) {
-    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
-    const int n = (int)min(cnt[C_SLIVER], (uint32_t)fp.n_tris);
+__global__ __launch_bounds__(256) void k_ghost(FrameParams fp, FrameBuffers fb_all) {
+    uint32_t *cnt = fb_all.counters + fp.parity * C_NCOUNTERS;
+    const int n = (int)min(cnt[C_SLIVER], (uint32_t)fp.n_tris * (uint32_t)fp.n_frames);
     const int waves = (int)gridDim.x * 4, gw = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     const int slices = n > 0 ? max(1, min(16, waves / n)) : 1;
     for (int item = gw; item < n * slices; item += waves) {
         const int s = item / slices, slice = item - s * slices;
-        const uint32_t tri = fb.slivers[s];
+        const uint32_t e = fb_all.slivers[s];   // frame * n_tris + triangle
+        const uint32_t frame = e / (uint32_t)fp.n_tris, tri = e - frame * (uint32_t)fp.n_tris;
+        const FrameBuffers fb = frame_view(fp, fb_all, (int)frame);
         const TriRec t = rec_from(reinterpret_cast<const float4 *>(&fb.recs[tri]));
-        sliver_pixels(fp, fb, cnt, t, tri, slice, 64 * slices);
+        sliver_pixels(fp, fb, cnt, t, tri, frame, slice, 64 * slices);
     }
 }
 
@@ -822,15 +837,17 @@ struct RasterShared {
 // sum of the box areas; passing pairs atomic-min their key into the tile's LDS key array.  Then
 // each thread owns one pixel: the winner's record and varyings are fetched by index, (u, v, w)
 // recomputed with the identical arithmetic, the pixel shaded and written.
+// fb: the frame's view (frame_view); draws: the whole batch's draw table; rt: raster tile of the frame.
 __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
-                                            const uint32_t *cnt, uint32_t n_frag, int rt, const uint2 (&pbx)[CAND / 256],
-                                            bool prefetched, RasterShared &sh, uint64_t *tl) {
+                                            const uint32_t *cnt, uint32_t n_frag, int frame, int rt,
+                                            const uint2 (&pbx)[CAND / 256], bool prefetched, RasterShared &sh, uint64_t *tl) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tls = fp.setup_grid + (int)blockIdx.x;
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
     const int X0 = col * RTW, Y0 = row * RTH;
     const int X1 = X0 + RTW - 1, Y1 = Y0 + RTH - 1;
     const int bt = (row / (TILE / RTH)) * fp.tiles_x + col;
+    const int bt_spill = frame * fp.tiles_x * fp.tiles_y + bt;   // the bin tile's key in spill entries
     __syncthreads();   // the previous tile's key resets are done
 
     // candidate sources.  scan mode: every triangle's bin box.  bin mode: the bin tile's list, then
@@ -870,7 +887,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                     id = bin[item];
                 } else {
                     const uint2 e = fb.spill[item - n_bin];
-                    if ((int)e.x == bt) id = e.y;
+                    if ((int)e.x == bt_spill) id = e.y;
                 }
             }
             ids[k] = id;
@@ -1015,7 +1032,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
         for (uint32_t f = tid; f < n_frag; f += 256) {
             const GhostFrag g = fb.frags[f];
             const int gx = (int)(g.xy & 0xffffu), gy = (int)(g.xy >> 16);
-            if (gx >= X0 && gx <= X1 && gy >= Y0 && gy <= Y1)
+            if (g.frame == (uint32_t)frame && gx >= X0 && gx <= X1 && gy >= Y0 && gy <= Y1)
                 atomicMin(&sh.key[(gy - Y0) * RTW + (gx - X0)], cand_key(g.z, g.id, slot_keys, SLOT_NONE));
         }
     }
@@ -1090,8 +1107,9 @@ __device__ __forceinline__ void clear_tile(const FrameParams &fp, const FrameBuf
     }
 }
 
-// Persistent raster: workgroup b takes owned raster tiles j = b, b + G, b + 2G, ...: the busy ones
-// are rasterized, the others cleared -- every pixel of the frame is written exactly once.
+// Persistent raster: workgroup b takes owned raster tiles j = b, b + G, b + 2G, ... of the whole
+// batch (frame j / n_owned_rt): the busy ones are rasterized, the others cleared -- every pixel of
+// every frame is written exactly once.
 template <bool KARG>
 __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
@@ -1099,6 +1117,8 @@ __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers 
     const uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
     const DrawGPU *draws = draw_table<KARG>(fb, ka);
     const int G = (int)gridDim.x;
+    const int n_rt = fp.tiles_x * fp.rtiles_y;            // raster tiles per frame
+    const int n_all = fp.n_owned_rt * fp.n_frames;        // owned raster tiles of the batch
     const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
@@ -1107,19 +1127,25 @@ __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers 
     // (each costs ~1-2 us at kernel start): the first round's busy flags, the ghost-fragment count,
     // and for small scan-mode scenes every bin box (into registers).
     auto owned_tile = [&](int j) -> int {
-        // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it; -1 past the frame
-        if (j >= fp.n_owned_rt) return -1;
-        const int t = fp.rank + (j >> 2) * fp.count;
-        const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / RTH) + (j & 3);
-        return row < fp.rtiles_y ? row * fp.tiles_x + col : -1;
+        // owned raster tile j of the batch: frame f = j / n_owned_rt; inside it, bin tile
+        // rank + (j' / 4) * count, row (j' % 4); -> f * n_rt + raster tile (the busy-flag index), -1 past
+        // the frame
+        if (j >= n_all) return -1;
+        const int f = j / fp.n_owned_rt, jj = j - f * fp.n_owned_rt;
+        const int t = fp.rank + (jj >> 2) * fp.count;
+        const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / RTH) + (jj & 3);
+        return row < fp.rtiles_y ? f * n_rt + row * fp.tiles_x + col : -1;
     };
     const int rt_first = owned_tile((int)blockIdx.x + tid * G);
     const uint32_t busy_first = rt_first >= 0 ? fb.busy[rt_first] : 0u;
     const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
     static_assert(LDS_DRAWS * 4 == 256, "one per-draw uniform float4 per thread");
-    const float4 du_first = tid < min(fp.n_draws, LDS_DRAWS) * 4 ? reinterpret_cast<const float4 *>(draws[tid >> 2].light)[tid & 3]
-                                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-    const bool prefetched = fp.scan_mode && fp.n_tris <= CAND;
+    const int n_draws_all = fp.n_draws * fp.n_frames;
+    const float4 du_first = tid < min(n_draws_all, LDS_DRAWS) * 4 ? reinterpret_cast<const float4 *>(draws[tid >> 2].light)[tid & 3]
+                                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    // small single-frame scan-mode scenes: every bin box in registers from the start (batches load
+    // each busy tile's frame's boxes, L2-resident)
+    const bool prefetched = fp.scan_mode && fp.n_tris <= CAND && fp.n_frames == 1;
     uint2 pbx[CAND / 256];
 #pragma unroll
     for (int k = 0; k < CAND / 256; ++k) {
@@ -1130,9 +1156,9 @@ __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers 
     // round trip after the busy flags)
 #pragma unroll
     for (int k = 0; k < CAND / 256; ++k) asm volatile("" : "+v"(pbx[k].x), "+v"(pbx[k].y));
-    if (tid < min(fp.n_draws, LDS_DRAWS) * 4) sh.du[tid] = du_first;
+    if (tid < min(n_draws_all, LDS_DRAWS) * 4) sh.du[tid] = du_first;
     bool first = true;
-    for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
+    for (int j0 = (int)blockIdx.x; j0 < n_all; j0 += 256 * G) {
         __syncthreads();
         if (tid == 0) sh.nbusy = 0;
         __syncthreads();
@@ -1149,18 +1175,22 @@ __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers 
         // busy tiles first (latency-bound), then the clears (streaming stores that other workgroups'
         // busy tiles overlap with)
         for (int i = 0; i < nb; ++i) {
-            const int rt = sh.busy[i];
+            const int g = sh.busy[i], f = g / n_rt, rt = g - f * n_rt;
+            const FrameBuffers fv = frame_view(fp, fb, f);
             if (fp.flags & DBG_CLEAR_ONLY) {
                 __syncthreads();
-                clear_tile(fp, fb, rt);
-                if (tid == 0) fb.busy[rt] = 0u;
+                clear_tile(fp, fv, rt);
+                if (tid == 0) fv.busy[rt] = 0u;
                 continue;
             }
-            if (fp.flags & DBG_TWICE) raster_tile(fp, fb, draws, cnt, n_frag, rt, pbx, prefetched, sh, nullptr);   // warm run
-            raster_tile(fp, fb, draws, cnt, n_frag, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
+            if (fp.flags & DBG_TWICE) raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
+            raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
             first = false;
         }
-        for (int i = 0; i < ne; ++i) clear_tile(fp, fb, sh.busy[255 - i]);
+        for (int i = 0; i < ne; ++i) {
+            const int g = sh.busy[255 - i], f = g / n_rt;
+            clear_tile(fp, frame_view(fp, fb, f), g - f * n_rt);
+        }
     }
     __syncthreads();
     if (tid == 0) {
@@ -1181,8 +1211,8 @@ namespace shs_internal {
 using namespace shs_dev;
 
 hipError_t launch_setup(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, hipStream_t s) {
-    const int grid = fp.setup_blocks + fp.ghost_blocks + fp.clear_blocks;
-    if (fp.n_draws <= KARG_DRAWS)
+    const int grid = fp.setup_grid;   // n_frames * frame_blocks
+    if (fp.n_draws * fp.n_frames <= KARG_DRAWS)   // the whole batch's draws travel as kernel arguments
         hipLaunchKernelGGL(k_setup<true>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
     else
         hipLaunchKernelGGL(k_setup<false>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
@@ -1195,7 +1225,7 @@ hipError_t launch_ghost(const FrameParams &fp, const FrameBuffers &fb, hipStream
 }
 
 hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, int grid, hipStream_t s) {
-    if (fp.n_draws <= KARG_DRAWS)
+    if (fp.n_draws * fp.n_frames <= KARG_DRAWS)   // the whole batch's draws travel as kernel arguments
         hipLaunchKernelGGL(k_raster<true>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
     else
         hipLaunchKernelGGL(k_raster<false>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);

@@ -41,9 +41,14 @@ __global__ __launch_bounds__(256) void k_tonemap(TonemapParams p) {
     if (p.present) __builtin_nontemporal_store(rgba, &p.present[(size_t)(p.H - 1 - y) * p.W + x]);
 }
 
-// std::lround then the (int) cast of the reference: half away from zero, 64-bit, then truncated
-// (NaN and out-of-range values end up 0 or clamped exactly like x86-64's lround + cast).
-__device__ __forceinline__ int lround_int(float v) { return (int)(long long)roundf(v); }
+// std::lround then the (int) cast of the reference: half away from zero, 64-bit, then truncated.
+// x86-64's lround returns LONG_MIN (cvtss2si's "integer indefinite") for NaN and |v| >= 2^63, and
+// the (int) cast of LONG_MIN is 0; on AMDGPU that conversion would be poison, so it is explicit.
+__device__ __forceinline__ int lround_int(float v) {
+    const float r = roundf(v);
+    if (!(fabsf(r) < 9.2233720e18f)) return 0;
+    return (int)(long long)r;
+}
 
 __device__ __forceinline__ int clamp_i(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 

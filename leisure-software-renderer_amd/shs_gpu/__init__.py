@@ -146,6 +146,31 @@ class Context:
     def render(self, frame: Frame, draws):
         self.render_prepared(self.prepare(frame, draws))
 
+    def prepare_batch(self, frame: Frame, frames_draws):
+        """frames_draws: one draw list per frame (equal lengths and triangle counts) -> prepared batch."""
+        n = len(frames_draws[0])
+        assert all(len(d) == n for d in frames_draws), "every frame of a batch has the same number of draws"
+        flat = [d for fd in frames_draws for d in fd]
+        return frame, frame.desc(), self._draw_array(flat), n, len(frames_draws)
+
+    def render_batch_prepared(self, prepared):
+        frame, desc, arr, n, n_frames = prepared
+        self._check(self._lib.shs_render_legacy_batch(self._h, ctypes.byref(desc), arr, n, n_frames))
+        self._frame = frame
+        self._n_frames = n_frames
+
+    def render_batch(self, frame: Frame, frames_draws):
+        """shs_render_legacy_batch: one k_setup + k_raster pair renders every frame of the batch."""
+        self.render_batch_prepared(self.prepare_batch(frame, frames_draws))
+
+    def resolve_frame(self, index: int):
+        f = self._frame
+        color = np.empty((f.height, f.width, 4), dtype=np.uint8)
+        depth = np.empty((f.height, f.width), dtype=np.float32)
+        self._check(self._lib.shs_resolve_frame(self._h, int(index), color.ctypes.data_as(ctypes.c_void_p),
+                                                depth.ctypes.data_as(ctypes.c_void_p)))
+        return color, depth
+
     def synchronize(self):
         self._check(self._lib.shs_synchronize(self._h))
 

@@ -178,7 +178,10 @@ SIGNATURES = [
     ("shs_mesh_upload_soup", ctypes.c_int, [_P, _F, _F, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     ("shs_mesh_release", ctypes.c_int, [_P, ctypes.c_int32]),
     ("shs_render_legacy", ctypes.c_int, [_P, ctypes.POINTER(FrameDesc), ctypes.POINTER(LegacyDraw), ctypes.c_int32]),
+    ("shs_render_legacy_batch", ctypes.c_int, [_P, ctypes.POINTER(FrameDesc), ctypes.POINTER(LegacyDraw), ctypes.c_int32,
+                                               ctypes.c_int32]),
     ("shs_resolve", ctypes.c_int, [_P, _P, _P]),
+    ("shs_resolve_frame", ctypes.c_int, [_P, ctypes.c_int32, _P, _P]),
     ("shs_resolve_prequant", ctypes.c_int, [_P, _P]),
     ("shs_device_framebuffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("shs_get_stats", ctypes.c_int, [_P, ctypes.POINTER(RasterStats)]),

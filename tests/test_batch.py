@@ -1,0 +1,164 @@
+"""Frame batches (shs_render_legacy_batch): one k_setup + k_raster pair renders n_frames independent
+frames; every frame must be bit-identical to the frame shs_render_legacy renders from the same draws
+(and hence to the oracle).  Covers scan mode (C2 poses), bin mode with spill (C3 + tiny bin
+capacity), ghost fragments of unbounded slivers in both modes, shards, and the validation rules."""
+import numpy as np
+import pytest
+
+from helpers import FLT_MAX, assert_color_parity, assert_depth_bitexact
+from test_gpu_parity import _hair_soup, _identity_draw, _ndc_soup
+
+pytestmark = pytest.mark.gpu
+
+
+def _poses(n, shading=3, width=1920, height=1080):
+    from shs_gpu import scene
+    out = []
+    for k in range(n):
+        frame, draws = scene.monkey_scene(width, height, shading, yaw=-20.0 + 5.5 * k, pitch=-4.0 + 1.5 * k,
+                                          rotation=13.0 * k)
+        out.append(draws)
+    return frame, out
+
+
+def _singles(ctx, frame, frames_draws):
+    res = []
+    for d in frames_draws:
+        ctx.render(frame, d)
+        c, z = ctx.resolve()
+        res.append((c, z, ctx.stats()))
+    return res
+
+
+def _owned_mask(frame):
+    """Screen-row mask of the pixels a shard owns (32x32 tiles, tile % count == rank)."""
+    T = 32
+    ty, tx = np.mgrid[0:frame.height, 0:frame.width] // T
+    tiles_x = (frame.width + T - 1) // T
+    return (ty * tiles_x + tx) % frame.shard_count == frame.shard_rank
+
+
+def _assert_batch_equals_singles(ctx, frame, frames_draws, before_batch=None):
+    singles = _singles(ctx, frame, frames_draws)
+    if before_batch is not None:
+        before_batch(ctx)
+    ctx.render_batch(frame, frames_draws)
+    st = ctx.stats()
+    m = _owned_mask(frame)   # a shard writes only its own tiles; the rest of the buffer is stale
+    for k, (c1, z1, _) in enumerate(singles):
+        c, z = ctx.resolve_frame(k)
+        if frame.shard_count > 1:
+            z, z1 = np.where(m, z, 0.0), np.where(m, z1, 0.0)
+            mc = m[::-1][..., None]   # colour is in canvas rows
+            c, c1 = np.where(mc, c, 0), np.where(mc, c1, 0)
+        assert np.array_equal(z.view(np.uint32), z1.view(np.uint32)), f"frame {k}: depth differs from the single render"
+        assert np.array_equal(c, c1), f"frame {k}: colour differs from the single render"
+    assert st["tri_input"] == sum(s["tri_input"] for _, _, s in singles)
+    assert st["covered_pixels"] == sum(s["covered_pixels"] for _, _, s in singles)
+    return singles, st
+
+
+@pytest.mark.parametrize("n_frames", [1, 2, 7, 16])
+def test_batch_c2_poses_match_single_frames(gpu_ctx, n_frames):
+    frame, fd = _poses(n_frames)
+    _assert_batch_equals_singles(gpu_ctx, frame, fd)
+
+
+def test_batch_frames_match_oracle(gpu_ctx, oracle_mod):
+    """Frames 0 and the last of a mixed-shading 640x480 batch against the CPU oracle directly."""
+    from shs_gpu import scene
+    fds = []
+    for k, sh in enumerate([3, 2, 1, 0, 3]):
+        frame, draws = scene.monkey_scene(640, 480, sh, yaw=7.0 * k - 10.0, pitch=2.0 * k, rotation=31.0 * k,
+                                          cam_pos=(0.0, 5.0, -12.0))
+        fds.append(draws)
+    frame.prequant = True
+    gpu_ctx.render_batch(frame, fds)
+    for k in (0, len(fds) - 1):
+        c, z = gpu_ctx.resolve_frame(k)
+        rc, rd, rpq = oracle_mod.render_legacy(frame.width, frame.height, fds[k], threads=8, prequant=True)
+        assert_depth_bitexact(z, rd)
+        # bytes may only differ at truncation boundaries; without the batch prequant, require <= 1 and few
+        d8 = np.abs(c.astype(np.int16) - rc.astype(np.int16))
+        assert d8.max() <= 1 and (d8 > 0).sum() <= 8
+        assert np.array_equal(c[..., 3], rc[..., 3])
+
+
+def test_batch_c3_bins_with_spill(oracle_mod):
+    """C3 grid (bin mode) at 960x540, three poses, bin capacity 4: most entries spill to the shared
+    spill list whose entries carry the frame's bin tile."""
+    import shs_gpu
+    from shs_gpu import scene
+    fds = []
+    for k in range(3):
+        frame, draws = scene.grid_scene(960, 540, n=4, yaw=-6.0 + 6.0 * k)
+        fds.append(draws)
+    ctx = shs_gpu.Context(0)
+    try:
+        ctx.set_raster_mode(2)
+        # the context grows the capacity to the fullest tile it has seen: shrink it again for the batch
+        _, st = _assert_batch_equals_singles(ctx, frame, fds, before_batch=lambda c: c.set_bin_capacity(4))
+        assert st["spilled"] > 0
+        c, z = ctx.resolve_frame(2)
+        rc, rd, _ = oracle_mod.render_legacy(frame.width, frame.height, fds[2], threads=8)
+        assert_depth_bitexact(z, rd)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("mode", [1, 2], ids=["scan", "bins"])
+def test_batch_hair_slivers_ghost_fragments(mode):
+    """Unbounded slivers emit ghost fragments tagged with their frame (ghost waves in scan mode, the
+    sliver list + k_ghost in bin mode); frames with different slivers must not see each other's."""
+    import shs_gpu
+    from shs_gpu.scene import Mesh
+    W, H = 400, 300
+    fds = []
+    for seed in (99, 100, 101):
+        rng = np.random.default_rng(seed)
+        pos, nrm = _hair_soup(rng, W, H, 1500)
+        fds.append([_identity_draw(Mesh(pos, nrm), 3)])
+    ctx = shs_gpu.Context(0)
+    try:
+        ctx.set_raster_mode(mode)
+        _, st = _assert_batch_equals_singles(ctx, shs_gpu.Frame(W, H), fds)
+        assert st["ghost_fragments"] > 0
+    finally:
+        ctx.close()
+
+
+def test_batch_sharded_frames(gpu_ctx):
+    """Shard ownership applies to every frame of the batch."""
+    import shs_gpu
+    _, fd = _poses(3, width=640, height=480)
+    frame = shs_gpu.Frame(640, 480, shard_rank=1, shard_count=3)
+    _assert_batch_equals_singles(gpu_ctx, frame, fd)
+
+
+def test_batch_soup_multi_draw_device_table(gpu_ctx):
+    """2 draws x 4 frames = 8 draws: the device draw table (more than fit in kernel arguments)."""
+    import shs_gpu
+    from shs_gpu.scene import Mesh
+    W, H = 333, 241
+    fds = []
+    for seed in range(4):
+        rng = np.random.default_rng(40 + seed)
+        pos, nrm = _ndc_soup(rng, W, H, 600)
+        fds.append([_identity_draw(Mesh(pos[:300], nrm[:300]), seed % 4), _identity_draw(Mesh(pos[300:], nrm[300:]), 3)])
+    _assert_batch_equals_singles(gpu_ctx, shs_gpu.Frame(W, H), fds)
+
+
+def test_batch_validation(gpu_ctx):
+    import shs_gpu
+    from shs_gpu import ShsError
+    from shs_gpu.scene import Mesh
+    frame, fd = _poses(2, width=320, height=240)
+    rng = np.random.default_rng(1)
+    pos, nrm = _ndc_soup(rng, 320, 240, 50)
+    with pytest.raises(ShsError):   # unequal triangle counts across frames
+        gpu_ctx.render_batch(frame, [fd[0], [_identity_draw(Mesh(pos, nrm))]])
+    gpu_ctx.render_batch(frame, fd)
+    with pytest.raises(ShsError):
+        gpu_ctx.resolve_frame(2)
+    c, z = gpu_ctx.resolve_frame(1)
+    assert (z < FLT_MAX).sum() > 0

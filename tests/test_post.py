@@ -24,7 +24,7 @@ def _emulate(s, exposure, thr):
     return out
 
 
-@pytest.mark.parametrize("gamma", [2.2, 1.0, 1.8, 0.5])
+@pytest.mark.parametrize("gamma", [2.2, 1.0, 1.8, 0.5, 0.0, -1.0])
 def test_thresholds_match_reference_bytes(oracle_mod, gamma):
     import shs_gpu
     thr = shs_gpu.Context.tonemap_thresholds(gamma)
@@ -64,7 +64,7 @@ def _c5(W, H):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("exposure,gamma", [(1.0, 2.2), (2.5, 2.2), (0.7, 1.0), (1.0, 1.6)])
+@pytest.mark.parametrize("exposure,gamma", [(1.0, 2.2), (2.5, 2.2), (0.7, 1.0), (1.0, 1.6), (1.0, -1.0), (3.0, 0.0)])
 def test_tonemap_rendered_frame_exact(oracle_mod, exposure, gamma):
     import shs_gpu
     frame, draws = _c5(352, 200)
@@ -204,3 +204,35 @@ def test_motion_blur_requires_inputs():
         ctx.tonemap(ldr=False, present=True)
         with pytest.raises(ShsError):
             ctx.motion_blur()                         # the tonemap wrote no RT_ColorLDR
+
+
+@pytest.mark.gpu
+def test_motion_blur_nonfinite_motion_exact(oracle_mod):
+    """NaN / +-inf / huge motion vectors: the taps' lround of a NaN coordinate is x86-64's
+    LONG_MIN cast to int (0), restated explicitly in the kernel."""
+    import torch
+    import shs_gpu
+    frame, draws = _c5(160, 96)
+    H, W = frame.height, frame.width
+    rng = np.random.default_rng(11)
+    mot = rng.uniform(-40, 40, size=(H, W, 2)).astype(np.float32)
+    special = np.array([np.nan, np.inf, -np.inf, 3e38, -3e38, 1e20, np.nan, 0.0], np.float32)
+    sel = rng.integers(0, special.size, size=(H, W, 2))
+    mask = rng.random((H, W, 2)) < 0.3
+    mot[mask] = special[sel[mask]]
+    with shs_gpu.Context(0) as ctx:
+        ctx.render_pbr_forward(frame, draws)
+        ctx.synchronize_lib()
+        dev_motion = ctx.lib_device_targets()[2]
+        src = torch.from_numpy(mot.reshape(-1)).to("cuda:0")
+        torch.cuda.synchronize()
+        _memcpy_d2d(dev_motion, src.data_ptr(), mot.nbytes)
+        ctx.tonemap(1.0, 2.2, ldr=True, present=False)
+        ctx.motion_blur(min_velocity_px=0.0)
+        got, _ = ctx.resolve_motion_blur()
+        ldr, _ = ctx.resolve_ldr()
+        _, depth, motion = ctx.resolve_lib()
+    assert np.array_equal(motion.view(np.uint32), mot.view(np.uint32)), "injected motion was overwritten"
+    want = oracle_mod.motion_blur(ldr, depth, motion, min_velocity_px=0.0)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, f"{len(bad)} byte mismatches, first {bad[:4]}"
