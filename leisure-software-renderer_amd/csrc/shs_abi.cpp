@@ -77,7 +77,7 @@ int shs_destroy(shs_ctx *ctx) {
     shs_lib_release(ctx);
     release(ctx->draws); release(ctx->recs); release(ctx->shade); release(ctx->tile_count); release(ctx->bins);
     release(ctx->spill); release(ctx->frags); release(ctx->counters); release(ctx->busy); release(ctx->boxes);
-    release(ctx->slivers);
+    release(ctx->slivers); release(ctx->busy_list);
     release(ctx->blk_stat); release(ctx->rstat); release(ctx->timeline);
     release(ctx->color); release(ctx->depth); release(ctx->prequant);
     for (int i = 0; i < 2; ++i) {
@@ -223,6 +223,7 @@ static int enqueue_frame(shs_ctx *ctx) {
         if (ensure(ctx, ctx->busy, (size_t)n_rt * n_frames)) return SHS_ERR_HIP;
         reset = true;
     }
+    if (ensure(ctx, ctx->busy_list, (size_t)n_rt * n_frames)) return SHS_ERR_HIP;
     if (reset) {
         HIP_TRY(ctx, hipMemsetAsync(ctx->tile_count.p, 0, ctx->tile_count.cap * sizeof(uint32_t), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(ctx->busy.p, 0, ctx->busy.cap * sizeof(uint32_t), ctx->stream));
@@ -301,6 +302,8 @@ static int enqueue_frame(shs_ctx *ctx) {
         fp.ghost_slices = (uint32_t)std::min(16, std::max(1, 1024 / n_groups));
     }
     fp.parity = ctx->frame_index & 1u;
+    if (++ctx->busy_epoch == 0u) ctx->busy_epoch = 1u;   // busy[] is zeroed on reset; 0 is never an epoch
+    fp.epoch = ctx->busy_epoch;
     fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;
@@ -329,6 +332,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fb.spill = ctx->spill.p; fb.frags = ctx->frags.p; fb.counters = ctx->counters.p;
     fb.slivers = ctx->slivers.p;
     fb.busy = ctx->busy.p;
+    fb.busy_list = ctx->busy_list.p;
     fb.blk_stat = ctx->blk_stat.p;
     fb.rstat = ctx->rstat.p;
     fb.timeline = ctx->want_timeline ? ctx->timeline.p : nullptr;

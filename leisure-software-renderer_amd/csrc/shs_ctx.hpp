@@ -52,7 +52,9 @@ struct shs_ctx {
     DevBuf<uint32_t> slivers;        // unbounded sliver ids (ghost_list mode)
     DevBuf<uint2> boxes;             // per-triangle bin boxes
     DevBuf<uint32_t> counters;       // 2 parity sets
-    DevBuf<uint32_t> busy;           // per raster tile
+    DevBuf<uint32_t> busy;           // per raster tile: the epoch of the last launch that marked it
+    DevBuf<uint32_t> busy_list;      // busy tiles of the batch (k_raster's work items)
+    uint32_t busy_epoch = 0;         // FrameParams::epoch of the last launch (never 0)
     DevBuf<uint4> blk_stat;          // per setup block
     DevBuf<uint2> rstat;             // per raster block
     DevBuf<uint64_t> timeline;       // SHS_OPT_TIMELINE

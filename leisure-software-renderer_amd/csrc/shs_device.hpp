@@ -83,7 +83,8 @@ constexpr double GHOST_MAX_EXPAND = 48.0;  // larger danger boxes are handled as
 
 // counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one).
 // Only the append positions and the overflow flags live here; statistics go to per-block slots.
-constexpr int C_OVERFLOW = 0, C_SPILL = 1, C_FRAG = 2, C_SLIVER = 3, C_NCOUNTERS = 4;
+// C_BUSY: entries of the busy-tile list (k_setup / k_ghost); C_WORK: k_raster's work-item ticket.
+constexpr int C_OVERFLOW = 0, C_SPILL = 1, C_FRAG = 2, C_SLIVER = 3, C_BUSY = 4, C_WORK = 5, C_NCOUNTERS = 6;
 constexpr uint32_t OV_SPILL = 1u, OV_FRAG = 2u;
 
 // Timing-experiment switches (frame flags bits 8+; results are WRONG with any of them set): they
@@ -138,6 +139,7 @@ struct FrameParams {
     // the n_frames * n_owned_rt raster tiles of the whole batch.
     int32_t n_frames;
     int32_t frame_blocks;
+    uint32_t epoch;                  // busy[] value that means "busy in this launch" (never 0)
 };
 
 // Device buffers.  "per frame" buffers hold n_frames consecutive copies (frame_view() offsets them);
@@ -153,8 +155,10 @@ struct FrameBuffers {
     uint32_t *slivers;               // n_frames * n_tris: unbounded slivers, f * n_tris + tri (ghost_list)
     uint2 *boxes;                    // per frame: n_tris packed bin boxes (gbx, gby); empty for culled
     uint32_t *counters;              // 2 * C_NCOUNTERS
-    uint32_t *busy;                  // per frame, per raster tile: 1 = has candidates / fragments
-                                     // (k_raster resets)
+    uint32_t *busy;                  // per frame, per raster tile: == fp.epoch when the tile has
+                                     // candidates / fragments in this launch (no reset needed)
+    uint32_t *busy_list;             // C_BUSY entries f * n_raster_tiles + raster tile, each busy tile of
+                                     // the batch once (capacity n_frames * n_raster_tiles)
     uint4 *blk_stat;                 // per setup block: (set up, ghost, unbounded, bin entries)
     uint2 *rstat;                    // per raster block: (covered pixels, fullest bin seen)
     uint64_t *timeline;              // optional: TL_STRIDE slots per workgroup, k_setup then k_raster:

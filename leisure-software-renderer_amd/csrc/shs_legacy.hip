@@ -255,6 +255,44 @@ __device__ __forceinline__ bool owned_bin_tile(const FrameParams &fp, int bx, in
     return ((by * fp.tiles_x + bx) % fp.count) == fp.rank;
 }
 
+// ---- busy tiles --------------------------------------------------------------------------------
+// A raster tile is busy in this launch when busy[rt] == fp.epoch.  The first marker of a tile (the
+// atomic exchange returns another value) also enters it into the batch's busy list exactly once;
+// k_raster deals the list out as work items.
+__device__ __forceinline__ uint32_t busy_entry(const FrameParams &fp, int frame, int rt) {
+    return (uint32_t)(frame * fp.tiles_x * fp.rtiles_y + rt);
+}
+
+// Mark and append directly (rare callers: ghost fragments).
+__device__ __forceinline__ void mark_busy_direct(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int frame,
+                                                 int rt) {
+    if (atomicExch(&fb.busy[rt], fp.epoch) != fp.epoch) fb.busy_list[atomicAdd(&cnt[C_BUSY], 1u)] = busy_entry(fp, frame, rt);
+}
+
+// Setup blocks collect their newly busy tiles in LDS and append them with one atomic per block.
+constexpr int NEW_BUSY_CAP = 1024;
+struct NewBusy {
+    uint32_t n, base;
+    uint32_t e[NEW_BUSY_CAP];
+};
+
+__device__ __forceinline__ void mark_busy(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int frame, int rt,
+                                          NewBusy &nb) {
+    if (atomicExch(&fb.busy[rt], fp.epoch) == fp.epoch) return;
+    const uint32_t k = atomicAdd(&nb.n, 1u);
+    if (k < (uint32_t)NEW_BUSY_CAP) nb.e[k] = busy_entry(fp, frame, rt);
+    else fb.busy_list[atomicAdd(&cnt[C_BUSY], 1u)] = busy_entry(fp, frame, rt);
+}
+
+// Block-wide (all threads, after the marks): append the block's collected tiles.
+__device__ __forceinline__ void flush_busy(const FrameBuffers &fb, uint32_t *cnt, NewBusy &nb) {
+    __syncthreads();
+    const uint32_t n = min(nb.n, (uint32_t)NEW_BUSY_CAP);
+    if (threadIdx.x == 0 && n) nb.base = atomicAdd(&cnt[C_BUSY], n);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) fb.busy_list[nb.base + i] = nb.e[i];
+}
+
 // ---- ghost waves ------------------------------------------------------------------------------
 // The pixels the reference's tile clamp makes an unbounded sliver visit OUTSIDE its integer bbox
 // (blinn_phong_shading.cpp:208-224: per 80x80 tile job, the float bbox clamped to the tile).  The
@@ -401,7 +439,7 @@ __device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const Frame
                 g.frame = frame;
                 g.pad[0] = g.pad[1] = 0u;
                 fb.frags[slot] = g;
-                fb.busy[(py / RTH) * fp.tiles_x + px / RTW] = 1u;
+                mark_busy_direct(fp, fb, cnt, (int)frame, (py / RTH) * fp.tiles_x + px / RTW);
             } else {
                 atomicOr(&cnt[C_OVERFLOW], OV_FRAG);
             }
@@ -543,9 +581,10 @@ constexpr int SMALL_BT = 8;   // bin tiles a quad appends to by itself (2 per la
 // frame / lb: the batch frame and this block's index among the frame's setup blocks; draws = the
 // frame's draw slice (table entries dbase ..).
 __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, int dbase,
-                                            int frame, int lb, uint32_t *cnt, uint32_t (&s_stat)[4]) {
+                                            int frame, int lb, uint32_t *cnt, uint32_t (&s_stat)[4], NewBusy &nb) {
     const int tid = threadIdx.x, lane = __lane_id(), q = lane & 3;
     if (tid < 4) s_stat[tid] = 0u;
+    if (tid == 0) nb.n = 0u;
     __syncthreads();
     QuadTri qt = quad_tri(draws, fp.n_draws, fp.n_tris, lb * 64 + (tid >> 2));
     const int tri = qt.tri;
@@ -574,7 +613,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     if (n_rt > 0 && n_rt <= SMALL_RT) {
         for (int k = q; k < n_rt; k += 4) {
             const int rx = rx0 + k % nrx, ry = ry0 + k / nrx;
-            if (!sharded || owned_bin_tile(fp, rx, ry / (TILE / RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+            if (!sharded || owned_bin_tile(fp, rx, ry / (TILE / RTH))) mark_busy(fp, fb, cnt, frame, ry * fp.tiles_x + rx, nb);
         }
     }
     {
@@ -586,10 +625,11 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
             const int nx = bx1 - bx0 + 1, n = nx * (by1 - by0 + 1);
             for (int k = lane; k < n; k += 64) {
                 const int rx = bx0 + k % nx, ry = by0 + k / nx;
-                if (!sharded || owned_bin_tile(fp, rx, ry / (TILE / RTH))) fb.busy[ry * fp.tiles_x + rx] = 1u;
+                if (!sharded || owned_bin_tile(fp, rx, ry / (TILE / RTH))) mark_busy(fp, fb, cnt, frame, ry * fp.tiles_x + rx, nb);
             }
         }
     }
+    flush_busy(fb, cnt, nb);
     tl_mark(fb.timeline, blockIdx.x, 2);
 
     // -- bin appends (large scenes): bin tiles of the bin box, two per quad lane
@@ -657,6 +697,7 @@ template <bool KARG>
 __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
+    __shared__ NewBusy s_new;
     uint32_t *cnt = fb_all.counters + fp.parity * C_NCOUNTERS;
     const int b = (int)blockIdx.x;
     // frame of the batch and the block's role inside it
@@ -677,7 +718,7 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_a
         }
     }
     if (lb < fp.setup_blocks) {
-        setup_block(fp, fb, draws, dbase, frame, lb, cnt, s_stat);
+        setup_block(fp, fb, draws, dbase, frame, lb, cnt, s_stat, s_new);
     } else if (lb < fp.setup_blocks + fp.ghost_blocks) {
         const int wave = threadIdx.x >> 6;
         const int gw = (lb - fp.setup_blocks) * 4 + wave;
@@ -827,8 +868,8 @@ struct RasterShared {
     uint32_t id[RCHUNK];
     uint32_t cand[CAND];
     float4 du[LDS_DRAWS * 4];         // per-draw {light, cam, ocol, colf} (4 KB)
-    int busy[256];                    // this workgroup's busy tiles
-    uint32_t nc, nbusy, cov, maxbin, npairs;
+    uint8_t skip[512];                // clear strip: per raster tile across, 1 = not cleared (busy / not owned)
+    uint32_t nc, item, cov, maxbin, npairs;
     uint8_t wown[PAIR_WORDS];         // staged candidate owning each bitmap word's first pair
 };
 
@@ -1090,7 +1131,6 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
         __builtin_nontemporal_store(depth, &fb.depth[(size_t)py * fp.W + px]);
         if (fb.prequant) fb.prequant[(size_t)(fp.H - 1 - py) * fp.W + px] = pq;
     }
-    if (tid == 0) fb.busy[rt] = 0u;   // clean for the next frame
     tl_mark(tl, tls, 5);
 }
 
@@ -1107,37 +1147,74 @@ __device__ __forceinline__ void clear_tile(const FrameParams &fp, const FrameBuf
     }
 }
 
-// Persistent raster: workgroup b takes owned raster tiles j = b, b + G, b + 2G, ... of the whole
-// batch (frame j / n_owned_rt): the busy ones are rasterized, the others cleared -- every pixel of
-// every frame is written exactly once.
+// One clear strip: raster-tile row ry of frame f, full width -- every pixel of the row's tiles that
+// are owned and not busy gets the clear colour (canvas rows) and FLT_MAX (screen rows), as 16-B
+// stores (4 pixels per lane) along whole rows when W % 4 == 0.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBuffers &fb, int f, int ry, RasterShared &sh) {
+    const int tid = threadIdx.x;
+    const FrameBuffers fv = frame_view(fp, fb, f);
+    __syncthreads();   // sh.skip of the previous strip is no longer read
+    for (int t = tid; t < fp.tiles_x; t += 256)
+        sh.skip[t] = (uint8_t)(fv.busy[ry * fp.tiles_x + t] == fp.epoch ||
+                               (fp.count > 1 && !owned_bin_tile(fp, t, ry / (TILE / RTH))));
+    __syncthreads();
+    const int y0 = ry * RTH, y1 = min(y0 + RTH, fp.H);
+    uint32_t *color = reinterpret_cast<uint32_t *>(fv.color);
+    if ((fp.W & 3) == 0) {
+        const int ng = fp.W >> 2;
+        const u32x4 c4 = {fp.clear_rgba, fp.clear_rgba, fp.clear_rgba, fp.clear_rgba};
+        const f32x4 d4 = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+        for (int y = y0; y < y1; ++y) {
+            u32x4 *crow = reinterpret_cast<u32x4 *>(color + (size_t)(fp.H - 1 - y) * fp.W);
+            f32x4 *drow = reinterpret_cast<f32x4 *>(fv.depth + (size_t)y * fp.W);
+            for (int g = tid; g < ng; g += 256) {
+                if (sh.skip[g >> 3]) continue;   // 8 groups of 4 px per 32-px tile
+                __builtin_nontemporal_store(c4, &crow[g]);
+                __builtin_nontemporal_store(d4, &drow[g]);
+                if (fv.prequant) {
+                    float4 *pq = fv.prequant + (size_t)(fp.H - 1 - y) * fp.W + 4 * g;
+                    pq[0] = pq[1] = pq[2] = pq[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+        }
+    } else {
+        for (int y = y0; y < y1; ++y) {
+            for (int x = tid; x < fp.W; x += 256) {
+                if (sh.skip[x >> 5]) continue;
+                const size_t c = (size_t)(fp.H - 1 - y) * fp.W + x;
+                __builtin_nontemporal_store(fp.clear_rgba, &color[c]);
+                __builtin_nontemporal_store(FLT_MAX, &fv.depth[(size_t)y * fp.W + x]);
+                if (fv.prequant) fv.prequant[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    }
+}
+
+// Persistent raster over the whole batch.  Work items are the busy tiles (the busy list k_setup /
+// k_ghost built: latency-bound raster) and the clear strips (one raster-tile row of one frame:
+// streaming stores), interleaved in proportion so that every CU mixes both kinds at all times, and
+// handed out dynamically (one ticket atomic per item, fetched one item ahead).  Every owned pixel of
+// every frame is written exactly once: by its busy tile or by its strip.
 template <bool KARG>
 __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
     const int tid = threadIdx.x;
-    const uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
+    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
     const DrawGPU *draws = draw_table<KARG>(fb, ka);
-    const int G = (int)gridDim.x;
     const int n_rt = fp.tiles_x * fp.rtiles_y;            // raster tiles per frame
-    const int n_all = fp.n_owned_rt * fp.n_frames;        // owned raster tiles of the batch
     const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
     sh.key[tid] = KEY_EMPTY;
-    // Every independent first-touch load is issued up front so their HBM/MALL round trips overlap
-    // (each costs ~1-2 us at kernel start): the first round's busy flags, the ghost-fragment count,
-    // and for small scan-mode scenes every bin box (into registers).
-    auto owned_tile = [&](int j) -> int {
-        // owned raster tile j of the batch: frame f = j / n_owned_rt; inside it, bin tile
-        // rank + (j' / 4) * count, row (j' % 4); -> f * n_rt + raster tile (the busy-flag index), -1 past
-        // the frame
-        if (j >= n_all) return -1;
-        const int f = j / fp.n_owned_rt, jj = j - f * fp.n_owned_rt;
-        const int t = fp.rank + (jj >> 2) * fp.count;
-        const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / RTH) + (jj & 3);
-        return row < fp.rtiles_y ? f * n_rt + row * fp.tiles_x + col : -1;
-    };
-    const int rt_first = owned_tile((int)blockIdx.x + tid * G);
-    const uint32_t busy_first = rt_first >= 0 ? fb.busy[rt_first] : 0u;
+    // Every independent first-touch load is issued up front so their round trips overlap: the first
+    // work ticket, the busy-list length, the ghost-fragment count, the draws' shading uniforms and, for
+    // a small single-frame scan-mode scene, every bin box (into registers).
+    uint32_t ticket = 0u;
+    if (tid == 0) ticket = atomicAdd(&cnt[C_WORK], 1u);
+    const uint32_t n_busy = min(cnt[C_BUSY], (uint32_t)(n_rt * fp.n_frames));
     const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
     static_assert(LDS_DRAWS * 4 == 256, "one per-draw uniform float4 per thread");
     const int n_draws_all = fp.n_draws * fp.n_frames;
@@ -1153,44 +1230,40 @@ __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers 
         pbx[k] = (prefetched && i < fp.n_tris) ? fb.boxes[i] : make_uint2(0u, 0u);
     }
     // pin the box loads here (the compiler would otherwise sink them to their first use, a second
-    // round trip after the busy flags)
+    // round trip after the ticket)
 #pragma unroll
     for (int k = 0; k < CAND / 256; ++k) asm volatile("" : "+v"(pbx[k].x), "+v"(pbx[k].y));
     if (tid < min(n_draws_all, LDS_DRAWS) * 4) sh.du[tid] = du_first;
+    const uint32_t n_strips = (uint32_t)(fp.rtiles_y * fp.n_frames);
+    const uint64_t n_items = (uint64_t)n_strips + n_busy;
     bool first = true;
-    for (int j0 = (int)blockIdx.x; j0 < n_all; j0 += 256 * G) {
+    for (;;) {
+        __syncthreads();   // the previous item's reads of sh.item are done
+        if (tid == 0) sh.item = ticket;
         __syncthreads();
-        if (tid == 0) sh.nbusy = 0;
-        __syncthreads();
-        // thread t checks owned raster tile j0 + t*G: busy ones are queued, the others cleared
-        const int rt = j0 == (int)blockIdx.x ? rt_first : owned_tile(j0 + tid * G);
-        if (rt >= 0) {
-            const uint32_t b = j0 == (int)blockIdx.x ? busy_first : fb.busy[rt];
-            if (b) sh.busy[atomicAdd(&sh.nbusy, 1u) & 0xffffu] = rt;
-            else sh.busy[255 - atomicAdd(&sh.nbusy, 0x10000u) / 0x10000u] = rt;   // clear list from the top
+        const uint32_t item = sh.item;
+        if ((uint64_t)item >= n_items) break;
+        if (tid == 0) ticket = atomicAdd(&cnt[C_WORK], 1u);   // the next item, in flight meanwhile
+        // interleave: item i is a strip when the count of strips among items < i + 1 grows
+        const uint32_t s_lo = (uint32_t)(((uint64_t)item * n_strips) / n_items);
+        const uint32_t s_hi = (uint32_t)(((uint64_t)(item + 1) * n_strips) / n_items);
+        if (s_hi > s_lo) {
+            const int f = (int)(s_lo / (uint32_t)fp.rtiles_y);
+            clear_strip(fp, fb, f, (int)s_lo - f * fp.rtiles_y, sh);
+            continue;
         }
-        __syncthreads();
+        const uint32_t g = fb.busy_list[item - s_lo];
+        const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
+        const FrameBuffers fv = frame_view(fp, fb, f);
+        if (fp.flags & DBG_CLEAR_ONLY) {
+            __syncthreads();
+            clear_tile(fp, fv, rt);
+            continue;
+        }
+        if (fp.flags & DBG_TWICE) raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
         tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
-        const int nb = (int)(sh.nbusy & 0xffffu), ne = (int)(sh.nbusy >> 16);
-        // busy tiles first (latency-bound), then the clears (streaming stores that other workgroups'
-        // busy tiles overlap with)
-        for (int i = 0; i < nb; ++i) {
-            const int g = sh.busy[i], f = g / n_rt, rt = g - f * n_rt;
-            const FrameBuffers fv = frame_view(fp, fb, f);
-            if (fp.flags & DBG_CLEAR_ONLY) {
-                __syncthreads();
-                clear_tile(fp, fv, rt);
-                if (tid == 0) fv.busy[rt] = 0u;
-                continue;
-            }
-            if (fp.flags & DBG_TWICE) raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
-            raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
-            first = false;
-        }
-        for (int i = 0; i < ne; ++i) {
-            const int g = sh.busy[255 - i], f = g / n_rt;
-            clear_tile(fp, frame_view(fp, fb, f), g - f * n_rt);
-        }
+        raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
+        first = false;
     }
     __syncthreads();
     if (tid == 0) {

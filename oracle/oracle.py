@@ -51,6 +51,17 @@ def lib():
         L.ora_fnv1a64.argtypes = [P, ctypes.c_uint64]
         L.ora_mat4_inverse.argtypes = [P, P]
         L.ora_mat4_mul.argtypes = [P, P, P]
+        F = ctypes.c_float
+        L.ora_camera3d.restype = None
+        L.ora_camera3d.argtypes = [P, F, F, F, F, F, P, P]
+        L.ora_model_trs.restype = None
+        L.ora_model_trs.argtypes = [P, F, P, P]
+        L.ora_look_at_lh.restype = None
+        L.ora_look_at_lh.argtypes = [P, P, P, P]
+        L.ora_perspective_lh_no.restype = None
+        L.ora_perspective_lh_no.argtypes = [F, F, F, F, P]
+        L.ora_legacy_mvp.restype = None
+        L.ora_legacy_mvp.argtypes = [P, P, P, ctypes.c_int, P, P]
         _lib = L
     return _lib
 
@@ -448,3 +459,52 @@ def occlusion_pass(width, height, view, view_proj, objects, frustum_visible, dep
                               width, height, v16.ctypes.data, vp16.ctypes.data, float(depth_epsilon), occ.ctypes.data,
                               vis.ctypes.data)
     return occ[:n], vis[:nv], depth
+
+
+# ---- camera / model matrices (shs_oracle_camera.c) -------------------------------------------------
+def _f32(a, n):
+    a = np.ascontiguousarray(a, dtype=np.float32).reshape(-1)
+    assert a.size == n
+    return a
+
+
+def camera3d(position, yaw, pitch, fov=60.0, zn=0.1, zf=1000.0):
+    """Camera3D::update (shs_renderer.hpp:1224-1236) -> (view, proj) float32[16], column-major."""
+    L = lib()
+    pos = _f32(position, 3)
+    view = np.zeros(16, np.float32)
+    proj = np.zeros(16, np.float32)
+    L.ora_camera3d(pos.ctypes.data, yaw, pitch, fov, zn, zf, view.ctypes.data, proj.ctypes.data)
+    return view, proj
+
+
+def model_trs(position, rot_deg_y, scale):
+    """MonkeyObject::get_world_matrix (blinn_phong_shading.cpp:122-128)."""
+    L = lib()
+    p, s = _f32(position, 3), _f32(scale, 3)
+    out = np.zeros(16, np.float32)
+    L.ora_model_trs(p.ctypes.data, rot_deg_y, s.ctypes.data, out.ctypes.data)
+    return out
+
+
+def look_at_lh(eye, center, up):
+    out = np.zeros(16, np.float32)
+    e, c, u = _f32(eye, 3), _f32(center, 3), _f32(up, 3)
+    lib().ora_look_at_lh(e.ctypes.data, c.ctypes.data, u.ctypes.data, out.ctypes.data)
+    return out
+
+
+def perspective_lh_no(fovy, aspect, zn, zf):
+    out = np.zeros(16, np.float32)
+    lib().ora_perspective_lh_no(fovy, aspect, zn, zf, out.ctypes.data)
+    return out
+
+
+def legacy_mvp(view, proj, model, flat=False):
+    """RendererSystem::process uniforms: mvp = (proj * view) * model, or for the Flat pipeline
+    mv = view * model, mvp = proj * mv -> (mvp, mv or model)."""
+    v, p, m = _f32(view, 16), _f32(proj, 16), _f32(model, 16)
+    mvp = np.zeros(16, np.float32)
+    mv = np.zeros(16, np.float32)
+    lib().ora_legacy_mvp(v.ctypes.data, p.ctypes.data, m.ctypes.data, 1 if flat else 0, mvp.ctypes.data, mv.ctypes.data)
+    return mvp, mv

@@ -201,4 +201,14 @@ int ora_occlusion_pass(const ora_occ_object *objs, int n_objects, const uint32_t
 #ifdef __cplusplus
 }
 #endif
+
+/* shs_oracle_camera.c: Camera3D::update / glm::perspectiveLH / glm::lookAtLH / the monkey model
+ * matrix and the legacy MVP, restated independently of the product's host helpers. */
+void ora_camera3d(const float pos[3], float horizontal_angle, float vertical_angle, float fov, float zn, float zf,
+                  float view16[16], float proj16[16]);
+void ora_model_trs(const float pos[3], float rot_deg_y, const float scl[3], float out16[16]);
+void ora_perspective_lh_no(float fovy, float aspect, float zn, float zf, float out16[16]);
+void ora_legacy_mvp(const float view16[16], const float proj16[16], const float model16[16], int flat, float mvp16[16],
+                    float mv16[16]);
+
 #endif
