@@ -55,8 +55,8 @@ int shs_create(int device, shs_ctx **out) {
         return SHS_ERR_HIP;
     }
     std::memset(ctx->h_counters, 0, shs_dev::C_NCOUNTERS * sizeof(uint32_t));
-    if (ensure(ctx, ctx->counters, 2 * shs_dev::C_NCOUNTERS) != SHS_OK ||
-        hipMemset(ctx->counters.p, 0, 2 * shs_dev::C_NCOUNTERS * sizeof(uint32_t)) != hipSuccess) {
+    if (ensure(ctx, ctx->counters, 2 * shs_dev::CSET) != SHS_OK ||
+        hipMemset(ctx->counters.p, 0, 2 * shs_dev::CSET * sizeof(uint32_t)) != hipSuccess) {
         delete ctx;
         return SHS_ERR_HIP;
     }
@@ -381,7 +381,7 @@ static int finish_frame(shs_ctx *ctx) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (!ctx->need_check) return SHS_OK;
     for (int attempt = 0; attempt < 6; ++attempt) {
-        HIP_TRY(ctx, hipMemcpy(ctx->h_counters, ctx->counters.p + ctx->last_parity * shs_dev::C_NCOUNTERS,
+        HIP_TRY(ctx, hipMemcpy(ctx->h_counters, ctx->counters.p + ctx->last_parity * shs_dev::CSET,
                                shs_dev::C_NCOUNTERS * sizeof(uint32_t), hipMemcpyDeviceToHost));
         const uint32_t *c = ctx->h_counters;
         // per-block statistics: setup blocks (triangle classes, bin entries), raster blocks

@@ -83,8 +83,12 @@ constexpr double GHOST_MAX_EXPAND = 48.0;  // larger danger boxes are handled as
 
 // counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one).
 // Only the append positions and the overflow flags live here; statistics go to per-block slots.
-// C_BUSY: entries of the busy-tile list (k_setup / k_ghost); C_WORK: k_raster's work-item ticket.
-constexpr int C_OVERFLOW = 0, C_SPILL = 1, C_FRAG = 2, C_SLIVER = 3, C_BUSY = 4, C_WORK = 5, C_NCOUNTERS = 6;
+// C_BUSY: entries of the busy-tile list (k_setup / k_ghost).  The host reads the first C_NCOUNTERS
+// words of a set.  k_raster's work tickets live in N_WORKQ queues, one 128-B line each from C_WORK
+// (one queue per XCD-sized group of workgroups: a same-address returning atomic serialises).
+constexpr int C_OVERFLOW = 0, C_SPILL = 1, C_FRAG = 2, C_SLIVER = 3, C_BUSY = 4, C_NCOUNTERS = 5;
+constexpr int N_WORKQ = 8, WORKQ_STRIDE = 32, C_WORK = 32;
+constexpr int CSET = C_WORK + N_WORKQ * WORKQ_STRIDE;   // words per counter set (2 parity sets)
 constexpr uint32_t OV_SPILL = 1u, OV_FRAG = 2u;
 
 // Timing-experiment switches (frame flags bits 8+; results are WRONG with any of them set): they
@@ -154,7 +158,7 @@ struct FrameBuffers {
     GhostFrag *frags;                // tile-clamp pixels of unbounded slivers that pass (frag_cap)
     uint32_t *slivers;               // n_frames * n_tris: unbounded slivers, f * n_tris + tri (ghost_list)
     uint2 *boxes;                    // per frame: n_tris packed bin boxes (gbx, gby); empty for culled
-    uint32_t *counters;              // 2 * C_NCOUNTERS
+    uint32_t *counters;              // 2 * CSET
     uint32_t *busy;                  // per frame, per raster tile: == fp.epoch when the tile has
                                      // candidates / fragments in this launch (no reset needed)
     uint32_t *busy_list;             // C_BUSY entries f * n_raster_tiles + raster tile, each busy tile of

@@ -698,7 +698,7 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_a
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
     __shared__ NewBusy s_new;
-    uint32_t *cnt = fb_all.counters + fp.parity * C_NCOUNTERS;
+    uint32_t *cnt = fb_all.counters + fp.parity * CSET;
     const int b = (int)blockIdx.x;
     // frame of the batch and the block's role inside it
     const int frame = b / fp.frame_blocks, lb = b - frame * fp.frame_blocks;
@@ -709,7 +709,8 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_a
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     // zero the other counter set and every frame's other bin-count set for the next batch (block 0
     // exists even for an empty frame)
-    if (b == 0 && threadIdx.x < C_NCOUNTERS) fb_all.counters[(fp.parity ^ 1u) * C_NCOUNTERS + threadIdx.x] = 0u;
+    if (b == 0)
+        for (int i = threadIdx.x; i < CSET; i += 256) fb_all.counters[(fp.parity ^ 1u) * CSET + i] = 0u;
     {
         const int n_bt = fp.tiles_x * fp.tiles_y;
         for (int i = b * 256 + (int)threadIdx.x; i < n_bt * fp.n_frames; i += (int)gridDim.x * 256) {
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_a
 constexpr int GHOST_LIST_BLOCKS = 512;
 
 __global__ __launch_bounds__(256) void k_ghost(FrameParams fp, FrameBuffers fb_all) {
-    uint32_t *cnt = fb_all.counters + fp.parity * C_NCOUNTERS;
+    uint32_t *cnt = fb_all.counters + fp.parity * CSET;
     const int n = (int)min(cnt[C_SLIVER], (uint32_t)fp.n_tris * (uint32_t)fp.n_frames);
     const int waves = (int)gridDim.x * 4, gw = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     const int slices = n > 0 ? max(1, min(16, waves / n)) : 1;
@@ -1195,25 +1196,25 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
 
 // Persistent raster over the whole batch.  Work items are the busy tiles (the busy list k_setup /
 // k_ghost built: latency-bound raster) and the clear strips (one raster-tile row of one frame:
-// streaming stores), interleaved in proportion so that every CU mixes both kinds at all times, and
-// handed out dynamically (one ticket atomic per item, fetched one item ahead).  Every owned pixel of
-// every frame is written exactly once: by its busy tile or by its strip.
+// streaming stores), interleaved in proportion so that every CU mixes both kinds at all times.
+// Workgroup b's first item is b (no atomic: a single frame needs none); the rest come from N_WORKQ
+// ticket queues -- queue q deals items G + q + N_WORKQ * j to the workgroups b = q (mod N_WORKQ) --
+// fetched one item ahead.  Every owned pixel of every frame is written exactly once: by its busy
+// tile or by its strip.
 template <bool KARG>
 __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
     const int tid = threadIdx.x;
-    uint32_t *cnt = fb.counters + fp.parity * C_NCOUNTERS;
+    uint32_t *cnt = fb.counters + fp.parity * CSET;
     const DrawGPU *draws = draw_table<KARG>(fb, ka);
     const int n_rt = fp.tiles_x * fp.rtiles_y;            // raster tiles per frame
     const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
     sh.key[tid] = KEY_EMPTY;
-    // Every independent first-touch load is issued up front so their round trips overlap: the first
-    // work ticket, the busy-list length, the ghost-fragment count, the draws' shading uniforms and, for
-    // a small single-frame scan-mode scene, every bin box (into registers).
-    uint32_t ticket = 0u;
-    if (tid == 0) ticket = atomicAdd(&cnt[C_WORK], 1u);
+    // Every independent first-touch load is issued up front so their round trips overlap: the
+    // busy-list length, the ghost-fragment count, the draws' shading uniforms and, for a small
+    // single-frame scan-mode scene, every bin box (into registers).
     const uint32_t n_busy = min(cnt[C_BUSY], (uint32_t)(n_rt * fp.n_frames));
     const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
     static_assert(LDS_DRAWS * 4 == 256, "one per-draw uniform float4 per thread");
@@ -1229,41 +1230,44 @@ __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers 
         const int i = tid + 256 * k;
         pbx[k] = (prefetched && i < fp.n_tris) ? fb.boxes[i] : make_uint2(0u, 0u);
     }
-    // pin the box loads here (the compiler would otherwise sink them to their first use, a second
-    // round trip after the ticket)
+    // pin the box loads here (the compiler would otherwise sink them to their first use)
 #pragma unroll
     for (int k = 0; k < CAND / 256; ++k) asm volatile("" : "+v"(pbx[k].x), "+v"(pbx[k].y));
     if (tid < min(n_draws_all, LDS_DRAWS) * 4) sh.du[tid] = du_first;
     const uint32_t n_strips = (uint32_t)(fp.rtiles_y * fp.n_frames);
     const uint64_t n_items = (uint64_t)n_strips + n_busy;
+    const uint32_t G = gridDim.x, q = blockIdx.x % (uint32_t)N_WORKQ;
+    uint32_t *queue = &cnt[C_WORK + WORKQ_STRIDE * q];
+    const bool queued = (uint64_t)G + q < n_items;        // this queue deals any item at all
+    uint32_t item = blockIdx.x, ticket = 0u;
     bool first = true;
-    for (;;) {
-        __syncthreads();   // the previous item's reads of sh.item are done
-        if (tid == 0) sh.item = ticket;
-        __syncthreads();
-        const uint32_t item = sh.item;
-        if ((uint64_t)item >= n_items) break;
-        if (tid == 0) ticket = atomicAdd(&cnt[C_WORK], 1u);   // the next item, in flight meanwhile
+    while ((uint64_t)item < n_items) {
+        if (tid == 0 && queued) ticket = atomicAdd(queue, 1u);   // the next item, in flight meanwhile
         // interleave: item i is a strip when the count of strips among items < i + 1 grows
         const uint32_t s_lo = (uint32_t)(((uint64_t)item * n_strips) / n_items);
         const uint32_t s_hi = (uint32_t)(((uint64_t)(item + 1) * n_strips) / n_items);
         if (s_hi > s_lo) {
             const int f = (int)(s_lo / (uint32_t)fp.rtiles_y);
             clear_strip(fp, fb, f, (int)s_lo - f * fp.rtiles_y, sh);
-            continue;
+        } else {
+            const uint32_t g = fb.busy_list[item - s_lo];
+            const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
+            const FrameBuffers fv = frame_view(fp, fb, f);
+            if (fp.flags & DBG_CLEAR_ONLY) {
+                __syncthreads();
+                clear_tile(fp, fv, rt);
+            } else {
+                if (fp.flags & DBG_TWICE) raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
+                tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
+                raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
+                first = false;
+            }
         }
-        const uint32_t g = fb.busy_list[item - s_lo];
-        const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
-        const FrameBuffers fv = frame_view(fp, fb, f);
-        if (fp.flags & DBG_CLEAR_ONLY) {
-            __syncthreads();
-            clear_tile(fp, fv, rt);
-            continue;
-        }
-        if (fp.flags & DBG_TWICE) raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
-        tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
-        raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
-        first = false;
+        if (!queued) break;
+        __syncthreads();   // every thread is done with sh.item of the previous round
+        if (tid == 0) sh.item = G + q + (uint32_t)N_WORKQ * ticket;
+        __syncthreads();
+        item = sh.item;
     }
     __syncthreads();
     if (tid == 0) {

@@ -1,0 +1,37 @@
+"""The C ABI from a compiled C++ host (tests/abi_c/abi_legacy.cpp, g++ against include/shs_gpu.h only):
+create -> upload -> shs_render_legacy -> shs_resolve (+ a frame batch), every frame compared with the
+oracle inside the program.  CPU: the program builds, links libshs_gpu.so and reports "no device"
+(exit 3) without a GPU; GPU: it passes every comparison."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ABI_C = os.path.join(ROOT, "tests", "abi_c")
+EXE = os.path.join(ABI_C, "_build", "abi_legacy")
+
+
+def _build():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    subprocess.run(["make", "-s", "-C", ABI_C], check=True)
+    assert os.path.exists(EXE)
+
+
+def test_abi_c_host_builds_and_links():
+    _build()
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: exercised by test_abi_c_host_renders_oracle_exact")
+    r = subprocess.run([EXE, ROOT], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=120)
+    assert r.returncode == 3, r.stdout   # shs_create -> SHS_ERR_NO_DEVICE, reported, no crash
+    assert "no gfx950 device" in r.stdout
+
+
+@pytest.mark.gpu
+def test_abi_c_host_renders_oracle_exact():
+    assert os.path.exists(EXE), "build tests/abi_c first (__graft_entry__.build())"
+    r = subprocess.run([EXE, ROOT], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+    assert "abi_legacy: all passed" in r.stdout

@@ -12,5 +12,7 @@ for l in open("gpurun_out/eb.log"):
         print(f"{sys.argv[1]:40s} ms/step {d['ms_per_step']:.4f} setup {d['kernels_ms']['setup']*1e3:8.1f}us raster {d['kernels_ms']['raster']*1e3:8.1f}us frac {r['frac']} step_frac {r['step_frac']}")
 PY
 }
-for a in ${ARGS_LIST:-"--debug-flags 0" "--debug-flags 0x400" "--debug-flags 0x4000" "--debug-flags 0x200" "--debug-flags 0x100" "--frames-per-step 16" "--frames-per-step 32" "--frames-per-step 128"}; do run $a; done
+# ARGS_LIST: ';'-separated argument sets
+IFS=';' read -ra SETS <<< "${ARGS_LIST:---debug-flags 0;--debug-flags 0x400;--debug-flags 0x4000;--debug-flags 0x200;--debug-flags 0x100;--frames-per-step 1;--frames-per-step 16;--frames-per-step 32;--frames-per-step 128}"
+for a in "${SETS[@]}"; do run $a; done
 cat $out
