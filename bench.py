@@ -128,7 +128,7 @@ def run_gpu(args, rank, local_rank, world, dist):
     n_launches, kms = ctx.timing_read()
     ctx.enable_timing(False)
     single = None
-    if F > 1 and not args.child:
+    if F > 1 and not args.child and not args.no_single:
         # the single-frame latency figure beside it: one shs_render_legacy per step
         one = ctx.prepare(frame, sets[0][0])
         for _ in range(10):
@@ -384,6 +384,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-single", action="store_true", help="skip the single-frame latency leg (profiling)")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--debug-flags", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
     ap.add_argument("--raster-mode", type=int, default=0, help="legacy path: 0 auto, 1 scan, 2 bins")

@@ -46,18 +46,23 @@ int shs_create(int device, shs_ctx **out) {
         return SHS_ERR_HIP;
     }
     ctx->stream = ctx->own_stream;
-    for (int i = 0; i < 2; ++i)
-        if (hipEventCreateWithFlags(&ctx->slot_ev[i], hipEventDisableTiming) != hipSuccess) { delete ctx; return SHS_ERR_HIP; }
+    if (hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking) != hipSuccess) { shs_destroy(ctx); return SHS_ERR_HIP; }
+    for (auto &w : ctx->lslot)
+        if (hipEventCreateWithFlags(&w.setup_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&w.raster_done, hipEventDisableTiming) != hipSuccess) {
+            shs_destroy(ctx);
+            return SHS_ERR_HIP;
+        }
     for (int i = 0; i < 5; ++i)
-        if (hipEventCreateWithFlags(&ctx->tev[i], hipEventDisableSystemFence) != hipSuccess) { delete ctx; return SHS_ERR_HIP; }
+        if (hipEventCreateWithFlags(&ctx->tev[i], hipEventDisableSystemFence) != hipSuccess) { shs_destroy(ctx); return SHS_ERR_HIP; }
     if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_counters), shs_dev::C_NCOUNTERS * sizeof(uint32_t)) != hipSuccess) {
-        delete ctx;
+        shs_destroy(ctx);
         return SHS_ERR_HIP;
     }
     std::memset(ctx->h_counters, 0, shs_dev::C_NCOUNTERS * sizeof(uint32_t));
     if (ensure(ctx, ctx->counters, 2 * shs_dev::CSET) != SHS_OK ||
         hipMemset(ctx->counters.p, 0, 2 * shs_dev::CSET * sizeof(uint32_t)) != hipSuccess) {
-        delete ctx;
+        shs_destroy(ctx);
         return SHS_ERR_HIP;
     }
     *out = ctx;
@@ -68,6 +73,7 @@ int shs_destroy(shs_ctx *ctx) {
     if (!ctx) return SHS_ERR_INVALID;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->setup_stream) (void)hipStreamSynchronize(ctx->setup_stream);
     for (auto &m : ctx->meshes) {
         if (m.pos) (void)hipFree(m.pos);
         if (m.nrm) (void)hipFree(m.nrm);
@@ -75,15 +81,16 @@ int shs_destroy(shs_ctx *ctx) {
         if (m.idx) (void)hipFree(m.idx);
     }
     shs_lib_release(ctx);
-    release(ctx->draws); release(ctx->recs); release(ctx->shade); release(ctx->tile_count); release(ctx->bins);
-    release(ctx->spill); release(ctx->frags); release(ctx->counters); release(ctx->busy); release(ctx->boxes);
-    release(ctx->slivers); release(ctx->busy_list);
-    release(ctx->blk_stat); release(ctx->rstat); release(ctx->timeline);
-    release(ctx->color); release(ctx->depth); release(ctx->prequant);
-    for (int i = 0; i < 2; ++i) {
-        if (ctx->h_draws[i]) (void)hipHostFree(ctx->h_draws[i]);
-        if (ctx->slot_ev[i]) (void)hipEventDestroy(ctx->slot_ev[i]);
+    for (auto &w : ctx->lslot) {
+        release(w.draws); release(w.recs); release(w.shade); release(w.tile_count); release(w.bins);
+        release(w.spill); release(w.frags); release(w.busy); release(w.boxes); release(w.slivers); release(w.busy_list);
+        release(w.blk_stat); release(w.rstat);
+        if (w.h_draws) (void)hipHostFree(w.h_draws);
+        if (w.setup_done) (void)hipEventDestroy(w.setup_done);
+        if (w.raster_done) (void)hipEventDestroy(w.raster_done);
     }
+    release(ctx->counters); release(ctx->timeline);
+    release(ctx->color); release(ctx->depth); release(ctx->prequant);
     for (int i = 0; i < 5; ++i)
         if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
     for (int k = 0; k < shs_ctx::RING; ++k)
@@ -91,6 +98,7 @@ int shs_destroy(shs_ctx *ctx) {
             if (ctx->ring_ev[k][i]) (void)hipEventDestroy(ctx->ring_ev[k][i]);
     if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
     delete ctx;
     return SHS_OK;
 }
@@ -100,6 +108,7 @@ const char *shs_last_error(shs_ctx *ctx) { return ctx ? ctx->err.c_str() : "null
 int shs_set_stream(shs_ctx *ctx, void *s) {
     if (!ctx) return SHS_ERR_INVALID;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
     ctx->stream = s ? reinterpret_cast<hipStream_t>(s) : ctx->own_stream;
     return SHS_OK;
 }
@@ -125,6 +134,7 @@ int shs_mesh_upload_soup(shs_ctx *ctx, const float *positions, const float *norm
 int shs_mesh_release(shs_ctx *ctx, int32_t id) {
     if (!ctx || id < 0 || id >= (int32_t)ctx->meshes.size() || !ctx->meshes[id].live) return SHS_ERR_INVALID;
     if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     Mesh &m = ctx->meshes[id];
     HIP_TRY(ctx, hipFree(m.pos));
@@ -169,10 +179,11 @@ static int harvest_slot(shs_ctx *ctx, int k) {
     if (!ctx->ring_pending[k]) return SHS_OK;
     HIP_TRY(ctx, hipEventSynchronize(ctx->ring_ev[k][2]));
     float ms[4];
-    // [0] k_setup (ev0..ev1), [3] k_raster (ev1..ev2: k_raster starts when k_setup ends)
+    // [0] k_setup (ev0..ev1, setup_stream), [3] k_raster (ev3..ev2, stream: ev3 is recorded after the
+    // wait for the setup, so it marks the raster's start)
     ms[1] = ms[2] = 0.0f;
     HIP_TRY(ctx, hipEventElapsedTime(&ms[0], ctx->ring_ev[k][0], ctx->ring_ev[k][1]));
-    HIP_TRY(ctx, hipEventElapsedTime(&ms[3], ctx->ring_ev[k][1], ctx->ring_ev[k][2]));
+    HIP_TRY(ctx, hipEventElapsedTime(&ms[3], ctx->ring_ev[k][3], ctx->ring_ev[k][2]));
     for (int i = 0; i < 4; ++i) { ctx->acc_ms[i] += ms[i]; ctx->last_ms[i] = ms[i]; }
     ctx->acc_frames++;
     ctx->ring_pending[k] = false;
@@ -206,44 +217,51 @@ static int enqueue_frame(shs_ctx *ctx) {
     const int n_tris = (int)total;   // per frame (every frame of a batch has the same count)
     const size_t nt_all = (size_t)std::max(n_tris, 1) * n_frames;
 
-    if (ensure(ctx, ctx->recs, nt_all) || ensure(ctx, ctx->shade, nt_all) || ensure(ctx, ctx->boxes, nt_all) ||
-        ensure(ctx, ctx->slivers, nt_all))
+    // This batch's workspace slot.  Its previous user (batch n - 2) is complete on the host side once
+    // its k_setup is (the pinned draw table is rewritten below), and on the device side once its
+    // k_raster is (setup_stream waits for raster_done before reusing the slot's buffers).
+    const int slot = (int)(ctx->frame_index & 1u);
+    shs_ctx::LegacySlot &ws = ctx->lslot[slot];
+    hipStream_t sst = ctx->setup_stream, st = ctx->stream;
+    if (ws.used) HIP_TRY(ctx, hipEventSynchronize(ws.setup_done));
+
+    if (ensure(ctx, ws.recs, nt_all) || ensure(ctx, ws.shade, nt_all) || ensure(ctx, ws.boxes, nt_all) ||
+        ensure(ctx, ws.slivers, nt_all))
         return SHS_ERR_HIP;
-    // Bin counts (2 parity sets) and busy flags are kept zero by the kernels themselves (k_setup's
-    // clear blocks zero the next frame's counts, k_raster resets the flags it consumed); they are
-    // reset here only when the buffers are new or the tile geometry / shard changes.
+    const size_t n_bt_all = (size_t)n_tiles * n_frames;
+    if (ensure(ctx, ws.tile_count, n_bt_all) || ensure(ctx, ws.busy_list, (size_t)n_rt * n_frames)) return SHS_ERR_HIP;
+    // busy flags hold the epoch of the batch that marked them: reset only when the buffer is new or the
+    // tile geometry / shard / batch size changes
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)f.shard_rank << 16) ^
                           (uint64_t)f.shard_count ^ ((uint64_t)n_frames << 24);
-    bool reset = gkey != ctx->geom_key;
-    if (ctx->tile_count.cap < 2 * (size_t)n_tiles * n_frames || !ctx->tile_count.p) {
-        if (ensure(ctx, ctx->tile_count, 2 * (size_t)n_tiles * n_frames)) return SHS_ERR_HIP;
+    bool reset = gkey != ctx->geom_key[slot];
+    if (ws.busy.cap < (size_t)n_rt * n_frames || !ws.busy.p) {
+        if (ensure(ctx, ws.busy, (size_t)n_rt * n_frames)) return SHS_ERR_HIP;
         reset = true;
     }
-    if (ctx->busy.cap < (size_t)n_rt * n_frames || !ctx->busy.p) {
-        if (ensure(ctx, ctx->busy, (size_t)n_rt * n_frames)) return SHS_ERR_HIP;
-        reset = true;
-    }
-    if (ensure(ctx, ctx->busy_list, (size_t)n_rt * n_frames)) return SHS_ERR_HIP;
-    if (reset) {
-        HIP_TRY(ctx, hipMemsetAsync(ctx->tile_count.p, 0, ctx->tile_count.cap * sizeof(uint32_t), ctx->stream));
-        HIP_TRY(ctx, hipMemsetAsync(ctx->busy.p, 0, ctx->busy.cap * sizeof(uint32_t), ctx->stream));
-        ctx->geom_key = gkey;
-    }
-    if (ensure(ctx, ctx->bins, (size_t)n_tiles * ctx->bin_cap * n_frames)) return SHS_ERR_HIP;
+    if (ensure(ctx, ws.bins, (size_t)n_tiles * ctx->bin_cap * n_frames)) return SHS_ERR_HIP;
     const int setup_blocks = (n_tris + 63) / 64;   // a quad of lanes per triangle, per frame
-    if (ensure(ctx, ctx->blk_stat, (size_t)std::max(setup_blocks, 1) * n_frames)) return SHS_ERR_HIP;
-    if (!ctx->spill.p && ensure(ctx, ctx->spill, 1 << 16)) return SHS_ERR_HIP;
-    if (!ctx->frags.p && ensure(ctx, ctx->frags, 1 << 12)) return SHS_ERR_HIP;
+    if (ensure(ctx, ws.blk_stat, (size_t)std::max(setup_blocks, 1) * n_frames)) return SHS_ERR_HIP;
+    if (!ws.spill.p && ensure(ctx, ws.spill, 1 << 16)) return SHS_ERR_HIP;
+    if (!ws.frags.p && ensure(ctx, ws.frags, 1 << 12)) return SHS_ERR_HIP;
     if (ensure(ctx, ctx->color, npx * 4 * n_frames) || ensure(ctx, ctx->depth, npx * n_frames)) return SHS_ERR_HIP;
     const bool want_pq = (f.flags & SHS_FRAME_PREQUANT) != 0;
     if (want_pq && ensure(ctx, ctx->prequant, npx * n_frames)) return SHS_ERR_HIP;
 
-    // per-draw uniform blocks: kernel arguments for small scenes, a device table otherwise
+    // ---- setup_stream: wait for the slot's last k_raster, reset, upload, set up ----
+    if (ws.used) HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.raster_done, 0));
+    if (reset) {
+        HIP_TRY(ctx, hipMemsetAsync(ws.busy.p, 0, ws.busy.cap * sizeof(uint32_t), sst));
+        ctx->geom_key[slot] = gkey;
+    }
+    uint32_t *cset = ctx->counters.p + (size_t)slot * shs_dev::CSET;
+    HIP_TRY(ctx, hipMemsetAsync(cset, 0, shs_dev::CSET * sizeof(uint32_t), sst));
+
+    // per-draw uniform blocks: kernel arguments for small batches, the slot's device table otherwise.
+    // tri_base restarts at 0 in every frame (submission order is per frame)
     shs_dev::KArgDraws ka;
     std::memset(&ka, 0, sizeof ka);
-    hipStream_t st = ctx->stream;
     int32_t base = 0;
-    // tri_base restarts at 0 in every frame (submission order is per frame)
     if (n_draws_all <= shs_dev::KARG_DRAWS) {
         for (int i = 0; i < n_draws_all; ++i) {
             if (i % std::max(n_draws, 1) == 0) base = 0;
@@ -252,30 +270,21 @@ static int enqueue_frame(shs_ctx *ctx) {
             base += ctx->meshes[d.mesh_id].n_tris;
         }
     } else {
-        if (ensure(ctx, ctx->draws, n_draws_all)) return SHS_ERR_HIP;
-        const int s = ctx->slot;
-        ctx->slot ^= 1;
-        if (ctx->slot_used[s]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[s]));
-        if ((size_t)n_draws_all > ctx->h_cap) {
-            for (int i = 0; i < 2; ++i) {
-                if (i != s && ctx->slot_used[i]) HIP_TRY(ctx, hipEventSynchronize(ctx->slot_ev[i]));
-                if (ctx->h_draws[i]) HIP_TRY(ctx, hipHostFree(ctx->h_draws[i]));
-                ctx->h_draws[i] = nullptr;
-            }
+        if (ensure(ctx, ws.draws, n_draws_all)) return SHS_ERR_HIP;
+        if ((size_t)n_draws_all > ws.h_cap) {
+            if (ws.h_draws) HIP_TRY(ctx, hipHostFree(ws.h_draws));
+            ws.h_draws = nullptr;
             const size_t cap = std::max<size_t>(n_draws_all, 64);
-            for (int i = 0; i < 2; ++i)
-                HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_draws[i]), cap * sizeof(DrawGPU)));
-            ctx->h_cap = cap;
+            HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ws.h_draws), cap * sizeof(DrawGPU)));
+            ws.h_cap = cap;
         }
         for (int i = 0; i < n_draws_all; ++i) {
             if (i % std::max(n_draws, 1) == 0) base = 0;
             const shs_legacy_draw &d = ctx->last_draws[i];
-            build_draw(d, ctx->meshes[d.mesh_id], base, ctx->h_draws[s][i]);
+            build_draw(d, ctx->meshes[d.mesh_id], base, ws.h_draws[i]);
             base += ctx->meshes[d.mesh_id].n_tris;
         }
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->draws.p, ctx->h_draws[s], n_draws_all * sizeof(DrawGPU), hipMemcpyHostToDevice, st));
-        HIP_TRY(ctx, hipEventRecord(ctx->slot_ev[s], st));
-        ctx->slot_used[s] = true;
+        HIP_TRY(ctx, hipMemcpyAsync(ws.draws.p, ws.h_draws, n_draws_all * sizeof(DrawGPU), hipMemcpyHostToDevice, sst));
     }
 
     FrameParams fp;
@@ -292,8 +301,8 @@ static int enqueue_frame(shs_ctx *ctx) {
                     ((uint32_t)f.clear_color[3] << 24);
     fp.flags = (f.flags & ~shs_dev::RF_PER_PIXEL) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
     fp.bin_cap = ctx->bin_cap;
-    fp.spill_cap = (uint32_t)std::min<size_t>(ctx->spill.cap, 0xffffffffu);
-    fp.frag_cap = (uint32_t)std::min<size_t>(ctx->frags.cap, 0xffffffffu);
+    fp.spill_cap = (uint32_t)std::min<size_t>(ws.spill.cap, 0xffffffffu);
+    fp.frag_cap = (uint32_t)std::min<size_t>(ws.frags.cap, 0xffffffffu);
     {   // ~1K ghost waves per launch: small scenes split each sliver group over a few waves.  Measured
         // at C2 (61 groups, ~17 unbounded slivers): 4K waves 8.9 us setup, 2K 7.7, 1K 7.3, 512 8.1,
         // 256 9.3 -- past ~1K the extra workgroup launches cost more than the shorter enumerations save.
@@ -301,16 +310,17 @@ static int enqueue_frame(shs_ctx *ctx) {
         const int n_groups = std::max(1, (n_tris + 15) / 16) * n_frames;
         fp.ghost_slices = (uint32_t)std::min(16, std::max(1, 1024 / n_groups));
     }
-    fp.parity = ctx->frame_index & 1u;
+    fp.parity = (uint32_t)slot;   // the slot's counter set
     if (++ctx->busy_epoch == 0u) ctx->busy_epoch = 1u;   // busy[] is zeroed on reset; 0 is never an epoch
     fp.epoch = ctx->busy_epoch;
     fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
+    if (!fp.scan_mode) HIP_TRY(ctx, hipMemsetAsync(ws.tile_count.p, 0, n_bt_all * sizeof(uint32_t), sst));
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;
     fp.setup_blocks = setup_blocks;
     // Binned (large) scenes list their unbounded slivers in k_setup and enumerate them in k_ghost:
     // ghost waves would recompute every triangle's record (C3: ~1/3 of k_setup's time).  Scan-mode
-    // scenes keep the ghost waves inside k_setup (one launch fewer on a latency-bound frame).
+    // scenes keep the ghost waves inside k_setup (one launch fewer).
     fp.ghost_list = fp.scan_mode ? 0u : 1u;
     fp.ghost_blocks = fp.ghost_list ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
     fp.clear_blocks = 0;
@@ -319,24 +329,24 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.frame_blocks = std::max(1, fp.setup_blocks + fp.ghost_blocks + fp.clear_blocks);
     // persistent raster grid: one resident wave of workgroups (k_raster runs 4 per CU)
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt * n_frames, 256 * 4));
-    if (ensure(ctx, ctx->rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
+    if (ensure(ctx, ws.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
     fp.setup_grid = fp.frame_blocks * n_frames;
     if (ctx->want_timeline) {
         const size_t n = (size_t)shs_dev::TL_STRIDE * (fp.setup_grid + raster_grid);
         if (ensure(ctx, ctx->timeline, n)) return SHS_ERR_HIP;
-        HIP_TRY(ctx, hipMemsetAsync(ctx->timeline.p, 0, n * sizeof(uint64_t), st));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->timeline.p, 0, n * sizeof(uint64_t), sst));
     }
 
     FrameBuffers fb;
-    fb.draws = ctx->draws.p; fb.recs = ctx->recs.p; fb.shade = ctx->shade.p; fb.tile_count = ctx->tile_count.p; fb.bins = ctx->bins.p;
-    fb.spill = ctx->spill.p; fb.frags = ctx->frags.p; fb.counters = ctx->counters.p;
-    fb.slivers = ctx->slivers.p;
-    fb.busy = ctx->busy.p;
-    fb.busy_list = ctx->busy_list.p;
-    fb.blk_stat = ctx->blk_stat.p;
-    fb.rstat = ctx->rstat.p;
+    fb.draws = ws.draws.p; fb.recs = ws.recs.p; fb.shade = ws.shade.p; fb.tile_count = ws.tile_count.p; fb.bins = ws.bins.p;
+    fb.spill = ws.spill.p; fb.frags = ws.frags.p; fb.counters = ctx->counters.p;
+    fb.slivers = ws.slivers.p;
+    fb.busy = ws.busy.p;
+    fb.busy_list = ws.busy_list.p;
+    fb.blk_stat = ws.blk_stat.p;
+    fb.rstat = ws.rstat.p;
     fb.timeline = ctx->want_timeline ? ctx->timeline.p : nullptr;
-    fb.boxes = ctx->boxes.p;
+    fb.boxes = ws.boxes.p;
     fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;
 
     hipEvent_t *ev = nullptr;
@@ -349,14 +359,22 @@ static int enqueue_frame(shs_ctx *ctx) {
         ev = ctx->ring_ev[k];
         ctx->ring_pending[k] = true;
     }
-    // kernel durations: [0] k_setup (+ k_ghost in ghost_list mode), [1] [2] (unused), [3] k_raster
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], st));
-    HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, ka, st));
-    if (fp.ghost_list && !(fp.flags & shs_dev::DBG_SKIP_GHOST)) HIP_TRY(ctx, shs_internal::launch_ghost(fp, fb, st));
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], st));
+    // kernel durations: [0]..[1] k_setup (+ k_ghost in ghost_list mode) on setup_stream,
+    // [3]..[2] k_raster on stream
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], sst));
+    HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, ka, sst));
+    if (fp.ghost_list && !(fp.flags & shs_dev::DBG_SKIP_GHOST)) HIP_TRY(ctx, shs_internal::launch_ghost(fp, fb, sst));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], sst));
+    HIP_TRY(ctx, hipEventRecord(ws.setup_done, sst));
+    // ---- stream: after the previous batch's raster (stream order) and this batch's setup ----
+    HIP_TRY(ctx, hipStreamWaitEvent(st, ws.setup_done, 0));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], st));
     HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, ka, raster_grid, st));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));
+    HIP_TRY(ctx, hipEventRecord(ws.raster_done, st));
+    ws.used = true;
     ctx->last_parity = fp.parity;
+    ctx->last_slot = slot;
     ctx->frame_index++;
     ctx->have_frame = true;
     ctx->need_check = true;
@@ -378,7 +396,7 @@ static uint32_t next_pow2(uint32_t v) {
 
 // Wait for the frame and read its counters; if a capacity overflowed, grow it and re-issue the frame.
 static int finish_frame(shs_ctx *ctx) {
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // k_raster waited for its k_setup
     if (!ctx->need_check) return SHS_OK;
     for (int attempt = 0; attempt < 6; ++attempt) {
         HIP_TRY(ctx, hipMemcpy(ctx->h_counters, ctx->counters.p + ctx->last_parity * shs_dev::CSET,
@@ -389,9 +407,9 @@ static int finish_frame(shs_ctx *ctx) {
         ctx->h_blk_stat.resize(ctx->last_setup_blocks);
         ctx->h_rstat.resize(ctx->last_raster_grid);
         if (ctx->last_setup_blocks)
-            HIP_TRY(ctx, hipMemcpy(ctx->h_blk_stat.data(), ctx->blk_stat.p, ctx->last_setup_blocks * sizeof(uint4),
+            HIP_TRY(ctx, hipMemcpy(ctx->h_blk_stat.data(), ctx->lslot[ctx->last_slot].blk_stat.p, ctx->last_setup_blocks * sizeof(uint4),
                                    hipMemcpyDeviceToHost));
-        HIP_TRY(ctx, hipMemcpy(ctx->h_rstat.data(), ctx->rstat.p, ctx->last_raster_grid * sizeof(uint2),
+        HIP_TRY(ctx, hipMemcpy(ctx->h_rstat.data(), ctx->lslot[ctx->last_slot].rstat.p, ctx->last_raster_grid * sizeof(uint2),
                                hipMemcpyDeviceToHost));
         ctx->last_covered = ctx->last_bins = ctx->last_maxbin = ctx->last_setup = ctx->last_ghost = ctx->last_unb = 0;
         for (const uint4 &b : ctx->h_blk_stat) {
@@ -407,13 +425,17 @@ static int finish_frame(shs_ctx *ctx) {
         if (!ov) break;
         if (ov & shs_dev::OV_SPILL) {
             const size_t need = c[shs_dev::C_SPILL];
-            release(ctx->spill);
-            if (ensure(ctx, ctx->spill, need + need / 4 + 1024)) return SHS_ERR_HIP;
+            for (auto &w : ctx->lslot) {
+                release(w.spill);
+                if (ensure(ctx, w.spill, need + need / 4 + 1024)) return SHS_ERR_HIP;
+            }
         }
         if (ov & shs_dev::OV_FRAG) {
             const size_t need = c[shs_dev::C_FRAG];
-            release(ctx->frags);
-            if (ensure(ctx, ctx->frags, need + need / 4 + 1024)) return SHS_ERR_HIP;
+            for (auto &w : ctx->lslot) {
+                release(w.frags);
+                if (ensure(ctx, w.frags, need + need / 4 + 1024)) return SHS_ERR_HIP;
+            }
         }
         int rc = enqueue_frame(ctx);
         if (rc) return rc;
@@ -569,7 +591,7 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
     *n_out = ctx->last_n_tris;
     if (out && capacity > 0) {
         const size_t n = (size_t)std::min<int64_t>(capacity, ctx->last_n_tris);
-        HIP_TRY(ctx, hipMemcpy(out, ctx->recs.p, n * sizeof(TriRec), hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(out, ctx->lslot[ctx->last_slot].recs.p, n * sizeof(TriRec), hipMemcpyDeviceToHost));
     }
     return SHS_OK;
 }
@@ -612,6 +634,7 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
     if (option == SHS_OPT_BIN_CAPACITY) {
         if (value < 1 || value > (1 << 24)) return SHS_ERR_INVALID;
         if (set_dev(ctx)) return SHS_ERR_HIP;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         ctx->bin_cap = (uint32_t)value;
         return SHS_OK;

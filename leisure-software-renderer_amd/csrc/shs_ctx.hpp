@@ -42,27 +42,39 @@ struct shs_ctx {
     std::string err;
     std::vector<Mesh> meshes;
 
-    DevBuf<shs_dev::DrawGPU> draws;
-    DevBuf<shs_dev::TriRec> recs;
-    DevBuf<shs_dev::ShadeRec> shade;
-    DevBuf<uint32_t> tile_count;     // 2 parity sets of per-bin-tile counts
-    DevBuf<uint32_t> bins;           // n_tiles * bin_cap
-    DevBuf<uint2> spill;
-    DevBuf<shs_dev::GhostFrag> frags; // ghost fragments
-    DevBuf<uint32_t> slivers;        // unbounded sliver ids (ghost_list mode)
-    DevBuf<uint2> boxes;             // per-triangle bin boxes
-    DevBuf<uint32_t> counters;       // 2 parity sets
-    DevBuf<uint32_t> busy;           // per raster tile: the epoch of the last launch that marked it
-    DevBuf<uint32_t> busy_list;      // busy tiles of the batch (k_raster's work items)
+    // Legacy-path workspace, double-buffered: batch n uses slot n & 1.  Its k_setup (plus the draw-table
+    // copy and the counter resets) runs on setup_stream while batch n-1's k_raster still runs on
+    // stream; setup of slot s waits for the k_raster that last used slot s (raster_done).
+    struct LegacySlot {
+        DevBuf<shs_dev::DrawGPU> draws;      // device draw table (> KARG_DRAWS draws)
+        shs_dev::DrawGPU *h_draws = nullptr; // pinned staging of that table
+        size_t h_cap = 0;
+        DevBuf<shs_dev::TriRec> recs;
+        DevBuf<shs_dev::ShadeRec> shade;
+        DevBuf<uint32_t> tile_count;         // per frame: per-bin-tile counts (zeroed per batch)
+        DevBuf<uint32_t> bins;               // per frame: n_tiles * bin_cap
+        DevBuf<uint2> spill;
+        DevBuf<shs_dev::GhostFrag> frags;    // ghost fragments
+        DevBuf<uint32_t> slivers;            // unbounded sliver ids (ghost_list mode)
+        DevBuf<uint2> boxes;                 // per-triangle bin boxes
+        DevBuf<uint32_t> busy;               // per raster tile: the epoch of the last batch that marked it
+        DevBuf<uint32_t> busy_list;          // busy tiles of the batch (k_raster's work items)
+        DevBuf<uint4> blk_stat;              // per setup block
+        DevBuf<uint2> rstat;                 // per raster block
+        hipEvent_t setup_done = nullptr, raster_done = nullptr;
+        bool used = false;
+    };
+    LegacySlot lslot[2];
+    hipStream_t setup_stream = nullptr;
+    DevBuf<uint32_t> counters;       // 2 sets (one per slot) of CSET words
     uint32_t busy_epoch = 0;         // FrameParams::epoch of the last launch (never 0)
-    DevBuf<uint4> blk_stat;          // per setup block
-    DevBuf<uint2> rstat;             // per raster block
+    int last_slot = 0;
     DevBuf<uint64_t> timeline;       // SHS_OPT_TIMELINE
     bool want_timeline = false;
     int last_setup_grid = 0, last_ghost_blocks = 0, last_clear_blocks = 0;
     std::vector<uint4> h_blk_stat;
     std::vector<uint2> h_rstat;
-    uint64_t geom_key = ~0ull;       // (tiles, shard) of the last frame: a change resets the counts
+    uint64_t geom_key[2] = {~0ull, ~0ull};   // (tiles, shard, frames) per slot: a change resets its busy flags
     int last_setup_blocks = 0, last_raster_grid = 0;
     uint64_t last_covered = 0, last_bins = 0, last_maxbin = 0, last_setup = 0, last_ghost = 0, last_unb = 0;
     uint32_t bin_cap = 256;
@@ -74,12 +86,6 @@ struct shs_ctx {
     DevBuf<float> depth;
     DevBuf<float4> prequant;
 
-    // pinned staging for the per-frame draw table (2 slots, guarded by events)
-    shs_dev::DrawGPU *h_draws[2] = {nullptr, nullptr};
-    size_t h_cap = 0;
-    hipEvent_t slot_ev[2] = {nullptr, nullptr};
-    bool slot_used[2] = {false, false};
-    int slot = 0;
     uint32_t *h_counters = nullptr;  // pinned, C_NCOUNTERS
 
     // last frame (re-issued if a bin capacity overflowed)
@@ -95,7 +101,8 @@ struct shs_ctx {
     bool timing = false;
     hipEvent_t tev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     float last_ms[4] = {0, 0, 0, 0};
-    // ring of per-frame kernel events, harvested lazily: sums of kernel durations over many frames
+    // ring of per-frame kernel events, harvested lazily: sums of kernel durations over many frames.
+    // [0] [1] around k_setup (+ k_ghost) on setup_stream, [3] [2] around k_raster on stream.
     static constexpr int RING = 64;
     hipEvent_t ring_ev[RING][5] = {};
     bool ring_pending[RING] = {};
@@ -187,8 +194,9 @@ inline int ensure(shs_ctx *ctx, DevBuf<T> &b, size_t n) {
     if (n <= b.cap && b.p) return SHS_OK;
     size_t want = std::max<size_t>(n, 16);
     if (b.p) {
-        // the old buffer may still be read by queued work on the stream
+        // the old buffer may still be read by queued work on the streams
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (ctx->setup_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
         HIP_TRY(ctx, hipFree(b.p));
         b.p = nullptr;
         b.cap = 0;

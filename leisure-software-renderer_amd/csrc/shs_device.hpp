@@ -81,7 +81,7 @@ constexpr int CAND = 1024;           // candidate ids gathered per round (4 per 
 constexpr int SCAN_MAX_TRIS = 4096;  // scenes up to this size skip binning (scan mode)
 constexpr double GHOST_MAX_EXPAND = 48.0;  // larger danger boxes are handled as TRI_UNBOUNDED
 
-// counters[] slots (two parity sets: frame f uses set f&1 and k_setup zeroes the other one).
+// counters[] slots (two sets, one per workspace slot, zeroed on the setup stream before each batch).
 // Only the append positions and the overflow flags live here; statistics go to per-block slots.
 // C_BUSY: entries of the busy-tile list (k_setup / k_ghost).  The host reads the first C_NCOUNTERS
 // words of a set.  k_raster's work tickets live in N_WORKQ queues, one 128-B line each from C_WORK
@@ -152,7 +152,7 @@ struct FrameBuffers {
     const DrawGPU *draws;            // device draw table (n_frames * n_draws > KARG_DRAWS)
     TriRec *recs;                    // per frame: n_tris
     ShadeRec *shade;                 // per frame: n_tris
-    uint32_t *tile_count;            // per frame: 2 parity sets x n_bin_tiles; k_setup zeroes the next set
+    uint32_t *tile_count;            // per frame: n_bin_tiles counts (zeroed before each launch)
     uint32_t *bins;                  // per frame: n_bin_tiles * bin_cap
     uint2 *spill;                    // (f * n_bin_tiles + bin tile, tri) pairs beyond bin_cap
     GhostFrag *frags;                // tile-clamp pixels of unbounded slivers that pass (frag_cap)
@@ -180,7 +180,7 @@ __device__ __forceinline__ FrameBuffers frame_view(const FrameParams &fp, const 
     v.recs += f * nt;
     v.shade += f * nt;
     v.boxes += f * nt;
-    v.tile_count += f * 2 * n_bt;
+    v.tile_count += f * n_bt;
     v.bins += f * n_bt * fp.bin_cap;
     v.busy += f * n_rt;
     v.color += f * npx * 4;

@@ -635,7 +635,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     // -- bin appends (large scenes): bin tiles of the bin box, two per quad lane
     uint32_t n_bin = 0;
     if (!fp.scan_mode && !(fp.flags & DBG_SKIP_BIN)) {
-        uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
+        uint32_t *tcount = fb.tile_count;
         const int bx0 = gx0 / TILE, bx1 = live ? gx1 / TILE : -1, by0 = gy0 / TILE, by1 = live ? gy1 / TILE : -1;
         const int nbx = max(bx1 - bx0 + 1, 1), n_bt = live ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0;
         int key[2];
@@ -707,17 +707,7 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_a
     const DrawGPU *draws = draw_table<KARG>(fb_all, ka) + dbase;
     const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
-    // zero the other counter set and every frame's other bin-count set for the next batch (block 0
-    // exists even for an empty frame)
-    if (b == 0)
-        for (int i = threadIdx.x; i < CSET; i += 256) fb_all.counters[(fp.parity ^ 1u) * CSET + i] = 0u;
-    {
-        const int n_bt = fp.tiles_x * fp.tiles_y;
-        for (int i = b * 256 + (int)threadIdx.x; i < n_bt * fp.n_frames; i += (int)gridDim.x * 256) {
-            const int f = i / n_bt, t = i - f * n_bt;
-            fb_all.tile_count[((size_t)f * 2 + (fp.parity ^ 1u)) * n_bt + t] = 0u;
-        }
-    }
+    // (the counter set and the bin counts were zeroed on the setup stream before this launch)
     if (lb < fp.setup_blocks) {
         setup_block(fp, fb, draws, dbase, frame, lb, cnt, s_stat, s_new);
     } else if (lb < fp.setup_blocks + fp.ghost_blocks) {
@@ -898,7 +888,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     if (fp.scan_mode) {
         n_items = (uint32_t)fp.n_tris;
     } else {
-        n_bin_total = fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + bt];
+        n_bin_total = fb.tile_count[bt];
         n_bin = n_bin_total < fp.bin_cap ? n_bin_total : fp.bin_cap;
         if (n_bin_total > fp.bin_cap) n_spill = min(cnt[C_SPILL], fp.spill_cap);
         n_items = n_bin + n_spill;
