@@ -31,14 +31,15 @@ def assert_color_parity(gpu_c, ref_c, gpu_pq=None, ref_pq=None):
 
 
 def assert_float_close(gpu, ref, tol=TOL, what="hdr"):
-    """Shaded floats (library path: HDR colour, motion): |gpu - ref| <= tol * max(1, |ref|) per
-    channel (north_star: within 1e-5 per channel; relative above 1 for HDR values).  Returns the
-    number of channels that are not bit-identical (libm powf ulp differences)."""
+    """Shaded floats (library path: HDR colour, motion): |gpu - ref| <= tol per channel, absolute
+    (north_star: within 1e-5 per channel), whatever the magnitude.  Returns the number of channels
+    that are not bit-identical (libm powf ulp differences)."""
     assert gpu.shape == ref.shape
-    assert np.isfinite(gpu).all() == np.isfinite(ref).all(), f"{what}: non-finite values differ"
-    err = np.abs(gpu.astype(np.float64) - ref.astype(np.float64))
-    lim = tol * np.maximum(1.0, np.abs(ref.astype(np.float64)))
-    bad = np.argwhere(err > lim)
+    assert np.array_equal(np.isfinite(gpu), np.isfinite(ref)), f"{what}: non-finite values differ"
+    fin = np.isfinite(ref)
+    err = np.zeros(ref.shape, np.float64)
+    err[fin] = np.abs(gpu[fin].astype(np.float64) - ref[fin].astype(np.float64))
+    bad = np.argwhere(err > tol)
     assert bad.size == 0, (f"{what}: {len(bad)} channels off by > {tol} (max {err.max():.3g}), first at "
                            f"{bad[:3].tolist()}: gpu={gpu[tuple(bad[0])]!r} ref={ref[tuple(bad[0])]!r}")
     return int((gpu.view(np.uint32) != ref.view(np.uint32)).sum())
