@@ -46,9 +46,9 @@ WORKLOADS = {
     "c1": "C1: Suzanne monkey.rawobj Blinn-Phong + z-buffer, 800x600, a batch of camera poses per step",
     "c3": "C3: 64-instance Suzanne grid, Phong, 1920x1080, a batch of camera poses per step",
     "c5": "C5: Suzanne + floor, PassShadowMap 2048^2 + PassPBRForward (PBR Cook-Torrance, PCF 5x5, motion) "
-          "3840x2160, 1 frame (both passes) per step",
-    "c4": "C4: Forward+ tiled, 1M synthetic triangles, 256 point lights, 3840x2160 (light cull + lit forward pass), "
-          "1 frame per step",
+          "3840x2160 + PassTonemap into the RGBA8 present staging, 1 frame per step",
+    "c4": "C4: Forward+ tiled, 1M synthetic triangles, 256 point lights, 3840x2160 (light cull + lit forward pass "
+          "+ PassTonemap into the RGBA8 present staging), 1 frame per step",
 }
 LIB_CONFIGS = {"c5", "c4"}
 
@@ -154,14 +154,15 @@ def lib_workload(args, rank=0):
     from shs_gpu import scene_lib
     if args.config == "c4":
         return scene_lib.c4_scene(3840, 2160)
-    return scene_lib.c5_scene(3840, 2160, 2048, yaw=3.0 * rank)
+    return scene_lib.c5_scene(3840, 2160, 2048)
 
 
 def run_gpu_c4(args, rank, local_rank, world, dist):
     """C4 frame = Forward+ light-list binning (shs_light_cull) + PassPBRForward with the per-pixel
-    point-light program over 1M triangles at 3840x2160.  N > 1: the frame's 32x32 tiles are sharded
-    (tile % N == rank) and the owned tiles are gathered into rank 0 over RCCL every frame
-    (strong scaling: the total work per step is one frame)."""
+    point-light program over 1M triangles at 3840x2160 + PassTonemap into the RGBA8 present staging.
+    N > 1: the frame's 32x32 tiles are sharded (tile % N == rank): every rank culls, renders and
+    tonemaps only its tiles, and the owned present tiles (4 B/px) are gathered into rank 0 over RCCL
+    every frame (strong scaling: the total work per step is one frame)."""
     import shs_gpu
     from shs_gpu import shard
     frame, draws, lights, cull = lib_workload(args, rank)
@@ -174,12 +175,14 @@ def run_gpu_c4(args, rank, local_rank, world, dist):
     ctx.upload_lights(lights)
     ctx.light_cull(cull)
     prepared = ctx.prepare_lib(frame, draws)
+    gbufs = [None]
 
     def one_frame():
         ctx.light_cull(cull)
         ctx.render_pbr_forward_prepared(prepared)
+        ctx.tonemap(1.0, 2.2, ldr=False, present=True)
         if dist is not None:
-            shard.gather_frame_device(dist, ctx, ctx.TARGET_LIB)
+            gbufs[0] = shard.gather_frame_device(dist, ctx, ctx.TARGET_LIB_PRESENT, out=gbufs[0])
 
     for _ in range(max(args.warmup, 1)):
         one_frame()
@@ -207,7 +210,8 @@ def run_gpu_c4(args, rank, local_rank, world, dist):
     ctx.close()
     n_tri = sum(d.mesh.n_tris for d in draws)
     B_cam_raster = frame.width * frame.height * 28
-    B_frame = n_tri * 72 + frame.width * frame.height * 28 + len(lights) * 160 + cull.n_lists * 4
+    # + the tonemap: HDR read (16 B/px) and the RGBA8 present staging written (4 B/px)
+    B_frame = n_tri * 72 + frame.width * frame.height * (28 + 20) + len(lights) * 160 + cull.n_lists * 4
     return frame, stats, elapsed, n_passes["camera"], kms, B_cam_raster, B_frame, n_tri, None
 
 
@@ -219,11 +223,17 @@ def lib_mesh_bytes(mesh, with_attrs=True):
 
 
 def run_gpu_lib(args, rank, local_rank, world, dist):
-    """C5 frame = PassShadowMap + PassPBRForward (shs_render_shadow_map + shs_render_pbr_forward)."""
+    """C5 frame = PassShadowMap + PassPBRForward + PassTonemap (present staging).  N > 1: tile-sharded
+    like C4 -- the shadow map (every rank's PCF reads all of it) is rendered on every rank, the camera
+    pass and the tonemap only on the rank's tiles, and the present tiles are gathered into rank 0."""
     import shs_gpu
-    from shs_gpu import scene_lib
-    frame, draws, casters, sun, S = lib_workload(args, rank)
+    from shs_gpu import scene_lib, shard
+    frame, draws, casters, sun, S = lib_workload(args, 0)
     ctx = shs_gpu.Context(local_rank)
+    if dist is not None:
+        import torch
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        frame.shard_rank, frame.shard_count = rank, world
     lvp = ctx.render_shadow_map(S, sun, casters)
     scene_lib.wire_shadow(draws, lvp)
     prepared = ctx.prepare_lib(frame, draws)
@@ -238,9 +248,14 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
     sd = (ctypes.c_float * 3)(*[float(x) for x in sun])
     L = ctx._lib
 
+    gbufs = [None]
+
     def one_frame():
         ctx._check(L.shs_render_shadow_map(ctx._h, S, S, sd, carr, len(casters), None))
         ctx.render_pbr_forward_prepared(prepared)
+        ctx.tonemap(1.0, 2.2, ldr=False, present=True)
+        if dist is not None:
+            gbufs[0] = shard.gather_frame_device(dist, ctx, ctx.TARGET_LIB_PRESENT, out=gbufs[0])
 
     for _ in range(max(args.warmup, 1)):
         one_frame()
@@ -267,7 +282,7 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
     ctx.close()
     B_cam_raster = frame.width * frame.height * 28 + S * S * 4
     B_frame = (sum(lib_mesh_bytes(d.mesh) for d in draws) + sum(lib_mesh_bytes(c.mesh, False) for c in casters)
-               + 2 * S * S * 4 + frame.width * frame.height * 28)
+               + 2 * S * S * 4 + frame.width * frame.height * (28 + 20))
     n_tri = sum(d.mesh.n_tris for d in draws)
     return frame, stats, elapsed, n_passes["camera"], kms, B_cam_raster, B_frame, n_tri, S
 
@@ -502,10 +517,7 @@ def main():
 def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     runner = run_gpu_c4 if args.config == "c4" else run_gpu_lib
     frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, S = runner(args, rank, local_rank, world, dist)
-    if args.config == "c4" and dist is not None:
-        world_tri = n_tri          # one frame split over the ranks (strong scaling)
-    else:
-        world_tri = world * n_tri
+    world_tri = n_tri              # one frame per step, split over the ranks at N > 1 (strong scaling)
     el_max = elapsed
     covered_total = float(stats["covered_pixels"])
     if dist is not None:
@@ -538,15 +550,16 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     if c4:
         data = ("synthetic: 1000 seeded objects x 1000 small triangles (seed 0x5EED), 256 point lights (seed 0x11A7, "
                 "range U[2,8], Smooth attenuation), 16-px tiles, max 128 lights per tile")
-        parallelism = f"tile-sharded x{world} + RCCL gather to rank 0" if world > 1 else "single GPU"
+        parallelism = f"tile-sharded x{world} + RCCL gather of RGBA8 present tiles to rank 0" if world > 1 else "single GPU"
     else:
         data = ("synthetic: Suzanne (indexed from the reference's monkey.rawobj) + make_plane floor, reference "
                 "defaults (sun normalize(0.4668,-0.3487,0.8127), intensity 5, PCF 2, bias 0.0008/0.0015)")
-        parallelism = f"frame-parallel x{world}" if world > 1 else "single GPU"
+        parallelism = (f"tile-sharded x{world} (shadow map on every rank) + RCCL gather of RGBA8 present tiles "
+                       "to rank 0") if world > 1 else "single GPU"
     line = {
         "metric": METRIC, "value": round(world_tri * steps / el_max / 1e6, 3), "unit": "Mtri/s", "n_gpus": world,
         "steps": steps, "warmup": args.warmup, "ms_per_step": round(el_max / steps * 1e3, 5), "higher_is_better": True,
-        "scaling": "strong" if (c4 and world > 1) else "weak", "vs_baseline": None, "dtype": "f32", "data": data,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
         "config": {"workload": WORKLOADS[args.config], "width": frame.width, "height": frame.height,
                    "shadow_map": S, "tris_per_frame": n_tri, "frames_per_step_per_gpu": 1,
                    "parallelism": parallelism},

@@ -70,6 +70,7 @@ typedef struct shs_frame_desc {
 } shs_frame_desc;
 
 #define SHS_FRAME_PREQUANT 1u     /* also keep the shader's pre-truncation floats (tests)     */
+#define SHS_FRAME_PRESENT 2u      /* also write the SDL present staging (shs_resolve_present)  */
 
 typedef struct shs_raster_stats {
     uint64_t tri_input;           /* triangles submitted (rasterizer.hpp:208 tri_input)        */
@@ -121,6 +122,13 @@ int shs_render_legacy_batch(shs_ctx *ctx, const shs_frame_desc *frame, const shs
  * pipelines index it).  Either pointer may be NULL.  shs_resolve = frame 0 of the last batch. */
 int shs_resolve(shs_ctx *ctx, uint8_t *color, float *depth);
 int shs_resolve_frame(shs_ctx *ctx, int32_t frame_index, uint8_t *color, float *depth);
+/* Present staging (SHS_FRAME_PRESENT), written by the same launch as the canvas: the RGBA32 surface
+ * Canvas::copy_to_SDLSurface fills (shs_renderer.hpp:833-848) -- surface row h-1-y holds canvas row
+ * y, SDL_MapRGBA into create_sdl_surface's little-endian RGBA32 masks (:850-856) is the Color bytes.
+ * shs_resolve_present copies it into a caller surface (pixels + pitch in bytes >= W*4), replacing
+ * the per-pixel copy loop; shs_present_device returns the device pointer (W*H words, rows top-down). */
+int shs_resolve_present(shs_ctx *ctx, int32_t frame_index, uint8_t *pixels, int32_t pitch);
+int shs_present_device(shs_ctx *ctx, int32_t frame_index, void **present_dev);
 /* Pre-truncation shader floats, W*H*4 (canvas rows), only when SHS_FRAME_PREQUANT was set. */
 int shs_resolve_prequant(shs_ctx *ctx, float *prequant);
 /* Device pointers of the current frame (zero-copy hand-off to torch / RCCL). */
@@ -319,6 +327,32 @@ int shs_light_cull(shs_ctx *ctx, const shs_light_cull_desc *desc);
 int shs_resolve_light_lists(shs_ctx *ctx, uint32_t *counts, uint32_t *indices, float *ranges);
 #define SHS_PROGRAM_FORWARD_PLUS 5  /* per-pixel point lights from the tile lists (light_runtime.hpp:321-333) */
 
+/* ---- the software library's CPU light binning -----------------------------
+ * build_light_bin_culling (shs-renderer-lib/include/shs/lighting/light_culling_runtime.hpp:266-371):
+ * cull_lights_tiled / cull_lights_tiled_view_depth_range / cull_lights_clustered
+ * (lighting/jolt_light_culling.hpp:135-412) -- per bin, the cell of make_screen_tile_cell (:95-133)
+ * against every camera-frustum-visible light with classify_vs_cell (geometry/jolt_culling.hpp:129-257).
+ * The lights are the SceneShapes' world AABBs (min xyz, max xyz; SceneShape::world_aabb()): the
+ * binning reads only those and the bounding sphere Jolt derives from them.  Lists hold local light
+ * indices in ascending order: counts[bin] = every match, indices[bin * max_per_bin + k] the first
+ * max_per_bin (use max_per_bin = n_lights for the reference's unbounded vectors).  Bins are tile-row-
+ * major (top-origin tile rows), clusters slice-major; bins_xyz = (bins_x, bins_y, bins_z), all 0 for
+ * SHS_LIGHT_CULL_NONE or no lights.  Synchronous: host arrays in, host arrays out. */
+typedef struct shs_light_bin_desc {
+    int32_t width, height;
+    uint32_t tile_size;           /* LightBinCullingConfig::tile_size (16)                        */
+    uint32_t mode;                /* SHS_LIGHT_CULL_NONE / _TILED / _TILED_DEPTH / _CLUSTERED       */
+    uint32_t z_slices;            /* cluster_depth_slices (16)                                    */
+    uint32_t max_per_bin;
+    float view_proj[16];
+    float z_near, z_far;          /* LightBinCullingConfig::z_near / z_far                         */
+    const float *tile_min_view_depth;   /* mode 2: tiles_x * tiles_y linear view depths each, or NULL */
+    const float *tile_max_view_depth;
+    int32_t n_depth_tiles;
+} shs_light_bin_desc;
+int shs_light_bin_culling(shs_ctx *ctx, const shs_light_bin_desc *desc, const float *light_aabbs, int32_t n_lights,
+                          uint32_t bins_xyz[3], uint32_t *counts, uint32_t *indices);
+
 /* ---- multi-GPU tile shards -------------------------------------------------------
  * A frame rendered with shard_rank / shard_count holds only its own 32x32 tiles (tile % count ==
  * rank).  shs_tiles_pack writes them into a caller-owned DEVICE buffer (e.g. a torch tensor on the
@@ -327,7 +361,11 @@ int shs_resolve_light_lists(shs_ctx *ctx, uint32_t *counts, uint32_t *indices, f
  * are enqueued on the context stream (see shs_set_stream). */
 #define SHS_TARGET_LEGACY 0   /* shs_render_legacy frame: RGBA8 canvas rows + f32 depth  */
 #define SHS_TARGET_LIB 1      /* library frame: RGBA32F HDR (+ depth + motion)           */
+#define SHS_TARGET_PRESENT 2  /* legacy SDL staging (SHS_FRAME_PRESENT): RGBA8, 4 B/px    */
+#define SHS_TARGET_LIB_PRESENT 3 /* tonemap present staging (SHS_TONEMAP_PRESENT): RGBA8  */
 int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t shard_count, int64_t *words_per_rank);
+/* shs_tiles_pack first finishes the frame (a capacity overflow re-issues it), so the packed tiles are
+ * final; it is enqueued on the context stream after that. */
 int shs_tiles_pack(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, void *dst_dev);
 int shs_tiles_unpack(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, const void *src_dev);
 

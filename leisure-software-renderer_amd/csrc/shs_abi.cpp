@@ -90,7 +90,7 @@ int shs_destroy(shs_ctx *ctx) {
         if (w.raster_done) (void)hipEventDestroy(w.raster_done);
     }
     release(ctx->counters); release(ctx->timeline);
-    release(ctx->color); release(ctx->depth); release(ctx->prequant);
+    release(ctx->color); release(ctx->depth); release(ctx->prequant); release(ctx->present);
     for (int i = 0; i < 5; ++i)
         if (ctx->tev[i]) (void)hipEventDestroy(ctx->tev[i]);
     for (int k = 0; k < shs_ctx::RING; ++k)
@@ -247,6 +247,8 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (ensure(ctx, ctx->color, npx * 4 * n_frames) || ensure(ctx, ctx->depth, npx * n_frames)) return SHS_ERR_HIP;
     const bool want_pq = (f.flags & SHS_FRAME_PREQUANT) != 0;
     if (want_pq && ensure(ctx, ctx->prequant, npx * n_frames)) return SHS_ERR_HIP;
+    const bool want_present = (f.flags & SHS_FRAME_PRESENT) != 0;
+    if (want_present && ensure(ctx, ctx->present, npx * n_frames)) return SHS_ERR_HIP;
 
     // ---- setup_stream: wait for the slot's last k_raster, reset, upload, set up ----
     if (ws.used) HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.raster_done, 0));
@@ -348,6 +350,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fb.timeline = ctx->want_timeline ? ctx->timeline.p : nullptr;
     fb.boxes = ws.boxes.p;
     fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;
+    fb.present = want_present ? ctx->present.p : nullptr;
 
     hipEvent_t *ev = nullptr;
     if (ctx->timing) {
@@ -510,6 +513,28 @@ int shs_resolve_frame(shs_ctx *ctx, int32_t frame_index, uint8_t *color, float *
 }
 
 int shs_resolve(shs_ctx *ctx, uint8_t *color, float *depth) { return shs_resolve_frame(ctx, 0, color, depth); }
+
+int shs_resolve_present(shs_ctx *ctx, int32_t frame_index, uint8_t *pixels, int32_t pitch) {
+    if (!ctx || !pixels) return SHS_ERR_INVALID;
+    if (!ctx->have_frame || !(ctx->frame.flags & SHS_FRAME_PRESENT)) { ctx->err = "frame has no present staging (SHS_FRAME_PRESENT)"; return SHS_ERR_INVALID; }
+    if (frame_index < 0 || frame_index >= ctx->last_n_frames) { ctx->err = "frame index outside the batch"; return SHS_ERR_INVALID; }
+    const int W = ctx->frame.width, H = ctx->frame.height;
+    if (pitch < W * 4) { ctx->err = "pitch below width * 4"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
+    const uint32_t *src = ctx->present.p + (size_t)W * H * frame_index;
+    HIP_TRY(ctx, hipMemcpy2D(pixels, (size_t)pitch, src, (size_t)W * 4, (size_t)W * 4, (size_t)H, hipMemcpyDeviceToHost));
+    return SHS_OK;
+}
+
+int shs_present_device(shs_ctx *ctx, int32_t frame_index, void **present_dev) {
+    if (!ctx || !present_dev) return SHS_ERR_INVALID;
+    if (!ctx->have_frame || !(ctx->frame.flags & SHS_FRAME_PRESENT)) { ctx->err = "frame has no present staging (SHS_FRAME_PRESENT)"; return SHS_ERR_INVALID; }
+    if (frame_index < 0 || frame_index >= ctx->last_n_frames) { ctx->err = "frame index outside the batch"; return SHS_ERR_INVALID; }
+    *present_dev = ctx->present.p + (size_t)ctx->frame.width * ctx->frame.height * frame_index;
+    return SHS_OK;
+}
 
 int shs_resolve_prequant(shs_ctx *ctx, float *pq) {
     if (!ctx || !pq) return SHS_ERR_INVALID;

@@ -315,6 +315,7 @@ void shs_lib_release(shs_ctx *ctx) {
     release(ctx->lights); release(ctx->light_proj); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
     release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
+    release(ctx->lb_lights); release(ctx->lb_ndc); release(ctx->lb_counts); release(ctx->lb_indices);
     release(ctx->occ_depth); release(ctx->occ_visible); release(ctx->occ_flags); release(ctx->occ_objs); release(ctx->occ_rects); release(ctx->occ_tris);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
@@ -648,6 +649,18 @@ static int tile_params(shs_ctx *ctx, int target, int32_t rank, int32_t count, sh
         p.color_words = 1; p.color_flip = 1;
         p.color = reinterpret_cast<uint32_t *>(ctx->color.p);
         p.depth = reinterpret_cast<uint32_t *>(ctx->depth.p);
+    } else if (target == SHS_TARGET_PRESENT) {
+        // the legacy frame's SDL staging: screen rows, the legacy tiles' own row order
+        if (!ctx->have_frame || !(ctx->frame.flags & SHS_FRAME_PRESENT)) { ctx->err = "no legacy present staging"; return SHS_ERR_INVALID; }
+        p.W = ctx->frame.width; p.H = ctx->frame.height;
+        p.color_words = 1; p.color_flip = 0;
+        p.color = ctx->present.p;
+    } else if (target == SHS_TARGET_LIB_PRESENT) {
+        // the last tonemap's present staging: rows top-down, library tiles count rows y up
+        if (!ctx->have_ldr || !(ctx->tm_desc.flags & SHS_TONEMAP_PRESENT)) { ctx->err = "no tonemap present staging"; return SHS_ERR_INVALID; }
+        p.W = ctx->lib_frame.width; p.H = ctx->lib_frame.height;
+        p.color_words = 1; p.color_flip = 1;
+        p.color = ctx->lib_present.p;
     } else if (target == SHS_TARGET_LIB) {
         if (!ctx->have_lib_frame) { ctx->err = "no library frame rendered"; return SHS_ERR_INVALID; }
         p.W = ctx->lib_frame.width; p.H = ctx->lib_frame.height;
@@ -679,6 +692,11 @@ int shs_tiles_pack(shs_ctx *ctx, int target, int32_t rank, int32_t count, void *
     shs_dev::TileCopyParams p;
     if (tile_params(ctx, target, rank, count, p)) return SHS_ERR_INVALID;
     if (set_dev(ctx)) return SHS_ERR_HIP;
+    // A frame whose capacity overflowed is re-issued when it is finished: finish it before its tiles
+    // leave the rank (legacy: shs_synchronize; library: the pass chain, tonemap included).
+    const int rc = (target == SHS_TARGET_LEGACY || target == SHS_TARGET_PRESENT) ? shs_synchronize(ctx)
+                                                                                : shs_resolve_lib(ctx, nullptr, nullptr, nullptr);
+    if (rc) return rc;
     HIP_TRY(ctx, shs_internal::launch_tiles_copy(p, true, dst_dev, ctx->stream));
     return SHS_OK;
 }

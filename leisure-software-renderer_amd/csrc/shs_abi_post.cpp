@@ -72,6 +72,10 @@ int enqueue_tonemap(shs_ctx *ctx) {
     p.present = (d.flags & SHS_TONEMAP_PRESENT) ? ctx->lib_present.p : nullptr;
     p.W = W;
     p.H = H;
+    // a tile-sharded camera pass wrote only its own tiles: map only those (the others stay undefined,
+    // like the HDR target's)
+    p.rank = ctx->lib_frame.shard_count > 1 ? ctx->lib_frame.shard_rank : 0;
+    p.count = std::max(1, ctx->lib_frame.shard_count);
     p.exposure = std::max(0.0001f, d.exposure);
     p.inv_gamma = 1.0f / std::max(0.001f, d.gamma);
     std::memcpy(p.thr, ctx->tm_thr, sizeof p.thr);

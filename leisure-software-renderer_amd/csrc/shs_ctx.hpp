@@ -10,6 +10,7 @@
 #include "../../include/shs_gpu.h"
 #include "shs_device.hpp"
 #include "shs_lib_device.hpp"
+#include "shs_lightbin_internal.hpp"
 #include "shs_occlusion_internal.hpp"
 
 namespace shs_host_detail {
@@ -85,6 +86,7 @@ struct shs_ctx {
     DevBuf<uint8_t> color;
     DevBuf<float> depth;
     DevBuf<float4> prequant;
+    DevBuf<uint32_t> present;        // SHS_FRAME_PRESENT staging (per frame of the batch)
 
     uint32_t *h_counters = nullptr;  // pinned, C_NCOUNTERS
 
@@ -169,6 +171,10 @@ struct shs_ctx {
     DevBuf<uint32_t> lib_mb, lib_mb_present;
     shs_motion_blur_desc mb_desc{};
     bool have_mb = false;                 // a motion blur follows that tonemap
+    // CPU light binning on the GPU (shs_abi_lightbin.cpp)
+    DevBuf<shs_dev::BinLight> lb_lights;
+    DevBuf<float2> lb_ndc;
+    DevBuf<uint32_t> lb_counts, lb_indices;
     // software occlusion pass (shs_abi_occ.cpp)
     DevBuf<uint32_t> occ_depth, occ_visible;
     DevBuf<uint8_t> occ_flags;

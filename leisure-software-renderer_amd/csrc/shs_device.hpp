@@ -170,6 +170,8 @@ struct FrameBuffers {
     uint8_t *color;                  // per frame: W*H*4, canvas rows
     float *depth;                    // per frame: W*H, screen rows
     float4 *prequant;                // per frame: W*H (optional)
+    uint32_t *present;               // per frame: W*H RGBA8 SDL staging, rows top-down (optional,
+                                     // SHS_FRAME_PRESENT: Canvas::copy_to_SDLSurface's layout)
 };
 
 // The buffers of frame f of the batch (shared buffers unchanged).
@@ -186,6 +188,7 @@ __device__ __forceinline__ FrameBuffers frame_view(const FrameParams &fp, const 
     v.color += f * npx * 4;
     v.depth += f * npx;
     if (v.prequant) v.prequant += f * npx;
+    if (v.present) v.present += f * npx;
     return v;
 }
 

@@ -1121,6 +1121,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
         __builtin_nontemporal_store(rgba, &reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - py) * fp.W + px]);
         __builtin_nontemporal_store(depth, &fb.depth[(size_t)py * fp.W + px]);
         if (fb.prequant) fb.prequant[(size_t)(fp.H - 1 - py) * fp.W + px] = pq;
+        // copy_to_SDLSurface: surface row h-1-y takes canvas row y, i.e. the screen row
+        if (fb.present) __builtin_nontemporal_store(rgba, &fb.present[(size_t)py * fp.W + px]);
     }
     tl_mark(tl, tls, 5);
 }
@@ -1135,6 +1137,7 @@ __device__ __forceinline__ void clear_tile(const FrameParams &fp, const FrameBuf
         __builtin_nontemporal_store(fp.clear_rgba, &reinterpret_cast<uint32_t *>(fb.color)[c]);
         __builtin_nontemporal_store(FLT_MAX, &fb.depth[(size_t)py * fp.W + px]);
         if (fb.prequant) fb.prequant[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (fb.present) __builtin_nontemporal_store(fp.clear_rgba, &fb.present[(size_t)py * fp.W + px]);
     }
 }
 
@@ -1165,6 +1168,7 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
                 if (sh.skip[g >> 3]) continue;   // 8 groups of 4 px per 32-px tile
                 __builtin_nontemporal_store(c4, &crow[g]);
                 __builtin_nontemporal_store(d4, &drow[g]);
+                if (fv.present) __builtin_nontemporal_store(c4, &reinterpret_cast<u32x4 *>(fv.present + (size_t)y * fp.W)[g]);
                 if (fv.prequant) {
                     float4 *pq = fv.prequant + (size_t)(fp.H - 1 - y) * fp.W + 4 * g;
                     pq[0] = pq[1] = pq[2] = pq[3] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1179,6 +1183,7 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
                 __builtin_nontemporal_store(fp.clear_rgba, &color[c]);
                 __builtin_nontemporal_store(FLT_MAX, &fv.depth[(size_t)y * fp.W + x]);
                 if (fv.prequant) fv.prequant[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (fv.present) __builtin_nontemporal_store(fp.clear_rgba, &fv.present[(size_t)y * fp.W + x]);
             }
         }
     }

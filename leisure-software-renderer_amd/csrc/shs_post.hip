@@ -25,6 +25,15 @@ __device__ __forceinline__ uint32_t tonemap_byte(float s, float exposure, float 
     return (uint32_t)k;
 }
 
+__device__ __forceinline__ void tonemap_pixel(const TonemapParams &p, const float *thr, int x, int y) {
+    const float4 s = p.hdr[(size_t)y * p.W + x];
+    const uint32_t rgba = tonemap_byte(s.x, p.exposure, p.inv_gamma, thr) |
+                          (tonemap_byte(s.y, p.exposure, p.inv_gamma, thr) << 8) |
+                          (tonemap_byte(s.z, p.exposure, p.inv_gamma, thr) << 16) | (255u << 24);
+    if (p.ldr) __builtin_nontemporal_store(rgba, &p.ldr[(size_t)y * p.W + x]);
+    if (p.present) __builtin_nontemporal_store(rgba, &p.present[(size_t)(p.H - 1 - y) * p.W + x]);
+}
+
 // 64 x 4 pixels per workgroup: each wave reads 64 float4 of one row (1 KB) and writes 256 B rows.
 __global__ __launch_bounds__(256) void k_tonemap(TonemapParams p) {
     __shared__ float thr[256];
@@ -33,12 +42,23 @@ __global__ __launch_bounds__(256) void k_tonemap(TonemapParams p) {
     const int x = (int)blockIdx.x * 64 + (int)(threadIdx.x & 63u);
     const int y = (int)blockIdx.y * 4 + (int)(threadIdx.x >> 6);
     if (x >= p.W || y >= p.H) return;
-    const float4 s = p.hdr[(size_t)y * p.W + x];
-    const uint32_t rgba = tonemap_byte(s.x, p.exposure, p.inv_gamma, thr) |
-                          (tonemap_byte(s.y, p.exposure, p.inv_gamma, thr) << 8) |
-                          (tonemap_byte(s.z, p.exposure, p.inv_gamma, thr) << 16) | (255u << 24);
-    if (p.ldr) __builtin_nontemporal_store(rgba, &p.ldr[(size_t)y * p.W + x]);
-    if (p.present) __builtin_nontemporal_store(rgba, &p.present[(size_t)(p.H - 1 - y) * p.W + x]);
+    tonemap_pixel(p, thr, x, y);
+}
+
+// Tile-sharded camera pass: only the rank's 32x32 tiles (rows y up, tile % count == rank) hold
+// pixels, so one workgroup per owned tile maps them (32-px rows: 512-B reads, 128-B writes).
+__global__ __launch_bounds__(256) void k_tonemap_tiles(TonemapParams p) {
+    __shared__ float thr[256];
+    thr[threadIdx.x] = p.thr[threadIdx.x];
+    __syncthreads();
+    const int tiles_x = (p.W + 31) / 32;
+    const int t = p.rank + (int)blockIdx.x * p.count;
+    const int x = (t % tiles_x) * 32 + (int)(threadIdx.x & 31u);
+    const int y0 = (t / tiles_x) * 32 + (int)(threadIdx.x >> 5);
+    if (x >= p.W) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (y0 + 8 * k < p.H) tonemap_pixel(p, thr, x, y0 + 8 * k);
 }
 
 // std::lround then the (int) cast of the reference: half away from zero, 64-bit, then truncated.
@@ -107,6 +127,12 @@ hipError_t launch_motion_blur(const MotionBlurParams &p, hipStream_t s) {
 }
 
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s) {
+    if (p.count > 1) {
+        const int n_tiles = ((p.W + 31) / 32) * ((p.H + 31) / 32);
+        const int n_owned = (n_tiles - p.rank + p.count - 1) / p.count;
+        if (n_owned > 0) hipLaunchKernelGGL(k_tonemap_tiles, dim3((unsigned)n_owned), dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
     const dim3 grid((unsigned)((p.W + 63) / 64), (unsigned)((p.H + 3) / 4));
     hipLaunchKernelGGL(k_tonemap, grid, dim3(256), 0, s, p);
     return hipGetLastError();

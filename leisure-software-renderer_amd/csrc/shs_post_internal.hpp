@@ -15,6 +15,7 @@ struct TonemapParams {
     uint32_t *ldr;          // W*H RGBA8, rows y up (RT_ColorLDR), or null
     uint32_t *present;      // W*H RGBA8, rows top-down (upload_ldr_to_rgba8), or null
     int W, H;
+    int rank, count;        // the camera pass's tile shard (count 1: the whole frame)
     float exposure;         // max(0.0001, exposure)
     float inv_gamma;        // 1 / max(0.001, gamma): only steers the first guess
     float thr[256];         // thr[0] unused

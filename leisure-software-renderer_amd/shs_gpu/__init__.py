@@ -13,7 +13,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _abi
-from ._abi import (FRAME_PREQUANT, SHADING_BLINN_PHONG, SHADING_FLAT, SHADING_GOURAUD, SHADING_NAMES,
+from ._abi import (FRAME_PREQUANT, FRAME_PRESENT, SHADING_BLINN_PHONG, SHADING_FLAT, SHADING_GOURAUD, SHADING_NAMES,
                    SHADING_PHONG, FrameDesc, LegacyDraw, RasterStats)
 
 __all__ = [
@@ -55,6 +55,7 @@ class Frame:
     shard_count: int = 1
     clear_color: tuple = (0, 0, 0, 255)
     prequant: bool = False
+    present: bool = False             # SHS_FRAME_PRESENT: also write the SDL staging
     debug_flags: int = 0         # timing experiments only (bits 8+, wrong images)
 
     def desc(self) -> FrameDesc:
@@ -62,7 +63,8 @@ class Frame:
         d.width, d.height = self.width, self.height
         d.ref_tile_w, d.ref_tile_h = self.ref_tile
         d.shard_rank, d.shard_count = self.shard_rank, self.shard_count
-        d.flags = (FRAME_PREQUANT if self.prequant else 0) | (int(self.debug_flags) & ~0xff)
+        d.flags = (FRAME_PREQUANT if self.prequant else 0) | (FRAME_PRESENT if self.present else 0) | \
+                  (int(self.debug_flags) & ~0xff)
         for i in range(4):
             d.clear_color[i] = self.clear_color[i]
         return d
@@ -181,6 +183,15 @@ class Context:
         self._check(self._lib.shs_resolve(self._h, color.ctypes.data_as(ctypes.c_void_p),
                                           depth.ctypes.data_as(ctypes.c_void_p)))
         return color, depth
+
+    def resolve_present(self, index: int = 0, pitch: int = 0):
+        """The SDL staging of frame `index` (Canvas::copy_to_SDLSurface): uint8 [H, W, 4], rows top-down.
+        pitch > W*4 pads rows as an SDL surface would (returned array [H, pitch] bytes)."""
+        f = self._frame
+        pitch = pitch or f.width * 4
+        out = np.zeros((f.height, pitch), dtype=np.uint8)
+        self._check(self._lib.shs_resolve_present(self._h, int(index), out.ctypes.data_as(ctypes.c_void_p), pitch))
+        return out if pitch != f.width * 4 else out.reshape(f.height, f.width, 4)
 
     def resolve_prequant(self):
         f = self._frame
@@ -451,7 +462,7 @@ class Context:
             self.resolve_shadow_map()
 
     # -- tile shards (multi-GPU gather) ----------------------------------------------------------
-    TARGET_LEGACY, TARGET_LIB = 0, 1
+    TARGET_LEGACY, TARGET_LIB, TARGET_PRESENT, TARGET_LIB_PRESENT = 0, 1, 2, 3
 
     def tiles_packed_words(self, target, count):
         n = ctypes.c_int64()
@@ -488,6 +499,22 @@ class Context:
         self._check(self._lib.shs_resolve_light_lists(self._h, counts.ctypes.data_as(vp), idx.ctypes.data_as(vp),
                                                       ranges.ctypes.data_as(vp)))
         return counts, idx, ranges
+
+    def light_bin_culling(self, lb, aabbs):
+        """build_light_bin_culling on the GPU: lb = lib_path.LightBin, aabbs float32 [n, 6] (min, max) ->
+        (bins_xyz, counts uint32 [bins], indices uint32 [bins, cap])."""
+        aabbs = np.ascontiguousarray(aabbs, dtype=np.float32).reshape(-1, 6)
+        keep = []
+        d = lb.desc(aabbs.shape[0], keep)
+        ts = max(lb.tile_size, 1)
+        bx, by = (lb.width + ts - 1) // ts, (lb.height + ts - 1) // ts
+        n_bins = bx * by * (max(lb.z_slices, 1) if lb.mode == 3 else 1)
+        counts = np.zeros(n_bins, np.uint32)
+        idx = np.zeros((n_bins, d.max_per_bin), np.uint32)
+        bins = np.zeros(3, np.uint32)
+        self._check(self._lib.shs_light_bin_culling(self._h, ctypes.byref(d), aabbs.ctypes.data, aabbs.shape[0],
+                                                    bins.ctypes.data, counts.ctypes.data, idx.ctypes.data))
+        return tuple(int(b) for b in bins), counts, idx
 
     def lib_timing_reset(self):
         self._check(self._lib.shs_lib_timing_reset(self._h))

@@ -22,6 +22,7 @@ SHADING_BLINN_PHONG = 3
 SHADING_NAMES = {"flat": 0, "gouraud": 1, "phong": 2, "blinn_phong": 3}
 
 FRAME_PREQUANT = 1
+FRAME_PRESENT = 2
 OPT_BIN_CAPACITY = 1
 OPT_RASTER_MODE = 2
 OPT_TIMELINE = 3
@@ -163,6 +164,14 @@ class LightCullDescC(ctypes.Structure):
                 ("depth_linear", ctypes.c_int32), ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32)]
 
 
+class LightBinDescC(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("tile_size", ctypes.c_uint32),
+                ("mode", ctypes.c_uint32), ("z_slices", ctypes.c_uint32), ("max_per_bin", ctypes.c_uint32),
+                ("view_proj", _F16), ("z_near", ctypes.c_float), ("z_far", ctypes.c_float),
+                ("tile_min_view_depth", ctypes.c_void_p), ("tile_max_view_depth", ctypes.c_void_p),
+                ("n_depth_tiles", ctypes.c_int32)]
+
+
 # (name, restype, argtypes) for every symbol include/shs_gpu.h declares.
 _P = ctypes.c_void_p
 _F = ctypes.POINTER(ctypes.c_float)
@@ -182,6 +191,8 @@ SIGNATURES = [
                                                ctypes.c_int32]),
     ("shs_resolve", ctypes.c_int, [_P, _P, _P]),
     ("shs_resolve_frame", ctypes.c_int, [_P, ctypes.c_int32, _P, _P]),
+    ("shs_resolve_present", ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.c_int32]),
+    ("shs_present_device", ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(_P)]),
     ("shs_resolve_prequant", ctypes.c_int, [_P, _P]),
     ("shs_device_framebuffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("shs_get_stats", ctypes.c_int, [_P, ctypes.POINTER(RasterStats)]),
@@ -222,6 +233,7 @@ SIGNATURES = [
     ("shs_tiles_unpack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
     ("shs_lights_upload", ctypes.c_int, [_P, ctypes.POINTER(CullingLightC), ctypes.c_int32]),
     ("shs_light_cull", ctypes.c_int, [_P, ctypes.POINTER(LightCullDescC)]),
+    ("shs_light_bin_culling", ctypes.c_int, [_P, ctypes.POINTER(LightBinDescC), _P, ctypes.c_int32, _P, _P, _P]),
     ("shs_resolve_light_lists", ctypes.c_int, [_P, _P, _P, _P]),
     ("shs_look_at_lh", ctypes.c_int, [_F, _F, _F, _F]),
     ("shs_perspective_lh_no", ctypes.c_int, [ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F]),

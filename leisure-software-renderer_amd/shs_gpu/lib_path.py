@@ -247,3 +247,44 @@ def dir_light_camera_aabb(sun_dir, mn, mx, margin=10.0, res=2048):
     s, a, b = _v3(sun_dir), _v3(mn), _v3(mx)
     assert _abi.lib().shs_dir_light_camera_aabb(_fp(s), _fp(a), _fp(b), margin, res, _fp(v), _fp(p), _fp(vp)) == 0
     return v, p, vp
+
+
+# ---- the software library's CPU light binning (build_light_bin_culling) ------
+@dataclass
+class LightBin:
+    """LightBinCullingConfig + the call's view_proj / viewport (light_culling_runtime.hpp:29-36, 266-275).
+    mode: 0 none, 1 tiled, 2 tiled + per-tile view-depth range, 3 clustered."""
+    width: int
+    height: int
+    view_proj: np.ndarray
+    mode: int = 1
+    tile_size: int = 16
+    z_slices: int = 16
+    z_near: float = 0.1
+    z_far: float = 1000.0
+    max_per_bin: int = 0               # 0: unbounded (n_lights)
+    tile_min_view_depth: np.ndarray = None
+    tile_max_view_depth: np.ndarray = None
+
+    def desc(self, n_lights, keep):
+        d = _abi.LightBinDescC()
+        d.width, d.height = self.width, self.height
+        d.tile_size, d.mode, d.z_slices = self.tile_size, self.mode, self.z_slices
+        d.max_per_bin = self.max_per_bin if self.max_per_bin > 0 else max(int(n_lights), 1)
+        for k in range(16):
+            d.view_proj[k] = float(self.view_proj[k])
+        d.z_near, d.z_far = self.z_near, self.z_far
+        if self.tile_min_view_depth is not None:
+            mn = np.ascontiguousarray(self.tile_min_view_depth, dtype=np.float32)
+            mx = np.ascontiguousarray(self.tile_max_view_depth, dtype=np.float32)
+            keep += [mn, mx]
+            d.tile_min_view_depth, d.tile_max_view_depth = mn.ctypes.data, mx.ctypes.data
+            d.n_depth_tiles = int(mn.size)
+        return d
+
+
+def light_aabbs(lights):
+    """World AABBs of point lights as Jolt sphere SceneShapes of radius = range: position -/+ range."""
+    pr = np.asarray(lights["position_range"], np.float32)
+    pos, r = pr[:, :3], pr[:, 3:4]
+    return np.concatenate([pos - r, pos + r], axis=1).astype(np.float32)

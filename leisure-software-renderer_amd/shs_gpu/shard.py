@@ -112,25 +112,34 @@ def unpack_padded(planes, packed, width, height, rank, count, tile=32):
             p[y0:y1, x0:x1] = blk[i, c, :y1 - y0, :x1 - x0]
 
 
-def gather_frame_device(dist, ctx, target, stream=None):
-    """RCCL gather of a tile-sharded frame into rank 0's context framebuffers (device to device).
-    Every rank packs its owned tiles on the GPU (shs_tiles_pack), rank 0 receives the peers' buffers
-    with dist.gather (ncclSend/Recv over xGMI) and unpacks them in place (shs_tiles_unpack).  The
-    context runs on torch's current stream so RCCL and the kernels are ordered."""
+def gather_frame_device(dist, ctx, target, stream=None, out=None):
+    """RCCL gather of a tile-sharded frame into rank 0's context buffers (device to device).
+    Every rank packs its owned tiles on the GPU (shs_tiles_pack, which first finishes the frame: a
+    capacity overflow is re-issued before anything leaves the rank), rank 0 receives the peers'
+    buffers with dist.gather (ncclSend/Recv over xGMI) and unpacks them in place (shs_tiles_unpack).
+    The context runs on torch's current stream so RCCL and the kernels are ordered; it is re-pointed
+    only when it is not on that stream already (shs_set_stream synchronises).
+    target: ctx.TARGET_PRESENT / TARGET_LIB_PRESENT (RGBA8, 4 B/px: what the SDL present needs) or
+    TARGET_LEGACY / TARGET_LIB (colour + depth (+ motion): 8 / 28 B/px).
+    out: optional list of preallocated int32 device buffers [count + 1] (send + receive) to reuse."""
     rank, count = dist.get_rank(), dist.get_world_size()
     s = stream if stream is not None else torch.cuda.current_stream()
-    ctx.set_stream(s.cuda_stream)
+    if ctx.stream != s.cuda_stream:
+        ctx.set_stream(s.cuda_stream)
     words = ctx.tiles_packed_words(target, count)
-    buf = torch.empty(words, dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if out is None or out[0].numel() != words:
+        out = [torch.empty(words, dtype=torch.int32, device=dev) for _ in range(count + 1)]
+    buf = out[0]
     ctx.tiles_pack(target, rank, count, buf.data_ptr())
     if rank == 0:
-        bufs = [torch.empty_like(buf) for _ in range(count)]
+        bufs = out[1:]
         dist.gather(buf, gather_list=bufs, dst=0)
         for r in range(1, count):
             ctx.tiles_unpack(target, r, count, bufs[r].data_ptr())
     else:
         dist.gather(buf, dst=0)
-    return rank == 0
+    return out
 
 
 def gather_frame(dist, color, depth, tile, device=None):

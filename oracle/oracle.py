@@ -508,3 +508,58 @@ def legacy_mvp(view, proj, model, flat=False):
     mv = np.zeros(16, np.float32)
     lib().ora_legacy_mvp(v.ctypes.data, p.ctypes.data, m.ctypes.data, 1 if flat else 0, mvp.ctypes.data, mv.ctypes.data)
     return mvp, mv
+
+
+def sdl_present(canvas_rgba):
+    """Canvas::copy_to_SDLSurface (shs_renderer.hpp:833-848) into create_sdl_surface's RGBA32 surface
+    (:850-856, little-endian masks R 0x000000ff .. A 0xff000000): surface row h-1-y = canvas row y,
+    SDL_MapRGBA(r, g, b, a) = the Color bytes.  canvas_rgba: uint8 [H, W, 4] canvas rows -> uint8
+    [H, W, 4] surface rows (top-down)."""
+    c = np.ascontiguousarray(canvas_rgba, dtype=np.uint8)
+    h, w = c.shape[:2]
+    out = np.empty_like(c)
+    for y in range(h):
+        out[h - 1 - y] = c[y]
+    return out
+
+
+
+class OraLightBinDesc(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("tile_size", ctypes.c_uint32),
+                ("mode", ctypes.c_uint32), ("z_slices", ctypes.c_uint32), ("max_per_bin", ctypes.c_uint32),
+                ("view_proj", _F16), ("z_near", ctypes.c_float), ("z_far", ctypes.c_float),
+                ("tile_min_view_depth", ctypes.c_void_p), ("tile_max_view_depth", ctypes.c_void_p),
+                ("n_depth_tiles", ctypes.c_int32)]
+
+
+def light_bin_culling(lb, aabbs):
+    """build_light_bin_culling (light_culling_runtime.hpp:266-371), oracle/shs_oracle_lightbin.c.
+    lb: shs_gpu.lib_path.LightBin; aabbs float32 [n, 6] -> (bins_xyz, counts, indices [bins, cap])."""
+    L = lib()
+    if not getattr(L, "_lb_ready", False):
+        L.ora_light_bin_culling.restype = ctypes.c_int
+        L.ora_light_bin_culling.argtypes = [ctypes.POINTER(OraLightBinDesc), ctypes.c_void_p, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L._lb_ready = True
+    aabbs = np.ascontiguousarray(aabbs, dtype=np.float32).reshape(-1, 6)
+    n = aabbs.shape[0]
+    d = OraLightBinDesc()
+    d.width, d.height, d.tile_size, d.mode, d.z_slices = lb.width, lb.height, lb.tile_size, lb.mode, lb.z_slices
+    d.max_per_bin = lb.max_per_bin if lb.max_per_bin > 0 else max(n, 1)
+    for k in range(16):
+        d.view_proj[k] = float(lb.view_proj[k])
+    d.z_near, d.z_far = lb.z_near, lb.z_far
+    keep = []
+    if lb.tile_min_view_depth is not None:
+        mn = np.ascontiguousarray(lb.tile_min_view_depth, dtype=np.float32)
+        mx = np.ascontiguousarray(lb.tile_max_view_depth, dtype=np.float32)
+        keep += [mn, mx]
+        d.tile_min_view_depth, d.tile_max_view_depth, d.n_depth_tiles = mn.ctypes.data, mx.ctypes.data, mn.size
+    ts = max(lb.tile_size, 1)
+    bx, by = (lb.width + ts - 1) // ts, (lb.height + ts - 1) // ts
+    n_bins = bx * by * (max(lb.z_slices, 1) if lb.mode == 3 else 1)
+    counts = np.zeros(n_bins, np.uint32)
+    idx = np.zeros((n_bins, d.max_per_bin), np.uint32)
+    bins = np.zeros(3, np.uint32)
+    L.ora_light_bin_culling(ctypes.byref(d), aabbs.ctypes.data, n, bins.ctypes.data, counts.ctypes.data, idx.ctypes.data)
+    return tuple(int(b) for b in bins), counts, idx

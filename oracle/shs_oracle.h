@@ -211,4 +211,19 @@ void ora_perspective_lh_no(float fovy, float aspect, float zn, float zf, float o
 void ora_legacy_mvp(const float view16[16], const float proj16[16], const float model16[16], int flat, float mvp16[16],
                     float mv16[16]);
 
+/* shs_oracle_lightbin.c: build_light_bin_culling (light_culling_runtime.hpp:266-371) over lights given as
+ * world AABBs (min xyz, max xyz per light: SceneShape::world_aabb()).  Lists: counts[bin] (all matches)
+ * and indices[bin * max_per_bin + k] (the first max_per_bin, ascending); bins tile-row-major, clusters
+ * slice-major; bins_xyz = (bins_x, bins_y, bins_z), all 0 for mode None / no lights. */
+typedef struct ora_light_bin_desc {
+    int32_t width, height;
+    uint32_t tile_size, mode, z_slices, max_per_bin;
+    float view_proj[16];
+    float z_near, z_far;
+    const float *tile_min_view_depth, *tile_max_view_depth;   /* mode 2, tiles_x * tiles_y each */
+    int32_t n_depth_tiles;
+} ora_light_bin_desc;
+int ora_light_bin_culling(const ora_light_bin_desc *d, const float *aabbs, int n_lights, uint32_t *bins_xyz,
+                          uint32_t *counts, uint32_t *indices);
+
 #endif

@@ -71,3 +71,95 @@ def test_legacy_shards_gather_on_device():
     assert np.array_equal(gc, fc) and np.array_equal(gd.view(np.uint32), fd.view(np.uint32))
     for c in ctxs + [full]:
         c.close()
+
+
+@pytest.mark.parametrize("count", [2, 8])
+def test_lib_present_gather_after_sharded_tonemap(count):
+    """The multi-GPU frame as bench C4 / C5 run it: every rank renders its tiles, tonemaps only those
+    (k_tonemap_tiles) into the present staging, and ships 4 B/px (SHS_TARGET_LIB_PRESENT); rank 0's
+    composed staging equals the unsharded frame's tonemapped staging."""
+    import torch
+    import shs_gpu
+    from shs_gpu import scene_lib, shard
+    frame, draws, _, _, _ = scene_lib.c5_scene(352, 200)
+    full = shs_gpu.Context(0)
+    full.render_pbr_forward(frame, draws)
+    full.tonemap(1.0, 2.2, ldr=False, present=True)
+    _, want = full.resolve_ldr()
+    ctxs, bufs = [], []
+    for r in range(count):
+        c = shs_gpu.Context(0)
+        frame.shard_rank, frame.shard_count = r, count
+        c.render_pbr_forward(frame, draws)
+        c.tonemap(1.0, 2.2, ldr=False, present=True)
+        buf = torch.zeros(c.tiles_packed_words(c.TARGET_LIB_PRESENT, count), dtype=torch.int32, device="cuda:0")
+        c.tiles_pack(c.TARGET_LIB_PRESENT, r, count, buf.data_ptr())   # finishes the pass chain first
+        c.synchronize_lib()
+        _, pres = c.resolve_ldr()
+        host = shard.pack_padded(shard.planes_of([(pres, True)]), 352, 200, r, count)
+        assert np.array_equal(buf.cpu().numpy().view(np.uint32)[:host.size], host)
+        ctxs.append(c)
+        bufs.append(buf)
+    for r in range(1, count):
+        ctxs[0].tiles_unpack(ctxs[0].TARGET_LIB_PRESENT, r, count, bufs[r].data_ptr())
+    _, got = ctxs[0].resolve_ldr()
+    assert np.array_equal(got, want)
+    for c in ctxs + [full]:
+        c.close()
+
+
+def test_legacy_present_gather():
+    import torch
+    import shs_gpu
+    from shs_gpu import scene
+    count = 3
+    frame, draws = scene.monkey_scene(640, 480, 3, cam_pos=(0.0, 5.0, -12.0))
+    frame.present = True
+    full = shs_gpu.Context(0)
+    full.render(frame, draws)
+    want = full.resolve_present(0)
+    ctxs, bufs = [], []
+    for r in range(count):
+        c = shs_gpu.Context(0)
+        f = shs_gpu.Frame(640, 480, shard_rank=r, shard_count=count)
+        f.present = True
+        c.render(f, draws)
+        buf = torch.zeros(c.tiles_packed_words(c.TARGET_PRESENT, count), dtype=torch.int32, device="cuda:0")
+        c.tiles_pack(c.TARGET_PRESENT, r, count, buf.data_ptr())
+        c.synchronize()
+        ctxs.append(c)
+        bufs.append(buf)
+    for r in range(1, count):
+        ctxs[0].tiles_unpack(ctxs[0].TARGET_PRESENT, r, count, bufs[r].data_ptr())
+    assert np.array_equal(ctxs[0].resolve_present(0), want)
+    for c in ctxs + [full]:
+        c.close()
+
+
+def test_legacy_binned_hair_shards_compose():
+    """sharded, binned frames with unbounded slivers (k_ghost reads k_setup's records and
+    the sliver list and applies the tile ownership): the shards compose to the unsharded frame."""
+    import shs_gpu
+    from shs_gpu.scene import Mesh
+    from test_gpu_parity import _hair_soup, _identity_draw
+    W, H, count = 400, 300, 3
+    rng = np.random.default_rng(99)
+    pos, nrm = _hair_soup(rng, W, H, 3000)
+    draw = _identity_draw(Mesh(pos, nrm), 3)
+    ctx = shs_gpu.Context(0)
+    try:
+        ctx.set_raster_mode(2)
+        ctx.render(shs_gpu.Frame(W, H), [draw])
+        fc, fd = ctx.resolve()
+        assert ctx.stats()["ghost_fragments"] > 0
+        oc, od = np.zeros_like(fc), np.zeros_like(fd)
+        ty, tx = np.mgrid[0:H, 0:W] // 32
+        for r in range(count):
+            ctx.render(shs_gpu.Frame(W, H, shard_rank=r, shard_count=count), [draw])
+            c, d = ctx.resolve()
+            own = (ty * ((W + 31) // 32) + tx) % count == r       # screen rows
+            od[own] = d[own]
+            oc[own[::-1]] = c[own[::-1]]                          # colour in canvas rows
+        assert np.array_equal(od.view(np.uint32), fd.view(np.uint32)) and np.array_equal(oc, fc)
+    finally:
+        ctx.close()
