@@ -435,6 +435,38 @@ int shs_occlusion_pass(shs_ctx *ctx, const shs_occlusion_desc *desc, const shs_o
                        const uint32_t *frustum_visible, int32_t n_frustum_visible, uint8_t *occluded,
                        uint32_t *visible, int32_t *n_visible, float *depth);
 
+/* ---- debug_draw colour + depth raster ----------------------------------------
+ * shs::debug_draw (shs-renderer-lib/include/shs/sw_render/debug_draw.hpp): draw_filled_triangle
+ * (:60-109) and draw_mesh_blinn_phong_transformed (:147-203), the lit-surface draw of the culling
+ * demos (hello_occlusion_culling_sw.cpp:387-407, hello_culling_sw.cpp:315).  rgba is the RT_ColorLDR
+ * (W*H Color, y * W + x, the rows as the canvas holds them) and depth the std::span<float> depth
+ * buffer (y * W + x); both are read and written in place, exactly as a sequential draw of the list in
+ * submission order leaves them.  Synchronous. */
+typedef struct shs_debug_draw_desc {
+    int32_t width, height;      /* canvas_w, canvas_h (== rt.w, rt.h) */
+    float view_proj[16];        /* vp (column-major) */
+    float camera_pos[3];
+    float light_dir_ws[3];
+} shs_debug_draw_desc;
+typedef struct shs_debug_mesh {
+    int32_t mesh_id;            /* indexed shs_mesh_upload mesh (DebugMesh vertices + indices) */
+    float model[16];            /* column-major */
+    float base_color[3];
+} shs_debug_mesh;
+/* The meshes in order, each draw_mesh_blinn_phong_transformed.  tri_lit (may be NULL): 4 floats per
+ * triangle in submission order -- lit.rgb before the byte conversion (0 when the triangle is culled
+ * before shading) and 1.0 when the triangle passes draw_filled_triangle's area test (0.0 otherwise). */
+int shs_debug_draw_meshes(shs_ctx *ctx, const shs_debug_draw_desc *desc, const shs_debug_mesh *meshes,
+                          int32_t n_meshes, uint8_t *rgba, float *depth, float *tri_lit);
+typedef struct shs_debug_triangle {
+    float p0[2], p1[2], p2[2];  /* screen points (pixels) */
+    float z[3];                 /* depths z0, z1, z2 */
+    uint8_t rgba[4];            /* Color */
+} shs_debug_triangle;
+/* draw_filled_triangle for each triangle in order. */
+int shs_debug_fill_triangles(shs_ctx *ctx, int32_t width, int32_t height, const shs_debug_triangle *tris,
+                             int32_t n_tris, uint8_t *rgba, float *depth);
+
 /* Host-only (no device): the byte thresholds for gamma (thr[0] = 0; +inf where a byte is never
  * reached).  Exposed for the parity tests. */
 int shs_tonemap_thresholds(float gamma, float thr[256]);

@@ -317,6 +317,8 @@ void shs_lib_release(shs_ctx *ctx) {
     release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
     release(ctx->lb_lights); release(ctx->lb_ndc); release(ctx->lb_counts); release(ctx->lb_indices);
     release(ctx->occ_depth); release(ctx->occ_visible); release(ctx->occ_flags); release(ctx->occ_objs); release(ctx->occ_rects); release(ctx->occ_tris);
+    release(ctx->dd_objs); release(ctx->dd_tris); release(ctx->dd_depth0); release(ctx->dd_depth); release(ctx->dd_lit_b);
+    release(ctx->dd_rgba); release(ctx->dd_keys); release(ctx->dd_big);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
 }

@@ -10,6 +10,7 @@
 #include "../../include/shs_gpu.h"
 #include "shs_device.hpp"
 #include "shs_lib_device.hpp"
+#include "shs_debugdraw_internal.hpp"
 #include "shs_lightbin_internal.hpp"
 #include "shs_occlusion_internal.hpp"
 
@@ -181,6 +182,13 @@ struct shs_ctx {
     DevBuf<shs_dev::OccObject> occ_objs;
     DevBuf<shs_dev::OccRect> occ_rects;
     DevBuf<shs_dev::OccTri> occ_tris;
+
+    // debug_draw (shs_abi_debugdraw.cpp)
+    DevBuf<shs_dev::DDObject> dd_objs;
+    DevBuf<shs_dev::DDTri> dd_tris;
+    DevBuf<float> dd_depth0, dd_depth, dd_lit_b;
+    DevBuf<uint32_t> dd_rgba, dd_big;
+    DevBuf<unsigned long long> dd_keys;
 };
 
 // Re-enqueues the tonemap after lib_finish re-issued the camera pass (shs_abi_post.cpp).

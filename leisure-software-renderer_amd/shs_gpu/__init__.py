@@ -324,6 +324,58 @@ class Context:
                                                  depth.ctypes.data_as(ctypes.c_void_p)))
         return occ[:n], vis[:nv.value], depth
 
+    def debug_draw_meshes(self, width, height, view_proj, camera_pos, light_dir_ws, meshes, rgba=None, depth=None,
+                          tri_lit=False):
+        """debug_draw::draw_mesh_blinn_phong_transformed (sw_render/debug_draw.hpp:147-203) over meshes =
+        sequence of (LibMesh with indices, model float[16], base_color[3]), in order.  rgba uint8
+        [height, width, 4] (RT_ColorLDR, y * W + x) and depth float32 [height, width] are drawn into in
+        place (defaults: cleared to 0 / 1.0).  Returns (rgba, depth) or, with tri_lit, (rgba, depth,
+        float32 [n_tris, 4] lit rgb + area-test flag)."""
+        rgba = np.zeros((height, width, 4), np.uint8) if rgba is None else rgba
+        depth = np.ones((height, width), np.float32) if depth is None else depth
+        assert rgba.shape == (height, width, 4) and rgba.dtype == np.uint8 and rgba.flags.c_contiguous
+        assert depth.shape == (height, width) and depth.dtype == np.float32 and depth.flags.c_contiguous
+        n = len(meshes)
+        arr = (_abi.DebugMeshC * max(n, 1))()
+        n_tris = 0
+        for i, (mesh, model, base) in enumerate(meshes):
+            arr[i].mesh_id = self.upload_lib_mesh(mesh)
+            for k in range(16):
+                arr[i].model[k] = float(model[k])
+            for k in range(3):
+                arr[i].base_color[k] = float(base[k])
+            n_tris += len(mesh.indices) // 3
+        d = _abi.DebugDrawDescC()
+        d.width, d.height = int(width), int(height)
+        for k in range(16):
+            d.view_proj[k] = float(view_proj[k])
+        for k in range(3):
+            d.camera_pos[k], d.light_dir_ws[k] = float(camera_pos[k]), float(light_dir_ws[k])
+        lit = np.zeros((max(n_tris, 1), 4), np.float32) if tri_lit else None
+        self._check(self._lib.shs_debug_draw_meshes(self._h, ctypes.byref(d), arr, n, rgba.ctypes.data_as(ctypes.c_void_p),
+                                                    depth.ctypes.data_as(ctypes.c_void_p),
+                                                    None if lit is None else lit.ctypes.data_as(ctypes.c_void_p)))
+        return (rgba, depth, lit[:n_tris]) if tri_lit else (rgba, depth)
+
+    def debug_fill_triangles(self, width, height, screen, z, colors, rgba=None, depth=None):
+        """debug_draw::draw_filled_triangle (debug_draw.hpp:60-109) for each triangle in order: screen
+        float32 [n, 3, 2] points, z float32 [n, 3], colors uint8 [n, 4]."""
+        rgba = np.zeros((height, width, 4), np.uint8) if rgba is None else rgba
+        depth = np.ones((height, width), np.float32) if depth is None else depth
+        assert rgba.shape == (height, width, 4) and rgba.dtype == np.uint8 and rgba.flags.c_contiguous
+        assert depth.shape == (height, width) and depth.dtype == np.float32 and depth.flags.c_contiguous
+        screen = np.asarray(screen, np.float32).reshape(-1, 6)
+        n = screen.shape[0]
+        rec = np.zeros((max(n, 1), ctypes.sizeof(_abi.DebugTriangleC) // 4), np.float32)
+        rec[:n, 0:6] = screen
+        rec[:n, 6:9] = np.asarray(z, np.float32).reshape(n, 3)
+        rec[:n, 9].view(np.uint32)[:] = np.ascontiguousarray(colors, np.uint8).reshape(n, 4).view(np.uint32).reshape(n)
+        self._check(self._lib.shs_debug_fill_triangles(self._h, int(width), int(height),
+                                                       rec.ctypes.data_as(ctypes.POINTER(_abi.DebugTriangleC)), n,
+                                                       rgba.ctypes.data_as(ctypes.c_void_p),
+                                                       depth.ctypes.data_as(ctypes.c_void_p)))
+        return rgba, depth
+
     def lib_device_targets(self):
         """Device pointers of the library targets: (hdr float4 W*H, depth W*H, motion float2 W*H)."""
         a, b, c = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()

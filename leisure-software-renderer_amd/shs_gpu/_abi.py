@@ -144,6 +144,20 @@ class OcclusionDescC(ctypes.Structure):
                 ("depth_epsilon", ctypes.c_float), ("enable", ctypes.c_int32)]
 
 
+class DebugDrawDescC(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("view_proj", _F16), ("camera_pos", _F3),
+                ("light_dir_ws", _F3)]
+
+
+class DebugMeshC(ctypes.Structure):
+    _fields_ = [("mesh_id", ctypes.c_int32), ("model", _F16), ("base_color", _F3)]
+
+
+class DebugTriangleC(ctypes.Structure):
+    _fields_ = [("p0", ctypes.c_float * 2), ("p1", ctypes.c_float * 2), ("p2", ctypes.c_float * 2), ("z", _F3),
+                ("rgba", ctypes.c_uint8 * 4)]
+
+
 class TonemapDescC(ctypes.Structure):
     _fields_ = [("exposure", ctypes.c_float), ("gamma", ctypes.c_float), ("flags", ctypes.c_uint32)]
 LIGHT_CULL_NONE, LIGHT_CULL_TILED, LIGHT_CULL_TILED_DEPTH, LIGHT_CULL_CLUSTERED = 0, 1, 2, 3
@@ -211,6 +225,10 @@ SIGNATURES = [
     ("shs_tonemap_thresholds", ctypes.c_int, [ctypes.c_float, _F]),
     ("shs_occlusion_pass", ctypes.c_int, [_P, ctypes.POINTER(OcclusionDescC), ctypes.POINTER(OccluderC), ctypes.c_int32,
                                           _P, ctypes.c_int32, _P, _P, ctypes.POINTER(ctypes.c_int32), _P]),
+    ("shs_debug_draw_meshes", ctypes.c_int, [_P, ctypes.POINTER(DebugDrawDescC), ctypes.POINTER(DebugMeshC), ctypes.c_int32,
+                                             _P, _P, _P]),
+    ("shs_debug_fill_triangles", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(DebugTriangleC),
+                                                ctypes.c_int32, _P, _P]),
     ("shs_motion_blur", ctypes.c_int, [_P, ctypes.POINTER(MotionBlurDescC)]),
     ("shs_resolve_motion_blur", ctypes.c_int, [_P, _P, _P]),
     ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),

@@ -563,3 +563,66 @@ def light_bin_culling(lb, aabbs):
     bins = np.zeros(3, np.uint32)
     L.ora_light_bin_culling(ctypes.byref(d), aabbs.ctypes.data, n, bins.ctypes.data, counts.ctypes.data, idx.ctypes.data)
     return tuple(int(b) for b in bins), counts, idx
+
+
+# ---- debug_draw (shs_oracle_debugdraw.c) -------------------------------------------------------------
+class OraDDMesh(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_void_p), ("n_verts", ctypes.c_int32), ("idx", ctypes.c_void_p), ("n_idx", ctypes.c_int32),
+                ("model", _F16), ("base", ctypes.c_float * 3)]
+
+
+def _dd_ready(L):
+    if not getattr(L, "_dd_ready", False):
+        P = ctypes.c_void_p
+        L.ora_debug_draw_meshes.restype = ctypes.c_int
+        L.ora_debug_draw_meshes.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P, P]
+        L.ora_draw_filled_triangle.restype = None
+        L.ora_draw_filled_triangle.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_float, P, ctypes.c_float,
+                                               P, ctypes.c_float, P]
+        L._dd_ready = True
+
+
+def debug_draw_meshes(width, height, view_proj, camera_pos, light_dir_ws, meshes, rgba=None, depth=None):
+    """draw_mesh_blinn_phong_transformed (debug_draw.hpp:147-203) over meshes = [(mesh, model[16],
+    base[3])] in order -> (rgba uint8 [H, W, 4], depth [H, W], tri_lit float32 [n_tris, 4])."""
+    L = lib()
+    _dd_ready(L)
+    rgba = np.zeros((height, width, 4), np.uint8) if rgba is None else np.array(rgba, np.uint8, copy=True)
+    depth = np.ones((height, width), np.float32) if depth is None else np.array(depth, np.float32, copy=True)
+    n = len(meshes)
+    arr = (OraDDMesh * max(n, 1))()
+    keep = []
+    n_tris = 0
+    for i, (mesh, model, base) in enumerate(meshes):
+        pos = np.ascontiguousarray(mesh.positions, dtype=np.float32)
+        idx = np.ascontiguousarray(mesh.indices, dtype=np.uint32)
+        keep += [pos, idx]
+        a = arr[i]
+        a.pos, a.n_verts, a.idx, a.n_idx = pos.ctypes.data, pos.shape[0], idx.ctypes.data, idx.size
+        for k in range(16):
+            a.model[k] = float(model[k])
+        for k in range(3):
+            a.base[k] = float(base[k])
+        n_tris += idx.size // 3
+    lit = np.zeros((max(n_tris, 1), 4), np.float32)
+    vp, cam, ld = _f32(view_proj, 16), _f32(camera_pos, 3), _f32(light_dir_ws, 3)
+    L.ora_debug_draw_meshes(ctypes.addressof(arr), n, width, height, vp.ctypes.data, cam.ctypes.data, ld.ctypes.data,
+                            rgba.ctypes.data, depth.ctypes.data, lit.ctypes.data)
+    return rgba, depth, lit[:n_tris]
+
+
+def draw_filled_triangles(width, height, screen, z, colors, rgba=None, depth=None):
+    """draw_filled_triangle (debug_draw.hpp:60-109) for each triangle in order."""
+    L = lib()
+    _dd_ready(L)
+    rgba = np.zeros((height, width, 4), np.uint8) if rgba is None else np.array(rgba, np.uint8, copy=True)
+    depth = np.ones((height, width), np.float32) if depth is None else np.array(depth, np.float32, copy=True)
+    screen = np.ascontiguousarray(screen, np.float32).reshape(-1, 3, 2)
+    z = np.ascontiguousarray(z, np.float32).reshape(-1, 3)
+    colors = np.ascontiguousarray(colors, np.uint8).reshape(-1, 4)
+    for t in range(screen.shape[0]):
+        p = screen[t]
+        L.ora_draw_filled_triangle(rgba.ctypes.data, depth.ctypes.data, width, height, p[0].ctypes.data, float(z[t, 0]),
+                                   p[1].ctypes.data, float(z[t, 1]), p[2].ctypes.data, float(z[t, 2]),
+                                   colors[t].ctypes.data)
+    return rgba, depth

@@ -226,4 +226,21 @@ typedef struct ora_light_bin_desc {
 int ora_light_bin_culling(const ora_light_bin_desc *d, const float *aabbs, int n_lights, uint32_t *bins_xyz,
                           uint32_t *counts, uint32_t *indices);
 
+/* shs_oracle_debugdraw.c: debug_draw::draw_filled_triangle (sw_render/debug_draw.hpp:60-109) and
+ * draw_mesh_blinn_phong_transformed (:147-203).  rgba W*H*4 and depth W*H (y * W + x) in place;
+ * tri_lit (may be NULL) 4 floats per triangle: lit rgb before the byte conversion (0 when culled
+ * before shading), 1.0 when the triangle reaches the pixel loop.  Returns the triangle count. */
+void ora_draw_filled_triangle(uint8_t *rgba, float *depth, int W, int H, const float *p0, float z0, const float *p1,
+                              float z1, const float *p2, float z2, const uint8_t *c);
+typedef struct ora_dd_mesh {
+    const float *pos;
+    int32_t n_verts;
+    const uint32_t *idx;
+    int32_t n_idx;
+    float model[16];
+    float base[3];
+} ora_dd_mesh;
+int ora_debug_draw_meshes(const ora_dd_mesh *meshes, int n_meshes, int W, int H, const float *vp, const float *cam,
+                          const float *light_dir, uint8_t *rgba, float *depth, float *tri_lit);
+
 #endif

@@ -10,6 +10,7 @@ if [ -n "${TESTS:-tests}" ] && [ "${TESTS}" != "none" ]; then
   tail -2 gpurun_out/${TAG}_tests.log
 fi
 for c in ${CONFIGS:-c2}; do
+  [ "$c" = none ] && continue
   timeout -k 10 300 python bench.py --config $c --no-pmc --no-cpu ${BENCH_ARGS:---steps 50 --warmup 10} \
     > gpurun_out/${TAG}_bench_$c.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench_$c.log; exit 1; }
   grep '^{' gpurun_out/${TAG}_bench_$c.log | tail -1
