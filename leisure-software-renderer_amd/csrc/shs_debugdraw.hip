@@ -204,26 +204,70 @@ __global__ __launch_bounds__(256) void k_dd_raster(DDParams p) {
     }
 }
 
-// The big triangles: every workgroup takes every G-th 256-pixel chunk of the concatenated bboxes.
+// The big triangles: their bboxes concatenated in 256-pixel chunks, chunk c to workgroup c % G.  Each
+// workgroup stages a round of DD_ROUND big triangles in LDS (triangle, inclusive chunk prefix) with one
+// parallel load, then finds the triangle of each chunk it owns by a binary search in LDS.
 constexpr int DD_BIG_GRID = 2048;
+constexpr int DD_ROUND = 1024;
 
 __global__ __launch_bounds__(256) void k_dd_raster_big(DDParams p) {
+    __shared__ uint32_t s_g[DD_ROUND], s_end[DD_ROUND], s_wave[4];
     const uint32_t nb = *p.big_count;
-    uint32_t base = 0;   // chunks of the big triangles before this one
-    for (uint32_t i = 0; i < nb; ++i) {
-        const uint32_t g = p.big_list[i];
-        const DDTri t = p.tris[g];
-        const int min_x = (int)(t.bmin & 0xffffu), min_y = (int)(t.bmin >> 16);
-        const int bw = (int)(t.bmax & 0xffffu) - min_x + 1, bh = (int)(t.bmax >> 16) - min_y + 1;
-        const uint32_t n = (uint32_t)bw * (uint32_t)bh, chunks = (n + 255u) / 256u;
-        const uint32_t c0 = (blockIdx.x + DD_BIG_GRID - base % DD_BIG_GRID) % DD_BIG_GRID;
-        for (uint32_t c = c0; c < chunks; c += DD_BIG_GRID) {
-            const uint32_t k = c * 256u + threadIdx.x;
-            if (k >= n) continue;
-            const int ry = (int)(k / (uint32_t)bw);
-            dd_test(p, t, min_x + ((int)k - ry * bw), min_y + ry, g);
+    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t base = 0;   // chunks of the rounds before
+    for (uint32_t r0 = 0; r0 < nb; r0 += DD_ROUND) {
+        const uint32_t m = min((uint32_t)DD_ROUND, nb - r0);
+        uint32_t cnt[4], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = (uint32_t)tid * 4u + (uint32_t)j;
+            cnt[j] = 0;
+            if (i < m) {
+                const uint32_t g = p.big_list[r0 + i];
+                const uint32_t bmin = p.tris[g].bmin, bmax = p.tris[g].bmax;
+                const uint32_t n = ((bmax & 0xffffu) - (bmin & 0xffffu) + 1u) * ((bmax >> 16) - (bmin >> 16) + 1u);
+                cnt[j] = (n + 255u) / 256u;
+                s_g[i] = g;
+            }
+            sum += cnt[j];
         }
-        base += chunks;
+        uint32_t incl = sum;   // wave inclusive scan of the per-thread sums
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= d) incl += v;
+        }
+        if (lane == 63) s_wave[wave] = incl;
+        __syncthreads();
+        uint32_t run = incl - sum;
+        for (int w = 0; w < wave; ++w) run += s_wave[w];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = (uint32_t)tid * 4u + (uint32_t)j;
+            run += cnt[j];
+            if (i < m) s_end[i] = run;
+        }
+        __syncthreads();
+        const uint32_t total = s_end[m - 1];
+        for (uint32_t c = (blockIdx.x + DD_BIG_GRID - base % DD_BIG_GRID) % DD_BIG_GRID; c < total; c += DD_BIG_GRID) {
+            uint32_t lo = 0, hi = m - 1;   // the first entry with s_end > c
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_end[mid] > c) hi = mid; else lo = mid + 1;
+            }
+            const uint32_t g = s_g[lo];
+            const uint32_t first = lo ? s_end[lo - 1] : 0u;
+            const DDTri t = p.tris[g];
+            const int min_x = (int)(t.bmin & 0xffffu), min_y = (int)(t.bmin >> 16);
+            const int bw = (int)(t.bmax & 0xffffu) - min_x + 1, bh = (int)(t.bmax >> 16) - min_y + 1;
+            const uint32_t k = (c - first) * 256u + (uint32_t)tid;
+            if (k < (uint32_t)bw * (uint32_t)bh) {
+                const int ry = (int)(k / (uint32_t)bw);
+                dd_test(p, t, min_x + ((int)k - ry * bw), min_y + ry, g);
+            }
+        }
+        base += total;
+        __syncthreads();   // s_g / s_end are rewritten by the next round
     }
 }
 

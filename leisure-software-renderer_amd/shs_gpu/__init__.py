@@ -336,15 +336,14 @@ class Context:
         assert rgba.shape == (height, width, 4) and rgba.dtype == np.uint8 and rgba.flags.c_contiguous
         assert depth.shape == (height, width) and depth.dtype == np.float32 and depth.flags.c_contiguous
         n = len(meshes)
-        arr = (_abi.DebugMeshC * max(n, 1))()
+        # shs_debug_mesh records (int32 mesh_id, float model[16], base_color[3]) built in numpy
+        arr = np.zeros((max(n, 1), ctypes.sizeof(_abi.DebugMeshC) // 4), np.float32)
         n_tris = 0
-        for i, (mesh, model, base) in enumerate(meshes):
-            arr[i].mesh_id = self.upload_lib_mesh(mesh)
-            for k in range(16):
-                arr[i].model[k] = float(model[k])
-            for k in range(3):
-                arr[i].base_color[k] = float(base[k])
-            n_tris += len(mesh.indices) // 3
+        if n:
+            arr[:n, 0].view(np.int32)[:] = [self.upload_lib_mesh(m[0]) for m in meshes]
+            arr[:n, 1:17] = np.asarray([m[1] for m in meshes], np.float32).reshape(n, 16)
+            arr[:n, 17:20] = np.asarray([m[2] for m in meshes], np.float32).reshape(n, 3)
+            n_tris = sum(len(m[0].indices) // 3 for m in meshes)
         d = _abi.DebugDrawDescC()
         d.width, d.height = int(width), int(height)
         for k in range(16):
@@ -352,7 +351,8 @@ class Context:
         for k in range(3):
             d.camera_pos[k], d.light_dir_ws[k] = float(camera_pos[k]), float(light_dir_ws[k])
         lit = np.zeros((max(n_tris, 1), 4), np.float32) if tri_lit else None
-        self._check(self._lib.shs_debug_draw_meshes(self._h, ctypes.byref(d), arr, n, rgba.ctypes.data_as(ctypes.c_void_p),
+        self._check(self._lib.shs_debug_draw_meshes(self._h, ctypes.byref(d), arr.ctypes.data_as(ctypes.POINTER(_abi.DebugMeshC)),
+                                                    n, rgba.ctypes.data_as(ctypes.c_void_p),
                                                     depth.ctypes.data_as(ctypes.c_void_p),
                                                     None if lit is None else lit.ctypes.data_as(ctypes.c_void_p)))
         return (rgba, depth, lit[:n_tris]) if tri_lit else (rgba, depth)
