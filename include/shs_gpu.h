@@ -467,6 +467,43 @@ typedef struct shs_debug_triangle {
 int shs_debug_fill_triangles(shs_ctx *ctx, int32_t width, int32_t height, const shs_debug_triangle *tris,
                              int32_t n_tris, uint8_t *rgba, float *depth);
 
+/* ---- Canvas-API multi-pass extras --------------------------------------------
+ * hello-render-target/ demos, paths relative to cpp-folders/src/hello-render-target/.  Colour buffers are
+ * shs::Canvas pixels (W*H Color), depth the ZBuffer (view z, FLT_MAX = empty) and velocity the
+ * Buffer<glm::vec2>, all indexed y * W + x as the passes index raw().  Host buffers: synchronous;
+ * flags SHS_CANVAS_DEVICE: device buffers, enqueued on the context stream. */
+#define SHS_CANVAS_DEVICE 1u
+#define SHS_CANVAS_MAX_AUTOFOCUS_RADIUS 32
+typedef struct shs_canvas_motion_blur_desc {
+    int32_t width, height;
+    float curr_view[16], curr_proj[16], prev_view[16], prev_proj[16];   /* column-major */
+    int32_t samples;            /* MB_SAMPLES (12) */
+    float strength;             /* MB_STRENGTH (0.85) */
+    float w_obj, w_cam;         /* MB_W_OBJ (1), MB_W_CAM (0.35) */
+    int32_t soft_knee;          /* MB_SOFT_KNEE (1) */
+    float knee_px;              /* MB_KNEE_PIXELS (18) */
+    float max_px;               /* MB_MAX_PIXELS (22) */
+} shs_canvas_motion_blur_desc;
+/* combined_motion_blur_pass (hello_pbr.cpp:1128-1252): src, depth, velocity -> dst. */
+int shs_canvas_motion_blur(shs_ctx *ctx, const shs_canvas_motion_blur_desc *desc, const uint8_t *src, const float *depth,
+                           const float *velocity, uint8_t *dst, uint32_t flags);
+/* gaussian_blur_pass (hello_depth_of_field.cpp:175-251): one 5-tap axis, src -> dst. */
+int shs_canvas_gaussian_blur(shs_ctx *ctx, int32_t width, int32_t height, const uint8_t *src, uint8_t *dst,
+                             int32_t horizontal, uint32_t flags);
+typedef struct shs_canvas_dof_desc {
+    int32_t width, height;
+    int32_t blur_iterations;    /* BLUR_ITERATIONS (3) */
+    int32_t autofocus_radius;   /* AUTOFOCUS_RADIUS (6), at most SHS_CANVAS_MAX_AUTOFOCUS_RADIUS */
+    int32_t focus_x, focus_y;   /* the autofocus centre (CANVAS_WIDTH / 2, CANVAS_HEIGHT / 2) */
+    float range;                /* dof_range (24) */
+    float max_blur;             /* dof_maxblur (0.6) */
+} shs_canvas_dof_desc;
+/* The depth-of-field step of hello_depth_of_field.cpp:786-812: color (ping.color) is the sharp frame
+ * in and the composite out; blur_out (may be NULL) receives the final blur (pong.color); focus_depth
+ * (may be NULL, host) the autofocus depth. */
+int shs_canvas_dof(shs_ctx *ctx, const shs_canvas_dof_desc *desc, uint8_t *color, const float *depth, uint8_t *blur_out,
+                   float *focus_depth, uint32_t flags);
+
 /* Host-only (no device): the byte thresholds for gamma (thr[0] = 0; +inf where a byte is never
  * reached).  Exposed for the parity tests. */
 int shs_tonemap_thresholds(float gamma, float thr[256]);

@@ -319,6 +319,7 @@ void shs_lib_release(shs_ctx *ctx) {
     release(ctx->occ_depth); release(ctx->occ_visible); release(ctx->occ_flags); release(ctx->occ_objs); release(ctx->occ_rects); release(ctx->occ_tris);
     release(ctx->dd_objs); release(ctx->dd_tris); release(ctx->dd_depth0); release(ctx->dd_depth); release(ctx->dd_lit_b);
     release(ctx->dd_rgba); release(ctx->dd_keys); release(ctx->dd_big);
+    release(ctx->cp_a); release(ctx->cp_b); release(ctx->cp_src); release(ctx->cp_depth); release(ctx->cp_vel); release(ctx->cp_focus);
     if (ctx->h_lib_counters) (void)hipHostFree(ctx->h_lib_counters);
     ctx->h_lib_counters = nullptr;
 }

@@ -10,6 +10,7 @@
 #include "../../include/shs_gpu.h"
 #include "shs_device.hpp"
 #include "shs_lib_device.hpp"
+#include "shs_canvas_post_internal.hpp"
 #include "shs_debugdraw_internal.hpp"
 #include "shs_lightbin_internal.hpp"
 #include "shs_occlusion_internal.hpp"
@@ -189,6 +190,10 @@ struct shs_ctx {
     DevBuf<float> dd_depth0, dd_depth, dd_lit_b;
     DevBuf<uint32_t> dd_rgba, dd_big;
     DevBuf<unsigned long long> dd_keys;
+
+    // Canvas-API multi-pass extras (shs_abi_canvas_post.cpp)
+    DevBuf<uint32_t> cp_a, cp_b, cp_src;
+    DevBuf<float> cp_depth, cp_vel, cp_focus;
 };
 
 // Re-enqueues the tonemap after lib_finish re-issued the camera pass (shs_abi_post.cpp).

@@ -376,6 +376,57 @@ class Context:
                                                        depth.ctypes.data_as(ctypes.c_void_p)))
         return rgba, depth
 
+    CANVAS_DEVICE = 1
+
+    def canvas_motion_blur(self, src, depth, velocity, curr_view, curr_proj, prev_view, prev_proj, samples=12,
+                           strength=0.85, w_obj=1.0, w_cam=0.35, soft_knee=True, knee_px=18.0, max_px=22.0, dst=None):
+        """combined_motion_blur_pass (hello_pbr.cpp:1128-1252).  Host arrays: src uint8 [H, W, 4], depth
+        float32 [H, W] (view z), velocity float32 [H, W, 2] -> dst uint8 [H, W, 4].  torch CUDA tensors of
+        the same shapes run on the device (asynchronous on the context stream)."""
+        H, W = src.shape[:2]
+        d = _abi.CanvasMotionBlurDescC()
+        d.width, d.height = W, H
+        for k in range(16):
+            d.curr_view[k], d.curr_proj[k] = float(curr_view[k]), float(curr_proj[k])
+            d.prev_view[k], d.prev_proj[k] = float(prev_view[k]), float(prev_proj[k])
+        d.samples, d.strength, d.w_obj, d.w_cam = int(samples), float(strength), float(w_obj), float(w_cam)
+        d.soft_knee, d.knee_px, d.max_px = 1 if soft_knee else 0, float(knee_px), float(max_px)
+        dev = _is_device(src)
+        if dst is None:
+            dst = _empty_like(src)
+        keep = (_host_c(src, np.uint8), _host_c(depth, np.float32), _host_c(velocity, np.float32), dst)
+        self._check(self._lib.shs_canvas_motion_blur(self._h, ctypes.byref(d), *[_ptr(a) for a in keep],
+                                                     self.CANVAS_DEVICE if dev else 0))
+        return dst
+
+    def canvas_gaussian_blur(self, src, horizontal, dst=None):
+        """gaussian_blur_pass (hello_depth_of_field.cpp:175-251), one axis."""
+        H, W = src.shape[:2]
+        dev = _is_device(src)
+        if dst is None:
+            dst = _empty_like(src)
+        src = _host_c(src, np.uint8)
+        self._check(self._lib.shs_canvas_gaussian_blur(self._h, W, H, _ptr(src), _ptr(dst),
+                                                       1 if horizontal else 0, self.CANVAS_DEVICE if dev else 0))
+        return dst
+
+    def canvas_dof(self, color, depth, iterations=3, radius=6, focus=None, range_=24.0, max_blur=0.6, blur=None):
+        """The DoF step of hello_depth_of_field.cpp:786-812 on color (sharp in, composite out, in place)
+        -> (color, blur, focus_depth)."""
+        H, W = color.shape[:2]
+        d = _abi.CanvasDofDescC()
+        d.width, d.height, d.blur_iterations, d.autofocus_radius = W, H, int(iterations), int(radius)
+        d.focus_x, d.focus_y = (W // 2, H // 2) if focus is None else focus
+        d.range, d.max_blur = float(range_), float(max_blur)
+        dev = _is_device(color)
+        if blur is None:
+            blur = _empty_like(color)
+        f = ctypes.c_float()
+        depth = _host_c(depth, np.float32)
+        self._check(self._lib.shs_canvas_dof(self._h, ctypes.byref(d), _ptr(color), _ptr(depth),
+                                             _ptr(blur), ctypes.byref(f), self.CANVAS_DEVICE if dev else 0))
+        return color, blur, f.value
+
     def lib_device_targets(self):
         """Device pointers of the library targets: (hdr float4 W*H, depth W*H, motion float2 W*H)."""
         a, b, c = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
@@ -589,3 +640,26 @@ class Context:
     @property
     def stream(self):
         return self._lib.shs_get_stream(self._h)
+
+
+def _is_device(a):
+    return hasattr(a, "is_cuda") and a.is_cuda
+
+
+def _empty_like(a):
+    if _is_device(a):
+        import torch
+        return torch.empty_like(a)
+    return np.empty_like(a)
+
+
+def _host_c(a, dtype):
+    return a if _is_device(a) else np.ascontiguousarray(a, dtype=dtype)
+
+
+def _ptr(a):
+    if _is_device(a):
+        assert a.is_contiguous()
+        return ctypes.c_void_p(a.data_ptr())
+    assert a.flags.c_contiguous
+    return a.ctypes.data_as(ctypes.c_void_p)

@@ -158,6 +158,19 @@ class DebugTriangleC(ctypes.Structure):
                 ("rgba", ctypes.c_uint8 * 4)]
 
 
+class CanvasMotionBlurDescC(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("curr_view", _F16), ("curr_proj", _F16),
+                ("prev_view", _F16), ("prev_proj", _F16), ("samples", ctypes.c_int32), ("strength", ctypes.c_float),
+                ("w_obj", ctypes.c_float), ("w_cam", ctypes.c_float), ("soft_knee", ctypes.c_int32),
+                ("knee_px", ctypes.c_float), ("max_px", ctypes.c_float)]
+
+
+class CanvasDofDescC(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("blur_iterations", ctypes.c_int32),
+                ("autofocus_radius", ctypes.c_int32), ("focus_x", ctypes.c_int32), ("focus_y", ctypes.c_int32),
+                ("range", ctypes.c_float), ("max_blur", ctypes.c_float)]
+
+
 class TonemapDescC(ctypes.Structure):
     _fields_ = [("exposure", ctypes.c_float), ("gamma", ctypes.c_float), ("flags", ctypes.c_uint32)]
 LIGHT_CULL_NONE, LIGHT_CULL_TILED, LIGHT_CULL_TILED_DEPTH, LIGHT_CULL_CLUSTERED = 0, 1, 2, 3
@@ -229,6 +242,9 @@ SIGNATURES = [
                                              _P, _P, _P]),
     ("shs_debug_fill_triangles", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(DebugTriangleC),
                                                 ctypes.c_int32, _P, _P]),
+    ("shs_canvas_motion_blur", ctypes.c_int, [_P, ctypes.POINTER(CanvasMotionBlurDescC), _P, _P, _P, _P, ctypes.c_uint32]),
+    ("shs_canvas_gaussian_blur", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_uint32]),
+    ("shs_canvas_dof", ctypes.c_int, [_P, ctypes.POINTER(CanvasDofDescC), _P, _P, _P, _F, ctypes.c_uint32]),
     ("shs_motion_blur", ctypes.c_int, [_P, ctypes.POINTER(MotionBlurDescC)]),
     ("shs_resolve_motion_blur", ctypes.c_int, [_P, _P, _P]),
     ("shs_camera3d", ctypes.c_int, [_F, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F, _F]),

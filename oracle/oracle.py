@@ -626,3 +626,66 @@ def draw_filled_triangles(width, height, screen, z, colors, rgba=None, depth=Non
                                    p[1].ctypes.data, float(z[t, 1]), p[2].ctypes.data, float(z[t, 2]),
                                    colors[t].ctypes.data)
     return rgba, depth
+
+
+# ---- Canvas-API multi-pass extras (shs_oracle_canvas_post.c) ----------------------------------------
+def _cp_ready(L):
+    if not getattr(L, "_cp_ready", False):
+        P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.ora_canvas_motion_blur.restype = None
+        L.ora_canvas_motion_blur.argtypes = [P, P, P, P, I, I, P, P, P, P, I, F, F, F, I, F, F]
+        L.ora_canvas_gaussian.restype = None
+        L.ora_canvas_gaussian.argtypes = [P, P, I, I, I]
+        L.ora_canvas_autofocus.restype = F
+        L.ora_canvas_autofocus.argtypes = [P, I, I, I, I, I]
+        L.ora_canvas_dof.restype = F
+        L.ora_canvas_dof.argtypes = [P, P, P, I, I, I, I, I, I, F, F]
+        L._cp_ready = True
+
+
+def canvas_motion_blur(src, depth, velocity, curr_view, curr_proj, prev_view, prev_proj, samples=12, strength=0.85,
+                       w_obj=1.0, w_cam=0.35, soft_knee=True, knee_px=18.0, max_px=22.0):
+    """combined_motion_blur_pass (hello_pbr.cpp:1128-1252): src uint8 [H, W, 4], depth float32 [H, W],
+    velocity float32 [H, W, 2] -> dst uint8 [H, W, 4]."""
+    L = lib()
+    _cp_ready(L)
+    src = np.ascontiguousarray(src, np.uint8)
+    H, W = src.shape[:2]
+    depth = np.ascontiguousarray(depth, np.float32)
+    velocity = np.ascontiguousarray(velocity, np.float32)
+    dst = np.zeros_like(src)
+    m = [_f32(a, 16) for a in (curr_view, curr_proj, prev_view, prev_proj)]
+    L.ora_canvas_motion_blur(src.ctypes.data, depth.ctypes.data, velocity.ctypes.data, dst.ctypes.data, W, H,
+                             *[a.ctypes.data for a in m], int(samples), float(strength), float(w_obj), float(w_cam),
+                             1 if soft_knee else 0, float(knee_px), float(max_px))
+    return dst
+
+
+def canvas_gaussian(src, horizontal):
+    L = lib()
+    _cp_ready(L)
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros_like(src)
+    L.ora_canvas_gaussian(src.ctypes.data, dst.ctypes.data, src.shape[1], src.shape[0], 1 if horizontal else 0)
+    return dst
+
+
+def canvas_autofocus(depth, cx, cy, radius):
+    L = lib()
+    _cp_ready(L)
+    depth = np.ascontiguousarray(depth, np.float32)
+    return L.ora_canvas_autofocus(depth.ctypes.data, depth.shape[1], depth.shape[0], int(cx), int(cy), int(radius))
+
+
+def canvas_dof(color, depth, iterations=3, radius=6, focus=None, range_=24.0, max_blur=0.6):
+    """The DoF step of hello_depth_of_field.cpp:786-812 -> (composite, blur, focus_depth)."""
+    L = lib()
+    _cp_ready(L)
+    out = np.array(color, np.uint8, copy=True)
+    H, W = out.shape[:2]
+    depth = np.ascontiguousarray(depth, np.float32)
+    blur = np.zeros_like(out)
+    cx, cy = (W // 2, H // 2) if focus is None else focus
+    f = L.ora_canvas_dof(out.ctypes.data, depth.ctypes.data, blur.ctypes.data, W, H, int(iterations), int(radius),
+                         int(cx), int(cy), float(range_), float(max_blur))
+    return out, blur, f

@@ -243,4 +243,15 @@ typedef struct ora_dd_mesh {
 int ora_debug_draw_meshes(const ora_dd_mesh *meshes, int n_meshes, int W, int H, const float *vp, const float *cam,
                           const float *light_dir, uint8_t *rgba, float *depth, float *tri_lit);
 
+/* shs_oracle_canvas_post.c: the Canvas-API multi-pass extras (hello-render-target/hello_pbr.cpp:1051-1252,
+ * hello_depth_of_field.cpp:175-343, 786-812).  Colours 4 bytes per pixel, buffers y * W + x. */
+void ora_canvas_motion_blur(const uint8_t *src, const float *depth, const float *vel, uint8_t *dst, int W, int H,
+                            const float *curr_view, const float *curr_proj, const float *prev_view,
+                            const float *prev_proj, int samples, float strength, float w_obj, float w_cam,
+                            int soft_knee, float knee, float max_px);
+void ora_canvas_gaussian(const uint8_t *src, uint8_t *dst, int W, int H, int horizontal);
+float ora_canvas_autofocus(const float *depth, int W, int H, int cx, int cy, int radius);
+float ora_canvas_dof(uint8_t *color, const float *depth, uint8_t *blur_out, int W, int H, int iterations, int radius,
+                     int cx, int cy, float range, float max_blur);
+
 #endif

@@ -1,0 +1,193 @@
+"""the Canvas-API multi-pass extras of hello-render-target/ on the GPU against the
+oracle restatement (oracle/shs_oracle_canvas_post.c):
+  combined_motion_blur_pass (hello_pbr.cpp:1128-1252) with its camera-velocity reconstruction;
+  gaussian_blur_pass, autofocus_depth_median_center, dof_composite_pass and the DoF step
+  (hello_depth_of_field.cpp:175-343, 786-812).
+Bar: bit-exact bytes (integer taps, the same IEEE float expressions) and the identical focus depth.
+Parity unpinned beyond the analytic cases: the reference ships no fixture and cannot be built here."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+FLT_MAX = np.finfo(np.float32).max
+
+
+def _cam(eye, target, W, H):
+    from shs_gpu.scene_lib import look_at_lh, perspective_lh_no
+    view = look_at_lh(eye, target)
+    proj = perspective_lh_no(np.float32(np.deg2rad(60.0)), np.float32(W) / np.float32(H), np.float32(0.1),
+                             np.float32(1000.0))
+    return view, proj
+
+
+def _inputs(rng, W, H, sky_frac=0.2, vmax=30.0, nan_frac=0.0):
+    src = rng.integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+    # smooth-ish image so the taps matter, plus noise
+    yy, xx = np.mgrid[0:H, 0:W]
+    src[..., 0] = ((xx * 255) // max(W - 1, 1)).astype(np.uint8)
+    depth = rng.uniform(0.5, 80.0, size=(H, W)).astype(np.float32)
+    depth[rng.random((H, W)) < sky_frac] = FLT_MAX
+    vel = rng.normal(0.0, vmax / 3, size=(H, W, 2)).astype(np.float32)
+    vel[rng.random((H, W)) < 0.1] = 0.0
+    if nan_frac:
+        vel[rng.random((H, W)) < nan_frac, 0] = np.nan
+    return src, depth, vel
+
+
+# ---- oracle known-answer tests (CPU) -------------------------------------------------------------
+
+def test_motion_blur_kat_static_sky_copies():
+    """Sky (FLT_MAX) pixels have no camera velocity; with zero object velocity every pixel is copied."""
+    rng = np.random.default_rng(0)
+    W, H = 40, 30
+    src = rng.integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+    depth = np.full((H, W), FLT_MAX, np.float32)
+    vel = np.zeros((H, W, 2), np.float32)
+    view, proj = _cam((0.0, 1.0, -5.0), (0.0, 1.0, 5.0), W, H)
+    out = oracle.canvas_motion_blur(src, depth, vel, view, proj, view, proj)
+    assert np.array_equal(out, src)
+
+
+def test_motion_blur_kat_static_camera_half_pixel_quirk():
+    """With an unmoved camera the reconstructed camera velocity is the reference's own half-pixel
+    offset: curr_screen uses x while prev_screen scales NDC by (W - 1), so v_cam.x = (x + 0.5) / W - 0.5
+    (|v| < 0.001 only near the centre) -- the pass is not the identity for a static frame."""
+    W, H = 64, 48
+    src = np.zeros((H, W, 4), np.uint8)
+    src[..., 0] = (np.arange(W) * 4).astype(np.uint8)[None, :]
+    src[..., 3] = 255
+    depth = np.full((H, W), 10.0, np.float32)
+    vel = np.zeros((H, W, 2), np.float32)
+    view, proj = _cam((0.0, 1.0, -5.0), (0.0, 1.0, 5.0), W, H)
+    out = oracle.canvas_motion_blur(src, depth, vel, view, proj, view, proj)
+    # |v| is at most ~0.5 * 0.35 * 0.85 px: every tap rounds back to the pixel itself or a neighbour
+    assert np.abs(out[..., 0].astype(int) - src[..., 0].astype(int)).max() <= 4
+    assert (out != src).any()
+
+
+def test_gaussian_kat_constant_and_impulse():
+    W, H = 9, 7
+    img = np.full((H, W, 4), 100, np.uint8)
+    out = oracle.canvas_gaussian(img, True)
+    assert np.abs(out.astype(int) - 100).max() <= 1
+    imp = np.zeros((H, W, 4), np.uint8)
+    imp[3, 4] = 200
+    h = oracle.canvas_gaussian(imp, True)
+    assert list(h[3, 2:7, 0]) == [int(np.float32(0.06136) * 200), int(np.float32(0.24477) * 200),
+                                  int(np.float32(0.38774) * 200), int(np.float32(0.24477) * 200),
+                                  int(np.float32(0.06136) * 200)]
+    assert not h[2].any() and not h[4].any()
+
+
+def test_autofocus_kat():
+    d = np.full((20, 20), FLT_MAX, np.float32)
+    assert oracle.canvas_autofocus(d, 10, 10, 3) == 15.0               # no finite sample: 15
+    d[10, 10] = 7.0
+    assert oracle.canvas_autofocus(d, 10, 10, 0) == 7.0
+    d[8:13, 8:13] = np.arange(25, dtype=np.float32).reshape(5, 5)     # 25 samples: the median is 12
+    assert oracle.canvas_autofocus(d, 10, 10, 2) == 12.0
+    assert oracle.canvas_autofocus(d, 10, 10, 6) == 12.0               # the rest of the window is empty
+
+
+def test_dof_kat_in_focus_is_sharp():
+    rng = np.random.default_rng(1)
+    W, H = 30, 20
+    img = rng.integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+    depth = np.full((H, W), 5.0, np.float32)
+    out, blur, f = oracle.canvas_dof(img, depth)
+    assert f == 5.0
+    assert np.array_equal(out[..., :3], img[..., :3]) and np.all(out[..., 3] == 255)
+    # empty depth: d = focus + range, coc 1, t = 0.6 (dof_maxblur)
+    depth[...] = FLT_MAX
+    out, blur, f = oracle.canvas_dof(img, depth)
+    assert f == 15.0
+    t = np.float32(0.6)
+    want = ((np.float32(1) - t) * img[..., :3].astype(np.float32) + t * blur[..., :3].astype(np.float32)).astype(np.int32)
+    assert np.array_equal(out[..., :3], want.astype(np.uint8))
+
+
+# ---- GPU parity ----------------------------------------------------------------------------------
+
+MB_CASES = [
+    # (W, H, samples, soft_knee, cam move, vmax, nan_frac)
+    (1200, 900, 12, True, (0.4, 0.1, 0.3), 30.0, 0.0),     # hello_pbr's canvas and constants
+    (380, 280, 12, False, (0.0, 0.0, 0.0), 10.0, 0.0),
+    (67, 45, 2, True, (1.5, -0.5, 2.0), 60.0, 0.02),
+    (128, 96, 1, True, (0.2, 0.0, 0.0), 20.0, 0.0),         # samples <= 1: copy
+    (97, 61, 32, True, (-2.0, 1.0, -1.0), 5.0, 0.0),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,samples,knee,move,vmax,nan_frac", MB_CASES)
+def test_canvas_motion_blur_bitexact(W, H, samples, knee, move, vmax, nan_frac):
+    import shs_gpu
+    rng = np.random.default_rng(W * 7 + samples)
+    src, depth, vel = _inputs(rng, W, H, vmax=vmax, nan_frac=nan_frac)
+    view, proj = _cam((0.0, 2.0, -6.0), (0.0, 1.0, 10.0), W, H)
+    pview, pproj = _cam((move[0], 2.0 + move[1], -6.0 + move[2]), (0.3, 1.0, 10.0), W, H)
+    want = oracle.canvas_motion_blur(src, depth, vel, view, proj, pview, pproj, samples=samples, soft_knee=knee)
+    ctx = shs_gpu.Context(0)
+    try:
+        got = ctx.canvas_motion_blur(src, depth, vel, view, proj, pview, pproj, samples=samples, soft_knee=knee)
+        bad = np.argwhere((got != want).any(-1))
+        assert bad.size == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
+        assert (got != src).any() or samples <= 1
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,iters,radius,focus", [(380, 280, 3, 6, None), (1200, 900, 3, 6, None),
+                                                    (61, 37, 0, 0, None), (64, 48, 2, 32, (2, 45)),
+                                                    (100, 80, 1, 4, (90, 5))])
+def test_canvas_dof_bitexact(W, H, iters, radius, focus):
+    import shs_gpu
+    rng = np.random.default_rng(W + iters)
+    src, depth, _ = _inputs(rng, W, H, sky_frac=0.3)
+    depth[: H // 3] = rng.uniform(1.0, 4.0, size=(H // 3, W)).astype(np.float32)
+    want_c, want_b, want_f = oracle.canvas_dof(src, depth, iterations=iters, radius=radius, focus=focus)
+    ctx = shs_gpu.Context(0)
+    try:
+        got_c, got_b, got_f = ctx.canvas_dof(src.copy(), depth, iterations=iters, radius=radius, focus=focus)
+        assert np.float32(got_f).view(np.uint32) == np.float32(want_f).view(np.uint32)
+        assert np.array_equal(got_b, want_b)
+        assert np.array_equal(got_c, want_c)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_canvas_passes_device_buffers():
+    """SHS_CANVAS_DEVICE: torch device tensors in and out, enqueued on the context stream; the same
+    bytes as the host-buffer calls."""
+    import torch
+    import shs_gpu
+    W, H = 320, 200
+    rng = np.random.default_rng(3)
+    src, depth, vel = _inputs(rng, W, H)
+    view, proj = _cam((0.0, 2.0, -6.0), (0.0, 1.0, 10.0), W, H)
+    pview, pproj = _cam((0.5, 2.0, -5.5), (0.3, 1.0, 10.0), W, H)
+    ctx = shs_gpu.Context(0)
+    try:
+        host_mb = ctx.canvas_motion_blur(src, depth, vel, view, proj, pview, pproj)
+        host_c, host_b, host_f = ctx.canvas_dof(src.copy(), depth)
+        host_g = ctx.canvas_gaussian_blur(src, False)
+        stream = torch.cuda.Stream()
+        torch.cuda.set_stream(stream)
+        t_src, t_depth, t_vel = (torch.from_numpy(a).cuda() for a in (src, depth, vel))
+        ctx.set_stream(stream.cuda_stream)
+        dev_mb = ctx.canvas_motion_blur(t_src, t_depth, t_vel, view, proj, pview, pproj)
+        dev_g = ctx.canvas_gaussian_blur(t_src, False)
+        t_col = t_src.clone()
+        _, dev_b, dev_f = ctx.canvas_dof(t_col, t_depth)
+        torch.cuda.synchronize()
+        assert np.array_equal(dev_mb.cpu().numpy(), host_mb)
+        assert np.array_equal(dev_g.cpu().numpy(), host_g)
+        assert np.array_equal(t_col.cpu().numpy(), host_c) and np.array_equal(dev_b.cpu().numpy(), host_b)
+        assert dev_f == host_f
+        assert np.array_equal(oracle.canvas_gaussian(src, False), host_g)
+    finally:
+        torch.cuda.set_stream(torch.cuda.default_stream())
+        ctx.close()
