@@ -276,7 +276,33 @@ SIGNATURES = [
 ]
 
 
+def _share_torch_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm wheels bundle their own libamdhip64.so /
+    libhsa-runtime64.so and load them by file name from torch/lib; libshs_gpu.so asks the dynamic
+    linker for the SONAMEs libamdhip64.so.7 / libhsa-runtime64.so.1.  If libshs_gpu.so is loaded first,
+    the system ROCm runtime comes up, and a later `import torch` maps a second HIP + HSA runtime into
+    the process whose device enumeration then fails ("No HIP GPUs are available" / hipErrorNoDevice:
+    tools/diag_runtime.py).  Loading torch's runtime first (by path, RTLD_GLOBAL,
+    without importing torch) makes libshs_gpu.so bind to it by SONAME, and torch later finds the same
+    file already mapped.  Without torch the system runtime is used.  SHS_GPU_HIP_RUNTIME=system skips."""
+    if os.environ.get("SHS_GPU_HIP_RUNTIME", "") == "system":
+        return None
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    for d in spec.submodule_search_locations:
+        hip = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(hip):
+            return ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+    return None
+
+
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    _share_torch_hip_runtime()
     if not os.path.exists(path):
         raise RuntimeError(
             f"libshs_gpu.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

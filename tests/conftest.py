@@ -14,20 +14,6 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run with -m gpu on the MI355X box)")
 
 
-@pytest.fixture(scope="session", autouse=True)
-def _torch_hip_first():
-    """Initialise PyTorch's HIP state before any libshs_gpu context exists: on this image a process
-    that has created many shs contexts (streams + buffers) can no longer bring up torch.cuda
-    (hipGetDeviceCount -> hipErrorNoDevice), while the reverse order works.
-    The device gather tests use torch tensors; without a GPU this is a no-op."""
-    try:
-        import torch
-    except ImportError:
-        return
-    if torch.cuda.is_available():
-        torch.cuda.init()
-
-
 @pytest.fixture(scope="session")
 def oracle_mod():
     from oracle import oracle

@@ -119,7 +119,7 @@ def test_tonemap_synthetic_hdr_exact(oracle_mod):
 
 def _memcpy_d2d(dst, src, nbytes):
     import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
+    hip = ctypes.CDLL("libamdhip64.so.7")   # by SONAME: the runtime already mapped (shs_gpu._abi.load)
     hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     rc = hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 3)   # hipMemcpyDeviceToDevice
     assert rc == 0, rc
