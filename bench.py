@@ -27,11 +27,14 @@ import csv
 import glob
 import json
 import os
+import platform
 import shutil
 import subprocess
 import sys
 import tempfile
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "leisure-software-renderer_amd")
@@ -146,8 +149,69 @@ def run_gpu(args, rank, local_rank, world, dist):
         ctx.enable_timing(False)
         single = {"ms_per_frame": round(el1 / n1 * 1e3, 5), "steps": n1,
                   "kernels_ms": {k: round(v, 5) for k, v in k1.items()}}
+    if F > 1 and world == 1 and not args.child and not args.no_pcie:
+        single = single or {}
+        pcie = seam1_pcie(args, ctx, frame, sets)
+        ctx.close()
+        return frame, sets[0][0], stats, elapsed, n_launches, kms, single, pcie
     ctx.close()
-    return frame, sets[0][0], stats, elapsed, n_launches, kms, single
+    return frame, sets[0][0], stats, elapsed, n_launches, kms, single, None
+
+
+def seam1_pcie(args, ctx, frame, sets):
+    """The end-to-end Seam-1 figure: every frame crosses PCIe into pinned host memory as the SDL
+    surface it is presented from (SHS_FRAME_PRESENT staging, 4 B/px, what copy_to_SDLSurface produces),
+    D2H overlapped with rendering: two contexts alternate batches, each batch's D2H queued behind its
+    render on that context's stream, so one context's copy runs under the other's render."""
+    import ctypes
+    import dataclasses
+    import shs_gpu
+    import torch
+    F = args.frames_per_step
+    hip = ctypes.CDLL("libamdhip64.so.7")   # the runtime already mapped (shs_gpu._abi.load)
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    pf = dataclasses.replace(frame, present=True)
+    nbytes = F * pf.width * pf.height * 4
+    ctxs = [ctx, shs_gpu.Context(0)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    hosts = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    prepared = []
+    for c, st in zip(ctxs, streams):
+        c.set_stream(st.cuda_stream)
+        prepared.append([c.prepare_batch(pf, fds) for fds in sets])
+
+    def step(i):
+        c = i % 2
+        ctxs[c].render_batch_prepared(prepared[c][(i // 2) % POSE_SETS])
+        rc = hip.hipMemcpyAsync(ctypes.c_void_p(hosts[c].data_ptr()), ctypes.c_void_p(ctxs[c].present_device(0)),
+                                nbytes, 2, ctypes.c_void_p(streams[c].cuda_stream))
+        assert rc == 0, rc
+    for i in range(4):
+        step(i)
+    torch.cuda.synchronize()
+    n = max(8, min(args.steps, 40))
+    t0 = time.perf_counter()
+    for i in range(n):
+        step(i)
+    for c in ctxs:
+        c.synchronize()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # the same copies alone: the PCIe ceiling of this figure
+    t1 = time.perf_counter()
+    for i in range(n):
+        hip.hipMemcpyAsync(ctypes.c_void_p(hosts[i % 2].data_ptr()), ctypes.c_void_p(ctxs[i % 2].present_device(0)),
+                           nbytes, 2, ctypes.c_void_p(streams[i % 2].cuda_stream))
+    torch.cuda.synchronize()
+    el_copy = time.perf_counter() - t1
+    ctxs[1].close()
+    ctx.set_stream(0)
+    n_tri = sum(d.mesh.n_tris for d in sets[0][0])
+    return {"frames": n * F, "ms_per_frame": round(el / (n * F) * 1e3, 5),
+            "mtri_s": round(n_tri * n * F / el / 1e6, 3), "d2h_gb_s": round(n * nbytes / el / 1e9, 2),
+            "d2h_only_gb_s": round(n * nbytes / el_copy / 1e9, 2), "bytes_per_frame": pf.width * pf.height * 4,
+            "what": "render + D2H of every frame's RGBA8 SDL staging into pinned host memory, two contexts "
+                    "alternating batches (D2H under the other context's render); PCIe-bound"}
 
 
 def lib_workload(args, rank=0):
@@ -328,64 +392,116 @@ def collect_pmc(args):
     return {"fetch_kib": out["FETCH_SIZE"], "write_kib": out["WRITE_SIZE"], "bytes": traffic}, None
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def hw_threads():
+    """std::thread::hardware_concurrency() (the reference's worker count, SURVEY 8d) and the cores this
+    process may run on (its affinity set)."""
+    hc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = hc
+    return hc, usable
+
+
+def _timed_frames(fn, seconds, max_frames=100000):
+    """Run fn() until `seconds` of wall time (at least 2 frames): -> (frames, elapsed s, median ms)."""
+    w0 = time.perf_counter()
+    while time.perf_counter() - w0 < min(0.5, 0.1 * seconds):   # warm: thread pools, page faults
+        fn()
+    times = []
+    t0 = time.perf_counter()
+    while True:
+        a = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - a)
+        el = time.perf_counter() - t0
+        if (el >= seconds and len(times) >= 2) or len(times) >= max_frames:
+            break
+    return len(times), el, 1e3 * float(np.median(times))
+
+
 def cpu_baseline_lib(args):
-    """The library-path oracle (PassShadowMap + PassPBRForward restated, sequential like the
-    reference's pass loop for these triangle sizes) on one host core, bounded sample."""
+    """The library-path oracle (PassShadowMap + PassPBRForward restated) on the box's host.  C5 uses the
+    reference's row-parallel split of big bboxes (rasterizer.hpp:424-436) on hardware_concurrency
+    threads; C4's 1M small triangles never reach that split's 128x128-pixel threshold, so the reference
+    rasterises them on one thread and so does the baseline."""
     from oracle import oracle
     from shs_gpu import scene_lib
+    hc, usable = hw_threads()
     if args.config == "c4":
         frame, draws, lights, cull = lib_workload(args, 0)
         n_tri = sum(d.mesh.n_tris for d in draws)
-        frames = 0
-        t0 = time.perf_counter()
-        while True:
+
+        def one():
             lists = oracle.light_cull(cull, lights)
-            oracle.forward_plus(frame, draws, lights, cull, lists[:2])
-            frames += 1
-            el = time.perf_counter() - t0
-            if el >= args.cpu_seconds:
-                break
+            return oracle.forward_plus(frame, draws, lights, cull, lists[:2])
+        frames, el, med = _timed_frames(one, args.cpu_seconds, 1000)
         return {"value": round(n_tri * frames / el / 1e6, 5), "unit": "Mtri/s", "cores": 1, "kind": "port",
+                "median_ms_per_frame": round(med, 2), "cpu_model": cpu_model(),
+                "hardware_concurrency": hc, "usable_cores": usable,
                 "sample": f"{frames} full frame(s) of the same workload (light cull + Forward+ pass, "
                           f"{frame.width}x{frame.height}, {n_tri} tris, {len(lights)} lights), {el:.1f} s wall, "
-                          "1 thread (oracle/shs_oracle_lib.c + shs_oracle_light.c, gcc -O3)"}
+                          "1 thread: no bbox reaches rasterize_mesh's row-parallel threshold "
+                          "(oracle/shs_oracle_lib.c + shs_oracle_light.c, gcc -O3)"}
     frame, draws, casters, sun, S = lib_workload(args, 0)
     n_tri = sum(d.mesh.n_tris for d in draws)
-    frames = 0
-    t0 = time.perf_counter()
-    while True:
+
+    def one():
         sm, lvp = oracle.shadow_map(S, sun, casters)
         scene_lib.wire_shadow(draws, lvp)
-        oracle.pbr_forward(frame, draws, sm)
-        frames += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
-    return {"value": round(n_tri * frames / el / 1e6, 5), "unit": "Mtri/s", "cores": 1, "kind": "port",
+        return oracle.pbr_forward(frame, draws, sm)
+    oracle.set_lib_threads(hc)
+    try:
+        frames, el, med = _timed_frames(one, args.cpu_seconds, 1000)
+    finally:
+        oracle.set_lib_threads(1)
+    return {"value": round(n_tri * frames / el / 1e6, 5), "unit": "Mtri/s", "cores": hc, "kind": "port",
+            "median_ms_per_frame": round(med, 2), "cpu_model": cpu_model(), "hardware_concurrency": hc,
+            "usable_cores": usable,
             "sample": f"{frames} frames of the same workload (shadow {S}^2 + {frame.width}x{frame.height} PBR, "
-                      f"{n_tri} tris), {el:.1f} s wall, 1 thread (oracle/shs_oracle_lib.c, gcc -O3)"}
+                      f"{n_tri} tris), {el:.1f} s wall, big bboxes row-parallel on {hc} threads as "
+                      "rasterize_mesh's job-system split does (oracle/shs_oracle_lib.c, gcc -O3)"}
 
 
 def cpu_baseline(args):
-    """The oracle (CPU restatement of the reference tile-job path) on this host, bounded sample."""
+    """The oracle (CPU restatement of the reference tile-job path) on this host, bounded samples:
+    hardware_concurrency workers (the headline), THREAD_COUNT=20 (the reference default,
+    blinn_phong_shading.cpp:28) and the cores this process may use; C1 single-threaded."""
     if args.config in LIB_CONFIGS:
         return cpu_baseline_lib(args)
     from oracle import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    hc, usable = hw_threads()
     frame, draws = build_workload(args.config, 0)
     n_tri = sum(d.mesh.n_tris for d in draws)
-    oracle.render_legacy(frame.width, frame.height, draws, threads=threads)  # warm
-    frames = 0
-    t0 = time.perf_counter()
-    while True:
-        oracle.render_legacy(frame.width, frame.height, draws, threads=threads)
-        frames += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or frames >= 100000:
-            break
-    return {"value": round(n_tri * frames / el / 1e6, 4), "unit": "Mtri/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} frames of the same workload ({frame.width}x{frame.height}, {n_tri} tris), "
-                      f"{el:.1f} s wall, 80x80 tile jobs on {threads} threads (oracle/shs_oracle.c, gcc -O3)"}
+    _, depth, _ = oracle.render_legacy(frame.width, frame.height, draws, threads=1)
+    covered = int((depth.view(np.uint32) != np.float32(np.finfo(np.float32).max).view(np.uint32)).sum())
+    legs = [("single_thread", 1)] if args.config == "c1" else [("hardware_concurrency", hc), ("thread_count_20", 20),
+                                                                ("usable_cores", usable)]
+    out = {}
+    for name, threads in legs:
+        frames, el, med = _timed_frames(
+            lambda: oracle.render_legacy(frame.width, frame.height, draws, threads=threads), args.cpu_seconds / len(legs))
+        out[name] = {"threads": threads, "frames": frames, "seconds": round(el, 2), "median_ms_per_frame": round(med, 3),
+                     "mtri_s": round(n_tri * frames / el / 1e6, 4), "mpix_s": round(covered * frames / el / 1e6, 3)}
+    head_name = legs[0][0]
+    head = out[head_name]
+    return {"value": head["mtri_s"], "unit": "Mtri/s", "cores": head["threads"], "kind": "port",
+            "median_ms_per_frame": head["median_ms_per_frame"], "mpix_s": head["mpix_s"], "cpu_model": cpu_model(),
+            "hardware_concurrency": hc, "usable_cores": usable, "legs": out,
+            "sample": f"{head['frames']} frames of the same workload ({frame.width}x{frame.height}, {n_tri} tris, "
+                      f"{covered} covered px) in {head['seconds']} s, 80x80 tile jobs on {head['threads']} threads "
+                      f"({head_name}; oracle/shs_oracle.c, gcc -O3)"}
 
 
 def main():
@@ -400,6 +516,7 @@ def main():
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-frame latency leg (profiling)")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive Seam-1 leg")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--debug-flags", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
     ap.add_argument("--raster-mode", type=int, default=0, help="legacy path: 0 auto, 1 scan, 2 bins")
@@ -430,7 +547,7 @@ def main():
 
     if args.config in LIB_CONFIGS:
         return main_lib(args, world, rank, local_rank, dist, pmc, pmc_err)
-    frame, draws, stats, elapsed, n_launches, kms, single = run_gpu(args, rank, local_rank, world, dist)
+    frame, draws, stats, elapsed, n_launches, kms, single, pcie = run_gpu(args, rank, local_rank, world, dist)
     B1, n_tri1 = algorithmic_bytes(frame, draws)
     F = args.frames_per_step
     B, n_tri = B1 * F, n_tri1 * F          # per step (= per k_raster launch)
@@ -504,8 +621,10 @@ def main():
         "timed_launches_with_events": n_launches,
         "roofline": roofline,
     }
-    if single is not None:
+    if single:
         line["single_frame"] = single
+    if pcie is not None:
+        line["seam1_pcie"] = pcie
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(line), flush=True)

@@ -184,6 +184,13 @@ class Context:
                                           depth.ctypes.data_as(ctypes.c_void_p)))
         return color, depth
 
+    def present_device(self, index: int = 0) -> int:
+        """Device address of frame `index`'s SDL staging (SHS_FRAME_PRESENT); a batch's frames are
+        contiguous, W * H * 4 bytes apart."""
+        p = ctypes.c_void_p()
+        self._check(self._lib.shs_present_device(self._h, int(index), ctypes.byref(p)))
+        return p.value
+
     def resolve_present(self, index: int = 0, pitch: int = 0):
         """The SDL staging of frame `index` (Canvas::copy_to_SDLSurface): uint8 [H, W, 4], rows top-down.
         pitch > W*4 pads rows as an SDL surface would (returned array [H, pitch] bytes)."""

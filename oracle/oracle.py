@@ -689,3 +689,11 @@ def canvas_dof(color, depth, iterations=3, radius=6, focus=None, range_=24.0, ma
     f = L.ora_canvas_dof(out.ctypes.data, depth.ctypes.data, blur.ctypes.data, W, H, int(iterations), int(radius),
                          int(cx), int(cy), float(range_), float(max_blur))
     return out, blur, f
+
+
+def set_lib_threads(n):
+    """rasterize_mesh's row-parallel split of big bboxes (rasterizer.hpp:424-436) on n host threads."""
+    L = _lib_lib()
+    L.ora_set_lib_threads.restype = None
+    L.ora_set_lib_threads.argtypes = [ctypes.c_int]
+    L.ora_set_lib_threads(int(n))

@@ -152,6 +152,8 @@ typedef struct ora_shadow_caster {   /* RenderItem with casts_shadow (scene/scen
 void ora_rasterize_mesh(const ora_lib_target *t, const ora_lib_draw *d, uint64_t *stats3);
 /* PassPBRForward::execute (passes/pass_pbr_forward.hpp:49-214): clears + one rasterize_mesh per draw */
 int ora_pbr_forward(const ora_lib_target *t, const ora_lib_draw *draws, int n_draws, uint64_t *stats3);
+/* Threads for rasterize_mesh's row-parallel split of big bboxes (rasterizer.hpp:424-436; default 1). */
+void ora_set_lib_threads(int n);
 /* PassShadowMap::execute (passes/pass_shadow_map.hpp:44-206) into sm[SW*SH]; returns the light viewproj */
 int ora_shadow_map(int SW, int SH, const float *sun_dir3, const ora_shadow_caster *casters, int n_casters, float *sm,
                    float *light_viewproj_out);

@@ -412,8 +412,114 @@ static void read_vertex(const ora_mesh *m, uint32_t idx, v3 *p, v3 *n, v2 *uv) {
 
 static int64_t mesh_tris(const ora_mesh *m) { return m->indices ? m->n_indices / 3 : m->n_verts / 3; }
 
-/* rasterize_mesh (rasterizer.hpp:181-442), sequential (the reference's row-parallel split writes
- * disjoint rows, so its result equals this order). */
+/* One triangle's pixel loop (rasterizer.hpp:336-420) over rows [y0, y1): the unit the reference's
+ * row-parallel split (parallel_for_1d over bbox rows, :424-436) hands to its job system. */
+typedef struct row_job {
+    const ora_lib_target *t;
+    const ora_lib_draw *u;
+    v2 s[3];
+    float iw[3], zw[3];
+    v4 varw[3][3];
+    float c2p[16];
+    int minx, maxx, miny, maxy, W, H, depth_motion, write_motion;
+    int next_chunk, n_chunks, grain;
+    pthread_mutex_t lock;
+} row_job;
+
+static void raster_rows(row_job *j, int y0, int y1) {
+    for (int y = y0; y < y1; ++y)
+        for (int x = j->minx; x <= j->maxx; ++x) {
+            const v2 p = {(float)x + 0.5f, (float)y + 0.5f};
+            const v3 bc = barycentric_2d(p, j->s[0], j->s[1], j->s[2]);
+            if (bc.x < 0.0f || bc.y < 0.0f || bc.z < 0.0f) continue;
+            const float denom = (bc.x * j->iw[0] + bc.y * j->iw[1]) + bc.z * j->iw[2];
+            if (denom <= 1e-10f) continue;
+            const float inv_denom = 1.0f / denom;
+            const float z_clip = (bc.x * j->zw[0] + bc.y * j->zw[1]) + bc.z * j->zw[2];
+            const float z_ndc = z_clip * inv_denom;
+            float z01 = g_clamp(z_ndc * 0.5f + 0.5f, 0.0f, 1.0f);
+            const size_t o = (size_t)y * j->W + x;
+            if (j->depth_motion) {
+                const float view_z = 1.0f / denom;
+                if (j->t->zf > j->t->zn + 1e-6f) z01 = g_clamp((view_z - j->t->zn) / (j->t->zf - j->t->zn), 0.0f, 1.0f);
+                if (z01 >= j->t->depth[o]) continue;
+                j->t->depth[o] = z01;
+            }
+            float fv[3][4];
+            for (int q = 0; q < 3; ++q) {
+                fv[q][0] = ((bc.x * j->varw[0][q].x + bc.y * j->varw[1][q].x) + bc.z * j->varw[2][q].x) * inv_denom;
+                fv[q][1] = ((bc.x * j->varw[0][q].y + bc.y * j->varw[1][q].y) + bc.z * j->varw[2][q].y) * inv_denom;
+                fv[q][2] = ((bc.x * j->varw[0][q].z + bc.y * j->varw[1][q].z) + bc.z * j->varw[2][q].z) * inv_denom;
+            }
+            frag_in fin;
+            fin.world_pos = V3(fv[0][0], fv[0][1], fv[0][2]);           /* the WorldPos varying wins (:375-378) */
+            fin.normal_ws = normalize3(V3(fv[1][0], fv[1][1], fv[1][2])); /* NormalWS (:379-382) */
+            fin.uv.x = fv[2][0]; fin.uv.y = fv[2][1];                    /* UV0 (:383-387) */
+            if (j->write_motion) {                                          /* :388-411 */
+                const v4 cw = {fin.world_pos.x, fin.world_pos.y, fin.world_pos.z, 1.0f};
+                const v4 pw = m4v4(j->c2p, cw);
+                const v4 cc = m4v4(j->u->viewproj, cw);
+                const v4 pc = m4v4(j->u->prev_viewproj, pw);
+                float mx = 0.0f, my = 0.0f;
+                if (fabsf(cc.w) > 1e-8f && fabsf(pc.w) > 1e-8f) {
+                    const float cnx = cc.x / cc.w, cny = cc.y / cc.w, pnx = pc.x / pc.w, pny = pc.y / pc.w;
+                    float vx = ((cnx - pnx) * 0.5f) * (float)j->W, vy = ((cny - pny) * 0.5f) * (float)j->H;
+                    const float len = sqrtf(vx * vx + vy * vy);
+                    if (len > 96.0f && len > 1e-6f) {
+                        const float sc = 96.0f / len;
+                        vx *= sc; vy *= sc;
+                    }
+                    mx = vx; my = vy;
+                }
+                j->t->motion[2 * o] = mx; j->t->motion[2 * o + 1] = my;
+            }
+            fin.depth01 = z01;
+            fin.px = x;
+            fin.py = y;
+            const v4 c = fragment(j->t, j->u, &fin);
+            j->t->hdr[4 * o] = c.x; j->t->hdr[4 * o + 1] = c.y; j->t->hdr[4 * o + 2] = c.z; j->t->hdr[4 * o + 3] = c.w;
+        }
+}
+
+static int g_lib_threads = 1;   /* 1: sequential (the reference without a job system) */
+
+void ora_set_lib_threads(int n) { g_lib_threads = n < 1 ? 1 : n; }
+
+static void *row_worker(void *arg) {
+    row_job *j = (row_job *)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->lock);
+        const int c = j->next_chunk++;
+        pthread_mutex_unlock(&j->lock);
+        if (c >= j->n_chunks) return NULL;
+        const int y0 = j->miny + c * j->grain;
+        const int y1 = y0 + j->grain < j->maxy + 1 ? y0 + j->grain : j->maxy + 1;
+        raster_rows(j, y0, y1);
+    }
+}
+
+/* RasterizerConfig defaults (rasterizer.hpp:37-39): parallel_min_rows 8, parallel_min_pixels 128*128.
+ * Rows are disjoint, so the result equals the sequential loop's. */
+static void raster_triangle(row_job *j) {
+    const int rows = j->maxy - j->miny + 1, pixels = (j->maxx - j->minx + 1) * rows;
+    if (g_lib_threads <= 1 || rows < 8 || pixels < 128 * 128) {
+        raster_rows(j, j->miny, j->maxy + 1);
+        return;
+    }
+    j->grain = 8;
+    j->n_chunks = (rows + j->grain - 1) / j->grain;
+    j->next_chunk = 0;
+    pthread_mutex_init(&j->lock, NULL);
+    pthread_t th[64];
+    const int n = g_lib_threads < 64 ? g_lib_threads : 64;
+    for (int i = 1; i < n; ++i) pthread_create(&th[i], NULL, row_worker, j);
+    row_worker(j);
+    for (int i = 1; i < n; ++i) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&j->lock);
+}
+
+/* rasterize_mesh (rasterizer.hpp:181-442); big bboxes row-parallel on g_lib_threads threads as the
+ * reference's job system splits them (disjoint rows: the result equals the sequential order). */
 void ora_rasterize_mesh(const ora_lib_target *t, const ora_lib_draw *u, uint64_t *stats3) {
     const int W = t->W, H = t->H;
     const ora_mesh *m = &u->mesh;
@@ -492,58 +598,16 @@ void ora_rasterize_mesh(const ora_lib_target *t, const ora_lib_draw *u, uint64_t
                     varw[j][q].z = r[j]->var[q].z * iw[j]; varw[j][q].w = r[j]->var[q].w * iw[j];
                 }
             }
-            for (int y = miny; y <= maxy; ++y)
-                for (int x = minx; x <= maxx; ++x) {
-                    const v2 p = {(float)x + 0.5f, (float)y + 0.5f};
-                    const v3 bc = barycentric_2d(p, s[0], s[1], s[2]);
-                    if (bc.x < 0.0f || bc.y < 0.0f || bc.z < 0.0f) continue;
-                    const float denom = (bc.x * iw[0] + bc.y * iw[1]) + bc.z * iw[2];
-                    if (denom <= 1e-10f) continue;
-                    const float inv_denom = 1.0f / denom;
-                    const float z_clip = (bc.x * zw[0] + bc.y * zw[1]) + bc.z * zw[2];
-                    const float z_ndc = z_clip * inv_denom;
-                    float z01 = g_clamp(z_ndc * 0.5f + 0.5f, 0.0f, 1.0f);
-                    const size_t o = (size_t)y * W + x;
-                    if (depth_motion) {
-                        const float view_z = 1.0f / denom;
-                        if (t->zf > t->zn + 1e-6f) z01 = g_clamp((view_z - t->zn) / (t->zf - t->zn), 0.0f, 1.0f);
-                        if (z01 >= t->depth[o]) continue;
-                        t->depth[o] = z01;
-                    }
-                    float fv[3][4];
-                    for (int q = 0; q < 3; ++q) {
-                        fv[q][0] = ((bc.x * varw[0][q].x + bc.y * varw[1][q].x) + bc.z * varw[2][q].x) * inv_denom;
-                        fv[q][1] = ((bc.x * varw[0][q].y + bc.y * varw[1][q].y) + bc.z * varw[2][q].y) * inv_denom;
-                        fv[q][2] = ((bc.x * varw[0][q].z + bc.y * varw[1][q].z) + bc.z * varw[2][q].z) * inv_denom;
-                    }
-                    frag_in fin;
-                    fin.world_pos = V3(fv[0][0], fv[0][1], fv[0][2]);           /* the WorldPos varying wins (:375-378) */
-                    fin.normal_ws = normalize3(V3(fv[1][0], fv[1][1], fv[1][2])); /* NormalWS (:379-382) */
-                    fin.uv.x = fv[2][0]; fin.uv.y = fv[2][1];                    /* UV0 (:383-387) */
-                    if (write_motion) {                                          /* :388-411 */
-                        const v4 cw = {fin.world_pos.x, fin.world_pos.y, fin.world_pos.z, 1.0f};
-                        const v4 pw = m4v4(c2p, cw);
-                        const v4 cc = m4v4(u->viewproj, cw);
-                        const v4 pc = m4v4(u->prev_viewproj, pw);
-                        float mx = 0.0f, my = 0.0f;
-                        if (fabsf(cc.w) > 1e-8f && fabsf(pc.w) > 1e-8f) {
-                            const float cnx = cc.x / cc.w, cny = cc.y / cc.w, pnx = pc.x / pc.w, pny = pc.y / pc.w;
-                            float vx = ((cnx - pnx) * 0.5f) * (float)W, vy = ((cny - pny) * 0.5f) * (float)H;
-                            const float len = sqrtf(vx * vx + vy * vy);
-                            if (len > 96.0f && len > 1e-6f) {
-                                const float sc = 96.0f / len;
-                                vx *= sc; vy *= sc;
-                            }
-                            mx = vx; my = vy;
-                        }
-                        t->motion[2 * o] = mx; t->motion[2 * o + 1] = my;
-                    }
-                    fin.depth01 = z01;
-                    fin.px = x;
-                    fin.py = y;
-                    const v4 c = fragment(t, u, &fin);
-                    t->hdr[4 * o] = c.x; t->hdr[4 * o + 1] = c.y; t->hdr[4 * o + 2] = c.z; t->hdr[4 * o + 3] = c.w;
-                }
+            row_job job;
+            job.t = t; job.u = u; job.W = W; job.H = H;
+            job.depth_motion = depth_motion; job.write_motion = write_motion;
+            memcpy(job.s, s, sizeof job.s);
+            memcpy(job.iw, iw, sizeof job.iw);
+            memcpy(job.zw, zw, sizeof job.zw);
+            memcpy(job.varw, varw, sizeof job.varw);
+            if (write_motion) memcpy(job.c2p, c2p, sizeof job.c2p);
+            job.minx = minx; job.maxx = maxx; job.miny = miny; job.maxy = maxy;
+            raster_triangle(&job);
         }
     }
 }

@@ -172,3 +172,22 @@ def test_lib_golden_fixture(oracle_mod):
     # shaded floats: pinned to 1e-5 (libm powf may differ by an ulp across hosts)
     for (y, x), v in zip(g["probe_px"], g["probe_hdr"]):
         assert np.allclose(hdr[y, x], v, rtol=1e-5, atol=1e-5)
+
+
+def test_row_parallel_split_matches_sequential():
+    """The oracle's row-parallel split of big bboxes (the reference's parallel_for_1d over rows,
+    rasterizer.hpp:424-436) leaves the same targets as the sequential loop."""
+    from oracle import oracle
+    from shs_gpu import scene_lib
+    frame, draws, casters, sun, S = scene_lib.c5_scene(640, 360, floor_seg=1)   # 2 floor triangles: big bboxes
+    sm, lvp = oracle.shadow_map(256, sun, casters)
+    scene_lib.wire_shadow(draws, lvp)
+    a = oracle.pbr_forward(frame, draws, sm)
+    try:
+        oracle.set_lib_threads(6)
+        b = oracle.pbr_forward(frame, draws, sm)
+    finally:
+        oracle.set_lib_threads(1)
+    for x, y in zip(a, b):
+        if isinstance(x, np.ndarray):
+            assert np.array_equal(x.view(np.uint8), y.view(np.uint8))
