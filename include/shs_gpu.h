@@ -254,6 +254,8 @@ typedef struct shs_lib_stats {
     uint64_t spilled;
     uint64_t clipped_extra;       /* fan triangles beyond the first of clipped input triangles */
 } shs_lib_stats;
+/* A tile-sharded pass (shard_count > 1) skips the clipping of triangles whose fans cannot reach its
+ * tiles: its tri_after_clip / tri_raster / clipped_extra leave those out. */
 
 /* PassPBRForward::execute: clear (gradient / clear_hdr, depth 1, motion 0) and one rasterize_mesh per
  * draw, in order, asynchronously on the context stream. */

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -50,7 +51,7 @@ void release_work(Work &w) {
             if (e) { (void)hipEventDestroy(e); e = nullptr; }
     release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase); release(w.zord);
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.dbase); release(w.rqueue);
     for (int i = 0; i < 2; ++i) {
         if (w.h_draws[i]) (void)hipHostFree(w.h_draws[i]);
         if (w.slot_ev[i]) (void)hipEventDestroy(w.slot_ev[i]);
@@ -149,7 +150,13 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (w.extra_cap == 0) w.extra_cap = (uint32_t)std::max(4096, n_tris / 4);
     const size_t n_slots = (size_t)std::max(n_tris, 1) + (shadow ? 0 : w.extra_cap);
     if (ensure(ctx, w.recs, n_slots) || ensure(ctx, w.boxes, n_slots) || ensure(ctx, w.zord, n_slots)) return SHS_ERR_HIP;
-    if (!shadow && (ensure(ctx, w.shade, n_slots) || ensure(ctx, w.xbase, (size_t)std::max(n_tris, 1)))) return SHS_ERR_HIP;
+    if (!shadow && (ensure(ctx, w.shade, n_slots) || ensure(ctx, w.xbase, (size_t)std::max(n_tris, 1)) ||
+                    ensure(ctx, w.clipq, (size_t)std::max(n_tris, 1))))
+        return SHS_ERR_HIP;
+    // every slot enters the large-primitive queue at most once
+    if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots + 1 + 256) ||
+        ensure(ctx, w.dbase, std::max<size_t>(w.last_draws.size(), 1)))
+        return SHS_ERR_HIP;
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count;
     bool reset = gkey != w.geom_key;
     if (w.tile_count.cap < 2 * (size_t)n_tiles || !w.tile_count.p) {
@@ -161,13 +168,15 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         reset = true;
     }
     if (!w.counters.p) {
-        if (ensure(ctx, w.counters, 2 * shs_dev::LC_N)) return SHS_ERR_HIP;
+        if (ensure(ctx, w.counters, 2 * shs_dev::LC_N) || ensure(ctx, w.rqueue, 2 * shs_dev::LIB_NQ * shs_dev::LIB_QSTRIDE))
+            return SHS_ERR_HIP;
         reset = true;
     }
     if (reset) {
         HIP_TRY(ctx, hipMemsetAsync(w.tile_count.p, 0, w.tile_count.cap * sizeof(uint32_t), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(w.busy.p, 0, w.busy.cap * sizeof(uint32_t), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(w.counters.p, 0, w.counters.cap * sizeof(uint32_t), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(w.rqueue.p, 0, w.rqueue.cap * sizeof(uint32_t), ctx->stream));
         w.geom_key = gkey;
     }
     if (ensure(ctx, w.bins, (size_t)n_tiles * w.bin_cap)) return SHS_ERR_HIP;
@@ -186,6 +195,10 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     // scan mode (every busy tile tests every primitive's box) for small passes, per-tile bins above
     fp.scan_mode = n_tris <= SCAN_MAX_PRIMS ? 1u : 0u;
     fp.setup_blocks = setup_blocks;
+    {
+        const char *e = std::getenv("SHS_LIB_EXP");   // timing experiments only: parts of the setup skipped
+        fp.exp_flags = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+    }
     const int owned_bt = (n_tiles - fp.rank + fp.count - 1) / fp.count;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / 8);
     int &resident = ctx->lib_resident[shadow ? 1 : 0];
@@ -198,6 +211,9 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.draws = w.draws.p; fb.recs = w.recs.p; fb.shade = w.shade.p; fb.boxes = w.boxes.p; fb.xbase = w.xbase.p; fb.zord = w.zord.p;
     fb.tile_count = w.tile_count.p; fb.bins = w.bins.p; fb.spill = w.spill.p; fb.counters = w.counters.p;
     fb.busy = w.busy.p; fb.blk_stat = w.blk_stat.p; fb.rstat = w.rstat.p;
+    fb.clipq = w.clipq.p; fb.bigq = w.bigq.p; fb.bigpre = w.bigpre.p; fb.dbase = w.dbase.p;
+    fb.bigpart = w.bigpre.p + n_slots + 1;   // BIG_PARTS (256) sums after the prefix
+    fb.rqueue = w.rqueue.p;
     if (shadow) {
         fb.depth = ctx->shadow_map.p;
     } else {

@@ -163,36 +163,73 @@ __device__ __forceinline__ float plane_dist(const LVert &v, int p) {   // plane_
     }
 }
 
-// detail::clip_polygon_frustum (:111-164) for the rare triangles that are not trivially inside.
-// Returns the polygon size (<= MAX_POLY); out holds the result.
-__device__ __forceinline__ int clip_frustum(const LVert (&tri)[3], LVert (&out)[MAX_POLY]) {
-    LVert buf[2][MAX_POLY];
+// detail::clip_polygon_frustum (:111-164) for the triangles k_lib_setup queues (not trivially inside).
+// The two polygon buffers live in LDS, one column per lane (component-major, lane-minor: no bank
+// conflicts, no scratch); a one-wave workgroup holds 2 x MAX_POLY x 12 x 64 floats.
+constexpr int CLIP_LANES = 64;
+typedef float ClipBuf[2][MAX_POLY][12][CLIP_LANES];
+
+__device__ __forceinline__ LVert clip_ld(const ClipBuf &B, int cur, int i, int lane) {
+    LVert o;
+    float *po = &o.cx;
+#pragma unroll
+    for (int c = 0; c < 12; ++c) po[c] = B[cur][i][c][lane];
+    return o;
+}
+
+__device__ __forceinline__ void clip_st(ClipBuf &B, int cur, int i, int lane, const LVert &v) {
+    const float *pv = &v.cx;
+#pragma unroll
+    for (int c = 0; c < 12; ++c) B[cur][i][c][lane] = pv[c];
+}
+
+// Returns the polygon size (<= MAX_POLY); polygon vertex j is buffer (*cur) entry (j + *rot) % n.
+// A plane that every current vertex is inside of emits the polygon rotated by one (each edge emits
+// its end vertex): that is kept as an index rotation instead of a copy, with the identical result.
+__device__ __forceinline__ int clip_frustum_lds(ClipBuf &B, int lane, const LVert (&tri)[3], int &cur, int &rot) {
     int n = 3;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) buf[0][k] = tri[k];
-    int cur = 0;
+    for (int k = 0; k < 3; ++k) clip_st(B, 0, k, lane, tri[k]);
+    cur = 0;
+    rot = 0;
     for (int p = 0; p < 6 && n > 0; ++p) {
-        int m = 0;
+        bool all_in = true;
         for (int i = 0; i < n; ++i) {
-            const LVert &c = buf[cur][i], &x = buf[cur][(i + 1) % n];
-            const float da = plane_dist(c, p), db = plane_dist(x, p);
+            LVert v;
+            v.cx = B[cur][i][0][lane]; v.cy = B[cur][i][1][lane]; v.cz = B[cur][i][2][lane]; v.cw = B[cur][i][3][lane];
+            all_in = all_in && plane_dist(v, p) >= 0.0f;
+        }
+        if (all_in) {
+            rot = rot + 1 == n ? 0 : rot + 1;
+            continue;
+        }
+        int m = 0;
+        LVert c = clip_ld(B, cur, rot, lane);
+        float da = plane_dist(c, p);
+        for (int i = 0; i < n; ++i) {
+            int j = rot + i + 1;
+            j = j >= n ? j - n : j;
+            const LVert x = clip_ld(B, cur, j, lane);
+            const float db = plane_dist(x, p);
             const bool cin = da >= 0.0f, xin = db >= 0.0f;
             if (m > MAX_POLY - 2) break;   // unreachable for a convex polygon (<= 1 vertex added per plane)
             if (cin && xin) {
-                buf[cur ^ 1][m++] = x;
+                clip_st(B, cur ^ 1, m++, lane, x);
             } else if (cin && !xin) {
                 const float denom = da - db;
-                if (fabsf(denom) > 1e-8f) buf[cur ^ 1][m++] = lerp_v(c, x, da / denom);
+                if (fabsf(denom) > 1e-8f) clip_st(B, cur ^ 1, m++, lane, lerp_v(c, x, da / denom));
             } else if (!cin && xin) {
                 const float denom = da - db;
-                if (fabsf(denom) > 1e-8f) buf[cur ^ 1][m++] = lerp_v(c, x, da / denom);
-                buf[cur ^ 1][m++] = x;
+                if (fabsf(denom) > 1e-8f) clip_st(B, cur ^ 1, m++, lane, lerp_v(c, x, da / denom));
+                clip_st(B, cur ^ 1, m++, lane, x);
             }
+            c = x;
+            da = db;
         }
         n = m;
         cur ^= 1;
+        rot = 0;
     }
-    for (int i = 0; i < n; ++i) out[i] = buf[cur][i];
     return n;
 }
 
@@ -281,6 +318,9 @@ __device__ __forceinline__ void store_box(const LibBuffers &fb, uint32_t slot, i
 // tri_after_clip / tri_raster like the reference.
 // lazy_ids (trivially inside triangles): a, b, c hold positions only; the normal / UV varyings are
 // loaded and transformed for primitives that survive the culls.
+// direct (k_lib_clip): marks without the block aggregation -- small boxes marked by the thread, large
+// ones queued for k_lib_bigmark (ss / pend unused).
+template <bool DIRECT = false>
 __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, const LibDrawGPU &dr, int d,
                          uint32_t seq, uint32_t slot, LVert a, LVert b, LVert c, uint32_t &n_clip,
                          uint32_t &n_rast, SetupShared &ss, Pend &pend, const uint32_t *lazy_ids = nullptr) {
@@ -345,7 +385,7 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     r.z0 = a.cz * iw0; r.z1 = b.cz * iw1; r.z2 = c.cz * iw2;
     r.seq = seq;
     r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
-    fb.recs[slot] = r;
+    if (!(fp.exp_flags & 4u)) fb.recs[slot] = r;
     fb.zord[slot] = (fp.flags & LF_DEPTH) ? lib_zmin_ord<false>(fp, r) : 0u;
     LibShade s;
     const float iw[3] = {iw0, iw1, iw2};
@@ -357,16 +397,25 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     }
     s.draw = d;
     s.pad[0] = s.pad[1] = s.pad[2] = 0;
-    fb.shade[slot] = s;
+    if (!(fp.exp_flags & 1u)) fb.shade[slot] = s;
     store_box(fb, slot, x0, x1, y0, y1);
-    lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot, ss, pend);
+    if (fp.exp_flags & 2u) return;
+    if (DIRECT) {
+        const int n_rt = (x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1);
+        if (n_rt > SMALL_MARK) fb.bigq[atomicAdd(&cnt[LC_BIGQ], 1u)] = make_uint4(slot, pack16(x0, x1), pack16(y0, y1), 0u);
+        else lib_mark_range(fp, fb, cnt, x0, x1, y0, y1, slot, 0, 1);
+    } else {
+        lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot, ss, pend);
+    }
 }
 
-__device__ __forceinline__ int lib_find_draw(const LibDrawGPU *draws, int n_draws, int gid) {
+// The draw of pass triangle gid: a binary search over the compact tri_base array (4 B per draw, one or
+// two cache lines for hundreds of draws) instead of the 400-B draw records.
+__device__ __forceinline__ int lib_find_draw(const int32_t *dbase, int n_draws, int gid) {
     int lo = 0, hi = n_draws - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (draws[mid].tri_base <= gid) lo = mid; else hi = mid - 1;
+        if (dbase[mid] <= gid) lo = mid; else hi = mid - 1;
     }
     return lo;
 }
@@ -377,19 +426,43 @@ __device__ __forceinline__ bool read_tri(const LibDrawGPU &dr, int local, uint32
     return id[0] < (uint32_t)dr.n_verts && id[1] < (uint32_t)dr.n_verts && id[2] < (uint32_t)dr.n_verts;
 }
 
-__device__ uint2 setup_clipped_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int d, int tri, uint32_t i0,
-                                   uint32_t i1, uint32_t i2, SetupShared &ss, Pend &pend);
+// Tile-sharded camera pass: can the clipped fans of a triangle that is not trivially inside land on
+// one of this rank's 32x32 tiles?  With every corner in front of the eye (w > 0) the clipped polygon
+// lies inside the triangle, whose projection is the 2D triangle of the projected corners: its bbox
+// (2 px of margin for the clipper's rounding), clamped to the screen, bounds every fan.  A corner
+// behind the eye gives no such bound (true).
+__device__ __forceinline__ bool clip_reaches_rank(const LibFrameParams &fp, const LVert (&t)[3]) {
+    if (!(t[0].cw > 0.0f && t[1].cw > 0.0f && t[2].cw > 0.0f)) return true;
+    float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float sx = (t[k].cx / t[k].cw * 0.5f + 0.5f) * (float)(fp.W - 1);
+        const float sy = (t[k].cy / t[k].cw * 0.5f + 0.5f) * (float)(fp.H - 1);
+        x0 = fminf(x0, sx); x1 = fmaxf(x1, sx); y0 = fminf(y0, sy); y1 = fmaxf(y1, sy);
+    }
+    if (!(x1 >= -2.0f && y1 >= -2.0f && x0 <= (float)fp.W + 1.0f && y0 <= (float)fp.H + 1.0f)) return false;  // off screen (NaN: kept)
+    const int tx0 = max(0, (int)fmaxf(x0 - 2.0f, 0.0f) / TILE), tx1 = min(fp.tiles_x - 1, (int)fminf(x1 + 2.0f, (float)(fp.W - 1)) / TILE);
+    const int ty0 = max(0, (int)fmaxf(y0 - 2.0f, 0.0f) / TILE), ty1 = min(fp.tiles_y - 1, (int)fminf(y1 + 2.0f, (float)(fp.H - 1)) / TILE);
+    if (tx1 - tx0 + 1 >= fp.count || ty1 - ty0 >= 64) return true;   // a row of count tiles holds every rank's
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx)
+            if (lib_owned(fp, tx, ty)) return true;
+    return false;
+}
 
-// Camera pass: one input triangle of rasterize_mesh.
-__device__ __forceinline__ void setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_clip,
+// Camera pass: one input triangle of rasterize_mesh.  A triangle that is not trivially inside the
+// frustum is queued for k_lib_clip (returns true): the clipper's polygon buffers live in scratch, and
+// running it here would stall every wave that holds one such triangle and give the whole setup
+// kernel a scratch allocation.
+__device__ __forceinline__ bool setup_camera_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_clip,
                                  uint32_t &n_rast, SetupShared &ss, Pend &pend, int d_uni) {
-    const int d = d_uni >= 0 ? d_uni : lib_find_draw(fb.draws, fp.n_draws, tri);
+    const int d = d_uni >= 0 ? d_uni : lib_find_draw(fb.dbase, fp.n_draws, tri);
     const LibDrawGPU &dr = fb.draws[d];
     const int local = tri - dr.tri_base;
     uint32_t id[3];
     if (!read_tri(dr, local, id)) {
         store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
-        return;
+        return false;
     }
     LVert t[3];
 #pragma unroll
@@ -397,52 +470,20 @@ __device__ __forceinline__ void setup_camera_tri(const LibFrameParams &fp, const
     const uint32_t seq0 = (uint32_t)tri * 16u;
     if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
         emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast, ss, pend, id);
-        return;
+        return false;
     }
-    const uint2 nc = setup_clipped_tri(fp, fb, cnt, d, tri, id[0], id[1], id[2], ss, pend);
-    n_clip += nc.x;
-    n_rast += nc.y;
-}
-
-// The clipping half of setup_camera_tri (inlined; only this branch touches the scratch-resident
-// polygon buffers, so the trivially-inside path keeps its vertices in registers).  The corners are
-// recomputed from their ids with the identical arithmetic.  Returns the (tri_after_clip,
-// tri_raster) increments.
-__device__ __forceinline__ uint2 setup_clipped_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int d, int tri,
-                                                   uint32_t i0, uint32_t i1, uint32_t i2, SetupShared &ss, Pend &pend) {
-    uint32_t n_clip = 0, n_rast = 0;
-    const LibDrawGPU &dr = fb.draws[d];
-    const LVert t[3] = {vertex_out(dr, i0), vertex_out(dr, i1), vertex_out(dr, i2)};
-    const uint32_t seq0 = (uint32_t)tri * 16u;
-    LVert poly[MAX_POLY];
-    const int n = clip_frustum(t, poly);
-    if (n < 3) {
+    if (fp.count > 1 && !clip_reaches_rank(fp, t)) {   // tile-sharded: no fan can land on an owned tile
         store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
-        return make_uint2(0u, 0u);
+        return false;
     }
-    uint32_t xb = 0;
-    if (n > 3) {   // fans 1 .. n-3 take consecutive extra slots
-        const uint32_t e = atomicAdd(&cnt[LC_EXTRA], (uint32_t)(n - 3));
-        if (e + (uint32_t)(n - 3) > fp.extra_cap) {
-            atomicOr(&cnt[LC_OVERFLOW], LOV_EXTRA);
-            store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
-            return make_uint2(0u, 0u);
-        }
-        xb = (uint32_t)fp.n_tris + e;
-        fb.xbase[tri] = xb;
-    }
-    for (int k = 1; k + 1 < n; ++k) {
-        const uint32_t slot = k == 1 ? (uint32_t)tri : xb + (uint32_t)(k - 2);
-        emit_fan(fp, fb, cnt, dr, d, seq0 + (uint32_t)(k - 1), slot, poly[0], poly[k], poly[k + 1], n_clip, n_rast, ss, pend);
-    }
-    return make_uint2(n_clip, n_rast);
+    return true;
 }
 
 // Shadow pass: one caster triangle of PassShadowMap (pass_shadow_map.hpp:155-203), draws[d].viewproj
 // holding the light camera's viewproj.  n_rast counts the triangles with a non-empty bbox.
 __device__ __forceinline__ void setup_shadow_tri(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int tri, uint32_t &n_rast,
                                  SetupShared &ss, Pend &pend, int d_uni) {
-    const int d = d_uni >= 0 ? d_uni : lib_find_draw(fb.draws, fp.n_draws, tri);
+    const int d = d_uni >= 0 ? d_uni : lib_find_draw(fb.dbase, fp.n_draws, tri);
     const LibDrawGPU &dr = fb.draws[d];
     const int local = tri - dr.tri_base;
     uint32_t id[3];
@@ -501,44 +542,17 @@ __device__ __forceinline__ void setup_shadow_tri(const LibFrameParams &fp, const
     lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri, ss, pend);
 }
 
-template <bool SHADOW>
-__global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
-    __shared__ SetupShared ss;
-    const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
-    uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    const bool stl = fb.stimeline != nullptr && tid == 0;
-    const uint64_t st0 = stl ? tl_now() : 0ull;
+__device__ __forceinline__ void setup_shared_init(SetupShared &ss, int tid) {
     if (tid < 2) ss.stat[tid] = 0u;
     if (tid == 0) ss.nbig = 0u;
     if (tid < 4) ss.ub[tid] = tid < 2 ? INT_MAX : -1;
     static_assert(AGG_BINS == 256, "one union bin tile per thread");
     ss.bcnt[tid] = 0u;
     ss.rbusy[tid] = 0u;
-    // zero the other counter set and bin counts for the next frame
-    if (b == 0 && tid < LC_N) fb.counters[(fp.parity ^ 1u) * LC_N + tid] = 0u;
-    {
-        const int n_bt = fp.tiles_x * fp.tiles_y;
-        uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
-        for (int t = b * 256 + tid; t < n_bt; t += (int)gridDim.x * 256) next_count[t] = 0u;
-    }
-    __syncthreads();
-    const int tri = b * 256 + tid;
-    uint32_t n_clip = 0, n_rast = 0;
-    Pend pend;
-    // the block's draw when all its triangles share one (block-uniform: its uniforms come in
-    // through scalar loads), else -1 and a per-thread search
-    const int t_first = b * 256, t_last = min(b * 256 + 255, fp.n_tris - 1);
-    const int d_first = lib_find_draw(fb.draws, fp.n_draws, t_first);
-    const int d_uni = (d_first + 1 >= fp.n_draws || fb.draws[d_first + 1].tri_base > t_last) ? d_first : -1;
-    if (tri < fp.n_tris) {
-        if (d_uni >= 0) {   // two inlined copies: this one sees d_uni as the (scalar) draw
-            if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, d_uni);
-            else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, d_uni);
-        } else {
-            if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, -1);
-            else setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, -1);
-        }
-    }
+}
+
+// Per-thread pass statistics into the block's ss.stat, and the thread's deferred box into the union.
+__device__ __forceinline__ void setup_gather(SetupShared &ss, const Pend &pend, uint32_t n_clip, uint32_t n_rast) {
     if (pend.valid) {
         atomicMin(&ss.ub[0], pend.x0 / TILE);
         atomicMin(&ss.ub[1], pend.y0 / TILE);
@@ -553,131 +567,133 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
         atomicAdd(&ss.stat[0], n_clip);
         atomicAdd(&ss.stat[1], n_rast);
     }
-    __syncthreads();
-    const uint64_t st1 = stl ? tl_now() : 0ull;
-    // the deferred primitives (<= 2x2 bin tiles each): busy rows and bin appends through LDS
-    {
-        const int ubx0 = ss.ub[0], uby0 = ss.ub[1], uw = ss.ub[2] - ubx0 + 1, uh = ss.ub[3] - uby0 + 1;
-        if (stl) fb.stimeline[(size_t)b * STL_STRIDE + 5] = (uint64_t)max(uw, 0) * (uint64_t)max(uh, 0);
-        const bool agg = uw > 0 && uh > 0 && uw * uh <= AGG_BINS;   // block-uniform
-        const bool sharded = fp.count > 1;
-        constexpr int RPB = TILE / LIB_RTH;                        // raster rows per bin tile
-        const int bx0 = pend.x0 / TILE, by0 = pend.y0 / TILE, bx1 = pend.x1 / TILE, by1 = pend.y1 / TILE;
-        uint32_t pos[2][2] = {{0u, 0u}, {0u, 0u}};
-        if (pend.valid) {
-            if (!agg) {
-                lib_mark_range(fp, fb, cnt, pend.x0, pend.x1, pend.y0, pend.y1, pend.slot, 0, 1);
-            } else {
-                for (int ry = pend.y0 / LIB_RTH; ry <= pend.y1 / LIB_RTH; ++ry) {
-                    const int by = ry / RPB;
-                    for (int rx = pend.x0 / LIB_RTW; rx <= pend.x1 / LIB_RTW; ++rx)
-                        if (!sharded || lib_owned(fp, rx, by))
-                            atomicOr(&ss.rbusy[(by - uby0) * uw + (rx - ubx0)], 1u << (ry % RPB));
-                }
-                if (!fp.scan_mode) {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-#pragma unroll
-                        for (int i = 0; i < 2; ++i)
-                            if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j)))
-                                pos[j][i] = atomicAdd(&ss.bcnt[(by0 + j - uby0) * uw + (bx0 + i - ubx0)], 1u);
-                }
+}
+
+// The deferred primitives (<= 2x2 bin tiles each): busy rows and bin appends through LDS (after a
+// barrier that follows setup_gather).  Returns the union's w * h (timeline).
+__device__ int setup_deferred(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, SetupShared &ss, const Pend &pend, int tid) {
+    const int ubx0 = ss.ub[0], uby0 = ss.ub[1], uw = ss.ub[2] - ubx0 + 1, uh = ss.ub[3] - uby0 + 1;
+    const bool agg = uw > 0 && uh > 0 && uw * uh <= AGG_BINS;   // block-uniform
+    const bool sharded = fp.count > 1;
+    constexpr int RPB = TILE / LIB_RTH;                        // raster rows per bin tile
+    const int bx0 = pend.x0 / TILE, by0 = pend.y0 / TILE, bx1 = pend.x1 / TILE, by1 = pend.y1 / TILE;
+    uint32_t pos[2][2] = {{0u, 0u}, {0u, 0u}};
+    if (pend.valid) {
+        if (!agg) {
+            lib_mark_range(fp, fb, cnt, pend.x0, pend.x1, pend.y0, pend.y1, pend.slot, 0, 1);
+        } else {
+            for (int ry = pend.y0 / LIB_RTH; ry <= pend.y1 / LIB_RTH; ++ry) {
+                const int by = ry / RPB;
+                for (int rx = pend.x0 / LIB_RTW; rx <= pend.x1 / LIB_RTW; ++rx)
+                    if (!sharded || lib_owned(fp, rx, by))
+                        atomicOr(&ss.rbusy[(by - uby0) * uw + (rx - ubx0)], 1u << (ry % RPB));
             }
-        }
-        if (agg) {
-            __syncthreads();
-            if (tid < uw * uh) {
-                const int bx = ubx0 + tid % uw, by = uby0 + tid / uw;
-                const uint32_t rb = ss.rbusy[tid];
-                for (int r = 0; r < RPB; ++r)
-                    if ((rb >> r) & 1u) fb.busy[(by * RPB + r) * fp.tiles_x + bx] = 1u;
-                const uint32_t n = ss.bcnt[tid];
-                if (!fp.scan_mode && n) {
-                    uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
-                    ss.bcnt[tid] = atomicAdd(&tcount[by * fp.tiles_x + bx], n);
-                }
-            }
-            __syncthreads();
-            if (pend.valid && !fp.scan_mode) {
+            if (!fp.scan_mode) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
 #pragma unroll
                     for (int i = 0; i < 2; ++i)
-                        if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j))) {
-                            const int u = (by0 + j - uby0) * uw + (bx0 + i - ubx0);
-                            lib_append_bin(fp, fb, cnt, (by0 + j) * fp.tiles_x + bx0 + i, ss.bcnt[u] + pos[j][i], pend.slot);
-                        }
+                        if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j)))
+                            pos[j][i] = atomicAdd(&ss.bcnt[(by0 + j - uby0) * uw + (bx0 + i - ubx0)], 1u);
             }
         }
     }
-    const uint64_t st2 = stl ? tl_now() : 0ull;
-    // The block's large primitives, all at once: their (primitive, raster tile) busy marks and
-    // (primitive, bin tile) appends are laid end to end (prefix sums over the queue) and dealt over
-    // the block; a task finds its primitive by binary search.
+    if (agg) {
+        __syncthreads();
+        if (tid < uw * uh) {
+            const int bx = ubx0 + tid % uw, by = uby0 + tid / uw;
+            const uint32_t rb = ss.rbusy[tid];
+            for (int r = 0; r < RPB; ++r)
+                if ((rb >> r) & 1u) fb.busy[(by * RPB + r) * fp.tiles_x + bx] = 1u;
+            const uint32_t n = ss.bcnt[tid];
+            if (!fp.scan_mode && n) {
+                uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
+                ss.bcnt[tid] = atomicAdd(&tcount[by * fp.tiles_x + bx], n);
+            }
+        }
+        __syncthreads();
+        if (pend.valid && !fp.scan_mode) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j))) {
+                        const int u = (by0 + j - uby0) * uw + (bx0 + i - ubx0);
+                        lib_append_bin(fp, fb, cnt, (by0 + j) * fp.tiles_x + bx0 + i, ss.bcnt[u] + pos[j][i], pend.slot);
+                    }
+        }
+    }
+    return max(uw, 0) * max(uh, 0);
+}
+
+// The block's large primitives go to the pass-wide queue that k_lib_bigmark spreads over the chip
+// (a floor triangle at 4K spans thousands of raster tiles; a few blocks holding all of them were the
+// setup's critical path).  Block-uniform; one atomic per block.
+__device__ __forceinline__ uint32_t setup_flush_big(const LibBuffers &fb, uint32_t *cnt, SetupShared &ss, int tid) {
     const uint32_t nbig = min(ss.nbig, (uint32_t)BIG_CAP);
-    if (nbig > 0) {   // block-uniform
-        auto extent = [&](uint32_t i, int cell_w, int cell_h, int &cx0, int &cy0, int &nx) {
-            const uint4 e = ss.big[i];
-            cx0 = lo16(e.y) / cell_w;
-            cy0 = lo16(e.z) / cell_h;
-            nx = hi16(e.y) / cell_w - cx0 + 1;
-            return (uint32_t)(nx * (hi16(e.z) / cell_h - cy0 + 1));
-        };
-        // exclusive scans of the task counts (BIG_CAP = 2 x 256: two values per thread)
-        static_assert(BIG_CAP == 512, "two queue entries per thread");
-        uint32_t c[2][2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t i = 2u * tid + h;
-            int a, b2, n;
-            c[0][h] = i < nbig ? extent(i, LIB_RTW, LIB_RTH, a, b2, n) : 0u;
-            c[1][h] = i < nbig && !fp.scan_mode ? extent(i, TILE, TILE, a, b2, n) : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t pair = c[q][0] + c[q][1];
-            uint32_t incl = pair;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t vv = (uint32_t)__shfl_up((int)incl, o);
-                if ((tid & 63) >= o) incl += vv;
-            }
-            __syncthreads();
-            if ((tid & 63) == 63) ss.bcnt[tid >> 6] = incl;    // per-wave totals (bcnt is free now)
-            __syncthreads();
-            uint32_t wb = 0;
-            for (int w2 = 0; w2 < (tid >> 6); ++w2) wb += ss.bcnt[w2];
-            const uint32_t excl = wb + incl - pair;
-            ss.pre[q][2 * tid] = excl;
-            ss.pre[q][2 * tid + 1] = excl + c[q][0];
-            __syncthreads();
-            if (tid == 0) ss.pre[q][BIG_CAP] = ss.bcnt[0] + ss.bcnt[1] + ss.bcnt[2] + ss.bcnt[3];
-            __syncthreads();
-        }
-        const bool sharded = fp.count > 1;
-        uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t total = ss.pre[q][BIG_CAP];
-            uint32_t lo = 0;   // the primitive of task t: non-decreasing in t, so carried along
-            int cx0 = 0, cy0 = 0, nx = 1;
-            bool have = false;
-            for (uint32_t t = tid; t < total; t += 256) {
-                bool moved = !have;
-                while (lo + 1 < nbig && ss.pre[q][lo + 1] <= t) { ++lo; moved = true; }
-                if (moved) (void)extent(lo, q == 0 ? LIB_RTW : TILE, q == 0 ? LIB_RTH : TILE, cx0, cy0, nx);
-                have = true;
-                const int k = (int)(t - ss.pre[q][lo]);
-                const int cx = cx0 + k % nx, cy = cy0 + k / nx;
-                if (q == 0) {
-                    if (!sharded || lib_owned(fp, cx, cy / (TILE / LIB_RTH))) fb.busy[cy * fp.tiles_x + cx] = 1u;
-                } else if (!sharded || lib_owned(fp, cx, cy)) {
-                    const int bt = cy * fp.tiles_x + cx;
-                    lib_append_bin(fp, fb, cnt, bt, atomicAdd(&tcount[bt], 1u), ss.big[lo].x);
-                }
-            }
+    if (nbig > 0) {
+        if (tid == 0) ss.pre[0][0] = atomicAdd(&cnt[LC_BIGQ], nbig);
+        __syncthreads();
+        const uint32_t base = ss.pre[0][0];
+        for (uint32_t i = (uint32_t)tid; i < nbig; i += 256) fb.bigq[base + i] = ss.big[i];
+    }
+    return nbig;
+}
+
+// Appends the lanes with `pred` to a queue: one atomic per wave; every lane of the wave calls it.
+__device__ __forceinline__ void wave_append(uint32_t *counter, uint32_t *queue, bool pred, uint32_t value) {
+    const uint64_t m = __ballot(pred);
+    if (m == 0ull) return;
+    const int lane = __lane_id();
+    uint32_t base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (pred) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = value;
+}
+
+template <bool SHADOW>
+__global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
+    __shared__ SetupShared ss;
+    const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
+    uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const bool stl = fb.stimeline != nullptr && tid == 0;
+    const uint64_t st0 = stl ? tl_now() : 0ull;
+    setup_shared_init(ss, tid);
+    // zero the other counter set, raster queues and bin counts for the next frame
+    if (b == 0 && tid < LC_N) fb.counters[(fp.parity ^ 1u) * LC_N + tid] = 0u;
+    if (b == 0 && tid < LIB_NQ) fb.rqueue[((fp.parity ^ 1u) * LIB_NQ + tid) * LIB_QSTRIDE] = 0u;
+    {
+        const int n_bt = fp.tiles_x * fp.tiles_y;
+        uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
+        for (int t = b * 256 + tid; t < n_bt; t += (int)gridDim.x * 256) next_count[t] = 0u;
+    }
+    __syncthreads();
+    const int tri = b * 256 + tid;
+    uint32_t n_clip = 0, n_rast = 0;
+    Pend pend;
+    bool need_clip = false;
+    // the block's draw when all its triangles share one (block-uniform: its uniforms come in
+    // through scalar loads), else -1 and a per-thread search
+    const int t_first = b * 256, t_last = min(b * 256 + 255, fp.n_tris - 1);
+    const int d_first = lib_find_draw(fb.dbase, fp.n_draws, t_first);
+    const int d_uni = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : -1;
+    if (tri < fp.n_tris) {
+        if (d_uni >= 0) {   // two inlined copies: this one sees d_uni as the (scalar) draw
+            if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, d_uni);
+            else need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, d_uni);
+        } else {
+            if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, -1);
+            else need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, -1);
         }
     }
+    if (!SHADOW) wave_append(&cnt[LC_CLIPQ], fb.clipq, need_clip, (uint32_t)tri);
+    setup_gather(ss, pend, n_clip, n_rast);
+    __syncthreads();
+    const uint64_t st1 = stl ? tl_now() : 0ull;
+    const int uwh = setup_deferred(fp, fb, cnt, ss, pend, tid);
+    if (stl) fb.stimeline[(size_t)b * STL_STRIDE + 5] = (uint64_t)uwh;
+    const uint64_t st2 = stl ? tl_now() : 0ull;
+    const uint32_t nbig = setup_flush_big(fb, cnt, ss, tid);
     if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(ss.stat[0], ss.stat[1]);
     if (fb.stimeline) {
         __syncthreads();
@@ -685,6 +701,196 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
             uint64_t *o = fb.stimeline + (size_t)b * STL_STRIDE;
             o[0] = st0; o[1] = st1; o[2] = st2; o[3] = tl_now(); o[4] = nbig;
         }
+    }
+}
+
+// The camera pass's queued triangles (k_lib_setup: not trivially inside): Sutherland-Hodgman against
+// the 6 planes and the fans (rasterizer.hpp:241-328), one lane per triangle, one-wave workgroups
+// striding the queue; the polygons live in LDS.  Same slots, submission order (tri * 16 + fan), marks
+// and counters as the reference's per-triangle clip.
+__global__ __launch_bounds__(CLIP_LANES) void k_lib_clip(LibFrameParams fp, LibBuffers fb) {
+    __shared__ ClipBuf B;
+    __shared__ SetupShared ss_unused;   // emit_fan<true> marks directly
+    const int lane = (int)threadIdx.x;
+    uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const uint32_t n = cnt[LC_CLIPQ];
+    uint32_t n_clip = 0, n_rast = 0;
+    Pend pend;
+    for (uint32_t q = blockIdx.x * CLIP_LANES + (uint32_t)lane; q < n; q += gridDim.x * CLIP_LANES) {
+        const int tri = (int)fb.clipq[q];
+        const int d = lib_find_draw(fb.dbase, fp.n_draws, tri);
+        const LibDrawGPU &dr = fb.draws[d];
+        uint32_t id[3];
+        (void)read_tri(dr, tri - dr.tri_base, id);   // in range: checked by k_lib_setup
+        const LVert t[3] = {vertex_out(dr, id[0]), vertex_out(dr, id[1]), vertex_out(dr, id[2])};
+        const uint32_t seq0 = (uint32_t)tri * 16u;
+        int cur = 0, rot = 0;
+        const int m = clip_frustum_lds(B, lane, t, cur, rot);
+        if (m < 3) {
+            store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+            continue;
+        }
+        uint32_t xb = 0;
+        if (m > 3) {   // fans 1 .. m-3 take consecutive extra slots
+            const uint32_t e = atomicAdd(&cnt[LC_EXTRA], (uint32_t)(m - 3));
+            if (e + (uint32_t)(m - 3) > fp.extra_cap) {
+                atomicOr(&cnt[LC_OVERFLOW], LOV_EXTRA);
+                store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+                continue;
+            }
+            xb = (uint32_t)fp.n_tris + e;
+            fb.xbase[tri] = xb;
+        }
+        auto at = [&](int j) { j += rot; return clip_ld(B, cur, j >= m ? j - m : j, lane); };
+        const LVert p0 = at(0);
+        for (int k = 1; k + 1 < m; ++k) {
+            const uint32_t slot = k == 1 ? (uint32_t)tri : xb + (uint32_t)(k - 2);
+            emit_fan<true>(fp, fb, cnt, dr, d, seq0 + (uint32_t)(k - 1), slot, p0, at(k), at(k + 1), n_clip, n_rast,
+                           ss_unused, pend);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        n_clip += __shfl_down(n_clip, o);
+        n_rast += __shfl_down(n_rast, o);
+    }
+    if (lane == 0 && (n_clip | n_rast)) {
+        atomicAdd(&fb.blk_stat[0].x, n_clip);
+        atomicAdd(&fb.blk_stat[0].y, n_rast);
+    }
+}
+
+// Exclusive task prefix of the large-primitive queue: per primitive its owned-or-not raster tiles
+// (busy marks) then, in bin mode, its bin tiles (appends).  One workgroup.
+__device__ __forceinline__ uint32_t big_tasks(const LibFrameParams &fp, uint4 e, uint32_t &n_busy) {
+    const int x0 = (int)lo16(e.y), x1 = (int)hi16(e.y), y0 = (int)lo16(e.z), y1 = (int)hi16(e.z);
+    n_busy = (uint32_t)((x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1));
+    const uint32_t n_bin = fp.scan_mode ? 0u : (uint32_t)((x1 / TILE - x0 / TILE + 1) * (y1 / TILE - y0 / TILE + 1));
+    return n_busy + n_bin;
+}
+
+// The queue is split into BIG_PARTS contiguous ranges: k_lib_bigsum sums each range's tasks,
+// k_lib_bigscan offsets each range by the sums before it and scans it (two parallel launches).
+constexpr int BIG_PARTS = 256;
+
+__device__ __forceinline__ uint32_t block_sum256(uint32_t v, uint32_t *s_wave) {
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_down((int)v, o);
+    if (__lane_id() == 0) s_wave[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const uint32_t t = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    __syncthreads();
+    return t;
+}
+
+__global__ __launch_bounds__(256) void k_lib_bigsum(LibFrameParams fp, LibBuffers fb) {
+    __shared__ uint32_t s_wave[4];
+    const uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const uint32_t n = cnt[LC_BIGQ];
+    const uint32_t per = (n + BIG_PARTS - 1) / BIG_PARTS;
+    const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+    uint32_t v = 0, nb;
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += 256) v += big_tasks(fp, fb.bigq[i], nb);
+    const uint32_t t = block_sum256(v, s_wave);
+    if (threadIdx.x == 0) fb.bigpart[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void k_lib_bigscan(LibFrameParams fp, LibBuffers fb) {
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_carry;
+    const uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const uint32_t n = cnt[LC_BIGQ];
+    const uint32_t per = (n + BIG_PARTS - 1) / BIG_PARTS;
+    const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t before = block_sum256(tid < (int)blockIdx.x ? fb.bigpart[tid] : 0u, s_wave);
+    if (tid == 0) s_carry = before;
+    __syncthreads();
+    for (uint32_t base = i0; base < i1; base += 256) {   // block-uniform
+        const uint32_t i = base + (uint32_t)tid;
+        uint32_t nb;
+        const uint32_t v = i < i1 ? big_tasks(fp, fb.bigq[i], nb) : 0u;
+        uint32_t incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) s_wave[wave] = incl;
+        __syncthreads();
+        uint32_t off = s_carry;
+        for (int w = 0; w < wave; ++w) off += s_wave[w];
+        if (i < i1) fb.bigpre[i] = off + incl - v;
+        __syncthreads();
+        if (tid == 255) s_carry = off + incl;
+        __syncthreads();
+    }
+    if (blockIdx.x == BIG_PARTS - 1 && tid == 0) fb.bigpre[n] = s_carry;
+}
+
+// Copies draws[i].tri_base into the compact array the triangle -> draw searches read.
+__global__ __launch_bounds__(256) void k_lib_dbase(LibFrameParams fp, LibBuffers fb) {
+    const int i = (int)(blockIdx.x * 256u + threadIdx.x);
+    if (i < fp.n_draws) fb.dbase[i] = fb.draws[i].tri_base;
+}
+
+// The large primitives' (primitive, tile) tasks, a contiguous range per workgroup: busy marks on the
+// owned raster tiles, then bin appends on the owned bin tiles.  Each workgroup stages the queue
+// window its range touches in LDS and finds a task's primitive by binary search there.
+constexpr int BIG_WIN = 1024;
+
+__global__ __launch_bounds__(256) void k_lib_bigmark(LibFrameParams fp, LibBuffers fb) {
+    __shared__ uint32_t s_pre[BIG_WIN + 1];
+    __shared__ uint4 s_e[BIG_WIN];
+    __shared__ uint32_t s_lo;
+    uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const uint32_t n = cnt[LC_BIGQ];
+    if (n == 0u) return;
+    const uint32_t total = fb.bigpre[n];
+    const uint32_t per = (total + gridDim.x - 1u) / gridDim.x;
+    const uint32_t t0 = blockIdx.x * per, t1 = min(total, t0 + per);
+    const int tid = (int)threadIdx.x;
+    const bool sharded = fp.count > 1;
+    uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
+    for (uint32_t w0 = t0; w0 < t1;) {   // block-uniform: windows of at most BIG_WIN primitives
+        if (tid == 0) {   // the primitive holding task w0: last i with bigpre[i] <= w0
+            uint32_t lo = 0, hi = n - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (fb.bigpre[mid] <= w0) lo = mid; else hi = mid - 1;
+            }
+            s_lo = lo;
+        }
+        __syncthreads();
+        const uint32_t e0 = s_lo, m = min((uint32_t)BIG_WIN, n - e0);
+        for (uint32_t i = (uint32_t)tid; i <= m; i += 256) s_pre[i] = fb.bigpre[e0 + i];
+        for (uint32_t i = (uint32_t)tid; i < m; i += 256) s_e[i] = fb.bigq[e0 + i];
+        __syncthreads();
+        const uint32_t w1 = min(t1, s_pre[m]);   // the tasks this window covers
+        for (uint32_t t = w0 + (uint32_t)tid; t < w1; t += 256) {
+            uint32_t lo = 0, hi = m - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (s_pre[mid] <= t) lo = mid; else hi = mid - 1;
+            }
+            const uint4 e = s_e[lo];
+            uint32_t nb;
+            (void)big_tasks(fp, e, nb);
+            const int k = (int)(t - s_pre[lo]);
+            const int x0 = (int)lo16(e.y), x1 = (int)hi16(e.y), y0 = (int)lo16(e.z);
+            if ((uint32_t)k < nb) {
+                const int nx = x1 / LIB_RTW - x0 / LIB_RTW + 1;
+                const int cx = x0 / LIB_RTW + k % nx, cy = y0 / LIB_RTH + k / nx;
+                if (!sharded || lib_owned(fp, cx, cy / (TILE / LIB_RTH))) fb.busy[cy * fp.tiles_x + cx] = 1u;
+            } else {
+                const int kb = k - (int)nb;
+                const int nx = x1 / TILE - x0 / TILE + 1;
+                const int cx = x0 / TILE + kb % nx, cy = y0 / TILE + kb / nx;
+                if (!sharded || lib_owned(fp, cx, cy)) {
+                    const int bt = cy * fp.tiles_x + cx;
+                    lib_append_bin(fp, fb, cnt, bt, atomicAdd(&tcount[bt], 1u), e.x);
+                }
+            }
+        }
+        w0 = w1;
+        __syncthreads();
     }
 }
 
@@ -993,6 +1199,7 @@ struct LibShared {
     uint32_t wtot[4][2];                  // per wave: surviving candidates, pairs
     uint32_t colmax[2][LIB_RTW];          // per pixel column: max key z (orderable bits) over its rows, by chunk parity
     uint32_t nc, nbusy, cov, maxbin, npairs;
+    int next[3];                          // the workgroup's next run, queue, queues tried
     uint64_t tl[LTL_STRIDE];              // SHS_OPT_TIMELINE accumulators (thread 0)
     uint8_t wown[LIB_PAIR_WORDS];         // surviving candidate owning each bitmap word's first pair
 };
@@ -1410,27 +1617,54 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
     }
     uint32_t chunk = 0;   // staging passes so far (selects the colmax slot)
     if (fb.timeline && tid < LTL_STRIDE) sh.tl[tid] = tid == LTL_START ? tl_now() : 0ull;
-    for (int j0 = (int)blockIdx.x; j0 < fp.n_owned_rt; j0 += 256 * G) {
-        __syncthreads();
-        if (tid == 0) sh.nbusy = 0;
-        __syncthreads();
-        const int j = j0 + tid * G;
-        if (j < fp.n_owned_rt) {
-            // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it
-            const int t = fp.rank + (j >> 2) * fp.count;
-            const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / LIB_RTH) + (j & 3);
-            if (row < fp.rtiles_y) {
-                const int rt = row * fp.tiles_x + col;
-                if (fb.busy[rt]) sh.busy[atomicAdd(&sh.nbusy, 1u) & 0xffffu] = rt;
-                else sh.busy[255 - atomicAdd(&sh.nbusy, 0x10000u) / 0x10000u] = rt;
+    // Owned raster tiles: the first S * G statically interleaved (tile b + i * G, i < S: no ticket
+    // latency), the rest from LIB_NQ ticket queues (the next ticket requested while the current tile
+    // renders; an exhausted queue sends the workgroup on to the others).  S covers about half of the
+    // tiles, so the dense tiles that end up late in some workgroup's static list are balanced by the
+    // dynamic half; one tile per ticket keeps a dense bin tile's 4 rows on different workgroups.
+    uint32_t *rq = fb.rqueue + (size_t)fp.parity * LIB_NQ * LIB_QSTRIDE;
+    const int S = max(1, fp.n_owned_rt / (2 * G));
+    const int dyn0 = S * G;
+    int j = (int)blockIdx.x;
+    int i_static = 0, q = (int)(blockIdx.x & (LIB_NQ - 1)), tried = 0;
+    while (j < fp.n_owned_rt) {   // block-uniform
+        const bool dynamic_next = i_static + 1 >= S;
+        uint32_t tk = 0;
+        if (tid == 0 && dynamic_next) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
+        // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it
+        const int t = fp.rank + (j >> 2) * fp.count;
+        const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / LIB_RTH) + (j & 3);
+        if (row < fp.rtiles_y) {
+            const int rt = row * fp.tiles_x + col;
+            if (fb.busy[rt]) {
+                lib_raster_tile<SHADOW>(fp, fb, cnt, rt, sh, chunk);
+            } else {
+                const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
+                lib_clear_tile<SHADOW>(fp, fb, rt);
+                if (fb.timeline && tid == 0) { sh.tl[LTL_CLEAR] += tl_now() - t_c; sh.tl[LTL_NCLEAR] += 1ull; }
             }
         }
+        if (!dynamic_next) {
+            ++i_static;
+            j += G;
+            continue;
+        }
+        i_static = S;
+        if (tid == 0) {
+            int nj = dyn0 + q + LIB_NQ * (int)tk;
+            while (nj >= fp.n_owned_rt && ++tried < LIB_NQ) {
+                q = (q + 1) & (LIB_NQ - 1);
+                nj = dyn0 + q + LIB_NQ * (int)atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
+            }
+            sh.next[0] = nj < fp.n_owned_rt ? nj : fp.n_owned_rt;
+            sh.next[1] = q;
+            sh.next[2] = tried;
+        }
         __syncthreads();
-        const int nb = (int)(sh.nbusy & 0xffffu), ne = (int)(sh.nbusy >> 16);
-        for (int i = 0; i < nb; ++i) lib_raster_tile<SHADOW>(fp, fb, cnt, sh.busy[i], sh, chunk);
-        const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
-        for (int i = 0; i < ne; ++i) lib_clear_tile<SHADOW>(fp, fb, sh.busy[255 - i]);
-        if (fb.timeline && tid == 0) { sh.tl[LTL_CLEAR] += tl_now() - t_c; sh.tl[LTL_NCLEAR] += (uint64_t)ne; }
+        j = sh.next[0];
+        q = sh.next[1];
+        tried = sh.next[2];
+        __syncthreads();
     }
     __syncthreads();
     if (tid == 0) fb.rstat[blockIdx.x] = make_uint2(sh.cov, sh.maxbin);
@@ -1445,10 +1679,21 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
 namespace shs_internal {
 using namespace shs_dev;
 
+// k_lib_setup, then (camera pass) k_lib_clip over the queued triangles, then the large primitives'
+// marks (k_lib_bigscan + k_lib_bigmark).  The queue lengths stay on the device: the later kernels'
+// grids are fixed and stride or split what the counters hold.
 hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, hipStream_t s) {
     const int grid = std::max(1, (fp.n_tris + 255) / 256);
-    if (shadow) hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
-    else hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
+    hipLaunchKernelGGL(k_lib_dbase, dim3((unsigned)std::max(1, (fp.n_draws + 255) / 256)), dim3(256), 0, s, fp, fb);
+    if (shadow) {
+        hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
+    } else {
+        hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
+        hipLaunchKernelGGL(k_lib_clip, dim3(std::min(grid * 4, 1024)), dim3(CLIP_LANES), 0, s, fp, fb);
+    }
+    hipLaunchKernelGGL(k_lib_bigsum, dim3(BIG_PARTS), dim3(256), 0, s, fp, fb);
+    hipLaunchKernelGGL(k_lib_bigscan, dim3(BIG_PARTS), dim3(256), 0, s, fp, fb);
+    hipLaunchKernelGGL(k_lib_bigmark, dim3(1024), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }
 

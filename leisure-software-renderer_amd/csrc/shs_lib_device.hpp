@@ -82,7 +82,8 @@ constexpr uint32_t LF_MOTION = 4u;      // motion buffer written (per draw: enab
 constexpr uint32_t LF_GRADIENT = 8u;    // PassPBRForward's no-sky background gradient, else clear[]
 
 // counters[] (two parity sets, frame f uses set f & 1, k_lib_setup zeroes the other)
-constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_N = 4;
+// LC_CLIPQ: input triangles queued for k_lib_clip; LC_BIGQ: primitives queued for k_lib_bigmark
+constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGQ = 4, LC_N = 5;
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
 struct LibFrameParams {
@@ -96,6 +97,7 @@ struct LibFrameParams {
     uint32_t bin_cap, spill_cap, extra_cap;
     uint32_t parity, scan_mode;
     int32_t setup_blocks, n_owned_rt;
+    uint32_t exp_flags;              // timing experiments only (SHS_LIB_EXP; wrong images): 1 no shade, 2 no marks, 4 no recs
     int32_t sm_w, sm_h;              // shadow map sampled by the programs
     // Forward+ program: the light lists of the last shs_light_cull
     uint32_t lt_size, lt_tx, lt_ty, lt_maxp, lt_mode, lt_zs, n_lights;
@@ -124,7 +126,17 @@ struct LibBuffers {
     const uint32_t *tile_counts, *tile_indices;
     uint64_t *timeline;              // SHS_OPT_TIMELINE (camera pass): LTL_STRIDE per raster workgroup
     uint64_t *stimeline;             // SHS_OPT_TIMELINE (camera pass): STL_STRIDE per setup workgroup
+    uint32_t *clipq;                 // input triangles that need clipping (camera pass), n_tris capacity
+    uint4 *bigq;                     // primitives over SMALL_MARK raster tiles: (slot, bx, by, 0), one per slot
+    uint32_t *bigpre;                // k_lib_bigscan: exclusive task prefix of bigq (+ the total)
+    uint32_t *bigpart;               // k_lib_bigsum: per-workgroup task sums (BIG_PARTS)
+    int32_t *dbase;                  // k_lib_dbase: draws[i].tri_base, compact (the triangle -> draw search)
+    uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQ x LIB_QSTRIDE words
 };
+
+// k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket
+// counters a cache line apart (k_lib_setup zeroes the next frame's set).
+constexpr int LIB_NQ = 8, LIB_QSTRIDE = 32;
 
 // Library setup timeline slots: start, after the per-triangle work, after the deferred marks,
 // after the large-primitive marks (= end), large primitives, deferred-union width x height.

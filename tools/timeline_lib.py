@@ -1,6 +1,6 @@
 """Per-workgroup timeline of the library camera pass (SHS_OPT_TIMELINE): where k_lib_raster's time goes.
 
-usage (GPU box): python tools/timeline_lib.py [c4|c5] [n_objects] [tris_per_object]
+usage (GPU box): python tools/timeline_lib.py [c4|c5] [n_objects] [tris_per_object] [shard_count]
 Per workgroup: duration, summed phase times over its busy tiles (gather / stage + pairs / resolve +
 shade), clear time, tile / chunk / pair / candidate counts; distribution over workgroups and the
 slowest workgroup."""
@@ -36,6 +36,11 @@ def main():
 
         def one():
             ctx.render_pbr_forward_prepared(prepared)
+    count = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    frame.shard_rank, frame.shard_count = 0, count
+    if cfg == "c4":
+        cull.shard_rank, cull.shard_count = 0, count
+        ctx.light_cull(cull)
     prepared = ctx.prepare_lib(frame, draws)
     for _ in range(5):
         one()
