@@ -51,7 +51,7 @@ void release_work(Work &w) {
             if (e) { (void)hipEventDestroy(e); e = nullptr; }
     release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase); release(w.zord);
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.dbase); release(w.rqueue);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
     for (int i = 0; i < 2; ++i) {
         if (w.h_draws[i]) (void)hipHostFree(w.h_draws[i]);
         if (w.slot_ev[i]) (void)hipEventDestroy(w.slot_ev[i]);
@@ -154,9 +154,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
                     ensure(ctx, w.clipq, (size_t)std::max(n_tris, 1))))
         return SHS_ERR_HIP;
     // every slot enters the large-primitive queue at most once
-    if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots + 1 + 256) ||
-        ensure(ctx, w.dbase, std::max<size_t>(w.last_draws.size(), 1)))
-        return SHS_ERR_HIP;
+    if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots + 1 + 256)) return SHS_ERR_HIP;
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count;
     bool reset = gkey != w.geom_key;
     if (w.tile_count.cap < 2 * (size_t)n_tiles || !w.tile_count.p) {
@@ -183,7 +181,22 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (!w.spill.p && ensure(ctx, w.spill, 1 << 16)) return SHS_ERR_HIP;
     const int setup_blocks = std::max(1, (n_tris + 255) / 256);
     if (ensure(ctx, w.blk_stat, (size_t)setup_blocks)) return SHS_ERR_HIP;
-    if (upload_draws(ctx, w, w.last_draws)) return SHS_ERR_HIP;
+    // The draw table travels with two int32 arrays appended (as whole 16-B-aligned pseudo records): the
+    // compact tri_base per draw (+ sentinel) and the draw of each setup block's first triangle, so the
+    // kernels' triangle -> draw lookups start from one load instead of a search over the records.
+    const size_t nd = w.last_draws.size();
+    const size_t n_int = (nd + 1) + (size_t)setup_blocks;
+    const size_t n_extra = (n_int * sizeof(int32_t) + sizeof(LibDrawGPU) - 1) / sizeof(LibDrawGPU);
+    std::vector<LibDrawGPU> table(w.last_draws);
+    table.resize(nd + n_extra);
+    int32_t *ints = reinterpret_cast<int32_t *>(table.data() + nd);
+    for (size_t i = 0; i < nd; ++i) ints[i] = w.last_draws[i].tri_base;
+    ints[nd] = n_tris;
+    for (int b = 0, d = 0; b < setup_blocks; ++b) {
+        while (d + 1 < (int)nd && w.last_draws[d + 1].tri_base <= b * 256) ++d;
+        ints[nd + 1 + b] = d;
+    }
+    if (upload_draws(ctx, w, table)) return SHS_ERR_HIP;
 
     fp.tiles_x = tiles_x; fp.tiles_y = tiles_y; fp.rtiles_y = rtiles_y;
     fp.n_tris = n_tris;
@@ -211,7 +224,9 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.draws = w.draws.p; fb.recs = w.recs.p; fb.shade = w.shade.p; fb.boxes = w.boxes.p; fb.xbase = w.xbase.p; fb.zord = w.zord.p;
     fb.tile_count = w.tile_count.p; fb.bins = w.bins.p; fb.spill = w.spill.p; fb.counters = w.counters.p;
     fb.busy = w.busy.p; fb.blk_stat = w.blk_stat.p; fb.rstat = w.rstat.p;
-    fb.clipq = w.clipq.p; fb.bigq = w.bigq.p; fb.bigpre = w.bigpre.p; fb.dbase = w.dbase.p;
+    fb.clipq = w.clipq.p; fb.bigq = w.bigq.p; fb.bigpre = w.bigpre.p;
+    fb.dbase = reinterpret_cast<int32_t *>(w.draws.p + nd);
+    fb.bdraw = fb.dbase + nd + 1;
     fb.bigpart = w.bigpre.p + n_slots + 1;   // BIG_PARTS (256) sums after the prefix
     fb.rqueue = w.rqueue.p;
     if (shadow) {

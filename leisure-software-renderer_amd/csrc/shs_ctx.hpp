@@ -122,7 +122,6 @@ struct shs_ctx {
         DevBuf<uint2> boxes;
         DevBuf<uint32_t> xbase, zord, tile_count, bins, counters, busy, clipq, bigpre;
         DevBuf<uint4> bigq;
-        DevBuf<int32_t> dbase;
         DevBuf<uint32_t> rqueue;
         DevBuf<uint2> spill, blk_stat, rstat;
         shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots

@@ -674,8 +674,8 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
     bool need_clip = false;
     // the block's draw when all its triangles share one (block-uniform: its uniforms come in
     // through scalar loads), else -1 and a per-thread search
-    const int t_first = b * 256, t_last = min(b * 256 + 255, fp.n_tris - 1);
-    const int d_first = lib_find_draw(fb.dbase, fp.n_draws, t_first);
+    const int t_last = min(b * 256 + 255, fp.n_tris - 1);
+    const int d_first = fb.bdraw[b];
     const int d_uni = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : -1;
     if (tri < fp.n_tris) {
         if (d_uni >= 0) {   // two inlined copies: this one sees d_uni as the (scalar) draw
@@ -823,12 +823,6 @@ __global__ __launch_bounds__(256) void k_lib_bigscan(LibFrameParams fp, LibBuffe
         __syncthreads();
     }
     if (blockIdx.x == BIG_PARTS - 1 && tid == 0) fb.bigpre[n] = s_carry;
-}
-
-// Copies draws[i].tri_base into the compact array the triangle -> draw searches read.
-__global__ __launch_bounds__(256) void k_lib_dbase(LibFrameParams fp, LibBuffers fb) {
-    const int i = (int)(blockIdx.x * 256u + threadIdx.x);
-    if (i < fp.n_draws) fb.dbase[i] = fb.draws[i].tri_base;
 }
 
 // The large primitives' (primitive, tile) tasks, a contiguous range per workgroup: busy marks on the
@@ -1684,7 +1678,6 @@ using namespace shs_dev;
 // grids are fixed and stride or split what the counters hold.
 hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, hipStream_t s) {
     const int grid = std::max(1, (fp.n_tris + 255) / 256);
-    hipLaunchKernelGGL(k_lib_dbase, dim3((unsigned)std::max(1, (fp.n_draws + 255) / 256)), dim3(256), 0, s, fp, fb);
     if (shadow) {
         hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     } else {

@@ -130,7 +130,8 @@ struct LibBuffers {
     uint4 *bigq;                     // primitives over SMALL_MARK raster tiles: (slot, bx, by, 0), one per slot
     uint32_t *bigpre;                // k_lib_bigscan: exclusive task prefix of bigq (+ the total)
     uint32_t *bigpart;               // k_lib_bigsum: per-workgroup task sums (BIG_PARTS)
-    int32_t *dbase;                  // k_lib_dbase: draws[i].tri_base, compact (the triangle -> draw search)
+    const int32_t *dbase;            // draws[i].tri_base, compact (+ n_tris): the triangle -> draw search
+    const int32_t *bdraw;            // per setup block: the draw of its first triangle
     uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQ x LIB_QSTRIDE words
 };
 
