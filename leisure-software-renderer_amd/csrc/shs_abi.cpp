@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -330,7 +331,12 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.n_frames = n_frames;
     fp.frame_blocks = std::max(1, fp.setup_blocks + fp.ghost_blocks + fp.clear_blocks);
     // persistent raster grid: one resident wave of workgroups (k_raster runs 4 per CU)
-    const int raster_grid = std::max(1, std::min(fp.n_owned_rt * n_frames, 256 * 4));
+    static const int rbpc = [] {   // timing experiments only: resident k_raster blocks per CU
+        const char *e = std::getenv("SHS_RASTER_PER_CU");
+        const int v = e ? std::atoi(e) : 4;
+        return v >= 1 && v <= 4 ? v : 4;
+    }();
+    const int raster_grid = std::max(1, std::min(fp.n_owned_rt * n_frames, 256 * rbpc));
     if (ensure(ctx, ws.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
     fp.setup_grid = fp.frame_blocks * n_frames;
     if (ctx->want_timeline) {

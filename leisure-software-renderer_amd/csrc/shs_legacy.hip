@@ -284,6 +284,25 @@ __device__ __forceinline__ void mark_busy(const FrameParams &fp, const FrameBuff
     else fb.busy_list[atomicAdd(&cnt[C_BUSY], 1u)] = busy_entry(fp, frame, rt);
 }
 
+// Bin mode: the first append to bin tile t (its counter returned 0) makes the tile's raster rows busy.
+// Exactly one appender sees 0, so the flags are plain stores and no raster tile is listed twice; a
+// row no primitive touches is rastered with no hits (written with the clear values), like a busy
+// tile whose candidates all miss.
+__device__ __forceinline__ void mark_bin_rows(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int frame, int t,
+                                              NewBusy &nb) {
+    const int bx = t % fp.tiles_x, ry0 = (t / fp.tiles_x) * (TILE / RTH);
+#pragma unroll
+    for (int r = 0; r < TILE / RTH; ++r) {
+        const int ry = ry0 + r;
+        if (ry >= fp.rtiles_y) break;
+        const int rt = ry * fp.tiles_x + bx;
+        fb.busy[rt] = fp.epoch;
+        const uint32_t k = atomicAdd(&nb.n, 1u);
+        if (k < (uint32_t)NEW_BUSY_CAP) nb.e[k] = busy_entry(fp, frame, rt);
+        else fb.busy_list[atomicAdd(&cnt[C_BUSY], 1u)] = busy_entry(fp, frame, rt);
+    }
+}
+
 // Block-wide (all threads, after the marks): append the block's collected tiles.
 __device__ __forceinline__ void flush_busy(const FrameBuffers &fb, uint32_t *cnt, NewBusy &nb) {
     __syncthreads();
@@ -606,10 +625,11 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     if (!live) { gx0 = 0; gx1 = -1; gy0 = 0; gy1 = -1; }
     const bool sharded = fp.count > 1;
 
-    // -- busy marks on the raster tiles (32x8) of the bin box (owned bin tiles only), the quad's
-    //    four lanes taking every fourth tile
+    // -- scan mode: busy marks on the raster tiles (32x8) of the bin box (owned bin tiles only), the
+    //    quad's four lanes taking every fourth tile (bin mode marks whole bin tiles at their first
+    //    append, below)
     const int rx0 = gx0 / RTW, rx1 = live ? gx1 / RTW : -1, ry0 = gy0 / RTH, ry1 = live ? gy1 / RTH : -1;
-    const int nrx = rx1 - rx0 + 1, n_rt = live ? nrx * (ry1 - ry0 + 1) : 0;
+    const int nrx = rx1 - rx0 + 1, n_rt = (live && fp.scan_mode) ? nrx * (ry1 - ry0 + 1) : 0;
     if (n_rt > 0 && n_rt <= SMALL_RT) {
         for (int k = q; k < n_rt; k += 4) {
             const int rx = rx0 + k % nrx, ry = ry0 + k / nrx;
@@ -629,7 +649,6 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
             }
         }
     }
-    flush_busy(fb, cnt, nb);
     tl_mark(fb.timeline, blockIdx.x, 2);
 
     // -- bin appends (large scenes): bin tiles of the bin box, two per quad lane
@@ -649,7 +668,11 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
         wave_append<2>(tcount, key, pos);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
-            if (key[k] >= 0) { append_bin(fp, fb, cnt, frame, key[k], pos[k], (uint32_t)tri); ++n_bin; }
+            if (key[k] >= 0) {
+                append_bin(fp, fb, cnt, frame, key[k], pos[k], (uint32_t)tri);
+                ++n_bin;
+                if (pos[k] == 0u) mark_bin_rows(fp, fb, cnt, frame, key[k], nb);
+            }
         uint64_t big = __ballot(n_bt > SMALL_BT && q == 0);
         while (big) {
             const int src = __ffsll((unsigned long long)big) - 1;
@@ -662,7 +685,9 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
                 const int bx = cx0 + k % nx, by = cy0 + k / nx;
                 if (sharded && !owned_bin_tile(fp, bx, by)) continue;
                 const int t = by * fp.tiles_x + bx;
-                append_bin(fp, fb, cnt, frame, t, atomicAdd(&tcount[t], 1u), id);
+                const uint32_t p = atomicAdd(&tcount[t], 1u);
+                append_bin(fp, fb, cnt, frame, t, p, id);
+                if (p == 0u) mark_bin_rows(fp, fb, cnt, frame, t, nb);
                 ++mine;
             }
             for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o);
@@ -670,6 +695,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
             if (lane == src) n_bin += tot;
         }
     }
+    flush_busy(fb, cnt, nb);
     tl_mark(fb.timeline, blockIdx.x, 3);
 
     // -- per-block statistics (no same-address global atomics); one lane per quad counts
