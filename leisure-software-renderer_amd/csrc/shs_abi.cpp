@@ -331,11 +331,16 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.n_frames = n_frames;
     fp.frame_blocks = std::max(1, fp.setup_blocks + fp.ghost_blocks + fp.clear_blocks);
     // persistent raster grid: one resident wave of workgroups (k_raster runs 4 per CU)
-    static const int rbpc = [] {   // timing experiments only: resident k_raster blocks per CU
+    // Resident k_raster workgroups per CU: 4 fill every CU; bin-mode scenes leave one slot so the next
+    // batch's k_setup / k_ghost (setup stream) run beside this raster instead of after it (measured,
+    // C3: 0.76 -> 0.68 ms per 16-frame step; scan-mode C2 is best at 4).  SHS_RASTER_PER_CU overrides
+    // (timing experiments).
+    static const int rbpc_env = [] {
         const char *e = std::getenv("SHS_RASTER_PER_CU");
-        const int v = e ? std::atoi(e) : 4;
-        return v >= 1 && v <= 4 ? v : 4;
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 1 && v <= 4 ? v : 0;
     }();
+    const int rbpc = rbpc_env ? rbpc_env : (fp.scan_mode ? 4 : 3);
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt * n_frames, 256 * rbpc));
     if (ensure(ctx, ws.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
     fp.setup_grid = fp.frame_blocks * n_frames;
