@@ -494,7 +494,9 @@ def cpu_baseline(args):
             lambda: oracle.render_legacy(frame.width, frame.height, draws, threads=threads), args.cpu_seconds / len(legs))
         out[name] = {"threads": threads, "frames": frames, "seconds": round(el, 2), "median_ms_per_frame": round(med, 3),
                      "mtri_s": round(n_tri * frames / el / 1e6, 4), "mpix_s": round(covered * frames / el / 1e6, 3)}
-    head_name = legs[0][0]
+    # the headline is the fastest leg: the baseline the GPU is compared with is the CPU at its best
+    # (hardware_concurrency oversubscribes a host whose process share is smaller than its core count)
+    head_name = max(out, key=lambda k: out[k]["mtri_s"])
     head = out[head_name]
     return {"value": head["mtri_s"], "unit": "Mtri/s", "cores": head["threads"], "kind": "port",
             "median_ms_per_frame": head["median_ms_per_frame"], "mpix_s": head["mpix_s"], "cpu_model": cpu_model(),
