@@ -107,8 +107,10 @@ def test_padded_layout_roundtrip(w, h, count):
     assert np.array_equal(dst_depth.view(np.uint32), depth.view(np.uint32))
 
 
-def _gloo_padded_worker(rank, world, port, q):
-    """The device gather's protocol over gloo: pack (host restatement), gather to rank 0, unpack."""
+def _gloo_padded_worker(rank, world, port, q, present=False):
+    """The device gather's protocol over gloo: pack (host restatement), gather to rank 0, unpack.
+    present: the 4 B/px RGBA8 present staging the sharded bench ships (SHS_TARGET_LIB_PRESENT: rows
+    top-down, so the plane is row-flipped into screen order like the device's tile parameters)."""
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -121,15 +123,18 @@ def _gloo_padded_worker(rank, world, port, q):
         n_tiles = ((w + 31) // 32) * ((h + 31) // 32)
         words = ((n_tiles + world - 1) // world) * 1024
         buf = np.zeros(words, np.uint32)
-        mine = shard.pack_padded([color], w, h, rank, world)
+        rgba = color.view(np.uint8).reshape(h, w, 4)
+        planes = shard.planes_of([(rgba, True)]) if present else [color]
+        mine = shard.pack_padded(planes, w, h, rank, world)
         buf[:mine.size] = mine
         t = torch.from_numpy(buf.view(np.int32))
         if rank == 0:
             bufs = [torch.empty_like(t) for _ in range(world)]
             dist.gather(t, gather_list=bufs, dst=0)
             out = np.zeros_like(color)
+            out_planes = shard.planes_of([(out.view(np.uint8).reshape(h, w, 4), True)]) if present else [out]
             for r in range(world):
-                shard.unpack_padded([out], bufs[r].numpy().view(np.uint32), w, h, r, world)
+                shard.unpack_padded(out_planes, bufs[r].numpy().view(np.uint32), w, h, r, world)
             q.put(bool(np.array_equal(out, color)))
         else:
             dist.gather(t, dst=0)
@@ -138,13 +143,14 @@ def _gloo_padded_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_device_protocol_gather():
+@pytest.mark.parametrize("present", [False, True])
+def test_gloo_device_protocol_gather(present):
     import torch.multiprocessing as mp
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_padded_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gloo_padded_worker, args=(r, world, port, q, present)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
