@@ -321,10 +321,10 @@ static int enqueue_frame(shs_ctx *ctx) {
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;
     fp.setup_blocks = setup_blocks;
-    // Binned (large) scenes list their unbounded slivers in k_setup and enumerate them in k_ghost:
-    // ghost waves would recompute every triangle's record (C3: ~1/3 of k_setup's time).  Scan-mode
-    // scenes keep the ghost waves inside k_setup (one launch fewer).
-    fp.ghost_list = fp.scan_mode ? 0u : 1u;
+    // Binned (large) scenes and batches list their unbounded slivers in k_setup and enumerate them in
+    // k_ghost: ghost waves would recompute every triangle's record (C3: ~1/3 of k_setup's time).  A
+    // single scan-mode frame keeps the ghost waves inside k_setup (one launch fewer on its latency path).
+    fp.ghost_list = (fp.scan_mode && n_frames == 1) ? 0u : 1u;
     fp.ghost_blocks = fp.ghost_list ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
     fp.clear_blocks = 0;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / shs_dev::RTH);

@@ -1173,27 +1173,24 @@ __device__ __forceinline__ void clear_tile(const FrameParams &fp, const FrameBuf
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBuffers &fb, int f, int ry, RasterShared &sh) {
+__device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBuffers &fb, int f, int ry) {
+    // No barrier and no LDS: each thread looks up the busy flag / ownership of the 32-px tile its
+    // 4-px column group lies in and writes that group down the strip's rows.
     const int tid = threadIdx.x;
     const FrameBuffers fv = frame_view(fp, fb, f);
-    __syncthreads();   // sh.skip of the previous strip is no longer read
-    for (int t = tid; t < fp.tiles_x; t += 256)
-        sh.skip[t] = (uint8_t)(fv.busy[ry * fp.tiles_x + t] == fp.epoch ||
-                               (fp.count > 1 && !owned_bin_tile(fp, t, ry / (TILE / RTH))));
-    __syncthreads();
     const int y0 = ry * RTH, y1 = min(y0 + RTH, fp.H);
+    const int by = ry / (TILE / RTH);
     uint32_t *color = reinterpret_cast<uint32_t *>(fv.color);
     if ((fp.W & 3) == 0) {
         const int ng = fp.W >> 2;
         const u32x4 c4 = {fp.clear_rgba, fp.clear_rgba, fp.clear_rgba, fp.clear_rgba};
         const f32x4 d4 = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
-        for (int y = y0; y < y1; ++y) {
-            u32x4 *crow = reinterpret_cast<u32x4 *>(color + (size_t)(fp.H - 1 - y) * fp.W);
-            f32x4 *drow = reinterpret_cast<f32x4 *>(fv.depth + (size_t)y * fp.W);
-            for (int g = tid; g < ng; g += 256) {
-                if (sh.skip[g >> 3]) continue;   // 8 groups of 4 px per 32-px tile
-                __builtin_nontemporal_store(c4, &crow[g]);
-                __builtin_nontemporal_store(d4, &drow[g]);
+        for (int g = tid; g < ng; g += 256) {
+            const int t = g >> 3;   // 8 groups of 4 px per 32-px tile
+            if (fv.busy[ry * fp.tiles_x + t] == fp.epoch || (fp.count > 1 && !owned_bin_tile(fp, t, by))) continue;
+            for (int y = y0; y < y1; ++y) {
+                __builtin_nontemporal_store(c4, &reinterpret_cast<u32x4 *>(color + (size_t)(fp.H - 1 - y) * fp.W)[g]);
+                __builtin_nontemporal_store(d4, &reinterpret_cast<f32x4 *>(fv.depth + (size_t)y * fp.W)[g]);
                 if (fv.present) __builtin_nontemporal_store(c4, &reinterpret_cast<u32x4 *>(fv.present + (size_t)y * fp.W)[g]);
                 if (fv.prequant) {
                     float4 *pq = fv.prequant + (size_t)(fp.H - 1 - y) * fp.W + 4 * g;
@@ -1202,9 +1199,10 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
             }
         }
     } else {
-        for (int y = y0; y < y1; ++y) {
-            for (int x = tid; x < fp.W; x += 256) {
-                if (sh.skip[x >> 5]) continue;
+        for (int x = tid; x < fp.W; x += 256) {
+            const int t = x >> 5;
+            if (fv.busy[ry * fp.tiles_x + t] == fp.epoch || (fp.count > 1 && !owned_bin_tile(fp, t, by))) continue;
+            for (int y = y0; y < y1; ++y) {
                 const size_t c = (size_t)(fp.H - 1 - y) * fp.W + x;
                 __builtin_nontemporal_store(fp.clear_rgba, &color[c]);
                 __builtin_nontemporal_store(FLT_MAX, &fv.depth[(size_t)y * fp.W + x]);
@@ -1214,6 +1212,8 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
         }
     }
 }
+
+constexpr int STRIP_RT = 2;   // raster-tile rows per clear item
 
 // Persistent raster over the whole batch.  Work items are the busy tiles (the busy list k_setup /
 // k_ghost built: latency-bound raster) and the clear strips (one raster-tile row of one frame:
@@ -1255,7 +1255,10 @@ __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers 
 #pragma unroll
     for (int k = 0; k < CAND / 256; ++k) asm volatile("" : "+v"(pbx[k].x), "+v"(pbx[k].y));
     if (tid < min(n_draws_all, LDS_DRAWS) * 4) sh.du[tid] = du_first;
-    const uint32_t n_strips = (uint32_t)(fp.rtiles_y * fp.n_frames);
+    // a strip item clears STRIP_RT raster-tile rows of one frame (fewer items: fewer tickets and
+    // barriers per cleared byte)
+    const int strips_y = (fp.rtiles_y + STRIP_RT - 1) / STRIP_RT;
+    const uint32_t n_strips = (uint32_t)(strips_y * fp.n_frames);
     const uint64_t n_items = (uint64_t)n_strips + n_busy;
     const uint32_t G = gridDim.x, q = blockIdx.x % (uint32_t)N_WORKQ;
     uint32_t *queue = &cnt[C_WORK + WORKQ_STRIDE * q];
@@ -1268,8 +1271,9 @@ __global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers 
         const uint32_t s_lo = (uint32_t)(((uint64_t)item * n_strips) / n_items);
         const uint32_t s_hi = (uint32_t)(((uint64_t)(item + 1) * n_strips) / n_items);
         if (s_hi > s_lo) {
-            const int f = (int)(s_lo / (uint32_t)fp.rtiles_y);
-            clear_strip(fp, fb, f, (int)s_lo - f * fp.rtiles_y, sh);
+            const int f = (int)(s_lo / (uint32_t)strips_y);
+            const int sy = (int)s_lo - f * strips_y;
+            for (int ry = sy * STRIP_RT; ry < min((sy + 1) * STRIP_RT, fp.rtiles_y); ++ry) clear_strip(fp, fb, f, ry);
         } else {
             const uint32_t g = fb.busy_list[item - s_lo];
             const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
