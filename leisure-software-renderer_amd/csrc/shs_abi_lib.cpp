@@ -50,6 +50,9 @@ void release_work(Work &w) {
         for (auto &e : ev)
             if (e) { (void)hipEventDestroy(e); e = nullptr; }
     release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase); release(w.zord);
+    w.dev_table.clear();
+    w.dev_table_at = nullptr;
+    w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
     release(w.spill); release(w.blk_stat); release(w.rstat); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
     for (int i = 0; i < 2; ++i) {
@@ -106,10 +109,15 @@ void build_lib_draw(const shs_lib_draw &in, const Mesh &m, int32_t base, LibDraw
     o.shp[3] = (1.0f < in.shadow_pcf_step) ? in.shadow_pcf_step : 1.0f;
 }
 
-// Upload the draw table through the work's pinned 2-slot staging.
+// Upload the draw table through the work's pinned 2-slot staging.  A table equal to the one the
+// device buffer already holds (a prepared pass re-rendered) is not sent again: the stream-ordered copy
+// is a DMA between two kernels, ~20 us of idle GPU per frame.
 int upload_draws(shs_ctx *ctx, Work &w, const std::vector<LibDrawGPU> &d) {
     const size_t n = std::max<size_t>(d.size(), 1);
     if (ensure(ctx, w.draws, n)) return SHS_ERR_HIP;
+    if (w.dev_table_at == w.draws.p && w.dev_table_cap == w.draws.cap && w.dev_table.size() == d.size() &&
+        (d.empty() || std::memcmp(w.dev_table.data(), d.data(), d.size() * sizeof(LibDrawGPU)) == 0))
+        return SHS_OK;
     const int s = w.slot;
     w.slot ^= 1;
     if (!w.slot_ev[0])
@@ -131,6 +139,9 @@ int upload_draws(shs_ctx *ctx, Work &w, const std::vector<LibDrawGPU> &d) {
     }
     HIP_TRY(ctx, hipEventRecord(w.slot_ev[s], ctx->stream));
     w.slot_used[s] = true;
+    w.dev_table = d;
+    w.dev_table_at = w.draws.p;
+    w.dev_table_cap = w.draws.cap;
     return SHS_OK;
 }
 
@@ -154,7 +165,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
                     ensure(ctx, w.clipq, (size_t)std::max(n_tris, 1))))
         return SHS_ERR_HIP;
     // every slot enters the large-primitive queue at most once
-    if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots + 1 + 256)) return SHS_ERR_HIP;
+    if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots)) return SHS_ERR_HIP;
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count;
     bool reset = gkey != w.geom_key;
     if (w.tile_count.cap < 2 * (size_t)n_tiles || !w.tile_count.p) {
@@ -227,7 +238,6 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.clipq = w.clipq.p; fb.bigq = w.bigq.p; fb.bigpre = w.bigpre.p;
     fb.dbase = reinterpret_cast<int32_t *>(w.draws.p + nd);
     fb.bdraw = fb.dbase + nd + 1;
-    fb.bigpart = w.bigpre.p + n_slots + 1;   // BIG_PARTS (256) sums after the prefix
     fb.rqueue = w.rqueue.p;
     if (shadow) {
         fb.depth = ctx->shadow_map.p;
@@ -343,7 +353,7 @@ void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_cam);
     release_work(ctx->lib_shadow);
     release(ctx->lib_hdr); release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
-    release(ctx->lights); release(ctx->light_proj); release(ctx->depth_ranges);
+    release(ctx->lights); release(ctx->cull_work); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
     release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
     release(ctx->lb_lights); release(ctx->lb_ndc); release(ctx->lb_counts); release(ctx->lb_indices);
@@ -647,11 +657,32 @@ int shs_light_cull(shs_ctx *ctx, const shs_light_cull_desc *d) {
     p.rank = d->shard_rank; p.count = d->shard_count;
     std::memcpy(p.view, d->view, sizeof p.view);
     std::memcpy(p.proj, d->proj, sizeof p.proj);
-    if (ensure(ctx, ctx->light_proj, 2 * (size_t)std::max(ctx->n_lights, 1)) ||
-        ensure(ctx, ctx->depth_ranges, (size_t)p.tiles_x * p.tiles_y) || ensure(ctx, ctx->list_counts, p.n_lists) ||
+    if (ensure(ctx, ctx->depth_ranges, (size_t)p.tiles_x * p.tiles_y) || ensure(ctx, ctx->list_counts, p.n_lists) ||
         ensure(ctx, ctx->list_indices, (size_t)p.n_lists * p.max_per_tile) || ensure(ctx, ctx->lights, 1))
         return SHS_ERR_HIP;
-    HIP_TRY(ctx, shs_internal::launch_light_cull(p, ctx->lights.p, ctx->light_proj.p, ctx->lib_depth.p, ctx->depth_ranges.p,
+    const uint32_t *work = nullptr;
+    uint32_t n_work = p.n_lists;
+    if (p.count > 1 && (32u % p.tile_size) == 0u) {   // tile-sharded: this rank's lists first
+        const shs_dev::LightCullParams &k = ctx->cull_work_key;
+        if (!ctx->cull_work.p || k.W != p.W || k.H != p.H || k.tile_size != p.tile_size || k.n_lists != p.n_lists ||
+            k.rank != p.rank || k.count != p.count) {
+            std::vector<uint32_t> mine, rest;
+            const uint32_t per_slice = p.tiles_x * p.tiles_y;
+            for (uint32_t l = 0; l < p.n_lists; ++l) {
+                const uint32_t rem = l % per_slice;
+                (shs_internal::light_list_owned(p, rem % p.tiles_x, rem / p.tiles_x) ? mine : rest).push_back(l);
+            }
+            ctx->cull_work_owned = (uint32_t)mine.size();
+            mine.insert(mine.end(), rest.begin(), rest.end());
+            if (ensure(ctx, ctx->cull_work, mine.size())) return SHS_ERR_HIP;
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // the previous table may still be read
+            HIP_TRY(ctx, hipMemcpy(ctx->cull_work.p, mine.data(), mine.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            ctx->cull_work_key = p;
+        }
+        work = ctx->cull_work.p;
+        n_work = ctx->cull_work_owned;
+    }
+    HIP_TRY(ctx, shs_internal::launch_light_cull(p, ctx->lights.p, ctx->lib_depth.p, ctx->depth_ranges.p, work, n_work,
                                                  ctx->list_counts.p, ctx->list_indices.p, ctx->stream));
     ctx->cull = p;
     ctx->have_cull = true;

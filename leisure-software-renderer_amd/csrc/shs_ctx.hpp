@@ -135,6 +135,9 @@ struct shs_ctx {
         bool need_check = false, done = false;
         uint64_t st_clip = 0, st_raster = 0, st_covered = 0, st_maxbin = 0, st_spill = 0, st_extra = 0;
         std::vector<shs_dev::LibDrawGPU> last_draws;   // host copies (re-issue on overflow)
+        std::vector<shs_dev::LibDrawGPU> dev_table;    // what w.draws holds (upload skipped when equal)
+        const shs_dev::LibDrawGPU *dev_table_at = nullptr;   // ... at this allocation (pointer, capacity)
+        size_t dev_table_cap = 0;
         shs_dev::LibFrameParams last_fp{};
         // kernel timing (ctx->timing): events before k_lib_setup, between, after k_lib_raster
         static constexpr int RING = 64;
@@ -160,7 +163,9 @@ struct shs_ctx {
     // Forward+ light lists (shs_light.hip)
     DevBuf<shs_dev::CullLight> lights;
     int32_t n_lights = 0;
-    DevBuf<float4> light_proj;
+    DevBuf<uint32_t> cull_work;           // tile-sharded light cull: this rank's lists, then the rest
+    uint32_t cull_work_owned = 0;         // ... how many of them are this rank's
+    shs_dev::LightCullParams cull_work_key{};   // the list geometry / shard cull_work was built for
     DevBuf<float2> depth_ranges;
     DevBuf<uint32_t> list_counts, list_indices;
     shs_dev::LightCullParams cull{};

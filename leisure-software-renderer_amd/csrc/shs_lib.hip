@@ -6,12 +6,16 @@
 // (passes/pass_shadow_map.hpp:144-204).  Paths are relative to
 // /root/reference/cpp-folders/src/shs-renderer-lib/include/shs/.
 //
-// Two launches per pass on one HIP stream:
-//   k_lib_setup   one thread per input triangle: VS x3, trivial accept or Sutherland-Hodgman against
-//                 the six clip planes, fan triangulation, NDC -> screen (rows y-up), area / cull /
-//                 bbox rejects, the per-primitive half of barycentric_2d and the 1/w terms (a 64-B
-//                 record + 112-B premultiplied varyings per primitive), "busy" marks on the 32x8
-//                 raster tiles of its bbox and, for large scenes, per-32x32-tile bin appends.
+// Launches per pass, on one HIP stream:
+//   k_lib_setup   one thread per input triangle: VS x3, trivial accept (or a queue entry for the
+//                 clipper), NDC -> screen (rows y-up), area / cull / bbox rejects, the per-primitive
+//                 half of barycentric_2d and the 1/w terms (a 64-B record + 112-B premultiplied
+//                 varyings per primitive), "busy" marks on the 32x8 raster tiles of its bbox and, for
+//                 large scenes, per-32x32-tile bin appends (block-aggregated in LDS); primitives over
+//                 many tiles go to a pass-wide queue with their task prefix.
+//   k_lib_clip    (camera pass) the queued triangles: Sutherland-Hodgman against the six clip planes
+//                 by 16-lane groups with the polygon in registers, then the fans as above.
+//   k_lib_bigmark the queued large primitives' (primitive, tile) marks / appends over the whole chip.
 //   k_lib_raster  persistent over the owned raster tiles: busy tiles stage their candidates'
 //                 records in LDS and deal every (primitive, pixel) pair to one lane; each passing
 //                 pair atomic-mins a 64-bit key (z01 bits, submission order) into LDS -- identical
@@ -163,71 +167,93 @@ __device__ __forceinline__ float plane_dist(const LVert &v, int p) {   // plane_
     }
 }
 
-// detail::clip_polygon_frustum (:111-164) for the triangles k_lib_setup queues (not trivially inside).
-// The two polygon buffers live in LDS, one column per lane (component-major, lane-minor: no bank
-// conflicts, no scratch); a one-wave workgroup holds 2 x MAX_POLY x 12 x 64 floats.
-constexpr int CLIP_LANES = 64;
-typedef float ClipBuf[2][MAX_POLY][12][CLIP_LANES];
+// detail::clip_polygon_frustum (:111-164) for the triangles k_lib_setup queues (not trivially inside),
+// run by a group of CLIP_G = 16 lanes per triangle with the polygon in registers: lane L holds polygon
+// buffer entry L (polygon vertex j is lane (j + rot) % n).  Per plane every lane evaluates the edge
+// that starts at its vertex (clip_polygon_plane's loop body: 0, 1 or 2 outputs), a scan over the edges
+// in polygon order gives each edge's output position, and every output lane pulls its vertex from the
+// edge that produced it -- the reference's sequential output, vertex for vertex, with no LDS and no
+// scratch.  A plane every vertex is inside of only rotates the polygon by one (each edge emits its end
+// vertex), kept as an index rotation.  Capacity MAX_POLY = CLIP_G: edges whose output position exceeds
+// MAX_POLY - 2 emit nothing (unreachable for a convex polygon: <= 1 vertex added per plane).
+constexpr int CLIP_G = 16;
 
-__device__ __forceinline__ LVert clip_ld(const ClipBuf &B, int cur, int i, int lane) {
+__device__ __forceinline__ float grp_shfl(float v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ int grp_shfl(int v, int src) { return __shfl(v, src, 64); }
+
+__device__ __forceinline__ LVert grp_shfl_v(const LVert &v, int src) {
     LVert o;
+    const float *pv = &v.cx;
     float *po = &o.cx;
 #pragma unroll
-    for (int c = 0; c < 12; ++c) po[c] = B[cur][i][c][lane];
+    for (int c = 0; c < 12; ++c) po[c] = grp_shfl(pv[c], src);
     return o;
 }
 
-__device__ __forceinline__ void clip_st(ClipBuf &B, int cur, int i, int lane, const LVert &v) {
-    const float *pv = &v.cx;
-#pragma unroll
-    for (int c = 0; c < 12; ++c) B[cur][i][c][lane] = pv[c];
-}
-
-// Returns the polygon size (<= MAX_POLY); polygon vertex j is buffer (*cur) entry (j + *rot) % n.
-// A plane that every current vertex is inside of emits the polygon rotated by one (each edge emits
-// its end vertex): that is kept as an index rotation instead of a copy, with the identical result.
-__device__ __forceinline__ int clip_frustum_lds(ClipBuf &B, int lane, const LVert (&tri)[3], int &cur, int &rot) {
+// Returns the polygon size (<= MAX_POLY); v = this lane's buffer vertex, rot as above.  Every lane of
+// the 16-lane group (lanes seg .. seg + 15 of the wave, li = lane - seg) calls it: group-uniform
+// control flow.
+__device__ __forceinline__ int clip_frustum_group(LVert &v, int li, int seg, int &rot) {
+    static_assert(MAX_POLY == CLIP_G, "one polygon vertex per group lane");
     int n = 3;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) clip_st(B, 0, k, lane, tri[k]);
-    cur = 0;
     rot = 0;
     for (int p = 0; p < 6 && n > 0; ++p) {
-        bool all_in = true;
-        for (int i = 0; i < n; ++i) {
-            LVert v;
-            v.cx = B[cur][i][0][lane]; v.cy = B[cur][i][1][lane]; v.cz = B[cur][i][2][lane]; v.cw = B[cur][i][3][lane];
-            all_in = all_in && plane_dist(v, p) >= 0.0f;
-        }
-        if (all_in) {
+        const bool has = li < n;
+        const float da = has ? plane_dist(v, p) : 0.0f;
+        const bool cin = da >= 0.0f;
+        const uint32_t out_mask = (uint32_t)(__ballot(has && !cin) >> seg) & 0xFFFFu;
+        if (out_mask == 0u) {
             rot = rot + 1 == n ? 0 : rot + 1;
             continue;
         }
-        int m = 0;
-        LVert c = clip_ld(B, cur, rot, lane);
-        float da = plane_dist(c, p);
-        for (int i = 0; i < n; ++i) {
-            int j = rot + i + 1;
-            j = j >= n ? j - n : j;
-            const LVert x = clip_ld(B, cur, j, lane);
-            const float db = plane_dist(x, p);
-            const bool cin = da >= 0.0f, xin = db >= 0.0f;
-            if (m > MAX_POLY - 2) break;   // unreachable for a convex polygon (<= 1 vertex added per plane)
+        // the edge (this vertex -> its successor) of clip_polygon_plane
+        const int succ = li + 1 >= n ? 0 : li + 1;
+        const LVert x = grp_shfl_v(v, seg + succ);
+        const float db = grp_shfl(da, seg + succ);
+        const bool xin = db >= 0.0f;
+        int cnt = 0;
+        LVert outA = x;
+        if (has) {
             if (cin && xin) {
-                clip_st(B, cur ^ 1, m++, lane, x);
-            } else if (cin && !xin) {
+                cnt = 1;
+            } else if (cin != xin) {
                 const float denom = da - db;
-                if (fabsf(denom) > 1e-8f) clip_st(B, cur ^ 1, m++, lane, lerp_v(c, x, da / denom));
-            } else if (!cin && xin) {
-                const float denom = da - db;
-                if (fabsf(denom) > 1e-8f) clip_st(B, cur ^ 1, m++, lane, lerp_v(c, x, da / denom));
-                clip_st(B, cur ^ 1, m++, lane, x);
+                const bool ok = fabsf(denom) > 1e-8f;
+                if (ok) outA = lerp_v(v, x, da / denom);
+                cnt = (ok ? 1 : 0) + (xin ? 1 : 0);
             }
-            c = x;
-            da = db;
         }
+        // edges in polygon order: logical edge i starts at lane (i + rot) % n
+        const int phys_of = has ? (li + rot >= n ? li + rot - n : li + rot) : li;
+        const int cl_raw = grp_shfl(cnt, seg + phys_of);
+        const int cl = has ? cl_raw : 0;
+        int incl = cl;
+#pragma unroll
+        for (int o = 1; o < CLIP_G; o <<= 1) {
+            const int u = __shfl_up(incl, o, CLIP_G);
+            if (li >= o) incl += u;
+        }
+        const int excl = incl - cl;
+        const int emit = (has && excl <= MAX_POLY - 2) ? cl : 0;   // the sequential loop's capacity break
+        int m = emit ? excl + emit : 0;
+#pragma unroll
+        for (int o = 1; o < CLIP_G; o <<= 1) m = max(m, __shfl_xor(m, o, CLIP_G));
+        // output k = li: the last logical edge i with excl_i <= k (binary lifting over the monotone
+        // excl; an edge that emits nothing shares its excl with the next one)
+        int src = 0;
+#pragma unroll
+        for (int step = CLIP_G / 2; step >= 1; step >>= 1) {
+            const int cand = src + step;
+            const int e = grp_shfl(excl, seg + (cand < CLIP_G ? cand : CLIP_G - 1));
+            if (cand < n && e <= li) src = cand;
+        }
+        const int e_src = grp_shfl(excl, seg + src);
+        const int p_src = src + rot >= n ? src + rot - n : src + rot;   // the edge's start vertex lane
+        const int p_nxt = p_src + 1 >= n ? 0 : p_src + 1;              // its end vertex lane
+        const LVert a_src = grp_shfl_v(outA, seg + p_src);
+        const LVert x_src = grp_shfl_v(v, seg + p_nxt);
+        if (li < m) v = (li == e_src) ? a_src : x_src;
         n = m;
-        cur ^= 1;
         rot = 0;
     }
     return n;
@@ -267,6 +293,23 @@ __device__ __forceinline__ void lib_mark_range(const LibFrameParams &fp, const L
     }
 }
 
+// The (primitive, tile) tasks of a large primitive: its owned-or-not raster tiles (busy marks) then, in
+// bin mode, its bin tiles (appends).
+__device__ __forceinline__ uint32_t big_tasks(const LibFrameParams &fp, uint4 e, uint32_t &n_busy) {
+    const int x0 = (int)lo16(e.y), x1 = (int)hi16(e.y), y0 = (int)lo16(e.z), y1 = (int)hi16(e.z);
+    n_busy = (uint32_t)((x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1));
+    const uint32_t n_bin = fp.scan_mode ? 0u : (uint32_t)((x1 / TILE - x0 / TILE + 1) * (y1 / TILE - y0 / TILE + 1));
+    return n_busy + n_bin;
+}
+
+// Appends n entries with `tasks` tasks in all to the large-primitive queue: -> (first entry, its task
+// prefix).  One 64-bit atomic: entries and tasks are handed out in the same order.
+__device__ __forceinline__ uint2 bigq_reserve(uint32_t *cnt, uint32_t n, uint32_t tasks) {
+    const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long *>(&cnt[LC_BIGT]),
+                                             ((unsigned long long)n << 32) | (unsigned long long)tasks);
+    return make_uint2((uint32_t)(old >> 32), (uint32_t)old);
+}
+
 // Primitives covering more than SMALL_MARK raster tiles are queued in LDS and marked by the whole
 // setup block after its triangles are done (a floor triangle at 4K spans thousands of tiles).
 constexpr int SMALL_MARK = 8;
@@ -284,7 +327,7 @@ struct Pend {
 };
 struct SetupShared {
     uint4 big[BIG_CAP];       // (slot, bx, by, 0)
-    uint32_t pre[2][BIG_CAP + 1]; // large primitives: first busy-mark task, first bin-append task
+    uint32_t pre[2][BIG_CAP + 1]; // large primitives: task prefix; [1]: queue bases, wave sums
     uint32_t nbig;
     uint32_t stat[2];
     int ub[4];                // union of deferred bin rects: bx0, by0, bx1, by1
@@ -320,13 +363,13 @@ __device__ __forceinline__ void store_box(const LibBuffers &fb, uint32_t slot, i
 // loaded and transformed for primitives that survive the culls.
 // direct (k_lib_clip): marks without the block aggregation -- small boxes marked by the thread, large
 // ones queued for k_lib_bigmark (ss / pend unused).
-template <bool DIRECT = false>
-__device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, const LibDrawGPU &dr, int d,
-                         uint32_t seq, uint32_t slot, LVert a, LVert b, LVert c, uint32_t &n_clip,
-                         uint32_t &n_rast, SetupShared &ss, Pend &pend, const uint32_t *lazy_ids = nullptr) {
-    ++n_clip;
-    LVert *v[3] = {&a, &b, &c};
-    float sx[3], sy[3];
+// The screen-space half of a fan triangle (rasterizer.hpp:255-292): NDC -> screen, the area / cull /
+// bbox rejects (n_rast counts a non-empty bbox) and barycentric_2d's den; in a tile-sharded pass a
+// primitive of <= 2x2 bin tiles on none of this rank's is dropped too.  -> live.
+__device__ __forceinline__ bool fan_screen(const LibFrameParams &fp, const LibDrawGPU &dr, const LVert &a, const LVert &b,
+                                           const LVert &c, float (&sx)[3], float (&sy)[3], int &x0, int &x1, int &y0,
+                                           int &y1, float &den, uint32_t &n_rast) {
+    const LVert *v[3] = {&a, &b, &c};
     bool finite = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -335,9 +378,9 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
         sx[k] = (nx * 0.5f + 0.5f) * (float)(fp.W - 1);
         sy[k] = (ny * 0.5f + 0.5f) * (float)(fp.H - 1);
     }
-    int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+    x0 = 0; x1 = -1; y0 = 0; y1 = -1;
     bool live = false;
-    float den = 0.0f;
+    den = 0.0f;
     if (finite) {
         const float e0x = sx[1] - sx[0], e0y = sy[1] - sy[0], e1x = sx[2] - sx[0], e1y = sy[2] - sy[0];
         const float area2 = e0x * e1y - e0y * e1x;
@@ -367,7 +410,18 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
             live = mine;
         }
     }
-    if (!live) {
+    return live;
+}
+
+template <bool DIRECT = false>
+__device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, const LibDrawGPU &dr, int d,
+                         uint32_t seq, uint32_t slot, LVert a, LVert b, LVert c, uint32_t &n_clip,
+                         uint32_t &n_rast, SetupShared &ss, Pend &pend, const uint32_t *lazy_ids = nullptr) {
+    ++n_clip;
+    LVert *v[3] = {&a, &b, &c};
+    float sx[3], sy[3], den;
+    int x0, x1, y0, y1;
+    if (!fan_screen(fp, dr, a, b, c, sx, sy, x0, x1, y0, y1, den, n_rast)) {
         store_box(fb, slot, 0, -1, 0, -1);
         return;
     }
@@ -402,8 +456,15 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     if (fp.exp_flags & 2u) return;
     if (DIRECT) {
         const int n_rt = (x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1);
-        if (n_rt > SMALL_MARK) fb.bigq[atomicAdd(&cnt[LC_BIGQ], 1u)] = make_uint4(slot, pack16(x0, x1), pack16(y0, y1), 0u);
-        else lib_mark_range(fp, fb, cnt, x0, x1, y0, y1, slot, 0, 1);
+        if (n_rt > SMALL_MARK) {
+            const uint4 e = make_uint4(slot, pack16(x0, x1), pack16(y0, y1), 0u);
+            uint32_t nb;
+            const uint2 at = bigq_reserve(cnt, 1u, big_tasks(fp, e, nb));
+            fb.bigq[at.x] = e;
+            fb.bigpre[at.x] = at.y;
+        } else {
+            lib_mark_range(fp, fb, cnt, x0, x1, y0, y1, slot, 0, 1);
+        }
     } else {
         lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot, ss, pend);
     }
@@ -426,11 +487,13 @@ __device__ __forceinline__ bool read_tri(const LibDrawGPU &dr, int local, uint32
     return id[0] < (uint32_t)dr.n_verts && id[1] < (uint32_t)dr.n_verts && id[2] < (uint32_t)dr.n_verts;
 }
 
-// Tile-sharded camera pass: can the clipped fans of a triangle that is not trivially inside land on
-// one of this rank's 32x32 tiles?  With every corner in front of the eye (w > 0) the clipped polygon
-// lies inside the triangle, whose projection is the 2D triangle of the projected corners: its bbox
-// (2 px of margin for the clipper's rounding), clamped to the screen, bounds every fan.  A corner
-// behind the eye gives no such bound (true).
+// Can the clipped fans of a triangle that is not trivially inside land on the screen (and, tile-sharded,
+// on one of this rank's 32x32 tiles)?  With every corner in front of the eye (w > 0) the clipped
+// polygon lies inside the triangle, whose projection is the 2D triangle of the projected corners: its
+// bbox (2 px of margin for the clipper's rounding), clamped to the screen, bounds every fan.  A bbox
+// more than 2 px off one screen edge puts every corner outside that edge's plane (margin 4 / (W - 1)
+// in NDC), so the reference's clipper returns an empty polygon and counts nothing.  A corner behind
+// the eye gives no such bound (true).
 __device__ __forceinline__ bool clip_reaches_rank(const LibFrameParams &fp, const LVert (&t)[3]) {
     if (!(t[0].cw > 0.0f && t[1].cw > 0.0f && t[2].cw > 0.0f)) return true;
     float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
@@ -472,7 +535,7 @@ __device__ __forceinline__ bool setup_camera_tri(const LibFrameParams &fp, const
         emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast, ss, pend, id);
         return false;
     }
-    if (fp.count > 1 && !clip_reaches_rank(fp, t)) {   // tile-sharded: no fan can land on an owned tile
+    if (!clip_reaches_rank(fp, t)) {   // off screen, or (tile-sharded) no fan can land on an owned tile
         store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
         return false;
     }
@@ -629,19 +692,46 @@ __device__ int setup_deferred(const LibFrameParams &fp, const LibBuffers &fb, ui
 // The block's large primitives go to the pass-wide queue that k_lib_bigmark spreads over the chip
 // (a floor triangle at 4K spans thousands of raster tiles; a few blocks holding all of them were the
 // setup's critical path).  Block-uniform; one atomic per block.
-__device__ __forceinline__ uint32_t setup_flush_big(const LibBuffers &fb, uint32_t *cnt, SetupShared &ss, int tid) {
+__device__ __forceinline__ uint32_t setup_flush_big(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt,
+                                                    SetupShared &ss, int tid) {
     const uint32_t nbig = min(ss.nbig, (uint32_t)BIG_CAP);
-    if (nbig > 0) {
-        if (tid == 0) ss.pre[0][0] = atomicAdd(&cnt[LC_BIGQ], nbig);
+    if (nbig > 0) {   // block-uniform: the entries' task prefix in LDS, then one reservation
+        static_assert(BIG_CAP == 2 * 256, "two queue entries per thread");
+        uint32_t nb;
+        const uint32_t i0 = 2u * (uint32_t)tid;
+        const uint32_t t0 = i0 < nbig ? big_tasks(fp, ss.big[i0], nb) : 0u;
+        const uint32_t t1 = i0 + 1 < nbig ? big_tasks(fp, ss.big[i0 + 1], nb) : 0u;
+        const int lane = tid & 63, wave = tid >> 6;
+        uint32_t incl = t0 + t1;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) ss.pre[1][2 + wave] = incl;
         __syncthreads();
-        const uint32_t base = ss.pre[0][0];
-        for (uint32_t i = (uint32_t)tid; i < nbig; i += 256) fb.bigq[base + i] = ss.big[i];
+        uint32_t off = 0;
+        for (int w = 0; w < wave; ++w) off += ss.pre[1][2 + w];
+        const uint32_t ex = off + incl - (t0 + t1);
+        if (i0 < nbig) ss.pre[0][i0] = ex;
+        if (i0 + 1 < nbig) ss.pre[0][i0 + 1] = ex + t0;
+        if (tid == 255) {
+            const uint2 at = bigq_reserve(cnt, nbig, off + incl);
+            ss.pre[1][0] = at.x;
+            ss.pre[1][1] = at.y;
+        }
+        __syncthreads();
+        const uint32_t base = ss.pre[1][0], tbase = ss.pre[1][1];
+        for (uint32_t i = (uint32_t)tid; i < nbig; i += 256) {
+            fb.bigq[base + i] = ss.big[i];
+            fb.bigpre[base + i] = tbase + ss.pre[0][i];
+        }
     }
     return nbig;
 }
 
 // Appends the lanes with `pred` to a queue: one atomic per wave; every lane of the wave calls it.
-__device__ __forceinline__ void wave_append(uint32_t *counter, uint32_t *queue, bool pred, uint32_t value) {
+template <typename T>
+__device__ __forceinline__ void wave_append(uint32_t *counter, T *queue, bool pred, T value) {
     const uint64_t m = __ballot(pred);
     if (m == 0ull) return;
     const int lane = __lane_id();
@@ -651,15 +741,9 @@ __device__ __forceinline__ void wave_append(uint32_t *counter, uint32_t *queue, 
     if (pred) queue[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = value;
 }
 
-template <bool SHADOW>
-__global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
-    __shared__ SetupShared ss;
-    const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
-    uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    const bool stl = fb.stimeline != nullptr && tid == 0;
-    const uint64_t st0 = stl ? tl_now() : 0ull;
+// Setup workgroup start: LDS state, and the next frame's counter set, raster queues and bin counts zeroed.
+__device__ __forceinline__ void setup_prologue(const LibFrameParams &fp, const LibBuffers &fb, SetupShared &ss, int b, int tid) {
     setup_shared_init(ss, tid);
-    // zero the other counter set, raster queues and bin counts for the next frame
     if (b == 0 && tid < LC_N) fb.counters[(fp.parity ^ 1u) * LC_N + tid] = 0u;
     if (b == 0 && tid < LIB_NQ) fb.rqueue[((fp.parity ^ 1u) * LIB_NQ + tid) * LIB_QSTRIDE] = 0u;
     {
@@ -668,16 +752,32 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
         for (int t = b * 256 + tid; t < n_bt; t += (int)gridDim.x * 256) next_count[t] = 0u;
     }
     __syncthreads();
+}
+
+// SHS_SETUP_WAVES (timing experiments): a minimum waves-per-SIMD bound for k_lib_setup.
+#ifdef SHS_SETUP_WAVES
+#define SHS_SETUP_BOUNDS __launch_bounds__(256, SHS_SETUP_WAVES)
+#else
+#define SHS_SETUP_BOUNDS __launch_bounds__(256)
+#endif
+template <bool SHADOW>
+__global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
+    __shared__ SetupShared ss;
+    const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
+    uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const bool stl = fb.stimeline != nullptr && tid == 0;
+    const uint64_t st0 = stl ? tl_now() : 0ull;
+    setup_prologue(fp, fb, ss, b, tid);
     const int tri = b * 256 + tid;
     uint32_t n_clip = 0, n_rast = 0;
     Pend pend;
     bool need_clip = false;
-    // the block's draw when all its triangles share one (block-uniform: its uniforms come in
-    // through scalar loads), else -1 and a per-thread search
-    const int t_last = min(b * 256 + 255, fp.n_tris - 1);
-    const int d_first = fb.bdraw[b];
-    const int d_uni = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : -1;
     if (tri < fp.n_tris) {
+        // the block's draw when all its triangles share one (block-uniform: its uniforms come in
+        // through scalar loads), else -1 and a per-thread search
+        const int t_last = min(b * 256 + 255, fp.n_tris - 1);
+        const int d_first = fb.bdraw[b];
+        const int d_uni = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : -1;
         if (d_uni >= 0) {   // two inlined copies: this one sees d_uni as the (scalar) draw
             if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, d_uni);
             else need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, d_uni);
@@ -693,7 +793,7 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
     const int uwh = setup_deferred(fp, fb, cnt, ss, pend, tid);
     if (stl) fb.stimeline[(size_t)b * STL_STRIDE + 5] = (uint64_t)uwh;
     const uint64_t st2 = stl ? tl_now() : 0ull;
-    const uint32_t nbig = setup_flush_big(fb, cnt, ss, tid);
+    const uint32_t nbig = setup_flush_big(fp, fb, cnt, ss, tid);
     if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(ss.stat[0], ss.stat[1]);
     if (fb.stimeline) {
         __syncthreads();
@@ -705,47 +805,56 @@ __global__ __launch_bounds__(256) void k_lib_setup(LibFrameParams fp, LibBuffers
 }
 
 // The camera pass's queued triangles (k_lib_setup: not trivially inside): Sutherland-Hodgman against
-// the 6 planes and the fans (rasterizer.hpp:241-328), one lane per triangle, one-wave workgroups
-// striding the queue; the polygons live in LDS.  Same slots, submission order (tri * 16 + fan), marks
-// and counters as the reference's per-triangle clip.
-__global__ __launch_bounds__(CLIP_LANES) void k_lib_clip(LibFrameParams fp, LibBuffers fb) {
-    __shared__ ClipBuf B;
+// the 6 planes and the fans (rasterizer.hpp:241-328), one 16-lane group per triangle striding the
+// queue, the fans emitted in parallel (lane k: fan k).  Same slots, submission order (tri * 16 + fan),
+// marks and counters as the reference's per-triangle clip.
+__global__ __launch_bounds__(256) void k_lib_clip(LibFrameParams fp, LibBuffers fb) {
     __shared__ SetupShared ss_unused;   // emit_fan<true> marks directly
-    const int lane = (int)threadIdx.x;
+    const int lane = __lane_id(), li = lane & (CLIP_G - 1), seg = lane & ~(CLIP_G - 1);
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
     const uint32_t n = cnt[LC_CLIPQ];
     uint32_t n_clip = 0, n_rast = 0;
     Pend pend;
-    for (uint32_t q = blockIdx.x * CLIP_LANES + (uint32_t)lane; q < n; q += gridDim.x * CLIP_LANES) {
+    const uint32_t groups = gridDim.x * (256 / CLIP_G);
+    for (uint32_t q = blockIdx.x * (256 / CLIP_G) + threadIdx.x / CLIP_G; q < n; q += groups) {   // group-uniform
         const int tri = (int)fb.clipq[q];
         const int d = lib_find_draw(fb.dbase, fp.n_draws, tri);
         const LibDrawGPU &dr = fb.draws[d];
         uint32_t id[3];
         (void)read_tri(dr, tri - dr.tri_base, id);   // in range: checked by k_lib_setup
-        const LVert t[3] = {vertex_out(dr, id[0]), vertex_out(dr, id[1]), vertex_out(dr, id[2])};
-        const uint32_t seq0 = (uint32_t)tri * 16u;
-        int cur = 0, rot = 0;
-        const int m = clip_frustum_lds(B, lane, t, cur, rot);
+        LVert v{};
+        if (li < 3) v = vertex_out(dr, id[li]);
+        int rot = 0;
+        const int m = clip_frustum_group(v, li, seg, rot);
         if (m < 3) {
-            store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+            if (li == 0) store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
             continue;
         }
         uint32_t xb = 0;
         if (m > 3) {   // fans 1 .. m-3 take consecutive extra slots
-            const uint32_t e = atomicAdd(&cnt[LC_EXTRA], (uint32_t)(m - 3));
-            if (e + (uint32_t)(m - 3) > fp.extra_cap) {
-                atomicOr(&cnt[LC_OVERFLOW], LOV_EXTRA);
-                store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+            int e = 0;
+            if (li == 0) e = (int)atomicAdd(&cnt[LC_EXTRA], (uint32_t)(m - 3));
+            e = grp_shfl(e, seg);
+            if ((uint32_t)e + (uint32_t)(m - 3) > fp.extra_cap) {
+                if (li == 0) {
+                    atomicOr(&cnt[LC_OVERFLOW], LOV_EXTRA);
+                    store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
+                }
                 continue;
             }
-            xb = (uint32_t)fp.n_tris + e;
-            fb.xbase[tri] = xb;
+            xb = (uint32_t)fp.n_tris + (uint32_t)e;
+            if (li == 0) fb.xbase[tri] = xb;
         }
-        auto at = [&](int j) { j += rot; return clip_ld(B, cur, j >= m ? j - m : j, lane); };
-        const LVert p0 = at(0);
-        for (int k = 1; k + 1 < m; ++k) {
+        // fan k = (p0, p_k, p_k+1) on lane k; polygon vertex j is lane (j + rot) % m
+        const int k = li;
+        const int l1 = k + rot >= m ? k + rot - m : k + rot;
+        const int l2 = l1 + 1 >= m ? 0 : l1 + 1;
+        const LVert p0 = grp_shfl_v(v, seg + rot);
+        const LVert pk = grp_shfl_v(v, seg + (k < m ? l1 : 0));
+        const LVert pk1 = grp_shfl_v(v, seg + (k < m ? l2 : 0));
+        if (k >= 1 && k + 1 < m) {
             const uint32_t slot = k == 1 ? (uint32_t)tri : xb + (uint32_t)(k - 2);
-            emit_fan<true>(fp, fb, cnt, dr, d, seq0 + (uint32_t)(k - 1), slot, p0, at(k), at(k + 1), n_clip, n_rast,
+            emit_fan<true>(fp, fb, cnt, dr, d, (uint32_t)tri * 16u + (uint32_t)(k - 1), slot, p0, pk, pk1, n_clip, n_rast,
                            ss_unused, pend);
         }
     }
@@ -757,72 +866,6 @@ __global__ __launch_bounds__(CLIP_LANES) void k_lib_clip(LibFrameParams fp, LibB
         atomicAdd(&fb.blk_stat[0].x, n_clip);
         atomicAdd(&fb.blk_stat[0].y, n_rast);
     }
-}
-
-// Exclusive task prefix of the large-primitive queue: per primitive its owned-or-not raster tiles
-// (busy marks) then, in bin mode, its bin tiles (appends).  One workgroup.
-__device__ __forceinline__ uint32_t big_tasks(const LibFrameParams &fp, uint4 e, uint32_t &n_busy) {
-    const int x0 = (int)lo16(e.y), x1 = (int)hi16(e.y), y0 = (int)lo16(e.z), y1 = (int)hi16(e.z);
-    n_busy = (uint32_t)((x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1));
-    const uint32_t n_bin = fp.scan_mode ? 0u : (uint32_t)((x1 / TILE - x0 / TILE + 1) * (y1 / TILE - y0 / TILE + 1));
-    return n_busy + n_bin;
-}
-
-// The queue is split into BIG_PARTS contiguous ranges: k_lib_bigsum sums each range's tasks,
-// k_lib_bigscan offsets each range by the sums before it and scans it (two parallel launches).
-constexpr int BIG_PARTS = 256;
-
-__device__ __forceinline__ uint32_t block_sum256(uint32_t v, uint32_t *s_wave) {
-    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_down((int)v, o);
-    if (__lane_id() == 0) s_wave[threadIdx.x >> 6] = v;
-    __syncthreads();
-    const uint32_t t = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-    __syncthreads();
-    return t;
-}
-
-__global__ __launch_bounds__(256) void k_lib_bigsum(LibFrameParams fp, LibBuffers fb) {
-    __shared__ uint32_t s_wave[4];
-    const uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    const uint32_t n = cnt[LC_BIGQ];
-    const uint32_t per = (n + BIG_PARTS - 1) / BIG_PARTS;
-    const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
-    uint32_t v = 0, nb;
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += 256) v += big_tasks(fp, fb.bigq[i], nb);
-    const uint32_t t = block_sum256(v, s_wave);
-    if (threadIdx.x == 0) fb.bigpart[blockIdx.x] = t;
-}
-
-__global__ __launch_bounds__(256) void k_lib_bigscan(LibFrameParams fp, LibBuffers fb) {
-    __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_carry;
-    const uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    const uint32_t n = cnt[LC_BIGQ];
-    const uint32_t per = (n + BIG_PARTS - 1) / BIG_PARTS;
-    const uint32_t i0 = blockIdx.x * per, i1 = min(n, i0 + per);
-    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t before = block_sum256(tid < (int)blockIdx.x ? fb.bigpart[tid] : 0u, s_wave);
-    if (tid == 0) s_carry = before;
-    __syncthreads();
-    for (uint32_t base = i0; base < i1; base += 256) {   // block-uniform
-        const uint32_t i = base + (uint32_t)tid;
-        uint32_t nb;
-        const uint32_t v = i < i1 ? big_tasks(fp, fb.bigq[i], nb) : 0u;
-        uint32_t incl = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = (uint32_t)__shfl_up((int)incl, o);
-            if (lane >= o) incl += u;
-        }
-        if (lane == 63) s_wave[wave] = incl;
-        __syncthreads();
-        uint32_t off = s_carry;
-        for (int w = 0; w < wave; ++w) off += s_wave[w];
-        if (i < i1) fb.bigpre[i] = off + incl - v;
-        __syncthreads();
-        if (tid == 255) s_carry = off + incl;
-        __syncthreads();
-    }
-    if (blockIdx.x == BIG_PARTS - 1 && tid == 0) fb.bigpre[n] = s_carry;
 }
 
 // The large primitives' (primitive, tile) tasks, a contiguous range per workgroup: busy marks on the
@@ -837,7 +880,7 @@ __global__ __launch_bounds__(256) void k_lib_bigmark(LibFrameParams fp, LibBuffe
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
     const uint32_t n = cnt[LC_BIGQ];
     if (n == 0u) return;
-    const uint32_t total = fb.bigpre[n];
+    const uint32_t total = cnt[LC_BIGT];
     const uint32_t per = (total + gridDim.x - 1u) / gridDim.x;
     const uint32_t t0 = blockIdx.x * per, t1 = min(total, t0 + per);
     const int tid = (int)threadIdx.x;
@@ -854,7 +897,7 @@ __global__ __launch_bounds__(256) void k_lib_bigmark(LibFrameParams fp, LibBuffe
         }
         __syncthreads();
         const uint32_t e0 = s_lo, m = min((uint32_t)BIG_WIN, n - e0);
-        for (uint32_t i = (uint32_t)tid; i <= m; i += 256) s_pre[i] = fb.bigpre[e0 + i];
+        for (uint32_t i = (uint32_t)tid; i <= m; i += 256) s_pre[i] = e0 + i < n ? fb.bigpre[e0 + i] : total;
         for (uint32_t i = (uint32_t)tid; i < m; i += 256) s_e[i] = fb.bigq[e0 + i];
         __syncthreads();
         const uint32_t w1 = min(t1, s_pre[m]);   // the tasks this window covers
@@ -1674,7 +1717,7 @@ namespace shs_internal {
 using namespace shs_dev;
 
 // k_lib_setup, then (camera pass) k_lib_clip over the queued triangles, then the large primitives'
-// marks (k_lib_bigscan + k_lib_bigmark).  The queue lengths stay on the device: the later kernels'
+// marks (k_lib_bigmark).  The queue lengths stay on the device: the later kernels'
 // grids are fixed and stride or split what the counters hold.
 hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, hipStream_t s) {
     const int grid = std::max(1, (fp.n_tris + 255) / 256);
@@ -1682,10 +1725,8 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
         hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     } else {
         hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
-        hipLaunchKernelGGL(k_lib_clip, dim3(std::min(grid * 4, 1024)), dim3(CLIP_LANES), 0, s, fp, fb);
+        hipLaunchKernelGGL(k_lib_clip, dim3(std::min((grid + 15) / 16, 1024)), dim3(256), 0, s, fp, fb);
     }
-    hipLaunchKernelGGL(k_lib_bigsum, dim3(BIG_PARTS), dim3(256), 0, s, fp, fb);
-    hipLaunchKernelGGL(k_lib_bigscan, dim3(BIG_PARTS), dim3(256), 0, s, fp, fb);
     hipLaunchKernelGGL(k_lib_bigmark, dim3(1024), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }

@@ -82,8 +82,12 @@ constexpr uint32_t LF_MOTION = 4u;      // motion buffer written (per draw: enab
 constexpr uint32_t LF_GRADIENT = 8u;    // PassPBRForward's no-sky background gradient, else clear[]
 
 // counters[] (two parity sets, frame f uses set f & 1, k_lib_setup zeroes the other)
-// LC_CLIPQ: input triangles queued for k_lib_clip; LC_BIGQ: primitives queued for k_lib_bigmark
-constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGQ = 4, LC_N = 5;
+// LC_CLIPQ: input triangles queued for k_lib_clip; LC_BIGT / LC_BIGQ: the large-primitive queue's
+// (primitive, tile) task total and length, one 64-bit word (tasks low, entries high) so that one
+// atomicAdd hands an appender both bases and the queue's task prefix stays monotone; LC_N even keeps
+// the second parity set's word 8-B aligned.
+constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT = 4, LC_BIGQ = 5, LC_N = 6;
+static_assert(LC_BIGQ == LC_BIGT + 1 && LC_BIGT % 2 == 0 && LC_N % 2 == 0, "64-bit big-queue word");
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
 struct LibFrameParams {
@@ -128,8 +132,7 @@ struct LibBuffers {
     uint64_t *stimeline;             // SHS_OPT_TIMELINE (camera pass): STL_STRIDE per setup workgroup
     uint32_t *clipq;                 // input triangles that need clipping (camera pass), n_tris capacity
     uint4 *bigq;                     // primitives over SMALL_MARK raster tiles: (slot, bx, by, 0), one per slot
-    uint32_t *bigpre;                // k_lib_bigscan: exclusive task prefix of bigq (+ the total)
-    uint32_t *bigpart;               // k_lib_bigsum: per-workgroup task sums (BIG_PARTS)
+    uint32_t *bigpre;                // exclusive task prefix of bigq (written with the entries)
     const int32_t *dbase;            // draws[i].tri_base, compact (+ n_tris): the triangle -> draw search
     const int32_t *bdraw;            // per setup block: the draw of its first triangle
     uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQ x LIB_QSTRIDE words

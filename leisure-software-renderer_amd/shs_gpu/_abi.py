@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libshs_gpu.so")
+# SHS_GPU_LIB: another in-tree build of the library (timing experiments with compile-time variants)
+LIB_PATH = os.environ.get("SHS_GPU_LIB") or os.path.join(HERE, "libshs_gpu.so")
 
 SHS_OK = 0
 SHS_ERR_INVALID = -1

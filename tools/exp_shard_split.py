@@ -1,6 +1,6 @@
 """Per-rank work of the tile-sharded C4 / C5 frame, measured on ONE GPU by rendering each rank's shard
 in turn (shard_rank / shard_count): the Amdahl inputs for the N-GPU projection.
-usage (GPU box): python tools/exp_shard_split.py [c4|c5] [frames]"""
+usage (GPU box): python tools/exp_shard_split.py [c4|c5] [frames] [N list, e.g. 1,2,4,8]"""
 import os
 import sys
 import time
@@ -16,6 +16,7 @@ from shs_gpu import scene_lib  # noqa: E402
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
     nf = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    ns = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 2, 4, 8]
     ctx = shs_gpu.Context(0)
     if cfg == "c4":
         frame, draws, lights, cull = scene_lib.c4_scene(3840, 2160)
@@ -24,7 +25,7 @@ def main():
         frame, draws, casters, sun, S = scene_lib.c5_scene(3840, 2160, 2048)
         lvp = ctx.render_shadow_map(S, sun, casters)
         scene_lib.wire_shadow(draws, lvp)
-    for N in (1, 2, 4, 8):
+    for N in ns:
         per_rank = []
         for r in range(N):
             frame.shard_rank, frame.shard_count = r, N
