@@ -1109,10 +1109,20 @@ __device__ __forceinline__ void point_light(const PLight &L, f3 world, f3 N, f3 
     lit = add3(lit, add3(mul3(base, sc3(rad, ndotl)), sc3(rad, spec)));
 }
 
+// The light lists of the raster tile being resolved, staged in LDS (k_lib_raster, tile lists only):
+// list hdr[4 + s] holds hdr[s] (already capped at max_per_tile) indices at ids[s * LT_STAGE_CAP ..].
+constexpr int LT_STAGE_CAP = 256, LT_STAGE_MAX = 4;
+struct LtStage {
+    const uint32_t *ids = nullptr;
+    const uint32_t *hdr = nullptr;
+    int n = 0;
+};
+
 // Forward+ program: the pixel's light list (fp_stress_scene.frag:644-685 selection: a saturated list
 // falls back to every light) through PointLightModel::sample, combined as the software light-culling
 // demo does (hello_light_types_culling_sw.cpp:404-416): ambient hemisphere + sum, clamped to [0,1].
-__device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, int px, int py) {
+__device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, int px, int py,
+                           const LtStage &st) {
     const f3 N = normalize3(nrm);
     f3 V = sub3(f3{dr.cam[0], dr.cam[1], dr.cam[2]}, world);
     const float vl2 = dot3(V, V);
@@ -1132,11 +1142,20 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
         const float zi = g_clamp(floorf(t * (float)fp.lt_zs), 0.0f, (float)(fp.lt_zs - 1u));
         list = ((uint32_t)zi * fp.lt_ty + ty) * fp.lt_tx + tx;
     }
-    const uint32_t count = fp.lt_mode == 0u ? maxp : min(fb.tile_counts[list], maxp);
     const bool lds = fp.n_lights <= (uint32_t)LIB_LDS_LIGHTS;   // k_lib_raster staged them
+    int s_st = -1;
+    for (int s = 0; s < st.n; ++s)
+        if (st.hdr[LT_STAGE_MAX + s] == list) s_st = s;
+    const uint32_t count = s_st >= 0 ? st.hdr[s_st] : fp.lt_mode == 0u ? maxp : min(fb.tile_counts[list], maxp);
     if (count >= maxp) {
         for (uint32_t i = 0; i < fp.n_lights; ++i)
             point_light(lds ? plight_lds(i) : plight_global(fb.lights[i]), world, N, V, base, lit);
+    } else if (s_st >= 0) {   // the list in LDS
+        const uint32_t *ids = st.ids + s_st * LT_STAGE_CAP;
+        for (uint32_t i = 0; i < count; ++i) {
+            const uint32_t idx = ids[i];
+            if (idx < fp.n_lights) point_light(lds ? plight_lds(idx) : plight_global(fb.lights[idx]), world, N, V, base, lit);
+        }
     } else {
         // the next index is loaded while the current light is evaluated
         const uint32_t *ids = fb.tile_indices + (size_t)list * maxp;
@@ -1152,9 +1171,9 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
 
 // The builtin fragment programs (builtin_shaders.hpp:105-245); no base_color_tex -> albedo_tex = 1.
 __device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, float depth01,
-                           int px, int py) {
+                           int px, int py, const LtStage &st) {
     const f3 bc = {dr.base[0], dr.base[1], dr.base[2]};
-    if (dr.program == 5) return forward_plus(fp, fb, dr, world, nrm, px, py);
+    if (dr.program == 5) return forward_plus(fp, fb, dr, world, nrm, px, py, st);
     if (dr.program == 2) return bc;                                                   // debug albedo
     if (dr.program == 3) return add3(sc3(normalize3(nrm), 0.5f), f3{0.5f, 0.5f, 0.5f});  // debug normal
     if (dr.program == 4) {                                                            // debug depth
@@ -1251,13 +1270,14 @@ __device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
 }
 
 __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
-                                         const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv);
+                                         const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv,
+                                         const LtStage &st);
 
 // Resolve one pixel of a tile (one thread): the winner of the key array is re-evaluated with the
 // identical arithmetic, shaded and written; pixels without a winner get the clear values.
 template <bool SHADOW>
 __device__ __forceinline__ void lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, unsigned long long key, int px,
-                                            int py, bool &covered) {
+                                            int py, bool &covered, const LtStage &st = LtStage{}) {
     covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
     if (px >= fp.W || py >= fp.H) return;
     const size_t o = (size_t)py * fp.W + px;
@@ -1276,8 +1296,8 @@ __device__ __forceinline__ void lib_resolve(const LibFrameParams &fp, const LibB
         const LibShade s = fb.shade[slot];
         // a wave whose covered pixels share one draw reads its uniforms with scalar loads
         const int d0 = __builtin_amdgcn_readfirstlane(s.draw);
-        if (__ballot(s.draw != d0) == 0) shade_px(fp, fb, fb.draws[d0], r, s, px, py, color, depth, mv);
-        else shade_px(fp, fb, fb.draws[s.draw], r, s, px, py, color, depth, mv);
+        if (__ballot(s.draw != d0) == 0) shade_px(fp, fb, fb.draws[d0], r, s, px, py, color, depth, mv, st);
+        else shade_px(fp, fb, fb.draws[s.draw], r, s, px, py, color, depth, mv, st);
     }
     fb.hdr[o] = color;
     if (fp.flags & LF_DEPTH) {
@@ -1289,7 +1309,8 @@ __device__ __forceinline__ void lib_resolve(const LibFrameParams &fp, const LibB
 // The winner of one pixel: identical re-evaluation of the pixel test, the varyings, motion and the
 // fragment program (rasterizer.hpp:341-419).
 __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
-                                         const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv) {
+                                         const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv,
+                                         const LtStage &st) {
     {
         float z01, u, v, w, idn;
         lib_test<false>(fp, r, px, py, z01, u, v, w, idn);
@@ -1316,7 +1337,7 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
                 mv = make_float2(vx, vy);
             }
         }
-        const f3 c = lib_fragment(fp, fb, dr, world, nrm, z01, px, py);
+        const f3 c = lib_fragment(fp, fb, dr, world, nrm, z01, px, py, st);
         color = make_float4(c.x, c.y, c.z, 1.0f);
     }
 }
@@ -1603,6 +1624,34 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     }
     __syncthreads();
     const uint64_t t_res = tlon ? tl_now() : 0ull;
+    // Forward+ tile lists: the (<= LT_STAGE_MAX) light lists under this raster tile go to LDS (the
+    // candidate-list arrays are free now), so the per-light index loads of the resolve hit LDS
+    LtStage st;
+    if (!SHADOW && fb.tile_counts && (fp.lt_mode == 1u || fp.lt_mode == 2u) && fp.lt_maxp <= (uint32_t)LT_STAGE_CAP &&
+        X0 < fp.W && Y0 < fp.H) {   // block-uniform
+        const uint32_t ts = fp.lt_size;
+        const int tx0 = min((uint32_t)X0 / ts, fp.lt_tx - 1u), tx1 = min((uint32_t)min(X1, fp.W - 1) / ts, fp.lt_tx - 1u);
+        const int ty0 = min((uint32_t)(fp.H - 1 - min(Y1, fp.H - 1)) / ts, fp.lt_ty - 1u);
+        const int ty1 = min((uint32_t)(fp.H - 1 - Y0) / ts, fp.lt_ty - 1u);
+        const int ntx = tx1 - tx0 + 1, n = ntx * (ty1 - ty0 + 1);
+        if (n <= LT_STAGE_MAX) {
+            uint32_t *hdr = sh.hist;   // [0, 4): counts, [4, 8): list ids
+            if (tid < n) {
+                const uint32_t list = (uint32_t)(ty0 + tid / ntx) * fp.lt_tx + (uint32_t)(tx0 + tid % ntx);
+                hdr[LT_STAGE_MAX + tid] = list;
+                hdr[tid] = min(fb.tile_counts[list], fp.lt_maxp);
+            }
+            __syncthreads();
+            for (int i = tid; i < n * LT_STAGE_CAP; i += 256) {
+                const int s2 = i / LT_STAGE_CAP, j = i % LT_STAGE_CAP;
+                if ((uint32_t)j < hdr[s2]) sh.lid[i] = fb.tile_indices[(size_t)hdr[LT_STAGE_MAX + s2] * fp.lt_maxp + j];
+            }
+            __syncthreads();
+            st.ids = sh.lid;
+            st.hdr = hdr;
+            st.n = n;
+        }
+    }
     // resolve: a wave takes a 16x4 block (one 16-px light tile wide, so Forward+ lanes share a list;
     // rows are still 256-B segments of the HDR target)
     const int lx = 16 * (wave & 1) + (lane & 15), ly = 4 * (wave >> 1) + (lane >> 4);
@@ -1610,7 +1659,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     const unsigned long long key = sh.key[ly * LIB_RTW + lx];
     sh.key[ly * LIB_RTW + lx] = KEY_EMPTY;   // this thread's pixel only: clean for the next tile
     bool covered;
-    lib_resolve<SHADOW>(fp, fb, key, px, py, covered);
+    lib_resolve<SHADOW>(fp, fb, key, px, py, covered, st);
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
     if (tid == 0) fb.busy[rt] = 0u;
