@@ -1780,7 +1780,9 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
         hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     } else {
         hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
-        hipLaunchKernelGGL(k_lib_clip, dim3(std::min((grid + 15) / 16, 1024)), dim3(256), 0, s, fp, fb);
+        // one 16-lane group per queued triangle (the queue can hold every input triangle), at most
+        // 1024 workgroups striding a longer queue
+        hipLaunchKernelGGL(k_lib_clip, dim3(std::max(1, std::min((fp.n_tris + 15) / 16, 1024))), dim3(256), 0, s, fp, fb);
     }
     hipLaunchKernelGGL(k_lib_bigmark, dim3(1024), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
