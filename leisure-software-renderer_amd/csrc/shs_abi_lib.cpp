@@ -24,7 +24,9 @@ using Work = shs_ctx::LibWork;
 
 namespace {
 
-constexpr int SCAN_MAX_PRIMS = 4096;   // smaller passes scan every primitive's box per busy tile
+// Smaller passes scan every primitive's box per busy tile (no bins); above this the per-tile bins win
+// even for ~1.5K primitives (C5: raster 0.51 -> 0.44 ms, the gather was a 1.5K-box scan per tile).
+constexpr int SCAN_MAX_PRIMS = 512;
 
 int harvest(shs_ctx *ctx, Work &w, int k) {
     if (!w.ring_pending[k]) return SHS_OK;
@@ -217,7 +219,11 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fp.extra_cap = shadow ? 0u : w.extra_cap;
     fp.parity = w.frame_index & 1u;
     // scan mode (every busy tile tests every primitive's box) for small passes, per-tile bins above
-    fp.scan_mode = n_tris <= SCAN_MAX_PRIMS ? 1u : 0u;
+    {
+        const char *e = std::getenv("SHS_LIB_SCAN_MAX");   // timing experiments: the scan / bin threshold
+        const long scan_max = e ? std::strtol(e, nullptr, 0) : SCAN_MAX_PRIMS;
+        fp.scan_mode = n_tris <= scan_max ? 1u : 0u;
+    }
     fp.setup_blocks = setup_blocks;
     {
         const char *e = std::getenv("SHS_LIB_EXP");   // timing experiments only: parts of the setup skipped
