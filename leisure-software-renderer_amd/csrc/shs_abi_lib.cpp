@@ -232,11 +232,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     const int owned_bt = (n_tiles - fp.rank + fp.count - 1) / fp.count;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / 8);
     int &resident = ctx->lib_resident[shadow ? 1 : 0];
-    const size_t dyn_lds = shs_internal::lib_raster_dyn_lds(fp, shadow);
-    if (resident <= 0 || ctx->lib_resident_lds[shadow ? 1 : 0] != dyn_lds) {
-        resident = shs_internal::lib_raster_resident_blocks(ctx->device, shadow, dyn_lds);
-        ctx->lib_resident_lds[shadow ? 1 : 0] = dyn_lds;
-    }
+    if (resident <= 0) resident = shs_internal::lib_raster_resident_blocks(ctx->device, shadow);
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt, resident));
     if (ensure(ctx, w.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
 
@@ -536,7 +532,6 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
         fp.lt_mode = c.mode; fp.lt_zs = c.z_slices; fp.n_lights = c.n_lights;
         fp.lt_view_z[0] = c.view[2]; fp.lt_view_z[1] = c.view[6]; fp.lt_view_z[2] = c.view[10]; fp.lt_view_z[3] = c.view[14];
         fp.lt_zn = c.zn; fp.lt_zf = c.zf;
-        fp.lt_lds = (c.n_lights > 0 && c.n_lights <= shs_dev::LIB_LDS_LIGHTS) ? 1u : 0u;
     }
     wk.last_fp = fp;
     ctx->lib_frame = f;

@@ -149,7 +149,6 @@ struct shs_ctx {
     };
     LibWork lib_cam, lib_shadow;
     int lib_resident[2] = {0, 0};         // resident k_lib_raster workgroups (camera, shadow)
-    size_t lib_resident_lds[2] = {0, 0};  // ... at this dynamic LDS size
     DevBuf<uint64_t> lib_timeline;        // SHS_OPT_TIMELINE, camera pass raster
     DevBuf<uint64_t> lib_stimeline;       // SHS_OPT_TIMELINE, camera pass setup
     DevBuf<float4> lib_hdr;

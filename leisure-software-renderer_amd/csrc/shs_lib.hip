@@ -1040,9 +1040,8 @@ struct PLight {
     float4 sa;        // shape_attenuation
     uint32_t model;   // type_shape_flags[3]: attenuation model
 };
-// Forward+ camera passes stage up to LIB_LDS_LIGHTS lights in k_lib_raster's dynamic LDS (sized at
-// launch: other passes keep the 16 KB for more resident workgroups).
-extern __shared__ float4 lib_lds_lights[];   // per light: pr, ci, sa, (model bits, 0, 0, 0)
+constexpr int LIB_LDS_LIGHTS = 256;                  // lights staged in LDS by the camera pass
+__shared__ float4 lib_lds_lights[LIB_LDS_LIGHTS * 4];  // per light: pr, ci, sa, (model bits, 0, 0, 0)
 
 __device__ __forceinline__ PLight plight_global(const CullLight &L) {
     PLight p;
@@ -1143,7 +1142,7 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
         const float zi = g_clamp(floorf(t * (float)fp.lt_zs), 0.0f, (float)(fp.lt_zs - 1u));
         list = ((uint32_t)zi * fp.lt_ty + ty) * fp.lt_tx + tx;
     }
-    const bool lds = fp.lt_lds != 0u;   // k_lib_raster staged them
+    const bool lds = fp.n_lights <= (uint32_t)LIB_LDS_LIGHTS;   // k_lib_raster staged them
     int s_st = -1;
     for (int s = 0; s < st.n; ++s)
         if (st.hdr[LT_STAGE_MAX + s] == list) s_st = s;
@@ -1601,7 +1600,6 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 if (tlon) sh.tl[LTL_NPAIRS] += ptot;
                 const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
                 // one pair: its owner (word's first owner + starts up to it), pixel, then the test
-                // one pair: its owner (word's first owner + starts up to it), pixel, then the test
                 auto pair = [&](int k0) {
                     const int k = k0 + lane;
                     if (k >= total) return;
@@ -1685,12 +1683,8 @@ __device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const L
     lib_resolve<SHADOW>(fp, fb, KEY_EMPTY, px, py, covered);
 }
 
-// SHS_RASTER_WAVES (timing experiments): k_lib_raster's minimum waves per SIMD.
-#ifndef SHS_RASTER_WAVES
-#define SHS_RASTER_WAVES 3
-#endif
 template <bool SHADOW>
-__global__ __launch_bounds__(256, SHS_RASTER_WAVES) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
+__global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
     __shared__ LibShared sh;
     const int tid = threadIdx.x;
     const uint32_t *cnt = fb.counters + fp.parity * LC_N;
@@ -1698,7 +1692,7 @@ __global__ __launch_bounds__(256, SHS_RASTER_WAVES) void k_lib_raster(LibFramePa
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
     if (tid < 2 * LIB_RTW) sh.colmax[tid / LIB_RTW][tid % LIB_RTW] = 0u;
     sh.key[tid] = KEY_EMPTY;
-    if (!SHADOW && fp.lt_lds) {   // Forward+ lights (read after the tile syncs)
+    if (!SHADOW && fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights (read after the tile syncs)
         for (int i = tid; i < fp.n_lights; i += 256) {
             const PLight p = plight_global(fb.lights[i]);
             lib_lds_lights[4 * i] = p.pr;
@@ -1788,25 +1782,20 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
     return hipGetLastError();
 }
 
-size_t lib_raster_dyn_lds(const LibFrameParams &fp, bool shadow) {
-    return (!shadow && fp.lt_lds) ? (size_t)fp.n_lights * 4 * sizeof(float4) : 0;
-}
-
-int lib_raster_resident_blocks(int device, bool shadow, size_t dyn_lds) {
+int lib_raster_resident_blocks(int device, bool shadow) {
     // persistent grid: every workgroup resident at once (CUs x the kernel's occupancy)
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-    const hipError_t e = shadow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lib_raster<true>, 256, dyn_lds)
-                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lib_raster<false>, 256, dyn_lds);
+    const hipError_t e = shadow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lib_raster<true>, 256, 0)
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lib_raster<false>, 256, 0);
     if (e != hipSuccess || per_cu <= 0) per_cu = 2;
     (void)hipGetLastError();   // a failed query must not leave a sticky error for the host's next HIP user
     return cus * per_cu;
 }
 
 hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, int grid, hipStream_t s) {
-    const size_t lds = lib_raster_dyn_lds(fp, shadow);
-    if (shadow) hipLaunchKernelGGL(k_lib_raster<true>, dim3(std::max(grid, 1)), dim3(256), lds, s, fp, fb);
-    else hipLaunchKernelGGL(k_lib_raster<false>, dim3(std::max(grid, 1)), dim3(256), lds, s, fp, fb);
+    if (shadow) hipLaunchKernelGGL(k_lib_raster<true>, dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
+    else hipLaunchKernelGGL(k_lib_raster<false>, dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }
 

@@ -89,7 +89,6 @@ constexpr uint32_t LF_GRADIENT = 8u;    // PassPBRForward's no-sky background gr
 constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT = 4, LC_BIGQ = 5, LC_N = 6;
 static_assert(LC_BIGQ == LC_BIGT + 1 && LC_BIGT % 2 == 0 && LC_N % 2 == 0, "64-bit big-queue word");
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
-constexpr uint32_t LIB_LDS_LIGHTS = 256;   // Forward+ lights k_lib_raster stages in LDS (64 B each)
 
 struct LibFrameParams {
     int32_t W, H;
@@ -106,7 +105,6 @@ struct LibFrameParams {
     int32_t sm_w, sm_h;              // shadow map sampled by the programs
     // Forward+ program: the light lists of the last shs_light_cull
     uint32_t lt_size, lt_tx, lt_ty, lt_maxp, lt_mode, lt_zs, n_lights;
-    uint32_t lt_lds;                 // k_lib_raster stages the n_lights (<= LIB_LDS_LIGHTS) lights in its dynamic LDS
     float lt_view_z[4];              // view matrix row 2 (view-space z, cluster slice)
     float lt_zn, lt_zf;              // the light cull's depth_params
 };

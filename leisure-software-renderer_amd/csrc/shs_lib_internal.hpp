@@ -7,8 +7,7 @@
 namespace shs_internal {
 // shadow = true: PassShadowMap's depth pass; false: rasterize_mesh + builtin programs.
 hipError_t launch_lib_setup(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, hipStream_t s);
-size_t lib_raster_dyn_lds(const shs_dev::LibFrameParams &fp, bool shadow);   // k_lib_raster's dynamic LDS bytes
-int lib_raster_resident_blocks(int device, bool shadow, size_t dyn_lds);   // CUs x occupancy of k_lib_raster
+int lib_raster_resident_blocks(int device, bool shadow);   // CUs x occupancy of k_lib_raster
 hipError_t launch_lib_raster(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, int grid,
                              hipStream_t s);
 }  // namespace shs_internal
