@@ -56,7 +56,7 @@ void release_work(Work &w) {
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
     for (int i = 0; i < 2; ++i) {
         if (w.h_draws[i]) (void)hipHostFree(w.h_draws[i]);
         if (w.slot_ev[i]) (void)hipEventDestroy(w.slot_ev[i]);
@@ -147,6 +147,46 @@ int upload_draws(shs_ctx *ctx, Work &w, const std::vector<LibDrawGPU> &d) {
     return SHS_OK;
 }
 
+
+// k_lib_raster's tile order.  Workgroups b and b + 8 share an XCD (and its L2), and workgroup b
+// takes positions b, b + G, ... then tickets of queue b & 7 (positions = q mod 8), so position j
+// runs on the XCD j % 8.  Owned bin tiles are grouped into supertiles of st x st bin tiles, the
+// supertiles dealt over the 8 XCDs; an XCD's positions walk its supertiles in order, the 4 raster
+// rows of a bin tile together.  A primitive's tiles, and a bin tile's 4 rows sharing one bin list,
+// then mostly land in one L2 instead of up to eight.  st = 0: the plain order (bin tile, row).
+std::vector<int32_t> build_rt_order(int tiles_x, int tiles_y, int rtiles_y, int rank, int count, int st) {
+    constexpr int RPB = shs_dev::TILE / 8;   // raster rows per bin tile
+    std::vector<int32_t> out;
+    auto push_bt = [&](std::vector<int32_t> &v, int t) {
+        const int col = t % tiles_x, brow = t / tiles_x;
+        for (int r = 0; r < RPB; ++r) {
+            const int row = brow * RPB + r;
+            if (row < rtiles_y) v.push_back(row * tiles_x + col);
+        }
+    };
+    if (st <= 0) {
+        for (int t = rank; t < tiles_x * tiles_y; t += count) push_bt(out, t);
+        return out;
+    }
+    const int nsx = (tiles_x + st - 1) / st, nsy = (tiles_y + st - 1) / st;
+    std::vector<std::vector<int32_t>> lists(8);
+    for (int sy = 0; sy < nsy; ++sy)
+        for (int sx = 0; sx < nsx; ++sx) {
+            std::vector<int32_t> &v = lists[(size_t)((sy * nsx + sx) + 3 * sy) & 7u];
+            for (int by = sy * st; by < std::min(tiles_y, (sy + 1) * st); ++by)
+                for (int bx = sx * st; bx < std::min(tiles_x, (sx + 1) * st); ++bx) {
+                    const int t = by * tiles_x + bx;
+                    if (t % count == rank) push_bt(v, t);
+                }
+        }
+    size_t longest = 0;
+    for (const auto &v : lists) longest = std::max(longest, v.size());
+    for (size_t m = 0; m < longest; ++m)
+        for (int x = 0; x < 8; ++x)
+            if (m < lists[x].size()) out.push_back(lists[x][m]);
+    return out;
+}
+
 // Enqueue one pass (w.last_fp / w.last_draws describe it): workspace sizing, draw upload, the two
 // kernels.  shadow: PassShadowMap's depth pass into ctx->shadow_map.
 int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
@@ -168,7 +208,10 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         return SHS_ERR_HIP;
     // every slot enters the large-primitive queue at most once
     if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots)) return SHS_ERR_HIP;
-    const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count;
+    int st = 2;   // supertile edge in bin tiles (SHS_LIB_XCD_ST: timing experiments; 0 = plain order)
+    if (const char *e = std::getenv("SHS_LIB_XCD_ST")) st = (int)std::strtol(e, nullptr, 0);
+    const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count ^
+                          ((uint64_t)(st & 0xff) << 56);
     bool reset = gkey != w.geom_key;
     if (w.tile_count.cap < 2 * (size_t)n_tiles || !w.tile_count.p) {
         if (ensure(ctx, w.tile_count, 2 * (size_t)n_tiles)) return SHS_ERR_HIP;
@@ -188,6 +231,11 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         HIP_TRY(ctx, hipMemsetAsync(w.busy.p, 0, w.busy.cap * sizeof(uint32_t), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(w.counters.p, 0, w.counters.cap * sizeof(uint32_t), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(w.rqueue.p, 0, w.rqueue.cap * sizeof(uint32_t), ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // the previous order's upload is done with h_rt_order
+        w.h_rt_order = build_rt_order(tiles_x, tiles_y, rtiles_y, fp.rank, fp.count, st);
+        if (ensure(ctx, w.rt_order, std::max<size_t>(w.h_rt_order.size(), 1))) return SHS_ERR_HIP;
+        HIP_TRY(ctx, hipMemcpyAsync(w.rt_order.p, w.h_rt_order.data(), w.h_rt_order.size() * sizeof(int32_t),
+                                    hipMemcpyHostToDevice, ctx->stream));
         w.geom_key = gkey;
     }
     if (ensure(ctx, w.bins, (size_t)n_tiles * w.bin_cap)) return SHS_ERR_HIP;
@@ -229,8 +277,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         const char *e = std::getenv("SHS_LIB_EXP");   // timing experiments only: parts of the setup skipped
         fp.exp_flags = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
     }
-    const int owned_bt = (n_tiles - fp.rank + fp.count - 1) / fp.count;
-    fp.n_owned_rt = owned_bt * (shs_dev::TILE / 8);
+    fp.n_owned_rt = (int)w.h_rt_order.size();
     int &resident = ctx->lib_resident[shadow ? 1 : 0];
     if (resident <= 0) resident = shs_internal::lib_raster_resident_blocks(ctx->device, shadow);
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt, resident));
@@ -245,6 +292,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.dbase = reinterpret_cast<int32_t *>(w.draws.p + nd);
     fb.bdraw = fb.dbase + nd + 1;
     fb.rqueue = w.rqueue.p;
+    fb.rt_order = w.rt_order.p;
     if (shadow) {
         fb.depth = ctx->shadow_map.p;
     } else {

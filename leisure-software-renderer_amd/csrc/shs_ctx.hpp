@@ -123,6 +123,8 @@ struct shs_ctx {
         DevBuf<uint32_t> xbase, zord, tile_count, bins, counters, busy, clipq, bigpre;
         DevBuf<uint4> bigq;
         DevBuf<uint32_t> rqueue;
+        DevBuf<int32_t> rt_order;                          // k_lib_raster tile order (built per geometry)
+        std::vector<int32_t> h_rt_order;                   // its host copy (alive while the upload runs)
         DevBuf<uint2> spill, blk_stat, rstat;
         shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots
         size_t h_cap = 0;

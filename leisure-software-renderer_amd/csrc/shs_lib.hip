@@ -1717,11 +1717,9 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
         const bool dynamic_next = i_static + 1 >= S;
         uint32_t tk = 0;
         if (tid == 0 && dynamic_next) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
-        // owned raster tile j: bin tile rank + (j / 4) * count, row (j % 4) inside it
-        const int t = fp.rank + (j >> 2) * fp.count;
-        const int col = t % fp.tiles_x, row = (t / fp.tiles_x) * (TILE / LIB_RTH) + (j & 3);
-        if (row < fp.rtiles_y) {
-            const int rt = row * fp.tiles_x + col;
+        // owned raster tile j (the host's XCD-coherent order, rows inside the frame only)
+        {
+            const int rt = fb.rt_order[j];
             if (fb.busy[rt]) {
                 lib_raster_tile<SHADOW>(fp, fb, cnt, rt, sh, chunk);
             } else {

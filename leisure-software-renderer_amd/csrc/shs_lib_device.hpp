@@ -136,6 +136,7 @@ struct LibBuffers {
     const int32_t *dbase;            // draws[i].tri_base, compact (+ n_tris): the triangle -> draw search
     const int32_t *bdraw;            // per setup block: the draw of its first triangle
     uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQ x LIB_QSTRIDE words
+    const int32_t *rt_order;         // the owned raster tiles in processing order (n_owned_rt; XCD-coherent)
 };
 
 // k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket

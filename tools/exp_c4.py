@@ -12,8 +12,10 @@ import shs_gpu  # noqa: E402
 from shs_gpu import lib_path, scene_lib  # noqa: E402
 
 
-def run(label, n_objects=1000, tpo=1000, program=None, width=3840, height=2160, frames=20, shard=(0, 1)):
-    frame, draws, lights, cull = scene_lib.c4_scene(width, height, n_objects=n_objects, tris_per_object=tpo)
+def run(label, n_objects=1000, tpo=1000, program=None, width=3840, height=2160, frames=20, shard=(0, 1), n_lights=256,
+        lists=False):
+    frame, draws, lights, cull = scene_lib.c4_scene(width, height, n_objects=n_objects, tris_per_object=tpo,
+                                                    n_lights=n_lights)
     frame.shard_rank, frame.shard_count = shard
     cull.shard_rank, cull.shard_count = shard
     if program is not None:
@@ -37,6 +39,9 @@ def run(label, n_objects=1000, tpo=1000, program=None, width=3840, height=2160, 
     ctx.synchronize_lib()
     dt = (time.perf_counter() - t0) / frames * 1e3
     _, kms = ctx.lib_timing_read()
+    if lists:
+        counts = ctx.resolve_light_lists()[0]
+        print(f"  light lists: mean {counts.mean():.1f}  p90 {sorted(counts.ravel())[int(0.9 * counts.size)]}  max {counts.max()}")
     ctx.close()
     print(f"{label:28s} frame {dt:7.3f} ms  setup {kms['setup']:7.3f}  raster {kms['raster']:7.3f}  "
           f"clip {st['tri_after_clip']} rast {st['tri_raster']} cov {st['covered_pixels']} maxbin {st['max_tile_bin']} "
@@ -45,6 +50,12 @@ def run(label, n_objects=1000, tpo=1000, program=None, width=3840, height=2160, 
 
 def main():
     frames = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    if len(sys.argv) > 2 and sys.argv[2] == "shade":
+        run("c4", frames=frames, lists=True)
+        for n in (1, 16, 64):
+            run(f"c4 {n} lights", frames=frames, n_lights=n)
+        run("c4 debug-albedo", program=lib_path.PROGRAM_DEBUG_ALBEDO, frames=frames)
+        return
     run("c4", frames=frames)
     run("c4 debug-albedo", program=lib_path.PROGRAM_DEBUG_ALBEDO, frames=frames)
     run("c4 250k tris", n_objects=250, frames=frames)
