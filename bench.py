@@ -240,11 +240,11 @@ def run_gpu_c4(args, rank, local_rank, world, dist):
     ctx.light_cull(cull)
     prepared = ctx.prepare_lib(frame, draws)
     gbufs = [None]
+    ctx.fuse_tonemap(1.0, 2.2, ldr=False, present=True)   # PassTonemap inside the pass's shading kernel
 
     def one_frame():
         ctx.light_cull(cull)
         ctx.render_pbr_forward_prepared(prepared)
-        ctx.tonemap(1.0, 2.2, ldr=False, present=True)
         if dist is not None:
             gbufs[0] = shard.gather_frame_device(dist, ctx, ctx.TARGET_LIB_PRESENT, out=gbufs[0])
 
@@ -273,9 +273,9 @@ def run_gpu_c4(args, rank, local_rank, world, dist):
     ctx.enable_timing(False)
     ctx.close()
     n_tri = sum(d.mesh.n_tris for d in draws)
-    B_cam_raster = frame.width * frame.height * 28
-    # + the tonemap: HDR read (16 B/px) and the RGBA8 present staging written (4 B/px)
-    B_frame = n_tri * 72 + frame.width * frame.height * (28 + 20) + len(lights) * 160 + cull.n_lists * 4
+    # the raster phase writes HDR + depth + motion (28 B/px) and the fused tonemap's RGBA8 present staging (4 B/px)
+    B_cam_raster = frame.width * frame.height * 32
+    B_frame = n_tri * 72 + frame.width * frame.height * 32 + len(lights) * 160 + cull.n_lists * 4
     return frame, stats, elapsed, n_passes["camera"], kms, B_cam_raster, B_frame, n_tri, None
 
 
@@ -313,11 +313,11 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
     L = ctx._lib
 
     gbufs = [None]
+    ctx.fuse_tonemap(1.0, 2.2, ldr=False, present=True)   # PassTonemap inside the pass's shading kernel
 
     def one_frame():
         ctx._check(L.shs_render_shadow_map(ctx._h, S, S, sd, carr, len(casters), None))
         ctx.render_pbr_forward_prepared(prepared)
-        ctx.tonemap(1.0, 2.2, ldr=False, present=True)
         if dist is not None:
             gbufs[0] = shard.gather_frame_device(dist, ctx, ctx.TARGET_LIB_PRESENT, out=gbufs[0])
 
@@ -344,21 +344,22 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
     n_passes, kms = ctx.lib_timing_read()
     ctx.enable_timing(False)
     ctx.close()
-    B_cam_raster = frame.width * frame.height * 28 + S * S * 4
+    B_cam_raster = frame.width * frame.height * 32 + S * S * 4
     B_frame = (sum(lib_mesh_bytes(d.mesh) for d in draws) + sum(lib_mesh_bytes(c.mesh, False) for c in casters)
-               + 2 * S * S * 4 + frame.width * frame.height * (28 + 20))
+               + 2 * S * S * 4 + frame.width * frame.height * 32)
     n_tri = sum(d.mesh.n_tris for d in draws)
     return frame, stats, elapsed, n_passes["camera"], kms, B_cam_raster, B_frame, n_tri, S
 
 
 def collect_pmc(args):
     """rocprofv3 --pmc child passes (one counter per pass: FETCH_SIZE costs 3 TCC slots and
-    WRITE_SIZE 2, they do not fit together).  Returns bytes per k_raster dispatch or None."""
+    WRITE_SIZE 2, they do not fit together).  Returns bytes per dominant-phase dispatch (k_raster; for
+    the library configs k_lib_raster<false> + k_lib_resolve, summed) or None."""
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None, "rocprofv3 not found"
     out = {}
-    kmatch = "k_lib_raster<false>" if args.config in LIB_CONFIGS else "k_raster<"
+    kmatch = ("k_lib_raster<false>", "k_lib_resolve<") if args.config in LIB_CONFIGS else ("k_raster<",)
     tmp = tempfile.mkdtemp(prefix="shs_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -372,16 +373,19 @@ def collect_pmc(args):
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if not files:
                 return None, f"no counter_collection.csv for {counter}"
-            vals = []
+            vals = {k: [] for k in kmatch}
             for f in files:
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
-                        if kmatch in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                            vals.append(float(row["Counter_Value"]))
-            if not vals:
-                return None, f"no k_raster rows for {counter}"
-            vals = vals[3:] if len(vals) > 6 else vals   # drop warmup dispatches
-            out[counter] = sum(vals) / len(vals)
+                        for k in kmatch:
+                            if k in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                                vals[k].append(float(row["Counter_Value"]))
+            if not all(vals.values()):
+                return None, f"no {kmatch} rows for {counter}"
+            out[counter] = 0.0
+            for v in vals.values():
+                v = v[3:] if len(v) > 6 else v   # drop warmup dispatches
+                out[counter] += sum(v) / len(v)
     except Exception as e:  # the measurement is optional; never fail the bench line over it
         return None, f"pmc failed: {e!r}"
     finally:
@@ -658,7 +662,8 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     t_k = kms["raster"]
     achieved = B_k / (t_k * 1e-3) / 1e9 if t_k > 0 else None
     t_frame = sum(kms.values())
-    roofline = {"kernel": "k_lib_raster<false> (camera pass)", "bound": "hbm",
+    roofline = {"kernel": "k_lib_raster<false> + k_lib_resolve (camera pass raster phase: coverage, then shading + "
+                          "fused tonemap)", "bound": "hbm",
                 "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": round(pmc["bytes"]) if pmc else None, "algorithmic_bytes": B_k,

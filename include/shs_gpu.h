@@ -392,6 +392,12 @@ typedef struct shs_tonemap_desc {
     uint32_t flags;             /* SHS_TONEMAP_* targets to write (at least one) */
 } shs_tonemap_desc;
 int shs_tonemap(shs_ctx *ctx, const shs_tonemap_desc *desc);
+/* Fused PassTonemap: with desc non-NULL, every later shs_render_pbr_forward also writes desc's
+ * targets from its shading kernel (one launch, no HDR re-read; the bytes are shs_tonemap's), and the
+ * frame counts as tonemapped (shs_resolve_ldr, shs_motion_blur, SHS_TARGET_LIB_PRESENT tiles) without
+ * a shs_tonemap call.  NULL turns it off.  The reference runs PassTonemap as a separate pass
+ * (pass_tonemap.hpp:36-83); this only fuses it into the producer. */
+int shs_lib_fuse_tonemap(shs_ctx *ctx, const shs_tonemap_desc *desc);
 /* Copy the tonemapped targets into caller-owned W*H*4-byte buffers (either may be NULL). */
 int shs_resolve_ldr(shs_ctx *ctx, uint8_t *ldr, uint8_t *present);
 int shs_ldr_device_targets(shs_ctx *ctx, void **ldr_dev, void **present_dev);

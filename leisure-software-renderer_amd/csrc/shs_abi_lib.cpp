@@ -297,6 +297,27 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         fb.depth = ctx->shadow_map.p;
     } else {
         fb.hdr = ctx->lib_hdr.p; fb.depth = ctx->lib_depth.p; fb.motion = ctx->lib_motion.p;
+        fb.keys = ctx->lib_keys.p;
+        if (w.tm_fused) {   // PassTonemap in k_lib_resolve (shs_lib_fuse_tonemap)
+            const shs_tonemap_desc &d = w.tm_desc;
+            const size_t npx = (size_t)W * H;
+            if ((d.flags & SHS_TONEMAP_LDR) && ensure(ctx, ctx->lib_ldr, npx)) return SHS_ERR_HIP;
+            if ((d.flags & SHS_TONEMAP_PRESENT) && ensure(ctx, ctx->lib_present, npx)) return SHS_ERR_HIP;
+            const float g = std::max(0.001f, d.gamma);
+            if (ensure(ctx, ctx->tm_thr_dev, 256)) return SHS_ERR_HIP;
+            if (ctx->tm_thr_dev_gamma != g) {   // rare (a new gamma): a synchronous upload
+                float thr[256];
+                shs_tonemap_thresholds(g, thr);
+                HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+                HIP_TRY(ctx, hipMemcpy(ctx->tm_thr_dev.p, thr, sizeof thr, hipMemcpyHostToDevice));
+                ctx->tm_thr_dev_gamma = g;
+            }
+            fb.tm_thr = ctx->tm_thr_dev.p;
+            fb.tm_ldr = (d.flags & SHS_TONEMAP_LDR) ? ctx->lib_ldr.p : nullptr;
+            fb.tm_present = (d.flags & SHS_TONEMAP_PRESENT) ? ctx->lib_present.p : nullptr;
+            fp.tm_exposure = std::max(0.0001f, d.exposure);
+            fp.tm_inv_gamma = 1.0f / g;
+        }
         fb.shadow_map = ctx->have_shadow ? ctx->shadow_map.p : nullptr;
         fb.lights = ctx->lights.p;
         fb.tile_counts = ctx->list_counts.p;
@@ -326,6 +347,16 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, ctx->stream));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], ctx->stream));
     HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, raster_grid, ctx->stream));
+    if (!shadow) {   // the camera pass's shading runs in its own kernel (event [2] closes both)
+        int prog = w.last_draws.empty() ? -1 : w.last_draws[0].program;
+        for (const auto &d : w.last_draws)
+            if (d.program != prog) prog = -1;
+        if (prog != 5 && prog != 0) prog = -1;
+        int &res = ctx->lib_resolve_resident[prog == 5 ? 0 : prog == 0 ? 1 : 2];
+        if (res <= 0) res = shs_internal::lib_resolve_resident_blocks(ctx->device, prog);
+        const int rgrid = std::max(1, std::min(fp.n_owned_rt, res));
+        HIP_TRY(ctx, shs_internal::launch_lib_resolve(fp, fb, prog, rgrid, ctx->stream));
+    }
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], ctx->stream));
     w.last_parity = fp.parity;
     w.frame_index++;
@@ -406,7 +437,7 @@ int check_lib_mesh(shs_ctx *ctx, int32_t id) {
 void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_cam);
     release_work(ctx->lib_shadow);
-    release(ctx->lib_hdr); release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
+    release(ctx->lib_hdr); release(ctx->lib_keys); release(ctx->tm_thr_dev); ctx->tm_thr_dev_gamma = -1.0f; release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
     release(ctx->lights); release(ctx->cull_work); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
     release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
@@ -550,7 +581,7 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     if (!ctx->h_lib_counters && hipHostMalloc(reinterpret_cast<void **>(&ctx->h_lib_counters), shs_dev::LC_N * sizeof(uint32_t)) != hipSuccess)
         return SHS_ERR_HIP;
     const size_t npx = (size_t)f.width * f.height;
-    if (ensure(ctx, ctx->lib_hdr, npx)) return SHS_ERR_HIP;
+    if (ensure(ctx, ctx->lib_hdr, npx) || ensure(ctx, ctx->lib_keys, npx)) return SHS_ERR_HIP;
     const bool dm = (f.flags & SHS_LIB_DEPTH_MOTION) != 0;
     if (dm && (ensure(ctx, ctx->lib_depth, npx) || ensure(ctx, ctx->lib_motion, npx))) return SHS_ERR_HIP;
 
@@ -584,10 +615,14 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     wk.last_fp = fp;
     ctx->lib_frame = f;
     ctx->cam_after_shadow = ctx->have_shadow;
+    wk.tm_fused = ctx->tm_fuse;
+    wk.tm_desc = ctx->tm_fuse_desc;
     const int rc = enqueue_pass(ctx, wk, false);
     if (rc) return rc;
     ctx->have_lib_frame = true;
-    ctx->have_ldr = false;   // a new camera pass: a tonemap (and motion blur) must follow it again
+    // a new camera pass: a tonemap (and motion blur) must follow it again, unless it ran fused
+    ctx->have_ldr = wk.tm_fused;
+    if (wk.tm_fused) ctx->tm_desc = wk.tm_desc;
     ctx->have_mb = false;
     return SHS_OK;
 }

@@ -120,6 +120,25 @@ int shs_tonemap_reissue(shs_ctx *ctx) {
 
 extern "C" {
 
+int shs_lib_fuse_tonemap(shs_ctx *ctx, const shs_tonemap_desc *desc) {
+    if (!ctx) return SHS_ERR_INVALID;
+    if (!desc) {
+        ctx->tm_fuse = false;
+        return SHS_OK;
+    }
+    if (!(desc->flags & (SHS_TONEMAP_LDR | SHS_TONEMAP_PRESENT)) || (desc->flags & ~(SHS_TONEMAP_LDR | SHS_TONEMAP_PRESENT))) {
+        ctx->err = "tonemap flags: SHS_TONEMAP_LDR and / or SHS_TONEMAP_PRESENT";
+        return SHS_ERR_INVALID;
+    }
+    if (!std::isfinite(desc->exposure) || !std::isfinite(desc->gamma)) {
+        ctx->err = "tonemap exposure / gamma must be finite";
+        return SHS_ERR_INVALID;
+    }
+    ctx->tm_fuse = true;
+    ctx->tm_fuse_desc = *desc;
+    return SHS_OK;
+}
+
 int shs_tonemap_thresholds(float gamma, float thr[256]) {
     if (!thr) return SHS_ERR_INVALID;
     tonemap_thresholds(gamma, thr);

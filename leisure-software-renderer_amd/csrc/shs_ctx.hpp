@@ -125,6 +125,8 @@ struct shs_ctx {
         DevBuf<uint32_t> rqueue;
         DevBuf<int32_t> rt_order;                          // k_lib_raster tile order (built per geometry)
         std::vector<int32_t> h_rt_order;                   // its host copy (alive while the upload runs)
+        bool tm_fused = false;                             // camera pass: the fused tonemap of tm_desc
+        shs_tonemap_desc tm_desc{};
         DevBuf<uint2> spill, blk_stat, rstat;
         shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots
         size_t h_cap = 0;
@@ -154,6 +156,8 @@ struct shs_ctx {
     DevBuf<uint64_t> lib_timeline;        // SHS_OPT_TIMELINE, camera pass raster
     DevBuf<uint64_t> lib_stimeline;       // SHS_OPT_TIMELINE, camera pass setup
     DevBuf<float4> lib_hdr;
+    DevBuf<unsigned long long> lib_keys;  // camera pass winner keys (k_lib_raster -> k_lib_resolve)
+    int lib_resolve_resident[3] = {0, 0, 0};   // resident k_lib_resolve workgroups (Forward+, PBR, mixed)
     DevBuf<float> lib_depth;
     DevBuf<float2> lib_motion;
     DevBuf<float> shadow_map;
@@ -179,6 +183,10 @@ struct shs_ctx {
     bool tm_thr_valid = false;            // tm_thr holds the thresholds of tm_gamma
     float tm_thr[256] = {};
     bool have_ldr = false;                // a tonemap follows the current camera pass
+    bool tm_fuse = false;                 // shs_lib_fuse_tonemap: camera passes write tm_fuse_desc's targets
+    shs_tonemap_desc tm_fuse_desc{};
+    DevBuf<float> tm_thr_dev;             // the fused tonemap's thresholds (of tm_thr_dev_gamma)
+    float tm_thr_dev_gamma = -1.0f;
     DevBuf<uint32_t> lib_mb, lib_mb_present;
     shs_motion_blur_desc mb_desc{};
     bool have_mb = false;                 // a motion blur follows that tonemap

@@ -34,6 +34,7 @@
 #include "shs_device.hpp"
 #include "shs_lib_device.hpp"
 #include "shs_lib_internal.hpp"
+#include "shs_post_internal.hpp"
 #include "shs_wave.hpp"
 
 namespace shs_dev {
@@ -1170,13 +1171,17 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
 }
 
 // The builtin fragment programs (builtin_shaders.hpp:105-245); no base_color_tex -> albedo_tex = 1.
+// PROG >= 0: every draw of the pass runs that program (k_lib_resolve specialisations: only its
+// registers are live); -1: per draw.
+template <int PROG>
 __device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, float depth01,
                            int px, int py, const LtStage &st) {
     const f3 bc = {dr.base[0], dr.base[1], dr.base[2]};
-    if (dr.program == 5) return forward_plus(fp, fb, dr, world, nrm, px, py, st);
-    if (dr.program == 2) return bc;                                                   // debug albedo
-    if (dr.program == 3) return add3(sc3(normalize3(nrm), 0.5f), f3{0.5f, 0.5f, 0.5f});  // debug normal
-    if (dr.program == 4) {                                                            // debug depth
+    const int program = PROG >= 0 ? PROG : dr.program;
+    if (program == 5) return forward_plus(fp, fb, dr, world, nrm, px, py, st);
+    if (program == 2) return bc;                                                   // debug albedo
+    if (program == 3) return add3(sc3(normalize3(nrm), 0.5f), f3{0.5f, 0.5f, 0.5f});  // debug normal
+    if (program == 4) {                                                            // debug depth
         const float dd = s_clamp(depth01, 0.0f, 1.0f);
         return f3{dd, dd, dd};
     }
@@ -1186,7 +1191,7 @@ __device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const
     const f3 albedo = gmax3(bc, f3{0.0f, 0.0f, 0.0f});   // base_color * vec3(1)
     const f3 N = normalize3(nrm);
     const f3 V = normalize3(sub3(cam, world));
-    if (dr.program == 1) {   // make_blinn_phong_program (:111-150)
+    if (program == 1) {   // make_blinn_phong_program (:111-150)
         const f3 H = normalize3(add3(L, V));
         const float NdotL = s_max(0.0f, dot3(N, L));
         const float NdotH = s_max(0.0f, dot3(N, H));
@@ -1269,21 +1274,22 @@ __device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
     return r;
 }
 
+template <int PROG>
 __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
                                          const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv,
                                          const LtStage &st);
 
 // Resolve one pixel of a tile (one thread): the winner of the key array is re-evaluated with the
 // identical arithmetic, shaded and written; pixels without a winner get the clear values.
-template <bool SHADOW>
-__device__ __forceinline__ void lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, unsigned long long key, int px,
-                                            int py, bool &covered, const LtStage &st = LtStage{}) {
+template <bool SHADOW, int PROG = -1>
+__device__ __forceinline__ float4 lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, unsigned long long key, int px,
+                                              int py, bool &covered, const LtStage &st = LtStage{}) {
     covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
-    if (px >= fp.W || py >= fp.H) return;
+    if (px >= fp.W || py >= fp.H) return make_float4(0.f, 0.f, 0.f, 0.f);
     const size_t o = (size_t)py * fp.W + px;
     if (SHADOW) {
         fb.depth[o] = covered ? __uint_as_float((uint32_t)(key >> 32) & 0x7fffffffu) : 1.0f;
-        return;
+        return make_float4(0.f, 0.f, 0.f, 0.f);
     }
     float4 color = bg_color(fp, py);
     float depth = 1.0f;
@@ -1296,18 +1302,20 @@ __device__ __forceinline__ void lib_resolve(const LibFrameParams &fp, const LibB
         const LibShade s = fb.shade[slot];
         // a wave whose covered pixels share one draw reads its uniforms with scalar loads
         const int d0 = __builtin_amdgcn_readfirstlane(s.draw);
-        if (__ballot(s.draw != d0) == 0) shade_px(fp, fb, fb.draws[d0], r, s, px, py, color, depth, mv, st);
-        else shade_px(fp, fb, fb.draws[s.draw], r, s, px, py, color, depth, mv, st);
+        if (__ballot(s.draw != d0) == 0) shade_px<PROG>(fp, fb, fb.draws[d0], r, s, px, py, color, depth, mv, st);
+        else shade_px<PROG>(fp, fb, fb.draws[s.draw], r, s, px, py, color, depth, mv, st);
     }
     fb.hdr[o] = color;
     if (fp.flags & LF_DEPTH) {
         fb.depth[o] = depth;
         fb.motion[o] = mv;
     }
+    return color;
 }
 
 // The winner of one pixel: identical re-evaluation of the pixel test, the varyings, motion and the
 // fragment program (rasterizer.hpp:341-419).
+template <int PROG>
 __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
                                          const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv,
                                          const LtStage &st) {
@@ -1337,7 +1345,7 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
                 mv = make_float2(vx, vy);
             }
         }
-        const f3 c = lib_fragment(fp, fb, dr, world, nrm, z01, px, py, st);
+        const f3 c = lib_fragment<PROG>(fp, fb, dr, world, nrm, z01, px, py, st);
         color = make_float4(c.x, c.y, c.z, 1.0f);
     }
 }
@@ -1624,42 +1632,19 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     }
     __syncthreads();
     const uint64_t t_res = tlon ? tl_now() : 0ull;
-    // Forward+ tile lists: the (<= LT_STAGE_MAX) light lists under this raster tile go to LDS (the
-    // candidate-list arrays are free now), so the per-light index loads of the resolve hit LDS
-    LtStage st;
-    if (!SHADOW && fb.tile_counts && (fp.lt_mode == 1u || fp.lt_mode == 2u) && fp.lt_maxp <= (uint32_t)LT_STAGE_CAP &&
-        X0 < fp.W && Y0 < fp.H) {   // block-uniform
-        const uint32_t ts = fp.lt_size;
-        const int tx0 = min((uint32_t)X0 / ts, fp.lt_tx - 1u), tx1 = min((uint32_t)min(X1, fp.W - 1) / ts, fp.lt_tx - 1u);
-        const int ty0 = min((uint32_t)(fp.H - 1 - min(Y1, fp.H - 1)) / ts, fp.lt_ty - 1u);
-        const int ty1 = min((uint32_t)(fp.H - 1 - Y0) / ts, fp.lt_ty - 1u);
-        const int ntx = tx1 - tx0 + 1, n = ntx * (ty1 - ty0 + 1);
-        if (n <= LT_STAGE_MAX) {
-            uint32_t *hdr = sh.hist;   // [0, 4): counts, [4, 8): list ids
-            if (tid < n) {
-                const uint32_t list = (uint32_t)(ty0 + tid / ntx) * fp.lt_tx + (uint32_t)(tx0 + tid % ntx);
-                hdr[LT_STAGE_MAX + tid] = list;
-                hdr[tid] = min(fb.tile_counts[list], fp.lt_maxp);
-            }
-            __syncthreads();
-            for (int i = tid; i < n * LT_STAGE_CAP; i += 256) {
-                const int s2 = i / LT_STAGE_CAP, j = i % LT_STAGE_CAP;
-                if ((uint32_t)j < hdr[s2]) sh.lid[i] = fb.tile_indices[(size_t)hdr[LT_STAGE_MAX + s2] * fp.lt_maxp + j];
-            }
-            __syncthreads();
-            st.ids = sh.lid;
-            st.hdr = hdr;
-            st.n = n;
-        }
-    }
-    // resolve: a wave takes a 16x4 block (one 16-px light tile wide, so Forward+ lanes share a list;
-    // rows are still 256-B segments of the HDR target)
+    // a wave takes a 16x4 block of the tile (rows are 128-B key / 256-B HDR segments); the shadow pass
+    // resolves here, the camera pass hands its keys to k_lib_resolve
     const int lx = 16 * (wave & 1) + (lane & 15), ly = 4 * (wave >> 1) + (lane >> 4);
     const int px = X0 + lx, py = Y0 + ly;
     const unsigned long long key = sh.key[ly * LIB_RTW + lx];
     sh.key[ly * LIB_RTW + lx] = KEY_EMPTY;   // this thread's pixel only: clean for the next tile
     bool covered;
-    lib_resolve<SHADOW>(fp, fb, key, px, py, covered, st);
+    if (SHADOW) {
+        lib_resolve<SHADOW>(fp, fb, key, px, py, covered);
+    } else {
+        covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
+        if (px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = key;
+    }
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
     if (tid == 0) fb.busy[rt] = 0u;
@@ -1679,8 +1664,12 @@ __device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const L
     const int tid = threadIdx.x;
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
     const int px = col * LIB_RTW + (tid & 31), py = row * LIB_RTH + (tid >> 5);
-    bool covered;
-    lib_resolve<SHADOW>(fp, fb, KEY_EMPTY, px, py, covered);
+    if (SHADOW) {
+        bool covered;
+        lib_resolve<SHADOW>(fp, fb, KEY_EMPTY, px, py, covered);
+    } else if (px < fp.W && py < fp.H) {
+        fb.keys[(size_t)py * fp.W + px] = KEY_EMPTY;
+    }
 }
 
 template <bool SHADOW>
@@ -1692,15 +1681,6 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
     if (tid < 2 * LIB_RTW) sh.colmax[tid / LIB_RTW][tid % LIB_RTW] = 0u;
     sh.key[tid] = KEY_EMPTY;
-    if (!SHADOW && fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights (read after the tile syncs)
-        for (int i = tid; i < fp.n_lights; i += 256) {
-            const PLight p = plight_global(fb.lights[i]);
-            lib_lds_lights[4 * i] = p.pr;
-            lib_lds_lights[4 * i + 1] = p.ci;
-            lib_lds_lights[4 * i + 2] = p.sa;
-            lib_lds_lights[4 * i + 3] = make_float4(__uint_as_float(p.model), 0.0f, 0.0f, 0.0f);
-        }
-    }
     uint32_t chunk = 0;   // staging passes so far (selects the colmax slot)
     if (fb.timeline && tid < LTL_STRIDE) sh.tl[tid] = tid == LTL_START ? tl_now() : 0ull;
     // Owned raster tiles: the first S * G statically interleaved (tile b + i * G, i < S: no ticket
@@ -1758,6 +1738,89 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
     }
 }
 
+// Forward+ tile lists: the (<= LT_STAGE_MAX) light lists under one raster tile go to LDS, so the
+// per-light index loads of its pixels hit LDS.  Block-uniform; ends with a barrier when it stages.
+__device__ __forceinline__ void stage_tile_lists(const LibFrameParams &fp, const LibBuffers &fb, int X0, int Y0, uint32_t *hdr,
+                                                 uint32_t *ids, LtStage &st) {
+    const int tid = threadIdx.x;
+    const int X1 = X0 + LIB_RTW - 1, Y1 = Y0 + LIB_RTH - 1;
+    if (!fb.tile_counts || !(fp.lt_mode == 1u || fp.lt_mode == 2u) || fp.lt_maxp > (uint32_t)LT_STAGE_CAP || X0 >= fp.W ||
+        Y0 >= fp.H)
+        return;
+    const uint32_t ts = fp.lt_size;
+    const int tx0 = min((uint32_t)X0 / ts, fp.lt_tx - 1u), tx1 = min((uint32_t)min(X1, fp.W - 1) / ts, fp.lt_tx - 1u);
+    const int ty0 = min((uint32_t)(fp.H - 1 - min(Y1, fp.H - 1)) / ts, fp.lt_ty - 1u);
+    const int ty1 = min((uint32_t)(fp.H - 1 - Y0) / ts, fp.lt_ty - 1u);
+    const int ntx = tx1 - tx0 + 1, n = ntx * (ty1 - ty0 + 1);
+    if (n > LT_STAGE_MAX) return;
+    if (tid < n) {   // hdr [0, 4): counts, [4, 8): list ids
+        const uint32_t list = (uint32_t)(ty0 + tid / ntx) * fp.lt_tx + (uint32_t)(tx0 + tid % ntx);
+        hdr[LT_STAGE_MAX + tid] = list;
+        hdr[tid] = min(fb.tile_counts[list], fp.lt_maxp);
+    }
+    __syncthreads();
+    for (int i = tid; i < n * LT_STAGE_CAP; i += 256) {
+        const int s2 = i / LT_STAGE_CAP, j = i % LT_STAGE_CAP;
+        if ((uint32_t)j < hdr[s2]) ids[i] = fb.tile_indices[(size_t)hdr[LT_STAGE_MAX + s2] * fp.lt_maxp + j];
+    }
+    __syncthreads();
+    st.ids = ids;
+    st.hdr = hdr;
+    st.n = n;
+}
+
+// The camera pass's resolve (rasterizer.hpp:341-419 per winner): every owned raster tile's pixels,
+// their winning key from k_lib_raster re-evaluated, shaded and written; pixels without a winner get
+// the clear values.  Persistent (tile j = b + i * G in k_lib_raster's order); the Forward+ lights and
+// each tile's light lists are staged in LDS.  A separate kernel: the shading's register and LDS
+// footprint stays out of the raster's (more raster workgroups per CU), and the shading's dependent
+// loads (key -> record -> draw -> shadow map) overlap across many more waves than one raster tile's.
+// Minimum waves per SIMD: 4 for the single-program kernels (no spills at 128 VGPRs), 3 for the mixed
+// one (its 137 VGPRs; 4 would spill); -DSHS_RESOLVE_WAVES_FP / _PBR override (timing experiments).
+#ifndef SHS_RESOLVE_WAVES_FP
+#define SHS_RESOLVE_WAVES_FP 4
+#endif
+#ifndef SHS_RESOLVE_WAVES_PBR
+#define SHS_RESOLVE_WAVES_PBR 4
+#endif
+template <int PROG>
+__global__ __launch_bounds__(256, PROG == 5 ? SHS_RESOLVE_WAVES_FP : PROG == 0 ? SHS_RESOLVE_WAVES_PBR : 3)
+void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
+    __shared__ uint32_t lt_hdr[2 * LT_STAGE_MAX];
+    __shared__ uint32_t lt_ids[LT_STAGE_MAX * LT_STAGE_CAP];
+    __shared__ float tm_thr[256];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (fb.tm_thr) tm_thr[tid] = fb.tm_thr[tid];
+    if (fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights (read after the tile syncs)
+        for (int i = tid; i < fp.n_lights; i += 256) {
+            const PLight p = plight_global(fb.lights[i]);
+            lib_lds_lights[4 * i] = p.pr;
+            lib_lds_lights[4 * i + 1] = p.ci;
+            lib_lds_lights[4 * i + 2] = p.sa;
+            lib_lds_lights[4 * i + 3] = make_float4(__uint_as_float(p.model), 0.0f, 0.0f, 0.0f);
+        }
+    }
+    for (int j = (int)blockIdx.x; j < fp.n_owned_rt; j += (int)gridDim.x) {   // block-uniform
+        __syncthreads();   // lights staged / the previous tile's lists read
+        const int rt = fb.rt_order[j];
+        const int X0 = (rt % fp.tiles_x) * LIB_RTW, Y0 = (rt / fp.tiles_x) * LIB_RTH;
+        LtStage st;
+        stage_tile_lists(fp, fb, X0, Y0, lt_hdr, lt_ids, st);
+        // a wave takes a 16x4 block (one 16-px light tile wide, so Forward+ lanes share a list)
+        const int px = X0 + 16 * (wave & 1) + (lane & 15), py = Y0 + 4 * (wave >> 1) + (lane >> 4);
+        const unsigned long long key = (px < fp.W && py < fp.H) ? fb.keys[(size_t)py * fp.W + px] : KEY_EMPTY;
+        bool covered;
+        const float4 c = lib_resolve<false, PROG>(fp, fb, key, px, py, covered, st);
+        if (fb.tm_thr && px < fp.W && py < fp.H) {   // fused PassTonemap of this pixel's HDR value
+            const uint32_t rgba = tonemap_byte(c.x, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) |
+                                  (tonemap_byte(c.y, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) << 8) |
+                                  (tonemap_byte(c.z, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) << 16) | (255u << 24);
+            if (fb.tm_ldr) __builtin_nontemporal_store(rgba, &fb.tm_ldr[(size_t)py * fp.W + px]);
+            if (fb.tm_present) __builtin_nontemporal_store(rgba, &fb.tm_present[(size_t)(fp.H - 1 - py) * fp.W + px]);
+        }
+    }
+}
+
 }  // namespace shs_dev
 
 namespace shs_internal {
@@ -1789,6 +1852,23 @@ int lib_raster_resident_blocks(int device, bool shadow) {
     if (e != hipSuccess || per_cu <= 0) per_cu = 2;
     (void)hipGetLastError();   // a failed query must not leave a sticky error for the host's next HIP user
     return cus * per_cu;
+}
+
+// k_lib_resolve per program class: 5 (Forward+ only), 0 (PBR metallic-roughness only), -1 (any mix)
+#define SHS_RESOLVE_KERNEL(prog) (prog == 5 ? k_lib_resolve<5> : prog == 0 ? k_lib_resolve<0> : k_lib_resolve<-1>)
+
+int lib_resolve_resident_blocks(int device, int prog) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, SHS_RESOLVE_KERNEL(prog), 256, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 2;
+    (void)hipGetLastError();
+    return cus * per_cu;
+}
+
+hipError_t launch_lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, int prog, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(SHS_RESOLVE_KERNEL(prog), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
+    return hipGetLastError();
 }
 
 hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, int grid, hipStream_t s) {

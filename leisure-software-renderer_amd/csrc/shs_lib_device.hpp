@@ -107,6 +107,7 @@ struct LibFrameParams {
     uint32_t lt_size, lt_tx, lt_ty, lt_maxp, lt_mode, lt_zs, n_lights;
     float lt_view_z[4];              // view matrix row 2 (view-space z, cluster slice)
     float lt_zn, lt_zf;              // the light cull's depth_params
+    float tm_exposure, tm_inv_gamma; // fused PassTonemap (LibBuffers::tm_thr)
 };
 
 struct LibBuffers {
@@ -137,6 +138,10 @@ struct LibBuffers {
     const int32_t *bdraw;            // per setup block: the draw of its first triangle
     uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQ x LIB_QSTRIDE words
     const int32_t *rt_order;         // the owned raster tiles in processing order (n_owned_rt; XCD-coherent)
+    unsigned long long *keys;        // camera pass: W*H winning (z, submission) keys, k_lib_raster -> k_lib_resolve
+    // fused PassTonemap (shs_lib_fuse_tonemap): k_lib_resolve also writes the tonemapped bytes
+    const float *tm_thr;             // the 256 byte thresholds (shs_post_internal.hpp), null: not fused
+    uint32_t *tm_ldr, *tm_present;   // RT_ColorLDR (rows y up) / present staging (rows top-down), or null
 };
 
 // k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket

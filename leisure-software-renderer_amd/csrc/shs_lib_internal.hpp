@@ -10,4 +10,9 @@ hipError_t launch_lib_setup(const shs_dev::LibFrameParams &fp, const shs_dev::Li
 int lib_raster_resident_blocks(int device, bool shadow);   // CUs x occupancy of k_lib_raster
 hipError_t launch_lib_raster(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, int grid,
                              hipStream_t s);
+// The camera pass's shading: every owned pixel's winner (fb.keys) shaded into hdr / depth / motion.
+// prog: the program every draw of the pass runs (5 Forward+, 0 PBR: specialised kernels) or -1.
+int lib_resolve_resident_blocks(int device, int prog);      // CUs x occupancy of k_lib_resolve<prog>
+hipError_t launch_lib_resolve(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, int prog, int grid,
+                              hipStream_t s);
 }  // namespace shs_internal

@@ -11,19 +11,7 @@
 
 namespace shs_dev {
 
-// One channel: exposure, std::max(0, c) (NaN -> 0), Reinhard, then the byte by threshold count.
-// The first guess comes from a fast pow; the two loops move it to the exact count.
-__device__ __forceinline__ uint32_t tonemap_byte(float s, float exposure, float inv_gamma, const float *thr) {
-    const float e = s * exposure;
-    const float c = (0.0f < e) ? e : 0.0f;
-    const float x = c / (1.0f + c);
-    if (!(x >= 0.0f)) return 0u;   // c = inf: inf / inf = NaN, and the reference's lround(NaN) casts to 0
-    const float g = x > 0.0f ? __builtin_amdgcn_exp2f(inv_gamma * __builtin_amdgcn_logf(x)) : 0.0f;
-    int k = (int)fminf(fmaxf(g * 255.0f + 0.5f, 0.0f), 255.0f);
-    while (k < 255 && thr[k + 1] <= x) ++k;
-    while (k > 0 && thr[k] > x) --k;
-    return (uint32_t)k;
-}
+// tonemap_byte: shs_post_internal.hpp (shared with k_lib_resolve's fused tonemap)
 
 __device__ __forceinline__ void tonemap_pixel(const TonemapParams &p, const float *thr, int x, int y) {
     const float4 s = p.hdr[(size_t)y * p.W + x];

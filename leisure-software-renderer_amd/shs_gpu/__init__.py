@@ -270,6 +270,19 @@ class Context:
         self._check(self._lib.shs_tonemap(self._h, ctypes.byref(d)))
         self._tonemap_flags = d.flags
 
+    def fuse_tonemap(self, exposure: float = 1.0, gamma: float = 2.2, ldr: bool = True, present: bool = True,
+                     enable: bool = True):
+        """Fused PassTonemap: later camera passes also write the tonemap targets from their shading
+        kernel (the same bytes as tonemap() after the pass); enable=False turns it off."""
+        if not enable:
+            self._check(self._lib.shs_lib_fuse_tonemap(self._h, None))
+            return
+        d = _abi.TonemapDescC()
+        d.exposure, d.gamma = float(exposure), float(gamma)
+        d.flags = (_abi.TONEMAP_LDR if ldr else 0) | (_abi.TONEMAP_PRESENT if present else 0)
+        self._check(self._lib.shs_lib_fuse_tonemap(self._h, ctypes.byref(d)))
+        self._tonemap_flags = d.flags
+
     def resolve_ldr(self):
         """-> (ldr uint8 [H, W, 4] rows y up or None, present uint8 [H, W, 4] rows top-down or None)."""
         f = self._lib_frame

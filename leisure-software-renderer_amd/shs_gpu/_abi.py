@@ -234,6 +234,7 @@ SIGNATURES = [
     ("shs_lib_debug_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_lib_debug_setup_timeline", ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_tonemap", ctypes.c_int, [_P, ctypes.POINTER(TonemapDescC)]),
+    ("shs_lib_fuse_tonemap", ctypes.c_int, [_P, ctypes.POINTER(TonemapDescC)]),
     ("shs_resolve_ldr", ctypes.c_int, [_P, _P, _P]),
     ("shs_ldr_device_targets", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("shs_tonemap_thresholds", ctypes.c_int, [ctypes.c_float, _F]),

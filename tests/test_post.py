@@ -236,3 +236,64 @@ def test_motion_blur_nonfinite_motion_exact(oracle_mod):
     want = oracle_mod.motion_blur(ldr, depth, motion, min_velocity_px=0.0)
     bad = np.argwhere(got != want)
     assert bad.size == 0, f"{len(bad)} byte mismatches, first {bad[:4]}"
+
+
+# ---- fused PassTonemap (shs_lib_fuse_tonemap: the camera pass's shading kernel writes the bytes) ----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exposure,gamma,ldr,present", [(1.0, 2.2, True, True), (2.5, 2.2, False, True),
+                                                        (0.7, 1.0, True, False), (3.0, 0.0, True, True)])
+def test_fused_tonemap_matches_pass(oracle_mod, exposure, gamma, ldr, present):
+    """The fused bytes equal the oracle's PassTonemap of the same pass's HDR target, and a following
+    frame without fusion needs shs_tonemap again."""
+    import shs_gpu
+    from shs_gpu import ShsError
+    frame, draws = _c5(352, 200)
+    with shs_gpu.Context(0) as ctx:
+        ctx.fuse_tonemap(exposure, gamma, ldr=ldr, present=present)
+        ctx.render_pbr_forward(frame, draws)
+        got_ldr, got_pre = ctx.resolve_ldr()
+        hdr, _, _ = ctx.resolve_lib()
+        want_ldr, want_pre = oracle_mod.tonemap(hdr, exposure, gamma)
+        if ldr:
+            assert np.array_equal(got_ldr, want_ldr)
+        else:
+            assert got_ldr is None
+        if present:
+            assert np.array_equal(got_pre, want_pre)
+        else:
+            assert got_pre is None
+        ctx.fuse_tonemap(enable=False)
+        ctx.render_pbr_forward(frame, draws)
+        with pytest.raises(ShsError):
+            ctx.resolve_ldr()
+
+
+@pytest.mark.gpu
+def test_fused_tonemap_forward_plus_sharded(oracle_mod):
+    """Forward+ (the C4 program) with the fused tonemap: the whole frame's present bytes, and each
+    rank's tiles of a 3-way tile-sharded pass, equal the separate tonemap's."""
+    import shs_gpu
+    from shs_gpu import scene_lib
+    frame, draws, lights, cull = scene_lib.c4_scene(640, 352, n_objects=60, tris_per_object=200)
+    with shs_gpu.Context(0) as ctx:
+        ctx.upload_lights(lights)
+        ctx.light_cull(cull)
+        ctx.render_pbr_forward(frame, draws)
+        ctx.tonemap(1.0, 2.2, ldr=True, present=True)
+        want_ldr, want_pre = ctx.resolve_ldr()
+        ctx.fuse_tonemap(1.0, 2.2, ldr=True, present=True)
+        ctx.render_pbr_forward(frame, draws)
+        got_ldr, got_pre = ctx.resolve_ldr()
+        assert np.array_equal(got_ldr, want_ldr) and np.array_equal(got_pre, want_pre)
+        H, W = frame.height, frame.width
+        ty, tx = np.mgrid[0:H, 0:W]
+        tile = (ty // 32) * ((W + 31) // 32) + tx // 32          # rows y up (RT_ColorLDR)
+        for r in range(3):
+            frame.shard_rank, frame.shard_count = r, 3
+            cull.shard_rank, cull.shard_count = r, 3
+            ctx.light_cull(cull)
+            ctx.render_pbr_forward(frame, draws)
+            sl, _ = ctx.resolve_ldr()
+            own = tile % 3 == r
+            assert np.array_equal(sl[own], want_ldr[own]), f"rank {r}"
