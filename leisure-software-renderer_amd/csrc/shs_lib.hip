@@ -113,13 +113,12 @@ struct LVert {
     float u, v;
 };
 
-// The normal and UV varyings of a vertex (the half of make_default_vertex_out that only surviving
-// primitives need).
+// The normal varying of a vertex (the half of make_default_vertex_out that only surviving
+// primitives need; UV0 is not read by any builtin program, LibShade).
 __device__ __forceinline__ void vertex_attrs(const LibDrawGPU &dr, uint32_t id, LVert &o) {
-    const float *N = dr.nrm + 3 * (size_t)id, *U = dr.uv + 2 * (size_t)id;
+    const float *N = dr.nrm + 3 * (size_t)id;
     const f3 n = normalize3(m3v(dr.nmat, f3{N[0], N[1], N[2]}));
     o.nx = n.x; o.ny = n.y; o.nz = n.z;
-    o.u = U[0]; o.v = U[1];
 }
 
 // Clip and world position (the varyings are left 0 until vertex_attrs).
@@ -448,10 +447,9 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     for (int k = 0; k < 3; ++k) {
         s.wp[3 * k] = v[k]->wx * iw[k]; s.wp[3 * k + 1] = v[k]->wy * iw[k]; s.wp[3 * k + 2] = v[k]->wz * iw[k];
         s.n[3 * k] = v[k]->nx * iw[k]; s.n[3 * k + 1] = v[k]->ny * iw[k]; s.n[3 * k + 2] = v[k]->nz * iw[k];
-        s.uv[2 * k] = v[k]->u * iw[k]; s.uv[2 * k + 1] = v[k]->v * iw[k];
     }
     s.draw = d;
-    s.pad[0] = s.pad[1] = s.pad[2] = 0;
+    s.pad = 0;
     if (!(fp.exp_flags & 1u)) fb.shade[slot] = s;
     store_box(fb, slot, x0, x1, y0, y1);
     if (fp.exp_flags & 2u) return;

@@ -45,15 +45,17 @@ struct alignas(16) LibRec {
 };
 static_assert(sizeof(LibRec) == 64, "LibRec must stay 64 B");
 
-// Perspective-premultiplied varyings of the primitive's corners (varw, rasterizer.hpp:309-328).
+// Perspective-premultiplied varyings of the primitive's corners (varw, rasterizer.hpp:309-328) that
+// the builtin programs read.  The UV0 varying is not kept: no builtin program samples a texture
+// (base_color_tex is out of scope), so it would be 24 B per primitive written
+// and never read.
 struct alignas(16) LibShade {
     float wp[9];                 // WorldPos varying * 1/w
     float n[9];                  // NormalWS varying * 1/w
-    float uv[6];                 // UV0 varying * 1/w
     int32_t draw;
-    int32_t pad[3];
+    int32_t pad;
 };
-static_assert(sizeof(LibShade) == 112, "LibShade must stay 112 B");
+static_assert(sizeof(LibShade) == 80, "LibShade must stay 80 B");
 
 // CullingLightGPU (lighting/light_types.hpp:141-166), 160 B, as the caller uploads it.
 struct alignas(16) CullLight {

@@ -25,6 +25,7 @@ def main():
         frame, draws, casters, sun, S = scene_lib.c5_scene(3840, 2160, 2048)
         lvp = ctx.render_shadow_map(S, sun, casters)
         scene_lib.wire_shadow(draws, lvp)
+    ctx.fuse_tonemap(1.0, 2.2, ldr=False, present=True)
     for N in ns:
         per_rank = []
         for r in range(N):
@@ -39,7 +40,7 @@ def main():
                 else:
                     ctx.render_shadow_map(S, sun, casters)
                 ctx.render_pbr_forward_prepared(prep)
-                ctx.tonemap(1.0, 2.2, ldr=False, present=True)
+                pass  # tonemap fused into the camera pass (ctx.fuse_tonemap)
 
             for _ in range(3):
                 one()
