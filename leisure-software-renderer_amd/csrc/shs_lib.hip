@@ -1108,20 +1108,30 @@ __device__ __forceinline__ void point_light(const PLight &L, f3 world, f3 N, f3 
     lit = add3(lit, add3(mul3(base, sc3(rad, ndotl)), sc3(rad, spec)));
 }
 
-// The light lists of the raster tile being resolved, staged in LDS (k_lib_raster, tile lists only):
-// list hdr[4 + s] holds hdr[s] (already capped at max_per_tile) indices at ids[s * LT_STAGE_CAP ..].
-constexpr int LT_STAGE_CAP = 256, LT_STAGE_MAX = 4;
-struct LtStage {
-    const uint32_t *ids = nullptr;
-    const uint32_t *hdr = nullptr;
-    int n = 0;
+// The Forward+ list of one resolve wave's 16x4 pixel block when every lane of the wave reads the same
+// list (tiled modes, light tiles a multiple of 16 x 4 px): its count and indices copied into the
+// wave's own LDS slice (<= 128 entries) by the whole wave, so the shading loop reads one broadcast
+// index per light -- no workgroup barrier (a wave's LDS accesses are in order).  (Not v_readlane of
+// per-lane registers: inside the shading branch the compiler may copy such a register for the active
+// lanes only, leaving the other lanes' entries stale.)  list = ~0: per-lane lists.
+struct LtWave {
+    uint32_t list = 0xffffffffu;
+    uint32_t count = 0;
+    const uint32_t *ids = nullptr;   // LDS
 };
+
+// The pixel's tile list (tiled modes; fp_stress_scene.frag:644-652 tile index).
+__device__ __forceinline__ uint32_t lt_tile_list(const LibFrameParams &fp, int px, int py) {
+    const uint32_t ts = fp.lt_size;
+    const uint32_t tx = min((uint32_t)px / ts, fp.lt_tx - 1u), ty = min((uint32_t)(fp.H - 1 - py) / ts, fp.lt_ty - 1u);
+    return ty * fp.lt_tx + tx;
+}
 
 // Forward+ program: the pixel's light list (fp_stress_scene.frag:644-685 selection: a saturated list
 // falls back to every light) through PointLightModel::sample, combined as the software light-culling
 // demo does (hello_light_types_culling_sw.cpp:404-416): ambient hemisphere + sum, clamped to [0,1].
 __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, int px, int py,
-                           const LtStage &st) {
+                           const LtWave &lw) {
     const f3 N = normalize3(nrm);
     f3 V = sub3(f3{dr.cam[0], dr.cam[1], dr.cam[2]}, world);
     const float vl2 = dot3(V, V);
@@ -1132,7 +1142,7 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
     f3 lit = sc3(base, amb);
     const uint32_t ts = fp.lt_size, maxp = fp.lt_maxp;
     const uint32_t tx = min((uint32_t)px / ts, fp.lt_tx - 1u), ty = min((uint32_t)(fp.H - 1 - py) / ts, fp.lt_ty - 1u);
-    uint32_t list = ty * fp.lt_tx + tx;
+    uint32_t list = lt_tile_list(fp, px, py);
     if (fp.lt_mode == 3u) {   // cluster_slice_from_view_depth (fp_stress_scene.frag:525-533)
         const float vz = (fp.lt_view_z[0] * world.x + fp.lt_view_z[1] * world.y) + (fp.lt_view_z[2] * world.z + fp.lt_view_z[3] * 1.0f);
         const float near_z = s_max(fp.lt_zn, 0.001f), far_z = s_max(fp.lt_zf, near_z + 0.01f);
@@ -1141,18 +1151,15 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
         const float zi = g_clamp(floorf(t * (float)fp.lt_zs), 0.0f, (float)(fp.lt_zs - 1u));
         list = ((uint32_t)zi * fp.lt_ty + ty) * fp.lt_tx + tx;
     }
-    const bool lds = fp.n_lights <= (uint32_t)LIB_LDS_LIGHTS;   // k_lib_raster staged them
-    int s_st = -1;
-    for (int s = 0; s < st.n; ++s)
-        if (st.hdr[LT_STAGE_MAX + s] == list) s_st = s;
-    const uint32_t count = s_st >= 0 ? st.hdr[s_st] : fp.lt_mode == 0u ? maxp : min(fb.tile_counts[list], maxp);
+    const bool lds = fp.n_lights <= (uint32_t)LIB_LDS_LIGHTS;   // k_lib_resolve staged them
+    const bool uni = lw.list != 0xffffffffu;   // wave-uniform: every lane's list is lw.list
+    const uint32_t count = uni ? lw.count : fp.lt_mode == 0u ? maxp : min(fb.tile_counts[list], maxp);
     if (count >= maxp) {
         for (uint32_t i = 0; i < fp.n_lights; ++i)
             point_light(lds ? plight_lds(i) : plight_global(fb.lights[i]), world, N, V, base, lit);
-    } else if (s_st >= 0) {   // the list in LDS
-        const uint32_t *ids = st.ids + s_st * LT_STAGE_CAP;
+    } else if (uni) {   // the list in the wave's LDS slice: one broadcast index per light
         for (uint32_t i = 0; i < count; ++i) {
-            const uint32_t idx = ids[i];
+            const uint32_t idx = lw.ids[i];
             if (idx < fp.n_lights) point_light(lds ? plight_lds(idx) : plight_global(fb.lights[idx]), world, N, V, base, lit);
         }
     } else {
@@ -1173,7 +1180,7 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
 // registers are live); -1: per draw.
 template <int PROG>
 __device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, float depth01,
-                           int px, int py, const LtStage &st) {
+                           int px, int py, const LtWave &st) {
     const f3 bc = {dr.base[0], dr.base[1], dr.base[2]};
     const int program = PROG >= 0 ? PROG : dr.program;
     if (program == 5) return forward_plus(fp, fb, dr, world, nrm, px, py, st);
@@ -1275,13 +1282,13 @@ __device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
 template <int PROG>
 __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
                                          const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv,
-                                         const LtStage &st);
+                                         const LtWave &st);
 
 // Resolve one pixel of a tile (one thread): the winner of the key array is re-evaluated with the
 // identical arithmetic, shaded and written; pixels without a winner get the clear values.
 template <bool SHADOW, int PROG = -1>
 __device__ __forceinline__ float4 lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, unsigned long long key, int px,
-                                              int py, bool &covered, const LtStage &st = LtStage{}) {
+                                              int py, bool &covered, const LtWave &st = LtWave{}) {
     covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
     if (px >= fp.W || py >= fp.H) return make_float4(0.f, 0.f, 0.f, 0.f);
     const size_t o = (size_t)py * fp.W + px;
@@ -1316,7 +1323,7 @@ __device__ __forceinline__ float4 lib_resolve(const LibFrameParams &fp, const Li
 template <int PROG>
 __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
                                          const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv,
-                                         const LtStage &st) {
+                                         const LtWave &st) {
     {
         float z01, u, v, w, idn;
         lib_test<false>(fp, r, px, py, z01, u, v, w, idn);
@@ -1736,60 +1743,29 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
     }
 }
 
-// Forward+ tile lists: the (<= LT_STAGE_MAX) light lists under one raster tile go to LDS, so the
-// per-light index loads of its pixels hit LDS.  Block-uniform; ends with a barrier when it stages.
-__device__ __forceinline__ void stage_tile_lists(const LibFrameParams &fp, const LibBuffers &fb, int X0, int Y0, uint32_t *hdr,
-                                                 uint32_t *ids, LtStage &st) {
-    const int tid = threadIdx.x;
-    const int X1 = X0 + LIB_RTW - 1, Y1 = Y0 + LIB_RTH - 1;
-    if (!fb.tile_counts || !(fp.lt_mode == 1u || fp.lt_mode == 2u) || fp.lt_maxp > (uint32_t)LT_STAGE_CAP || X0 >= fp.W ||
-        Y0 >= fp.H)
-        return;
-    const uint32_t ts = fp.lt_size;
-    const int tx0 = min((uint32_t)X0 / ts, fp.lt_tx - 1u), tx1 = min((uint32_t)min(X1, fp.W - 1) / ts, fp.lt_tx - 1u);
-    const int ty0 = min((uint32_t)(fp.H - 1 - min(Y1, fp.H - 1)) / ts, fp.lt_ty - 1u);
-    const int ty1 = min((uint32_t)(fp.H - 1 - Y0) / ts, fp.lt_ty - 1u);
-    const int ntx = tx1 - tx0 + 1, n = ntx * (ty1 - ty0 + 1);
-    if (n > LT_STAGE_MAX) return;
-    if (tid < n) {   // hdr [0, 4): counts, [4, 8): list ids
-        const uint32_t list = (uint32_t)(ty0 + tid / ntx) * fp.lt_tx + (uint32_t)(tx0 + tid % ntx);
-        hdr[LT_STAGE_MAX + tid] = list;
-        hdr[tid] = min(fb.tile_counts[list], fp.lt_maxp);
-    }
-    __syncthreads();
-    for (int i = tid; i < n * LT_STAGE_CAP; i += 256) {
-        const int s2 = i / LT_STAGE_CAP, j = i % LT_STAGE_CAP;
-        if ((uint32_t)j < hdr[s2]) ids[i] = fb.tile_indices[(size_t)hdr[LT_STAGE_MAX + s2] * fp.lt_maxp + j];
-    }
-    __syncthreads();
-    st.ids = ids;
-    st.hdr = hdr;
-    st.n = n;
-}
-
 // The camera pass's resolve (rasterizer.hpp:341-419 per winner): every owned raster tile's pixels,
 // their winning key from k_lib_raster re-evaluated, shaded and written; pixels without a winner get
-// the clear values.  Persistent (tile j = b + i * G in k_lib_raster's order); the Forward+ lights and
-// each tile's light lists are staged in LDS.  A separate kernel: the shading's register and LDS
-// footprint stays out of the raster's (more raster workgroups per CU), and the shading's dependent
-// loads (key -> record -> draw -> shadow map) overlap across many more waves than one raster tile's.
-// Minimum waves per SIMD: 4 for the single-program kernels (no spills at 128 VGPRs), 3 for the mixed
-// one (its 137 VGPRs; 4 would spill); -DSHS_RESOLVE_WAVES_FP / _PBR override (timing experiments).
+// the clear values.  Each wave independently takes 16x4 pixel blocks (4 per raster tile, tiles in
+// k_lib_raster's order, block w + i * waves): no barrier after the Forward+ lights are staged in LDS
+// at the start, so the waves' dependent loads (key -> record -> draw -> shadow map) and shading
+// overlap freely.  A separate kernel: the shading's register and LDS footprint stays out of the
+// raster's.  With fb.tm_thr the pixel's HDR value is also tonemapped (fused PassTonemap).
 #ifndef SHS_RESOLVE_WAVES_FP
 #define SHS_RESOLVE_WAVES_FP 4
 #endif
 #ifndef SHS_RESOLVE_WAVES_PBR
 #define SHS_RESOLVE_WAVES_PBR 4
 #endif
+// Minimum waves per SIMD: 4 for the single-program kernels (no spills), 3 for the mixed one
+// (-DSHS_RESOLVE_WAVES_FP / _PBR override: timing experiments).
 template <int PROG>
 __global__ __launch_bounds__(256, PROG == 5 ? SHS_RESOLVE_WAVES_FP : PROG == 0 ? SHS_RESOLVE_WAVES_PBR : 3)
 void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
-    __shared__ uint32_t lt_hdr[2 * LT_STAGE_MAX];
-    __shared__ uint32_t lt_ids[LT_STAGE_MAX * LT_STAGE_CAP];
     __shared__ float tm_thr[256];
+    __shared__ uint32_t wlist[PROG == 0 ? 1 : 4][128];   // per wave: its block's light list (LtWave)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (fb.tm_thr) tm_thr[tid] = fb.tm_thr[tid];
-    if (fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights (read after the tile syncs)
+    if (PROG != 0 && fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights
         for (int i = tid; i < fp.n_lights; i += 256) {
             const PLight p = plight_global(fb.lights[i]);
             lib_lds_lights[4 * i] = p.pr;
@@ -1798,18 +1774,41 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
             lib_lds_lights[4 * i + 3] = make_float4(__uint_as_float(p.model), 0.0f, 0.0f, 0.0f);
         }
     }
-    for (int j = (int)blockIdx.x; j < fp.n_owned_rt; j += (int)gridDim.x) {   // block-uniform
-        __syncthreads();   // lights staged / the previous tile's lists read
-        const int rt = fb.rt_order[j];
-        const int X0 = (rt % fp.tiles_x) * LIB_RTW, Y0 = (rt / fp.tiles_x) * LIB_RTH;
-        LtStage st;
-        stage_tile_lists(fp, fb, X0, Y0, lt_hdr, lt_ids, st);
-        // a wave takes a 16x4 block (one 16-px light tile wide, so Forward+ lanes share a list)
-        const int px = X0 + 16 * (wave & 1) + (lane & 15), py = Y0 + 4 * (wave >> 1) + (lane >> 4);
-        const unsigned long long key = (px < fp.W && py < fp.H) ? fb.keys[(size_t)py * fp.W + px] : KEY_EMPTY;
+    __syncthreads();
+    // tiled Forward+ lists can be wave-uniform (LtWave); clustered ones depend on the pixel's depth
+    const bool tiled = PROG != 0 && fb.tile_counts && (fp.lt_mode == 1u || fp.lt_mode == 2u) && fp.lt_maxp <= 128u;
+    const int n_blocks = 4 * fp.n_owned_rt;
+    for (int blk = 4 * (int)blockIdx.x + wave; blk < n_blocks; blk += 4 * (int)gridDim.x) {   // wave-uniform
+        const int rt = fb.rt_order[blk >> 2], sub = blk & 3;
+        const int px = (rt % fp.tiles_x) * LIB_RTW + 16 * (sub & 1) + (lane & 15);
+        const int py = (rt / fp.tiles_x) * LIB_RTH + 4 * (sub >> 1) + (lane >> 4);
+        const bool inb = px < fp.W && py < fp.H;
+        const unsigned long long key = inb ? fb.keys[(size_t)py * fp.W + px] : KEY_EMPTY;
+        LtWave lw;
+#ifdef SHS_RESOLVE_NO_LTWAVE
+        if (false) {
+#else
+        if (tiled && __ballot(key != KEY_EMPTY && inb) != 0ull) {
+#endif
+            const uint32_t list = lt_tile_list(fp, min(px, fp.W - 1), min(py, fp.H - 1));
+            const uint32_t l0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)list);
+            if (__ballot(list != l0) == 0ull) {   // every lane active here: the VGPR entries are whole
+                const uint32_t cnt = min(fb.tile_counts[l0], fp.lt_maxp);
+                const uint32_t *ids = fb.tile_indices + (size_t)l0 * fp.lt_maxp;
+                uint32_t *wl = wlist[PROG == 0 ? 0 : wave];
+                lw.list = l0;
+                lw.count = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
+                lw.ids = wl;
+                __builtin_amdgcn_wave_barrier();   // the previous block's reads of the slice are issued
+                if ((uint32_t)lane < lw.count) wl[lane] = ids[lane];
+                if ((uint32_t)(64 + lane) < lw.count) wl[64 + lane] = ids[64 + lane];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
         bool covered;
-        const float4 c = lib_resolve<false, PROG>(fp, fb, key, px, py, covered, st);
-        if (fb.tm_thr && px < fp.W && py < fp.H) {   // fused PassTonemap of this pixel's HDR value
+        const float4 c = lib_resolve<false, PROG>(fp, fb, key, px, py, covered, lw);
+        if (fb.tm_thr && inb) {   // fused PassTonemap of this pixel's HDR value
             const uint32_t rgba = tonemap_byte(c.x, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) |
                                   (tonemap_byte(c.y, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) << 8) |
                                   (tonemap_byte(c.z, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) << 16) | (255u << 24);
