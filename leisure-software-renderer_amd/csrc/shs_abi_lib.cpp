@@ -57,6 +57,10 @@ void release_work(Work &w) {
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
     release(w.spill); release(w.blk_stat); release(w.rstat); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
+    if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
+    if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
+    w.raster_ev = w.resolve_ev = nullptr;
+    w.resolve_ev_valid = false;
     for (int i = 0; i < 2; ++i) {
         if (w.h_draws[i]) (void)hipHostFree(w.h_draws[i]);
         if (w.slot_ev[i]) (void)hipEventDestroy(w.slot_ev[i]);
@@ -114,7 +118,7 @@ void build_lib_draw(const shs_lib_draw &in, const Mesh &m, int32_t base, LibDraw
 // Upload the draw table through the work's pinned 2-slot staging.  A table equal to the one the
 // device buffer already holds (a prepared pass re-rendered) is not sent again: the stream-ordered copy
 // is a DMA between two kernels, ~20 us of idle GPU per frame.
-int upload_draws(shs_ctx *ctx, Work &w, const std::vector<LibDrawGPU> &d) {
+int upload_draws(shs_ctx *ctx, Work &w, const std::vector<LibDrawGPU> &d, hipStream_t st) {
     const size_t n = std::max<size_t>(d.size(), 1);
     if (ensure(ctx, w.draws, n)) return SHS_ERR_HIP;
     if (w.dev_table_at == w.draws.p && w.dev_table_cap == w.draws.cap && w.dev_table.size() == d.size() &&
@@ -137,9 +141,9 @@ int upload_draws(shs_ctx *ctx, Work &w, const std::vector<LibDrawGPU> &d) {
     }
     if (!d.empty()) {
         std::memcpy(w.h_draws[s], d.data(), d.size() * sizeof(LibDrawGPU));
-        HIP_TRY(ctx, hipMemcpyAsync(w.draws.p, w.h_draws[s], d.size() * sizeof(LibDrawGPU), hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(w.draws.p, w.h_draws[s], d.size() * sizeof(LibDrawGPU), hipMemcpyHostToDevice, st));
     }
-    HIP_TRY(ctx, hipEventRecord(w.slot_ev[s], ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(w.slot_ev[s], st));
     w.slot_used[s] = true;
     w.dev_table = d;
     w.dev_table_at = w.draws.p;
@@ -191,6 +195,20 @@ std::vector<int32_t> build_rt_order(int tiles_x, int tiles_y, int rtiles_y, int 
 // kernels.  shadow: PassShadowMap's depth pass into ctx->shadow_map.
 int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     LibFrameParams fp = w.last_fp;
+    // After a shadow pass, the camera pass's setup and raster run on the side stream
+    // (ctx->setup_stream): they read only the meshes and the draw table, so they overlap the shadow
+    // pass on the main stream (C5 0.573 -> 0.555 ms/frame; without one the two event hops cost more
+    // than the light cull they could overlap, C4 at N = 8 0.255 -> 0.279 ms).  They wait for the
+    // previous camera resolve (it reads the records, the draw table and the keys this pass rewrites);
+    // the resolve waits for the raster.
+    hipStream_t ps = (shadow || !ctx->cam_after_shadow) ? ctx->stream : ctx->setup_stream;
+    if (!shadow) {
+        if (!w.raster_ev) {
+            HIP_TRY(ctx, hipEventCreateWithFlags(&w.raster_ev, hipEventDisableTiming));
+            HIP_TRY(ctx, hipEventCreateWithFlags(&w.resolve_ev, hipEventDisableTiming));
+        }
+        if (w.resolve_ev_valid && ps != ctx->stream) HIP_TRY(ctx, hipStreamWaitEvent(ps, w.resolve_ev, 0));
+    }
     const int W = fp.W, H = fp.H;
     const int tiles_x = (W + shs_dev::TILE - 1) / shs_dev::TILE, tiles_y = (H + shs_dev::TILE - 1) / shs_dev::TILE;
     const int n_tiles = tiles_x * tiles_y;
@@ -227,15 +245,15 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         reset = true;
     }
     if (reset) {
-        HIP_TRY(ctx, hipMemsetAsync(w.tile_count.p, 0, w.tile_count.cap * sizeof(uint32_t), ctx->stream));
-        HIP_TRY(ctx, hipMemsetAsync(w.busy.p, 0, w.busy.cap * sizeof(uint32_t), ctx->stream));
-        HIP_TRY(ctx, hipMemsetAsync(w.counters.p, 0, w.counters.cap * sizeof(uint32_t), ctx->stream));
-        HIP_TRY(ctx, hipMemsetAsync(w.rqueue.p, 0, w.rqueue.cap * sizeof(uint32_t), ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // the previous order's upload is done with h_rt_order
+        HIP_TRY(ctx, hipMemsetAsync(w.tile_count.p, 0, w.tile_count.cap * sizeof(uint32_t), ps));
+        HIP_TRY(ctx, hipMemsetAsync(w.busy.p, 0, w.busy.cap * sizeof(uint32_t), ps));
+        HIP_TRY(ctx, hipMemsetAsync(w.counters.p, 0, w.counters.cap * sizeof(uint32_t), ps));
+        HIP_TRY(ctx, hipMemsetAsync(w.rqueue.p, 0, w.rqueue.cap * sizeof(uint32_t), ps));
+        HIP_TRY(ctx, hipStreamSynchronize(ps));   // the previous order's upload is done with h_rt_order
         w.h_rt_order = build_rt_order(tiles_x, tiles_y, rtiles_y, fp.rank, fp.count, st);
         if (ensure(ctx, w.rt_order, std::max<size_t>(w.h_rt_order.size(), 1))) return SHS_ERR_HIP;
         HIP_TRY(ctx, hipMemcpyAsync(w.rt_order.p, w.h_rt_order.data(), w.h_rt_order.size() * sizeof(int32_t),
-                                    hipMemcpyHostToDevice, ctx->stream));
+                                    hipMemcpyHostToDevice, ps));
         w.geom_key = gkey;
     }
     if (ensure(ctx, w.bins, (size_t)n_tiles * w.bin_cap)) return SHS_ERR_HIP;
@@ -257,7 +275,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         while (d + 1 < (int)nd && w.last_draws[d + 1].tri_base <= b * 256) ++d;
         ints[nd + 1 + b] = d;
     }
-    if (upload_draws(ctx, w, table)) return SHS_ERR_HIP;
+    if (upload_draws(ctx, w, table, ps)) return SHS_ERR_HIP;
 
     fp.tiles_x = tiles_x; fp.tiles_y = tiles_y; fp.rtiles_y = rtiles_y;
     fp.n_tris = n_tris;
@@ -325,11 +343,11 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         if (ctx->want_timeline) {
             const size_t n = (size_t)raster_grid * shs_dev::LTL_STRIDE;
             if (ensure(ctx, ctx->lib_timeline, n)) return SHS_ERR_HIP;
-            HIP_TRY(ctx, hipMemsetAsync(ctx->lib_timeline.p, 0, n * sizeof(uint64_t), ctx->stream));
+            HIP_TRY(ctx, hipMemsetAsync(ctx->lib_timeline.p, 0, n * sizeof(uint64_t), ps));
             fb.timeline = ctx->lib_timeline.p;
             const size_t ns = (size_t)std::max(setup_blocks, 1) * shs_dev::STL_STRIDE;
             if (ensure(ctx, ctx->lib_stimeline, ns)) return SHS_ERR_HIP;
-            HIP_TRY(ctx, hipMemsetAsync(ctx->lib_stimeline.p, 0, ns * sizeof(uint64_t), ctx->stream));
+            HIP_TRY(ctx, hipMemsetAsync(ctx->lib_stimeline.p, 0, ns * sizeof(uint64_t), ps));
             fb.stimeline = ctx->lib_stimeline.p;
         }
     }
@@ -343,11 +361,15 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         ev = w.ring_ev[k];
         w.ring_pending[k] = true;
     }
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], ctx->stream));
-    HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, ctx->stream));
-    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], ctx->stream));
-    HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, raster_grid, ctx->stream));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], ps));
+    HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, ps));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], ps));
+    HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, raster_grid, ps));
     if (!shadow) {   // the camera pass's shading runs in its own kernel (event [2] closes both)
+        if (ps != ctx->stream) {
+            HIP_TRY(ctx, hipEventRecord(w.raster_ev, ps));
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, w.raster_ev, 0));
+        }
         int prog = w.last_draws.empty() ? -1 : w.last_draws[0].program;
         for (const auto &d : w.last_draws)
             if (d.program != prog) prog = -1;
@@ -356,6 +378,8 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         if (res <= 0) res = shs_internal::lib_resolve_resident_blocks(ctx->device, prog);
         const int rgrid = std::max(1, std::min(fp.n_owned_rt, res));
         HIP_TRY(ctx, shs_internal::launch_lib_resolve(fp, fb, prog, rgrid, ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(w.resolve_ev, ctx->stream));
+        w.resolve_ev_valid = true;
     }
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], ctx->stream));
     w.last_parity = fp.parity;

@@ -126,6 +126,8 @@ struct shs_ctx {
         DevBuf<int32_t> rt_order;                          // k_lib_raster tile order (built per geometry)
         std::vector<int32_t> h_rt_order;                   // its host copy (alive while the upload runs)
         bool tm_fused = false;                             // camera pass: the fused tonemap of tm_desc
+        hipEvent_t raster_ev = nullptr, resolve_ev = nullptr;   // camera pass: side-stream raster done, resolve done
+        bool resolve_ev_valid = false;
         shs_tonemap_desc tm_desc{};
         DevBuf<uint2> spill, blk_stat, rstat;
         shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots
