@@ -2,7 +2,7 @@
 against the CPU oracle (oracle/shs_oracle_lib.c), through the C ABI.
 
 Coverage, depth (z01) and the shadow map: bit-exact.  HDR colour and motion vectors: within 1e-5 per
-channel (relative above 1), helpers.assert_float_close."""
+channel, absolute (helpers.assert_float_close)."""
 import numpy as np
 import pytest
 
@@ -165,3 +165,22 @@ def test_lib_shards_compose(gpu_ctx):
                     oh[sl], od[sl] = h[sl], d[sl]
     assert np.array_equal(oh.view(np.uint32), fh.view(np.uint32))
     assert np.array_equal(od.view(np.uint32), fd.view(np.uint32))
+
+
+def test_back_to_back_frames_no_host_sync(gpu_ctx, oracle_mod):
+    """Two shadow + camera frames enqueued without a host sync between them: the second camera pass's
+    setup / raster run on the side stream beside its shadow pass and must wait only for the first
+    frame's resolve; the resolved targets are the second frame's, exactly."""
+    from shs_gpu import scene_lib
+    frames = [scene_lib.c5_scene(352, 200, 256, yaw=y) for y in (0.0, 23.0)]
+    for frame, draws, casters, sun, S in frames:        # no resolve in between
+        lvp = gpu_ctx.render_shadow_map(S, sun, casters)
+        scene_lib.wire_shadow(draws, lvp)
+        gpu_ctx.render_pbr_forward(frame, draws)
+    gh, gd, gm = gpu_ctx.resolve_lib()
+    frame, draws, casters, sun, S = frames[1]
+    sm_ref, _ = oracle_mod.shadow_map(S, sun, casters)
+    rh, rd, rm, _ = oracle_mod.pbr_forward(frame, draws, sm_ref)
+    assert_depth_bitexact(gd, rd)
+    assert_float_close(gm, rm, what="motion")
+    assert_float_close(gh, rh, what="hdr")

@@ -1,5 +1,14 @@
-import sys, numpy as np
-sys.path[:0]=['/root/repo/leisure-software-renderer_amd','/root/repo','/root/repo/tests']
+"""Forward+ debugging aid (GPU box): renders the small tiled-mode Forward+ scene of
+tests/test_light_parity.py on the GPU and with the oracle and lists the 16x4 resolve blocks whose HDR
+differs beyond 1e-5 (with their light lists), e.g. to bisect a resolve-kernel change with
+SHS_GPU_LIB=<variant build>.  usage: python tools/dbg_forward_plus.py"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "leisure-software-renderer_amd"), ROOT]
 import shs_gpu
 from shs_gpu import scene_lib
 from oracle import oracle
