@@ -1222,8 +1222,11 @@ constexpr int STRIP_RT = 2;   // raster-tile rows per clear item
 // ticket queues -- queue q deals items G + q + N_WORKQ * j to the workgroups b = q (mod N_WORKQ) --
 // fetched one item ahead.  Every owned pixel of every frame is written exactly once: by its busy
 // tile or by its strip.
+#ifndef SHS_LEGACY_RASTER_WAVES
+#define SHS_LEGACY_RASTER_WAVES 4   // minimum waves per SIMD (-D...: timing experiments)
+#endif
 template <bool KARG>
-__global__ __launch_bounds__(256, 4) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
+__global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
     const int tid = threadIdx.x;
     uint32_t *cnt = fb.counters + fp.parity * CSET;
