@@ -296,8 +296,12 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         fp.exp_flags = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
     }
     fp.n_owned_rt = (int)w.h_rt_order.size();
-    int &resident = ctx->lib_resident[shadow ? 1 : 0];
-    if (resident <= 0) resident = shs_internal::lib_raster_resident_blocks(ctx->device, shadow);
+    // the shallow raster (256-candidate rounds, twice the workgroups per CU) when the previous frame's
+    // fullest bin tile fit one such round (scan mode: every primitive is a candidate)
+    const uint64_t fullest = fp.scan_mode ? (uint64_t)n_tris + (shadow ? 0u : w.st_extra) : w.st_maxbin;
+    const bool shallow = w.st_checked && fullest <= 256u;
+    int &resident = ctx->lib_resident[shadow ? 1 : 0][shallow ? 1 : 0];
+    if (resident <= 0) resident = shs_internal::lib_raster_resident_blocks(ctx->device, shadow, shallow);
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt, resident));
     if (ensure(ctx, w.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
 
@@ -364,7 +368,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], ps));
     HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, ps));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], ps));
-    HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, raster_grid, ps));
+    HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, shallow, raster_grid, ps));
     if (!shadow) {   // the camera pass's shading runs in its own kernel (event [2] closes both)
         if (ps != ctx->stream) {
             HIP_TRY(ctx, hipEventRecord(w.raster_ev, ps));
@@ -414,6 +418,7 @@ int check_pass(shs_ctx *ctx, Work &w, bool &grew) {
     w.st_spill = c[shs_dev::LC_SPILL];
     w.st_extra = c[shs_dev::LC_EXTRA];
     if (w.st_maxbin > w.bin_cap) w.bin_cap = next_pow2(std::min<uint64_t>(w.st_maxbin, 1u << 24));
+    w.st_checked = true;
     const uint32_t ov = c[shs_dev::LC_OVERFLOW];
     if (ov & shs_dev::LOV_SPILL) {
         const size_t need = c[shs_dev::LC_SPILL];

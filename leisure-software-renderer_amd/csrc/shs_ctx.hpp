@@ -139,6 +139,7 @@ struct shs_ctx {
         uint32_t bin_cap = 256, extra_cap = 0, frame_index = 0, last_parity = 0;
         int last_setup_blocks = 0, last_raster_grid = 0, last_n_tris = 0;
         bool need_check = false, done = false;
+        bool st_checked = false;                           // st_* hold a finished pass's statistics
         uint64_t st_clip = 0, st_raster = 0, st_covered = 0, st_maxbin = 0, st_spill = 0, st_extra = 0;
         std::vector<shs_dev::LibDrawGPU> last_draws;   // host copies (re-issue on overflow)
         std::vector<shs_dev::LibDrawGPU> dev_table;    // what w.draws holds (upload skipped when equal)
@@ -154,7 +155,7 @@ struct shs_ctx {
         int64_t acc_n = 0;
     };
     LibWork lib_cam, lib_shadow;
-    int lib_resident[2] = {0, 0};         // resident k_lib_raster workgroups (camera, shadow)
+    int lib_resident[2][2] = {{0, 0}, {0, 0}};   // resident k_lib_raster workgroups [camera, shadow][deep, shallow]
     DevBuf<uint64_t> lib_timeline;        // SHS_OPT_TIMELINE, camera pass raster
     DevBuf<uint64_t> lib_stimeline;       // SHS_OPT_TIMELINE, camera pass setup
     DevBuf<float4> lib_hdr;

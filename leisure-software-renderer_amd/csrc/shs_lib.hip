@@ -61,7 +61,11 @@ __device__ __forceinline__ f4 m4v(const float *m, f4 v) {
 }
 
 constexpr int LIB_RTW = 32, LIB_RTH = 8;   // raster tile (one 256-thread workgroup, one pixel per lane)
-constexpr int LIB_CAND = 1024;             // candidate ids gathered per round
+// Candidate ids gathered per round: k_lib_raster comes in two sizes.  1024 (3 workgroups per CU by
+// LDS, 119 VGPRs): deep per-tile lists (C4: up to ~6K candidates per bin tile, depth-sorted per round).
+// 256 (24 KB LDS, 80 VGPRs: 6 workgroups per CU): passes whose fullest bin tile fits one round (C5's
+// 62), chosen from the previous frame's statistics (LibWork::st_maxbin).
+constexpr int LIB_CAND_DEEP = 1024, LIB_CAND_SHALLOW = 256;
 constexpr int LIB_CHUNK = 128;             // records staged in LDS per pass
 constexpr int MAX_POLY = 16;               // clipped polygon capacity (3 + 6 planes x up to 2 crossings)
 
@@ -1249,6 +1253,7 @@ __device__ __forceinline__ float4 bg_color(const LibFrameParams &fp, int y) {
 
 constexpr int LIB_PAIR_WORDS = LIB_CHUNK * LIB_RTW * LIB_RTH / 64;   // pair-start bitmap words
 
+template <int LIB_CAND>
 struct LibShared {
     float4 rec[LIB_CHUNK * 4];            // staged records (8 KB)
     unsigned long long key[LIB_RTH * LIB_RTW];
@@ -1355,8 +1360,8 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
     }
 }
 
-template <bool SHADOW>
-__device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared &sh,
+template <bool SHADOW, int LIB_CAND>
+__device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared<LIB_CAND> &sh,
                                 uint32_t &chunk) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool hiz = SHADOW || (fp.flags & LF_DEPTH);   // painter's order (no depth target): never
@@ -1677,9 +1682,9 @@ __device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const L
     }
 }
 
-template <bool SHADOW>
-__global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
-    __shared__ LibShared sh;
+template <bool SHADOW, int LIB_CAND>
+__global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
+    __shared__ LibShared<LIB_CAND> sh;
     const int tid = threadIdx.x;
     const uint32_t *cnt = fb.counters + fp.parity * LC_N;
     const int G = (int)gridDim.x;
@@ -1706,7 +1711,7 @@ __global__ __launch_bounds__(256, 3) void k_lib_raster(LibFrameParams fp, LibBuf
         {
             const int rt = fb.rt_order[j];
             if (fb.busy[rt]) {
-                lib_raster_tile<SHADOW>(fp, fb, cnt, rt, sh, chunk);
+                lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk);
             } else {
                 const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
                 lib_clear_tile<SHADOW>(fp, fb, rt);
@@ -1840,12 +1845,15 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
     return hipGetLastError();
 }
 
-int lib_raster_resident_blocks(int device, bool shadow) {
+#define SHS_RASTER_KERNEL(shadow, shallow)                                                                   \
+    ((shadow) ? ((shallow) ? k_lib_raster<true, LIB_CAND_SHALLOW> : k_lib_raster<true, LIB_CAND_DEEP>)         \
+              : ((shallow) ? k_lib_raster<false, LIB_CAND_SHALLOW> : k_lib_raster<false, LIB_CAND_DEEP>))
+
+int lib_raster_resident_blocks(int device, bool shadow, bool shallow) {
     // persistent grid: every workgroup resident at once (CUs x the kernel's occupancy)
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-    const hipError_t e = shadow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lib_raster<true>, 256, 0)
-                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lib_raster<false>, 256, 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, SHS_RASTER_KERNEL(shadow, shallow), 256, 0);
     if (e != hipSuccess || per_cu <= 0) per_cu = 2;
     (void)hipGetLastError();   // a failed query must not leave a sticky error for the host's next HIP user
     return cus * per_cu;
@@ -1868,9 +1876,8 @@ hipError_t launch_lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, in
     return hipGetLastError();
 }
 
-hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, int grid, hipStream_t s) {
-    if (shadow) hipLaunchKernelGGL(k_lib_raster<true>, dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
-    else hipLaunchKernelGGL(k_lib_raster<false>, dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
+hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, bool shallow, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(SHS_RASTER_KERNEL(shadow, shallow), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }
 

@@ -7,9 +7,10 @@
 namespace shs_internal {
 // shadow = true: PassShadowMap's depth pass; false: rasterize_mesh + builtin programs.
 hipError_t launch_lib_setup(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, hipStream_t s);
-int lib_raster_resident_blocks(int device, bool shadow);   // CUs x occupancy of k_lib_raster
-hipError_t launch_lib_raster(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, int grid,
-                             hipStream_t s);
+// shallow: the 256-candidate-round k_lib_raster (every bin tile's list fits one gather round)
+int lib_raster_resident_blocks(int device, bool shadow, bool shallow);   // CUs x occupancy of k_lib_raster
+hipError_t launch_lib_raster(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, bool shallow,
+                             int grid, hipStream_t s);
 // The camera pass's shading: every owned pixel's winner (fb.keys) shaded into hdr / depth / motion.
 // prog: the program every draw of the pass runs (5 Forward+, 0 PBR: specialised kernels) or -1.
 int lib_resolve_resident_blocks(int device, int prog);      // CUs x occupancy of k_lib_resolve<prog>

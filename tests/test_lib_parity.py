@@ -184,3 +184,24 @@ def test_back_to_back_frames_no_host_sync(gpu_ctx, oracle_mod):
     assert_depth_bitexact(gd, rd)
     assert_float_close(gm, rm, what="motion")
     assert_float_close(gh, rh, what="hdr")
+
+
+def test_shallow_raster_after_first_frame(oracle_mod):
+    """The first camera pass of a context runs the deep raster (1024-candidate rounds); once a pass's
+    fullest bin tile is known to fit 256, the next uses the shallow one (more workgroups per CU).
+    Both frames must equal the oracle, in a fresh context so the order is known."""
+    import shs_gpu
+    from shs_gpu import scene_lib
+    frame, draws, casters, sun, S = scene_lib.c5_scene(2560, 1440, 512)   # fullest bin tile ~140
+    sm_ref, _ = oracle_mod.shadow_map(S, sun, casters)
+    with shs_gpu.Context(0) as ctx:
+        lvp = ctx.render_shadow_map(S, sun, casters)
+        scene_lib.wire_shadow(draws, lvp)
+        rh, rd, rm, _ = oracle_mod.pbr_forward(frame, draws, sm_ref)
+        for _ in range(2):
+            ctx.render_pbr_forward(frame, draws)
+            gh, gd, gm = ctx.resolve_lib()
+            assert ctx.lib_stats()["max_tile_bin"] <= 256
+            assert_depth_bitexact(gd, rd)
+            assert_float_close(gm, rm, what="motion")
+            assert_float_close(gh, rh, what="hdr")
