@@ -359,7 +359,7 @@ def collect_pmc(args):
     if exe is None:
         return None, "rocprofv3 not found"
     out = {}
-    kmatch = ("k_lib_raster<false>", "k_lib_resolve<") if args.config in LIB_CONFIGS else ("k_raster<",)
+    kmatch = ("k_lib_raster<false,", "k_lib_resolve<") if args.config in LIB_CONFIGS else ("k_raster<",)
     tmp = tempfile.mkdtemp(prefix="shs_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
