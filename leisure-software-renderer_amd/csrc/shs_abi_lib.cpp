@@ -249,7 +249,9 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         HIP_TRY(ctx, hipMemsetAsync(w.busy.p, 0, w.busy.cap * sizeof(uint32_t), ps));
         HIP_TRY(ctx, hipMemsetAsync(w.counters.p, 0, w.counters.cap * sizeof(uint32_t), ps));
         HIP_TRY(ctx, hipMemsetAsync(w.rqueue.p, 0, w.rqueue.cap * sizeof(uint32_t), ps));
-        HIP_TRY(ctx, hipStreamSynchronize(ps));   // the previous order's upload is done with h_rt_order
+        // the previous order's upload (on either stream) is done with h_rt_order
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
         w.h_rt_order = build_rt_order(tiles_x, tiles_y, rtiles_y, fp.rank, fp.count, st);
         if (ensure(ctx, w.rt_order, std::max<size_t>(w.h_rt_order.size(), 1))) return SHS_ERR_HIP;
         HIP_TRY(ctx, hipMemcpyAsync(w.rt_order.p, w.h_rt_order.data(), w.h_rt_order.size() * sizeof(int32_t),
