@@ -322,6 +322,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     } else {
         fb.hdr = ctx->lib_hdr.p; fb.depth = ctx->lib_depth.p; fb.motion = ctx->lib_motion.p;
         fb.keys = ctx->lib_keys.p;
+        fb.blkcov = ctx->lib_blkcov.p;
         if (w.tm_fused) {   // PassTonemap in k_lib_resolve (shs_lib_fuse_tonemap)
             const shs_tonemap_desc &d = w.tm_desc;
             const size_t npx = (size_t)W * H;
@@ -468,7 +469,7 @@ int check_lib_mesh(shs_ctx *ctx, int32_t id) {
 void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_cam);
     release_work(ctx->lib_shadow);
-    release(ctx->lib_hdr); release(ctx->lib_keys); release(ctx->tm_thr_dev); ctx->tm_thr_dev_gamma = -1.0f; release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
+    release(ctx->lib_hdr); release(ctx->lib_keys); release(ctx->lib_blkcov); release(ctx->tm_thr_dev); ctx->tm_thr_dev_gamma = -1.0f; release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
     release(ctx->lights); release(ctx->cull_work); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
     release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
@@ -613,6 +614,8 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
         return SHS_ERR_HIP;
     const size_t npx = (size_t)f.width * f.height;
     if (ensure(ctx, ctx->lib_hdr, npx) || ensure(ctx, ctx->lib_keys, npx)) return SHS_ERR_HIP;
+    const size_t n_blk = (size_t)((f.width + 31) / 32) * ((f.height + 7) / 8) * 4;   // 16x4 blocks
+    if (ensure(ctx, ctx->lib_blkcov, n_blk)) return SHS_ERR_HIP;
     const bool dm = (f.flags & SHS_LIB_DEPTH_MOTION) != 0;
     if (dm && (ensure(ctx, ctx->lib_depth, npx) || ensure(ctx, ctx->lib_motion, npx))) return SHS_ERR_HIP;
 

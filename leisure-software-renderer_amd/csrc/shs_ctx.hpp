@@ -160,6 +160,7 @@ struct shs_ctx {
     DevBuf<uint64_t> lib_stimeline;       // SHS_OPT_TIMELINE, camera pass setup
     DevBuf<float4> lib_hdr;
     DevBuf<unsigned long long> lib_keys;  // camera pass winner keys (k_lib_raster -> k_lib_resolve)
+    DevBuf<uint32_t> lib_blkcov;          // ... and per 16x4 block whether it holds any
     int lib_resolve_resident[3] = {0, 0, 0};   // resident k_lib_resolve workgroups (Forward+, PBR, mixed)
     DevBuf<float> lib_depth;
     DevBuf<float2> lib_motion;

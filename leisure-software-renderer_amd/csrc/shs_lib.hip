@@ -1652,8 +1652,12 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     if (SHADOW) {
         lib_resolve<SHADOW>(fp, fb, key, px, py, covered);
     } else {
+        // keys only for 16x4 blocks holding a winner; the block's flag tells k_lib_resolve which
+        // (the wave's block is sub-block `wave` of the tile, k_lib_resolve's numbering)
         covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
-        if (px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = key;
+        const bool any = __ballot(covered) != 0ull;
+        if (any && px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = key;
+        if (lane == 0) fb.blkcov[(size_t)rt * 4 + wave] = any ? 1u : 0u;
     }
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
@@ -1677,8 +1681,8 @@ __device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const L
     if (SHADOW) {
         bool covered;
         lib_resolve<SHADOW>(fp, fb, KEY_EMPTY, px, py, covered);
-    } else if (px < fp.W && py < fp.H) {
-        fb.keys[(size_t)py * fp.W + px] = KEY_EMPTY;
+    } else if (tid < 4) {
+        fb.blkcov[(size_t)rt * 4 + tid] = 0u;   // no winner anywhere: k_lib_resolve reads no key
     }
 }
 
@@ -1788,7 +1792,8 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
         const int px = (rt % fp.tiles_x) * LIB_RTW + 16 * (sub & 1) + (lane & 15);
         const int py = (rt / fp.tiles_x) * LIB_RTH + 4 * (sub >> 1) + (lane >> 4);
         const bool inb = px < fp.W && py < fp.H;
-        const unsigned long long key = inb ? fb.keys[(size_t)py * fp.W + px] : KEY_EMPTY;
+        const bool any = fb.blkcov[(size_t)rt * 4 + sub] != 0u;   // wave-uniform
+        const unsigned long long key = inb && any ? fb.keys[(size_t)py * fp.W + px] : KEY_EMPTY;
         LtWave lw;
 #ifdef SHS_RESOLVE_NO_LTWAVE
         if (false) {

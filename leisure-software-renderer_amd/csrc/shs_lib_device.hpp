@@ -141,6 +141,7 @@ struct LibBuffers {
     uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQ x LIB_QSTRIDE words
     const int32_t *rt_order;         // the owned raster tiles in processing order (n_owned_rt; XCD-coherent)
     unsigned long long *keys;        // camera pass: W*H winning (z, submission) keys, k_lib_raster -> k_lib_resolve
+    uint32_t *blkcov;                // camera pass: per 16x4 block (4 per raster tile, rt * 4 + sub): keys written
     // fused PassTonemap (shs_lib_fuse_tonemap): k_lib_resolve also writes the tonemapped bytes
     const float *tm_thr;             // the 256 byte thresholds (shs_post_internal.hpp), null: not fused
     uint32_t *tm_ldr, *tm_present;   // RT_ColorLDR (rows y up) / present staging (rows top-down), or null
