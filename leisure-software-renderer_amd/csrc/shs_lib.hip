@@ -1789,7 +1789,7 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (fb.tm_thr) tm_thr[tid] = fb.tm_thr[tid];
     if (PROG != 0 && fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights
-        for (int i = tid; i < fp.n_lights; i += 256) {
+        for (int i = tid; i < (int)fp.n_lights; i += 256) {
             const PLight p = plight_global(fb.lights[i]);
             lib_lds_lights[4 * i] = p.pr;
             lib_lds_lights[4 * i + 1] = p.ci;
