@@ -73,11 +73,13 @@ def test_legacy_shards_gather_on_device():
         c.close()
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("count", [2, 8])
-def test_lib_present_gather_after_sharded_tonemap(count):
+def test_lib_present_gather_after_sharded_tonemap(count, fused):
     """The multi-GPU frame as bench C4 / C5 run it: every rank renders its tiles, tonemaps only those
-    (k_tonemap_tiles) into the present staging, and ships 4 B/px (SHS_TARGET_LIB_PRESENT); rank 0's
-    composed staging equals the unsharded frame's tonemapped staging."""
+    (k_tonemap_tiles, or fused into the pass's shading kernel as the bench does) into the present
+    staging, and ships 4 B/px (SHS_TARGET_LIB_PRESENT); rank 0's composed staging equals the unsharded
+    frame's tonemapped staging."""
     import torch
     import shs_gpu
     from shs_gpu import scene_lib, shard
@@ -90,8 +92,12 @@ def test_lib_present_gather_after_sharded_tonemap(count):
     for r in range(count):
         c = shs_gpu.Context(0)
         frame.shard_rank, frame.shard_count = r, count
-        c.render_pbr_forward(frame, draws)
-        c.tonemap(1.0, 2.2, ldr=False, present=True)
+        if fused:
+            c.fuse_tonemap(1.0, 2.2, ldr=False, present=True)
+            c.render_pbr_forward(frame, draws)
+        else:
+            c.render_pbr_forward(frame, draws)
+            c.tonemap(1.0, 2.2, ldr=False, present=True)
         buf = torch.zeros(c.tiles_packed_words(c.TARGET_LIB_PRESENT, count), dtype=torch.int32, device="cuda:0")
         c.tiles_pack(c.TARGET_LIB_PRESENT, r, count, buf.data_ptr())   # finishes the pass chain first
         c.synchronize_lib()
