@@ -146,6 +146,30 @@ def test_odd_reference_tiles(gpu_ctx, oracle_mod):
     _check(gpu_ctx, oracle_mod, frame, [_identity_draw(Mesh(pos, nrm), 2)])
 
 
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 37), (45, 1), (2, 2), (31, 33), (81, 79)])
+def test_tiny_and_ragged_frames(gpu_ctx, oracle_mod, W, H):
+    """Frames smaller than one 32x32 GPU tile / one 80x80 reference tile, single rows and columns,
+    and sizes one pixel either side of a tile edge: the edge clamps of both tilings."""
+    import shs_gpu
+    from shs_gpu.scene import Mesh
+    rng = np.random.default_rng(W * 131 + H)
+    pos, nrm = _ndc_soup(rng, max(W, 8), max(H, 8), 300)
+    frame = shs_gpu.Frame(W, H)
+    _check(gpu_ctx, oracle_mod, frame, [_identity_draw(Mesh(pos, nrm), (W + H) % 4)])
+
+
+@pytest.mark.parametrize("cam_z", [6.5, 8.0, 9.5])
+def test_vertices_behind_camera(gpu_ctx, oracle_mod, cam_z):
+    """Camera inside / just in front of the Suzanne: vertices with clip w < 0 and triangles straddling
+    the camera plane.  The legacy pipelines divide by w without clipping (Canvas::clip_to_screen,
+    shs_renderer.hpp:823-831) and clamp the bbox to the tile in float (draw_triangle_tile): the GPU
+    must reproduce the same flipped, huge-coordinate triangles."""
+    from shs_gpu import scene
+    frame, draws = scene.monkey_scene(320, 240, 3, rotation=31.0, cam_pos=(0.3, 0.4, cam_z))
+    stats, _ = _check(gpu_ctx, oracle_mod, frame, draws)
+    assert stats["covered_pixels"] > 0
+
+
 def test_empty_frame_clears(gpu_ctx):
     import shs_gpu
     frame = shs_gpu.Frame(100, 70, clear_color=(1, 2, 3, 255))
