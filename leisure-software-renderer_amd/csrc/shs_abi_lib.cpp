@@ -230,7 +230,8 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (const char *e = std::getenv("SHS_LIB_XCD_ST")) st = (int)std::strtol(e, nullptr, 0);
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count ^
                           ((uint64_t)(st & 0xff) << 56);
-    bool reset = gkey != w.geom_key;
+    // rtiles_y too: a height change inside the same bin-tile rows changes the raster-tile rows
+    bool reset = gkey != w.geom_key || rtiles_y != w.geom_rtiles_y;
     if (w.tile_count.cap < 2 * (size_t)n_tiles || !w.tile_count.p) {
         if (ensure(ctx, w.tile_count, 2 * (size_t)n_tiles)) return SHS_ERR_HIP;
         reset = true;
@@ -257,6 +258,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         HIP_TRY(ctx, hipMemcpyAsync(w.rt_order.p, w.h_rt_order.data(), w.h_rt_order.size() * sizeof(int32_t),
                                     hipMemcpyHostToDevice, ps));
         w.geom_key = gkey;
+        w.geom_rtiles_y = rtiles_y;
     }
     if (ensure(ctx, w.bins, (size_t)n_tiles * w.bin_cap)) return SHS_ERR_HIP;
     if (!w.spill.p && ensure(ctx, w.spill, 1 << 16)) return SHS_ERR_HIP;

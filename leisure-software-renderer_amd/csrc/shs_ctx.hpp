@@ -136,6 +136,7 @@ struct shs_ctx {
         bool slot_used[2] = {false, false};
         int slot = 0;
         uint64_t geom_key = ~0ull;
+        int geom_rtiles_y = -1;
         uint32_t bin_cap = 256, extra_cap = 0, frame_index = 0, last_parity = 0;
         int last_setup_blocks = 0, last_raster_grid = 0, last_n_tris = 0;
         bool need_check = false, done = false;

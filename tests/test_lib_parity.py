@@ -72,6 +72,16 @@ def test_c5_shadow_map_sizes(gpu_ctx, oracle_mod):
     _check(gpu_ctx, oracle_mod, frame, draws, shadow=(128, sun, casters))
 
 
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 29), (37, 1), (16, 4), (65, 33)])
+def test_tiny_frames(gpu_ctx, oracle_mod, W, H):
+    """Frames below one 16x16 raster tile / one 16x4 resolve block, single rows and columns: the
+    edge masks of the raster, the per-block coverage words and the resolve's pixel guard."""
+    from shs_gpu import scene_lib
+    frame, draws, casters, sun, _ = scene_lib.c5_scene(W, H, program=(W + H) % 5)
+    scene_lib.wire_shadow(draws, np.eye(4, dtype=np.float32).reshape(16))
+    _check(gpu_ctx, oracle_mod, frame, draws, shadow=(64, sun, casters))
+
+
 def _clip_soup(rng, n):
     """Random world-space triangles around a perspective camera: many cross the near / far / side
     planes (Sutherland-Hodgman + fan), some lie behind the eye, some are degenerate."""
