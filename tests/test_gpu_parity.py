@@ -158,6 +158,17 @@ def test_tiny_and_ragged_frames(gpu_ctx, oracle_mod, W, H):
     _check(gpu_ctx, oracle_mod, frame, [_identity_draw(Mesh(pos, nrm), (W + H) % 4)])
 
 
+def test_resize_sequence(gpu_ctx, oracle_mod):
+    """One context through sizes that keep or change the 32x32 bin-tile grid and the raster-tile
+    rows (the busy flags and per-slot workspaces are cached per geometry): every frame vs the oracle."""
+    import shs_gpu
+    from shs_gpu.scene import Mesh
+    rng = np.random.default_rng(23)
+    for W, H in [(160, 96), (160, 90), (150, 90), (33, 17), (160, 96), (160, 96)]:
+        pos, nrm = _ndc_soup(rng, W, H, 250)
+        _check(gpu_ctx, oracle_mod, shs_gpu.Frame(W, H), [_identity_draw(Mesh(pos, nrm), H % 4)])
+
+
 @pytest.mark.parametrize("cam_z", [6.5, 8.0, 9.5])
 def test_vertices_behind_camera(gpu_ctx, oracle_mod, cam_z):
     """Camera inside / just in front of the Suzanne: vertices with clip w < 0 and triangles straddling

@@ -82,6 +82,16 @@ def test_tiny_frames(gpu_ctx, oracle_mod, W, H):
     _check(gpu_ctx, oracle_mod, frame, draws, shadow=(64, sun, casters))
 
 
+def test_resize_sequence(gpu_ctx, oracle_mod):
+    """One context through heights / widths that keep or change the bin-tile grid and the raster-tile
+    rows, with the shadow map resized between frames: every frame vs the oracle."""
+    from shs_gpu import scene_lib
+    for (W, H), sm in zip([(96, 64), (96, 56), (96, 64), (90, 60), (33, 17), (96, 64)], [64, 64, 64, 48, 80, 64]):
+        frame, draws, casters, sun, _ = scene_lib.c5_scene(W, H, program=W % 5)
+        scene_lib.wire_shadow(draws, np.eye(4, dtype=np.float32).reshape(16))
+        _check(gpu_ctx, oracle_mod, frame, draws, shadow=(sm, sun, casters))
+
+
 def _clip_soup(rng, n):
     """Random world-space triangles around a perspective camera: many cross the near / far / side
     planes (Sutherland-Hodgman + fan), some lie behind the eye, some are degenerate."""

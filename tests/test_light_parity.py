@@ -64,6 +64,25 @@ def test_forward_plus_frame(gpu_ctx, oracle_mod, mode, tile, maxp):
         assert (lists >= 4).any(), "no saturated list: the full-loop fallback is not exercised"
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_forward_plus_resize_sequence(gpu_ctx, oracle_mod, mode):
+    """One context through frame sizes that keep / change the bin-tile grid, the raster-tile rows and
+    the light-tile grid (each cached per geometry on the device side): every frame vs the oracle."""
+    for W, H in [(480, 270), (480, 262), (470, 262), (200, 130), (17, 9), (480, 270)]:
+        frame, draws, lights, cull = _small_c4(mode, W=W, H=H, n_lights=32)
+        gpu_ctx.upload_lights(lights)
+        gpu_ctx.render_pbr_forward(frame, _prepass(draws))
+        _, depth, _ = gpu_ctx.resolve_lib()
+        gpu_ctx.light_cull(cull)
+        _check_lists(gpu_ctx, oracle_mod, cull, lights, depth)
+        gpu_ctx.render_pbr_forward(frame, draws)
+        gh, gd, _ = gpu_ctx.resolve_lib()
+        rc, ri, _ = oracle_mod.light_cull(cull, lights, depth)
+        rh, rd, _, _ = oracle_mod.forward_plus(frame, draws, lights, cull, (rc, ri))
+        assert_depth_bitexact(gd, rd)
+        assert_float_close(gh, rh, what=f"forward+ hdr {W}x{H}")
+
+
 def test_light_lists_sharded(gpu_ctx, oracle_mod):
     """Lists of a tile shard equal the full lists on the owned 32x32 tiles and are empty elsewhere."""
     frame, draws, lights, cull = _small_c4(1)
