@@ -146,6 +146,31 @@ def test_tonemap_follows_new_pass_and_validates(oracle_mod):
         assert np.array_equal(pre, want_pre)
 
 
+@pytest.mark.gpu
+def test_post_chain_resize_sequence(oracle_mod):
+    """One context through frame sizes down to 1x1 and single rows / columns: the fused tonemap, the
+    PassTonemap and PassMotionBlur after it (each sized and cached per frame) vs the oracle."""
+    import shs_gpu
+    with shs_gpu.Context(0) as ctx:
+        for i, (W, H) in enumerate([(96, 64), (96, 56), (1, 1), (37, 1), (1, 29), (17, 9), (96, 64)]):
+            frame, draws = _c5(W, H)
+            fused = i % 2 == 0
+            ctx.fuse_tonemap(1.3, 2.2, ldr=True, present=True, enable=fused)
+            ctx.render_pbr_forward(frame, draws)
+            if not fused:
+                ctx.tonemap(1.3, 2.2, ldr=True, present=True)
+            ldr, pre = ctx.resolve_ldr()
+            hdr, depth, motion = ctx.resolve_lib()
+            want_ldr, want_pre = oracle_mod.tonemap(hdr, 1.3, 2.2)
+            assert np.array_equal(ldr, want_ldr), (W, H, fused)
+            assert np.array_equal(pre, want_pre), (W, H, fused)
+            ctx.motion_blur(min_velocity_px=0.0)
+            got, _ = ctx.resolve_motion_blur()
+            want = oracle_mod.motion_blur(ldr, depth, motion, min_velocity_px=0.0)
+            assert np.array_equal(got, want), (W, H)
+        ctx.fuse_tonemap(enable=False)
+
+
 # ---- PassMotionBlur (SURVEY.md 8f row 4) ------------------------------------------------------------
 
 def test_oracle_motion_blur_identities(oracle_mod):
