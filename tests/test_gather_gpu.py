@@ -13,12 +13,13 @@ def _render_lib(ctx, frame, draws):
     return ctx.resolve_lib()
 
 
-@pytest.mark.parametrize("count", [3, 8])
-def test_lib_shards_gather_on_device(count):
+@pytest.mark.parametrize("W,H,count", [(352, 200, 3), (352, 200, 8), (70, 40, 5), (33, 17, 3), (1, 1, 2)])
+def test_lib_shards_gather_on_device(W, H, count):
+    """Also frames with fewer 32x32 tiles than ranks (ranks owning no tile pack nothing)."""
     import torch
     import shs_gpu
     from shs_gpu import scene_lib, shard
-    frame, draws, _, _, _ = scene_lib.c5_scene(352, 200)
+    frame, draws, _, _, _ = scene_lib.c5_scene(W, H)
     full = shs_gpu.Context(0)
     fh, fd, fm = _render_lib(full, frame, draws)
     ctxs, bufs = [], []
@@ -30,7 +31,7 @@ def test_lib_shards_gather_on_device(count):
         buf = torch.zeros(words, dtype=torch.int32, device="cuda:0")
         c.tiles_pack(c.TARGET_LIB, r, count, buf.data_ptr())
         c.synchronize_lib()
-        host = shard.pack_padded(shard.planes_of([(h, False), (d, False), (m, False)]), 352, 200, r, count)
+        host = shard.pack_padded(shard.planes_of([(h, False), (d, False), (m, False)]), W, H, r, count)
         got = buf.cpu().numpy().view(np.uint32)
         assert np.array_equal(got[:host.size], host)
         ctxs.append(c)
