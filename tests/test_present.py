@@ -50,6 +50,22 @@ def test_present_pitch_and_batch(gpu_ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 37), (45, 1), (81, 79)])
+def test_present_tiny_frames_batch(gpu_ctx, oracle_mod, W, H):
+    """Sub-tile frames, single rows / columns, a batch of two: the staging is each frame's row flip."""
+    from shs_gpu import scene
+    fds = []
+    for k in range(2):
+        frame, draws = scene.monkey_scene(W, H, k + 2, yaw=4.0 * k, cam_pos=(0.0, 0.0, -2.0))
+        fds.append(draws)
+    frame.present = True
+    gpu_ctx.render_batch(frame, fds)
+    for k in range(2):
+        c, _ = gpu_ctx.resolve_frame(k)
+        assert np.array_equal(gpu_ctx.resolve_present(k), oracle_mod.sdl_present(c))
+
+
+@pytest.mark.gpu
 def test_present_sharded_owned_tiles(gpu_ctx):
     import shs_gpu
     from shs_gpu import scene
