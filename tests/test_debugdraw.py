@@ -170,3 +170,27 @@ def test_draw_meshes_into_existing_buffers():
         _check_meshes(ctx, W, H, vp, (0.0, 3.0, -4.0), (0.3, -1.0, 0.2), meshes[60:], c1, d1)
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_fill_and_draw_resize_sequence():
+    """One context through canvas sizes down to 1x1 and single rows / columns: the filled-triangle
+    raster and the lit mesh draw, each vs the oracle."""
+    import shs_gpu
+    from shs_gpu import scene_lib
+    ctx = shs_gpu.Context(0)
+    try:
+        for seed, (W, H) in enumerate([(64, 48), (64, 40), (1, 1), (1, 29), (45, 1), (64, 48)]):
+            rng = np.random.default_rng(100 + seed)
+            scr, z, col = _random_triangles(rng, 60, max(W, 16), max(H, 16))
+            rgba0 = rng.integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+            depth0 = rng.uniform(0.0, 1.2, size=(H, W)).astype(np.float32)
+            want_c, want_d = oracle.draw_filled_triangles(W, H, scr, z, col, rgba0, depth0)
+            got_c, got_d = ctx.debug_fill_triangles(W, H, scr, z, col, rgba0.copy(), depth0.copy())
+            assert np.array_equal(got_d.view(np.uint32), want_d.view(np.uint32)), (W, H)
+            assert np.array_equal(got_c, want_c), (W, H)
+            objs, view, vp, _, _ = scene_lib.occlusion_scene(n_objects=40, width=W, height=H, seed=seed)
+            meshes = [(o[0], o[1], (0.7, 0.5, 0.3)) for o in objs]
+            _check_meshes(ctx, W, H, vp, (0.0, 3.0, -4.0), (-0.4, -1.0, 0.3), meshes)
+    finally:
+        ctx.close()

@@ -56,3 +56,18 @@ def test_occlusion_pass_large_buffer_and_disabled(oracle_mod):
     assert off[0].sum() == 0 and np.array_equal(off[1], fv)
     with shs_gpu.Context(0) as ctx, pytest.raises(shs_gpu.ShsError):
         ctx.occlusion_pass(65536, 2, view, vp, objs, fv)   # sides are limited to 16 bits
+
+
+@pytest.mark.gpu
+def test_occlusion_pass_resize_sequence(oracle_mod):
+    """One context through buffer sizes down to 1x1 and a single column (the depth buffer and the
+    per-object work are sized per call)."""
+    import shs_gpu
+    with shs_gpu.Context(0) as ctx:
+        for seed, (W, H) in enumerate([(300, 225), (300, 200), (64, 48), (1, 1), (7, 300), (300, 225)]):
+            objs, view, vp, _, _ = _scene(n_objects=150, seed=30 + seed, width=W, height=H)
+            fv = np.arange(len(objs), dtype=np.uint32)
+            want = oracle_mod.occlusion_pass(W, H, view, vp, objs, fv)
+            got = ctx.occlusion_pass(W, H, view, vp, objs, fv)
+            assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), (W, H)
+            assert np.array_equal(got[2].view(np.uint32), want[2].view(np.uint32)), (W, H)
