@@ -191,3 +191,26 @@ def test_canvas_passes_device_buffers():
     finally:
         torch.cuda.set_stream(torch.cuda.default_stream())
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_canvas_passes_resize_sequence():
+    """One context through canvas sizes down to 1x1 and single rows / columns: motion blur and DoF
+    (ping-pong buffers sized per call) vs the oracle."""
+    import shs_gpu
+    ctx = shs_gpu.Context(0)
+    try:
+        for seed, (W, H) in enumerate([(64, 48), (64, 40), (1, 1), (1, 29), (45, 1), (64, 48)]):
+            rng = np.random.default_rng(200 + seed)
+            src, depth, vel = _inputs(rng, W, H, vmax=20.0)
+            view, proj = _cam((0.0, 2.0, -6.0), (0.0, 1.0, 10.0), W, H)
+            pview, pproj = _cam((0.5, 2.0, -5.5), (0.3, 1.0, 10.0), W, H)
+            want = oracle.canvas_motion_blur(src, depth, vel, view, proj, pview, pproj, samples=8, soft_knee=True)
+            got = ctx.canvas_motion_blur(src, depth, vel, view, proj, pview, pproj, samples=8, soft_knee=True)
+            assert np.array_equal(got, want), (W, H)
+            want_c, want_b, want_f = oracle.canvas_dof(src, depth, iterations=2, radius=4, focus=None)
+            got_c, got_b, got_f = ctx.canvas_dof(src.copy(), depth, iterations=2, radius=4, focus=None)
+            assert np.float32(got_f).view(np.uint32) == np.float32(want_f).view(np.uint32), (W, H)
+            assert np.array_equal(got_b, want_b) and np.array_equal(got_c, want_c), (W, H)
+    finally:
+        ctx.close()
