@@ -64,6 +64,16 @@ def test_batch_c2_poses_match_single_frames(gpu_ctx, n_frames):
     _assert_batch_equals_singles(gpu_ctx, frame, fd)
 
 
+def test_batch_geometry_sequence(gpu_ctx):
+    """One context through batches whose frame size (inside and across the bin-tile grid), frame
+    count and shard change from call to call: every frame equals its single render."""
+    for W, H, n, rank, count in [(322, 181, 3, 0, 1), (322, 176, 5, 0, 1), (33, 17, 2, 0, 1), (322, 181, 4, 1, 3),
+                                 (322, 181, 1, 0, 1), (1, 1, 3, 0, 1), (322, 181, 6, 0, 1)]:
+        frame, fd = _poses(n, width=W, height=H)
+        frame.shard_rank, frame.shard_count = rank, count
+        _assert_batch_equals_singles(gpu_ctx, frame, fd)
+
+
 def test_batch_frames_match_oracle(gpu_ctx, oracle_mod):
     """Frames 0 and the last of a mixed-shading 640x480 batch against the CPU oracle directly."""
     from shs_gpu import scene
