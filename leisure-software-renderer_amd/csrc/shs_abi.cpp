@@ -321,10 +321,13 @@ static int enqueue_frame(shs_ctx *ctx) {
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;
     fp.setup_blocks = setup_blocks;
-    // Binned (large) scenes and batches list their unbounded slivers in k_setup and enumerate them in
-    // k_ghost: ghost waves would recompute every triangle's record (C3: ~1/3 of k_setup's time).  A
-    // single scan-mode frame keeps the ghost waves inside k_setup (one launch fewer on its latency path).
-    fp.ghost_list = (fp.scan_mode && n_frames == 1) ? 0u : 1u;
+    // Binned (large) scenes list their unbounded slivers in k_setup and enumerate them in k_ghost: ghost
+    // waves would recompute every triangle's record (C3: ~1/3 of k_setup's time).  Scan-mode frames and
+    // batches keep the ghost waves inside k_setup: one launch fewer on the latency path between two
+    // batches (C2: 0.282-0.285 vs 0.288-0.297 ms per 64-frame step).  SHS_GHOST_LIST=1 lists them in
+    // scan mode too (timing experiments).
+    static const bool ghost_list_env = std::getenv("SHS_GHOST_LIST") && std::atoi(std::getenv("SHS_GHOST_LIST")) != 0;
+    fp.ghost_list = (fp.scan_mode && !ghost_list_env) ? 0u : 1u;
     fp.ghost_blocks = fp.ghost_list ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
     fp.clear_blocks = 0;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / shs_dev::RTH);
