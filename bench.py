@@ -510,6 +510,37 @@ def cpu_baseline(args):
                       f"({head_name}; oracle/shs_oracle.c, gcc -O3)"}
 
 
+def launch_ranks(args):
+    """`--gpus N` without a launcher: run this script under torch.distributed.run with N processes on
+    this node (rendezvous on 127.0.0.1, a free port), the same command line the driver uses for N > 1.
+    The parent never initialises the GPU; its exit status is the launcher's."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_dry_run(world, rank, local_rank):
+    """The launcher check of tests/test_bench_launch.py: gloo group, no GPU, rank 0 prints one line."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == world
+    t = torch.tensor([rank, local_rank], dtype=torch.int64)
+    outs = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(outs, t)
+    if rank == 0:
+        print(json.dumps({"world": world, "ranks": [int(o[0]) for o in outs], "local_ranks": [int(o[1]) for o in outs]}),
+              flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -527,13 +558,24 @@ def main():
     ap.add_argument("--debug-flags", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
     ap.add_argument("--raster-mode", type=int, default=0, help="legacy path: 0 auto, 1 scan, 2 bins")
     ap.add_argument("--raster-loop", type=int, default=-1, help="legacy path: 0 per-pixel, 1 pair tasks (default)")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="rank launcher check: every rank joins a gloo group and rank 0 prints the ranks (no GPU)")
     args = ap.parse_args()
     if args.frames_per_step <= 0:
         args.frames_per_step = {"c1": 64, "c2": 64, "c3": 16}.get(args.config, 1)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.child:
+        # `python bench.py --gpus N` started directly: start the N ranks as child processes (one per
+        # GPU) before this process touches the GPU, and exit with their status
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not args.child and world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch with --nproc-per-node equal to --gpus")
+
+    if args.launch_dry_run:
+        return launch_dry_run(world, rank, local_rank)
 
     if args.child:  # profiled child: just render
         {"c4": run_gpu_c4, "c5": run_gpu_lib}.get(args.config, run_gpu)(args, 0, 0, 1, None)

@@ -105,6 +105,11 @@ int shs_mesh_release(shs_ctx *ctx, int32_t mesh_id);
  * asynchronously on the context stream.  Results stay in device memory until shs_resolve. */
 int shs_render_legacy(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws);
 
+/* Superseding: a render call while the previous batch is still in flight does not wait for it, but
+ * it reads that batch's capacity-overflow word first (final once the batch's setup is, copied to
+ * pinned memory beside its raster); an overflowed batch is finished -- re-issued with grown
+ * capacities -- before the new one is enqueued, so work queued behind a batch on the stream never
+ * sees an incomplete frame. */
 /* A batch of n_frames frames (1 <= n_frames <= SHS_MAX_BATCH_FRAMES) of one frame description, e.g.
  * the next n_frames camera poses of a render-ahead host or the views of a multi-view capture: frame f
  * draws draws[f * n_draws .. f * n_draws + n_draws - 1], in that order, and every frame must submit
@@ -126,12 +131,19 @@ int shs_resolve_frame(shs_ctx *ctx, int32_t frame_index, uint8_t *color, float *
  * Canvas::copy_to_SDLSurface fills (shs_renderer.hpp:833-848) -- surface row h-1-y holds canvas row
  * y, SDL_MapRGBA into create_sdl_surface's little-endian RGBA32 masks (:850-856) is the Color bytes.
  * shs_resolve_present copies it into a caller surface (pixels + pitch in bytes >= W*4), replacing
- * the per-pixel copy loop; shs_present_device returns the device pointer (W*H words, rows top-down). */
+ * the per-pixel copy loop; shs_present_device returns the device pointer (W*H words, rows top-down).
+ * shs_present_device and shs_device_framebuffers first finish the batch (wait for it; a capacity
+ * overflow re-issues it), so the pointer holds the final frame.  The pointer aliases the context's
+ * buffers: it is valid until the next shs_render_legacy* call on this context (which rewrites them,
+ * and reallocates them when the frame or batch grows); call again per batch. */
 int shs_resolve_present(shs_ctx *ctx, int32_t frame_index, uint8_t *pixels, int32_t pitch);
 int shs_present_device(shs_ctx *ctx, int32_t frame_index, void **present_dev);
-/* Pre-truncation shader floats, W*H*4 (canvas rows), only when SHS_FRAME_PREQUANT was set. */
+/* Pre-truncation shader floats, W*H*4 (canvas rows), only when SHS_FRAME_PREQUANT was set:
+ * shs_resolve_prequant_frame for frame frame_index of the batch, shs_resolve_prequant for frame 0. */
 int shs_resolve_prequant(shs_ctx *ctx, float *prequant);
-/* Device pointers of the current frame (zero-copy hand-off to torch / RCCL). */
+int shs_resolve_prequant_frame(shs_ctx *ctx, int32_t frame_index, float *prequant);
+/* Device pointers of the current batch's colour / depth planes (zero-copy hand-off to torch / RCCL);
+ * finished and valid as for shs_present_device. */
 int shs_device_framebuffers(shs_ctx *ctx, void **color_dev, void **depth_dev);
 int shs_get_stats(shs_ctx *ctx, shs_raster_stats *stats);
 
@@ -170,6 +182,12 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
 /* SHS_OPT_RASTER_LOOP: 1 = (candidate, pixel) pair tasks dealt over the waves (default), 0 = each
  * thread loops over the tile's candidates for its own pixel.  Results are identical in both. */
 #define SHS_OPT_RASTER_LOOP 4
+/* SHS_OPT_SPILL_CAPACITY / SHS_OPT_FRAG_CAPACITY (tests): reallocate the legacy workspaces' global
+ * bin-spill list / ghost-fragment list to `value` entries.  A batch that needs more raises its
+ * overflow flag and is re-issued with grown lists when it is finished (synchronise, resolve, present,
+ * superseded); results are identical. */
+#define SHS_OPT_SPILL_CAPACITY 5
+#define SHS_OPT_FRAG_CAPACITY 6
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 
 /* Debug / profiling hook: the last frame's workgroup timeline.  out[0..7] = {k_setup grid, k_raster
@@ -264,6 +282,8 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
  * (row y = bottom-up, exactly PixelBuffer2D::at(x, y)); any pointer may be NULL. */
 int shs_resolve_lib(shs_ctx *ctx, float *hdr, float *depth, float *motion);
 int shs_get_lib_stats(shs_ctx *ctx, shs_lib_stats *stats);
+/* Device pointers of the pass's targets; the pass chain is finished first (a capacity overflow
+ * re-issues it), valid until the next shs_render_pbr_forward on this context. */
 int shs_lib_device_targets(shs_ctx *ctx, void **hdr_dev, void **depth_dev, void **motion_dev);
 /* Kernel durations of the library passes enqueued since shs_lib_timing_reset while
  * shs_enable_timing(ctx, 1) is on (HIP events on the context stream): sum_ms4 = {shadow k_lib_setup,
@@ -400,6 +420,7 @@ int shs_tonemap(shs_ctx *ctx, const shs_tonemap_desc *desc);
 int shs_lib_fuse_tonemap(shs_ctx *ctx, const shs_tonemap_desc *desc);
 /* Copy the tonemapped targets into caller-owned W*H*4-byte buffers (either may be NULL). */
 int shs_resolve_ldr(shs_ctx *ctx, uint8_t *ldr, uint8_t *present);
+/* Device pointers of the tonemap targets (the pass chain finished first, as shs_lib_device_targets). */
 int shs_ldr_device_targets(shs_ctx *ctx, void **ldr_dev, void **present_dev);
 /* PassMotionBlur::execute (shs-renderer-lib/include/shs/passes/pass_motion_blur.hpp:38-170) on the
  * last tonemap's RT_ColorLDR (SHS_TONEMAP_LDR) with the camera pass's depth / motion planes
@@ -479,7 +500,10 @@ int shs_debug_fill_triangles(shs_ctx *ctx, int32_t width, int32_t height, const 
  * hello-render-target/ demos, paths relative to cpp-folders/src/hello-render-target/.  Colour buffers are
  * shs::Canvas pixels (W*H Color), depth the ZBuffer (view z, FLT_MAX = empty) and velocity the
  * Buffer<glm::vec2>, all indexed y * W + x as the passes index raw().  Host buffers: synchronous;
- * flags SHS_CANVAS_DEVICE: device buffers, enqueued on the context stream. */
+ * flags SHS_CANVAS_DEVICE: device buffers, enqueued on the context stream (shs_set_stream): the
+ * caller orders that stream against whatever produces the inputs and consumes the outputs -- run
+ * the context on the producer's stream (as the Python host does with torch's current stream) or
+ * make the streams wait on events. */
 #define SHS_CANVAS_DEVICE 1u
 #define SHS_CANVAS_MAX_AUTOFOCUS_RADIUS 32
 typedef struct shs_canvas_motion_blur_desc {

@@ -47,10 +47,16 @@ int shs_create(int device, shs_ctx **out) {
         return SHS_ERR_HIP;
     }
     ctx->stream = ctx->own_stream;
-    if (hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking) != hipSuccess) { shs_destroy(ctx); return SHS_ERR_HIP; }
+    if (hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->ov_stream, hipStreamNonBlocking) != hipSuccess) {
+        shs_destroy(ctx);
+        return SHS_ERR_HIP;
+    }
     for (auto &w : ctx->lslot)
         if (hipEventCreateWithFlags(&w.setup_done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&w.raster_done, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&w.raster_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&w.ov_ready, hipEventDisableTiming) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&w.h_ov), sizeof(uint32_t)) != hipSuccess) {
             shs_destroy(ctx);
             return SHS_ERR_HIP;
         }
@@ -75,6 +81,7 @@ int shs_destroy(shs_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->setup_stream) (void)hipStreamSynchronize(ctx->setup_stream);
+    if (ctx->ov_stream) (void)hipStreamSynchronize(ctx->ov_stream);
     for (auto &m : ctx->meshes) {
         if (m.pos) (void)hipFree(m.pos);
         if (m.nrm) (void)hipFree(m.nrm);
@@ -89,6 +96,8 @@ int shs_destroy(shs_ctx *ctx) {
         if (w.h_draws) (void)hipHostFree(w.h_draws);
         if (w.setup_done) (void)hipEventDestroy(w.setup_done);
         if (w.raster_done) (void)hipEventDestroy(w.raster_done);
+        if (w.ov_ready) (void)hipEventDestroy(w.ov_ready);
+        if (w.h_ov) (void)hipHostFree(w.h_ov);
     }
     release(ctx->counters); release(ctx->timeline);
     release(ctx->color); release(ctx->depth); release(ctx->prequant); release(ctx->present);
@@ -100,6 +109,7 @@ int shs_destroy(shs_ctx *ctx) {
     if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
+    if (ctx->ov_stream) (void)hipStreamDestroy(ctx->ov_stream);
     delete ctx;
     return SHS_OK;
 }
@@ -252,7 +262,10 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (want_present && ensure(ctx, ctx->present, npx * n_frames)) return SHS_ERR_HIP;
 
     // ---- setup_stream: wait for the slot's last k_raster, reset, upload, set up ----
-    if (ws.used) HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.raster_done, 0));
+    if (ws.used) {
+        HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.raster_done, 0));
+        HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.ov_ready, 0));   // its overflow word was copied out
+    }
     if (reset) {
         HIP_TRY(ctx, hipMemsetAsync(ws.busy.p, 0, ws.busy.cap * sizeof(uint32_t), sst));
         ctx->geom_key[slot] = gkey;
@@ -383,6 +396,10 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (fp.ghost_list && !(fp.flags & shs_dev::DBG_SKIP_GHOST)) HIP_TRY(ctx, shs_internal::launch_ghost(fp, fb, sst));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], sst));
     HIP_TRY(ctx, hipEventRecord(ws.setup_done, sst));
+    // the overflow word is final once the setup kernels are: copy it out beside the raster
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->ov_stream, ws.setup_done, 0));
+    HIP_TRY(ctx, hipMemcpyAsync(ws.h_ov, cset + shs_dev::C_OVERFLOW, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->ov_stream));
+    HIP_TRY(ctx, hipEventRecord(ws.ov_ready, ctx->ov_stream));
     // ---- stream: after the previous batch's raster (stream order) and this batch's setup ----
     HIP_TRY(ctx, hipStreamWaitEvent(st, ws.setup_done, 0));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], st));
@@ -493,9 +510,18 @@ int shs_render_legacy_batch(shs_ctx *ctx, const shs_frame_desc *frame, const shs
         else if (t != tris0) { ctx->err = "frames of a batch must submit equal triangle counts"; return SHS_ERR_INVALID; }
     }
     if (set_dev(ctx)) return SHS_ERR_HIP;
-    // No host sync here: a still-pending previous batch is superseded by this one (it rewrites every
-    // pixel); only the newest batch's overflow flags are checked (and the batch re-issued) when the
-    // caller synchronises / resolves.
+    // A still-pending previous batch is superseded by this one, but never unchecked: a stream-ordered
+    // consumer of its frames (a copy queued behind it) must not see a batch that overflowed a
+    // capacity.  Its overflow word is final once its setup is (long before its raster ends); if it is
+    // set, the batch is finished -- re-issued with grown capacities -- before this one is enqueued.
+    if (ctx->have_frame && ctx->need_check) {
+        const shs_ctx::LegacySlot &p = ctx->lslot[ctx->last_slot];
+        HIP_TRY(ctx, hipEventSynchronize(p.ov_ready));
+        if (*p.h_ov) {
+            const int rc = finish_frame(ctx);
+            if (rc) return rc;
+        }
+    }
     ctx->frame = f;
     ctx->last_draws.assign(draws, draws + n_all);
     ctx->last_n_frames = n_frames;
@@ -546,23 +572,33 @@ int shs_present_device(shs_ctx *ctx, int32_t frame_index, void **present_dev) {
     if (!ctx || !present_dev) return SHS_ERR_INVALID;
     if (!ctx->have_frame || !(ctx->frame.flags & SHS_FRAME_PRESENT)) { ctx->err = "frame has no present staging (SHS_FRAME_PRESENT)"; return SHS_ERR_INVALID; }
     if (frame_index < 0 || frame_index >= ctx->last_n_frames) { ctx->err = "frame index outside the batch"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    // the batch is final (overflow checked, re-issued if needed) before its staging is handed out
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
     *present_dev = ctx->present.p + (size_t)ctx->frame.width * ctx->frame.height * frame_index;
     return SHS_OK;
 }
 
-int shs_resolve_prequant(shs_ctx *ctx, float *pq) {
+int shs_resolve_prequant_frame(shs_ctx *ctx, int32_t frame_index, float *pq) {
     if (!ctx || !pq) return SHS_ERR_INVALID;
     if (!ctx->have_frame || !(ctx->frame.flags & SHS_FRAME_PREQUANT)) { ctx->err = "frame has no prequant buffer"; return SHS_ERR_INVALID; }
+    if (frame_index < 0 || frame_index >= ctx->last_n_frames) { ctx->err = "frame index outside the batch"; return SHS_ERR_INVALID; }
     if (set_dev(ctx)) return SHS_ERR_HIP;
     int rc = finish_frame(ctx);
     if (rc) return rc;
     const size_t npx = (size_t)ctx->frame.width * ctx->frame.height;
-    HIP_TRY(ctx, hipMemcpy(pq, ctx->prequant.p, npx * sizeof(float4), hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(pq, ctx->prequant.p + npx * frame_index, npx * sizeof(float4), hipMemcpyDeviceToHost));
     return SHS_OK;
 }
 
+int shs_resolve_prequant(shs_ctx *ctx, float *pq) { return shs_resolve_prequant_frame(ctx, 0, pq); }
+
 int shs_device_framebuffers(shs_ctx *ctx, void **color_dev, void **depth_dev) {
     if (!ctx || !ctx->have_frame) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    int rc = finish_frame(ctx);
+    if (rc) return rc;
     if (color_dev) *color_dev = ctx->color.p;
     if (depth_dev) *depth_dev = ctx->depth.p;
     return SHS_OK;
@@ -668,6 +704,26 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
     if (option == SHS_OPT_TIMELINE) {
         if (value < 0 || value > 1) return SHS_ERR_INVALID;
         ctx->want_timeline = value != 0;
+        return SHS_OK;
+    }
+    if (option == SHS_OPT_SPILL_CAPACITY || option == SHS_OPT_FRAG_CAPACITY) {
+        if (value < 1 || value > (1 << 28)) return SHS_ERR_INVALID;
+        if (set_dev(ctx)) return SHS_ERR_HIP;
+        int rc = finish_frame(ctx);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->ov_stream));
+        for (auto &w : ctx->lslot) {
+            if (option == SHS_OPT_SPILL_CAPACITY) {
+                release(w.spill);
+                if (ensure(ctx, w.spill, (size_t)value)) return SHS_ERR_HIP;
+                w.spill.cap = (size_t)value;   // ensure() allocates at least 16
+            } else {
+                release(w.frags);
+                if (ensure(ctx, w.frags, (size_t)value)) return SHS_ERR_HIP;
+                w.frags.cap = (size_t)value;
+            }
+        }
         return SHS_OK;
     }
     if (option == SHS_OPT_BIN_CAPACITY) {

@@ -60,6 +60,12 @@ void release_work(Work &w) {
     if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
+    if (w.ov_after) (void)hipEventDestroy(w.ov_after);
+    if (w.ov_ready) (void)hipEventDestroy(w.ov_ready);
+    if (w.h_ov) (void)hipHostFree(w.h_ov);
+    w.ov_after = w.ov_ready = nullptr;
+    w.h_ov = nullptr;
+    w.ov_valid = false;
     w.resolve_ev_valid = false;
     for (int i = 0; i < 2; ++i) {
         if (w.h_draws[i]) (void)hipHostFree(w.h_draws[i]);
@@ -370,9 +376,24 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         ev = w.ring_ev[k];
         w.ring_pending[k] = true;
     }
+    if (!w.ov_after) {
+        HIP_TRY(ctx, hipEventCreateWithFlags(&w.ov_after, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&w.ov_ready, hipEventDisableTiming));
+        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&w.h_ov), sizeof(uint32_t)));
+    }
+    // k_lib_setup zeroes the other parity's counters: the previous pass's overflow copy must have run
+    if (w.ov_valid) HIP_TRY(ctx, hipStreamWaitEvent(ps, w.ov_ready, 0));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], ps));
     HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, ps));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], ps));
+    // the pass's overflow word is final after its setup kernels (setup, clip, large-primitive marks):
+    // copied into pinned memory on the side stream, so superseding the pass can check it (no raster wait)
+    HIP_TRY(ctx, hipEventRecord(w.ov_after, ps));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->ov_stream, w.ov_after, 0));
+    HIP_TRY(ctx, hipMemcpyAsync(w.h_ov, w.counters.p + fp.parity * shs_dev::LC_N + shs_dev::LC_OVERFLOW, sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, ctx->ov_stream));
+    HIP_TRY(ctx, hipEventRecord(w.ov_ready, ctx->ov_stream));
+    w.ov_valid = true;
     HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, shallow, raster_grid, ps));
     if (!shadow) {   // the camera pass's shading runs in its own kernel (event [2] closes both)
         if (ps != ctx->stream) {
@@ -399,6 +420,16 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     w.need_check = true;
     w.done = true;
     return SHS_OK;
+}
+
+// A pass about to be superseded (its workspace and targets rewritten) whose overflow word is set is
+// finished first -- re-issued with grown capacities -- so no stream-ordered consumer of it (a tonemap,
+// a copy, a gather queued behind it) sees an incomplete pass.
+int lib_finish(shs_ctx *ctx);
+int check_superseded(shs_ctx *ctx, Work &w) {
+    if (!w.need_check || !w.ov_valid) return SHS_OK;
+    HIP_TRY(ctx, hipEventSynchronize(w.ov_ready));
+    return *w.h_ov ? lib_finish(ctx) : SHS_OK;
 }
 
 uint32_t next_pow2(uint64_t v) {
@@ -542,6 +573,12 @@ int shs_render_shadow_map(shs_ctx *ctx, int32_t w, int32_t h, const float sun_di
     if (set_dev(ctx)) return SHS_ERR_HIP;
     if (!ctx->h_lib_counters && hipHostMalloc(reinterpret_cast<void **>(&ctx->h_lib_counters), shs_dev::LC_N * sizeof(uint32_t)) != hipSuccess)
         return SHS_ERR_HIP;
+    {   // the pending passes are checked before this one rewrites the shadow map they read / wrote
+        const int rc = check_superseded(ctx, ctx->lib_shadow);
+        if (rc) return rc;
+        const int rc2 = check_superseded(ctx, ctx->lib_cam);
+        if (rc2) return rc2;
+    }
     using namespace shs_host;
     // scene AABB of the casters (pass_shadow_map.hpp:80-131)
     vec3 mn = {1e30f, 1e30f, 1e30f}, mx = {-1e30f, -1e30f, -1e30f};
@@ -614,6 +651,10 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     if (set_dev(ctx)) return SHS_ERR_HIP;
     if (!ctx->h_lib_counters && hipHostMalloc(reinterpret_cast<void **>(&ctx->h_lib_counters), shs_dev::LC_N * sizeof(uint32_t)) != hipSuccess)
         return SHS_ERR_HIP;
+    {   // the pending camera pass is checked before this one rewrites its targets
+        const int rc = check_superseded(ctx, ctx->lib_cam);
+        if (rc) return rc;
+    }
     const size_t npx = (size_t)f.width * f.height;
     if (ensure(ctx, ctx->lib_hdr, npx) || ensure(ctx, ctx->lib_keys, npx)) return SHS_ERR_HIP;
     const size_t n_blk = (size_t)((f.width + 31) / 32) * ((f.height + 7) / 8) * 4;   // 16x4 blocks
@@ -738,6 +779,9 @@ int shs_get_lib_stats(shs_ctx *ctx, shs_lib_stats *st) {
 
 int shs_lib_device_targets(shs_ctx *ctx, void **hdr_dev, void **depth_dev, void **motion_dev) {
     if (!ctx || !ctx->have_lib_frame) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    const int rc = lib_finish(ctx);   // the pass is final (re-issued on overflow) before it is handed out
+    if (rc) return rc;
     if (hdr_dev) *hdr_dev = ctx->lib_hdr.p;
     if (depth_dev) *depth_dev = ctx->lib_depth.p;
     if (motion_dev) *motion_dev = ctx->lib_motion.p;

@@ -217,6 +217,9 @@ int shs_resolve_ldr(shs_ctx *ctx, uint8_t *ldr, uint8_t *present) {
 int shs_ldr_device_targets(shs_ctx *ctx, void **ldr_dev, void **present_dev) {
     if (!ctx) return SHS_ERR_INVALID;
     if (!ctx->have_ldr) { ctx->err = "no tonemap since the last camera pass"; return SHS_ERR_INVALID; }
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    const int rc = shs_resolve_lib(ctx, nullptr, nullptr, nullptr);   // finishes (re-issues) the pass chain
+    if (rc) return rc;
     if (ldr_dev) *ldr_dev = (ctx->tm_desc.flags & SHS_TONEMAP_LDR) ? ctx->lib_ldr.p : nullptr;
     if (present_dev) *present_dev = (ctx->tm_desc.flags & SHS_TONEMAP_PRESENT) ? ctx->lib_present.p : nullptr;
     return SHS_OK;

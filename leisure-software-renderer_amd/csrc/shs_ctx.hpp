@@ -65,10 +65,15 @@ struct shs_ctx {
         DevBuf<uint4> blk_stat;              // per setup block
         DevBuf<uint2> rstat;                 // per raster block
         hipEvent_t setup_done = nullptr, raster_done = nullptr;
+        // the batch's overflow word, copied into pinned host memory on ov_stream once its setup is
+        // done (ov_ready): a batch about to be superseded is checked without waiting for its raster
+        uint32_t *h_ov = nullptr;
+        hipEvent_t ov_ready = nullptr;
         bool used = false;
     };
     LegacySlot lslot[2];
     hipStream_t setup_stream = nullptr;
+    hipStream_t ov_stream = nullptr; // overflow-word copies (legacy slots, library passes)
     DevBuf<uint32_t> counters;       // 2 sets (one per slot) of CSET words
     uint32_t busy_epoch = 0;         // FrameParams::epoch of the last launch (never 0)
     int last_slot = 0;
@@ -134,6 +139,11 @@ struct shs_ctx {
         size_t h_cap = 0;
         hipEvent_t slot_ev[2] = {nullptr, nullptr};
         bool slot_used[2] = {false, false};
+        // the pass's overflow word in pinned host memory, copied on ov_stream after its setup kernels
+        // (ov_after on the pass stream, ov_ready once copied): checked before the pass is superseded
+        uint32_t *h_ov = nullptr;
+        hipEvent_t ov_after = nullptr, ov_ready = nullptr;
+        bool ov_valid = false;
         int slot = 0;
         uint64_t geom_key = ~0ull;
         int geom_rtiles_y = -1;

@@ -200,10 +200,11 @@ class Context:
         self._check(self._lib.shs_resolve_present(self._h, int(index), out.ctypes.data_as(ctypes.c_void_p), pitch))
         return out if pitch != f.width * 4 else out.reshape(f.height, f.width, 4)
 
-    def resolve_prequant(self):
+    def resolve_prequant(self, index: int = 0):
+        """Pre-truncation shader floats of frame `index` of the last batch (SHS_FRAME_PREQUANT)."""
         f = self._frame
         pq = np.empty((f.height, f.width, 4), dtype=np.float32)
-        self._check(self._lib.shs_resolve_prequant(self._h, pq.ctypes.data_as(ctypes.c_void_p)))
+        self._check(self._lib.shs_resolve_prequant_frame(self._h, int(index), pq.ctypes.data_as(ctypes.c_void_p)))
         return pq
 
     def device_framebuffers(self):
@@ -398,6 +399,16 @@ class Context:
 
     CANVAS_DEVICE = 1
 
+    def _on_torch_stream(self):
+        """Device-tensor calls run on torch's current stream, so they are ordered after the torch work
+        that wrote their inputs and before the torch work that reads their outputs (tensors allocated
+        here, e.g. dst, belong to that stream too).  The context is re-pointed only when it is on
+        another stream (shs_set_stream synchronises)."""
+        import torch
+        s = torch.cuda.current_stream().cuda_stream
+        if self.stream != s:
+            self.set_stream(s)
+
     def canvas_motion_blur(self, src, depth, velocity, curr_view, curr_proj, prev_view, prev_proj, samples=12,
                            strength=0.85, w_obj=1.0, w_cam=0.35, soft_knee=True, knee_px=18.0, max_px=22.0, dst=None):
         """combined_motion_blur_pass (hello_pbr.cpp:1128-1252).  Host arrays: src uint8 [H, W, 4], depth
@@ -412,6 +423,8 @@ class Context:
         d.samples, d.strength, d.w_obj, d.w_cam = int(samples), float(strength), float(w_obj), float(w_cam)
         d.soft_knee, d.knee_px, d.max_px = 1 if soft_knee else 0, float(knee_px), float(max_px)
         dev = _is_device(src)
+        if dev:
+            self._on_torch_stream()
         if dst is None:
             dst = _empty_like(src)
         keep = (_host_c(src, np.uint8), _host_c(depth, np.float32), _host_c(velocity, np.float32), dst)
@@ -423,6 +436,8 @@ class Context:
         """gaussian_blur_pass (hello_depth_of_field.cpp:175-251), one axis."""
         H, W = src.shape[:2]
         dev = _is_device(src)
+        if dev:
+            self._on_torch_stream()
         if dst is None:
             dst = _empty_like(src)
         src = _host_c(src, np.uint8)
@@ -439,6 +454,8 @@ class Context:
         d.focus_x, d.focus_y = (W // 2, H // 2) if focus is None else focus
         d.range, d.max_blur = float(range_), float(max_blur)
         dev = _is_device(color)
+        if dev:
+            self._on_torch_stream()
         if blur is None:
             blur = _empty_like(color)
         f = ctypes.c_float()
@@ -503,6 +520,13 @@ class Context:
 
     def set_bin_capacity(self, cap: int):
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_BIN_CAPACITY, int(cap)))
+
+    def set_overflow_capacities(self, spill: int = 0, frags: int = 0):
+        """Tests: shrink the legacy bin-spill / ghost-fragment lists (0 = leave) to force overflows."""
+        if spill:
+            self._check(self._lib.shs_set_option(self._h, _abi.OPT_SPILL_CAPACITY, int(spill)))
+        if frags:
+            self._check(self._lib.shs_set_option(self._h, _abi.OPT_FRAG_CAPACITY, int(frags)))
 
     def set_stream(self, hip_stream):
         self._check(self._lib.shs_set_stream(self._h, ctypes.c_void_p(hip_stream)))

@@ -28,6 +28,8 @@ OPT_BIN_CAPACITY = 1
 OPT_RASTER_MODE = 2
 OPT_TIMELINE = 3
 OPT_RASTER_LOOP = 4
+OPT_SPILL_CAPACITY = 5
+OPT_FRAG_CAPACITY = 6
 
 
 class LegacyDraw(ctypes.Structure):
@@ -222,6 +224,7 @@ SIGNATURES = [
     ("shs_resolve_present", ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.c_int32]),
     ("shs_present_device", ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(_P)]),
     ("shs_resolve_prequant", ctypes.c_int, [_P, _P]),
+    ("shs_resolve_prequant_frame", ctypes.c_int, [_P, ctypes.c_int32, _P]),
     ("shs_device_framebuffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("shs_get_stats", ctypes.c_int, [_P, ctypes.POINTER(RasterStats)]),
     ("shs_enable_timing", ctypes.c_int, [_P, ctypes.c_int]),

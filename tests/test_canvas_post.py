@@ -160,8 +160,8 @@ def test_canvas_dof_bitexact(W, H, iters, radius, focus):
 
 @pytest.mark.gpu
 def test_canvas_passes_device_buffers():
-    """SHS_CANVAS_DEVICE: torch device tensors in and out, enqueued on the context stream; the same
-    bytes as the host-buffer calls."""
+    """SHS_CANVAS_DEVICE: torch device tensors in and out, enqueued on torch's current stream (the
+    wrapper points the context at it); the same bytes as the host-buffer calls."""
     import torch
     import shs_gpu
     W, H = 320, 200
@@ -177,8 +177,9 @@ def test_canvas_passes_device_buffers():
         stream = torch.cuda.Stream()
         torch.cuda.set_stream(stream)
         t_src, t_depth, t_vel = (torch.from_numpy(a).cuda() for a in (src, depth, vel))
-        ctx.set_stream(stream.cuda_stream)
+        # no ctx.set_stream: device-tensor calls run on torch's current stream by themselves
         dev_mb = ctx.canvas_motion_blur(t_src, t_depth, t_vel, view, proj, pview, pproj)
+        assert ctx.stream == stream.cuda_stream
         dev_g = ctx.canvas_gaussian_blur(t_src, False)
         t_col = t_src.clone()
         _, dev_b, dev_f = ctx.canvas_dof(t_col, t_depth)

@@ -170,3 +170,66 @@ def test_legacy_binned_hair_shards_compose():
         assert np.array_equal(od.view(np.uint32), fd.view(np.uint32)) and np.array_equal(oc, fc)
     finally:
         ctx.close()
+
+
+class _RankZeroDist:
+    """torch.distributed stand-in for rank 0 of `count` ranks in one process: gather() fills rank 0's
+    receive list with its own buffer and the peers' packed buffers (rendered by other contexts)."""
+
+    def __init__(self, count, peers):
+        self.count, self.peers = count, peers
+
+    def get_rank(self):
+        return 0
+
+    def get_world_size(self):
+        return self.count
+
+    def gather(self, buf, gather_list=None, dst=0):
+        assert dst == 0 and gather_list is not None and len(gather_list) == self.count
+        gather_list[0].copy_(buf)
+        for r in range(1, self.count):
+            gather_list[r].copy_(self.peers[r])
+
+
+def test_gather_frame_device_reuses_buffers():
+    """shard.gather_frame_device (the bench's N > 1 gather) called twice with the same `out` list, for
+    two different frames: rank 0's composed present staging equals the unsharded frame's each time
+    (it returns the buffer list; nothing called it in a test)."""
+    import torch
+    import shs_gpu
+    from shs_gpu import scene_lib, shard
+    count = 3
+    root = shs_gpu.Context(0)
+    peers = [shs_gpu.Context(0) for _ in range(count - 1)]
+    full = shs_gpu.Context(0)
+    out = None
+    try:
+        root.fuse_tonemap(1.0, 2.2, ldr=False, present=True)
+        for yaw in (0.0, 25.0):
+            frame, draws, _, _, _ = scene_lib.c5_scene(352, 200, yaw=yaw)
+            full.render_pbr_forward(frame, draws)
+            full.tonemap(1.0, 2.2, ldr=False, present=True)
+            _, want = full.resolve_ldr()
+            packed = [None]
+            for r, c in enumerate(peers, start=1):
+                frame.shard_rank, frame.shard_count = r, count
+                c.fuse_tonemap(1.0, 2.2, ldr=False, present=True)
+                c.render_pbr_forward(frame, draws)
+                b = torch.zeros(c.tiles_packed_words(c.TARGET_LIB_PRESENT, count), dtype=torch.int32, device="cuda:0")
+                c.tiles_pack(c.TARGET_LIB_PRESENT, r, count, b.data_ptr())
+                c.synchronize_lib()
+                packed.append(b)
+            frame.shard_rank, frame.shard_count = 0, count
+            root.render_pbr_forward(frame, draws)
+            prev = out
+            out = shard.gather_frame_device(_RankZeroDist(count, packed), root, root.TARGET_LIB_PRESENT, out=out)
+            assert len(out) == count + 1
+            if prev is not None:
+                assert all(a is b for a, b in zip(prev, out)), "the out buffers were not reused"
+            torch.cuda.synchronize()
+            _, got = root.resolve_ldr()
+            assert np.array_equal(got, want), f"yaw {yaw}: composed frame differs"
+    finally:
+        for c in [root, full] + peers:
+            c.close()

@@ -5,6 +5,8 @@ row pitch, for single frames and batches, clear colour and sharded frames."""
 import numpy as np
 import pytest
 
+from helpers import assert_color_parity
+
 
 def test_oracle_present_is_row_flip(oracle_mod):
     rng = np.random.default_rng(1)
@@ -18,16 +20,19 @@ def test_present_matches_oracle(gpu_ctx, oracle_mod, cfg):
     from shs_gpu import scene
     frame, draws = scene.config(cfg, yaw=5.0)
     frame.present = True
+    frame.prequant = True
     frame.clear_color = (9, 18, 27, 255)
     gpu_ctx.render(frame, draws)
     color, _ = gpu_ctx.resolve()
+    pq = gpu_ctx.resolve_prequant(0)
     pres = gpu_ctx.resolve_present(0)
     assert np.array_equal(pres, oracle_mod.sdl_present(color))
-    rc, rd, _ = oracle_mod.render_legacy(frame.width, frame.height, draws, threads=8)
+    rc, rd, rpq = oracle_mod.render_legacy(frame.width, frame.height, draws, threads=8, prequant=True)
     rc[(rd == np.finfo(np.float32).max)[::-1]] = (9, 18, 27, 255)   # depth: screen rows; colour: canvas rows
-    ref = oracle_mod.sdl_present(rc)
-    d8 = np.abs(pres.astype(np.int16) - ref.astype(np.int16))
-    assert d8.max() <= 1 and (d8 > 0).sum() <= 16   # truncation-boundary bytes only (see test_gpu_parity)
+    # the staging is the canvas's row flip, and the canvas matches the oracle under the colour rule
+    # (a byte may differ by 1 only where both pre-truncation floats agree within 1e-5)
+    assert_color_parity(color, rc, pq, rpq)
+    assert_color_parity(pres, oracle_mod.sdl_present(rc), pq[::-1], rpq[::-1])
 
 
 @pytest.mark.gpu
