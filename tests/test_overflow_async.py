@@ -63,9 +63,12 @@ def test_overflowed_batch_through_present_device_async_copy(oracle_mod, mode):
             assert rc == 0
         ctx.synchronize()
         st = ctx.stats()
+        # the first pass overflowed: more ghost fragments than the 8-entry list held and, in bin mode,
+        # more bin entries than one per 32x32 tile plus an 8-entry spill list (the statistics are the
+        # re-issued pass's, whose bin capacity already grew to the fullest tile: nothing spills there)
         assert st["ghost_fragments"] > 8, st
         if mode == 2:
-            assert st["spilled"] > 8, st
+            assert st["bin_entries"] > 3 * ((W + 31) // 32) * ((H + 31) // 32) + 8, st
         pqs = [ctx.resolve_prequant(k) for k in range(len(fds))]
         _check_frames(oracle_mod, fds, host.numpy(), pqs)
     finally:
