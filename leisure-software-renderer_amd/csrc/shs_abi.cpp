@@ -47,16 +47,11 @@ int shs_create(int device, shs_ctx **out) {
         return SHS_ERR_HIP;
     }
     ctx->stream = ctx->own_stream;
-    if (hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->ov_stream, hipStreamNonBlocking) != hipSuccess) {
-        shs_destroy(ctx);
-        return SHS_ERR_HIP;
-    }
+    if (hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking) != hipSuccess) { shs_destroy(ctx); return SHS_ERR_HIP; }
     for (auto &w : ctx->lslot)
         if (hipEventCreateWithFlags(&w.setup_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&w.raster_done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&w.ov_ready, hipEventDisableTiming) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void **>(&w.h_ov), sizeof(uint32_t)) != hipSuccess) {
+            shs_host_ov_alloc(&w.h_ov) != hipSuccess) {
             shs_destroy(ctx);
             return SHS_ERR_HIP;
         }
@@ -81,7 +76,6 @@ int shs_destroy(shs_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->setup_stream) (void)hipStreamSynchronize(ctx->setup_stream);
-    if (ctx->ov_stream) (void)hipStreamSynchronize(ctx->ov_stream);
     for (auto &m : ctx->meshes) {
         if (m.pos) (void)hipFree(m.pos);
         if (m.nrm) (void)hipFree(m.nrm);
@@ -96,8 +90,7 @@ int shs_destroy(shs_ctx *ctx) {
         if (w.h_draws) (void)hipHostFree(w.h_draws);
         if (w.setup_done) (void)hipEventDestroy(w.setup_done);
         if (w.raster_done) (void)hipEventDestroy(w.raster_done);
-        if (w.ov_ready) (void)hipEventDestroy(w.ov_ready);
-        if (w.h_ov) (void)hipHostFree(w.h_ov);
+        if (w.h_ov) (void)hipHostFree(const_cast<uint32_t *>(w.h_ov));
     }
     release(ctx->counters); release(ctx->timeline);
     release(ctx->color); release(ctx->depth); release(ctx->prequant); release(ctx->present);
@@ -109,7 +102,6 @@ int shs_destroy(shs_ctx *ctx) {
     if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
-    if (ctx->ov_stream) (void)hipStreamDestroy(ctx->ov_stream);
     delete ctx;
     return SHS_OK;
 }
@@ -235,6 +227,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     shs_ctx::LegacySlot &ws = ctx->lslot[slot];
     hipStream_t sst = ctx->setup_stream, st = ctx->stream;
     if (ws.used) HIP_TRY(ctx, hipEventSynchronize(ws.setup_done));
+    *ws.h_ov = 0u;   // the slot's previous setup (the only other writer) is done
 
     if (ensure(ctx, ws.recs, nt_all) || ensure(ctx, ws.shade, nt_all) || ensure(ctx, ws.boxes, nt_all) ||
         ensure(ctx, ws.slivers, nt_all))
@@ -262,10 +255,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (want_present && ensure(ctx, ctx->present, npx * n_frames)) return SHS_ERR_HIP;
 
     // ---- setup_stream: wait for the slot's last k_raster, reset, upload, set up ----
-    if (ws.used) {
-        HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.raster_done, 0));
-        HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.ov_ready, 0));   // its overflow word was copied out
-    }
+    if (ws.used) HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.raster_done, 0));
     if (reset) {
         HIP_TRY(ctx, hipMemsetAsync(ws.busy.p, 0, ws.busy.cap * sizeof(uint32_t), sst));
         ctx->geom_key[slot] = gkey;
@@ -378,6 +368,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fb.boxes = ws.boxes.p;
     fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;
     fb.present = want_present ? ctx->present.p : nullptr;
+    fb.ov_host = const_cast<uint32_t *>(ws.h_ov);
 
     hipEvent_t *ev = nullptr;
     if (ctx->timing) {
@@ -396,10 +387,6 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (fp.ghost_list && !(fp.flags & shs_dev::DBG_SKIP_GHOST)) HIP_TRY(ctx, shs_internal::launch_ghost(fp, fb, sst));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], sst));
     HIP_TRY(ctx, hipEventRecord(ws.setup_done, sst));
-    // the overflow word is final once the setup kernels are: copy it out beside the raster
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->ov_stream, ws.setup_done, 0));
-    HIP_TRY(ctx, hipMemcpyAsync(ws.h_ov, cset + shs_dev::C_OVERFLOW, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->ov_stream));
-    HIP_TRY(ctx, hipEventRecord(ws.ov_ready, ctx->ov_stream));
     // ---- stream: after the previous batch's raster (stream order) and this batch's setup ----
     HIP_TRY(ctx, hipStreamWaitEvent(st, ws.setup_done, 0));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[3], st));
@@ -516,7 +503,7 @@ int shs_render_legacy_batch(shs_ctx *ctx, const shs_frame_desc *frame, const shs
     // set, the batch is finished -- re-issued with grown capacities -- before this one is enqueued.
     if (ctx->have_frame && ctx->need_check) {
         const shs_ctx::LegacySlot &p = ctx->lslot[ctx->last_slot];
-        HIP_TRY(ctx, hipEventSynchronize(p.ov_ready));
+        HIP_TRY(ctx, hipEventSynchronize(p.setup_done));
         if (*p.h_ov) {
             const int rc = finish_frame(ctx);
             if (rc) return rc;
@@ -712,7 +699,6 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
         int rc = finish_frame(ctx);
         if (rc) return rc;
         HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->ov_stream));
         for (auto &w : ctx->lslot) {
             if (option == SHS_OPT_SPILL_CAPACITY) {
                 release(w.spill);

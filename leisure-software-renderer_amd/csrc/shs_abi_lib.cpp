@@ -61,9 +61,8 @@ void release_work(Work &w) {
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
     if (w.ov_after) (void)hipEventDestroy(w.ov_after);
-    if (w.ov_ready) (void)hipEventDestroy(w.ov_ready);
-    if (w.h_ov) (void)hipHostFree(w.h_ov);
-    w.ov_after = w.ov_ready = nullptr;
+    if (w.h_ov) (void)hipHostFree(const_cast<uint32_t *>(w.h_ov));
+    w.ov_after = nullptr;
     w.h_ov = nullptr;
     w.ov_valid = false;
     w.resolve_ev_valid = false;
@@ -378,21 +377,18 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     }
     if (!w.ov_after) {
         HIP_TRY(ctx, hipEventCreateWithFlags(&w.ov_after, hipEventDisableTiming));
-        HIP_TRY(ctx, hipEventCreateWithFlags(&w.ov_ready, hipEventDisableTiming));
-        HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&w.h_ov), sizeof(uint32_t)));
+        HIP_TRY(ctx, shs_host_ov_alloc(&w.h_ov));
     }
-    // k_lib_setup zeroes the other parity's counters: the previous pass's overflow copy must have run
-    if (w.ov_valid) HIP_TRY(ctx, hipStreamWaitEvent(ps, w.ov_ready, 0));
+    // the previous pass's setup (the only other writer of the word) is done before it is zeroed
+    if (w.ov_valid) HIP_TRY(ctx, hipEventSynchronize(w.ov_after));
+    *w.h_ov = 0u;
+    fb.ov_host = const_cast<uint32_t *>(w.h_ov);
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], ps));
     HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, ps));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], ps));
-    // the pass's overflow word is final after its setup kernels (setup, clip, large-primitive marks):
-    // copied into pinned memory on the side stream, so superseding the pass can check it (no raster wait)
+    // the pass's overflow word is final after its setup kernels (setup, clip, large-primitive marks), so
+    // superseding the pass checks it at ov_after, without waiting for the raster
     HIP_TRY(ctx, hipEventRecord(w.ov_after, ps));
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->ov_stream, w.ov_after, 0));
-    HIP_TRY(ctx, hipMemcpyAsync(w.h_ov, w.counters.p + fp.parity * shs_dev::LC_N + shs_dev::LC_OVERFLOW, sizeof(uint32_t),
-                                hipMemcpyDeviceToHost, ctx->ov_stream));
-    HIP_TRY(ctx, hipEventRecord(w.ov_ready, ctx->ov_stream));
     w.ov_valid = true;
     HIP_TRY(ctx, shs_internal::launch_lib_raster(fp, fb, shadow, shallow, raster_grid, ps));
     if (!shadow) {   // the camera pass's shading runs in its own kernel (event [2] closes both)
@@ -428,7 +424,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
 int lib_finish(shs_ctx *ctx);
 int check_superseded(shs_ctx *ctx, Work &w) {
     if (!w.need_check || !w.ov_valid) return SHS_OK;
-    HIP_TRY(ctx, hipEventSynchronize(w.ov_ready));
+    HIP_TRY(ctx, hipEventSynchronize(w.ov_after));
     return *w.h_ov ? lib_finish(ctx) : SHS_OK;
 }
 

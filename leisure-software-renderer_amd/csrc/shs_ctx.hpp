@@ -65,15 +65,14 @@ struct shs_ctx {
         DevBuf<uint4> blk_stat;              // per setup block
         DevBuf<uint2> rstat;                 // per raster block
         hipEvent_t setup_done = nullptr, raster_done = nullptr;
-        // the batch's overflow word, copied into pinned host memory on ov_stream once its setup is
-        // done (ov_ready): a batch about to be superseded is checked without waiting for its raster
-        uint32_t *h_ov = nullptr;
-        hipEvent_t ov_ready = nullptr;
+        // the batch's overflow word in mapped, coherent host memory: the setup kernels store 1 into it
+        // with every overflow bit, so once setup_done has fired the host reads it without a copy and
+        // without waiting for the raster (checked before the batch is superseded)
+        volatile uint32_t *h_ov = nullptr;
         bool used = false;
     };
     LegacySlot lslot[2];
     hipStream_t setup_stream = nullptr;
-    hipStream_t ov_stream = nullptr; // overflow-word copies (legacy slots, library passes)
     DevBuf<uint32_t> counters;       // 2 sets (one per slot) of CSET words
     uint32_t busy_epoch = 0;         // FrameParams::epoch of the last launch (never 0)
     int last_slot = 0;
@@ -139,10 +138,10 @@ struct shs_ctx {
         size_t h_cap = 0;
         hipEvent_t slot_ev[2] = {nullptr, nullptr};
         bool slot_used[2] = {false, false};
-        // the pass's overflow word in pinned host memory, copied on ov_stream after its setup kernels
-        // (ov_after on the pass stream, ov_ready once copied): checked before the pass is superseded
-        uint32_t *h_ov = nullptr;
-        hipEvent_t ov_after = nullptr, ov_ready = nullptr;
+        // the pass's overflow word in mapped host memory (raise_overflow), final at ov_after (recorded
+        // after its setup kernels): checked before the pass is superseded
+        volatile uint32_t *h_ov = nullptr;
+        hipEvent_t ov_after = nullptr;
         bool ov_valid = false;
         int slot = 0;
         uint64_t geom_key = ~0ull;
@@ -262,6 +261,17 @@ inline void release(DevBuf<T> &b) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.cap = 0;
+}
+
+// One overflow word in mapped, coherent (fine-grained) host memory, zeroed: kernels store into it
+// through its device alias (the same address under unified addressing), the host reads it directly.
+inline hipError_t shs_host_ov_alloc(volatile uint32_t **out) {
+    void *p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    *static_cast<volatile uint32_t *>(p) = 0u;
+    *out = static_cast<volatile uint32_t *>(p);
+    return hipSuccess;
 }
 
 inline int set_dev(shs_ctx *ctx) {

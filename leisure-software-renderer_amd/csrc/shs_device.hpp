@@ -172,7 +172,16 @@ struct FrameBuffers {
     float4 *prequant;                // per frame: W*H (optional)
     uint32_t *present;               // per frame: W*H RGBA8 SDL staging, rows top-down (optional,
                                      // SHS_FRAME_PRESENT: Canvas::copy_to_SDLSurface's layout)
+    uint32_t *ov_host;               // the slot's overflow word in mapped host memory: set to 1 with
+                                     // every overflow bit (read by the host before superseding)
 };
+
+// A capacity overflow: the counter-set bit (finish_frame / check_pass read it) and the mapped host
+// word the host reads when the batch is superseded (a system-scope vector store, rare).
+__device__ __forceinline__ void raise_overflow(uint32_t *word, uint32_t bit, uint32_t *ov_host) {
+    atomicOr(word, bit);
+    if (ov_host) __hip_atomic_store(ov_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // The buffers of frame f of the batch (shared buffers unchanged).
 __device__ __forceinline__ FrameBuffers frame_view(const FrameParams &fp, const FrameBuffers &fb, int f) {

@@ -460,7 +460,7 @@ __device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const Frame
                 fb.frags[slot] = g;
                 mark_busy_direct(fp, fb, cnt, (int)frame, (py / RTH) * fp.tiles_x + px / RTW);
             } else {
-                atomicOr(&cnt[C_OVERFLOW], OV_FRAG);
+                raise_overflow(&cnt[C_OVERFLOW], OV_FRAG, fb.ov_host);
             }
         }
     }
@@ -499,7 +499,7 @@ __device__ __forceinline__ void append_bin(const FrameParams &fp, const FrameBuf
     } else {
         const uint32_t sp = atomicAdd(&cnt[C_SPILL], 1u);
         if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)(frame * fp.tiles_x * fp.tiles_y + t), id);
-        else atomicOr(&cnt[C_OVERFLOW], OV_SPILL);
+        else raise_overflow(&cnt[C_OVERFLOW], OV_SPILL, fb.ov_host);
     }
 }
 

@@ -270,7 +270,7 @@ __device__ __forceinline__ void lib_append_bin(const LibFrameParams &fp, const L
     } else {
         const uint32_t sp = atomicAdd(&cnt[LC_SPILL], 1u);
         if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t, id);
-        else atomicOr(&cnt[LC_OVERFLOW], LOV_SPILL);
+        else raise_overflow(&cnt[LC_OVERFLOW], LOV_SPILL, fb.ov_host);
     }
 }
 
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(256) void k_lib_clip(LibFrameParams fp, LibBuffers 
             e = grp_shfl(e, seg);
             if ((uint32_t)e + (uint32_t)(m - 3) > fp.extra_cap) {
                 if (li == 0) {
-                    atomicOr(&cnt[LC_OVERFLOW], LOV_EXTRA);
+                    raise_overflow(&cnt[LC_OVERFLOW], LOV_EXTRA, fb.ov_host);
                     store_box(fb, (uint32_t)tri, 0, -1, 0, -1);
                 }
                 continue;

@@ -145,6 +145,7 @@ struct LibBuffers {
     // fused PassTonemap (shs_lib_fuse_tonemap): k_lib_resolve also writes the tonemapped bytes
     const float *tm_thr;             // the 256 byte thresholds (shs_post_internal.hpp), null: not fused
     uint32_t *tm_ldr, *tm_present;   // RT_ColorLDR (rows y up) / present staging (rows top-down), or null
+    uint32_t *ov_host;               // the pass's overflow word in mapped host memory (raise_overflow)
 };
 
 // k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket
