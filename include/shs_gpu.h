@@ -230,6 +230,15 @@ int shs_gpu_tile_size(void);
 int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const float *normals, int32_t n_normals,
                     const float *uvs, int32_t n_uvs, const uint32_t *indices, int64_t n_indices, int32_t *mesh_id);
 
+/* Texture2DData (resources/texture.hpp:23-49): w * h Color texels (RGBA8, texel (x, y) at byte
+ * 4 * (y * w + x)), device resident from here on.  *tex_id is >= 1 (the TextureAssetHandle convention,
+ * resource_registry.hpp:62-66: 0 = no texture).  The PBR and Blinn-Phong programs sample it at the
+ * perspective-correct UV0 varying with sample_texture2d_bilinear_repeat_linear (shader/
+ * builtin_shaders.hpp:25-55; the sRGB decode uses the host's std::pow values).  A texture that fails
+ * Texture2DData::valid() is not uploaded: the caller passes 0, as the sampler then returns vec3(1). */
+int shs_texture_upload(shs_ctx *ctx, const uint8_t *rgba, int32_t w, int32_t h, int32_t *tex_id);
+int shs_texture_release(shs_ctx *ctx, int32_t tex_id);
+
 /* One rasterize_mesh call as PassPBRForward issues it per RenderItem: the ShaderUniforms fields the
  * builtin programs read (shader/types.hpp:87-116) and RasterizerConfig's cull mode / front face.
  * shadow != 0: u.shadow_map = the context's shadow map (last shs_render_shadow_map). */
@@ -247,6 +256,7 @@ typedef struct shs_lib_draw {
     int32_t shadow_pcf_radius;
     float shadow_pcf_step, shadow_strength;
     int32_t enable_motion_vectors;
+    int32_t base_color_tex;       /* u.base_color_tex: a shs_texture_upload id, 0 = none (sample = vec3(1)) */
 } shs_lib_draw;
 
 #define SHS_LIB_DEPTH_MOTION 1u   /* RasterizerTarget::depth_motion present: z test, depth + motion */

@@ -184,13 +184,34 @@ private:
     std::unordered_map<const shs::MeshData *, int32_t> ids_;
 };
 
-// Shared by the passes of one pipeline: the device context, its meshes and whether the device shadow
-// map belongs to the current frame.
+// Device-resident Texture2DData (resources/texture.hpp:23-49), uploaded on first use; an invalid one
+// (Texture2DData::valid() false) maps to 0 -- the sampler's vec3(1) (builtin_shaders.hpp:35).
+class GpuTextures {
+public:
+    explicit GpuTextures(shs_ctx *ctx) : ctx_(ctx) {}
+    int32_t id(const shs::Texture2DData *t) {
+        if (!t || !t->valid()) return 0;
+        auto it = ids_.find(t);
+        if (it != ids_.end()) return it->second;
+        int32_t id = 0;
+        check(ctx_, shs_texture_upload(ctx_, &t->texels[0].r, t->w, t->h, &id));
+        ids_.emplace(t, id);
+        return id;
+    }
+
+private:
+    shs_ctx *ctx_;
+    std::unordered_map<const shs::Texture2DData *, int32_t> ids_;
+};
+
+// Shared by the passes of one pipeline: the device context, its meshes and textures, and whether the
+// device shadow map belongs to the current frame.
 struct GpuPassRuntime {
     Device device;
     GpuMeshes meshes;
+    GpuTextures textures;
     bool resolve_shadow_to_host = false;   // also fill RT_ShadowDepth (for CPU consumers: shadow debug)
-    explicit GpuPassRuntime(int device_index = 0) : device(device_index), meshes(device.ctx) {}
+    explicit GpuPassRuntime(int device_index = 0) : device(device_index), meshes(device.ctx), textures(device.ctx) {}
 };
 
 // RenderItem transform, as both passes build it (pass_shadow_map.hpp:56-64, pass_pbr_forward.hpp:136-141).
@@ -303,7 +324,10 @@ public:
             const shs::MeshData *mesh = scene.resources->get_mesh((shs::MeshAssetHandle)item.mesh);
             if (!mesh || mesh->empty()) continue;
             const shs::MaterialData *mat = scene.resources->get_material((shs::MaterialAssetHandle)item.mat);
-            if (mat && mat->base_color_tex != 0) unsupported("base-colour textures");
+            // u.base_color_tex (:173-176): the registry's Texture2DData, sampled on the device
+            const int32_t tex_id = (mat && mat->base_color_tex != 0)
+                                       ? rt_->textures.id(scene.resources->get_texture(mat->base_color_tex))
+                                       : 0;
             const glm::mat4 model = item_model(item);
             uint64_t key = item.object_id;                                         // :143-148
             if (key == 0) {
@@ -344,6 +368,7 @@ public:
                 d.shadow_strength = fp.pass.shadow.strength;
             }
             d.enable_motion_vectors = fp.pass.motion_vectors.enable ? 1 : 0;
+            d.base_color_tex = tex_id;
             draws_.push_back(d);
         }
 

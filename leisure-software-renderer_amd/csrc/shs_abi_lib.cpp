@@ -56,7 +56,7 @@ void release_work(Work &w) {
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
     if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
@@ -118,6 +118,15 @@ void build_lib_draw(const shs_lib_draw &in, const Mesh &m, int32_t base, LibDraw
     const int32_t rad = std::max(0, in.shadow_pcf_radius);
     std::memcpy(&o.shp[2], &rad, sizeof rad);
     o.shp[3] = (1.0f < in.shadow_pcf_step) ? in.shadow_pcf_step : 1.0f;
+}
+
+// u.base_color_tex (pass_pbr_forward.hpp:173-176): texture id k >= 1, 0 = none.
+void bind_texture(const shs_ctx *ctx, int32_t id, LibDrawGPU &o) {
+    if (id <= 0) return;
+    const Texture &t = ctx->textures[(size_t)id - 1];
+    o.tex = t.texels;
+    o.tex_w = t.w;
+    o.tex_h = t.h;
 }
 
 // Upload the draw table through the work's pinned 2-slot staging.  A table equal to the one the
@@ -229,6 +238,17 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (!shadow && (ensure(ctx, w.shade, n_slots) || ensure(ctx, w.xbase, (size_t)std::max(n_tris, 1)) ||
                     ensure(ctx, w.clipq, (size_t)std::max(n_tris, 1))))
         return SHS_ERR_HIP;
+    bool textured = false;
+    for (const auto &d : w.last_draws) textured = textured || d.tex != nullptr;
+    if (textured && !shadow) {
+        if (ensure(ctx, w.uvw, 2 * n_slots)) return SHS_ERR_HIP;
+        if (!ctx->srgb_lut.p) {   // srgb_to_linear_rgb (builtin_shaders.hpp:25-31) with the host's std::pow
+            float lut[256];
+            for (int i = 0; i < 256; ++i) lut[i] = std::pow((float)i / 255.0f, 2.2f);
+            if (ensure(ctx, ctx->srgb_lut, 256)) return SHS_ERR_HIP;
+            HIP_TRY(ctx, hipMemcpy(ctx->srgb_lut.p, lut, sizeof lut, hipMemcpyHostToDevice));
+        }
+    }
     // every slot enters the large-primitive queue at most once
     if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots)) return SHS_ERR_HIP;
     int st = 2;   // supertile edge in bin tiles (SHS_LIB_XCD_ST: timing experiments; 0 = plain order)
@@ -329,6 +349,8 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     } else {
         fb.hdr = ctx->lib_hdr.p; fb.depth = ctx->lib_depth.p; fb.motion = ctx->lib_motion.p;
         fb.keys = ctx->lib_keys.p;
+        fb.uvw = textured ? w.uvw.p : nullptr;
+        fb.srgb_lut = ctx->srgb_lut.p;
         fb.blkcov = ctx->lib_blkcov.p;
         if (w.tm_fused) {   // PassTonemap in k_lib_resolve (shs_lib_fuse_tonemap)
             const shs_tonemap_desc &d = w.tm_desc;
@@ -498,6 +520,10 @@ int check_lib_mesh(shs_ctx *ctx, int32_t id) {
 void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_cam);
     release_work(ctx->lib_shadow);
+    for (auto &t : ctx->textures)
+        if (t.texels) (void)hipFree(t.texels);
+    ctx->textures.clear();
+    release(ctx->srgb_lut);
     release(ctx->lib_hdr); release(ctx->lib_keys); release(ctx->lib_blkcov); release(ctx->tm_thr_dev); ctx->tm_thr_dev_gamma = -1.0f; release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
     release(ctx->lights); release(ctx->cull_work); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
@@ -557,6 +583,33 @@ int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const
     m.live = true;
     ctx->meshes.push_back(m);
     *mesh_id = (int32_t)ctx->meshes.size() - 1;
+    return SHS_OK;
+}
+
+int shs_texture_upload(shs_ctx *ctx, const uint8_t *rgba, int32_t w, int32_t h, int32_t *tex_id) {
+    if (!ctx || !rgba || !tex_id || w <= 0 || h <= 0 || (int64_t)w * h > (1ll << 28)) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    Texture t;
+    const size_t bytes = (size_t)w * h * 4;
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&t.texels), bytes));
+    HIP_TRY(ctx, hipMemcpy(t.texels, rgba, bytes, hipMemcpyHostToDevice));
+    t.w = w;
+    t.h = h;
+    t.live = true;
+    ctx->textures.push_back(t);
+    *tex_id = (int32_t)ctx->textures.size();   // TextureAssetHandle convention: 1-based, 0 = none
+    return SHS_OK;
+}
+
+int shs_texture_release(shs_ctx *ctx, int32_t tex_id) {
+    if (!ctx || tex_id <= 0 || tex_id > (int32_t)ctx->textures.size() || !ctx->textures[(size_t)tex_id - 1].live)
+        return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
+    Texture &t = ctx->textures[(size_t)tex_id - 1];
+    HIP_TRY(ctx, hipFree(t.texels));
+    t = Texture{};
     return SHS_OK;
 }
 
@@ -643,6 +696,11 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
         }
         if (draws[i].cull_mode < SHS_CULL_NONE || draws[i].cull_mode > SHS_CULL_FRONT) { ctx->err = "bad cull mode"; return SHS_ERR_INVALID; }
         if (draws[i].shadow && !ctx->have_shadow) { ctx->err = "draw samples a shadow map but none was rendered"; return SHS_ERR_INVALID; }
+        const int32_t tx = draws[i].base_color_tex;
+        if (tx < 0 || tx > (int32_t)ctx->textures.size() || (tx > 0 && !ctx->textures[(size_t)tx - 1].live)) {
+            ctx->err = "bad base_color_tex (not a live texture id)";
+            return SHS_ERR_INVALID;
+        }
     }
     if (set_dev(ctx)) return SHS_ERR_HIP;
     if (!ctx->h_lib_counters && hipHostMalloc(reinterpret_cast<void **>(&ctx->h_lib_counters), shs_dev::LC_N * sizeof(uint32_t)) != hipSuccess)
@@ -664,6 +722,7 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     for (int i = 0; i < n_draws; ++i) {
         const Mesh &m = ctx->meshes[draws[i].mesh_id];
         build_lib_draw(draws[i], m, base, wk.last_draws[i]);
+        bind_texture(ctx, draws[i].base_color_tex, wk.last_draws[i]);
         base += m.n_tris;
     }
     LibFrameParams fp;

@@ -29,6 +29,13 @@ struct Mesh {
     float bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
 };
 
+// A Texture2DData (resources/texture.hpp:23-49) on the device: w * h Color texels, y * w + x.
+struct Texture {
+    uint32_t *texels = nullptr;
+    int32_t w = 0, h = 0;
+    bool live = false;
+};
+
 template <typename T>
 struct DevBuf {
     T *p = nullptr;
@@ -36,6 +43,7 @@ struct DevBuf {
 };
 }  // namespace shs_host_detail
 using shs_host_detail::Mesh;
+using shs_host_detail::Texture;
 using shs_host_detail::DevBuf;
 
 struct shs_ctx {
@@ -44,6 +52,7 @@ struct shs_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     std::vector<Mesh> meshes;
+    std::vector<Texture> textures;   // texture id k (>= 1, the TextureAssetHandle convention) at k - 1
 
     // Legacy-path workspace, double-buffered: batch n uses slot n & 1.  Its k_setup (plus the draw-table
     // copy and the counter resets) runs on setup_stream while batch n-1's k_raster still runs on
@@ -134,6 +143,7 @@ struct shs_ctx {
         bool resolve_ev_valid = false;
         shs_tonemap_desc tm_desc{};
         DevBuf<uint2> spill, blk_stat, rstat;
+        DevBuf<float4> uvw;                                // UV0 varyings of textured draws' slots
         shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots
         size_t h_cap = 0;
         hipEvent_t slot_ev[2] = {nullptr, nullptr};
@@ -172,6 +182,7 @@ struct shs_ctx {
     DevBuf<unsigned long long> lib_keys;  // camera pass winner keys (k_lib_raster -> k_lib_resolve)
     DevBuf<uint32_t> lib_blkcov;          // ... and per 16x4 block whether it holds any
     int lib_resolve_resident[3] = {0, 0, 0};   // resident k_lib_resolve workgroups (Forward+, PBR, mixed)
+    DevBuf<float> srgb_lut;               // srgb_to_linear_rgb table (texture sampling)
     DevBuf<float> lib_depth;
     DevBuf<float2> lib_motion;
     DevBuf<float> shadow_map;

@@ -117,12 +117,16 @@ struct LVert {
     float u, v;
 };
 
-// The normal varying of a vertex (the half of make_default_vertex_out that only surviving
-// primitives need; UV0 is not read by any builtin program, LibShade).
+// The normal and UV0 varyings of a vertex (the half of make_default_vertex_out that only surviving
+// primitives need; UV0 only for draws that sample a base_color_tex).
 __device__ __forceinline__ void vertex_attrs(const LibDrawGPU &dr, uint32_t id, LVert &o) {
     const float *N = dr.nrm + 3 * (size_t)id;
     const f3 n = normalize3(m3v(dr.nmat, f3{N[0], N[1], N[2]}));
     o.nx = n.x; o.ny = n.y; o.nz = n.z;
+    if (dr.tex) {
+        const float2 t = *reinterpret_cast<const float2 *>(dr.uv + 2 * (size_t)id);
+        o.u = t.x; o.v = t.y;
+    }
 }
 
 // Clip and world position (the varyings are left 0 until vertex_attrs).
@@ -455,6 +459,10 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     s.draw = d;
     s.pad = 0;
     if (!(fp.exp_flags & 1u)) fb.shade[slot] = s;
+    if (dr.tex) {   // UV0 varying * 1/w (varw, rasterizer.hpp:319-326)
+        fb.uvw[2 * (size_t)slot] = make_float4(a.u * iw0, a.v * iw0, b.u * iw1, b.v * iw1);
+        fb.uvw[2 * (size_t)slot + 1] = make_float4(c.u * iw2, c.v * iw2, 0.0f, 0.0f);
+    }
     store_box(fb, slot, x0, x1, y0, y1);
     if (fp.exp_flags & 2u) return;
     if (DIRECT) {
@@ -1193,12 +1201,38 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
     return f3{g_clamp(lit.x, 0.0f, 1.0f), g_clamp(lit.y, 0.0f, 1.0f), g_clamp(lit.z, 0.0f, 1.0f)};
 }
 
-// The builtin fragment programs (builtin_shaders.hpp:105-245); no base_color_tex -> albedo_tex = 1.
+// sample_texture2d_bilinear_repeat_linear (builtin_shaders.hpp:33-55): repeat wrap, bilinear over
+// srgb_to_linear_rgb (:25-31) texels; the sRGB decode is the host-computed table of the reference's
+// own std::pow values (bit-identical), the lerps glm::mix's x * (1 - a) + y * a.  Indices are clamped
+// into the texture, which only changes non-finite UVs (where the reference reads out of bounds).
+__device__ __forceinline__ f3 srgb_texel(const LibBuffers &fb, uint32_t c) {
+    return f3{fb.srgb_lut[c & 0xffu], fb.srgb_lut[(c >> 8) & 0xffu], fb.srgb_lut[(c >> 16) & 0xffu]};
+}
+
+__device__ __noinline__ f3 sample_base_color(const LibBuffers &fb, const LibDrawGPU &dr, float uvx, float uvy) {
+    const float u = uvx - floorf(uvx);
+    const float v = uvy - floorf(uvy);
+    const float fx = u * (float)(dr.tex_w - 1);
+    const float fy = v * (float)(dr.tex_h - 1);
+    const int x0 = min(max((int)floorf(fx), 0), dr.tex_w - 1);
+    const int y0 = min(max((int)floorf(fy), 0), dr.tex_h - 1);
+    const int x1 = min(x0 + 1, dr.tex_w - 1);
+    const int y1 = min(y0 + 1, dr.tex_h - 1);
+    const float tx = fx - (float)x0;
+    const float ty = fy - (float)y0;
+    const uint32_t *row0 = dr.tex + (size_t)y0 * dr.tex_w, *row1 = dr.tex + (size_t)y1 * dr.tex_w;
+    const f3 c00 = srgb_texel(fb, row0[x0]), c10 = srgb_texel(fb, row0[x1]);
+    const f3 c01 = srgb_texel(fb, row1[x0]), c11 = srgb_texel(fb, row1[x1]);
+    return mix3(mix3(c00, c10, tx), mix3(c01, c11, tx), ty);
+}
+
+// The builtin fragment programs (builtin_shaders.hpp:105-245); tex = the base_color_tex sample
+// (vec3(1) without a texture, :35).
 // PROG >= 0: every draw of the pass runs that program (k_lib_resolve specialisations: only its
 // registers are live); -1: per draw.
 template <int PROG>
 __device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, float depth01,
-                           int px, int py, const LtWave &st) {
+                           int px, int py, const LtWave &st, f3 tex = f3{1.0f, 1.0f, 1.0f}) {
     const f3 bc = {dr.base[0], dr.base[1], dr.base[2]};
     const int program = PROG >= 0 ? PROG : dr.program;
     if (program == 5) return forward_plus(fp, fb, dr, world, nrm, px, py, st);
@@ -1211,7 +1245,7 @@ __device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const
     const f3 L = {dr.L[0], dr.L[1], dr.L[2]};
     const f3 cam = {dr.cam[0], dr.cam[1], dr.cam[2]};
     const f3 lcol = {dr.lcol[0], dr.lcol[1], dr.lcol[2]};
-    const f3 albedo = gmax3(bc, f3{0.0f, 0.0f, 0.0f});   // base_color * vec3(1)
+    const f3 albedo = gmax3(mul3(bc, tex), f3{0.0f, 0.0f, 0.0f});   // max(base_color * albedo_tex, 0)
     const f3 N = normalize3(nrm);
     const f3 V = normalize3(sub3(cam, world));
     if (program == 1) {   // make_blinn_phong_program (:111-150)
@@ -1300,8 +1334,8 @@ __device__ __forceinline__ LibRec lib_rec_from(const float4 *s) {
 
 template <int PROG>
 __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
-                                         const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv,
-                                         const LtWave &st);
+                                         const LibShade &s, uint32_t slot, int px, int py, float4 &color, float &depth,
+                                         float2 &mv, const LtWave &st);
 
 // Resolve one pixel of a tile (one thread): the winner of the key array is re-evaluated with the
 // identical arithmetic, shaded and written; pixels without a winner get the clear values.
@@ -1326,8 +1360,8 @@ __device__ __forceinline__ float4 lib_resolve(const LibFrameParams &fp, const Li
         const LibShade s = fb.shade[slot];
         // a wave whose covered pixels share one draw reads its uniforms with scalar loads
         const int d0 = __builtin_amdgcn_readfirstlane(s.draw);
-        if (__ballot(s.draw != d0) == 0) shade_px<PROG>(fp, fb, fb.draws[d0], r, s, px, py, color, depth, mv, st);
-        else shade_px<PROG>(fp, fb, fb.draws[s.draw], r, s, px, py, color, depth, mv, st);
+        if (__ballot(s.draw != d0) == 0) shade_px<PROG>(fp, fb, fb.draws[d0], r, s, slot, px, py, color, depth, mv, st);
+        else shade_px<PROG>(fp, fb, fb.draws[s.draw], r, s, slot, px, py, color, depth, mv, st);
     }
     fb.hdr[o] = color;
     if (fp.flags & LF_DEPTH) {
@@ -1341,8 +1375,8 @@ __device__ __forceinline__ float4 lib_resolve(const LibFrameParams &fp, const Li
 // fragment program (rasterizer.hpp:341-419).
 template <int PROG>
 __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, const LibRec &r,
-                                         const LibShade &s, int px, int py, float4 &color, float &depth, float2 &mv,
-                                         const LtWave &st) {
+                                         const LibShade &s, uint32_t slot, int px, int py, float4 &color, float &depth,
+                                         float2 &mv, const LtWave &st) {
     {
         float z01, u, v, w, idn;
         lib_test<false>(fp, r, px, py, z01, u, v, w, idn);
@@ -1369,7 +1403,15 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
                 mv = make_float2(vx, vy);
             }
         }
-        const f3 c = lib_fragment<PROG>(fp, fb, dr, world, nrm, z01, px, py, st);
+        f3 tex = {1.0f, 1.0f, 1.0f};
+        if (PROG != 5 && dr.tex) {   // fin.uv from the UV0 varying (rasterizer.hpp:383-387)
+            const size_t slot2 = 2 * (size_t)slot;
+            const float4 a = fb.uvw[slot2], b = fb.uvw[slot2 + 1];
+            const float uvx = ((u * a.x + v * a.z) + w * b.x) * idn;
+            const float uvy = ((u * a.y + v * a.w) + w * b.y) * idn;
+            tex = sample_base_color(fb, dr, uvx, uvy);
+        }
+        const f3 c = lib_fragment<PROG>(fp, fb, dr, world, nrm, z01, px, py, st, tex);
         color = make_float4(c.x, c.y, c.z, 1.0f);
     }
 }

@@ -30,6 +30,8 @@ struct alignas(16) LibDrawGPU {
     float base[4];           // u.base_color, u.metallic
     float mat[4];            // u.roughness, u.ao, u.shadow_strength, 0
     float shp[4];            // bias_const, bias_slope, pcf radius (int bits), pcf_step
+    const uint32_t *tex;     // u.base_color_tex: Texture2DData texels (Color RGBA8, y * w + x), or null
+    int32_t tex_w, tex_h;
 };
 
 // Raster record of one primitive (a fan triangle of a clipped input triangle, or a shadow-pass
@@ -46,9 +48,8 @@ struct alignas(16) LibRec {
 static_assert(sizeof(LibRec) == 64, "LibRec must stay 64 B");
 
 // Perspective-premultiplied varyings of the primitive's corners (varw, rasterizer.hpp:309-328) that
-// the builtin programs read.  The UV0 varying is not kept: no builtin program samples a texture
-// (base_color_tex is out of scope), so it would be 24 B per primitive written
-// and never read.
+// the builtin programs read.  The UV0 varying lives in its own per-slot plane (LibBuffers::uvw), written
+// and read only for draws with a base_color_tex: untextured passes move no UV bytes.
 struct alignas(16) LibShade {
     float wp[9];                 // WorldPos varying * 1/w
     float n[9];                  // NormalWS varying * 1/w
@@ -146,6 +147,8 @@ struct LibBuffers {
     const float *tm_thr;             // the 256 byte thresholds (shs_post_internal.hpp), null: not fused
     uint32_t *tm_ldr, *tm_present;   // RT_ColorLDR (rows y up) / present staging (rows top-down), or null
     uint32_t *ov_host;               // the pass's overflow word in mapped host memory (raise_overflow)
+    float4 *uvw;                     // per slot, 2 float4: UV0 varying * 1/w of the 3 corners (textured draws)
+    const float *srgb_lut;           // srgb_to_linear_rgb's 256 values, std::pow(c / 255.0f, 2.2f) on the host
 };
 
 // k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket

@@ -571,12 +571,27 @@ class Context:
         self._check(self._lib.shs_resolve_shadow_map(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         return out
 
+    def upload_texture(self, tex) -> int:
+        """shs_texture_upload of a lib_path.Texture2D (cached per object) -> texture id (>= 1)."""
+        key = ("tex", id(tex))
+        if key in self._meshes:
+            return self._meshes[key][0]
+        rgba = np.ascontiguousarray(tex.rgba, dtype=np.uint8)
+        assert rgba.ndim == 3 and rgba.shape[2] == 4
+        tid = ctypes.c_int32()
+        self._check(self._lib.shs_texture_upload(self._h, rgba.ctypes.data_as(ctypes.c_void_p), rgba.shape[1],
+                                                 rgba.shape[0], ctypes.byref(tid)))
+        self._meshes[key] = (tid.value, tex)
+        return tid.value
+
     def prepare_lib(self, frame, draws):
         from ._abi import LibDrawC
         from .lib_path import fill_draw_struct
         arr = (LibDrawC * max(len(draws), 1))()
         for i, d in enumerate(draws):
-            fill_draw_struct(arr[i], d, d.mesh if isinstance(d.mesh, int) else self.upload_lib_mesh(d.mesh))
+            tex = getattr(d, "base_color_tex", None)
+            fill_draw_struct(arr[i], d, d.mesh if isinstance(d.mesh, int) else self.upload_lib_mesh(d.mesh),
+                             0 if tex is None else self.upload_texture(tex))
         return frame, frame.desc(), arr, len(draws)
 
     def render_pbr_forward_prepared(self, prepared):

@@ -100,6 +100,7 @@ class LibDrawC(ctypes.Structure):
         ("shadow_pcf_radius", ctypes.c_int32),
         ("shadow_pcf_step", ctypes.c_float), ("shadow_strength", ctypes.c_float),
         ("enable_motion_vectors", ctypes.c_int32),
+        ("base_color_tex", ctypes.c_int32),
     ]
 
 
@@ -225,6 +226,8 @@ SIGNATURES = [
     ("shs_present_device", ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(_P)]),
     ("shs_resolve_prequant", ctypes.c_int, [_P, _P]),
     ("shs_resolve_prequant_frame", ctypes.c_int, [_P, ctypes.c_int32, _P]),
+    ("shs_texture_upload", ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    ("shs_texture_release", ctypes.c_int, [_P, ctypes.c_int32]),
     ("shs_device_framebuffers", ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     ("shs_get_stats", ctypes.c_int, [_P, ctypes.POINTER(RasterStats)]),
     ("shs_enable_timing", ctypes.c_int, [_P, ctypes.c_int]),

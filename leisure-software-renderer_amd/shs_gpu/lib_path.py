@@ -17,7 +17,7 @@ from ._abi import (CULL_BACK, CULL_FRONT, CULL_NONE, LIB_BG_GRADIENT, LIB_DEPTH_
                    PROGRAM_DEBUG_DEPTH, PROGRAM_DEBUG_NORMAL, PROGRAM_FORWARD_PLUS, PROGRAM_PBR_MR)
 
 __all__ = [
-    "LibMesh", "LibDraw", "LibFrame", "ShadowCaster", "PROGRAM_PBR_MR", "PROGRAM_BLINN_PHONG", "PROGRAM_DEBUG_ALBEDO",
+    "LibMesh", "LibDraw", "Texture2D", "LibFrame", "ShadowCaster", "PROGRAM_PBR_MR", "PROGRAM_BLINN_PHONG", "PROGRAM_DEBUG_ALBEDO",
     "PROGRAM_DEBUG_NORMAL", "PROGRAM_DEBUG_DEPTH", "CULL_NONE", "CULL_BACK", "CULL_FRONT", "IDENTITY",
     "look_at_lh", "perspective_lh_no", "model_euler", "mat_mul", "dir_light_camera_aabb",
 ]
@@ -36,6 +36,13 @@ class LibMesh:
     @property
     def n_tris(self):
         return int(self.indices.size // 3) if self.indices is not None else int(self.positions.shape[0] // 3)
+
+
+@dataclass(eq=False)
+class Texture2D:
+    """Texture2DData (resources/texture.hpp:23-49): Color texels, rgba uint8 [h, w, 4], texel (x, y) at
+    rgba[y, x].  Uploaded once per context (Context.upload_texture)."""
+    rgba: np.ndarray
 
 
 @dataclass
@@ -65,6 +72,7 @@ class LibDraw:
     shadow_pcf_step: float = 1.0
     shadow_strength: float = 1.0
     enable_motion_vectors: bool = False
+    base_color_tex: Optional[Texture2D] = None     # u.base_color_tex (None: albedo_tex = vec3(1))
 
 
 @dataclass
@@ -178,8 +186,9 @@ class LightCull:
         return tx * ty * (self.z_slices if self.mode == 3 else 1)
 
 
-def fill_draw_struct(a, d: LibDraw, mesh_id: int):
+def fill_draw_struct(a, d: LibDraw, mesh_id: int, tex_id: int = 0):
     a.mesh_id = mesh_id
+    a.base_color_tex = int(tex_id)
     a.program = int(d.program)
     a.cull_mode = int(d.cull_mode)
     a.front_face_ccw = 1 if d.front_face_ccw else 0

@@ -9,8 +9,8 @@ zn 0.1, zf 200 (scene_types.hpp:43-60), the no-material fallback (0.8,0.5,0.2) m
 """
 import numpy as np
 
-from .lib_path import (CULL_BACK, CULL_NONE, PROGRAM_PBR_MR, LibDraw, LibFrame, LibMesh, ShadowCaster, look_at_lh, mat_mul,
-                  model_euler, perspective_lh_no)
+from .lib_path import (CULL_BACK, CULL_NONE, PROGRAM_PBR_MR, LibDraw, LibFrame, LibMesh, ShadowCaster, Texture2D, look_at_lh,
+                       mat_mul, model_euler, perspective_lh_no)
 from .scene import monkey
 
 f32 = np.float32
@@ -79,9 +79,28 @@ def make_plane(width=10.0, depth=10.0, seg_x=10, seg_z=10) -> LibMesh:
                    indices=np.asarray(idx, np.uint32))
 
 
-def c5_scene(width=3840, height=2160, shadow_size=2048, program=PROGRAM_PBR_MR, motion=True, yaw=0.0, floor_seg=16):
+def noise_texture(w, h, seed) -> Texture2D:
+    """A seeded RGBA8 Texture2DData of w x h texels (any size, 1x1 included)."""
+    rng = np.random.default_rng(seed)
+    return Texture2D(rgba=rng.integers(0, 256, size=(h, w, 4), dtype=np.uint8))
+
+
+def monkey_lib_uv() -> LibMesh:
+    """Suzanne with a synthetic UV0 (cylindrical projection of the positions, u wrapping past 1)."""
+    m = monkey_lib()
+    p = m.positions
+    u = (np.arctan2(p[:, 0], p[:, 2]) / np.float32(np.pi) * np.float32(1.5)).astype(np.float32)
+    v = (p[:, 1] * np.float32(0.7) + np.float32(0.5)).astype(np.float32)
+    return LibMesh(positions=p, normals=m.normals, uvs=np.stack([u, v], axis=1).astype(np.float32), indices=m.indices)
+
+
+def c5_scene(width=3840, height=2160, shadow_size=2048, program=PROGRAM_PBR_MR, motion=True, yaw=0.0, floor_seg=16,
+             textured=False, floor_tex=(37, 23), monkey_tex=(1, 1)):
     """-> (frame, draws without shadow wiring, casters, sun_dir, shadow_size).  Call
-    `wire_shadow(draws, light_viewproj)` after the shadow pass."""
+    `wire_shadow(draws, light_viewproj)` after the shadow pass.
+    textured: the materials carry a base_color_tex (pass_pbr_forward.hpp:173-176) -- the floor a
+    floor_tex-sized noise texture with UVs running from -2.25 to 4.25 (repeat wrap, negative UVs), clipped
+    at the frustum; Suzanne a monkey_tex-sized one over a cylindrical UV0."""
     zn, zf = 0.1, 200.0
     ang = np.deg2rad(yaw)
     eye = (f32(16.0 * np.sin(ang)), f32(7.0), f32(-16.0 * np.cos(ang)))
@@ -94,15 +113,23 @@ def c5_scene(width=3840, height=2160, shadow_size=2048, program=PROGRAM_PBR_MR, 
     pm_monkey = model_euler((0.0, 2.2, 0.0), (0.0, -0.05, 0.0), (2.0, 2.0, 2.0))
     m_floor = model_euler((0.0, 0.0, 0.0))
     floor = make_plane(55.0, 140.0, floor_seg, floor_seg)
+    mk = monkey_lib()
+    if textured:
+        floor = LibMesh(positions=floor.positions, normals=floor.normals,
+                        uvs=(floor.uvs * np.float32(6.5) - np.float32(2.25)).astype(np.float32), indices=floor.indices)
+        mk = monkey_lib_uv()
     common = dict(viewproj=vp, prev_viewproj=prev_vp, light_dir_ws=SUN_DIR, light_color=(1.0, 1.0, 1.0),
                   light_intensity=5.0, camera_pos=eye, program=program, enable_motion_vectors=motion)
     draws = [
         LibDraw(mesh=floor, model=m_floor, base_color=(0.6, 0.6, 0.6), metallic=0.0, roughness=0.8, ao=1.0,
                 cull_mode=CULL_NONE, **common),
-        LibDraw(mesh=monkey_lib(), model=m_monkey, prev_model=pm_monkey, base_color=(0.8, 0.5, 0.2), metallic=0.1,
+        LibDraw(mesh=mk, model=m_monkey, prev_model=pm_monkey, base_color=(0.8, 0.5, 0.2), metallic=0.1,
                 roughness=0.5, ao=1.0, cull_mode=CULL_NONE, **common),
     ]
-    casters = [ShadowCaster(floor, m_floor), ShadowCaster(monkey_lib(), m_monkey)]
+    if textured:
+        draws[0].base_color_tex = noise_texture(*floor_tex, seed=0x7E1)
+        draws[1].base_color_tex = noise_texture(*monkey_tex, seed=0x7E2)
+    casters = [ShadowCaster(floor, m_floor), ShadowCaster(mk, m_monkey)]
     frame = LibFrame(width, height, depth_motion=True, zn=zn, zf=zf, bg_gradient=True)
     return frame, draws, casters, SUN_DIR, shadow_size
 

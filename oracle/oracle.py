@@ -152,6 +152,7 @@ class OraLibDraw(ctypes.Structure):
         ("shadow_pcf_radius", ctypes.c_int32),
         ("shadow_pcf_step", ctypes.c_float), ("shadow_strength", ctypes.c_float),
         ("enable_motion_vectors", ctypes.c_int32),
+        ("base_color_tex", ctypes.c_void_p), ("tex_w", ctypes.c_int32), ("tex_h", ctypes.c_int32),
     ]
 
 
@@ -235,6 +236,12 @@ def _lib_draws(draws, keep):
         a.shadow_pcf_radius = int(d.shadow_pcf_radius)
         a.shadow_pcf_step, a.shadow_strength = float(d.shadow_pcf_step), float(d.shadow_strength)
         a.enable_motion_vectors = 1 if d.enable_motion_vectors else 0
+        tex = getattr(d, "base_color_tex", None)
+        if tex is not None:   # lib_path.Texture2D: rgba uint8 [h, w, 4]
+            t = np.ascontiguousarray(tex.rgba, dtype=np.uint8)
+            keep.append(t)
+            a.base_color_tex = t.ctypes.data
+            a.tex_h, a.tex_w = int(t.shape[0]), int(t.shape[1])
     return arr
 
 
@@ -373,6 +380,20 @@ def forward_plus(frame, draws, lights, cull, lists, shadow_map=None):
 
 
 _FWD_CTX = None
+
+
+def sample_texture(rgba, u, v):
+    """sample_texture2d_bilinear_repeat_linear (builtin_shaders.hpp:33-55): rgba uint8 [h, w, 4] -> float32[3]."""
+    L = lib()
+    if not getattr(L, "_tex_ready", False):
+        L.ora_sample_texture.restype = None
+        L.ora_sample_texture.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
+                                         ctypes.c_void_p]
+        L._tex_ready = True
+    t = np.ascontiguousarray(rgba, dtype=np.uint8)
+    out = np.zeros(3, np.float32)
+    L.ora_sample_texture(t.ctypes.data, t.shape[1], t.shape[0], float(u), float(v), out.ctypes.data)
+    return out
 
 
 def tonemap(hdr, exposure=1.0, gamma=2.2):

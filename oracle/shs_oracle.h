@@ -122,6 +122,9 @@ typedef struct ora_lib_draw {
     int32_t shadow_pcf_radius;
     float shadow_pcf_step, shadow_strength;
     int32_t enable_motion_vectors;
+    /* u.base_color_tex (shader/types.hpp:105): Texture2DData texels (Color RGBA8, y * w + x), NULL = none */
+    const uint8_t *base_color_tex;
+    int32_t tex_w, tex_h;
 } ora_lib_draw;
 
 /* RasterizerTarget: hdr (RT_ColorHDR, W*H*4 floats, rows y-up) and optionally depth_motion
@@ -152,6 +155,8 @@ typedef struct ora_shadow_caster {   /* RenderItem with casts_shadow (scene/scen
 void ora_rasterize_mesh(const ora_lib_target *t, const ora_lib_draw *d, uint64_t *stats3);
 /* PassPBRForward::execute (passes/pass_pbr_forward.hpp:49-214): clears + one rasterize_mesh per draw */
 int ora_pbr_forward(const ora_lib_target *t, const ora_lib_draw *draws, int n_draws, uint64_t *stats3);
+/* sample_texture2d_bilinear_repeat_linear (builtin_shaders.hpp:33-55) over rgba (w x h Color texels) */
+void ora_sample_texture(const uint8_t *rgba, int32_t w, int32_t h, float u, float v, float out3[3]);
 /* Threads for rasterize_mesh's row-parallel split of big bboxes (rasterizer.hpp:424-436; default 1). */
 void ora_set_lib_threads(int n);
 /* PassShadowMap::execute (passes/pass_shadow_map.hpp:44-206) into sm[SW*SH]; returns the light viewproj */

@@ -280,10 +280,52 @@ static v3 forward_plus(const ora_lib_target *t, const ora_lib_draw *u, const fra
     return V3(g_clamp(lit[0], 0.0f, 1.0f), g_clamp(lit[1], 0.0f, 1.0f), g_clamp(lit[2], 0.0f, 1.0f));
 }
 
-/* The builtin fragment programs.  Texture sampling: no base_color_tex -> vec3(1) (:35). */
+/* srgb_to_linear_rgb (builtin_shaders.hpp:25-31): std::pow((float)c / 255.0f, 2.2f) per channel */
+static v3 srgb_to_linear_rgb(const uint8_t *c) {
+    return V3(powf((float)c[0] / 255.0f, 2.2f), powf((float)c[1] / 255.0f, 2.2f), powf((float)c[2] / 255.0f, 2.2f));
+}
+
+/* sample_texture2d_bilinear_repeat_linear (builtin_shaders.hpp:33-55): no texture -> vec3(1); repeat
+ * wrap u - floor(u); bilinear between the four srgb_to_linear_rgb texels with glm::mix. */
+static v3 sample_texture2d_bilinear_repeat_linear(const ora_lib_draw *u, v2 uv) {
+    if (!u->base_color_tex || u->tex_w <= 0 || u->tex_h <= 0) return V3(1.0f, 1.0f, 1.0f);
+    const int w = u->tex_w, h = u->tex_h;
+    const float uu = uv.x - floorf(uv.x);
+    const float vv = uv.y - floorf(uv.y);
+    const float fx = uu * (float)(w - 1);
+    const float fy = vv * (float)(h - 1);
+    const int x0 = (int)floorf(fx);
+    const int y0 = (int)floorf(fy);
+    const int x1 = x0 + 1 < w - 1 ? x0 + 1 : w - 1;   /* std::min(x0 + 1, tex->w - 1) */
+    const int y1 = y0 + 1 < h - 1 ? y0 + 1 : h - 1;
+    const float tx = fx - (float)x0;
+    const float ty = fy - (float)y0;
+    const uint8_t *T = u->base_color_tex;
+    const v3 c00 = srgb_to_linear_rgb(T + 4 * ((size_t)y0 * w + x0));
+    const v3 c10 = srgb_to_linear_rgb(T + 4 * ((size_t)y0 * w + x1));
+    const v3 c01 = srgb_to_linear_rgb(T + 4 * ((size_t)y1 * w + x0));
+    const v3 c11 = srgb_to_linear_rgb(T + 4 * ((size_t)y1 * w + x1));
+    const v3 cx0 = v3mix(c00, c10, tx);
+    const v3 cx1 = v3mix(c01, c11, tx);
+    return v3mix(cx0, cx1, ty);
+}
+
+/* The sampler alone (known-answer tests). */
+void ora_sample_texture(const uint8_t *rgba, int32_t w, int32_t h, float u, float v, float out3[3]) {
+    ora_lib_draw d;
+    memset(&d, 0, sizeof d);
+    d.base_color_tex = rgba;
+    d.tex_w = w;
+    d.tex_h = h;
+    const v3 c = sample_texture2d_bilinear_repeat_linear(&d, (v2){u, v});
+    out3[0] = c.x; out3[1] = c.y; out3[2] = c.z;
+}
+
+/* The builtin fragment programs (builtin_shaders.hpp:105-245); albedo_tex = the base_color_tex sample
+ * at fin.uv (:113, :162). */
 static v4 fragment(const ora_lib_target *t, const ora_lib_draw *u, const frag_in *fin) {
     v4 o = {0.0f, 0.0f, 0.0f, 1.0f};
-    const v3 albedo_tex = V3(1.0f, 1.0f, 1.0f);
+    const v3 albedo_tex = sample_texture2d_bilinear_repeat_linear(u, fin->uv);
     const v3 bc = V3(u->base_color[0], u->base_color[1], u->base_color[2]);
     const v3 cam = V3(u->camera_pos[0], u->camera_pos[1], u->camera_pos[2]);
     const v3 ldir = V3(u->light_dir_ws[0], u->light_dir_ws[1], u->light_dir_ws[2]);
