@@ -146,7 +146,7 @@ def test_light_camera_host_matches_oracle(oracle_mod):
 
 def test_lib_struct_layouts():
     from shs_gpu import _abi
-    assert ctypes.sizeof(_abi.LibDrawC) == 4 * 4 + 4 * 64 + 4 * (3 + 3 + 1 + 3 + 3 + 3) + 4 + 64 + 4 * 6
+    assert ctypes.sizeof(_abi.LibDrawC) == 4 * 4 + 4 * 64 + 4 * (3 + 3 + 1 + 3 + 3 + 3) + 4 + 64 + 4 * 6 + 4   # + base_color_tex
     assert ctypes.sizeof(_abi.LibFrameC) == 5 * 4 + 2 * 4 + 16
     assert ctypes.sizeof(_abi.LibStats) == 7 * 8
     assert ctypes.sizeof(_abi.ShadowCasterC) == 4 + 64
