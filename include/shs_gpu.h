@@ -396,8 +396,9 @@ int shs_light_bin_culling(shs_ctx *ctx, const shs_light_bin_desc *desc, const fl
 #define SHS_TARGET_PRESENT 2  /* legacy SDL staging (SHS_FRAME_PRESENT): RGBA8, 4 B/px    */
 #define SHS_TARGET_LIB_PRESENT 3 /* tonemap present staging (SHS_TONEMAP_PRESENT): RGBA8  */
 int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t shard_count, int64_t *words_per_rank);
-/* shs_tiles_pack first finishes the frame (a capacity overflow re-issues it), so the packed tiles are
- * final; it is enqueued on the context stream after that. */
+/* shs_tiles_pack first makes the frame final: it waits for the frame's setup (not its raster) and,
+ * if a capacity overflowed, re-issues it; the pack is then enqueued on the context stream behind it,
+ * so the packed tiles are final without a host wait for the render. */
 int shs_tiles_pack(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, void *dst_dev);
 int shs_tiles_unpack(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, const void *src_dev);
 
@@ -545,6 +546,43 @@ typedef struct shs_canvas_dof_desc {
  * (may be NULL, host) the autofocus depth. */
 int shs_canvas_dof(shs_ctx *ctx, const shs_canvas_dof_desc *desc, uint8_t *color, const float *depth, uint8_t *blur_out,
                    float *focus_depth, uint32_t flags);
+
+/* ---- multi-GPU from one host process (SURVEY.md 5 "Distributed communication backend", 8e) ---------
+ * The reference host is one C++ process driving one render loop (hello_pipeline_blinn_phong_shading.cpp
+ * :369-455; PluggablePipeline::execute, pipeline/pluggable_pipeline.hpp:980).  A group is n contexts
+ * in this process, context r on devices[r] (a device may repeat), each rendering the 32x32 tiles with
+ * tile % n == r of every frame.  Per-rank work (uploads, passes) runs on one host worker thread per
+ * rank, so the enqueue cost does not serialise over the GPUs.  shs_group_gather composes a frame on
+ * rank 0's context: every rank packs its tiles on its own stream, copies them to rank 0's device
+ * (hipMemcpyPeerAsync: xGMI between MI355X peers) and rank 0 unpacks them -- all stream-ordered, no
+ * host wait, receive buffers double-buffered so the next frame's render overlaps this one's transfer.
+ * Rank 0's context then resolves the full frame with the single-context calls (shs_resolve_lib,
+ * shs_resolve_ldr, shs_resolve, shs_resolve_present).  Geometry, textures and lights are uploaded to
+ * every rank (the ids agree across ranks when every rank uploads the same sequence). */
+typedef struct shs_group shs_group;
+int shs_group_create(const int32_t *devices, int32_t n, shs_group **out);
+int shs_group_destroy(shs_group *g);
+const char *shs_group_last_error(shs_group *g);
+int shs_group_size(shs_group *g);
+/* The rank's context (for the single-context calls; do not destroy it). */
+int shs_group_context(shs_group *g, int32_t rank, shs_ctx **ctx);
+/* Replicated uploads: the same call on every rank; *id is the (common) id. */
+int shs_group_mesh_upload(shs_group *g, const float *positions, int32_t n_verts, const float *normals, int32_t n_normals,
+                          const float *uvs, int32_t n_uvs, const uint32_t *indices, int64_t n_indices, int32_t *mesh_id);
+int shs_group_mesh_upload_soup(shs_group *g, const float *positions, const float *normals, int32_t n_tris, int32_t *mesh_id);
+int shs_group_texture_upload(shs_group *g, const uint8_t *rgba, int32_t w, int32_t h, int32_t *tex_id);
+int shs_group_lights_upload(shs_group *g, const shs_culling_light *lights, int32_t n_lights);
+int shs_group_lib_fuse_tonemap(shs_group *g, const shs_tonemap_desc *desc);
+/* Sharded passes: rank r runs the call with shard_rank = r, shard_count = n (the frame's own shard
+ * fields are ignored).  The shadow map is rendered whole on every rank (every rank's PCF reads all of it). */
+int shs_group_light_cull(shs_group *g, const shs_light_cull_desc *desc);
+int shs_group_render_shadow_map(shs_group *g, int32_t w, int32_t h, const float sun_dir[3], const shs_shadow_caster *casters,
+                                int32_t n_casters, float light_viewproj_out[16]);
+int shs_group_render_pbr_forward(shs_group *g, const shs_lib_frame *frame, const shs_lib_draw *draws, int32_t n_draws);
+int shs_group_render_legacy(shs_group *g, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws);
+/* Compose the last frame's target (SHS_TARGET_*) on rank 0's context, asynchronously. */
+int shs_group_gather(shs_group *g, int target);
+int shs_group_synchronize(shs_group *g);
 
 /* Host-only (no device): the byte thresholds for gamma (thr[0] = 0; +inf where a byte is never
  * reached).  Exposed for the parity tests. */

@@ -468,6 +468,17 @@ static int finish_frame(shs_ctx *ctx) {
     return SHS_OK;
 }
 
+}  // extern "C"
+
+int shs_legacy_ensure_final(shs_ctx *ctx) {
+    if (!ctx->have_frame || !ctx->need_check) return SHS_OK;
+    const shs_ctx::LegacySlot &p = ctx->lslot[ctx->last_slot];
+    HIP_TRY(ctx, hipEventSynchronize(p.setup_done));
+    return *p.h_ov ? finish_frame(ctx) : SHS_OK;
+}
+
+extern "C" {
+
 int shs_render_legacy_batch(shs_ctx *ctx, const shs_frame_desc *frame, const shs_legacy_draw *draws, int32_t n_draws,
                             int32_t n_frames) {
     if (!ctx || !frame || n_draws < 0 || (n_draws > 0 && !draws) || n_frames < 1 || n_frames > SHS_MAX_BATCH_FRAMES)
@@ -501,13 +512,9 @@ int shs_render_legacy_batch(shs_ctx *ctx, const shs_frame_desc *frame, const shs
     // consumer of its frames (a copy queued behind it) must not see a batch that overflowed a
     // capacity.  Its overflow word is final once its setup is (long before its raster ends); if it is
     // set, the batch is finished -- re-issued with grown capacities -- before this one is enqueued.
-    if (ctx->have_frame && ctx->need_check) {
-        const shs_ctx::LegacySlot &p = ctx->lslot[ctx->last_slot];
-        HIP_TRY(ctx, hipEventSynchronize(p.setup_done));
-        if (*p.h_ov) {
-            const int rc = finish_frame(ctx);
-            if (rc) return rc;
-        }
+    {
+        const int rc = shs_legacy_ensure_final(ctx);
+        if (rc) return rc;
     }
     ctx->frame = f;
     ctx->last_draws.assign(draws, draws + n_all);

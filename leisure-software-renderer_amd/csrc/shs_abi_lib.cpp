@@ -517,6 +517,11 @@ int check_lib_mesh(shs_ctx *ctx, int32_t id) {
 
 }  // namespace
 
+int shs_lib_ensure_final(shs_ctx *ctx) {
+    const int rc = check_superseded(ctx, ctx->lib_shadow);
+    return rc ? rc : check_superseded(ctx, ctx->lib_cam);
+}
+
 void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_cam);
     release_work(ctx->lib_shadow);
@@ -981,10 +986,11 @@ int shs_tiles_pack(shs_ctx *ctx, int target, int32_t rank, int32_t count, void *
     shs_dev::TileCopyParams p;
     if (tile_params(ctx, target, rank, count, p)) return SHS_ERR_INVALID;
     if (set_dev(ctx)) return SHS_ERR_HIP;
-    // A frame whose capacity overflowed is re-issued when it is finished: finish it before its tiles
-    // leave the rank (legacy: shs_synchronize; library: the pass chain, tonemap included).
-    const int rc = (target == SHS_TARGET_LEGACY || target == SHS_TARGET_PRESENT) ? shs_synchronize(ctx)
-                                                                                : shs_resolve_lib(ctx, nullptr, nullptr, nullptr);
+    // A frame whose capacity overflowed is re-issued before its tiles leave the rank (legacy: the batch;
+    // library: the pass chain, tonemap included).  Only its setup is waited for: the overflow word is
+    // final then, and the pack below is stream-ordered after the (possibly re-issued) frame.
+    const int rc = (target == SHS_TARGET_LEGACY || target == SHS_TARGET_PRESENT) ? shs_legacy_ensure_final(ctx)
+                                                                                : shs_lib_ensure_final(ctx);
     if (rc) return rc;
     HIP_TRY(ctx, shs_internal::launch_tiles_copy(p, true, dst_dev, ctx->stream));
     return SHS_OK;

@@ -240,6 +240,11 @@ struct shs_ctx {
 
 // Re-enqueues the tonemap after lib_finish re-issued the camera pass (shs_abi_post.cpp).
 int shs_tonemap_reissue(shs_ctx *ctx);
+// Make the pending frame final in stream order without waiting for its raster: wait for its setup
+// (the overflow word is final then) and re-issue it only if a capacity overflowed.  Work queued on
+// the context stream afterwards sees the final frame (shs_abi.cpp: legacy; shs_abi_lib.cpp: library).
+int shs_legacy_ensure_final(shs_ctx *ctx);
+int shs_lib_ensure_final(shs_ctx *ctx);
 
 #define HIP_TRY(ctx, expr)                                                                       \
     do {                                                                                         \

@@ -281,6 +281,25 @@ SIGNATURES = [
     ("shs_perspective_lh_no", ctypes.c_int, [ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _F]),
     ("shs_model_euler", ctypes.c_int, [_F, _F, _F, _F]),
     ("shs_dir_light_camera_aabb", ctypes.c_int, [_F, _F, _F, ctypes.c_float, ctypes.c_uint32, _F, _F, _F]),
+    # multi-GPU from one host process
+    ("shs_group_create", ctypes.c_int, [ctypes.POINTER(ctypes.c_int32), ctypes.c_int32, ctypes.POINTER(_P)]),
+    ("shs_group_destroy", ctypes.c_int, [_P]),
+    ("shs_group_last_error", ctypes.c_char_p, [_P]),
+    ("shs_group_size", ctypes.c_int, [_P]),
+    ("shs_group_context", ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(_P)]),
+    ("shs_group_mesh_upload", ctypes.c_int, [_P, _F, ctypes.c_int32, _F, ctypes.c_int32, _F, ctypes.c_int32,
+                                             ctypes.POINTER(ctypes.c_uint32), ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)]),
+    ("shs_group_mesh_upload_soup", ctypes.c_int, [_P, _F, _F, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    ("shs_group_texture_upload", ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    ("shs_group_lights_upload", ctypes.c_int, [_P, ctypes.POINTER(CullingLightC), ctypes.c_int32]),
+    ("shs_group_lib_fuse_tonemap", ctypes.c_int, [_P, ctypes.POINTER(TonemapDescC)]),
+    ("shs_group_light_cull", ctypes.c_int, [_P, ctypes.POINTER(LightCullDescC)]),
+    ("shs_group_render_shadow_map", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _F, ctypes.POINTER(ShadowCasterC),
+                                                   ctypes.c_int32, _F]),
+    ("shs_group_render_pbr_forward", ctypes.c_int, [_P, ctypes.POINTER(LibFrameC), ctypes.POINTER(LibDrawC), ctypes.c_int32]),
+    ("shs_group_render_legacy", ctypes.c_int, [_P, ctypes.POINTER(FrameDesc), ctypes.POINTER(LegacyDraw), ctypes.c_int32]),
+    ("shs_group_gather", ctypes.c_int, [_P, ctypes.c_int]),
+    ("shs_group_synchronize", ctypes.c_int, [_P]),
 ]
 
 

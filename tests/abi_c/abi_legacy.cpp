@@ -195,7 +195,8 @@ int main(int argc, char **argv) {
         }
     }
 
-    // A batch of the four poses at 1920x1080: every frame equals the oracle's.
+    // A batch of the four poses at 1920x1080: every frame equals the oracle's (colour with the frame's
+    // own pre-truncation floats, shs_resolve_prequant_frame).
     {
         const int W = 1920, H = 1080, F = 4;
         std::vector<shs_legacy_draw> draws(F);
@@ -205,29 +206,18 @@ int main(int argc, char **argv) {
         f.width = W; f.height = H;
         f.ref_tile_w = 80; f.ref_tile_h = 80;
         f.shard_rank = 0; f.shard_count = 1;
+        f.flags = SHS_FRAME_PREQUANT;
         f.clear_color[3] = 255;
         SHS_CHECK(ctx, shs_render_legacy_batch(ctx, &f, draws.data(), 1, F));
         for (int k = 0; k < F; ++k) {
             std::vector<uint8_t> gc((size_t)W * H * 4), rc((size_t)W * H * 4);
-            std::vector<float> gd((size_t)W * H), rd((size_t)W * H), rpq((size_t)W * H * 4);
+            std::vector<float> gd((size_t)W * H), rd((size_t)W * H), gpq((size_t)W * H * 4), rpq((size_t)W * H * 4);
             SHS_CHECK(ctx, shs_resolve_frame(ctx, k, gc.data(), gd.data()));
+            SHS_CHECK(ctx, shs_resolve_prequant_frame(ctx, k, gpq.data()));
             EXPECT(ora_render_legacy(W, H, 80, 80, 8, &odraws[k], 1, rc.data(), rd.data(), rpq.data()) == 0, "oracle failed");
-            // no prequant for batches: a byte may still differ by one at a truncation boundary; bound it
-            size_t bad_depth = 0, off1 = 0, worse = 0;
-            for (size_t i = 0; i < (size_t)W * H; ++i) {
-                uint32_t a, b;
-                std::memcpy(&a, &gd[i], 4);
-                std::memcpy(&b, &rd[i], 4);
-                bad_depth += a != b;
-            }
-            for (size_t i = 0; i < gc.size(); ++i) {
-                const int dd = std::abs((int)gc[i] - (int)rc[i]);
-                off1 += dd == 1;
-                worse += dd > 1;
-            }
-            std::printf("batch frame %d/%d                      %dx%d depth_mismatch=%zu colour_off_by_1=%zu worse=%zu\n", k, F, W,
-                        H, bad_depth, off1, worse);
-            EXPECT(bad_depth == 0 && worse == 0 && off1 <= 16, "batch frame %d differs from the oracle", k);
+            char what[64];
+            std::snprintf(what, sizeof what, "batch frame %d/%d", k, F);
+            compare(what, W, H, gc, gd, &gpq, rc, rd, rpq);
         }
         EXPECT(shs_resolve_frame(ctx, F, nullptr, nullptr) == SHS_ERR_INVALID, "frame index past the batch accepted");
     }

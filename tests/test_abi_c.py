@@ -35,3 +35,19 @@ def test_abi_c_host_renders_oracle_exact():
     print(r.stdout)
     assert r.returncode == 0, r.stdout
     assert "abi_legacy: all passed" in r.stdout
+
+
+GROUP_EXE = os.path.join(ABI_C, "_build", "abi_group")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [8, 3])
+def test_abi_c_group_composes_sharded_frames(n):
+    """A single-process C++ host drives N contexts through shs_group_* (VERDICT r2 item 6): the
+    gathered legacy, library and fused-tonemap frames equal the unsharded context's bit for bit.  On
+    the 1-GPU box the N contexts share device 0 (the peer copies become device-local)."""
+    assert os.path.exists(GROUP_EXE), "build tests/abi_c first (__graft_entry__.build())"
+    r = subprocess.run([GROUP_EXE, ROOT, str(n)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+    assert "abi_group: all passed" in r.stdout
