@@ -48,12 +48,17 @@ def test_c2_bench_batch_every_frame_vs_oracle(oracle_mod, pose_set):
 
 
 def _owned_light_lists(cull, rank, count):
-    """Light tiles (cull.tile_size px) whose 32x32 GPU tile belongs to rank (tile % count == rank)."""
+    """Light tiles (cull.tile_size px, rows down) covering a pixel of one of rank's 32x32 GPU tiles (rows
+    up, tile % count == rank): a light tile straddling two bin rows belongs to both owners."""
     tx, ty = cull.tiles
-    ts = cull.tile_size
+    ts, H = cull.tile_size, cull.height
     ly, lx = np.mgrid[0:ty, 0:tx]
-    g = (ly * ts // 32) * ((cull.width + 31) // 32) + (lx * ts // 32)
-    return ((g % count) == rank).reshape(-1)
+    top = H - 1 - ly * ts
+    bot = np.maximum(top - ts + 1, 0)
+    bw = (cull.width + 31) // 32
+    own = ((top // 32) * bw + lx * ts // 32) % count == rank
+    own |= ((bot // 32) * bw + lx * ts // 32) % count == rank
+    return own.reshape(-1)
 
 
 @pytest.mark.parametrize("cfg", ["c4", "c5"])
