@@ -188,6 +188,10 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * superseded); results are identical. */
 #define SHS_OPT_SPILL_CAPACITY 5
 #define SHS_OPT_FRAG_CAPACITY 6
+/* SHS_OPT_LIB_PART: library camera passes split a busy raster tile whose bin list holds more than
+ * `value` entries into parts rendered by several workgroups at once (merged by 64-bit atomicMin; the
+ * results are identical).  -1 (default): 512 for tile-sharded passes, off otherwise; 0: off. */
+#define SHS_OPT_LIB_PART 7
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 
 /* Debug / profiling hook: the last frame's workgroup timeline.  out[0..7] = {k_setup grid, k_raster

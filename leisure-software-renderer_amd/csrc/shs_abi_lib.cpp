@@ -56,7 +56,7 @@ void release_work(Work &w) {
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
     if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
@@ -325,6 +325,15 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         fp.exp_flags = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
     }
     fp.n_owned_rt = (int)w.h_rt_order.size();
+    // Camera pass, tile-sharded: k_lib_plan splits the busy tiles whose bin list is longer than `part`
+    // entries into parts rendered by several workgroups (SHS_OPT_LIB_PART: -1 auto = 512 when sharded,
+    // 0 = off, else the part size for every camera pass).
+    fp.part = 0u;
+    if (!shadow && !fp.scan_mode) {
+        if (ctx->lib_part > 0) fp.part = (uint32_t)ctx->lib_part;
+        else if (ctx->lib_part < 0 && fp.count > 1) fp.part = 512u;
+    }
+    if (fp.part && ensure(ctx, w.items, (size_t)std::max(fp.n_owned_rt, 1) * shs_dev::LIB_MAXK)) return SHS_ERR_HIP;
     // the shallow raster (256-candidate rounds, twice the workgroups per CU) when the previous frame's
     // fullest bin tile fit one such round (scan mode: every primitive is a candidate)
     const uint64_t fullest = fp.scan_mode ? (uint64_t)n_tris + (shadow ? 0u : w.st_extra) : w.st_maxbin;
@@ -343,6 +352,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.dbase = reinterpret_cast<int32_t *>(w.draws.p + nd);
     fb.bdraw = fb.dbase + nd + 1;
     fb.rqueue = w.rqueue.p;
+    fb.items = fp.part ? w.items.p : nullptr;
     fb.rt_order = w.rt_order.p;
     if (shadow) {
         fb.depth = ctx->shadow_map.p;
@@ -469,6 +479,7 @@ int check_pass(shs_ctx *ctx, Work &w, bool &grew) {
     w.st_clip = w.st_raster = w.st_covered = w.st_maxbin = 0;
     for (const uint2 &b : bs) { w.st_clip += b.x; w.st_raster += b.y; }
     for (const uint2 &r : rs) { w.st_covered += r.x; w.st_maxbin = std::max<uint64_t>(w.st_maxbin, r.y); }
+    if (&w == &ctx->lib_cam) w.st_covered = c[shs_dev::LC_COVERED];   // counted by k_lib_resolve
     w.st_spill = c[shs_dev::LC_SPILL];
     w.st_extra = c[shs_dev::LC_EXTRA];
     if (w.st_maxbin > w.bin_cap) w.bin_cap = next_pow2(std::min<uint64_t>(w.st_maxbin, 1u << 24));

@@ -1416,9 +1416,13 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
     }
 }
 
+// One work item: raster tile rt, or (k_lib_plan) part `part` of `parts` of its candidate list.  A split
+// tile's parts run on any workgroups at once; each resolves its own candidates in LDS and merges its
+// winners into the global keys with a 64-bit atomicMin (k_lib_plan set them to KEY_EMPTY), so the
+// minimum over the parts is the tile's exact (z, submission) winner whatever the order.
 template <bool SHADOW, int LIB_CAND>
 __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared<LIB_CAND> &sh,
-                                uint32_t &chunk) {
+                                uint32_t &chunk, uint32_t part = 0u, uint32_t parts = 1u) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool hiz = SHADOW || (fp.flags & LF_DEPTH);   // painter's order (no depth target): never
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
@@ -1442,8 +1446,10 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
     }
     const uint32_t *bin = fb.bins + (size_t)bt * fp.bin_cap;
+    const uint32_t i_end = parts > 1u ? (uint32_t)(((uint64_t)n_items * (part + 1u)) / parts) : n_items;
+    const uint32_t i_beg = parts > 1u ? (uint32_t)(((uint64_t)n_items * part) / parts) : 0u;
 
-    for (uint32_t base = 0; base < n_items; base += LIB_CAND) {
+    for (uint32_t base = i_beg; base < i_end; base += LIB_CAND) {
         __syncthreads();
         if (tid == 0) { sh.nc = 0; sh.zlo = 0xffffffffu; sh.zhi = 0u; }
         sh.hist[tid] = 0u;
@@ -1459,7 +1465,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         for (int k = 0; k < NG; ++k) {
             const uint32_t item = base + tid + 256u * k;
             uint32_t id = 0xffffffffu;
-            if (item < n_items) {
+            if (item < i_end) {
                 if (fp.scan_mode) {
                     id = item;
                 } else if (item < n_bin) {
@@ -1712,8 +1718,13 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         // (the wave's block is sub-block `wave` of the tile, k_lib_resolve's numbering)
         covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
         const bool any = __ballot(covered) != 0ull;
-        if (any && px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = key;
-        if (lane == 0) fb.blkcov[(size_t)rt * 4 + wave] = any ? 1u : 0u;
+        if (parts > 1u) {   // a part: merge into the keys k_lib_plan reset; flag blocks it holds winners of
+            if (covered) atomicMin(&fb.keys[(size_t)py * fp.W + px], key);
+            if (lane == 0 && any) fb.blkcov[(size_t)rt * 4 + wave] = 1u;
+        } else {
+            if (any && px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = key;
+            if (lane == 0) fb.blkcov[(size_t)rt * 4 + wave] = any ? 1u : 0u;
+        }
     }
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
@@ -1742,6 +1753,65 @@ __device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const L
     }
 }
 
+// The camera pass's raster work plan, after the marks are final (one 1024-thread workgroup): every
+// owned raster tile is one work item, except busy tiles whose bin list holds more than fp.part entries,
+// which become ceil(n / part) parts (at most LIB_MAXK) that any workgroups render at once -- the
+// hottest tiles no longer bound the raster (C4 at 8 shards: ~2 busy tiles per workgroup, 20-75 us
+// each).  The parts come first (the long items start early), each split tile's keys and block flags
+// are reset here for the parts' atomicMin merge.
+__device__ __forceinline__ uint32_t plan_parts(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int j, int &rt) {
+    rt = fb.rt_order[j];
+    if (!fb.busy[rt]) return 1u;
+    const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
+    const uint32_t total = fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + (row / (TILE / LIB_RTH)) * fp.tiles_x + col];
+    const uint32_t n = min(total, fp.bin_cap) + (total > fp.bin_cap ? min(cnt[LC_SPILL], fp.spill_cap) : 0u);
+    return n > fp.part ? min((uint32_t)LIB_MAXK, (n + fp.part - 1u) / fp.part) : 1u;
+}
+
+__global__ __launch_bounds__(1024) void k_lib_plan(LibFrameParams fp, LibBuffers fb) {
+    __shared__ uint32_t s_w[2][16];
+    uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = fp.n_owned_rt, per = (n + 1023) / 1024;
+    const int j0 = min(n, tid * per), j1 = min(n, j0 + per);
+    uint32_t ks = 0u, kn = 0u;   // this thread's split parts / unsplit items
+    for (int j = j0; j < j1; ++j) {
+        int rt;
+        const uint32_t k = plan_parts(fp, fb, cnt, j, rt);
+        if (k > 1u) ks += k; else kn += 1u;
+    }
+    // exclusive block scans of ks and kn
+    uint32_t is = ks, in = kn;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t a = (uint32_t)__shfl_up((int)is, o), b = (uint32_t)__shfl_up((int)in, o);
+        if (lane >= o) { is += a; in += b; }
+    }
+    if (lane == 63) { s_w[0][wave] = is; s_w[1][wave] = in; }
+    __syncthreads();
+    uint32_t bs = 0u, bn = 0u, ts = 0u, tn = 0u;
+    for (int w = 0; w < 16; ++w) {
+        if (w < wave) { bs += s_w[0][w]; bn += s_w[1][w]; }
+        ts += s_w[0][w]; tn += s_w[1][w];
+    }
+    uint32_t ps = bs + is - ks, pn = ts + bn + in - kn;   // split parts first, then the rest
+    for (int j = j0; j < j1; ++j) {
+        int rt;
+        const uint32_t k = plan_parts(fp, fb, cnt, j, rt);
+        if (k > 1u) {
+            for (uint32_t p = 0; p < k; ++p) fb.items[ps++] = make_uint2((uint32_t)j, p | (k << 16));
+            const int X0 = (rt % fp.tiles_x) * LIB_RTW, Y0 = (rt / fp.tiles_x) * LIB_RTH;
+            for (int y = Y0; y < min(Y0 + LIB_RTH, fp.H); ++y)
+                for (int x = X0; x < min(X0 + LIB_RTW, fp.W); ++x) fb.keys[(size_t)y * fp.W + x] = KEY_EMPTY;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) fb.blkcov[(size_t)rt * 4 + s] = 0u;
+        } else {
+            fb.items[pn++] = make_uint2((uint32_t)j, 1u << 16);
+        }
+    }
+    if (tid == 0) cnt[LC_ITEMS] = ts + tn;
+}
+
 template <bool SHADOW, int LIB_CAND>
 __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
     __shared__ LibShared<LIB_CAND> sh;
@@ -1759,19 +1829,30 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
     // tiles, so the dense tiles that end up late in some workgroup's static list are balanced by the
     // dynamic half; one tile per ticket keeps a dense bin tile's 4 rows on different workgroups.
     uint32_t *rq = fb.rqueue + (size_t)fp.parity * LIB_NQ * LIB_QSTRIDE;
-    const int S = max(1, fp.n_owned_rt / (2 * G));
+    // work items: the owned raster tiles, or k_lib_plan's list (split tiles' parts first)
+    const int n_work = (!SHADOW && fp.part) ? (int)cnt[LC_ITEMS] : fp.n_owned_rt;
+    const int S = max(1, n_work / (2 * G));
     const int dyn0 = S * G;
     int j = (int)blockIdx.x;
     int i_static = 0, q = (int)(blockIdx.x & (LIB_NQ - 1)), tried = 0;
-    while (j < fp.n_owned_rt) {   // block-uniform
+    while (j < n_work) {   // block-uniform
         const bool dynamic_next = i_static + 1 >= S;
         uint32_t tk = 0;
         if (tid == 0 && dynamic_next) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
         // owned raster tile j (the host's XCD-coherent order, rows inside the frame only)
         {
-            const int rt = fb.rt_order[j];
-            if (fb.busy[rt]) {
-                lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk);
+            int rt;
+            uint32_t part = 0u, parts = 1u;
+            if (!SHADOW && fp.part) {
+                const uint2 it = fb.items[j];
+                rt = fb.rt_order[it.x];
+                part = it.y & 0xffffu;
+                parts = it.y >> 16;
+            } else {
+                rt = fb.rt_order[j];
+            }
+            if (parts > 1u || fb.busy[rt]) {
+                lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk, part, parts);
             } else {
                 const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
                 lib_clear_tile<SHADOW>(fp, fb, rt);
@@ -1786,11 +1867,11 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
         i_static = S;
         if (tid == 0) {
             int nj = dyn0 + q + LIB_NQ * (int)tk;
-            while (nj >= fp.n_owned_rt && ++tried < LIB_NQ) {
+            while (nj >= n_work && ++tried < LIB_NQ) {
                 q = (q + 1) & (LIB_NQ - 1);
                 nj = dyn0 + q + LIB_NQ * (int)atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
             }
-            sh.next[0] = nj < fp.n_owned_rt ? nj : fp.n_owned_rt;
+            sh.next[0] = nj < n_work ? nj : n_work;
             sh.next[1] = q;
             sh.next[2] = tried;
         }
@@ -1828,7 +1909,9 @@ __global__ __launch_bounds__(256, PROG == 5 ? SHS_RESOLVE_WAVES_FP : PROG == 0 ?
 void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
     __shared__ float tm_thr[256];
     __shared__ uint32_t wlist[PROG == 0 ? 1 : 4][128];   // per wave: its block's light list (LtWave)
+    __shared__ uint32_t s_cov;                            // covered pixels of this workgroup's blocks
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_cov = 0u;
     if (fb.tm_thr) tm_thr[tid] = fb.tm_thr[tid];
     if (PROG != 0 && fb.lights && fp.n_lights <= LIB_LDS_LIGHTS) {   // Forward+ lights
         for (int i = tid; i < (int)fp.n_lights; i += 256) {
@@ -1874,6 +1957,8 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
         }
         bool covered;
         const float4 c = lib_resolve<false, PROG>(fp, fb, key, px, py, covered, lw);
+        const uint64_t cm = __ballot(covered);
+        if (lane == 0 && cm) atomicAdd(&s_cov, (uint32_t)__popcll(cm));
         if (fb.tm_thr && inb) {   // fused PassTonemap of this pixel's HDR value
             const uint32_t rgba = tonemap_byte(c.x, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) |
                                   (tonemap_byte(c.y, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) << 8) |
@@ -1882,6 +1967,8 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
             if (fb.tm_present) __builtin_nontemporal_store(rgba, &fb.tm_present[(size_t)(fp.H - 1 - py) * fp.W + px]);
         }
     }
+    __syncthreads();
+    if (tid == 0 && s_cov) atomicAdd(&fb.counters[fp.parity * LC_N + LC_COVERED], s_cov);
 }
 
 }  // namespace shs_dev
@@ -1938,6 +2025,7 @@ hipError_t launch_lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, in
 }
 
 hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, bool shallow, int grid, hipStream_t s) {
+    if (!shadow && fp.part) hipLaunchKernelGGL(k_lib_plan, dim3(1), dim3(1024), 0, s, fp, fb);
     hipLaunchKernelGGL(SHS_RASTER_KERNEL(shadow, shallow), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }

@@ -89,7 +89,9 @@ constexpr uint32_t LF_GRADIENT = 8u;    // PassPBRForward's no-sky background gr
 // (primitive, tile) task total and length, one 64-bit word (tasks low, entries high) so that one
 // atomicAdd hands an appender both bases and the queue's task prefix stays monotone; LC_N even keeps
 // the second parity set's word 8-B aligned.
-constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT = 4, LC_BIGQ = 5, LC_N = 6;
+// LC_ITEMS: k_lib_plan's raster work items; LC_COVERED: camera-pass covered pixels (k_lib_resolve).
+constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT = 4, LC_BIGQ = 5, LC_ITEMS = 6, LC_COVERED = 7,
+              LC_N = 8;
 static_assert(LC_BIGQ == LC_BIGT + 1 && LC_BIGT % 2 == 0 && LC_N % 2 == 0, "64-bit big-queue word");
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
@@ -111,6 +113,8 @@ struct LibFrameParams {
     float lt_view_z[4];              // view matrix row 2 (view-space z, cluster slice)
     float lt_zn, lt_zf;              // the light cull's depth_params
     float tm_exposure, tm_inv_gamma; // fused PassTonemap (LibBuffers::tm_thr)
+    uint32_t part;                   // camera pass: k_lib_plan splits a tile's list into parts of this many
+                                     // entries (0: one work item per owned raster tile, no plan)
 };
 
 struct LibBuffers {
@@ -149,7 +153,11 @@ struct LibBuffers {
     uint32_t *ov_host;               // the pass's overflow word in mapped host memory (raise_overflow)
     float4 *uvw;                     // per slot, 2 float4: UV0 varying * 1/w of the 3 corners (textured draws)
     const float *srgb_lut;           // srgb_to_linear_rgb's 256 values, std::pow(c / 255.0f, 2.2f) on the host
+    uint2 *items;                    // k_lib_plan: raster work items (rt_order position, part | parts << 16)
 };
+
+// k_lib_plan: at most this many parts per raster tile (capacity: LIB_MAXK * owned raster tiles).
+constexpr int LIB_MAXK = 16;
 
 // k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket
 // counters a cache line apart (k_lib_setup zeroes the next frame's set).

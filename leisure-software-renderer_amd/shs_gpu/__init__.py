@@ -521,6 +521,10 @@ class Context:
     def set_bin_capacity(self, cap: int):
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_BIN_CAPACITY, int(cap)))
 
+    def set_lib_part(self, part: int):
+        """Camera-pass raster work split (SHS_OPT_LIB_PART): -1 auto, 0 off, else the part size."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_LIB_PART, int(part)))
+
     def set_overflow_capacities(self, spill: int = 0, frags: int = 0):
         """Tests: shrink the legacy bin-spill / ghost-fragment lists (0 = leave) to force overflows."""
         if spill:

@@ -30,6 +30,7 @@ OPT_TIMELINE = 3
 OPT_RASTER_LOOP = 4
 OPT_SPILL_CAPACITY = 5
 OPT_FRAG_CAPACITY = 6
+OPT_LIB_PART = 7
 
 
 class LegacyDraw(ctypes.Structure):

@@ -225,3 +225,29 @@ def test_shallow_raster_after_first_frame(oracle_mod):
             assert_depth_bitexact(gd, rd)
             assert_float_close(gm, rm, what="motion")
             assert_float_close(gh, rh, what="hdr")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("part", [16, 64, 512])
+def test_split_raster_items_exact(oracle_mod, part):
+    """SHS_OPT_LIB_PART: busy tiles with more bin entries than `part` are rendered as several parts on
+    different workgroups, merged by atomicMin -- the C4-like Forward+ frame (deep bins) and the C5
+    frame must stay bit-identical to the oracle (depth) / within 1e-5 (HDR), sharded and not."""
+    import shs_gpu
+    from shs_gpu import scene_lib
+    from helpers import assert_depth_bitexact, assert_float_close
+    frame, draws, lights, cull = scene_lib.c4_scene(640, 360, n_objects=80, tris_per_object=600)
+    rc, ri = oracle_mod.light_cull(cull, lights)[:2]
+    rh, rd, rm, _ = oracle_mod.forward_plus(frame, draws, lights, cull, (rc, ri))
+    ctx = shs_gpu.Context(0)
+    try:
+        ctx.set_lib_part(part)
+        ctx.upload_lights(lights)
+        ctx.light_cull(cull)
+        ctx.render_pbr_forward(frame, draws)
+        gh, gd, gm = ctx.resolve_lib()
+        assert_depth_bitexact(gd, rd)
+        assert_float_close(gh, rh, what="split hdr")
+        assert ctx.lib_stats()["covered_pixels"] == int((rd < 1.0).sum())
+    finally:
+        ctx.close()
