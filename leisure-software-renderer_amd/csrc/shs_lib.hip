@@ -1416,18 +1416,22 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
     }
 }
 
-// One work item: raster tile rt, or (k_lib_plan) part `part` of `parts` of its candidate list.  A split
-// tile's parts run on any workgroups at once; each resolves its own candidates in LDS and merges its
-// winners into the global keys with a 64-bit atomicMin (k_lib_plan set them to KEY_EMPTY), so the
-// minimum over the parts is the tile's exact (z, submission) winner whatever the order.
+// One work item: raster tile rt, or (k_lib_plan) part `part` of `parts` (2: the 32x4 halves, 4: the
+// 16x4 blocks) of it.  A part gathers the tile's list but tests only the pixels of its rectangle and
+// writes only its blocks' keys and flags, so the parts of a hot tile render on several workgroups at
+// once with no merge.  T0 = the tile origin (LDS key layout); X0..Y1 = the item's rectangle.
 template <bool SHADOW, int LIB_CAND>
 __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared<LIB_CAND> &sh,
                                 uint32_t &chunk, uint32_t part = 0u, uint32_t parts = 1u) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool hiz = SHADOW || (fp.flags & LF_DEPTH);   // painter's order (no depth target): never
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
-    const int X0 = col * LIB_RTW, Y0 = row * LIB_RTH;
-    const int X1 = X0 + LIB_RTW - 1, Y1 = Y0 + LIB_RTH - 1;
+    const int TX0 = col * LIB_RTW, TY0 = row * LIB_RTH;
+    const int X0 = TX0 + (parts == 4u ? 16 * (int)(part & 1u) : 0), Y0 = TY0 + (parts == 1u ? 0 : 4 * (int)(part >> (parts == 4u ? 1 : 0)));
+    const int X1 = X0 + (parts == 4u ? 15 : LIB_RTW - 1), Y1 = Y0 + (parts == 1u ? LIB_RTH - 1 : 3);
+    // this thread's pixel (tile layout: wave w = 16x4 block w) and whether the item covers it
+    const int my_lx = 16 * (wave & 1) + (lane & 15), my_ly = 4 * (wave >> 1) + (lane >> 4);
+    const bool mine = TX0 + my_lx >= X0 && TX0 + my_lx <= X1 && TY0 + my_ly >= Y0 && TY0 + my_ly <= Y1;
     const int bt = (row / (TILE / LIB_RTH)) * fp.tiles_x + col;
     __syncthreads();   // the previous tile's key resets are done
     const bool tlon = fb.timeline != nullptr && tid == 0;
@@ -1446,10 +1450,8 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
     }
     const uint32_t *bin = fb.bins + (size_t)bt * fp.bin_cap;
-    const uint32_t i_end = parts > 1u ? (uint32_t)(((uint64_t)n_items * (part + 1u)) / parts) : n_items;
-    const uint32_t i_beg = parts > 1u ? (uint32_t)(((uint64_t)n_items * part) / parts) : 0u;
 
-    for (uint32_t base = i_beg; base < i_end; base += LIB_CAND) {
+    for (uint32_t base = 0; base < n_items; base += LIB_CAND) {
         __syncthreads();
         if (tid == 0) { sh.nc = 0; sh.zlo = 0xffffffffu; sh.zhi = 0u; }
         sh.hist[tid] = 0u;
@@ -1465,7 +1467,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         for (int k = 0; k < NG; ++k) {
             const uint32_t item = base + tid + 256u * k;
             uint32_t id = 0xffffffffu;
-            if (item < i_end) {
+            if (item < n_items) {
                 if (fp.scan_mode) {
                     id = item;
                 } else if (item < n_bin) {
@@ -1574,6 +1576,10 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
             } else {
                 if (hiz) {   // per pixel column, the largest key z so far
                     uint32_t o = (uint32_t)(sh.key[tid] >> 32);
+                    if (parts > 1u) {   // only the item's pixels bound its hierarchical z
+                        const int cx = TX0 + (tid & (LIB_RTW - 1)), cy = TY0 + tid / LIB_RTW;
+                        if (cx < X0 || cx > X1 || cy < Y0 || cy > Y1) o = 0u;
+                    }
                     o = max(o, (uint32_t)__shfl_xor((int)o, 32));   // a wave holds two rows of the column
                     if (lane < LIB_RTW) atomicMax(&sh.colmax[chunk & 1u][lane], o);
                 }
@@ -1596,7 +1602,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                         alive = true;
                         if (hiz) {
                             const uint2 b = sh.lbox[q];
-                            const int x0 = max(lo16(b.x), X0) - X0, x1 = min(hi16(b.x), X1) - X0;
+                            const int x0 = max(lo16(b.x), X0) - TX0, x1 = min(hi16(b.x), X1) - TX0;
                             uint32_t cm = 0u;
                             for (int x = x0; x <= x1; ++x) cm = max(cm, colmax[x]);
                             alive = sh.lkey[q] <= cm;
@@ -1689,7 +1695,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                     const int local = k - (int)pi.x, ow = (int)(pi.z & 0xffffu);
                     const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * ow;
                     const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
-                    const int kp = (py - Y0) * LIB_RTW + (px - X0);
+                    const int kp = (py - TY0) * LIB_RTW + (px - TX0);
                     // per-pixel hierarchical z: the pixel's current key already beats the
                     // primitive's depth bound (a stale, higher key only skips less)
                     if (sh.zord[o] > reinterpret_cast<const uint32_t *>(sh.key)[2 * kp + 1]) return;
@@ -1706,8 +1712,8 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     const uint64_t t_res = tlon ? tl_now() : 0ull;
     // a wave takes a 16x4 block of the tile (rows are 128-B key / 256-B HDR segments); the shadow pass
     // resolves here, the camera pass hands its keys to k_lib_resolve
-    const int lx = 16 * (wave & 1) + (lane & 15), ly = 4 * (wave >> 1) + (lane >> 4);
-    const int px = X0 + lx, py = Y0 + ly;
+    const int lx = my_lx, ly = my_ly;
+    const int px = TX0 + lx, py = TY0 + ly;
     const unsigned long long key = sh.key[ly * LIB_RTW + lx];
     sh.key[ly * LIB_RTW + lx] = KEY_EMPTY;   // this thread's pixel only: clean for the next tile
     bool covered;
@@ -1716,19 +1722,17 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     } else {
         // keys only for 16x4 blocks holding a winner; the block's flag tells k_lib_resolve which
         // (the wave's block is sub-block `wave` of the tile, k_lib_resolve's numbering)
+        // (a part writes only its own blocks: `mine` is wave-uniform)
         covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
         const bool any = __ballot(covered) != 0ull;
-        if (parts > 1u) {   // a part: merge into the keys k_lib_plan reset; flag blocks it holds winners of
-            if (covered) atomicMin(&fb.keys[(size_t)py * fp.W + px], key);
-            if (lane == 0 && any) fb.blkcov[(size_t)rt * 4 + wave] = 1u;
-        } else {
+        if (mine) {
             if (any && px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = key;
             if (lane == 0) fb.blkcov[(size_t)rt * 4 + wave] = any ? 1u : 0u;
         }
     }
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
-    if (tid == 0) fb.busy[rt] = 0u;
+    if (SHADOW && tid == 0) fb.busy[rt] = 0u;   // camera pass: k_lib_resolve resets it (split tiles' parts)
     if (tlon) {
         const uint64_t t_end = tl_now();
         sh.tl[LTL_GATHER] += t_gather;
@@ -1753,63 +1757,39 @@ __device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const L
     }
 }
 
-// The camera pass's raster work plan, after the marks are final (one 1024-thread workgroup): every
-// owned raster tile is one work item, except busy tiles whose bin list holds more than fp.part entries,
-// which become ceil(n / part) parts (at most LIB_MAXK) that any workgroups render at once -- the
-// hottest tiles no longer bound the raster (C4 at 8 shards: ~2 busy tiles per workgroup, 20-75 us
-// each).  The parts come first (the long items start early), each split tile's keys and block flags
-// are reset here for the parts' atomicMin merge.
-__device__ __forceinline__ uint32_t plan_parts(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int j, int &rt) {
-    rt = fb.rt_order[j];
+// The camera pass's raster work plan, after the marks are final (one thread per owned raster tile):
+// a busy tile whose bin list holds more than fp.part entries is split into its two 32x4 halves, above
+// 4 * fp.part into its four 16x4 blocks; the parts (cnt[LC_ITEMS] of them, in fb.items) are rendered
+// first, by any workgroups at once, then the owned tiles in order with the split ones skipped.  The
+// hottest tiles no longer bound the raster (C4 at 8 shards: ~2 busy tiles per workgroup, 20-75 us each).
+__device__ __forceinline__ uint32_t plan_parts(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt) {
     if (!fb.busy[rt]) return 1u;
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
     const uint32_t total = fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + (row / (TILE / LIB_RTH)) * fp.tiles_x + col];
     const uint32_t n = min(total, fp.bin_cap) + (total > fp.bin_cap ? min(cnt[LC_SPILL], fp.spill_cap) : 0u);
-    return n > fp.part ? min((uint32_t)LIB_MAXK, (n + fp.part - 1u) / fp.part) : 1u;
+    return n > 4u * fp.part ? 4u : n > fp.part ? 2u : 1u;
 }
 
-__global__ __launch_bounds__(1024) void k_lib_plan(LibFrameParams fp, LibBuffers fb) {
-    __shared__ uint32_t s_w[2][16];
+__global__ __launch_bounds__(256) void k_lib_plan(LibFrameParams fp, LibBuffers fb) {
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = fp.n_owned_rt, per = (n + 1023) / 1024;
-    const int j0 = min(n, tid * per), j1 = min(n, j0 + per);
-    uint32_t ks = 0u, kn = 0u;   // this thread's split parts / unsplit items
-    for (int j = j0; j < j1; ++j) {
-        int rt;
-        const uint32_t k = plan_parts(fp, fb, cnt, j, rt);
-        if (k > 1u) ks += k; else kn += 1u;
-    }
-    // exclusive block scans of ks and kn
-    uint32_t is = ks, in = kn;
+    const int j = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int rt = j < fp.n_owned_rt ? fb.rt_order[j] : 0;
+    const uint32_t k = j < fp.n_owned_rt ? plan_parts(fp, fb, cnt, rt) : 1u;
+    const uint32_t kk = k > 1u ? k : 0u;
+    // wave-aggregated reservation of this wave's parts
+    uint32_t incl = kk;
+    const int lane = __lane_id();
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t a = (uint32_t)__shfl_up((int)is, o), b = (uint32_t)__shfl_up((int)in, o);
-        if (lane >= o) { is += a; in += b; }
+        const uint32_t a = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += a;
     }
-    if (lane == 63) { s_w[0][wave] = is; s_w[1][wave] = in; }
-    __syncthreads();
-    uint32_t bs = 0u, bn = 0u, ts = 0u, tn = 0u;
-    for (int w = 0; w < 16; ++w) {
-        if (w < wave) { bs += s_w[0][w]; bn += s_w[1][w]; }
-        ts += s_w[0][w]; tn += s_w[1][w];
-    }
-    uint32_t ps = bs + is - ks, pn = ts + bn + in - kn;   // split parts first, then the rest
-    for (int j = j0; j < j1; ++j) {
-        int rt;
-        const uint32_t k = plan_parts(fp, fb, cnt, j, rt);
-        if (k > 1u) {
-            for (uint32_t p = 0; p < k; ++p) fb.items[ps++] = make_uint2((uint32_t)j, p | (k << 16));
-            const int X0 = (rt % fp.tiles_x) * LIB_RTW, Y0 = (rt / fp.tiles_x) * LIB_RTH;
-            for (int y = Y0; y < min(Y0 + LIB_RTH, fp.H); ++y)
-                for (int x = X0; x < min(X0 + LIB_RTW, fp.W); ++x) fb.keys[(size_t)y * fp.W + x] = KEY_EMPTY;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) fb.blkcov[(size_t)rt * 4 + s] = 0u;
-        } else {
-            fb.items[pn++] = make_uint2((uint32_t)j, 1u << 16);
-        }
-    }
-    if (tid == 0) cnt[LC_ITEMS] = ts + tn;
+    const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+    uint32_t base = 0u;
+    if (lane == 63 && tot) base = atomicAdd(&cnt[LC_ITEMS], tot);
+    base = (uint32_t)__shfl((int)base, 63) + incl - kk;
+    for (uint32_t p = 0; p < kk; ++p) fb.items[base + p] = make_uint2((uint32_t)rt, p | (k << 16));
+    if (kk) fb.busy[rt] = 2u;   // split: the in-order pass skips it (k_lib_resolve resets the flag)
 }
 
 template <bool SHADOW, int LIB_CAND>
@@ -1830,7 +1810,8 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
     // dynamic half; one tile per ticket keeps a dense bin tile's 4 rows on different workgroups.
     uint32_t *rq = fb.rqueue + (size_t)fp.parity * LIB_NQ * LIB_QSTRIDE;
     // work items: the owned raster tiles, or k_lib_plan's list (split tiles' parts first)
-    const int n_work = (!SHADOW && fp.part) ? (int)cnt[LC_ITEMS] : fp.n_owned_rt;
+    const int n_split = (!SHADOW && fp.part) ? (int)cnt[LC_ITEMS] : 0;
+    const int n_work = n_split + fp.n_owned_rt;
     const int S = max(1, n_work / (2 * G));
     const int dyn0 = S * G;
     int j = (int)blockIdx.x;
@@ -1843,15 +1824,18 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
         {
             int rt;
             uint32_t part = 0u, parts = 1u;
-            if (!SHADOW && fp.part) {
+            bool skip = false;
+            if (j < n_split) {
                 const uint2 it = fb.items[j];
-                rt = fb.rt_order[it.x];
+                rt = (int)it.x;
                 part = it.y & 0xffffu;
                 parts = it.y >> 16;
             } else {
-                rt = fb.rt_order[j];
+                rt = fb.rt_order[j - n_split];
+                skip = !SHADOW && fb.busy[rt] == 2u;   // rendered as parts (k_lib_plan)
             }
-            if (parts > 1u || fb.busy[rt]) {
+            if (skip) {
+            } else if (parts > 1u || fb.busy[rt]) {
                 lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk, part, parts);
             } else {
                 const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
@@ -1932,6 +1916,7 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
         const int py = (rt / fp.tiles_x) * LIB_RTH + 4 * (sub >> 1) + (lane >> 4);
         const bool inb = px < fp.W && py < fp.H;
         const bool any = fb.blkcov[(size_t)rt * 4 + sub] != 0u;   // wave-uniform
+        if (sub == 0 && lane == 0) fb.busy[rt] = 0u;   // the raster's busy / split flag, for the next pass
         const unsigned long long key = inb && any ? fb.keys[(size_t)py * fp.W + px] : KEY_EMPTY;
         LtWave lw;
 #ifdef SHS_RESOLVE_NO_LTWAVE
@@ -2025,7 +2010,7 @@ hipError_t launch_lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, in
 }
 
 hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, bool shallow, int grid, hipStream_t s) {
-    if (!shadow && fp.part) hipLaunchKernelGGL(k_lib_plan, dim3(1), dim3(1024), 0, s, fp, fb);
+    if (!shadow && fp.part) hipLaunchKernelGGL(k_lib_plan, dim3(std::max(1, (fp.n_owned_rt + 255) / 256)), dim3(256), 0, s, fp, fb);
     hipLaunchKernelGGL(SHS_RASTER_KERNEL(shadow, shallow), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }
