@@ -192,6 +192,10 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * `value` entries into parts rendered by several workgroups at once (merged by 64-bit atomicMin; the
  * results are identical).  -1 (default): 512 for tile-sharded passes, off otherwise; 0: off. */
 #define SHS_OPT_LIB_PART 7
+/* SHS_OPT_SHARD_CULL: 1 (default) = a tile-sharded camera pass first keeps the triangles that can
+ * reach the rank's tiles (a positions-only pass) and sets up only those; 0 = every rank sets up every
+ * triangle.  Results identical. */
+#define SHS_OPT_SHARD_CULL 8
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 
 /* Debug / profiling hook: the last frame's workgroup timeline.  out[0..7] = {k_setup grid, k_raster

@@ -700,6 +700,11 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
         ctx->want_timeline = value != 0;
         return SHS_OK;
     }
+    if (option == SHS_OPT_SHARD_CULL) {
+        if (value < 0 || value > 1) return SHS_ERR_INVALID;
+        ctx->shard_cull = value != 0;
+        return SHS_OK;
+    }
     if (option == SHS_OPT_LIB_PART) {
         if (value < -1 || value > (1 << 20)) return SHS_ERR_INVALID;
         ctx->lib_part = value;

@@ -771,6 +771,62 @@ __device__ __forceinline__ void setup_prologue(const LibFrameParams &fp, const L
 #else
 #define SHS_SETUP_BOUNDS __launch_bounds__(256)
 #endif
+// Tile-sharded camera pass, before k_lib_setup: every rank reads all triangles, but keeps only those
+// k_lib_setup would not drop -- a trivially inside triangle whose fan_screen is live (on screen, not
+// culled, on one of this rank's tiles), a triangle that needs clipping and can reach the rank
+// (clip_reaches_rank) -- as a (triangle, draw) list.  The same functions as k_lib_setup decide, so the
+// kept set is exactly the triangles whose records, marks or clip-queue entries this rank needs.  Lean:
+// positions only, PRE_PER triangles per thread (their loads in flight together), no LDS; C4 at 8
+// shards drops 7 in 8 triangles here instead of in k_lib_setup's heavier blocks.  The dropped
+// trivially-inside triangles' counts (tri_after_clip / tri_raster) go to LC_PCLIP / LC_PRAST.
+constexpr int PRE_PER = 4;
+
+__global__ __launch_bounds__(256) void k_lib_shard_cull(LibFrameParams fp, LibBuffers fb) {
+    uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    const int tid = (int)threadIdx.x;
+    uint32_t n_clip = 0u, n_rast = 0u;
+    const int span = 256 * PRE_PER;
+    for (int base = (int)blockIdx.x * span; base < fp.n_tris; base += (int)gridDim.x * span) {   // block-uniform
+#pragma unroll
+        for (int k = 0; k < PRE_PER; ++k) {
+            const int tri = base + 256 * k + tid;
+            const int c = (base >> 8) + k;   // this 256-triangle chunk = setup block c (its bdraw entry)
+            bool keep = false;
+            int d = 0;
+            if (tri < fp.n_tris) {
+                const int t_last = min(c * 256 + 255, fp.n_tris - 1);
+                const int d_first = fb.bdraw[c];
+                d = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : lib_find_draw(fb.dbase, fp.n_draws, tri);
+                const LibDrawGPU &dr = fb.draws[d];
+                uint32_t id[3];
+                if (read_tri(dr, tri - dr.tri_base, id)) {
+                    LVert t[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) t[q] = vertex_pos(dr, id[q]);
+                    if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
+                        float sx[3], sy[3], den;
+                        int x0, x1, y0, y1;
+                        uint32_t nr = 0u;
+                        keep = fan_screen(fp, dr, t[0], t[1], t[2], sx, sy, x0, x1, y0, y1, den, nr);
+                        if (!keep) { ++n_clip; n_rast += nr; }   // emit_fan's counts for fan 0
+                    } else {
+                        keep = clip_reaches_rank(fp, t);
+                    }
+                }
+            }
+            wave_append(&cnt[LC_LIST], fb.tri_list, keep, make_uint2((uint32_t)tri, (uint32_t)d));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        n_clip += __shfl_down(n_clip, o);
+        n_rast += __shfl_down(n_rast, o);
+    }
+    if (__lane_id() == 0 && (n_clip | n_rast)) {
+        atomicAdd(&cnt[LC_PCLIP], n_clip);
+        atomicAdd(&cnt[LC_PRAST], n_rast);
+    }
+}
+
 template <bool SHADOW>
 __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     __shared__ SetupShared ss;
@@ -779,38 +835,65 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     const bool stl = fb.stimeline != nullptr && tid == 0;
     const uint64_t st0 = stl ? tl_now() : 0ull;
     setup_prologue(fp, fb, ss, b, tid);
-    const int tri = b * 256 + tid;
-    uint32_t n_clip = 0, n_rast = 0;
-    Pend pend;
-    bool need_clip = false;
-    if (tri < fp.n_tris) {
-        // the block's draw when all its triangles share one (block-uniform: its uniforms come in
-        // through scalar loads), else -1 and a per-thread search
-        const int t_last = min(b * 256 + 255, fp.n_tris - 1);
-        const int d_first = fb.bdraw[b];
-        const int d_uni = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : -1;
-        if (d_uni >= 0) {   // two inlined copies: this one sees d_uni as the (scalar) draw
-            if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, d_uni);
-            else need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, d_uni);
-        } else {
-            if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, -1);
-            else need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, -1);
+    // the triangles: b * 256 + tid (one chunk per block), or (tile-sharded camera pass) k_lib_shard_cull's
+    // list, 256 entries per chunk, the grid striding it
+    const bool listed = !SHADOW && fb.tri_list != nullptr;
+    const int n_items = listed ? (int)cnt[LC_LIST] : fp.n_tris;
+    uint32_t acc_clip = 0u, acc_rast = 0u, nbig = 0u;
+    uint64_t st1 = 0ull, st2 = 0ull;
+    int uwh = 0;
+    for (int chunk = b; chunk == b || chunk * 256 < n_items; chunk += (int)gridDim.x) {   // block-uniform
+        if (chunk != b) {
+            __syncthreads();   // the previous chunk's LDS state is consumed
+            setup_shared_init(ss, tid);
+            __syncthreads();
         }
+        int tri = chunk * 256 + tid;
+        uint32_t n_clip = 0, n_rast = 0;
+        Pend pend;
+        bool need_clip = false;
+        if (listed) {
+            const bool act = tri < n_items;
+            uint2 e = make_uint2(0u, 0u);
+            if (act) e = fb.tri_list[tri];
+            tri = act ? (int)e.x : -1;
+            const int d = (int)e.y;
+            const int d0 = __builtin_amdgcn_readfirstlane(d);
+            if (__ballot(act && d != d0) == 0ull) {   // wave-uniform draw: scalar uniform loads
+                if (act) need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, d0);
+            } else if (act) {
+                need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, d);
+            }
+        } else if (tri < fp.n_tris) {
+            // the block's draw when all its triangles share one (block-uniform: its uniforms come in
+            // through scalar loads), else -1 and a per-thread search
+            const int t_last = min(chunk * 256 + 255, fp.n_tris - 1);
+            const int d_first = fb.bdraw[chunk];
+            const int d_uni = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : -1;
+            if (d_uni >= 0) {   // two inlined copies: this one sees d_uni as the (scalar) draw
+                if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, d_uni);
+                else need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, d_uni);
+            } else {
+                if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, -1);
+                else need_clip = setup_camera_tri(fp, fb, cnt, tri, n_clip, n_rast, ss, pend, -1);
+            }
+        }
+        if (!SHADOW) wave_append(&cnt[LC_CLIPQ], fb.clipq, need_clip, (uint32_t)tri);
+        setup_gather(ss, pend, n_clip, n_rast);
+        __syncthreads();
+        if (stl) st1 = tl_now();
+        uwh = setup_deferred(fp, fb, cnt, ss, pend, tid);
+        if (stl) st2 = tl_now();
+        nbig += setup_flush_big(fp, fb, cnt, ss, tid);
+        if (tid == 0) { acc_clip += ss.stat[0]; acc_rast += ss.stat[1]; }
+        if (!listed) break;
     }
-    if (!SHADOW) wave_append(&cnt[LC_CLIPQ], fb.clipq, need_clip, (uint32_t)tri);
-    setup_gather(ss, pend, n_clip, n_rast);
-    __syncthreads();
-    const uint64_t st1 = stl ? tl_now() : 0ull;
-    const int uwh = setup_deferred(fp, fb, cnt, ss, pend, tid);
-    if (stl) fb.stimeline[(size_t)b * STL_STRIDE + 5] = (uint64_t)uwh;
-    const uint64_t st2 = stl ? tl_now() : 0ull;
-    const uint32_t nbig = setup_flush_big(fp, fb, cnt, ss, tid);
-    if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(ss.stat[0], ss.stat[1]);
+    if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(acc_clip, acc_rast);
     if (fb.stimeline) {
         __syncthreads();
         if (tid == 0) {
             uint64_t *o = fb.stimeline + (size_t)b * STL_STRIDE;
-            o[0] = st0; o[1] = st1; o[2] = st2; o[3] = tl_now(); o[4] = nbig;
+            o[0] = st0; o[1] = st1; o[2] = st2; o[3] = tl_now(); o[4] = nbig; o[5] = (uint64_t)uwh;
         }
     }
 }
@@ -1964,12 +2047,18 @@ using namespace shs_dev;
 // k_lib_setup, then (camera pass) k_lib_clip over the queued triangles, then the large primitives'
 // marks (k_lib_bigmark).  The queue lengths stay on the device: the later kernels'
 // grids are fixed and stride or split what the counters hold.
-hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, hipStream_t s) {
+hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, int setup_grid, hipStream_t s) {
     const int grid = std::max(1, (fp.n_tris + 255) / 256);
     if (shadow) {
         hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     } else {
-        hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
+        if (fb.tri_list) {   // tile-sharded: the rank's triangles first, then a grid striding that list
+            hipLaunchKernelGGL(k_lib_shard_cull, dim3(std::max(1, (fp.n_tris + 256 * PRE_PER - 1) / (256 * PRE_PER))), dim3(256),
+                               0, s, fp, fb);
+            hipLaunchKernelGGL(k_lib_setup<false>, dim3(std::max(1, std::min(setup_grid, grid))), dim3(256), 0, s, fp, fb);
+        } else {
+            hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
+        }
         // one 16-lane group per queued triangle (the queue can hold every input triangle), at most
         // 1024 workgroups striding a longer queue
         hipLaunchKernelGGL(k_lib_clip, dim3(std::max(1, std::min((fp.n_tris + 15) / 16, 1024))), dim3(256), 0, s, fp, fb);

@@ -89,9 +89,10 @@ constexpr uint32_t LF_GRADIENT = 8u;    // PassPBRForward's no-sky background gr
 // (primitive, tile) task total and length, one 64-bit word (tasks low, entries high) so that one
 // atomicAdd hands an appender both bases and the queue's task prefix stays monotone; LC_N even keeps
 // the second parity set's word 8-B aligned.
-// LC_ITEMS: k_lib_plan's raster work items; LC_COVERED: camera-pass covered pixels (k_lib_resolve).
+// LC_ITEMS: k_lib_plan's raster work items; LC_COVERED: camera-pass covered pixels (k_lib_resolve);
+// LC_LIST: k_lib_shard_cull's kept triangles, LC_PCLIP / LC_PRAST: the statistics of the ones it dropped.
 constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT = 4, LC_BIGQ = 5, LC_ITEMS = 6, LC_COVERED = 7,
-              LC_N = 8;
+              LC_LIST = 8, LC_PCLIP = 9, LC_PRAST = 10, LC_N = 12;
 static_assert(LC_BIGQ == LC_BIGT + 1 && LC_BIGT % 2 == 0 && LC_N % 2 == 0, "64-bit big-queue word");
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
@@ -154,6 +155,7 @@ struct LibBuffers {
     float4 *uvw;                     // per slot, 2 float4: UV0 varying * 1/w of the 3 corners (textured draws)
     const float *srgb_lut;           // srgb_to_linear_rgb's 256 values, std::pow(c / 255.0f, 2.2f) on the host
     uint2 *items;                    // k_lib_plan: raster work items (rt_order position, part | parts << 16)
+    uint2 *tri_list;                 // tile-sharded camera pass: k_lib_shard_cull's kept (triangle, draw)
 };
 
 // k_lib_plan: at most this many parts per raster tile (capacity: LIB_MAXK * owned raster tiles).

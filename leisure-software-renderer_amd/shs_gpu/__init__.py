@@ -525,6 +525,10 @@ class Context:
         """Camera-pass raster work split (SHS_OPT_LIB_PART): -1 auto, 0 off, else the part size."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_LIB_PART, int(part)))
 
+    def set_shard_cull(self, on: bool):
+        """SHS_OPT_SHARD_CULL: tile-sharded camera passes set up only the rank's triangles (default on)."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_SHARD_CULL, 1 if on else 0))
+
     def set_overflow_capacities(self, spill: int = 0, frags: int = 0):
         """Tests: shrink the legacy bin-spill / ghost-fragment lists (0 = leave) to force overflows."""
         if spill:

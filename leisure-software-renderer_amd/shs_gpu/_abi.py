@@ -31,6 +31,7 @@ OPT_RASTER_LOOP = 4
 OPT_SPILL_CAPACITY = 5
 OPT_FRAG_CAPACITY = 6
 OPT_LIB_PART = 7
+OPT_SHARD_CULL = 8
 
 
 class LegacyDraw(ctypes.Structure):

@@ -251,3 +251,38 @@ def test_split_raster_items_exact(oracle_mod, part):
         assert ctx.lib_stats()["covered_pixels"] == int((rd < 1.0).sum())
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("count", [2, 5, 8])
+def test_shard_cull_prepass_identical(count):
+    """SHS_OPT_SHARD_CULL: a tile-sharded camera pass with the positions-only pre-pass (the rank's
+    triangles only) renders the same tiles and counts the same statistics as without it."""
+    import shs_gpu
+    from shs_gpu import scene_lib
+    frame, draws, lights, cull = scene_lib.c4_scene(800, 450, n_objects=120, tris_per_object=400)
+    res = {}
+    for on in (True, False):
+        ctx = shs_gpu.Context(0)
+        try:
+            ctx.set_shard_cull(on)
+            ctx.upload_lights(lights)
+            outs = []
+            for r in range(count):
+                frame.shard_rank, frame.shard_count = r, count
+                cull.shard_rank, cull.shard_count = r, count
+                ctx.light_cull(cull)
+                ctx.render_pbr_forward(frame, draws)
+                h, d, m = ctx.resolve_lib()
+                ty, tx = np.mgrid[0:450, 0:800] // 32
+                own = ((ty * 25 + tx) % count) == r
+                outs.append((h[own].copy(), d[own].copy(), m[own].copy(), ctx.lib_stats()))
+            res[on] = outs
+        finally:
+            ctx.close()
+    frame.shard_rank, frame.shard_count = 0, 1
+    for a, b in zip(res[True], res[False]):
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+        for k in ("tri_input", "tri_after_clip", "tri_raster", "covered_pixels"):
+            assert a[3][k] == b[3][k], (k, a[3][k], b[3][k])
