@@ -782,11 +782,14 @@ __device__ __forceinline__ void setup_prologue(const LibFrameParams &fp, const L
 constexpr int PRE_PER = 4;
 
 __global__ __launch_bounds__(256) void k_lib_shard_cull(LibFrameParams fp, LibBuffers fb) {
+    __shared__ uint32_t s_wave[4], s_base;
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    const int tid = (int)threadIdx.x;
+    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t n_clip = 0u, n_rast = 0u;
     const int span = 256 * PRE_PER;
     for (int base = (int)blockIdx.x * span; base < fp.n_tris; base += (int)gridDim.x * span) {   // block-uniform
+        bool keep_k[PRE_PER];
+        int d_k[PRE_PER];
 #pragma unroll
         for (int k = 0; k < PRE_PER; ++k) {
             const int tri = base + 256 * k + tid;
@@ -814,8 +817,34 @@ __global__ __launch_bounds__(256) void k_lib_shard_cull(LibFrameParams fp, LibBu
                     }
                 }
             }
-            wave_append(&cnt[LC_LIST], fb.tri_list, keep, make_uint2((uint32_t)tri, (uint32_t)d));
+            keep_k[k] = keep;
+            d_k[k] = d;
         }
+        // one reservation per block and pass (a single list counter: per-wave atomics would queue on it)
+        uint32_t mine = 0u;
+#pragma unroll
+        for (int k = 0; k < PRE_PER; ++k) mine += keep_k[k] ? 1u : 0u;
+        uint32_t incl = mine;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) s_wave[wave] = incl;
+        __syncthreads();
+        uint32_t wbase = 0u, total = 0u;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            wbase += w < wave ? s_wave[w] : 0u;
+            total += s_wave[w];
+        }
+        if (tid == 0) s_base = total ? atomicAdd(&cnt[LC_LIST], total) : 0u;
+        __syncthreads();
+        uint32_t at = s_base + wbase + incl - mine;
+#pragma unroll
+        for (int k = 0; k < PRE_PER; ++k)
+            if (keep_k[k]) fb.tri_list[at++] = make_uint2((uint32_t)(base + 256 * k + tid), (uint32_t)d_k[k]);
+        __syncthreads();   // s_wave / s_base reused by the next pass
     }
     for (int o = 32; o > 0; o >>= 1) {
         n_clip += __shfl_down(n_clip, o);
@@ -827,7 +856,7 @@ __global__ __launch_bounds__(256) void k_lib_shard_cull(LibFrameParams fp, LibBu
     }
 }
 
-template <bool SHADOW>
+template <bool SHADOW, bool LISTED = false>
 __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     __shared__ SetupShared ss;
     const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
@@ -837,7 +866,7 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     setup_prologue(fp, fb, ss, b, tid);
     // the triangles: b * 256 + tid (one chunk per block), or (tile-sharded camera pass) k_lib_shard_cull's
     // list, 256 entries per chunk, the grid striding it
-    const bool listed = !SHADOW && fb.tri_list != nullptr;
+    constexpr bool listed = !SHADOW && LISTED;
     const int n_items = listed ? (int)cnt[LC_LIST] : fp.n_tris;
     uint32_t acc_clip = 0u, acc_rast = 0u, nbig = 0u;
     uint64_t st1 = 0ull, st2 = 0ull;
@@ -852,7 +881,7 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
         uint32_t n_clip = 0, n_rast = 0;
         Pend pend;
         bool need_clip = false;
-        if (listed) {
+        if constexpr (listed) {
             const bool act = tri < n_items;
             uint2 e = make_uint2(0u, 0u);
             if (act) e = fb.tri_list[tri];
@@ -2055,7 +2084,7 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
         if (fb.tri_list) {   // tile-sharded: the rank's triangles first, then a grid striding that list
             hipLaunchKernelGGL(k_lib_shard_cull, dim3(std::max(1, (fp.n_tris + 256 * PRE_PER - 1) / (256 * PRE_PER))), dim3(256),
                                0, s, fp, fb);
-            hipLaunchKernelGGL(k_lib_setup<false>, dim3(std::max(1, std::min(setup_grid, grid))), dim3(256), 0, s, fp, fb);
+            hipLaunchKernelGGL((k_lib_setup<false, true>), dim3(std::max(1, std::min(setup_grid, grid))), dim3(256), 0, s, fp, fb);
         } else {
             hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
         }
