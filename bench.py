@@ -221,62 +221,98 @@ def lib_workload(args, rank=0):
     return scene_lib.c5_scene(3840, 2160, 2048)
 
 
-def run_gpu_c4(args, rank, local_rank, world, dist):
-    """C4 frame = Forward+ light-list binning (shs_light_cull) + PassPBRForward with the per-pixel
-    point-light program over 1M triangles at 3840x2160 + PassTonemap into the RGBA8 present staging.
-    N > 1: the frame's 32x32 tiles are sharded (tile % N == rank): every rank culls, renders and
-    tonemaps only its tiles, and the owned present tiles (4 B/px) are gathered into rank 0 over RCCL
-    every frame (strong scaling: the total work per step is one frame)."""
-    import shs_gpu
-    from shs_gpu import shard
-    frame, draws, lights, cull = lib_workload(args, rank)
-    ctx = shs_gpu.Context(local_rank)
-    if dist is not None:
-        import torch
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-        frame.shard_rank, frame.shard_count = rank, world
-        cull.shard_rank, cull.shard_count = rank, world
-    ctx.upload_lights(lights)
-    ctx.light_cull(cull)
-    prepared = ctx.prepare_lib(frame, draws)
-    gbufs = [None]
-    ctx.fuse_tonemap(1.0, 2.2, ldr=False, present=True)   # PassTonemap inside the pass's shading kernel
+class LibSlot:
+    """One frame in flight: a context with its own stream, workspace and targets (frames k, k + D, ...)."""
 
-    def one_frame():
-        ctx.light_cull(cull)
-        ctx.render_pbr_forward_prepared(prepared)
+    def __init__(self, local_rank, dist):
+        import shs_gpu
+        self.ctx = shs_gpu.Context(local_rank)
+        self.stream = None
         if dist is not None:
-            gbufs[0] = shard.gather_frame_device(dist, ctx, ctx.TARGET_LIB_PRESENT, out=gbufs[0])
+            import torch
+            self.stream = torch.cuda.Stream()
+            self.ctx.set_stream(self.stream.cuda_stream)
+        self.gbufs = [None]
+        self.prepared = None
 
-    for _ in range(max(args.warmup, 1)):
-        one_frame()
-    ctx.synchronize_lib()
-    stats = ctx.lib_stats()
+    def gather(self, dist):
+        """The frame's owned present tiles into rank 0 over RCCL, ordered on this slot's stream."""
+        import torch
+        from shs_gpu import shard
+        with torch.cuda.stream(self.stream):
+            self.gbufs[0] = shard.gather_frame_device(dist, self.ctx, self.ctx.TARGET_LIB_PRESENT, stream=self.stream,
+                                                      out=self.gbufs[0])
+
+
+def lib_timed_loop(args, slots, frame_fn, dist):
+    """Warm-up, then exactly args.steps frames round-robin over the slots (frame i on slot i % D) between
+    two barriers; then kernel event times of 20 frames on slot 0 alone (nothing else in flight: the
+    roofline's kernel durations).  -> (elapsed s, stats, (n_frames, kms))"""
+    D = len(slots)
+    for i in range(max(args.warmup, D)):
+        frame_fn(slots[i % D])
 
     def barrier_sync():
-        ctx.synchronize_lib()
+        for sl in slots:
+            sl.ctx.synchronize_lib()
         if dist is not None:
             import torch
             torch.cuda.synchronize()
             dist.barrier()
 
-    ctx.enable_timing(True)
-    ctx.lib_timing_reset()
     barrier_sync()
+    stats = slots[0].ctx.lib_stats()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_frame()
+    for i in range(args.steps):
+        frame_fn(slots[i % D])
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    ctx = slots[0].ctx
+    ctx.enable_timing(True)
+    ctx.lib_timing_reset()
+    for _ in range(20):
+        frame_fn(slots[0])
+    barrier_sync()
     n_passes, kms = ctx.lib_timing_read()
-    kms = {"setup": kms["setup"], "raster": kms["raster"]}
     ctx.enable_timing(False)
-    ctx.close()
+    for sl in slots:
+        sl.ctx.close()
+    return elapsed, stats, (n_passes["camera"], kms)
+
+
+def run_gpu_c4(args, rank, local_rank, world, dist):
+    """C4 frame = Forward+ light-list binning (shs_light_cull) + PassPBRForward with the per-pixel
+    point-light program over 1M triangles at 3840x2160 + PassTonemap into the RGBA8 present staging.
+    N > 1: the frame's 32x32 tiles are sharded (tile % N == rank): every rank culls, renders and
+    tonemaps only its tiles, and the owned present tiles (4 B/px) are gathered into rank 0 over RCCL
+    every frame (strong scaling: the total work per step is one frame).  args.inflight contexts render
+    consecutive frames round-robin (frames in flight, at every N alike)."""
+    frame, draws, lights, cull = lib_workload(args, rank)
+    if dist is not None:
+        frame.shard_rank, frame.shard_count = rank, world
+        cull.shard_rank, cull.shard_count = rank, world
+    slots = []
+    for _ in range(args.inflight):
+        sl = LibSlot(local_rank, dist)
+        sl.ctx.upload_lights(lights)
+        sl.ctx.light_cull(cull)
+        sl.prepared = sl.ctx.prepare_lib(frame, draws)
+        sl.ctx.fuse_tonemap(1.0, 2.2, ldr=False, present=True)   # PassTonemap inside the pass's shading kernel
+        slots.append(sl)
+
+    def one_frame(sl):
+        sl.ctx.light_cull(cull)
+        sl.ctx.render_pbr_forward_prepared(sl.prepared)
+        if dist is not None:
+            sl.gather(dist)
+
+    elapsed, stats, (n_cam, kms) = lib_timed_loop(args, slots, one_frame, dist)
+    kms = {"setup": kms["setup"], "raster": kms["raster"]}
     n_tri = sum(d.mesh.n_tris for d in draws)
     # the raster phase writes HDR + depth + motion (28 B/px) and the fused tonemap's RGBA8 present staging (4 B/px)
     B_cam_raster = frame.width * frame.height * 32
     B_frame = n_tri * 72 + frame.width * frame.height * 32 + len(lights) * 160 + cull.n_lists * 4
-    return frame, stats, elapsed, n_passes["camera"], kms, B_cam_raster, B_frame, n_tri, None
+    return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, None
 
 
 def lib_mesh_bytes(mesh, with_attrs=True):
@@ -289,66 +325,41 @@ def lib_mesh_bytes(mesh, with_attrs=True):
 def run_gpu_lib(args, rank, local_rank, world, dist):
     """C5 frame = PassShadowMap + PassPBRForward + PassTonemap (present staging).  N > 1: tile-sharded
     like C4 -- the shadow map (every rank's PCF reads all of it) is rendered on every rank, the camera
-    pass and the tonemap only on the rank's tiles, and the present tiles are gathered into rank 0."""
-    import shs_gpu
-    from shs_gpu import scene_lib, shard
-    frame, draws, casters, sun, S = lib_workload(args, 0)
-    ctx = shs_gpu.Context(local_rank)
-    if dist is not None:
-        import torch
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-        frame.shard_rank, frame.shard_count = rank, world
-    lvp = ctx.render_shadow_map(S, sun, casters)
-    scene_lib.wire_shadow(draws, lvp)
-    prepared = ctx.prepare_lib(frame, draws)
-    from shs_gpu import _abi
-    ShadowArr = _abi.ShadowCasterC * len(casters)
-    carr = ShadowArr()
-    for i, c in enumerate(casters):
-        carr[i].mesh_id = ctx.upload_lib_mesh(c.mesh)
-        for k in range(16):
-            carr[i].model[k] = float(c.model[k])
+    pass and the tonemap only on the rank's tiles, and the present tiles are gathered into rank 0.
+    args.inflight contexts render consecutive frames round-robin."""
     import ctypes
+    from shs_gpu import scene_lib, _abi
+    frame, draws, casters, sun, S = lib_workload(args, 0)
+    if dist is not None:
+        frame.shard_rank, frame.shard_count = rank, world
     sd = (ctypes.c_float * 3)(*[float(x) for x in sun])
-    L = ctx._lib
+    slots = []
+    for _ in range(args.inflight):
+        sl = LibSlot(local_rank, dist)
+        ctx = sl.ctx
+        lvp = ctx.render_shadow_map(S, sun, casters)
+        scene_lib.wire_shadow(draws, lvp)
+        sl.prepared = ctx.prepare_lib(frame, draws)
+        sl.carr = (_abi.ShadowCasterC * len(casters))()
+        for i, c in enumerate(casters):
+            sl.carr[i].mesh_id = ctx.upload_lib_mesh(c.mesh)
+            for k in range(16):
+                sl.carr[i].model[k] = float(c.model[k])
+        ctx.fuse_tonemap(1.0, 2.2, ldr=False, present=True)   # PassTonemap inside the pass's shading kernel
+        slots.append(sl)
 
-    gbufs = [None]
-    ctx.fuse_tonemap(1.0, 2.2, ldr=False, present=True)   # PassTonemap inside the pass's shading kernel
-
-    def one_frame():
-        ctx._check(L.shs_render_shadow_map(ctx._h, S, S, sd, carr, len(casters), None))
-        ctx.render_pbr_forward_prepared(prepared)
+    def one_frame(sl):
+        sl.ctx._check(sl.ctx._lib.shs_render_shadow_map(sl.ctx._h, S, S, sd, sl.carr, len(casters), None))
+        sl.ctx.render_pbr_forward_prepared(sl.prepared)
         if dist is not None:
-            gbufs[0] = shard.gather_frame_device(dist, ctx, ctx.TARGET_LIB_PRESENT, out=gbufs[0])
+            sl.gather(dist)
 
-    for _ in range(max(args.warmup, 1)):
-        one_frame()
-    ctx.synchronize_lib()
-    stats = ctx.lib_stats()
-
-    def barrier_sync():
-        ctx.synchronize_lib()
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
-
-    ctx.enable_timing(True)
-    ctx.lib_timing_reset()
-    barrier_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_frame()
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    n_passes, kms = ctx.lib_timing_read()
-    ctx.enable_timing(False)
-    ctx.close()
+    elapsed, stats, (n_cam, kms) = lib_timed_loop(args, slots, one_frame, dist)
     B_cam_raster = frame.width * frame.height * 32 + S * S * 4
     B_frame = (sum(lib_mesh_bytes(d.mesh) for d in draws) + sum(lib_mesh_bytes(c.mesh, False) for c in casters)
                + 2 * S * S * 4 + frame.width * frame.height * 32)
     n_tri = sum(d.mesh.n_tris for d in draws)
-    return frame, stats, elapsed, n_passes["camera"], kms, B_cam_raster, B_frame, n_tri, S
+    return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, S
 
 
 def collect_pmc(args):
@@ -549,6 +560,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--frames-per-step", type=int, default=0,
                     help="legacy configs: frames per shs_render_legacy_batch step (default 64 for c1/c2, 16 for c3)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="c4/c5: frames in flight (contexts rendering consecutive frames round-robin)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -730,10 +743,11 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
         "config": {"workload": WORKLOADS[args.config], "width": frame.width, "height": frame.height,
                    "shadow_map": S, "tris_per_frame": n_tri, "frames_per_step_per_gpu": 1,
-                   "parallelism": parallelism},
+                   "frames_in_flight": args.inflight, "parallelism": parallelism},
         "shaded_mpix_s": round(covered_total * steps / el_max / 1e6, 3),
         "frame_stats": stats, "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
-        "timed_frames_with_events": n_frames, "roofline": roofline,
+        "kernel_timing": f"{n_frames} frames on one context alone after the timed loop (HIP events)",
+        "roofline": roofline,
     }
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)

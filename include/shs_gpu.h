@@ -188,13 +188,15 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * superseded); results are identical. */
 #define SHS_OPT_SPILL_CAPACITY 5
 #define SHS_OPT_FRAG_CAPACITY 6
-/* SHS_OPT_LIB_PART: library camera passes split a busy raster tile whose bin list holds more than
- * `value` entries into parts rendered by several workgroups at once (merged by 64-bit atomicMin; the
- * results are identical).  -1 (default): 512 for tile-sharded passes, off otherwise; 0: off. */
+/* SHS_OPT_LIB_PART: library camera passes split a busy 32x8 raster tile whose bin list holds more than
+ * `value` entries into spatial parts (32x4 halves or 16x4 blocks) rendered by several workgroups at
+ * once, each over the whole list but only its own pixels (no merge; results identical).  -1: 512 for
+ * tile-sharded passes, off otherwise; 0 (default): off. */
 #define SHS_OPT_LIB_PART 7
-/* SHS_OPT_SHARD_CULL: 1 (default) = a tile-sharded camera pass first keeps the triangles that can
- * reach the rank's tiles (a positions-only pass) and sets up only those; 0 = every rank sets up every
- * triangle.  Results identical. */
+/* SHS_OPT_SHARD_CULL: 1 = each setup workgroup of a tile-sharded camera pass first keeps the triangles
+ * of its inputs that can reach the rank's tiles (positions only) and sets up only those; 0 (default) =
+ * every rank sets up every triangle, dropping the ones off its tiles after the transform.  Results
+ * identical. */
 #define SHS_OPT_SHARD_CULL 8
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 

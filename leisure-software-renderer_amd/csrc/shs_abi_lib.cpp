@@ -56,7 +56,7 @@ void release_work(Work &w) {
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.tri_list); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
     if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
@@ -353,15 +353,10 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.bdraw = fb.dbase + nd + 1;
     fb.rqueue = w.rqueue.p;
     fb.items = fp.part ? w.items.p : nullptr;
-    // Tile-sharded camera pass in bin mode: k_lib_shard_cull keeps the rank's triangles, k_lib_setup strides
-    // that list with about 1.5x the rank's share of the full grid (SHS_OPT_SHARD_CULL 0: off).
-    int setup_grid = setup_blocks;
-    fb.tri_list = nullptr;
-    if (!shadow && !fp.scan_mode && fp.count > 1 && ctx->shard_cull) {
-        if (ensure(ctx, w.tri_list, (size_t)std::max(n_tris, 1))) return SHS_ERR_HIP;
-        fb.tri_list = w.tri_list.p;
-        setup_grid = std::min(setup_blocks, (int)((3LL * setup_blocks) / (2LL * fp.count)) + 16);
-    }
+    // Tile-sharded camera pass in bin mode: each setup workgroup first keeps the rank's triangles of its
+    // inputs, positions only (SHS_OPT_SHARD_CULL 0: off).
+    const bool listed = !shadow && !fp.scan_mode && fp.count > 1 && ctx->shard_cull;
+    const int setup_grid = shs_internal::lib_setup_grid(n_tris, listed);
     fb.rt_order = w.rt_order.p;
     if (shadow) {
         fb.depth = ctx->shadow_map.p;
@@ -425,7 +420,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     *w.h_ov = 0u;
     fb.ov_host = const_cast<uint32_t *>(w.h_ov);
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], ps));
-    HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, setup_grid, ps));
+    HIP_TRY(ctx, shs_internal::launch_lib_setup(fp, fb, shadow, listed, ps));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[1], ps));
     // the pass's overflow word is final after its setup kernels (setup, clip, large-primitive marks), so
     // superseding the pass checks it at ov_after, without waiting for the raster
@@ -451,7 +446,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], ctx->stream));
     w.last_parity = fp.parity;
     w.frame_index++;
-    w.last_setup_blocks = fb.tri_list ? setup_grid : setup_blocks;
+    w.last_setup_blocks = setup_grid;
     w.last_raster_grid = raster_grid;
     w.last_n_tris = n_tris;
     w.need_check = true;
@@ -487,8 +482,6 @@ int check_pass(shs_ctx *ctx, Work &w, bool &grew) {
     HIP_TRY(ctx, hipMemcpy(rs.data(), w.rstat.p, rs.size() * sizeof(uint2), hipMemcpyDeviceToHost));
     w.st_clip = w.st_raster = w.st_covered = w.st_maxbin = 0;
     for (const uint2 &b : bs) { w.st_clip += b.x; w.st_raster += b.y; }
-    w.st_clip += c[shs_dev::LC_PCLIP];   // k_lib_shard_cull's dropped triangles (0 otherwise)
-    w.st_raster += c[shs_dev::LC_PRAST];
     for (const uint2 &r : rs) { w.st_covered += r.x; w.st_maxbin = std::max<uint64_t>(w.st_maxbin, r.y); }
     if (&w == &ctx->lib_cam) w.st_covered = c[shs_dev::LC_COVERED];   // counted by k_lib_resolve
     w.st_spill = c[shs_dev::LC_SPILL];

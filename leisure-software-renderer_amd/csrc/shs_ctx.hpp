@@ -145,7 +145,6 @@ struct shs_ctx {
         DevBuf<uint2> spill, blk_stat, rstat;
         DevBuf<float4> uvw;                                // UV0 varyings of textured draws' slots
         DevBuf<uint2> items;                               // k_lib_plan's raster work items
-        DevBuf<uint2> tri_list;                            // k_lib_shard_cull's kept (triangle, draw)
         shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots
         size_t h_cap = 0;
         hipEvent_t slot_ev[2] = {nullptr, nullptr};
@@ -177,8 +176,8 @@ struct shs_ctx {
         int64_t acc_n = 0;
     };
     LibWork lib_cam, lib_shadow;
-    int64_t lib_part = -1;                // SHS_OPT_LIB_PART
-    bool shard_cull = true;               // SHS_OPT_SHARD_CULL
+    int64_t lib_part = 0;                 // SHS_OPT_LIB_PART (off by default: measured)
+    bool shard_cull = false;              // SHS_OPT_SHARD_CULL (off by default: measured)
     int lib_resident[2][2] = {{0, 0}, {0, 0}};   // resident k_lib_raster workgroups [camera, shadow][deep, shallow]
     DevBuf<uint64_t> lib_timeline;        // SHS_OPT_TIMELINE, camera pass raster
     DevBuf<uint64_t> lib_stimeline;       // SHS_OPT_TIMELINE, camera pass setup

@@ -142,6 +142,17 @@ __device__ __forceinline__ LVert vertex_pos(const LibDrawGPU &dr, uint32_t id) {
     return o;
 }
 
+__device__ __forceinline__ LVert vertex_pos_xyz(const LibDrawGPU &dr, float x, float y, float z) {
+    LVert o;
+    const f4 wp = m4v(dr.model, f4{x, y, z, 1.0f});
+    const f4 c = m4v(dr.viewproj, wp);
+    o.cx = c.x; o.cy = c.y; o.cz = c.z; o.cw = c.w;
+    o.wx = wp.x; o.wy = wp.y; o.wz = wp.z;
+    o.nx = o.ny = o.nz = 0.0f;
+    o.u = o.v = 0.0f;
+    return o;
+}
+
 __device__ __forceinline__ LVert vertex_out(const LibDrawGPU &dr, uint32_t id) {
     LVert o = vertex_pos(dr, id);
     vertex_attrs(dr, id, o);
@@ -771,120 +782,137 @@ __device__ __forceinline__ void setup_prologue(const LibFrameParams &fp, const L
 #else
 #define SHS_SETUP_BOUNDS __launch_bounds__(256)
 #endif
-// Tile-sharded camera pass, before k_lib_setup: every rank reads all triangles, but keeps only those
-// k_lib_setup would not drop -- a trivially inside triangle whose fan_screen is live (on screen, not
-// culled, on one of this rank's tiles), a triangle that needs clipping and can reach the rank
-// (clip_reaches_rank) -- as a (triangle, draw) list.  The same functions as k_lib_setup decide, so the
-// kept set is exactly the triangles whose records, marks or clip-queue entries this rank needs.  Lean:
-// positions only, PRE_PER triangles per thread (their loads in flight together), no LDS; C4 at 8
-// shards drops 7 in 8 triangles here instead of in k_lib_setup's heavier blocks.  The dropped
-// trivially-inside triangles' counts (tri_after_clip / tri_raster) go to LC_PCLIP / LC_PRAST.
-constexpr int PRE_PER = 4;
+// Tile-sharded camera pass (LISTED): a setup workgroup first reads the positions of CULL_PER x 256
+// consecutive input triangles and keeps in LDS those k_lib_setup would not drop -- a trivially inside
+// triangle whose fan_screen is live (on screen, not culled, on one of this rank's tiles), a triangle
+// that needs clipping and can reach the rank (clip_reaches_rank) -- then sets up only the kept ones,
+// 256 per round.  The same functions decide, so the kept set is exactly the triangles whose records,
+// marks or clip-queue entries this rank needs; at 8 shards C4 drops 7 in 8 triangles after a
+// positions-only transform.  No global list and no same-address atomics (the counts of the dropped
+// trivially inside triangles go into the block's blk_stat slot): a separate pre-pass kernel with a
+// global list reservation and per-wave statistic atomics took 114 us for C4's 1M triangles.
+constexpr int CULL_PER = 4;
 
-__global__ __launch_bounds__(256) void k_lib_shard_cull(LibFrameParams fp, LibBuffers fb) {
-    __shared__ uint32_t s_wave[4], s_base;
-    uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t n_clip = 0u, n_rast = 0u;
-    const int span = 256 * PRE_PER;
-    for (int base = (int)blockIdx.x * span; base < fp.n_tris; base += (int)gridDim.x * span) {   // block-uniform
-        bool keep_k[PRE_PER];
-        int d_k[PRE_PER];
-#pragma unroll
-        for (int k = 0; k < PRE_PER; ++k) {
-            const int tri = base + 256 * k + tid;
-            const int c = (base >> 8) + k;   // this 256-triangle chunk = setup block c (its bdraw entry)
-            bool keep = false;
-            int d = 0;
-            if (tri < fp.n_tris) {
-                const int t_last = min(c * 256 + 255, fp.n_tris - 1);
-                const int d_first = fb.bdraw[c];
-                d = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : lib_find_draw(fb.dbase, fp.n_draws, tri);
-                const LibDrawGPU &dr = fb.draws[d];
-                uint32_t id[3];
-                if (read_tri(dr, tri - dr.tri_base, id)) {
-                    LVert t[3];
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) t[q] = vertex_pos(dr, id[q]);
-                    if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
-                        float sx[3], sy[3], den;
-                        int x0, x1, y0, y1;
-                        uint32_t nr = 0u;
-                        keep = fan_screen(fp, dr, t[0], t[1], t[2], sx, sy, x0, x1, y0, y1, den, nr);
-                        if (!keep) { ++n_clip; n_rast += nr; }   // emit_fan's counts for fan 0
-                    } else {
-                        keep = clip_reaches_rank(fp, t);
-                    }
-                }
-            }
-            keep_k[k] = keep;
-            d_k[k] = d;
-        }
-        // one reservation per block and pass (a single list counter: per-wave atomics would queue on it)
-        uint32_t mine = 0u;
-#pragma unroll
-        for (int k = 0; k < PRE_PER; ++k) mine += keep_k[k] ? 1u : 0u;
-        uint32_t incl = mine;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
-            if (lane >= o) incl += v;
-        }
-        if (lane == 63) s_wave[wave] = incl;
-        __syncthreads();
-        uint32_t wbase = 0u, total = 0u;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            wbase += w < wave ? s_wave[w] : 0u;
-            total += s_wave[w];
-        }
-        if (tid == 0) s_base = total ? atomicAdd(&cnt[LC_LIST], total) : 0u;
-        __syncthreads();
-        uint32_t at = s_base + wbase + incl - mine;
-#pragma unroll
-        for (int k = 0; k < PRE_PER; ++k)
-            if (keep_k[k]) fb.tri_list[at++] = make_uint2((uint32_t)(base + 256 * k + tid), (uint32_t)d_k[k]);
-        __syncthreads();   // s_wave / s_base reused by the next pass
+// The tile-sharded front end's decision for one input triangle (clip-space corners t): would k_lib_setup
+// keep it on this rank?  The dropped trivially inside ones count like emit_fan's fan 0.
+__device__ __forceinline__ bool cull_keep(const LibFrameParams &fp, const LibDrawGPU &dr, const LVert (&t)[3],
+                                          uint32_t &pre_clip, uint32_t &pre_rast) {
+    if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
+        float sx[3], sy[3], den;
+        int x0, x1, y0, y1;
+        uint32_t nr = 0u;
+        const bool keep = fan_screen(fp, dr, t[0], t[1], t[2], sx, sy, x0, x1, y0, y1, den, nr);
+        if (!keep) { ++pre_clip; pre_rast += nr; }
+        return keep;
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        n_clip += __shfl_down(n_clip, o);
-        n_rast += __shfl_down(n_rast, o);
-    }
-    if (__lane_id() == 0 && (n_clip | n_rast)) {
-        atomicAdd(&cnt[LC_PCLIP], n_clip);
-        atomicAdd(&cnt[LC_PRAST], n_rast);
-    }
+    return clip_reaches_rank(fp, t);
 }
 
 template <bool SHADOW, bool LISTED = false>
 __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     __shared__ SetupShared ss;
+    constexpr bool listed = !SHADOW && LISTED;
+    __shared__ uint2 s_kept[listed ? 256 * CULL_PER : 1];   // (triangle, draw)
+    __shared__ uint32_t s_nkept;
     const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
     const bool stl = fb.stimeline != nullptr && tid == 0;
     const uint64_t st0 = stl ? tl_now() : 0ull;
+    if (listed && tid == 0) s_nkept = 0u;
     setup_prologue(fp, fb, ss, b, tid);
-    // the triangles: b * 256 + tid (one chunk per block), or (tile-sharded camera pass) k_lib_shard_cull's
-    // list, 256 entries per chunk, the grid striding it
-    constexpr bool listed = !SHADOW && LISTED;
-    const int n_items = listed ? (int)cnt[LC_LIST] : fp.n_tris;
+    // the triangles: b * 256 + tid (one chunk per block), or (tile-sharded camera pass) the block's kept
+    // triangles of its CULL_PER x 256 inputs, 256 per round
+    uint32_t pre_clip = 0u, pre_rast = 0u;
+    uint64_t stf = 0ull;
+    int n_items = 256;
+    if constexpr (listed) {
+        const int lane = tid & 63;
+        const int base = b * 256 * CULL_PER;
+        const int t_end = min(base + 256 * CULL_PER, fp.n_tris) - 1;
+        bool keep_k[CULL_PER];
+        int d_k[CULL_PER];
+        const int d_first = fb.bdraw[base >> 8];
+        if (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_end) {   // block-uniform: one draw
+            // scalar draw uniforms; every index load of the CULL_PER triangles issued, then every
+            // position load, then the math (two memory round trips instead of one chain per triangle)
+            const LibDrawGPU &dr = fb.draws[d_first];
+            uint32_t id[CULL_PER][3];
+            bool ok[CULL_PER];
+#pragma unroll
+            for (int k = 0; k < CULL_PER; ++k) {
+                const int tri = base + 256 * k + tid;
+                ok[k] = read_tri(dr, min(tri, t_end) - dr.tri_base, id[k]) && tri <= t_end;
+            }
+            float P[CULL_PER][3][3];
+#pragma unroll
+            for (int k = 0; k < CULL_PER; ++k)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const float *pp = dr.pos + 3 * (size_t)(ok[k] ? id[k][q] : 0u);
+                    P[k][q][0] = pp[0]; P[k][q][1] = pp[1]; P[k][q][2] = pp[2];
+                }
+#pragma unroll
+            for (int k = 0; k < CULL_PER; ++k) {
+                LVert t[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) t[q] = vertex_pos_xyz(dr, P[k][q][0], P[k][q][1], P[k][q][2]);
+                keep_k[k] = ok[k] && cull_keep(fp, dr, t, pre_clip, pre_rast);
+                d_k[k] = d_first;
+            }
+        } else {   // the span straddles draws: per-lane draw search
+#pragma unroll
+            for (int k = 0; k < CULL_PER; ++k) {
+                const int tri = base + 256 * k + tid;
+                bool keep = false;
+                int d = 0;
+                if (tri <= t_end) {
+                    d = lib_find_draw(fb.dbase, fp.n_draws, tri);
+                    const LibDrawGPU &dr = fb.draws[d];
+                    uint32_t id[3];
+                    if (read_tri(dr, tri - dr.tri_base, id)) {
+                        LVert t[3];
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) t[q] = vertex_pos(dr, id[q]);
+                        keep = cull_keep(fp, dr, t, pre_clip, pre_rast);
+                    }
+                }
+                keep_k[k] = keep;
+                d_k[k] = d;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CULL_PER; ++k) {   // one LDS atomic per wave and triangle round
+            const uint64_t m = __ballot(keep_k[k]);
+            if (m == 0ull) continue;
+            const int first = __ffsll((long long)m) - 1;
+            uint32_t at = 0u;
+            if (lane == first) at = atomicAdd(&s_nkept, (uint32_t)__popcll(m));
+            at = (uint32_t)__shfl((int)at, first);
+            if (keep_k[k]) s_kept[at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = make_uint2((uint32_t)(base + 256 * k + tid), (uint32_t)d_k[k]);
+        }
+        __syncthreads();
+        n_items = (int)s_nkept;
+        if (stl) stf = tl_now();
+        if (fp.exp_flags & 8u) n_items = 0;
+    }
     uint32_t acc_clip = 0u, acc_rast = 0u, nbig = 0u;
     uint64_t st1 = 0ull, st2 = 0ull;
     int uwh = 0;
-    for (int chunk = b; chunk == b || chunk * 256 < n_items; chunk += (int)gridDim.x) {   // block-uniform
-        if (chunk != b) {
-            __syncthreads();   // the previous chunk's LDS state is consumed
+    for (int round = 0; round == 0 || round * 256 < n_items; ++round) {   // block-uniform
+        if (round != 0) {
+            __syncthreads();   // the previous round's LDS state is consumed
             setup_shared_init(ss, tid);
             __syncthreads();
         }
-        int tri = chunk * 256 + tid;
-        uint32_t n_clip = 0, n_rast = 0;
+        int tri = b * 256 + tid;
+        uint32_t n_clip = round == 0 ? pre_clip : 0u, n_rast = round == 0 ? pre_rast : 0u;
         Pend pend;
         bool need_clip = false;
         if constexpr (listed) {
-            const bool act = tri < n_items;
+            const int i = round * 256 + tid;
+            const bool act = i < n_items;
             uint2 e = make_uint2(0u, 0u);
-            if (act) e = fb.tri_list[tri];
+            if (act) e = s_kept[i];
             tri = act ? (int)e.x : -1;
             const int d = (int)e.y;
             const int d0 = __builtin_amdgcn_readfirstlane(d);
@@ -896,8 +924,8 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
         } else if (tri < fp.n_tris) {
             // the block's draw when all its triangles share one (block-uniform: its uniforms come in
             // through scalar loads), else -1 and a per-thread search
-            const int t_last = min(chunk * 256 + 255, fp.n_tris - 1);
-            const int d_first = fb.bdraw[chunk];
+            const int t_last = min(b * 256 + 255, fp.n_tris - 1);
+            const int d_first = fb.bdraw[b];
             const int d_uni = (d_first + 1 >= fp.n_draws || fb.dbase[d_first + 1] > t_last) ? d_first : -1;
             if (d_uni >= 0) {   // two inlined copies: this one sees d_uni as the (scalar) draw
                 if (SHADOW) setup_shadow_tri(fp, fb, cnt, tri, n_rast, ss, pend, d_uni);
@@ -923,6 +951,7 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
         if (tid == 0) {
             uint64_t *o = fb.stimeline + (size_t)b * STL_STRIDE;
             o[0] = st0; o[1] = st1; o[2] = st2; o[3] = tl_now(); o[4] = nbig; o[5] = (uint64_t)uwh;
+            o[6] = stf; o[7] = listed ? (uint64_t)n_items : 0ull;
         }
     }
 }
@@ -2076,15 +2105,18 @@ using namespace shs_dev;
 // k_lib_setup, then (camera pass) k_lib_clip over the queued triangles, then the large primitives'
 // marks (k_lib_bigmark).  The queue lengths stay on the device: the later kernels'
 // grids are fixed and stride or split what the counters hold.
-hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, int setup_grid, hipStream_t s) {
-    const int grid = std::max(1, (fp.n_tris + 255) / 256);
+int lib_setup_grid(int n_tris, bool listed) {
+    const int span = listed ? 256 * CULL_PER : 256;
+    return std::max(1, (n_tris + span - 1) / span);
+}
+
+hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, bool listed, hipStream_t s) {
+    const int grid = lib_setup_grid(fp.n_tris, listed && !shadow);
     if (shadow) {
         hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     } else {
-        if (fb.tri_list) {   // tile-sharded: the rank's triangles first, then a grid striding that list
-            hipLaunchKernelGGL(k_lib_shard_cull, dim3(std::max(1, (fp.n_tris + 256 * PRE_PER - 1) / (256 * PRE_PER))), dim3(256),
-                               0, s, fp, fb);
-            hipLaunchKernelGGL((k_lib_setup<false, true>), dim3(std::max(1, std::min(setup_grid, grid))), dim3(256), 0, s, fp, fb);
+        if (listed) {   // tile-sharded: each workgroup culls CULL_PER x 256 triangles, then sets up the kept ones
+            hipLaunchKernelGGL((k_lib_setup<false, true>), dim3(grid), dim3(256), 0, s, fp, fb);
         } else {
             hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
         }

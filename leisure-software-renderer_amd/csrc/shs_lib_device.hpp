@@ -90,9 +90,8 @@ constexpr uint32_t LF_GRADIENT = 8u;    // PassPBRForward's no-sky background gr
 // atomicAdd hands an appender both bases and the queue's task prefix stays monotone; LC_N even keeps
 // the second parity set's word 8-B aligned.
 // LC_ITEMS: k_lib_plan's raster work items; LC_COVERED: camera-pass covered pixels (k_lib_resolve);
-// LC_LIST: k_lib_shard_cull's kept triangles, LC_PCLIP / LC_PRAST: the statistics of the ones it dropped.
 constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT = 4, LC_BIGQ = 5, LC_ITEMS = 6, LC_COVERED = 7,
-              LC_LIST = 8, LC_PCLIP = 9, LC_PRAST = 10, LC_N = 12;
+              LC_N = 8;
 static_assert(LC_BIGQ == LC_BIGT + 1 && LC_BIGT % 2 == 0 && LC_N % 2 == 0, "64-bit big-queue word");
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
@@ -107,7 +106,8 @@ struct LibFrameParams {
     uint32_t bin_cap, spill_cap, extra_cap;
     uint32_t parity, scan_mode;
     int32_t setup_blocks, n_owned_rt;
-    uint32_t exp_flags;              // timing experiments only (SHS_LIB_EXP; wrong images): 1 no shade, 2 no marks, 4 no recs
+    uint32_t exp_flags;              // timing experiments only (SHS_LIB_EXP; wrong images): 1 no shade, 2 no marks, 4 no recs,
+                                     // 8 tile-sharded setup: cull front end only
     int32_t sm_w, sm_h;              // shadow map sampled by the programs
     // Forward+ program: the light lists of the last shs_light_cull
     uint32_t lt_size, lt_tx, lt_ty, lt_maxp, lt_mode, lt_zs, n_lights;
@@ -155,7 +155,6 @@ struct LibBuffers {
     float4 *uvw;                     // per slot, 2 float4: UV0 varying * 1/w of the 3 corners (textured draws)
     const float *srgb_lut;           // srgb_to_linear_rgb's 256 values, std::pow(c / 255.0f, 2.2f) on the host
     uint2 *items;                    // k_lib_plan: raster work items (rt_order position, part | parts << 16)
-    uint2 *tri_list;                 // tile-sharded camera pass: k_lib_shard_cull's kept (triangle, draw)
 };
 
 // k_lib_plan: at most this many parts per raster tile (capacity: LIB_MAXK * owned raster tiles).
@@ -166,8 +165,9 @@ constexpr int LIB_MAXK = 16;
 constexpr int LIB_NQ = 8, LIB_QSTRIDE = 32;
 
 // Library setup timeline slots: start, after the per-triangle work, after the deferred marks,
-// after the large-primitive marks (= end), large primitives, deferred-union width x height.
-constexpr int STL_STRIDE = 6;
+// after the large-primitive marks (= end), large primitives, deferred-union width x height, after the
+// tile-sharded cull front end (0 without it), kept triangles.
+constexpr int STL_STRIDE = 8;
 
 // Library raster timeline slots (s_memrealtime, 100 MHz ticks): per workgroup start, end, summed
 // phase ticks over its busy tiles (gather, stage + pairs, resolve + shade), clear ticks, counts.

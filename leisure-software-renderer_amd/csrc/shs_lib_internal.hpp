@@ -6,10 +6,11 @@
 
 namespace shs_internal {
 // shadow = true: PassShadowMap's depth pass; false: rasterize_mesh + builtin programs.
-// setup_grid: k_lib_setup's grid when fb.tri_list is set (tile-sharded camera pass: it strides the
-// k_lib_shard_cull list); otherwise one workgroup per 256 triangles.
-hipError_t launch_lib_setup(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, int setup_grid,
+// listed (tile-sharded camera pass): each setup workgroup culls CULL_PER x 256 triangles to the rank's
+// and sets up those (lib_setup_grid); otherwise one workgroup per 256 triangles.
+hipError_t launch_lib_setup(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, bool listed,
                             hipStream_t s);
+int lib_setup_grid(int n_tris, bool listed);
 // shallow: the 256-candidate-round k_lib_raster (every bin tile's list fits one gather round)
 int lib_raster_resident_blocks(int device, bool shadow, bool shallow);   // CUs x occupancy of k_lib_raster
 hipError_t launch_lib_raster(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, bool shadow, bool shallow,

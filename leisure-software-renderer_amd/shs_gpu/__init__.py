@@ -497,14 +497,15 @@ class Context:
         return out.reshape(-1, len(self.LIB_TIMELINE_FIELDS))
 
     def lib_debug_setup_timeline(self):
-        """Last camera pass's k_lib_setup workgroup timeline: uint64 [blocks, 6] (start, triangles done,
-        deferred marks done, end in 10-ns ticks; large primitives; deferred union w*h)."""
+        """Last camera pass's k_lib_setup workgroup timeline: uint64 [blocks, 8] (start, triangles done,
+        deferred marks done, end in 10-ns ticks; large primitives; deferred union w*h; tile-sharded cull
+        front end done (0 without it); kept triangles)."""
         n = ctypes.c_int64()
         self._check(self._lib.shs_lib_debug_setup_timeline(self._h, None, 0, ctypes.byref(n)))
         out = np.zeros(n.value, dtype=np.uint64)
         self._check(self._lib.shs_lib_debug_setup_timeline(self._h, out.ctypes.data_as(ctypes.c_void_p), n.value,
                                                            ctypes.byref(n)))
-        return out.reshape(-1, 6)
+        return out.reshape(-1, 8)
 
     def debug_timeline(self):
         """Last frame's workgroup timeline: (header dict, setup [n,2], raster [n,2]) in 10-ns ticks."""
@@ -522,11 +523,11 @@ class Context:
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_BIN_CAPACITY, int(cap)))
 
     def set_lib_part(self, part: int):
-        """Camera-pass raster work split (SHS_OPT_LIB_PART): -1 auto, 0 off, else the part size."""
+        """Camera-pass raster work split (SHS_OPT_LIB_PART): -1 auto (512 when sharded), 0 off (default), else the part size."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_LIB_PART, int(part)))
 
     def set_shard_cull(self, on: bool):
-        """SHS_OPT_SHARD_CULL: tile-sharded camera passes set up only the rank's triangles (default on)."""
+        """SHS_OPT_SHARD_CULL: tile-sharded camera passes set up only the rank's triangles (default off)."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_SHARD_CULL, 1 if on else 0))
 
     def set_overflow_capacities(self, spill: int = 0, frags: int = 0):

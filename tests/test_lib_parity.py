@@ -230,9 +230,9 @@ def test_shallow_raster_after_first_frame(oracle_mod):
 @pytest.mark.gpu
 @pytest.mark.parametrize("part", [16, 64, 512])
 def test_split_raster_items_exact(oracle_mod, part):
-    """SHS_OPT_LIB_PART: busy tiles with more bin entries than `part` are rendered as several parts on
-    different workgroups, merged by atomicMin -- the C4-like Forward+ frame (deep bins) and the C5
-    frame must stay bit-identical to the oracle (depth) / within 1e-5 (HDR), sharded and not."""
+    """SHS_OPT_LIB_PART: busy tiles with more bin entries than `part` are rendered as spatial parts
+    (32x4 halves / 16x4 blocks) on different workgroups -- the C4-like Forward+ frame (deep bins) must
+    stay bit-identical to the oracle (depth) / within 1e-5 (HDR)."""
     import shs_gpu
     from shs_gpu import scene_lib
     from helpers import assert_depth_bitexact, assert_float_close

@@ -1,6 +1,7 @@
 """Per-rank work of the tile-sharded C4 / C5 frame, measured on ONE GPU by rendering each rank's shard
 in turn (shard_rank / shard_count): the Amdahl inputs for the N-GPU projection.
-usage (GPU box): python tools/exp_shard_split.py [c4|c5] [frames] [N list, e.g. 1,2,4,8]"""
+usage (GPU box): python tools/exp_shard_split.py [c4|c5] [frames] [N list, e.g. 1,2,4,8]
+(env SPLIT_CULL=0|1: SHS_OPT_SHARD_CULL, SPLIT_PART=-1|0|n: SHS_OPT_LIB_PART)"""
 import os
 import sys
 import time
@@ -18,6 +19,10 @@ def main():
     nf = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     ns = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 2, 4, 8]
     ctx = shs_gpu.Context(0)
+    if os.environ.get("SPLIT_CULL") is not None:
+        ctx.set_shard_cull(os.environ["SPLIT_CULL"] == "1")
+    if os.environ.get("SPLIT_PART") is not None:
+        ctx.set_lib_part(int(os.environ["SPLIT_PART"]))
     if cfg == "c4":
         frame, draws, lights, cull = scene_lib.c4_scene(3840, 2160)
         ctx.upload_lights(lights)

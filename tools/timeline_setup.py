@@ -33,7 +33,7 @@ def main():
     ctx.synchronize_lib()
     ctx.render_pbr_forward_prepared(prep)
     ctx.synchronize_lib()
-    t = ctx.lib_debug_setup_timeline().reshape(-1, 6).astype(np.int64)
+    t = ctx.lib_debug_setup_timeline().reshape(-1, 8).astype(np.int64)
     t = t[t[:, 0] != 0]   # a listed (tile-sharded) setup runs fewer workgroups than setup blocks
     t0 = t[:, 0].min()
     span = (t[:, 3].max() - t0) / 100.0
@@ -46,6 +46,10 @@ def main():
     for name, v in (("triangles", tri), ("deferred marks", dfr), ("large prims", big), ("total", tri + dfr + big)):
         print(f"  {name:15s} p50 {np.median(v):7.2f}  p90 {np.percentile(v, 90):7.2f}  max {v.max():7.2f} us")
     print(f"  large prims per block: mean {t[:, 4].mean():.1f} max {t[:, 4].max()}; union w*h mean {t[:, 5].mean():.1f}")
+    if t[:, 6].any():
+        fe = (t[:, 6] - t[:, 0]) / 100.0
+        print(f"  cull front end  p50 {np.median(fe):7.2f}  p90 {np.percentile(fe, 90):7.2f}  max {fe.max():7.2f} us; "
+              f"kept per block mean {t[:, 7].mean():.1f} max {t[:, 7].max()}")
     w = np.argmax(tri + dfr + big)
     print(f"  slowest block {w}: start {start[w]:.1f} tri {tri[w]:.1f} deferred {dfr[w]:.1f} big {big[w]:.1f} us, "
           f"nbig {t[w, 4]}")
