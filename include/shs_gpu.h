@@ -198,7 +198,26 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * every rank sets up every triangle, dropping the ones off its tiles after the transform.  Results
  * identical. */
 #define SHS_OPT_SHARD_CULL 8
+/* SHS_OPT_SHARD_LAYOUT: which 32x32 bin tiles a tile-sharded library frame's rank owns.
+ * SHS_SHARD_INTERLEAVED (default): tile % count == rank.  SHS_SHARD_REGIONS: one rectangle per rank,
+ * from a recursive bisection of the bin grid at equal predicted cost, predicted from the context's
+ * previous camera pass (the bin-tile bounds of its 256-triangle setup blocks; the first pass, or one
+ * after a resize, splits by pixels).  Every rank derives the same rectangles from the same frames, with
+ * no exchange; a rank then skips whole setup blocks whose bounds miss its rectangle.  Applies to
+ * shs_light_cull, shs_render_pbr_forward, shs_tonemap and shs_tiles_* of sharded library frames (the
+ * legacy path stays interleaved).  Images identical; a region-sharded pass's statistics count only the
+ * setup blocks that reach the rank. */
+#define SHS_OPT_SHARD_LAYOUT 9
+#define SHS_SHARD_INTERLEAVED 0
+#define SHS_SHARD_REGIONS 1
+/* SHS_OPT_SHARD_ROOT_SHARE: rank 0's share of a region layout's predicted cost, in permille of the other
+ * ranks' (default 1000).  Rank 0 also unpacks every peer's tiles of the gathered frame; a smaller share
+ * leaves it room for that.  Every rank must use the same value. */
+#define SHS_OPT_SHARD_ROOT_SHARE 10
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
+/* The regions of the last region-sharded camera pass: rects[4 r .. 4 r + 3] = (bx0, by0, bx1, by1) of
+ * rank r, bin tiles, inclusive (bx1 < bx0: rank r owns nothing). */
+int shs_get_shard_regions(shs_ctx *ctx, int32_t shard_count, int32_t *rects);
 
 /* Debug / profiling hook: the last frame's workgroup timeline.  out[0..7] = {k_setup grid, k_raster
  * grid, setup blocks, ghost blocks, clear blocks, stride S, 0, 0} (k_setup's block roles in that
@@ -397,7 +416,7 @@ int shs_light_bin_culling(shs_ctx *ctx, const shs_light_bin_desc *desc, const fl
 
 /* ---- multi-GPU tile shards -------------------------------------------------------
  * A frame rendered with shard_rank / shard_count holds only its own 32x32 tiles (tile % count ==
- * rank).  shs_tiles_pack writes them into a caller-owned DEVICE buffer (e.g. a torch tensor on the
+ * rank, or its region: SHS_OPT_SHARD_LAYOUT).  shs_tiles_pack writes them into a caller-owned DEVICE buffer (e.g. a torch tensor on the
  * context's device) -- one 32x32-padded block per owned tile, planes colour / depth / motion --
  * for an RCCL gather; rank 0 calls shs_tiles_unpack once per peer to compose the full frame.  Both
  * are enqueued on the context stream (see shs_set_stream). */
@@ -405,7 +424,9 @@ int shs_light_bin_culling(shs_ctx *ctx, const shs_light_bin_desc *desc, const fl
 #define SHS_TARGET_LIB 1      /* library frame: RGBA32F HDR (+ depth + motion)           */
 #define SHS_TARGET_PRESENT 2  /* legacy SDL staging (SHS_FRAME_PRESENT): RGBA8, 4 B/px    */
 #define SHS_TARGET_LIB_PRESENT 3 /* tonemap present staging (SHS_TONEMAP_PRESENT): RGBA8  */
-int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t shard_count, int64_t *words_per_rank);
+int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t shard_count, int64_t *words_per_rank);   /* the largest rank's */
+/* The packed size of one rank's tiles (regions differ in size). */
+int shs_tiles_rank_words(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, int64_t *words);
 /* shs_tiles_pack first makes the frame final: it waits for the frame's setup (not its raster) and,
  * if a capacity overflowed, re-issues it; the pack is then enqueued on the context stream behind it,
  * so the packed tiles are final without a host wait for the render. */
@@ -582,6 +603,8 @@ int shs_group_mesh_upload(shs_group *g, const float *positions, int32_t n_verts,
 int shs_group_mesh_upload_soup(shs_group *g, const float *positions, const float *normals, int32_t n_tris, int32_t *mesh_id);
 int shs_group_texture_upload(shs_group *g, const uint8_t *rgba, int32_t w, int32_t h, int32_t *tex_id);
 int shs_group_lights_upload(shs_group *g, const shs_culling_light *lights, int32_t n_lights);
+/* shs_set_option on every rank's context (e.g. SHS_OPT_SHARD_LAYOUT). */
+int shs_group_set_option(shs_group *g, int option, int64_t value);
 int shs_group_lib_fuse_tonemap(shs_group *g, const shs_tonemap_desc *desc);
 /* Sharded passes: rank r runs the call with shard_rank = r, shard_count = n (the frame's own shard
  * fields are ignored).  The shadow map is rendered whole on every rank (every rank's PCF reads all of it). */

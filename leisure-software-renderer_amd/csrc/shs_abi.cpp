@@ -81,6 +81,7 @@ int shs_destroy(shs_ctx *ctx) {
         if (m.nrm) (void)hipFree(m.nrm);
         if (m.uv) (void)hipFree(m.uv);
         if (m.idx) (void)hipFree(m.idx);
+        if (m.cbox) (void)hipFree(m.cbox);
     }
     shs_lib_release(ctx);
     for (auto &w : ctx->lslot) {
@@ -144,6 +145,7 @@ int shs_mesh_release(shs_ctx *ctx, int32_t id) {
     HIP_TRY(ctx, hipFree(m.nrm));
     if (m.uv) HIP_TRY(ctx, hipFree(m.uv));
     if (m.idx) HIP_TRY(ctx, hipFree(m.idx));
+    if (m.cbox) HIP_TRY(ctx, hipFree(m.cbox));
     m = Mesh{};
     return SHS_OK;
 }
@@ -703,6 +705,18 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
     if (option == SHS_OPT_SHARD_CULL) {
         if (value < 0 || value > 1) return SHS_ERR_INVALID;
         ctx->shard_cull = value != 0;
+        return SHS_OK;
+    }
+    if (option == SHS_OPT_SHARD_LAYOUT) {
+        if (value != SHS_SHARD_INTERLEAVED && value != SHS_SHARD_REGIONS) return SHS_ERR_INVALID;
+        ctx->shard_layout = (int)value;
+        ctx->reg_next_fresh = false;
+        return SHS_OK;
+    }
+    if (option == SHS_OPT_SHARD_ROOT_SHARE) {
+        if (value < 0 || value > 1000) return SHS_ERR_INVALID;
+        ctx->shard_root_permille = (int)value;
+        ctx->reg_next_fresh = false;
         return SHS_OK;
     }
     if (option == SHS_OPT_LIB_PART) {

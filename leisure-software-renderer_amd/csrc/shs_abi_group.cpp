@@ -258,6 +258,11 @@ int shs_group_texture_upload(shs_group *g, const uint8_t *rgba, int32_t w, int32
     return SHS_OK;
 }
 
+int shs_group_set_option(shs_group *g, int option, int64_t value) {
+    if (!g) return SHS_ERR_INVALID;
+    return for_ranks(g, [&](int, shs_ctx *c) { return shs_set_option(c, option, value); });
+}
+
 int shs_group_lights_upload(shs_group *g, const shs_culling_light *lights, int32_t n_lights) {
     if (!g) return SHS_ERR_INVALID;
     return for_ranks(g, [&](int, shs_ctx *c) { return shs_lights_upload(c, lights, n_lights); });
@@ -330,9 +335,12 @@ int shs_group_gather(shs_group *g, int target) {
         shs_group::Link &l = g->links[r];
         int e = shs_tiles_pack(c, target, r, n, l.send);
         if (e) return e;
+        int64_t mine = 0;   // this rank's packed size (regions differ)
+        e = shs_tiles_rank_words(c, target, r, n, &mine);
+        if (e) return e;
         HIP_TRY(c, hipSetDevice(g->dev[r]));
         if (l.consumed_valid[p]) HIP_TRY(c, hipStreamWaitEvent(c->stream, l.consumed[p], 0));
-        HIP_TRY(c, hipMemcpyPeerAsync(l.recv[p], g->dev[0], l.send, g->dev[r], l.bytes, c->stream));
+        if (mine > 0) HIP_TRY(c, hipMemcpyPeerAsync(l.recv[p], g->dev[0], l.send, g->dev[r], (size_t)mine * 4, c->stream));
         HIP_TRY(c, hipEventRecord(l.sent[p], c->stream));
         return SHS_OK;
     });

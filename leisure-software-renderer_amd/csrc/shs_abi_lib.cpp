@@ -56,12 +56,16 @@ void release_work(Work &w) {
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue); release(w.rt_order);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
     if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
     if (w.ov_after) (void)hipEventDestroy(w.ov_after);
     if (w.h_ov) (void)hipHostFree(const_cast<uint32_t *>(w.h_ov));
+    if (w.h_blkrect) (void)hipHostFree(w.h_blkrect);
+    w.h_blkrect = nullptr;
+    w.blkrect_cap = 0;
+    w.blkrect_valid = false;
     w.ov_after = nullptr;
     w.h_ov = nullptr;
     w.ov_valid = false;
@@ -80,6 +84,7 @@ void build_lib_draw(const shs_lib_draw &in, const Mesh &m, int32_t base, LibDraw
     using namespace shs_host;
     std::memset(&o, 0, sizeof o);
     o.pos = m.pos; o.nrm = m.nrm; o.uv = m.uv; o.idx = m.idx;
+    o.cbox = m.cbox;
     o.n_verts = m.n_verts;
     o.tri_base = base;
     o.n_tris = m.n_tris;
@@ -172,7 +177,9 @@ int upload_draws(shs_ctx *ctx, Work &w, const std::vector<LibDrawGPU> &d, hipStr
 // supertiles dealt over the 8 XCDs; an XCD's positions walk its supertiles in order, the 4 raster
 // rows of a bin tile together.  A primitive's tiles, and a bin tile's 4 rows sharing one bin list,
 // then mostly land in one L2 instead of up to eight.  st = 0: the plain order (bin tile, row).
-std::vector<int32_t> build_rt_order(int tiles_x, int tiles_y, int rtiles_y, int rank, int count, int st) {
+std::vector<int32_t> build_rt_order(int tiles_x, int tiles_y, int rtiles_y, int rank, int count, const shs_dev::ShardRegion &reg,
+                                    int st) {
+    auto owned = [&](int t) { return shs_dev::shard_owned(rank, count, reg, t % tiles_x, t / tiles_x, tiles_x); };
     constexpr int RPB = shs_dev::TILE / 8;   // raster rows per bin tile
     std::vector<int32_t> out;
     auto push_bt = [&](std::vector<int32_t> &v, int t) {
@@ -183,7 +190,8 @@ std::vector<int32_t> build_rt_order(int tiles_x, int tiles_y, int rtiles_y, int 
         }
     };
     if (st <= 0) {
-        for (int t = rank; t < tiles_x * tiles_y; t += count) push_bt(out, t);
+        for (int t = 0; t < tiles_x * tiles_y; ++t)
+            if (owned(t)) push_bt(out, t);
         return out;
     }
     const int nsx = (tiles_x + st - 1) / st, nsy = (tiles_y + st - 1) / st;
@@ -194,7 +202,7 @@ std::vector<int32_t> build_rt_order(int tiles_x, int tiles_y, int rtiles_y, int 
             for (int by = sy * st; by < std::min(tiles_y, (sy + 1) * st); ++by)
                 for (int bx = sx * st; bx < std::min(tiles_x, (sx + 1) * st); ++bx) {
                     const int t = by * tiles_x + bx;
-                    if (t % count == rank) push_bt(v, t);
+                    if (owned(t)) push_bt(v, t);
                 }
         }
     size_t longest = 0;
@@ -203,6 +211,41 @@ std::vector<int32_t> build_rt_order(int tiles_x, int tiles_y, int rtiles_y, int 
         for (int x = 0; x < 8; ++x)
             if (m < lists[x].size()) out.push_back(lists[x][m]);
     return out;
+}
+
+// A device table (raster tile order, owned light lists) for a 4-word key, built and uploaded once into
+// its own buffer: a synchronous copy into fresh memory waits for no stream, so a changed shard layout
+// costs no pipeline drain.  Past ORDER_CACHE entries the cache is dropped (after the streams drain).
+constexpr size_t ORDER_CACHE = 48;
+
+template <typename Build>
+int order_lookup(shs_ctx *ctx, std::vector<shs_ctx::OrderEntry> &cache, const uint64_t (&key)[4], Build build,
+                 const shs_ctx::OrderEntry *&out) {
+    for (const auto &e : cache)
+        if (std::memcmp(e.key, key, sizeof key) == 0) { out = &e; return SHS_OK; }
+    if (cache.size() >= ORDER_CACHE) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
+        for (auto &e : cache) (void)hipFree(e.dev);
+        cache.clear();
+    }
+    std::vector<int32_t> v;
+    int n_owned = 0;
+    build(v, n_owned);
+    shs_ctx::OrderEntry e;
+    std::memcpy(e.key, key, sizeof key);
+    e.n = (int)v.size();
+    e.n_owned = n_owned;
+    HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&e.dev), std::max<size_t>(v.size(), 1) * sizeof(int32_t)));
+    if (!v.empty()) HIP_TRY(ctx, hipMemcpy(e.dev, v.data(), v.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    cache.push_back(e);
+    out = &cache.back();
+    return SHS_OK;
+}
+
+uint64_t region_key(const shs_dev::ShardRegion &g) {
+    return (uint64_t)(uint16_t)g.x0 | ((uint64_t)(uint16_t)g.y0 << 16) | ((uint64_t)(uint16_t)g.x1 << 32) |
+           ((uint64_t)(uint16_t)g.y1 << 48);
 }
 
 // Enqueue one pass (w.last_fp / w.last_draws describe it): workspace sizing, draw upload, the two
@@ -253,8 +296,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots)) return SHS_ERR_HIP;
     int st = 2;   // supertile edge in bin tiles (SHS_LIB_XCD_ST: timing experiments; 0 = plain order)
     if (const char *e = std::getenv("SHS_LIB_XCD_ST")) st = (int)std::strtol(e, nullptr, 0);
-    const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)fp.rank << 16) ^ (uint64_t)fp.count ^
-                          ((uint64_t)(st & 0xff) << 56);
+    const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32);
     // rtiles_y too: a height change inside the same bin-tile rows changes the raster-tile rows
     bool reset = gkey != w.geom_key || rtiles_y != w.geom_rtiles_y;
     if (w.tile_count.cap < 2 * (size_t)n_tiles || !w.tile_count.p) {
@@ -275,15 +317,22 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         HIP_TRY(ctx, hipMemsetAsync(w.busy.p, 0, w.busy.cap * sizeof(uint32_t), ps));
         HIP_TRY(ctx, hipMemsetAsync(w.counters.p, 0, w.counters.cap * sizeof(uint32_t), ps));
         HIP_TRY(ctx, hipMemsetAsync(w.rqueue.p, 0, w.rqueue.cap * sizeof(uint32_t), ps));
-        // the previous order's upload (on either stream) is done with h_rt_order
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
-        w.h_rt_order = build_rt_order(tiles_x, tiles_y, rtiles_y, fp.rank, fp.count, st);
-        if (ensure(ctx, w.rt_order, std::max<size_t>(w.h_rt_order.size(), 1))) return SHS_ERR_HIP;
-        HIP_TRY(ctx, hipMemcpyAsync(w.rt_order.p, w.h_rt_order.data(), w.h_rt_order.size() * sizeof(int32_t),
-                                    hipMemcpyHostToDevice, ps));
         w.geom_key = gkey;
         w.geom_rtiles_y = rtiles_y;
+    }
+    const shs_ctx::OrderEntry *order = nullptr;
+    {   // the raster tile order of this geometry and ownership
+        const shs_dev::ShardRegion reg = fp.count > 1 ? fp.reg : shs_dev::ShardRegion{0, 0, 0, 0, 0};
+        const int rank = fp.count > 1 ? fp.rank : 0, count = std::max(fp.count, 1);
+        const uint64_t key[4] = {(uint64_t)tiles_x | ((uint64_t)tiles_y << 16) | ((uint64_t)rtiles_y << 32) | ((uint64_t)(st & 0xff) << 56),
+                                 (uint64_t)(uint32_t)rank | ((uint64_t)(uint32_t)count << 32), region_key(reg), (uint64_t)reg.on};
+        if (order_lookup(ctx, ctx->rt_orders, key,
+                         [&](std::vector<int32_t> &v, int &n_owned) {
+                             v = build_rt_order(tiles_x, tiles_y, rtiles_y, rank, count, reg, st);
+                             n_owned = (int)v.size();
+                         },
+                         order))
+            return SHS_ERR_HIP;
     }
     if (ensure(ctx, w.bins, (size_t)n_tiles * w.bin_cap)) return SHS_ERR_HIP;
     if (!w.spill.p && ensure(ctx, w.spill, 1 << 16)) return SHS_ERR_HIP;
@@ -324,7 +373,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         const char *e = std::getenv("SHS_LIB_EXP");   // timing experiments only: parts of the setup skipped
         fp.exp_flags = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
     }
-    fp.n_owned_rt = (int)w.h_rt_order.size();
+    fp.n_owned_rt = order->n;
     // Camera pass, tile-sharded: k_lib_plan splits the busy tiles whose bin list is longer than `part`
     // entries into parts rendered by several workgroups (SHS_OPT_LIB_PART: -1 auto = 512 when sharded,
     // 0 = off, else the part size for every camera pass).
@@ -355,9 +404,29 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.items = fp.part ? w.items.p : nullptr;
     // Tile-sharded camera pass in bin mode: each setup workgroup first keeps the rank's triangles of its
     // inputs, positions only (SHS_OPT_SHARD_CULL 0: off).
-    const bool listed = !shadow && !fp.scan_mode && fp.count > 1 && ctx->shard_cull;
+    const bool listed = !shadow && !fp.scan_mode && fp.count > 1 && !fp.reg.on && ctx->shard_cull;
     const int setup_grid = shs_internal::lib_setup_grid(n_tris, listed);
-    fb.rt_order = w.rt_order.p;
+    fb.rt_order = order->dev;
+    if (!shadow && fp.count > 1 && fp.reg.on) {
+        // region-sharded camera pass: per setup block its chunk bounds, into mapped host memory (the
+        // next pass's region balance reads them once this pass's setup is done)
+        if ((size_t)setup_blocks > w.blkrect_cap) {
+            if (w.h_blkrect) {
+                if (w.ov_valid) HIP_TRY(ctx, hipEventSynchronize(w.ov_after));
+                HIP_TRY(ctx, hipHostFree(w.h_blkrect));
+                w.h_blkrect = nullptr;
+            }
+            const size_t cap = std::max<size_t>((size_t)setup_blocks, 1024);
+            HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&w.h_blkrect), cap * sizeof(uint4),
+                                       hipHostMallocMapped | hipHostMallocCoherent));
+            w.blkrect_cap = cap;
+        }
+        fb.blkrect = w.h_blkrect;
+        w.blkrect_n = setup_blocks;
+        w.blkrect_w = W;
+        w.blkrect_h = H;
+        w.blkrect_valid = true;
+    }
     if (shadow) {
         fb.depth = ctx->shadow_map.p;
     } else {
@@ -540,12 +609,16 @@ int shs_lib_ensure_final(shs_ctx *ctx) {
 void shs_lib_release(shs_ctx *ctx) {
     release_work(ctx->lib_cam);
     release_work(ctx->lib_shadow);
+    for (auto *cache : {&ctx->rt_orders, &ctx->cull_orders}) {
+        for (auto &e : *cache) (void)hipFree(e.dev);
+        cache->clear();
+    }
     for (auto &t : ctx->textures)
         if (t.texels) (void)hipFree(t.texels);
     ctx->textures.clear();
     release(ctx->srgb_lut);
     release(ctx->lib_hdr); release(ctx->lib_keys); release(ctx->lib_blkcov); release(ctx->tm_thr_dev); ctx->tm_thr_dev_gamma = -1.0f; release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
-    release(ctx->lights); release(ctx->cull_work); release(ctx->depth_ranges);
+    release(ctx->lights); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
     release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
     release(ctx->lb_lights); release(ctx->lb_ndc); release(ctx->lb_counts); release(ctx->lb_indices);
@@ -599,6 +672,28 @@ int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const
         HIP_TRY(ctx, hipMemcpy(m.idx, indices, (size_t)n_tris * 3 * sizeof(uint32_t), hipMemcpyHostToDevice));
     } else if (indices) {
         m.n_tris = 0;
+    }
+    if (m.n_tris > 0) {   // chunk boxes (k_lib_setup's block bounds): out-of-range indices are skipped there
+        const int64_t n_chunks = ((int64_t)m.n_tris + 255) / 256;
+        std::vector<float4> cb((size_t)n_chunks * 2);
+        for (int64_t c = 0; c < n_chunks; ++c) {
+            float mn[3] = {3.402823466e38f, 3.402823466e38f, 3.402823466e38f}, mx[3] = {-3.402823466e38f, -3.402823466e38f, -3.402823466e38f};
+            const int64_t t1 = std::min<int64_t>(m.n_tris, (c + 1) * 256);
+            for (int64_t t = c * 256; t < t1; ++t)
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t v = indices ? indices[3 * t + k] : (uint32_t)(3 * t + k);
+                    if (v >= (uint32_t)n_verts) continue;
+                    for (int q = 0; q < 3; ++q) {
+                        const float p = positions[3 * (size_t)v + q];
+                        mn[q] = std::min(mn[q], p);
+                        mx[q] = std::max(mx[q], p);
+                    }
+                }
+            cb[2 * c] = make_float4(mn[0], mn[1], mn[2], 0.0f);
+            cb[2 * c + 1] = make_float4(mx[0], mx[1], mx[2], 0.0f);
+        }
+        HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.cbox), cb.size() * sizeof(float4)));
+        HIP_TRY(ctx, hipMemcpy(m.cbox, cb.data(), cb.size() * sizeof(float4), hipMemcpyHostToDevice));
     }
     m.live = true;
     ctx->meshes.push_back(m);
@@ -749,6 +844,11 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     std::memset(&fp, 0, sizeof fp);
     fp.W = f.width; fp.H = f.height;
     fp.rank = f.shard_rank; fp.count = f.shard_count;
+    const bool regions = f.shard_count > 1 && ctx->shard_layout == SHS_SHARD_REGIONS;
+    if (regions) {   // this rank's rectangle of the balanced layout (the pass's light cull used the same)
+        if (shs_regions_next(ctx, f.shard_count, f.width, f.height)) return SHS_ERR_HIP;
+        fp.reg = ctx->reg_next[(size_t)f.shard_rank];
+    }
     fp.flags = (f.flags & SHS_LIB_BG_GRADIENT) ? shs_dev::LF_GRADIENT : 0u;
     if (dm) {
         fp.flags |= shs_dev::LF_DEPTH | shs_dev::LF_MOTION;
@@ -771,6 +871,14 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     wk.tm_desc = ctx->tm_fuse_desc;
     const int rc = enqueue_pass(ctx, wk, false);
     if (rc) return rc;
+    if (regions) {   // the layout of this pass (tonemap, gather); the next pass balances anew
+        ctx->reg_last = ctx->reg_next;
+        ctx->reg_last_count = f.shard_count;
+        ctx->reg_next_fresh = false;
+    } else {
+        ctx->reg_last.clear();
+        ctx->reg_last_count = 0;
+    }
     ctx->have_lib_frame = true;
     // a new camera pass: a tonemap (and motion blur) must follow it again, unless it ran fused
     ctx->have_ldr = wk.tm_fused;
@@ -899,6 +1007,10 @@ int shs_light_cull(shs_ctx *ctx, const shs_light_cull_desc *d) {
     p.zn = d->zn; p.zf = d->zf;
     p.depth_linear = d->depth_linear;
     p.rank = d->shard_rank; p.count = d->shard_count;
+    if (p.count > 1 && ctx->shard_layout == SHS_SHARD_REGIONS) {   // the upcoming camera pass's rectangle
+        if (shs_regions_next(ctx, p.count, p.W, p.H)) return SHS_ERR_HIP;
+        p.reg = ctx->reg_next[(size_t)p.rank];
+    }
     std::memcpy(p.view, d->view, sizeof p.view);
     std::memcpy(p.proj, d->proj, sizeof p.proj);
     if (ensure(ctx, ctx->depth_ranges, (size_t)p.tiles_x * p.tiles_y) || ensure(ctx, ctx->list_counts, p.n_lists) ||
@@ -906,25 +1018,27 @@ int shs_light_cull(shs_ctx *ctx, const shs_light_cull_desc *d) {
         return SHS_ERR_HIP;
     const uint32_t *work = nullptr;
     uint32_t n_work = p.n_lists;
-    if (p.count > 1 && (32u % p.tile_size) == 0u) {   // tile-sharded: this rank's lists first
-        const shs_dev::LightCullParams &k = ctx->cull_work_key;
-        if (!ctx->cull_work.p || k.W != p.W || k.H != p.H || k.tile_size != p.tile_size || k.n_lists != p.n_lists ||
-            k.rank != p.rank || k.count != p.count) {
-            std::vector<uint32_t> mine, rest;
-            const uint32_t per_slice = p.tiles_x * p.tiles_y;
-            for (uint32_t l = 0; l < p.n_lists; ++l) {
-                const uint32_t rem = l % per_slice;
-                (shs_internal::light_list_owned(p, rem % p.tiles_x, rem / p.tiles_x) ? mine : rest).push_back(l);
-            }
-            ctx->cull_work_owned = (uint32_t)mine.size();
-            mine.insert(mine.end(), rest.begin(), rest.end());
-            if (ensure(ctx, ctx->cull_work, mine.size())) return SHS_ERR_HIP;
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // the previous table may still be read
-            HIP_TRY(ctx, hipMemcpy(ctx->cull_work.p, mine.data(), mine.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-            ctx->cull_work_key = p;
-        }
-        work = ctx->cull_work.p;
-        n_work = ctx->cull_work_owned;
+    if (p.count > 1 && (32u % p.tile_size) == 0u) {   // tile-sharded: this rank's lists first (cached table)
+        const shs_ctx::OrderEntry *e = nullptr;
+        const uint64_t key[4] = {(uint64_t)(uint32_t)p.W | ((uint64_t)(uint32_t)p.H << 32),
+                                 (uint64_t)p.tile_size | ((uint64_t)p.n_lists << 32),
+                                 (uint64_t)(uint32_t)p.rank | ((uint64_t)(uint32_t)p.count << 32),
+                                 p.reg.on ? region_key(p.reg) ^ (1ull << 63) : 0ull};
+        if (order_lookup(ctx, ctx->cull_orders, key,
+                         [&](std::vector<int32_t> &v, int &n_owned) {
+                             std::vector<int32_t> rest;
+                             const uint32_t per_slice = p.tiles_x * p.tiles_y;
+                             for (uint32_t l = 0; l < p.n_lists; ++l) {
+                                 const uint32_t rem = l % per_slice;
+                                 (shs_internal::light_list_owned(p, rem % p.tiles_x, rem / p.tiles_x) ? v : rest).push_back((int32_t)l);
+                             }
+                             n_owned = (int)v.size();
+                             v.insert(v.end(), rest.begin(), rest.end());
+                         },
+                         e))
+            return SHS_ERR_HIP;
+        work = reinterpret_cast<const uint32_t *>(e->dev);
+        n_work = (uint32_t)e->n_owned;
     }
     HIP_TRY(ctx, shs_internal::launch_light_cull(p, ctx->lights.p, ctx->lib_depth.p, ctx->depth_ranges.p, work, n_work,
                                                  ctx->list_counts.p, ctx->list_indices.p, ctx->stream));
@@ -952,6 +1066,9 @@ static int tile_params(shs_ctx *ctx, int target, int32_t rank, int32_t count, sh
     if (count <= 0 || rank < 0 || rank >= count) { ctx->err = "bad shard"; return SHS_ERR_INVALID; }
     p.rank = rank;
     p.count = count;
+    // a region-sharded library frame: rank's rectangle of the last camera pass's layout
+    if ((target == SHS_TARGET_LIB || target == SHS_TARGET_LIB_PRESENT) && count > 1 && ctx->reg_last_count == count)
+        p.reg = ctx->reg_last[(size_t)rank];
     if (target == SHS_TARGET_LEGACY) {
         if (!ctx->have_frame) { ctx->err = "no legacy frame rendered"; return SHS_ERR_INVALID; }
         p.W = ctx->frame.width; p.H = ctx->frame.height;
@@ -987,12 +1104,24 @@ static int tile_params(shs_ctx *ctx, int target, int32_t rank, int32_t count, sh
     return SHS_OK;
 }
 
-int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t count, int64_t *words_out) {
+int shs_tiles_rank_words(shs_ctx *ctx, int target, int32_t rank, int32_t count, int64_t *words_out) {
     if (!ctx || !words_out) return SHS_ERR_INVALID;
     shs_dev::TileCopyParams p;
-    if (tile_params(ctx, target, 0, count, p)) return SHS_ERR_INVALID;
-    const int64_t n_tiles = (int64_t)((p.W + 31) / 32) * ((p.H + 31) / 32);
-    *words_out = ((n_tiles + count - 1) / count) * 32 * 32 * p.words;
+    if (tile_params(ctx, target, rank, count, p)) return SHS_ERR_INVALID;
+    const int n_tiles = ((p.W + 31) / 32) * ((p.H + 31) / 32);
+    *words_out = (int64_t)shs_dev::shard_n_owned(rank, count, p.reg, n_tiles) * 32 * 32 * p.words;
+    return SHS_OK;
+}
+
+int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t count, int64_t *words_out) {
+    if (!ctx || !words_out) return SHS_ERR_INVALID;
+    int64_t most = 0;
+    for (int32_t r = 0; r < std::max(count, 1); ++r) {
+        int64_t w = 0;
+        if (shs_tiles_rank_words(ctx, target, r, count, &w)) return SHS_ERR_INVALID;
+        most = std::max(most, w);
+    }
+    *words_out = most;
     return SHS_OK;
 }
 

@@ -76,6 +76,7 @@ int enqueue_tonemap(shs_ctx *ctx) {
     // like the HDR target's)
     p.rank = ctx->lib_frame.shard_count > 1 ? ctx->lib_frame.shard_rank : 0;
     p.count = std::max(1, ctx->lib_frame.shard_count);
+    if (p.count > 1 && ctx->reg_last_count == p.count) p.reg = ctx->reg_last[(size_t)p.rank];
     p.exposure = std::max(0.0001f, d.exposure);
     p.inv_gamma = 1.0f / std::max(0.001f, d.gamma);
     std::memcpy(p.thr, ctx->tm_thr, sizeof p.thr);

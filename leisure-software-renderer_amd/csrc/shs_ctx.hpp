@@ -27,6 +27,7 @@ struct Mesh {
     uint32_t *idx = nullptr;
     int32_t n_verts = 0;
     float bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
+    float4 *cbox = nullptr;          // library mesh: per 256-triangle chunk its model-space box (min, max)
 };
 
 // A Texture2DData (resources/texture.hpp:23-49) on the device: w * h Color texels, y * w + x.
@@ -136,8 +137,6 @@ struct shs_ctx {
         DevBuf<uint32_t> xbase, zord, tile_count, bins, counters, busy, clipq, bigpre;
         DevBuf<uint4> bigq;
         DevBuf<uint32_t> rqueue;
-        DevBuf<int32_t> rt_order;                          // k_lib_raster tile order (built per geometry)
-        std::vector<int32_t> h_rt_order;                   // its host copy (alive while the upload runs)
         bool tm_fused = false;                             // camera pass: the fused tonemap of tm_desc
         hipEvent_t raster_ev = nullptr, resolve_ev = nullptr;   // camera pass: side-stream raster done, resolve done
         bool resolve_ev_valid = false;
@@ -167,6 +166,11 @@ struct shs_ctx {
         const shs_dev::LibDrawGPU *dev_table_at = nullptr;   // ... at this allocation (pointer, capacity)
         size_t dev_table_cap = 0;
         shs_dev::LibFrameParams last_fp{};
+        // camera pass: per setup block its chunk bounds (k_lib_setup, mapped host memory), final at ov_after
+        uint4 *h_blkrect = nullptr;
+        size_t blkrect_cap = 0;
+        int blkrect_n = 0, blkrect_w = 0, blkrect_h = 0;
+        bool blkrect_valid = false;
         // kernel timing (ctx->timing): events before k_lib_setup, between, after k_lib_raster
         static constexpr int RING = 64;
         hipEvent_t ring_ev[RING][3] = {};
@@ -178,6 +182,24 @@ struct shs_ctx {
     LibWork lib_cam, lib_shadow;
     int64_t lib_part = 0;                 // SHS_OPT_LIB_PART (off by default: measured)
     bool shard_cull = false;              // SHS_OPT_SHARD_CULL (off by default: measured)
+    int shard_layout = 0;                 // SHS_OPT_SHARD_LAYOUT: 0 interleaved tiles, 1 cost-balanced regions
+    // Region layout (shs_abi_shard.cpp): every rank's rectangle for the upcoming camera pass (computed
+    // once per pass from the previous camera pass's block bounds; its light cull uses the same) and for
+    // the last one (its tonemap and tile gather).
+    std::vector<shs_dev::ShardRegion> reg_next, reg_last;
+    int reg_next_count = 0, reg_next_w = 0, reg_next_h = 0, reg_last_count = 0;
+    bool reg_next_fresh = false;
+    int shard_root_permille = 1000;       // SHS_OPT_SHARD_ROOT_SHARE: rank 0's share of a region layout (it also unpacks)
+    std::vector<uint4> reg_in;            // the block bounds reg_next was last balanced from (identical: reused)
+    int reg_in_count = -1, reg_in_w = 0, reg_in_h = 0, reg_in_root = 0;
+    // Tile orders / owned-list tables by geometry + ownership, uploaded once into their own buffers (a
+    // changed region layout costs no stream synchronisation)
+    struct OrderEntry {
+        uint64_t key[4];
+        int32_t *dev;
+        int n, n_owned;
+    };
+    std::vector<OrderEntry> rt_orders, cull_orders;
     int lib_resident[2][2] = {{0, 0}, {0, 0}};   // resident k_lib_raster workgroups [camera, shadow][deep, shallow]
     DevBuf<uint64_t> lib_timeline;        // SHS_OPT_TIMELINE, camera pass raster
     DevBuf<uint64_t> lib_stimeline;       // SHS_OPT_TIMELINE, camera pass setup
@@ -197,9 +219,6 @@ struct shs_ctx {
     // Forward+ light lists (shs_light.hip)
     DevBuf<shs_dev::CullLight> lights;
     int32_t n_lights = 0;
-    DevBuf<uint32_t> cull_work;           // tile-sharded light cull: this rank's lists, then the rest
-    uint32_t cull_work_owned = 0;         // ... how many of them are this rank's
-    shs_dev::LightCullParams cull_work_key{};   // the list geometry / shard cull_work was built for
     DevBuf<float2> depth_ranges;
     DevBuf<uint32_t> list_counts, list_indices;
     shs_dev::LightCullParams cull{};
@@ -248,6 +267,13 @@ int shs_tonemap_reissue(shs_ctx *ctx);
 // the context stream afterwards sees the final frame (shs_abi.cpp: legacy; shs_abi_lib.cpp: library).
 int shs_legacy_ensure_final(shs_ctx *ctx);
 int shs_lib_ensure_final(shs_ctx *ctx);
+// Region layout (shs_abi_shard.cpp).  shs_shard_balance: `count` rectangles of the tiles_x x tiles_y bin
+// grid of a W x H frame with equal predicted cost, from n_blk setup-block bounds (null: pixels only).
+void shs_shard_balance(const uint4 *blk, int n_blk, int tiles_x, int tiles_y, int W, int H, int count,
+                       std::vector<shs_dev::ShardRegion> &out, double root_share = 1.0);
+// The regions of the next camera pass of a W x H frame over `count` ranks (ctx->reg_next), from the
+// last camera pass's block bounds when it had the same frame size (waits for its setup).
+int shs_regions_next(shs_ctx *ctx, int count, int w, int h);
 
 #define HIP_TRY(ctx, expr)                                                                       \
     do {                                                                                         \

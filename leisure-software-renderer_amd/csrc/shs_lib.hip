@@ -70,7 +70,7 @@ constexpr int LIB_CHUNK = 128;             // records staged in LDS per pass
 constexpr int MAX_POLY = 16;               // clipped polygon capacity (3 + 6 planes x up to 2 crossings)
 
 __device__ __forceinline__ bool lib_owned(const LibFrameParams &fp, int bx, int by) {
-    return ((by * fp.tiles_x + bx) % fp.count) == fp.rank;
+    return shard_owned(fp.rank, fp.count, fp.reg, bx, by, fp.tiles_x);
 }
 
 // Orderable key bits (z_key's high word) of a conservative lower bound of the depth lib_test can
@@ -419,10 +419,13 @@ __device__ __forceinline__ bool fan_screen(const LibFrameParams &fp, const LibDr
         }
     }
     if (live && fp.count > 1) {
-        // tile-sharded pass: a small primitive on no owned 32x32 tile is not needed on this rank
-        // (its record, varyings and marks are skipped; the frame counters still count it)
+        // tile-sharded pass: a small primitive (any primitive, region ownership) on no owned 32x32 tile
+        // is not needed on this rank (its record, varyings and marks are skipped; the frame counters
+        // still count it)
         const int tx0 = x0 / TILE, tx1 = x1 / TILE, ty0 = y0 / TILE, ty1 = y1 / TILE;
-        if ((tx1 - tx0) < 2 && (ty1 - ty0) < 2) {
+        if (fp.reg.on) {
+            live = shard_owns_any(fp.rank, fp.count, fp.reg, tx0, tx1, ty0, ty1, fp.tiles_x);
+        } else if ((tx1 - tx0) < 2 && (ty1 - ty0) < 2) {
             bool mine = false;
             for (int ty = ty0; ty <= ty1; ++ty)
                 for (int tx = tx0; tx <= tx1; ++tx) mine = mine || lib_owned(fp, tx, ty);
@@ -528,11 +531,8 @@ __device__ __forceinline__ bool clip_reaches_rank(const LibFrameParams &fp, cons
     if (!(x1 >= -2.0f && y1 >= -2.0f && x0 <= (float)fp.W + 1.0f && y0 <= (float)fp.H + 1.0f)) return false;  // off screen (NaN: kept)
     const int tx0 = max(0, (int)fmaxf(x0 - 2.0f, 0.0f) / TILE), tx1 = min(fp.tiles_x - 1, (int)fminf(x1 + 2.0f, (float)(fp.W - 1)) / TILE);
     const int ty0 = max(0, (int)fmaxf(y0 - 2.0f, 0.0f) / TILE), ty1 = min(fp.tiles_y - 1, (int)fminf(y1 + 2.0f, (float)(fp.H - 1)) / TILE);
-    if (tx1 - tx0 + 1 >= fp.count || ty1 - ty0 >= 64) return true;   // a row of count tiles holds every rank's
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx)
-            if (lib_owned(fp, tx, ty)) return true;
-    return false;
+    if (!fp.reg.on && ty1 - ty0 >= 64) return true;
+    return shard_owns_any(fp.rank, fp.count, fp.reg, tx0, tx1, ty0, ty1, fp.tiles_x);
 }
 
 // Camera pass: one input triangle of rasterize_mesh.  A triangle that is not trivially inside the
@@ -808,6 +808,86 @@ __device__ __forceinline__ bool cull_keep(const LibFrameParams &fp, const LibDra
     return clip_reaches_rank(fp, t);
 }
 
+// Camera pass: the screen bounds of setup block b's triangles from their 256-triangle chunks'
+// model-space boxes (LibDrawGPU::cbox; wave 0, one lane per box corner).  Every point of a box whose
+// corners are all in front of the eye projects inside the hull of the projected corners, so the bin
+// tiles of that bbox (2 px of margin for the rounding of the per-vertex transforms, as
+// clip_reaches_rank) bound every fan of every triangle of the block ("bounded").  A box with corners
+// behind the eye gets an estimate instead: the hull of the part of the box with clip w >= 1e-3 of its
+// largest |w| (corners there and box edges cut at that w) -- what a floor reaching behind the camera
+// covers -- used as a cost estimate only, never to skip.  The bounds go to fb.blkrect (the region
+// balancer's input, shs_abi_shard.cpp; w: 1 bounded, 2 estimate, 0 none -- a block straddling draws).
+// -> true when the pass is region-sharded and bounded bounds miss the rank's rectangle: no triangle of
+// the block can reach this rank.  Block-uniform.
+__device__ bool setup_block_bounds(const LibFrameParams &fp, const LibBuffers &fb, int b, int tid) {
+    __shared__ int s_skip;
+    if (tid < 64) {
+        const int t0 = b * 256, t1 = min(t0 + 255, fp.n_tris - 1);
+        const int d = fb.bdraw[b];
+        const LibDrawGPU &dr = fb.draws[d];
+        const bool have = t0 <= t1 && (d + 1 >= fp.n_draws || fb.dbase[d + 1] > t1) && dr.cbox != nullptr;
+        bool bounded = false, finite = false;
+        float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+        if (have) {   // wave-uniform
+            const int c0 = (t0 - dr.tri_base) >> 8, c1 = (t1 - dr.tri_base) >> 8;   // at most two chunks
+            const int c = c0 + ((tid >> 3) & 1);
+            const bool mine = tid < 16 && c <= c1;
+            f4 cp = {0.0f, 0.0f, 0.0f, 1.0f};
+            if (mine) {
+                const float4 mn = dr.cbox[2 * c], mx = dr.cbox[2 * c + 1];
+                const int k = tid & 7;
+                cp = m4v(dr.viewproj, m4v(dr.model, f4{(k & 1) ? mx.x : mn.x, (k & 2) ? mx.y : mn.y, (k & 4) ? mx.z : mn.z, 1.0f}));
+            }
+            const bool fin = !mine || (isfinite(cp.x) && isfinite(cp.y) && isfinite(cp.w));
+            finite = __ballot(!fin) == 0ull;
+            bounded = finite && __ballot(mine && !(cp.w > 0.0f)) == 0ull;
+            float wmax = fabsf(cp.w);
+            for (int o = 1; o < 16; o <<= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o));
+            const float eps = bounded ? 0.0f : 1e-3f * wmax;
+            auto add = [&](float cx, float cy, float cw) {
+                const float sx = (cx / cw * 0.5f + 0.5f) * (float)(fp.W - 1);
+                const float sy = (cy / cw * 0.5f + 0.5f) * (float)(fp.H - 1);
+                x0 = fminf(x0, sx); x1 = fmaxf(x1, sx); y0 = fminf(y0, sy); y1 = fmaxf(y1, sy);
+            };
+            if (mine && cp.w > eps) add(cp.x, cp.y, cp.w);
+#pragma unroll
+            for (int m = 1; m < 8; m <<= 1) {   // the box edges from this corner, cut at w = eps
+                const float nx = __shfl_xor(cp.x, m), ny = __shfl_xor(cp.y, m), nw = __shfl_xor(cp.w, m);
+                if (mine && !bounded && (cp.w - eps) * (nw - eps) < 0.0f) {
+                    const float t = (eps - cp.w) / (nw - cp.w);
+                    add(cp.x + (nx - cp.x) * t, cp.y + (ny - cp.y) * t, eps);
+                }
+            }
+            for (int o = 1; o < 16; o <<= 1) {
+                x0 = fminf(x0, __shfl_xor(x0, o));
+                x1 = fmaxf(x1, __shfl_xor(x1, o));
+                y0 = fminf(y0, __shfl_xor(y0, o));
+                y1 = fmaxf(y1, __shfl_xor(y1, o));
+            }
+        }
+        if (tid == 0) {
+            int bx0 = 0, bx1 = fp.tiles_x - 1, by0 = 0, by1 = fp.tiles_y - 1;
+            const bool est = finite && !(x1 < x0);   // some point in front of the eye
+            if (finite && (bounded || est)) {
+                if (!(x1 >= -2.0f && y1 >= -2.0f && x0 <= (float)fp.W + 1.0f && y0 <= (float)fp.H + 1.0f)) {
+                    bx0 = 1; bx1 = 0; by0 = 1; by1 = 0;   // off screen: no fan reaches a pixel
+                } else {
+                    bx0 = max(0, (int)fmaxf(x0 - 2.0f, 0.0f) / TILE);
+                    bx1 = min(fp.tiles_x - 1, (int)fminf(x1 + 2.0f, (float)(fp.W - 1)) / TILE);
+                    by0 = max(0, (int)fmaxf(y0 - 2.0f, 0.0f) / TILE);
+                    by1 = min(fp.tiles_y - 1, (int)fminf(y1 + 2.0f, (float)(fp.H - 1)) / TILE);
+                }
+            }
+            fb.blkrect[b] = make_uint4((uint32_t)bx0 | ((uint32_t)bx1 << 16), (uint32_t)by0 | ((uint32_t)by1 << 16),
+                                       (uint32_t)max(0, t1 - t0 + 1), bounded ? 1u : (finite && est) ? 2u : 0u);
+            s_skip = (fp.count > 1 && fp.reg.on && bounded && !shard_owns_any(fp.rank, fp.count, fp.reg, bx0, bx1, by0, by1, fp.tiles_x))
+                         ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    return s_skip != 0;
+}
+
 template <bool SHADOW, bool LISTED = false>
 __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     __shared__ SetupShared ss;
@@ -820,6 +900,19 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     const uint64_t st0 = stl ? tl_now() : 0ull;
     if (listed && tid == 0) s_nkept = 0u;
     setup_prologue(fp, fb, ss, b, tid);
+    if constexpr (!SHADOW && !listed) {
+        if (fb.blkrect != nullptr && setup_block_bounds(fp, fb, b, tid)) {
+            // region-sharded pass, block off the rank's rectangle: its slots read as not rasterised
+            const int t = b * 256 + tid;
+            if (t < fp.n_tris) store_box(fb, (uint32_t)t, 0, -1, 0, -1);
+            if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(0u, 0u);
+            if (fb.stimeline && tid == 0) {
+                uint64_t *o = fb.stimeline + (size_t)b * STL_STRIDE;
+                o[0] = st0; o[1] = o[2] = o[3] = tl_now(); o[4] = o[5] = o[6] = o[7] = 0ull;
+            }
+            return;
+        }
+    }
     // the triangles: b * 256 + tid (one chunk per block), or (tile-sharded camera pass) the block's kept
     // triangles of its CULL_PER x 256 inputs, 256 per round
     uint32_t pre_clip = 0u, pre_rast = 0u;

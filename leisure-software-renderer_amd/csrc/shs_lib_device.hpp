@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "shs_shard.hpp"
+
 namespace shs_dev {
 
 // Per-draw block of one rasterize_mesh call (ShaderUniforms, shader/types.hpp:87-116, reduced to
@@ -32,6 +34,7 @@ struct alignas(16) LibDrawGPU {
     float shp[4];            // bias_const, bias_slope, pcf radius (int bits), pcf_step
     const uint32_t *tex;     // u.base_color_tex: Texture2DData texels (Color RGBA8, y * w + x), or null
     int32_t tex_w, tex_h;
+    const float4 *cbox;      // model-space bounds of the mesh's 256-triangle chunks (min, max per chunk)
 };
 
 // Raster record of one primitive (a fan triangle of a clipped input triangle, or a shadow-pass
@@ -77,6 +80,7 @@ struct LightCullParams {
     int32_t rank, count;                                // lists of owned 32x32 bin tiles only (tile sharding)
     int32_t pad;
     float view[16], proj[16];
+    ShardRegion reg;                                    // count > 1: region ownership (shs_shard.hpp)
 };
 
 constexpr uint32_t LF_DEPTH = 1u;       // target.depth_motion present: strict-less z test, depth written
@@ -97,7 +101,7 @@ constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
 struct LibFrameParams {
     int32_t W, H;
-    int32_t rank, count;             // shard ownership of 32x32 bin tiles (tile % count == rank)
+    int32_t rank, count;             // shard ownership of 32x32 bin tiles (tile % count == rank, or reg)
     int32_t tiles_x, tiles_y, rtiles_y;
     int32_t n_tris, n_draws;
     uint32_t flags;                  // LF_*
@@ -116,6 +120,7 @@ struct LibFrameParams {
     float tm_exposure, tm_inv_gamma; // fused PassTonemap (LibBuffers::tm_thr)
     uint32_t part;                   // camera pass: k_lib_plan splits a tile's list into parts of this many
                                      // entries (0: one work item per owned raster tile, no plan)
+    ShardRegion reg;                 // count > 1 with reg.on: this rank's rectangle of bin tiles
 };
 
 struct LibBuffers {
@@ -155,6 +160,8 @@ struct LibBuffers {
     float4 *uvw;                     // per slot, 2 float4: UV0 varying * 1/w of the 3 corners (textured draws)
     const float *srgb_lut;           // srgb_to_linear_rgb's 256 values, std::pow(c / 255.0f, 2.2f) on the host
     uint2 *items;                    // k_lib_plan: raster work items (rt_order position, part | parts << 16)
+    uint4 *blkrect;                  // camera pass: per setup block (bx0 | bx1 << 16, by0 | by1 << 16, triangles,
+                                     // bounded) of its chunk bounds, mapped host memory (the region balancer's input)
 };
 
 // k_lib_plan: at most this many parts per raster tile (capacity: LIB_MAXK * owned raster tiles).

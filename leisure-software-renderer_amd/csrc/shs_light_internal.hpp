@@ -16,7 +16,7 @@ __host__ __device__ inline bool light_list_owned(const shs_dev::LightCullParams 
     const int bot_up = top_up - (int)p.tile_size + 1 < 0 ? 0 : top_up - (int)p.tile_size + 1;
     const int bx = (int)px / 32, by0 = top_up / 32, by1 = bot_up / 32;
     const int tiles_x = (p.W + 31) / 32;
-    return ((by0 * tiles_x + bx) % p.count) == p.rank || ((by1 * tiles_x + bx) % p.count) == p.rank;
+    return shs_dev::shard_owned(p.rank, p.count, p.reg, bx, by0, tiles_x) || shs_dev::shard_owned(p.rank, p.count, p.reg, bx, by1, tiles_x);
 }
 
 // (mode 2) k_depth_reduce over `depth`, then k_light_cull over lists work[0 .. n_work) (work == nullptr:

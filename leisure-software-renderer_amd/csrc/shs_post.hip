@@ -33,14 +33,14 @@ __global__ __launch_bounds__(256) void k_tonemap(TonemapParams p) {
     tonemap_pixel(p, thr, x, y);
 }
 
-// Tile-sharded camera pass: only the rank's 32x32 tiles (rows y up, tile % count == rank) hold
+// Tile-sharded camera pass: only the rank's 32x32 tiles (rows y up, tile % count == rank or its region) hold
 // pixels, so one workgroup per owned tile maps them (32-px rows: 512-B reads, 128-B writes).
 __global__ __launch_bounds__(256) void k_tonemap_tiles(TonemapParams p) {
     __shared__ float thr[256];
     thr[threadIdx.x] = p.thr[threadIdx.x];
     __syncthreads();
     const int tiles_x = (p.W + 31) / 32;
-    const int t = p.rank + (int)blockIdx.x * p.count;
+    const int t = shard_tile(p.rank, p.count, p.reg, (int)blockIdx.x, tiles_x);
     const int x = (t % tiles_x) * 32 + (int)(threadIdx.x & 31u);
     const int y0 = (t / tiles_x) * 32 + (int)(threadIdx.x >> 5);
     if (x >= p.W) return;
@@ -117,7 +117,7 @@ hipError_t launch_motion_blur(const MotionBlurParams &p, hipStream_t s) {
 hipError_t launch_tonemap(const TonemapParams &p, hipStream_t s) {
     if (p.count > 1) {
         const int n_tiles = ((p.W + 31) / 32) * ((p.H + 31) / 32);
-        const int n_owned = (n_tiles - p.rank + p.count - 1) / p.count;
+        const int n_owned = shard_n_owned(p.rank, p.count, p.reg, n_tiles);
         if (n_owned > 0) hipLaunchKernelGGL(k_tonemap_tiles, dim3((unsigned)n_owned), dim3(256), 0, s, p);
         return hipGetLastError();
     }

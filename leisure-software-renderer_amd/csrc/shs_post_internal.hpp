@@ -4,6 +4,8 @@
 
 #include <cstdint>
 
+#include "shs_shard.hpp"
+
 namespace shs_dev {
 
 // PassTonemap + the present staging.  thr[k] (k = 1..255) is the smallest x = c / (1 + c) whose
@@ -16,6 +18,7 @@ struct TonemapParams {
     uint32_t *present;      // W*H RGBA8, rows top-down (upload_ldr_to_rgba8), or null
     int W, H;
     int rank, count;        // the camera pass's tile shard (count 1: the whole frame)
+    ShardRegion reg;        // ... its region (reg.on) or interleaved tiles
     float exposure;         // max(0.0001, exposure)
     float inv_gamma;        // 1 / max(0.001, gamma): only steers the first guess
     float thr[256];         // thr[0] unused

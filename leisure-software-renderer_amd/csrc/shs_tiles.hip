@@ -1,5 +1,6 @@
 // shs_tiles.hip -- device-side packing of a tile shard's framebuffer pixels for the multi-GPU
-// final-image gather: rank r owns the 32x32 tiles t = r, r + N, ... ; its pixels are
+// final-image gather: rank r owns the 32x32 tiles t = r, r + N, ... (or its region's
+// tiles, row-major: shs_shard.hpp); its pixels are
 // packed tile after tile into a contiguous device buffer (each tile padded to 32x32), exchanged with
 // RCCL, and unpacked on rank 0 into the full frame.  One workgroup per owned tile, coalesced 32-px
 // row segments.  Word layout per tile: colour words (legacy RGBA8: 1, library HDR: 4), then depth
@@ -14,8 +15,8 @@ namespace shs_dev {
 template <bool PACK>
 __global__ __launch_bounds__(256) void k_tiles_copy(TileCopyParams p, uint32_t *packed) {
     const int i = (int)blockIdx.x;
-    const int t = p.rank + i * p.count;
     const int tiles_x = (p.W + TILE - 1) / TILE;
+    const int t = shard_tile(p.rank, p.count, p.reg, i, tiles_x);
     const int x0 = (t % tiles_x) * TILE, y0 = (t / tiles_x) * TILE;
     uint32_t *base = packed + (size_t)i * TILE * TILE * p.words;
     for (int k = threadIdx.x; k < TILE * TILE; k += 256) {
@@ -48,7 +49,7 @@ using namespace shs_dev;
 
 hipError_t launch_tiles_copy(const TileCopyParams &p, bool pack, void *packed, hipStream_t s) {
     const int n_tiles = ((p.W + TILE - 1) / TILE) * ((p.H + TILE - 1) / TILE);
-    const int n_owned = (n_tiles - p.rank + p.count - 1) / p.count;
+    const int n_owned = shard_n_owned(p.rank, p.count, p.reg, n_tiles);
     if (n_owned <= 0) return hipSuccess;
     if (pack) hipLaunchKernelGGL(k_tiles_copy<true>, dim3(n_owned), dim3(256), 0, s, p, static_cast<uint32_t *>(packed));
     else hipLaunchKernelGGL(k_tiles_copy<false>, dim3(n_owned), dim3(256), 0, s, p, static_cast<uint32_t *>(packed));

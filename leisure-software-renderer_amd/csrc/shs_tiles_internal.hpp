@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "shs_shard.hpp"
+
 namespace shs_dev {
 struct TileCopyParams {
     int32_t W, H, rank, count;
@@ -12,6 +14,7 @@ struct TileCopyParams {
     uint32_t *color;        // framebuffer words
     uint32_t *depth;        // nullptr if absent
     uint32_t *motion;       // nullptr if absent (2 words per pixel)
+    ShardRegion reg;        // reg.on: rank's rectangle of bin tiles (else tile % count == rank)
 };
 }  // namespace shs_dev
 

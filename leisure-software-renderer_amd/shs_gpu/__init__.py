@@ -530,6 +530,22 @@ class Context:
         """SHS_OPT_SHARD_CULL: tile-sharded camera passes set up only the rank's triangles (default off)."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_SHARD_CULL, 1 if on else 0))
 
+    def set_shard_layout(self, regions: bool):
+        """SHS_OPT_SHARD_LAYOUT: tile-sharded library frames own interleaved 32x32 tiles (default) or one
+        cost-balanced rectangle per rank (regions=True)."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_SHARD_LAYOUT,
+                                             _abi.SHARD_REGIONS if regions else _abi.SHARD_INTERLEAVED))
+
+    def set_shard_root_share(self, share: float):
+        """SHS_OPT_SHARD_ROOT_SHARE: rank 0's share of a region layout relative to the others (0..1)."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_SHARD_ROOT_SHARE, int(round(share * 1000))))
+
+    def shard_regions(self, count):
+        """The last region-sharded camera pass's layout: [(bx0, by0, bx1, by1)] per rank (bin tiles, inclusive)."""
+        arr = (ctypes.c_int32 * (4 * count))()
+        self._check(self._lib.shs_get_shard_regions(self._h, count, arr))
+        return [tuple(arr[4 * r:4 * r + 4]) for r in range(count)]
+
     def set_overflow_capacities(self, spill: int = 0, frags: int = 0):
         """Tests: shrink the legacy bin-spill / ghost-fragment lists (0 = leave) to force overflows."""
         if spill:
@@ -636,8 +652,15 @@ class Context:
     TARGET_LEGACY, TARGET_LIB, TARGET_PRESENT, TARGET_LIB_PRESENT = 0, 1, 2, 3
 
     def tiles_packed_words(self, target, count):
+        """Packed words of the largest rank's tiles (a buffer size every rank's tiles fit)."""
         n = ctypes.c_int64()
         self._check(self._lib.shs_tiles_packed_words(self._h, target, count, ctypes.byref(n)))
+        return n.value
+
+    def tiles_rank_words(self, target, rank, count):
+        """Packed words of rank's own tiles (region layouts differ per rank)."""
+        n = ctypes.c_int64()
+        self._check(self._lib.shs_tiles_rank_words(self._h, target, rank, count, ctypes.byref(n)))
         return n.value
 
     def tiles_pack(self, target, rank, count, dst_ptr):

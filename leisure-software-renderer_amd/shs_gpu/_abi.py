@@ -32,6 +32,10 @@ OPT_SPILL_CAPACITY = 5
 OPT_FRAG_CAPACITY = 6
 OPT_LIB_PART = 7
 OPT_SHARD_CULL = 8
+OPT_SHARD_LAYOUT = 9
+SHARD_INTERLEAVED = 0
+SHARD_REGIONS = 1
+OPT_SHARD_ROOT_SHARE = 10
 
 
 class LegacyDraw(ctypes.Structure):
@@ -273,6 +277,8 @@ SIGNATURES = [
                                              ctypes.c_int32, _F]),
     ("shs_resolve_shadow_map", ctypes.c_int, [_P, _P]),
     ("shs_tiles_packed_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
+    ("shs_tiles_rank_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
+    ("shs_get_shard_regions", ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     ("shs_tiles_pack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
     ("shs_tiles_unpack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
     ("shs_lights_upload", ctypes.c_int, [_P, ctypes.POINTER(CullingLightC), ctypes.c_int32]),
@@ -294,6 +300,7 @@ SIGNATURES = [
     ("shs_group_mesh_upload_soup", ctypes.c_int, [_P, _F, _F, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     ("shs_group_texture_upload", ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     ("shs_group_lights_upload", ctypes.c_int, [_P, ctypes.POINTER(CullingLightC), ctypes.c_int32]),
+    ("shs_group_set_option", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int64]),
     ("shs_group_lib_fuse_tonemap", ctypes.c_int, [_P, ctypes.POINTER(TonemapDescC)]),
     ("shs_group_light_cull", ctypes.c_int, [_P, ctypes.POINTER(LightCullDescC)]),
     ("shs_group_render_shadow_map", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _F, ctypes.POINTER(ShadowCasterC),

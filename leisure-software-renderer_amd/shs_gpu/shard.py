@@ -1,7 +1,8 @@
 """Screen-tile sharding of one frame across ranks.
 
 Rank r of N renders only the bin tiles with `tile % N == r` (shs_frame_desc.shard_rank/count; a tile
-is shs_gpu_tile_size() px square, row-major).  The owned tiles of every rank are then gathered into
+is shs_gpu_tile_size() px square, row-major), or -- library frames with SHS_OPT_SHARD_LAYOUT regions --
+one cost-balanced rectangle of tiles per rank.  The owned tiles of every rank are then gathered into
 the full frame on rank 0.  On GPUs the collective runs over RCCL ("nccl" backend) on device tensors;
 the same code runs over gloo on CPU tensors (tests/test_shard.py).
 
@@ -17,10 +18,18 @@ except ImportError:  # pragma: no cover - torch is present in this image
     torch = None
 
 
-def owned_tiles(width, height, tile, rank, count):
-    """Row-major tile indices owned by `rank` (tile % count == rank)."""
+def owned_tiles(width, height, tile, rank, count, regions=None):
+    """Tile indices owned by `rank`: tile % count == rank, or with a region layout (regions[r] =
+    (bx0, by0, bx1, by1), inclusive, SHS_OPT_SHARD_LAYOUT) the rank's rectangle row-major -- the order
+    of shs_tiles_pack's blocks (shs_shard.hpp shard_tile)."""
     tx = (width + tile - 1) // tile
     ty = (height + tile - 1) // tile
+    if regions is not None and count > 1:
+        x0, y0, x1, y1 = regions[rank]
+        if x1 < x0 or y1 < y0:
+            return np.zeros(0, np.int64)
+        yy, xx = np.mgrid[y0:y1 + 1, x0:x1 + 1]
+        return (yy * tx + xx).reshape(-1).astype(np.int64)
     return np.arange(rank, tx * ty, count, dtype=np.int64)
 
 
@@ -91,9 +100,9 @@ def planes_of(frame_planes):
     return out
 
 
-def pack_padded(planes, width, height, rank, count, tile=32):
+def pack_padded(planes, width, height, rank, count, tile=32, regions=None):
     """CPU restatement of shs_tiles_pack for screen-row planes (list of uint32 [H, W])."""
-    owned = owned_tiles(width, height, tile, rank, count)
+    owned = owned_tiles(width, height, tile, rank, count, regions)
     nw = len(planes)
     out = np.zeros((len(owned), nw, tile, tile), np.uint32)
     for i, t in enumerate(owned):
@@ -103,8 +112,8 @@ def pack_padded(planes, width, height, rank, count, tile=32):
     return out.reshape(-1)
 
 
-def unpack_padded(planes, packed, width, height, rank, count, tile=32):
-    owned = owned_tiles(width, height, tile, rank, count)
+def unpack_padded(planes, packed, width, height, rank, count, tile=32, regions=None):
+    owned = owned_tiles(width, height, tile, rank, count, regions)
     blk = np.asarray(packed).view(np.uint32).reshape(-1, len(planes), tile, tile)
     for i, t in enumerate(owned):
         y0, y1, x0, x1 = _tile_slices(t, width, height, tile)
@@ -115,31 +124,44 @@ def unpack_padded(planes, packed, width, height, rank, count, tile=32):
 def gather_frame_device(dist, ctx, target, stream=None, out=None):
     """RCCL gather of a tile-sharded frame into rank 0's context buffers (device to device).
     Every rank packs its owned tiles on the GPU (shs_tiles_pack, which first finishes the frame: a
-    capacity overflow is re-issued before anything leaves the rank), rank 0 receives the peers'
-    buffers with dist.gather (ncclSend/Recv over xGMI) and unpacks them in place (shs_tiles_unpack).
-    The context runs on torch's current stream so RCCL and the kernels are ordered; it is re-pointed
-    only when it is not on that stream already (shs_set_stream synchronises).
+    capacity overflow is re-issued before anything leaves the rank); each peer sends exactly its own
+    packed tiles to rank 0 (point-to-point ncclSend / ncclRecv over xGMI, batched: the region layout's
+    ranks differ in size) and rank 0 unpacks them in place (shs_tiles_unpack).
+    The context runs on the given stream (default torch's current one) so RCCL and the kernels are
+    ordered; it is re-pointed only when it is not on that stream already (shs_set_stream synchronises).
     target: ctx.TARGET_PRESENT / TARGET_LIB_PRESENT (RGBA8, 4 B/px: what the SDL present needs) or
     TARGET_LEGACY / TARGET_LIB (colour + depth (+ motion): 8 / 28 B/px).
-    out: optional list of preallocated int32 device buffers [count + 1] (send + receive) to reuse."""
+    out: optional list of preallocated int32 device buffers [count + 1] (send + receive) to reuse;
+    returns the list used."""
     rank, count = dist.get_rank(), dist.get_world_size()
     s = stream if stream is not None else torch.cuda.current_stream()
     if ctx.stream != s.cuda_stream:
         ctx.set_stream(s.cuda_stream)
     words = ctx.tiles_packed_words(target, count)
+    sizes = [ctx.tiles_rank_words(target, r, count) for r in range(count)]
     dev = torch.device("cuda", torch.cuda.current_device())
-    if out is None or out[0].numel() != words:
+    if out is None or out[0].numel() < words:
         out = [torch.empty(words, dtype=torch.int32, device=dev) for _ in range(count + 1)]
     buf = out[0]
     ctx.tiles_pack(target, rank, count, buf.data_ptr())
+    send_to_root(dist, buf, out[1:], sizes)
     if rank == 0:
-        bufs = out[1:]
-        dist.gather(buf, gather_list=bufs, dst=0)
         for r in range(1, count):
-            ctx.tiles_unpack(target, r, count, bufs[r].data_ptr())
-    else:
-        dist.gather(buf, dst=0)
+            if sizes[r] > 0:
+                ctx.tiles_unpack(target, r, count, out[1 + r].data_ptr())
     return out
+
+
+def send_to_root(dist, buf, recvs, sizes):
+    """Rank r > 0 sends buf[:sizes[r]] to rank 0, which receives it into recvs[r][:sizes[r]]: one
+    batch of point-to-point operations (sizes may differ per rank; empty ranks send nothing)."""
+    rank, count = dist.get_rank(), dist.get_world_size()
+    if rank == 0:
+        ops = [dist.P2POp(dist.irecv, recvs[r][:sizes[r]], r) for r in range(1, count) if sizes[r] > 0]
+    else:
+        ops = [dist.P2POp(dist.isend, buf[:sizes[rank]], 0)] if sizes[rank] > 0 else []
+    for q in (dist.batch_isend_irecv(ops) if ops else []):
+        q.wait()
 
 
 def gather_frame(dist, color, depth, tile, device=None):

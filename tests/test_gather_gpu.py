@@ -173,8 +173,8 @@ def test_legacy_binned_hair_shards_compose():
 
 
 class _RankZeroDist:
-    """torch.distributed stand-in for rank 0 of `count` ranks in one process: gather() fills rank 0's
-    receive list with its own buffer and the peers' packed buffers (rendered by other contexts)."""
+    """torch.distributed stand-in for rank 0 of `count` ranks in one process: its point-to-point
+    receives take the peers' packed buffers (rendered by other contexts)."""
 
     def __init__(self, count, peers):
         self.count, self.peers = count, peers
@@ -185,11 +185,17 @@ class _RankZeroDist:
     def get_world_size(self):
         return self.count
 
-    def gather(self, buf, gather_list=None, dst=0):
-        assert dst == 0 and gather_list is not None and len(gather_list) == self.count
-        gather_list[0].copy_(buf)
-        for r in range(1, self.count):
-            gather_list[r].copy_(self.peers[r])
+    irecv, isend = "irecv", "isend"
+
+    @staticmethod
+    def P2POp(op, tensor, peer):
+        return (op, tensor, peer)
+
+    def batch_isend_irecv(self, ops):
+        for op, t, peer in ops:
+            assert op == "irecv" and 1 <= peer < self.count
+            t.copy_(self.peers[peer][:t.numel()])
+        return []
 
 
 def test_gather_frame_device_reuses_buffers():

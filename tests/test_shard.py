@@ -107,10 +107,16 @@ def test_padded_layout_roundtrip(w, h, count):
     assert np.array_equal(dst_depth.view(np.uint32), depth.view(np.uint32))
 
 
-def _gloo_padded_worker(rank, world, port, q, present=False):
-    """The device gather's protocol over gloo: pack (host restatement), gather to rank 0, unpack.
-    present: the 4 B/px RGBA8 present staging the sharded bench ships (SHS_TARGET_LIB_PRESENT: rows
-    top-down, so the plane is row-flipped into screen order like the device's tile parameters)."""
+# region layouts of a 333x241 frame (11 x 8 bin tiles) for 2 and 3 ranks, one with an empty rank
+_REGIONS = {2: [(0, 0, 3, 7), (4, 0, 10, 7)], 3: [(0, 0, 10, 2), (0, 3, 10, 7), (1, 1, 0, 0)]}
+
+
+def _gloo_padded_worker(rank, world, port, q, present=False, regions=False):
+    """The device gather's protocol over gloo: pack (host restatement), point-to-point sends of each
+    rank's exact packed size to rank 0 (shard.send_to_root, what gather_frame_device runs over RCCL),
+    unpack.  present: the 4 B/px RGBA8 present staging the sharded bench ships (SHS_TARGET_LIB_PRESENT:
+    rows top-down, so the plane is row-flipped into screen order like the device's tile parameters).
+    regions: a region layout (ranks of different sizes, possibly empty) instead of interleaved tiles."""
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -118,39 +124,39 @@ def _gloo_padded_worker(rank, world, port, q, present=False):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         w, h = 333, 241
+        reg = _REGIONS[world] if regions else None
         rng = np.random.default_rng(12)
         color = rng.integers(0, 2**31, size=(h, w), dtype=np.int64).astype(np.uint32)
-        n_tiles = ((w + 31) // 32) * ((h + 31) // 32)
-        words = ((n_tiles + world - 1) // world) * 1024
-        buf = np.zeros(words, np.uint32)
         rgba = color.view(np.uint8).reshape(h, w, 4)
         planes = shard.planes_of([(rgba, True)]) if present else [color]
-        mine = shard.pack_padded(planes, w, h, rank, world)
+        sizes = [len(shard.owned_tiles(w, h, 32, r, world, reg)) * 1024 for r in range(world)]
+        buf = np.zeros(max(sizes) + 7, np.uint32)   # capacity above the payload: only sizes[r] words travel
+        mine = shard.pack_padded(planes, w, h, rank, world, regions=reg)
+        assert mine.size == sizes[rank]
         buf[:mine.size] = mine
         t = torch.from_numpy(buf.view(np.int32))
+        recvs = [torch.zeros_like(t) for _ in range(world)]
+        shard.send_to_root(dist, t, recvs, sizes)
         if rank == 0:
-            bufs = [torch.empty_like(t) for _ in range(world)]
-            dist.gather(t, gather_list=bufs, dst=0)
             out = np.zeros_like(color)
             out_planes = shard.planes_of([(out.view(np.uint8).reshape(h, w, 4), True)]) if present else [out]
-            for r in range(world):
-                shard.unpack_padded(out_planes, bufs[r].numpy().view(np.uint32), w, h, r, world)
+            shard.unpack_padded(out_planes, mine, w, h, 0, world, regions=reg)
+            for r in range(1, world):
+                shard.unpack_padded(out_planes, recvs[r].numpy().view(np.uint32)[:sizes[r]], w, h, r, world, regions=reg)
             q.put(bool(np.array_equal(out, color)))
         else:
-            dist.gather(t, dst=0)
             q.put(True)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("present", [False, True])
-def test_gloo_device_protocol_gather(present):
+@pytest.mark.parametrize("present,regions,world", [(False, False, 2), (True, False, 2), (True, True, 2), (False, True, 3)])
+def test_gloo_device_protocol_gather(present, regions, world):
     import torch.multiprocessing as mp
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_padded_worker, args=(r, world, port, q, present)) for r in range(world)]
+    procs = [ctx.Process(target=_gloo_padded_worker, args=(r, world, port, q, present, regions)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -3,7 +3,7 @@ its own stream and workspace) render consecutive frames round-robin, so frame k+
 while frame k's are still in flight.  Measured on ONE GPU, each rank's shard in turn (as
 exp_shard_split.py), without the gather.
 usage (GPU box): python tools/exp_pipeline.py [c4|c5] [frames] [N list] [depth list, e.g. 1,2,3]
-(env SPLIT_CULL / SPLIT_PART as exp_shard_split.py)"""
+(env SPLIT_CULL / SPLIT_PART / SPLIT_REGIONS as exp_shard_split.py; SPLIT_ONLY=r: rank r's shard only)"""
 import os
 import sys
 import time
@@ -22,6 +22,8 @@ def make_ctx(cfg):
         ctx.set_shard_cull(os.environ["SPLIT_CULL"] == "1")
     if os.environ.get("SPLIT_PART") is not None:
         ctx.set_lib_part(int(os.environ["SPLIT_PART"]))
+    if os.environ.get("SPLIT_REGIONS") == "1":
+        ctx.set_shard_layout(True)
     if cfg == "c4":
         frame, draws, lights, cull = scene_lib.c4_scene(3840, 2160)
         ctx.upload_lights(lights)
@@ -43,8 +45,9 @@ def main():
     pool = [make_ctx(cfg) for _ in range(max(depths))]
     for N in ns:
         for D in depths:
-            per_rank = []
-            for r in range(N):
+            per_rank, host_ms = [], []
+            only = os.environ.get("SPLIT_ONLY")
+            for r in ([int(only)] if only is not None and N > 1 else range(N)):
                 ones = []
                 for ctx, frame, draws, extra in pool[:D]:
                     frame.shard_rank, frame.shard_count = r, N
@@ -64,14 +67,20 @@ def main():
                 for ctx, *_ in pool[:D]:
                     ctx.synchronize_lib()
                 t0 = time.perf_counter()
+                host = 0.0
                 for i in range(nf):
+                    h0 = time.perf_counter()
                     ones[i % D]()
+                    host += time.perf_counter() - h0
                 for ctx, *_ in pool[:D]:
                     ctx.synchronize_lib()
                 per_rank.append((time.perf_counter() - t0) / nf * 1e3)
+                host_ms.append(host / nf * 1e3)
             ms = np.array(per_rank)
-            print(f"{cfg} N={N} frames in flight {D}: per-rank ms/frame max {ms.max():.4f} mean {ms.mean():.4f}",
-                  flush=True)
+            print(f"{cfg} N={N} frames in flight {D}: per-rank ms/frame max {ms.max():.4f} mean {ms.mean():.4f}"
+                  f" | " + " ".join(f"{x:.4f}" for x in ms) + f" | host enqueue ms/frame {np.mean(host_ms):.4f}", flush=True)
+            if N > 1 and os.environ.get("SPLIT_REGIONS") == "1":
+                print(f"   regions {pool[0][0].shard_regions(N)}", flush=True)
     for ctx, *_ in pool:
         ctx.close()
 

@@ -1,7 +1,7 @@
 """Per-rank work of the tile-sharded C4 / C5 frame, measured on ONE GPU by rendering each rank's shard
 in turn (shard_rank / shard_count): the Amdahl inputs for the N-GPU projection.
 usage (GPU box): python tools/exp_shard_split.py [c4|c5] [frames] [N list, e.g. 1,2,4,8]
-(env SPLIT_CULL=0|1: SHS_OPT_SHARD_CULL, SPLIT_PART=-1|0|n: SHS_OPT_LIB_PART)"""
+(env SPLIT_CULL=0|1: SHS_OPT_SHARD_CULL, SPLIT_PART=-1|0|n: SHS_OPT_LIB_PART, SPLIT_REGIONS=1: region layout)"""
 import os
 import sys
 import time
@@ -23,6 +23,8 @@ def main():
         ctx.set_shard_cull(os.environ["SPLIT_CULL"] == "1")
     if os.environ.get("SPLIT_PART") is not None:
         ctx.set_lib_part(int(os.environ["SPLIT_PART"]))
+    if os.environ.get("SPLIT_REGIONS") == "1":
+        ctx.set_shard_layout(True)
     if cfg == "c4":
         frame, draws, lights, cull = scene_lib.c4_scene(3840, 2160)
         ctx.upload_lights(lights)
