@@ -224,9 +224,13 @@ def lib_workload(args, rank=0):
 class LibSlot:
     """One frame in flight: a context with its own stream, workspace and targets (frames k, k + D, ...)."""
 
-    def __init__(self, local_rank, dist):
+    def __init__(self, local_rank, dist, args=None):
         import shs_gpu
         self.ctx = shs_gpu.Context(local_rank)
+        if dist is not None and args is not None and args.shard_layout == "regions":
+            # one cost-balanced rectangle per rank (SHS_OPT_SHARD_LAYOUT); rank 0 also unpacks the gather
+            self.ctx.set_shard_layout(True)
+            self.ctx.set_shard_root_share(args.root_share)
         self.stream = None
         if dist is not None:
             import torch
@@ -293,7 +297,7 @@ def run_gpu_c4(args, rank, local_rank, world, dist):
         cull.shard_rank, cull.shard_count = rank, world
     slots = []
     for _ in range(args.inflight):
-        sl = LibSlot(local_rank, dist)
+        sl = LibSlot(local_rank, dist, args)
         sl.ctx.upload_lights(lights)
         sl.ctx.light_cull(cull)
         sl.prepared = sl.ctx.prepare_lib(frame, draws)
@@ -335,7 +339,7 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
     sd = (ctypes.c_float * 3)(*[float(x) for x in sun])
     slots = []
     for _ in range(args.inflight):
-        sl = LibSlot(local_rank, dist)
+        sl = LibSlot(local_rank, dist, args)
         ctx = sl.ctx
         lvp = ctx.render_shadow_map(S, sun, casters)
         scene_lib.wire_shadow(draws, lvp)
@@ -562,6 +566,10 @@ def main():
                     help="legacy configs: frames per shs_render_legacy_batch step (default 64 for c1/c2, 16 for c3)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="c4/c5: frames in flight (contexts rendering consecutive frames round-robin)")
+    ap.add_argument("--shard-layout", default="regions", choices=["regions", "interleaved"],
+                    help="c4/c5 at N > 1: tile ownership (one cost-balanced rectangle per rank, or tile %% N)")
+    ap.add_argument("--root-share", type=float, default=0.85,
+                    help="c4/c5 regions: rank 0's share of the predicted cost (it also unpacks the gather)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -731,12 +739,13 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     if c4:
         data = ("synthetic: 1000 seeded objects x 1000 small triangles (seed 0x5EED), 256 point lights (seed 0x11A7, "
                 "range U[2,8], Smooth attenuation), 16-px tiles, max 128 lights per tile")
-        parallelism = f"tile-sharded x{world} + RCCL gather of RGBA8 present tiles to rank 0" if world > 1 else "single GPU"
+        parallelism = (f"tile-sharded x{world} ({args.shard_layout}) + RCCL gather of RGBA8 present tiles to rank 0"
+                       if world > 1 else "single GPU")
     else:
         data = ("synthetic: Suzanne (indexed from the reference's monkey.rawobj) + make_plane floor, reference "
                 "defaults (sun normalize(0.4668,-0.3487,0.8127), intensity 5, PCF 2, bias 0.0008/0.0015)")
-        parallelism = (f"tile-sharded x{world} (shadow map on every rank) + RCCL gather of RGBA8 present tiles "
-                       "to rank 0") if world > 1 else "single GPU"
+        parallelism = (f"tile-sharded x{world} ({args.shard_layout}; shadow map on every rank) + RCCL gather of RGBA8 "
+                       "present tiles to rank 0") if world > 1 else "single GPU"
     line = {
         "metric": METRIC, "value": round(world_tri * steps / el_max / 1e6, 3), "unit": "Mtri/s", "n_gpus": world,
         "steps": steps, "warmup": args.warmup, "ms_per_step": round(el_max / steps * 1e3, 5), "higher_is_better": True,

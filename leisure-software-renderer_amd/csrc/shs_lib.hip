@@ -764,8 +764,7 @@ __device__ __forceinline__ void wave_append(uint32_t *counter, T *queue, bool pr
 }
 
 // Setup workgroup start: LDS state, and the next frame's counter set, raster queues and bin counts zeroed.
-__device__ __forceinline__ void setup_prologue(const LibFrameParams &fp, const LibBuffers &fb, SetupShared &ss, int b, int tid) {
-    setup_shared_init(ss, tid);
+__device__ __forceinline__ void setup_zero_next(const LibFrameParams &fp, const LibBuffers &fb, int b, int tid) {
     if (b == 0 && tid < LC_N) fb.counters[(fp.parity ^ 1u) * LC_N + tid] = 0u;
     if (b == 0 && tid < LIB_NQ) fb.rqueue[((fp.parity ^ 1u) * LIB_NQ + tid) * LIB_QSTRIDE] = 0u;
     {
@@ -773,6 +772,11 @@ __device__ __forceinline__ void setup_prologue(const LibFrameParams &fp, const L
         uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
         for (int t = b * 256 + tid; t < n_bt; t += (int)gridDim.x * 256) next_count[t] = 0u;
     }
+}
+
+__device__ __forceinline__ void setup_prologue(const LibFrameParams &fp, const LibBuffers &fb, SetupShared &ss, int b, int tid) {
+    setup_shared_init(ss, tid);
+    setup_zero_next(fp, fb, b, tid);
     __syncthreads();
 }
 
@@ -899,10 +903,11 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     const bool stl = fb.stimeline != nullptr && tid == 0;
     const uint64_t st0 = stl ? tl_now() : 0ull;
     if (listed && tid == 0) s_nkept = 0u;
-    setup_prologue(fp, fb, ss, b, tid);
     if constexpr (!SHADOW && !listed) {
         if (fb.blkrect != nullptr && setup_block_bounds(fp, fb, b, tid)) {
-            // region-sharded pass, block off the rank's rectangle: its slots read as not rasterised
+            // region-sharded pass, block off the rank's rectangle: its share of the next frame's zeroing,
+            // and its slots read as not rasterised
+            setup_zero_next(fp, fb, b, tid);
             const int t = b * 256 + tid;
             if (t < fp.n_tris) store_box(fb, (uint32_t)t, 0, -1, 0, -1);
             if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(0u, 0u);
@@ -913,6 +918,7 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
             return;
         }
     }
+    setup_prologue(fp, fb, ss, b, tid);
     // the triangles: b * 256 + tid (one chunk per block), or (tile-sharded camera pass) the block's kept
     // triangles of its CULL_PER x 256 inputs, 256 per round
     uint32_t pre_clip = 0u, pre_rast = 0u;
