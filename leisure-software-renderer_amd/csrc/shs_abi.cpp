@@ -62,8 +62,8 @@ int shs_create(int device, shs_ctx **out) {
         return SHS_ERR_HIP;
     }
     std::memset(ctx->h_counters, 0, shs_dev::C_NCOUNTERS * sizeof(uint32_t));
-    if (ensure(ctx, ctx->counters, 2 * shs_dev::CSET) != SHS_OK ||
-        hipMemset(ctx->counters.p, 0, 2 * shs_dev::CSET * sizeof(uint32_t)) != hipSuccess) {
+    if (ensure(ctx, ctx->counters, shs_dev::N_CSETS * shs_dev::CSET) != SHS_OK ||
+        hipMemset(ctx->counters.p, 0, shs_dev::N_CSETS * shs_dev::CSET * sizeof(uint32_t)) != hipSuccess) {
         shs_destroy(ctx);
         return SHS_ERR_HIP;
     }
@@ -262,8 +262,6 @@ static int enqueue_frame(shs_ctx *ctx) {
         HIP_TRY(ctx, hipMemsetAsync(ws.busy.p, 0, ws.busy.cap * sizeof(uint32_t), sst));
         ctx->geom_key[slot] = gkey;
     }
-    uint32_t *cset = ctx->counters.p + (size_t)slot * shs_dev::CSET;
-    HIP_TRY(ctx, hipMemsetAsync(cset, 0, shs_dev::CSET * sizeof(uint32_t), sst));
 
     // per-draw uniform blocks: kernel arguments for small batches, the slot's device table otherwise.
     // tri_base restarts at 0 in every frame (submission order is per frame)
@@ -318,7 +316,8 @@ static int enqueue_frame(shs_ctx *ctx) {
         const int n_groups = std::max(1, (n_tris + 15) / 16) * n_frames;
         fp.ghost_slices = (uint32_t)std::min(16, std::max(1, 1024 / n_groups));
     }
-    fp.parity = (uint32_t)slot;   // the slot's counter set
+    fp.parity = (uint32_t)(ctx->frame_index % shs_dev::N_CSETS);   // counter sets round-robin (zeroed by the
+    fp.zero_set = (uint32_t)((ctx->frame_index + 1) % shs_dev::N_CSETS);   // previous batch's k_setup)
     if (++ctx->busy_epoch == 0u) ctx->busy_epoch = 1u;   // busy[] is zeroed on reset; 0 is never an epoch
     fp.epoch = ctx->busy_epoch;
     fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;

@@ -81,14 +81,17 @@ constexpr int CAND = 1024;           // candidate ids gathered per round (4 per 
 constexpr int SCAN_MAX_TRIS = 4096;  // scenes up to this size skip binning (scan mode)
 constexpr double GHOST_MAX_EXPAND = 48.0;  // larger danger boxes are handled as TRI_UNBOUNDED
 
-// counters[] slots (two sets, one per workspace slot, zeroed on the setup stream before each batch).
+// counters[] slots (three sets used round-robin by consecutive batches; batch k's k_setup zeroes the set
+// of batch k + 1, last used by batch k - 2, whose raster its setup stream has waited for -- no memset
+// node between two batches).
 // Only the append positions and the overflow flags live here; statistics go to per-block slots.
 // C_BUSY: entries of the busy-tile list (k_setup / k_ghost).  The host reads the first C_NCOUNTERS
 // words of a set.  k_raster's work tickets live in N_WORKQ queues, one 128-B line each from C_WORK
 // (one queue per XCD-sized group of workgroups: a same-address returning atomic serialises).
 constexpr int C_OVERFLOW = 0, C_SPILL = 1, C_FRAG = 2, C_SLIVER = 3, C_BUSY = 4, C_NCOUNTERS = 5;
 constexpr int N_WORKQ = 8, WORKQ_STRIDE = 32, C_WORK = 32;
-constexpr int CSET = C_WORK + N_WORKQ * WORKQ_STRIDE;   // words per counter set (2 parity sets)
+constexpr int CSET = C_WORK + N_WORKQ * WORKQ_STRIDE;   // words per counter set (N_CSETS sets)
+constexpr int N_CSETS = 3;
 constexpr uint32_t OV_SPILL = 1u, OV_FRAG = 2u;
 
 // Timing-experiment switches (frame flags bits 8+; results are WRONG with any of them set): they
@@ -129,7 +132,8 @@ struct FrameParams {
     uint32_t spill_cap;
     uint32_t frag_cap;               // ghost fragment capacity
     uint32_t ghost_slices;           // ghost waves per GHOST_GROUP triangles (k_setup)
-    uint32_t parity;                 // counter / bin-count set used by this frame
+    uint32_t parity;                 // counter set used by this batch
+    uint32_t zero_set;               // counter set k_setup zeroes (the next batch's)
     uint32_t scan_mode;              // 1: no bins, busy raster tiles scan all bin boxes (small scenes)
     uint32_t ghost_list;             // 1: k_setup lists the unbounded slivers, k_ghost enumerates them
                                      // (binned scenes); 0: k_setup's ghost waves (scan-mode scenes)

@@ -726,6 +726,8 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_a
     __shared__ NewBusy s_new;
     uint32_t *cnt = fb_all.counters + fp.parity * CSET;
     const int b = (int)blockIdx.x;
+    if (b == 0)   // the next batch's counter set (its previous user, batch k - 2, has finished)
+        for (int i = (int)threadIdx.x; i < CSET; i += 256) fb_all.counters[(size_t)fp.zero_set * CSET + i] = 0u;
     // frame of the batch and the block's role inside it
     const int frame = b / fp.frame_blocks, lb = b - frame * fp.frame_blocks;
     const FrameBuffers fb = frame_view(fp, fb_all, frame);
