@@ -2211,6 +2211,8 @@ int lib_setup_grid(int n_tris, bool listed) {
 
 hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, bool listed, hipStream_t s) {
     const int grid = lib_setup_grid(fp.n_tris, listed && !shadow);
+    // the striding kernels' grid: 1024 workgroups, a region-sharded rank's share of them
+    const int wide = (fp.count > 1 && fp.reg.on) ? std::max(128, 1024 / fp.count) : 1024;
     if (shadow) {
         hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     } else {
@@ -2220,10 +2222,10 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
             hipLaunchKernelGGL(k_lib_setup<false>, dim3(grid), dim3(256), 0, s, fp, fb);
         }
         // one 16-lane group per queued triangle (the queue can hold every input triangle), at most
-        // 1024 workgroups striding a longer queue
-        hipLaunchKernelGGL(k_lib_clip, dim3(std::max(1, std::min((fp.n_tris + 15) / 16, 1024))), dim3(256), 0, s, fp, fb);
+        // 1024 workgroups striding a longer queue (a region-sharded rank queues about 1 / count of them)
+        hipLaunchKernelGGL(k_lib_clip, dim3(std::max(1, std::min((fp.n_tris + 15) / 16, wide))), dim3(256), 0, s, fp, fb);
     }
-    hipLaunchKernelGGL(k_lib_bigmark, dim3(1024), dim3(256), 0, s, fp, fb);
+    hipLaunchKernelGGL(k_lib_bigmark, dim3(wide), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }
 

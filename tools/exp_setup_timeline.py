@@ -1,6 +1,6 @@
 """Library camera-pass setup, per-workgroup timeline (SHS_OPT_TIMELINE, shs_lib_debug_setup_timeline):
 start / triangles-done / deferred-marks-done / end per workgroup, for C4 at shard r of N.
-usage (GPU box): python tools/exp_setup_timeline.py [N] [rank]"""
+usage (GPU box): python tools/exp_setup_timeline.py [N] [rank]   (env SPLIT_REGIONS=1: region layout)"""
 import os
 import sys
 
@@ -15,6 +15,8 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 R = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 frame, draws, lights, cull = scene_lib.c4_scene(3840, 2160)
 ctx = shs_gpu.Context(0)
+if os.environ.get("SPLIT_REGIONS") == "1":
+    ctx.set_shard_layout(True)
 ctx.upload_lights(lights)
 frame.shard_rank, frame.shard_count = R, N
 cull.shard_rank, cull.shard_count = R, N
@@ -32,6 +34,11 @@ t = ctx.lib_debug_setup_timeline().astype(np.int64)
 t0 = t[:, 0].min()
 st, a, b, e = (t[:, k] - t0 for k in range(4))
 dur = e - st
+live = (a - st) > 0 if os.environ.get("SPLIT_REGIONS") == "1" else np.ones(len(t), bool)
+if os.environ.get("SPLIT_REGIONS") == "1":   # skipped blocks record start == triangles-done
+    live = t[:, 1] != t[:, 3]
+    print(f"  surviving blocks {int(live.sum())} of {len(t)}; their duration median {np.median(dur[live]) / 100:.2f} us, "
+          f"triangles phase {np.median((a - st)[live]) / 100:.2f}, skipped blocks' duration median {np.median(dur[~live]) / 100:.2f} us")
 print(f"C4 shard {R}/{N}: {len(t)} setup workgroups, span {(e.max()) / 100:.1f} us (10 ns ticks / 100)")
 print(f"  per-workgroup duration us: median {np.median(dur) / 100:.2f} p90 {np.percentile(dur, 90) / 100:.2f} max {dur.max() / 100:.2f}")
 print(f"  triangles phase us: median {np.median(a - st) / 100:.2f}; deferred marks median {np.median(b - a) / 100:.2f}; "
