@@ -405,8 +405,9 @@ def collect_pmc(args):
         return None, f"pmc failed: {e!r}"
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    # gfx950: FETCH_SIZE counts half the bytes of a wide coalesced read (MI355X_MICROARCH.md HBM);
-    # WRITE_SIZE is exact for 16-B-per-lane stores (k_raster's colour/depth stores); unit KiB.
+    # gfx950: FETCH_SIZE counts half the bytes of a wide coalesced read, WRITE_SIZE all of them (unit
+    # KiB): measured with a 1 GiB streaming read / write, FETCH_SIZE 0.500x, WRITE_SIZE 1.000x
+    # (tools/pmc_calibrate.py, profiles/r03_pmc_calibration.txt; MI355X_MICROARCH.md HBM section).
     traffic = (2.0 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024.0
     return {"fetch_kib": out["FETCH_SIZE"], "write_kib": out["WRITE_SIZE"], "bytes": traffic}, None
 
@@ -653,6 +654,7 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "traffic": round(pmc["bytes"]) if pmc else None,
+        "traffic_raw_kib": {"fetch_size": round(pmc["fetch_kib"]), "write_size": round(pmc["write_kib"])} if pmc else None,
         "algorithmic_bytes": B,
         "kernel_ms": round(t_raster_ms, 5),
     }
@@ -729,7 +731,9 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
                           "fused tonemap)", "bound": "hbm",
                 "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": round(pmc["bytes"]) if pmc else None, "algorithmic_bytes": B_k,
+                "traffic": round(pmc["bytes"]) if pmc else None,
+                "traffic_raw_kib": {"fetch_size": round(pmc["fetch_kib"]), "write_size": round(pmc["write_kib"])} if pmc else None,
+                "algorithmic_bytes": B_k,
                 "kernel_ms": round(t_k, 5), "frame_kernels_ms": round(t_frame, 5),
                 "frame_algorithmic_bytes": B_frame,
                 "frame_frac": round(B_frame / (t_frame * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if t_frame > 0 else None}
