@@ -1,6 +1,6 @@
 """Per-kernel dispatch statistics (count, median, mean, max in us) from a rocprofv3 results database
 (rocprofv3 --kernel-trace -d DIR -o NAME ...).
-usage: python tools/kstats.py DIR_OR_DB [name filter] [--skip-first K]
+usage: python tools/kstats.py DIR_OR_DB [name filter] [--skip-first K] [--last K]
 --skip-first K drops each kernel's first K dispatches (the warm-up launches before the timed loop)."""
 import csv
 import glob
@@ -18,6 +18,11 @@ def main():
     if "--skip-first" in args:
         i = args.index("--skip-first")
         skip = int(args[i + 1])
+        del args[i:i + 2]
+    last = 0
+    if "--last" in args:   # only each kernel's last K dispatches (bench.py's isolated kernel-timing leg)
+        i = args.index("--last")
+        last = int(args[i + 1])
         del args[i:i + 2]
     flt = args[0] if args else ""
     dbs = [path] if path.endswith(".db") else glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
@@ -38,6 +43,8 @@ def main():
             if flt and flt not in name:
                 continue
             v = np.array(v[skip:] if len(v) > skip else v)
+            if last and len(v) > last:
+                v = v[-last:]
             print(f"  {name[:70]:70s} n={len(v):5d} median={np.median(v):9.2f} mean={v.mean():9.2f} max={v.max():9.2f} us")
 
 
