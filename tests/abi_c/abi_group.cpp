@@ -201,7 +201,10 @@ int main(int argc, char **argv) {
         f.flags = SHS_LIB_DEPTH_MOTION | SHS_LIB_BG_GRADIENT;
         f.zn = 0.1f; f.zf = 200.0f;
         const size_t np = (size_t)W * H;
-        for (int fused = 0; fused < 2; ++fused) {
+        for (int lay = 0; lay < 4; ++lay) {   // (interleaved, regions) x (raw targets, fused tonemap)
+            const int layout = lay < 2 ? SHS_SHARD_INTERLEAVED : SHS_SHARD_REGIONS, fused = lay & 1;
+            const char *lname = layout == SHS_SHARD_REGIONS ? "regions" : "interleaved";
+            CK(shs_group_set_option(g_grp, SHS_OPT_SHARD_LAYOUT, layout));
             shs_tonemap_desc tm{1.0f, 2.2f, SHS_TONEMAP_PRESENT};
             CK(shs_lib_fuse_tonemap(g_ctx, fused ? &tm : nullptr));
             CK(shs_group_lib_fuse_tonemap(g_grp, fused ? &tm : nullptr));
@@ -222,7 +225,7 @@ int main(int argc, char **argv) {
                 CK(shs_resolve_ldr(g_ctx, nullptr, p1.data()));
                 CK(shs_resolve_ldr(root0, nullptr, pg.data()));
                 const size_t dp = count_diff(p1, pg);
-                std::printf("library fused tonemap %d ranks, 3rd frame: present %zu differing\n", n, dp);
+                std::printf("library fused tonemap %d ranks (%s), 3rd frame: present %zu differing\n", n, lname, dp);
                 EXPECT(dp == 0, "sharded present staging differs");
             } else {
                 CK(shs_resolve_lib(g_ctx, h1.data(), z1.data(), m1.data()));
@@ -230,10 +233,23 @@ int main(int argc, char **argv) {
                 const size_t dh = count_diff(h1, hg), dz = count_diff(z1, zg), dm = count_diff(m1, mgv);
                 size_t cov = 0;
                 for (float z : z1) cov += z < 1.0f;
-                std::printf("library %d ranks, 3rd frame: hdr %zu / depth %zu / motion %zu differing, %zu covered px\n", n, dh,
-                            dz, dm, cov);
+                std::printf("library %d ranks (%s), 3rd frame: hdr %zu / depth %zu / motion %zu differing, %zu covered px\n", n,
+                            lname, dh, dz, dm, cov);
                 EXPECT(dh == 0 && dz == 0 && dm == 0, "sharded library frame differs");
                 EXPECT(cov > 10000, "library frame nearly empty");
+            }
+            if (layout == SHS_SHARD_REGIONS) {   // the rectangles every rank used tile the bin grid exactly
+                std::vector<int32_t> rects((size_t)4 * n);
+                CK(shs_get_shard_regions(root0, n, rects.data()));
+                const int tx = (W + 31) / 32, ty = (H + 31) / 32;
+                std::vector<int> cover((size_t)tx * ty, 0);
+                for (int r = 0; r < n; ++r)
+                    for (int y = rects[4 * r + 1]; y <= rects[4 * r + 3]; ++y)
+                        for (int x = rects[4 * r]; x <= rects[4 * r + 2]; ++x)
+                            if (x >= 0 && x < tx && y >= 0 && y < ty) cover[(size_t)y * tx + x]++;
+                size_t bad = 0;
+                for (int c : cover) bad += c != 1;
+                EXPECT(bad == 0, "region layout does not tile the bin grid (%zu tiles)", bad);
             }
         }
     }

@@ -44,7 +44,8 @@ GROUP_EXE = os.path.join(ABI_C, "_build", "abi_group")
 @pytest.mark.parametrize("n", [8, 3])
 def test_abi_c_group_composes_sharded_frames(n):
     """A single-process C++ host drives N contexts through shs_group_* (VERDICT r2 item 6): the
-    gathered legacy, library and fused-tonemap frames equal the unsharded context's bit for bit.  On
+    gathered legacy, library and fused-tonemap frames -- interleaved tiles and the region layout, whose
+    ranks send packed tiles of different sizes -- equal the unsharded context's bit for bit.  On
     the 1-GPU box the N contexts share device 0 (the peer copies become device-local)."""
     assert os.path.exists(GROUP_EXE), "build tests/abi_c first (__graft_entry__.build())"
     r = subprocess.run([GROUP_EXE, ROOT, str(n)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
