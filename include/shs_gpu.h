@@ -218,6 +218,10 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 /* The regions of the last region-sharded camera pass: rects[4 r .. 4 r + 3] = (bx0, by0, bx1, by1) of
  * rank r, bin tiles, inclusive (bx1 < bx0: rank r owns nothing). */
 int shs_get_shard_regions(shs_ctx *ctx, int32_t shard_count, int32_t *rects);
+/* Host-only (no device): the region balance itself, for tests -- blocks[4 i .. 4 i + 3] = k_lib_setup's
+ * per-block record (bx0 | bx1 << 16, by0 | by1 << 16, triangles, 1 bounded / 2 estimate / 0 none). */
+int shs_shard_balance_rects(const uint32_t *blocks, int32_t n_blocks, int32_t width, int32_t height, int32_t shard_count,
+                            int32_t root_permille, int32_t *rects);
 
 /* Debug / profiling hook: the last frame's workgroup timeline.  out[0..7] = {k_setup grid, k_raster
  * grid, setup blocks, ghost blocks, clear blocks, stride S, 0, 0} (k_setup's block roles in that

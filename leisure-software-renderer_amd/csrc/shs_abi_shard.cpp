@@ -158,6 +158,22 @@ int shs_regions_next(shs_ctx *ctx, int count, int w, int h) {
 
 extern "C" {
 
+int shs_shard_balance_rects(const uint32_t *blocks, int32_t n_blocks, int32_t width, int32_t height, int32_t count,
+                            int32_t root_permille, int32_t *rects) {
+    if (width <= 0 || height <= 0 || count <= 0 || n_blocks < 0 || (n_blocks > 0 && !blocks) || !rects || root_permille < 0 ||
+        root_permille > 1000)
+        return SHS_ERR_INVALID;
+    const int tiles_x = (width + shs_dev::TILE - 1) / shs_dev::TILE, tiles_y = (height + shs_dev::TILE - 1) / shs_dev::TILE;
+    std::vector<ShardRegion> out;
+    shs_shard_balance(reinterpret_cast<const uint4 *>(blocks), n_blocks, tiles_x, tiles_y, width, height, count, out,
+                      root_permille / 1000.0);
+    for (int r = 0; r < count; ++r) {
+        rects[4 * r] = out[(size_t)r].x0; rects[4 * r + 1] = out[(size_t)r].y0;
+        rects[4 * r + 2] = out[(size_t)r].x1; rects[4 * r + 3] = out[(size_t)r].y1;
+    }
+    return SHS_OK;
+}
+
 int shs_get_shard_regions(shs_ctx *ctx, int32_t count, int32_t *rects) {
     if (!ctx || !rects || count <= 0) return SHS_ERR_INVALID;
     if (ctx->reg_last_count != count || (int)ctx->reg_last.size() != count) {

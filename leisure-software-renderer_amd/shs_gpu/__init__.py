@@ -484,6 +484,18 @@ class Context:
             raise ShsError(rc, "shs_tonemap_thresholds")
         return thr
 
+    @staticmethod
+    def shard_balance(blocks, width, height, count, root_share=1.0):
+        """Host-side region balance (shs_shard_balance_rects): blocks uint32 [n, 4] as k_lib_setup writes them
+        -> [(bx0, by0, bx1, by1)] per rank."""
+        b = np.ascontiguousarray(np.asarray(blocks, np.uint32).reshape(-1, 4))
+        out = np.zeros(4 * count, np.int32)
+        rc = lib().shs_shard_balance_rects(b.ctypes.data if b.size else None, b.shape[0], int(width), int(height), int(count),
+                                           int(round(root_share * 1000)), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        if rc != 0:
+            raise ShsError(rc, "shs_shard_balance_rects")
+        return [tuple(int(v) for v in out[4 * r:4 * r + 4]) for r in range(count)]
+
     LIB_TIMELINE_FIELDS = ("start", "end", "gather", "pairs", "shade", "clear", "n_busy", "n_clear", "chunks",
                            "n_pairs", "n_cand", "max_tile")
 

@@ -279,6 +279,8 @@ SIGNATURES = [
     ("shs_tiles_packed_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_tiles_rank_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_get_shard_regions", ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    ("shs_shard_balance_rects", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     ("shs_tiles_pack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
     ("shs_tiles_unpack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
     ("shs_lights_upload", ctypes.c_int, [_P, ctypes.POINTER(CullingLightC), ctypes.c_int32]),
