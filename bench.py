@@ -593,6 +593,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on a one-GPU box (tests only: every rank on device 0, gloo for the
+    # barrier and the max-over-ranks reduction); never used for a reported line
+    rehearse = os.environ.get("SHS_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local_rank = 0
+    args.reduce_device = "cpu" if rehearse else f"cuda:{local_rank}"   # where the timing reductions run
     if not args.child and world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch with --nproc-per-node equal to --gpus")
 
@@ -612,7 +618,7 @@ def main():
         import torch
         import torch.distributed as dist_mod
         torch.cuda.set_device(local_rank)
-        dist_mod.init_process_group("nccl")
+        dist_mod.init_process_group("gloo" if rehearse else "nccl")
         dist = dist_mod
 
     if args.config in LIB_CONFIGS:
@@ -626,10 +632,10 @@ def main():
     covered = stats["covered_pixels"]       # batch total
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=args.reduce_device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el_max = float(t.item())
-        c = torch.tensor([covered], dtype=torch.float64, device=f"cuda:{local_rank}")
+        c = torch.tensor([covered], dtype=torch.float64, device=args.reduce_device)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         covered_total = float(c.item())
     else:
@@ -712,10 +718,10 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     covered_total = float(stats["covered_pixels"])
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=args.reduce_device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el_max = float(t.item())
-        c = torch.tensor([covered_total], dtype=torch.float64, device=f"cuda:{local_rank}")
+        c = torch.tensor([covered_total], dtype=torch.float64, device=args.reduce_device)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         covered_total = float(c.item())
     if rank != 0:

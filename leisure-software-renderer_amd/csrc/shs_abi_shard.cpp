@@ -10,9 +10,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
-#include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -122,10 +119,7 @@ int shs_regions_next(shs_ctx *ctx, int count, int w, int h) {
     const int tiles_x = (w + shs_dev::TILE - 1) / shs_dev::TILE, tiles_y = (h + shs_dev::TILE - 1) / shs_dev::TILE;
     auto &wk = ctx->lib_cam;
     const bool have = wk.blkrect_valid && wk.blkrect_w == w && wk.blkrect_h == h && wk.h_blkrect;
-    static const bool dbg = std::getenv("SHS_DEBUG_REGIONS") != nullptr;
-    const auto c0 = std::chrono::steady_clock::now();
     if (have && wk.ov_valid) HIP_TRY(ctx, hipEventSynchronize(wk.ov_after));   // that pass's setup wrote them
-    const auto c1 = std::chrono::steady_clock::now();
     // the same bounds as last time (a static camera, or every rank's first frames): the same layout
     const int n_in = have ? wk.blkrect_n : 0;
     const bool same = ctx->reg_in_count == count && ctx->reg_in_w == w && ctx->reg_in_h == h &&
@@ -140,14 +134,6 @@ int shs_regions_next(shs_ctx *ctx, int count, int w, int h) {
         ctx->reg_in_w = w;
         ctx->reg_in_h = h;
         ctx->reg_in_root = ctx->shard_root_permille;
-    }
-    if (dbg) {
-        const auto c2 = std::chrono::steady_clock::now();
-        static double acc[2] = {0, 0};
-        static long n = 0;
-        acc[0] += std::chrono::duration<double, std::micro>(c1 - c0).count();
-        acc[1] += std::chrono::duration<double, std::micro>(c2 - c1).count();
-        if (++n % 100 == 0) std::fprintf(stderr, "regions_next: wait %.1f us, balance %.1f us (mean of 100)\n", acc[0] / 100, acc[1] / 100), acc[0] = acc[1] = 0;
     }
     ctx->reg_next_count = count;
     ctx->reg_next_w = w;
