@@ -339,6 +339,10 @@ constexpr int BIG_CAP = 512;
 // small; C4's 1M triangles otherwise hit each bin counter ~120 times).  List order inside a bin does
 // not matter: the raster resolves by (z, submission index) keys.
 constexpr int AGG_BINS = 256;             // union capacity in bin tiles (else the per-primitive path)
+#ifndef SHS_DEFER_BT
+#define SHS_DEFER_BT 2
+#endif
+constexpr int DEFER_BT = SHS_DEFER_BT;    // deferred primitives span at most DEFER_BT x DEFER_BT bin tiles
 struct Pend {
     uint32_t slot = 0;
     int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
@@ -356,7 +360,7 @@ struct SetupShared {
 
 __device__ __forceinline__ void lib_mark(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
                          uint32_t slot, SetupShared &ss, Pend &pend) {
-    if (!pend.valid && (x1 / TILE - x0 / TILE) < 2 && (y1 / TILE - y0 / TILE) < 2) {
+    if (!pend.valid && (x1 / TILE - x0 / TILE) < DEFER_BT && (y1 / TILE - y0 / TILE) < DEFER_BT) {
         pend.slot = slot; pend.x0 = x0; pend.x1 = x1; pend.y0 = y0; pend.y1 = y1; pend.valid = true;
         return;
     }
@@ -662,7 +666,7 @@ __device__ int setup_deferred(const LibFrameParams &fp, const LibBuffers &fb, ui
     const bool sharded = fp.count > 1;
     constexpr int RPB = TILE / LIB_RTH;                        // raster rows per bin tile
     const int bx0 = pend.x0 / TILE, by0 = pend.y0 / TILE, bx1 = pend.x1 / TILE, by1 = pend.y1 / TILE;
-    uint32_t pos[2][2] = {{0u, 0u}, {0u, 0u}};
+    uint32_t pos[DEFER_BT][DEFER_BT] = {};
     if (pend.valid) {
         if (!agg) {
             lib_mark_range(fp, fb, cnt, pend.x0, pend.x1, pend.y0, pend.y1, pend.slot, 0, 1);
@@ -675,9 +679,9 @@ __device__ int setup_deferred(const LibFrameParams &fp, const LibBuffers &fb, ui
             }
             if (!fp.scan_mode) {
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < DEFER_BT; ++j)
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
+                    for (int i = 0; i < DEFER_BT; ++i)
                         if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j)))
                             pos[j][i] = atomicAdd(&ss.bcnt[(by0 + j - uby0) * uw + (bx0 + i - ubx0)], 1u);
             }
@@ -699,9 +703,9 @@ __device__ int setup_deferred(const LibFrameParams &fp, const LibBuffers &fb, ui
         __syncthreads();
         if (pend.valid && !fp.scan_mode) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < DEFER_BT; ++j)
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < DEFER_BT; ++i)
                     if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j))) {
                         const int u = (by0 + j - uby0) * uw + (bx0 + i - ubx0);
                         lib_append_bin(fp, fb, cnt, (by0 + j) * fp.tiles_x + bx0 + i, ss.bcnt[u] + pos[j][i], pend.slot);
