@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "shs_device.hpp"
 #include "shs_lib_device.hpp"
@@ -1550,21 +1551,26 @@ struct LibShared {
     float4 rec[LIB_CHUNK * 4];            // staged records (8 KB)
     unsigned long long key[LIB_RTH * LIB_RTW];
     unsigned long long bits[LIB_PAIR_WORDS]; // bit k: a surviving candidate's pairs start at pair k (4 KB)
-    uint4 pinfo[LIB_CHUNK];               // per surviving candidate: first pair, x0 | y0 << 16, width | slot << 16, 2^16/width
+    // deep raster: per nonempty row span (segment) first pair | x0 << 16 | row << 21 | slot << 24;
+    // shallow: per staged box (uint4 pinfo) first pair, x0 | y0 << 16, width | slot << 16, 2^16/width
+    alignas(16) uint32_t seg[LIB_CAND == LIB_CAND_DEEP ? LIB_CHUNK * LIB_RTH : LIB_CHUNK * 4];
     uint32_t zord[LIB_CHUNK];             // per staged candidate: its depth bound (0: never skipped)
     uint2 lbox[LIB_CAND];                 // the tile's candidate list, front to back: boxes,
     uint32_t lid[LIB_CAND];               //   slots
     uint32_t lkey[LIB_CAND];              //   and depth bounds (lib_zmin_ord; 0 without a depth test)
     uint32_t sel[LIB_CHUNK];              // list positions staged by the current pass
-    uint32_t hist[256];                   // depth buckets: counts, then first positions
+    union alignas(16) {   // span rows are read 8 at a time (ds_read_b128)
+        uint32_t hist[256];               // depth buckets: counts, then first positions (the sort)
+        uint16_t span[LIB_CHUNK * LIB_RTH]; // staging passes: row spans of the staged boxes (x0 | x1 << 8, tile-relative)
+    };
     uint32_t zlo, zhi;
-    int busy[256];
     uint32_t wtot[4][2];                  // per wave: surviving candidates, pairs
     uint32_t colmax[2][LIB_RTW];          // per pixel column: max key z (orderable bits) over its rows, by chunk parity
     uint32_t nc, nbusy, cov, maxbin, npairs;
     int next[3];                          // the workgroup's next run, queue, queues tried
     uint64_t tl[LTL_STRIDE];              // SHS_OPT_TIMELINE accumulators (thread 0)
-    uint8_t wown[LIB_PAIR_WORDS];         // surviving candidate owning each bitmap word's first pair
+    // segment (deep) or staged box (shallow) owning each bitmap word's first pair
+    typename std::conditional<LIB_CAND == LIB_CAND_DEEP, uint16_t, uint8_t>::type wown[LIB_PAIR_WORDS];
 };
 
 
@@ -1658,6 +1664,46 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
         const f3 c = lib_fragment<PROG>(fp, fb, dr, world, nrm, z01, px, py, st, tex);
         color = make_float4(c.x, c.y, c.z, 1.0f);
     }
+}
+
+// Conservative row span of a staged primitive inside its clipped box [bx0, bx1]: the pixels of row py
+// that can pass lib_test's inside test.  With t = px + 0.5 - ax, dy = py + 0.5 - ay the exact
+// barycentrics of the record's float values are linear in t:
+//   v = av t + cv dy,  w = aw t + cw dy,  u = 1 + au t + cu dy,
+//   av = id v1y, cv = -id v1x, aw = -id v0y, cw = id v0x, au = id (v0y - v1y), cu = id (v1x - v0x).
+// lib_test's float evaluation (no contraction) is within 4 u Mv of v, Mv = |id| (|v1y t| + |v1x dy|)
+// (u = 2^-24; likewise w), and u's within 4 u (1 + 2 Mv + 2 Mw); a pixel can pass only where every
+// exact barycentric is >= minus its bound.  Each half-line a t >= -e - c is solved here in float with
+// e = E (...) at E = 2^-18, 16x the bound: the slack absorbs this computation's own roundings (a few
+// ulps of |e| + |c|, divided by a), and 2^-12 px more covers the conversion to pixel indices.
+// Non-finite inputs keep the whole box row.
+__device__ __forceinline__ void lib_row_span(const float4 *rec, int py, int bx0, int bx1, int &x0, int &x1) {
+    x0 = bx0; x1 = bx1;
+    const float4 r0 = rec[0], r1 = rec[1];   // ax ay v0x v0y | v1x v1y inv_den z0
+    const float ax = r0.x, ay = r0.y, v0x = r0.z, v0y = r0.w, v1x = r1.x, v1y = r1.y, id = r1.z;
+    if (!(isfinite(ax) && isfinite(ay) && isfinite(v0x) && isfinite(v0y) && isfinite(v1x) && isfinite(v1y) && isfinite(id)))
+        return;
+    constexpr float E = 0x1p-18f;
+    const float dy = ((float)py + 0.5f) - ay, ady = fabsf(dy);
+    const float T = fmaxf(fabsf(((float)bx0 + 0.5f) - ax), fabsf(((float)bx1 + 0.5f) - ax));
+    const float aid = fabsf(id);
+    const float mv = aid * (fabsf(v1y) * T + fabsf(v1x) * ady), mw = aid * (fabsf(v0y) * T + fabsf(v0x) * ady);
+    float lo = -1e30f, hi = 1e30f;
+    // a t + c >= -e: a > 0: t >= (-e - c) / a; a < 0: t <= (-e - c) / a; a == 0: all or none
+    auto edge = [&](float a, float c, float e) {
+        const float b = -e - c;
+        if (a > 0.0f) lo = fmaxf(lo, b / a);
+        else if (a < 0.0f) hi = fminf(hi, b / a);
+        else if (b > 0.0f) { lo = 1e30f; hi = -1e30f; }
+    };
+    edge(id * v1y, -id * v1x * dy, E * mv);
+    edge(-id * v0y, id * v0x * dy, E * mw);
+    edge(id * (v0y - v1y), 1.0f + id * (v1x - v0x) * dy, E * (1.0f + 2.0f * (mv + mw)));
+    // pixels with px + 0.5 - ax in [lo, hi]
+    const float flo = (lo + ax) - 0.5f, fhi = (hi + ax) - 0.5f;
+    const float slo = 0x1p-12f * (fabsf(lo) + fabsf(ax) + 1.0f), shi = 0x1p-12f * (fabsf(hi) + fabsf(ax) + 1.0f);
+    x0 = max(bx0, (int)ceilf(fmaxf(fminf(flo - slo, 1e9f), -1e9f)));
+    x1 = min(bx1, (int)floorf(fmaxf(fminf(fhi + shi, 1e9f), -1e9f)));
 }
 
 // One work item: raster tile rt, or (k_lib_plan) part `part` of `parts` (2: the 32x4 halves, 4: the
@@ -1888,10 +1934,95 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 }
             }
             __syncthreads();
-            // Pair tasks: the staged boxes laid end to end (block prefix of the areas); every
-            // (primitive, pixel) pair is dealt to one lane, 64-pair windows round-robin over the
+            // Pair tasks.  Deep camera-pass raster (C4: many small primitives per tile): each staged
+            // box's rows narrowed to conservative spans (lib_row_span), the nonempty spans (segments)
+            // laid end to end (block prefix of (pairs, segments) per primitive).  Shallow raster and
+            // shadow pass (C5: few, mostly large primitives; the span arithmetic would spill the shallow
+            // raster's 80 registers, and measured 10 % slower on C5's shadow map): the boxes laid end to end.
+            // Every (primitive, pixel) pair is dealt to one lane, 64-pair windows round-robin over the
             // waves (start bitmap + word owners, as in shs_legacy.hip).
-            {
+            if constexpr (LIB_CAND == LIB_CAND_DEEP && !SHADOW) {
+                // the spans, one (staged primitive, row) per thread and step
+                for (int i = tid; i < (int)m * LIB_RTH; i += 256) {
+                    const int c = i / LIB_RTH, py = TY0 + i % LIB_RTH;
+                    const uint2 b = sh.lbox[sh.sel[c]];
+                    const int x0 = max(lo16(b.x), X0), x1 = min(hi16(b.x), X1);
+                    const int y0 = max(lo16(b.y), Y0), y1 = min(hi16(b.y), Y1);
+                    int s0 = 1, s1 = 0;
+                    if (py >= y0 && py <= y1) lib_row_span(&sh.rec[c * 4], py, x0, x1, s0, s1);
+                    sh.span[i] = s1 >= s0 ? (uint16_t)((s0 - TX0) | ((s1 - TX0) << 8)) : (uint16_t)0x001fu;   // empty: 31 > 0
+                }
+                __syncthreads();
+                uint4 spv = make_uint4(0x001f001fu, 0x001f001fu, 0x001f001fu, 0x001f001fu);
+                uint32_t pk = 0u;   // pairs << 11 | segments
+                if (tid < (int)m) {
+                    sh.zord[tid] = sh.lkey[sh.sel[tid]];
+                    spv = reinterpret_cast<const uint4 *>(sh.span)[tid];
+#pragma unroll
+                    for (int r = 0; r < LIB_RTH; ++r) {
+                        const uint32_t wv = r < 2 ? spv.x : r < 4 ? spv.y : r < 6 ? spv.z : spv.w;
+                        const uint32_t e = (wv >> (16 * (r & 1))) & 0xffffu;
+                        const int s0 = (int)(e & 0xffu), s1 = (int)(e >> 8);
+                        if (s1 >= s0) pk += ((uint32_t)(s1 - s0 + 1) << 11) + 1u;
+                    }
+                }
+                uint32_t incl = pk;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t vv = (uint32_t)__shfl_up((int)incl, o);
+                    if (lane >= o) incl += vv;
+                }
+                if (lane == 63) sh.wtot[wave][1] = incl;
+                __syncthreads();
+                uint32_t pbase = 0, ptot = 0;
+#pragma unroll
+                for (int w2 = 0; w2 < 4; ++w2) {
+                    const uint32_t p2 = sh.wtot[w2][1];
+                    if (w2 < wave) pbase += p2;
+                    ptot += p2;
+                }
+                if (pk) {
+                    const uint32_t ex = pbase + incl - pk;
+                    uint32_t ps = ex >> 11, sg = ex & 2047u;
+#pragma unroll
+                    for (int r = 0; r < LIB_RTH; ++r) {
+                        const uint32_t wv = r < 2 ? spv.x : r < 4 ? spv.y : r < 6 ? spv.z : spv.w;
+                        const uint32_t e = (wv >> (16 * (r & 1))) & 0xffffu;
+                        const int s0 = (int)(e & 0xffu), s1 = (int)(e >> 8);
+                        if (s1 < s0) continue;
+                        const uint32_t wdt = (uint32_t)(s1 - s0 + 1);
+                        sh.seg[sg] = ps | ((uint32_t)s0 << 16) | ((uint32_t)r << 21) | ((uint32_t)tid << 24);
+                        atomicOr(&sh.bits[ps >> 6], 1ull << (ps & 63u));
+                        for (uint32_t wd = (ps + 63u) >> 6; wd * 64u < ps + wdt; ++wd) sh.wown[wd] = (uint16_t)sg;
+                        ps += wdt;
+                        ++sg;
+                    }
+                }
+                __syncthreads();
+                const int total = (int)(ptot >> 11);
+                if (tlon) sh.tl[LTL_NPAIRS] += (uint32_t)total;
+                const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
+                // one pair: its segment (word's first owner + starts up to it), pixel, then the test
+                auto pair = [&](int k0) {
+                    const int k = k0 + lane;
+                    if (k >= total) return;
+                    const unsigned long long wb = sh.bits[k0 >> 6];
+                    const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
+                    const uint32_t sgi = sh.seg[o];
+                    const int lx = (int)((sgi >> 16) & 31u) + (k - (int)(sgi & 0xffffu)), ly = (int)((sgi >> 21) & 7u);
+                    const int slot = (int)(sgi >> 24);
+                    const int kp = ly * LIB_RTW + lx;
+                    // per-pixel hierarchical z: the pixel's current key already beats the
+                    // primitive's depth bound (a stale, higher key only skips less)
+                    if (sh.zord[slot] > reinterpret_cast<const uint32_t *>(sh.key)[2 * kp + 1]) return;
+                    const LibRec r = lib_rec_from(&sh.rec[slot * 4]);
+                    float z01, u, v, w, idn;
+                    if (lib_test<SHADOW>(fp, r, TX0 + lx, TY0 + ly, z01, u, v, w, idn))
+                        atomicMin(&sh.key[kp], lib_key(fp, z01, r.seq, SHADOW));
+                };
+                for (int k0 = 64 * wave; k0 < total; k0 += 256) pair(k0);
+            } else {
+                uint4 *pinfo = reinterpret_cast<uint4 *>(sh.seg);   // per staged box: first pair, x0 | y0 << 16, width | slot << 16, 2^16/width
                 int area = 0, bx0 = 0, by0 = 0, bw = 1;
                 uint32_t zord = 0u;
                 if (tid < (int)m) {
@@ -1919,7 +2050,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 }
                 if (area > 0) {
                     const int start = (int)pbase + incl - area;
-                    sh.pinfo[tid] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16),
+                    pinfo[tid] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16),
                                                (uint32_t)bw | ((uint32_t)tid << 16), (65536u + (uint32_t)bw - 1u) / (uint32_t)bw);
                     sh.zord[tid] = zord;
                     atomicOr(&sh.bits[start >> 6], 1ull << (start & 63));
@@ -1935,7 +2066,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                     if (k >= total) return;
                     const unsigned long long wb = sh.bits[k0 >> 6];
                     const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
-                    const uint4 pi = sh.pinfo[o];
+                    const uint4 pi = pinfo[o];
                     const int local = k - (int)pi.x, ow = (int)(pi.z & 0xffffu);
                     const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * ow;
                     const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
