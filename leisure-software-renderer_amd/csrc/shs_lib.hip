@@ -1268,12 +1268,13 @@ __device__ float shadow_visibility(const LibFrameParams &fp, const LibBuffers &f
     return (float)lit / (float)count;
 }
 
-// x^5 as (x^2)^2 x: within 3.5 ulp relative of the exact power (libm's powf(x, 5.0f) within 1), far
-// inside the 1e-5 bar for the Schlick factors (|x| <= 1 up to rounding), at 3 multiplications instead of
-// a general powf's log / exp evaluation.
+// x^5 by (x^2)^2 x in double, narrowed to float: x^2 is exact and the two other products carry 2^-53
+// each, so the float result is the correctly rounded power (libm's powf(x, 5.0f)) except within ~1e-15
+// relative of a float rounding boundary -- at a few multiplications instead of a general powf's log / exp
+// evaluation (the device powf itself is not correctly rounded).
 __device__ __forceinline__ float pow5(float x) {
-    const float x2 = x * x;
-    return (x2 * x2) * x;
+    const double d = (double)x, d2 = d * d;
+    return (float)((d2 * d2) * d);
 }
 
 // eval_fake_ibl (builtin_shaders.hpp:57-85)
