@@ -248,10 +248,32 @@ class LibSlot:
                                                       out=self.gbufs[0])
 
 
-def lib_timed_loop(args, slots, frame_fn, dist):
+def camera_phase_bytes(width, height, owned_px, shadow_size=None):
+    """Algorithmic bytes of one camera pass's raster phase (k_lib_raster + k_lib_resolve) on one rank:
+    per OWNED pixel HDR 16 + depth 4 + motion 8 + the fused tonemap's RGBA8 present 4 = 32 B (SURVEY
+    8d); C5 adds the shadow map's PCF reads, 4 B/texel once, apportioned to the rank's pixel share.  At
+    N = 1 owned_px = width * height; at N > 1 it is rank 0's share (shard.owned_pixels), the pixels
+    rank 0's timed kernels actually produce."""
+    b = owned_px * 32
+    if shadow_size:
+        b += shadow_size * shadow_size * 4 * owned_px // (width * height)
+    return b
+
+
+def rank_owned_pixels(ctx, frame, rank, world, regions_layout):
+    """Pixels `rank` renders in the last camera pass of ctx (its region rectangle, or tile % world)."""
+    from shs_gpu import shard
+    if world <= 1:
+        return frame.width * frame.height
+    regions = ctx.shard_regions(world) if regions_layout else None
+    return shard.owned_pixels(frame.width, frame.height, 32, rank, world, regions)
+
+
+def lib_timed_loop(args, slots, frame_fn, dist, frame=None, rank=0, world=1):
     """Warm-up, then exactly args.steps frames round-robin over the slots (frame i on slot i % D) between
     two barriers; then kernel event times of 20 frames on slot 0 alone (nothing else in flight: the
-    roofline's kernel durations).  -> (elapsed s, stats, (n_frames, kms))"""
+    roofline's kernel durations).  -> (elapsed s, stats, (n_frames, kms), pixels this rank owned in the
+    timed kernels' passes)"""
     D = len(slots)
     for i in range(max(args.warmup, D)):
         frame_fn(slots[i % D])
@@ -279,9 +301,12 @@ def lib_timed_loop(args, slots, frame_fn, dist):
     barrier_sync()
     n_passes, kms = ctx.lib_timing_read()
     ctx.enable_timing(False)
+    owned = None
+    if frame is not None:
+        owned = rank_owned_pixels(ctx, frame, rank, world, dist is not None and args.shard_layout == "regions")
     for sl in slots:
         sl.ctx.close()
-    return elapsed, stats, (n_passes["camera"], kms)
+    return elapsed, stats, (n_passes["camera"], kms), owned
 
 
 def run_gpu_c4(args, rank, local_rank, world, dist):
@@ -310,13 +335,14 @@ def run_gpu_c4(args, rank, local_rank, world, dist):
         if dist is not None:
             sl.gather(dist)
 
-    elapsed, stats, (n_cam, kms) = lib_timed_loop(args, slots, one_frame, dist)
+    elapsed, stats, (n_cam, kms), owned = lib_timed_loop(args, slots, one_frame, dist, frame, rank, world)
     kms = {"setup": kms["setup"], "raster": kms["raster"]}
     n_tri = sum(d.mesh.n_tris for d in draws)
-    # the raster phase writes HDR + depth + motion (28 B/px) and the fused tonemap's RGBA8 present staging (4 B/px)
-    B_cam_raster = frame.width * frame.height * 32
+    # the raster phase writes HDR + depth + motion (28 B/px) and the fused tonemap's RGBA8 present staging
+    # (4 B/px) for the pixels this rank owns
+    B_cam_raster = camera_phase_bytes(frame.width, frame.height, owned)
     B_frame = n_tri * 72 + frame.width * frame.height * 32 + len(lights) * 160 + cull.n_lists * 4
-    return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, None
+    return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, None, owned
 
 
 def lib_mesh_bytes(mesh, with_attrs=True):
@@ -358,12 +384,12 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
         if dist is not None:
             sl.gather(dist)
 
-    elapsed, stats, (n_cam, kms) = lib_timed_loop(args, slots, one_frame, dist)
-    B_cam_raster = frame.width * frame.height * 32 + S * S * 4
+    elapsed, stats, (n_cam, kms), owned = lib_timed_loop(args, slots, one_frame, dist, frame, rank, world)
+    B_cam_raster = camera_phase_bytes(frame.width, frame.height, owned, S)
     B_frame = (sum(lib_mesh_bytes(d.mesh) for d in draws) + sum(lib_mesh_bytes(c.mesh, False) for c in casters)
                + 2 * S * S * 4 + frame.width * frame.height * 32)
     n_tri = sum(d.mesh.n_tris for d in draws)
-    return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, S
+    return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, S, owned
 
 
 def collect_pmc(args):
@@ -712,7 +738,7 @@ def main():
 
 def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     runner = run_gpu_c4 if args.config == "c4" else run_gpu_lib
-    frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, S = runner(args, rank, local_rank, world, dist)
+    frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, S, owned = runner(args, rank, local_rank, world, dist)
     world_tri = n_tri              # one frame per step, split over the ranks at N > 1 (strong scaling)
     el_max = elapsed
     covered_total = float(stats["covered_pixels"])
@@ -733,6 +759,9 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     t_k = kms["raster"]
     achieved = B_k / (t_k * 1e-3) / 1e9 if t_k > 0 else None
     t_frame = sum(kms.values())
+    # at N > 1 the timed kernels are rank 0's: its frame bytes are the whole frame's minus the 32 B of
+    # every pixel another rank renders (geometry and the shadow map are still read whole on every rank)
+    B_frame -= (frame.width * frame.height - owned) * 32
     roofline = {"kernel": "k_lib_raster<false> + k_lib_resolve (camera pass raster phase: coverage, then shading + "
                           "fused tonemap)", "bound": "hbm",
                 "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -741,6 +770,7 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
                 "traffic_raw_kib": {"fetch_size": round(pmc["fetch_kib"]), "write_size": round(pmc["write_kib"])} if pmc else None,
                 "algorithmic_bytes": B_k,
                 "kernel_ms": round(t_k, 5), "frame_kernels_ms": round(t_frame, 5),
+                "rank0_owned_pixels": owned,
                 "frame_algorithmic_bytes": B_frame,
                 "frame_frac": round(B_frame / (t_frame * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if t_frame > 0 else None}
     if pmc is None:

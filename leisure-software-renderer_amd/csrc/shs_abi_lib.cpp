@@ -707,12 +707,21 @@ int shs_texture_upload(shs_ctx *ctx, const uint8_t *rgba, int32_t w, int32_t h, 
     Texture t;
     const size_t bytes = (size_t)w * h * 4;
     HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&t.texels), bytes));
-    HIP_TRY(ctx, hipMemcpy(t.texels, rgba, bytes, hipMemcpyHostToDevice));
+    const hipError_t e = hipMemcpy(t.texels, rgba, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(t.texels);
+        ctx->err = hipGetErrorString(e);
+        return SHS_ERR_HIP;
+    }
     t.w = w;
     t.h = h;
     t.live = true;
-    ctx->textures.push_back(t);
-    *tex_id = (int32_t)ctx->textures.size();   // TextureAssetHandle convention: 1-based, 0 = none
+    // a released slot is reused (ids stay small); TextureAssetHandle convention: 1-based, 0 = none
+    size_t slot = 0;
+    while (slot < ctx->textures.size() && ctx->textures[slot].live) ++slot;
+    if (slot == ctx->textures.size()) ctx->textures.push_back(t);
+    else ctx->textures[slot] = t;
+    *tex_id = (int32_t)slot + 1;
     return SHS_OK;
 }
 
@@ -994,7 +1003,24 @@ int shs_light_cull(shs_ctx *ctx, const shs_light_cull_desc *d) {
         ctx->err = "tiled-depth culling needs a library frame with a depth target of the same size";
         return SHS_ERR_INVALID;
     }
+    if (d->mode == 2u && d->shard_count > 1 && ctx->shard_layout == SHS_SHARD_REGIONS) {
+        // the depth ranges come from the previous camera pass's depth, which a region rank holds only for
+        // its previous rectangle; rectangles move between passes, so a newly owned tile would read stale
+        // depth.  Interleaved ownership is static and keeps the depth of every owned tile.
+        ctx->err = "tiled-depth culling needs the interleaved shard layout (region rectangles move between passes)";
+        return SHS_ERR_INVALID;
+    }
+    if (d->mode == 2u && d->shard_count > 1 && (32u % d->tile_size) == 0u && ((uint32_t)d->height % 32u) % d->tile_size != 0u) {
+        // light tiles count rows top-down, bin tiles bottom-up: at this height a light tile straddles two
+        // bin rows, i.e. two ranks' pixels, and its depth range would read the other rank's stale depth
+        ctx->err = "sharded tiled-depth culling needs height % 32 to be a multiple of the light tile size";
+        return SHS_ERR_INVALID;
+    }
     if (set_dev(ctx)) return SHS_ERR_HIP;
+    if (d->mode == 2u) {   // the depth it reduces must be final: an overflowed camera pass is re-issued first
+        const int rc = check_superseded(ctx, ctx->lib_cam);
+        if (rc) return rc;
+    }
     shs_dev::LightCullParams p;
     std::memset(&p, 0, sizeof p);
     p.W = d->width; p.H = d->height;

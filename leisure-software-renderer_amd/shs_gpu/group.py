@@ -127,6 +127,17 @@ class Group:
         for r in self.ranks:
             r._tonemap_flags = d.flags
 
+    def set_option(self, option, value):
+        """shs_group_set_option: shs_set_option on every rank's context."""
+        self._check(self._lib.shs_group_set_option(self._h, int(option), int(value)))
+
+    def set_shard_layout(self, regions: bool, root_share: float = None):
+        """SHS_OPT_SHARD_LAYOUT on every rank: interleaved tiles (default) or one cost-balanced rectangle
+        per rank; root_share: SHS_OPT_SHARD_ROOT_SHARE (rank 0's share, it also composes the gather)."""
+        self.set_option(_abi.OPT_SHARD_LAYOUT, _abi.SHARD_REGIONS if regions else _abi.SHARD_INTERLEAVED)
+        if root_share is not None:
+            self.set_option(_abi.OPT_SHARD_ROOT_SHARE, int(round(root_share * 1000)))
+
     # -- sharded passes ---------------------------------------------------------------------------
     def light_cull(self, cull):
         self._check(self._lib.shs_group_light_cull(self._h, ctypes.byref(cull.desc())))

@@ -33,6 +33,17 @@ def owned_tiles(width, height, tile, rank, count, regions=None):
     return np.arange(rank, tx * ty, count, dtype=np.int64)
 
 
+def owned_pixels(width, height, tile, rank, count, regions=None):
+    """Pixels of the frame that `rank` renders (its owned tiles clipped to the frame): the share of a
+    sharded camera pass's per-pixel algorithmic bytes that one rank's kernels move (bench.py's N > 1
+    roofline)."""
+    n = 0
+    for t in owned_tiles(width, height, tile, rank, count, regions):
+        y0, y1, x0, x1 = _tile_slices(int(t), width, height, tile)
+        n += (y1 - y0) * (x1 - x0)
+    return n
+
+
 def _tile_slices(t, width, height, tile):
     tx = (width + tile - 1) // tile
     x0, y0 = (t % tx) * tile, (t // tx) * tile
@@ -137,19 +148,41 @@ def gather_frame_device(dist, ctx, target, stream=None, out=None):
     s = stream if stream is not None else torch.cuda.current_stream()
     if ctx.stream != s.cuda_stream:
         ctx.set_stream(s.cuda_stream)
-    words = ctx.tiles_packed_words(target, count)
-    sizes = [ctx.tiles_rank_words(target, r, count) for r in range(count)]
-    dev = torch.device("cuda", torch.cuda.current_device())
-    if out is None or out[0].numel() < words:
-        out = [torch.empty(words, dtype=torch.int32, device=dev) for _ in range(count + 1)]
-    buf = out[0]
-    ctx.tiles_pack(target, rank, count, buf.data_ptr())
-    send_to_root(dist, buf, out[1:], sizes)
-    if rank == 0:
-        for r in range(1, count):
-            if sizes[r] > 0:
-                ctx.tiles_unpack(target, r, count, out[1 + r].data_ptr())
+    ensure_group_ready(dist)
+    # everything below -- pack, the point-to-point batch (RCCL enqueues on the current stream; the gloo
+    # staging copies too) and the unpacks -- is ordered on s, whichever stream the caller has current
+    with torch.cuda.stream(s):
+        words = ctx.tiles_packed_words(target, count)
+        sizes = [ctx.tiles_rank_words(target, r, count) for r in range(count)]
+        dev = torch.device("cuda", torch.cuda.current_device())
+        if out is None or out[0].numel() < words:
+            out = [torch.empty(words, dtype=torch.int32, device=dev) for _ in range(count + 1)]
+        buf = out[0]
+        ctx.tiles_pack(target, rank, count, buf.data_ptr())
+        send_to_root(dist, buf, out[1:], sizes)
+        if rank == 0:
+            for r in range(1, count):
+                if sizes[r] > 0:
+                    ctx.tiles_unpack(target, r, count, out[1 + r].data_ptr())
     return out
+
+
+_READY = set()
+
+
+def ensure_group_ready(dist):
+    """One barrier per process group before its first point-to-point batch.  batch_isend_irecv must be
+    joined by every rank when it is the group's first NCCL collective, but a rank whose region is empty
+    (or rank 0 with no non-empty peer) posts no operation at all; a barrier first makes the batches
+    ordinary point-to-point traffic on an initialised communicator."""
+    world = getattr(getattr(dist, "group", None), "WORLD", None)   # the default group (a new one after re-init)
+    key = id(world if world is not None else dist)
+    if key in _READY:
+        return
+    barrier = getattr(dist, "barrier", None)
+    if barrier is not None:
+        barrier()
+    _READY.add(key)
 
 
 def send_to_root(dist, buf, recvs, sizes):

@@ -30,3 +30,20 @@ def test_bench_world_mismatch_is_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--launch-dry-run"],
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_camera_phase_bytes_scale_with_owned_pixels():
+    """bench.py's library roofline at N > 1: rank 0's timed raster phase is priced
+    at the 32 B of each pixel it owns, not the whole frame's, so `frac` does not grow with N."""
+    import bench
+    from shs_gpu import shard
+    W, H, S = 3840, 2160, 2048
+    full = bench.camera_phase_bytes(W, H, W * H)
+    assert full == W * H * 32
+    assert bench.camera_phase_bytes(W, H, W * H, S) == W * H * 32 + S * S * 4
+    for n in (2, 4, 8):
+        shares = [bench.camera_phase_bytes(W, H, shard.owned_pixels(W, H, 32, r, n)) for r in range(n)]
+        assert sum(shares) == full
+        assert max(shares) <= full // n + 120 * 32 * 32 * 32    # within one tile row of an even split
+        with_shadow = [bench.camera_phase_bytes(W, H, shard.owned_pixels(W, H, 32, r, n), S) for r in range(n)]
+        assert abs(sum(with_shadow) - (full + S * S * 4)) < n   # the shadow reads apportioned, floor per rank

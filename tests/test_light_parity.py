@@ -125,3 +125,54 @@ def test_c4_full_size_properties(gpu_ctx):
     assert np.array_equal(h1.view(np.uint32), h2.view(np.uint32)) and np.array_equal(d1.view(np.uint32), d2.view(np.uint32))
     cov = d1 < 1.0
     assert cov.sum() > 500_000 and np.isfinite(h1[cov]).all() and (h1[cov][:, :3] <= 1.0).all()
+
+
+def test_tiled_depth_cull_sharded(oracle_mod):
+    """tiled-depth-range culling (mode 2) reads the previous camera pass's depth.  Sharded over
+    3 ranks with the interleaved layout (static ownership: a rank keeps the depth of every tile it owns)
+    for 3 frames, each rank's own lists equal the oracle's lists over the same depth; the region layout,
+    whose rectangles move between passes, is refused instead of reading stale depth."""
+    import shs_gpu
+    from test_shipped_frames import _owned_light_lists
+    count = 3
+    frame, draws, lights, cull = _small_c4(2, W=480, H=272)   # 272 % 32 = 16: light tiles inside one bin row
+    ref = shs_gpu.Context(0)
+    ctxs = [shs_gpu.Context(0) for _ in range(count)]
+    try:
+        ref.render_pbr_forward(frame, _prepass(draws))
+        _, depth, _ = ref.resolve_lib()                      # the depth prepass every frame re-renders
+        rc, ri, _ = oracle_mod.light_cull(cull, lights, depth)
+        for c in ctxs:
+            c.upload_lights(lights)
+        for it in range(3):
+            for r, c in enumerate(ctxs):
+                frame.shard_rank, frame.shard_count = r, count
+                cull.shard_rank, cull.shard_count = r, count
+                c.render_pbr_forward(frame, _prepass(draws))   # the rank's owned tiles of the prepass
+                c.light_cull(cull)
+                gc, gi, _ = c.resolve_light_lists()
+                own = _owned_light_lists(cull, r, count)
+                assert own.any()
+                assert np.array_equal(gc[own], rc[own]), f"frame {it} rank {r}: counts differ"
+                for l in np.nonzero(own & (rc > 0))[0]:
+                    assert np.array_equal(gi[l, :rc[l]], ri[l, :rc[l]]), f"frame {it} rank {r}: list {l}"
+        regional = ctxs[0]
+        regional.set_shard_layout(True)
+        frame.shard_rank, frame.shard_count = 0, count
+        cull.shard_rank, cull.shard_count = 0, count
+        regional.render_pbr_forward(frame, _prepass(draws))
+        with pytest.raises(shs_gpu.ShsError):
+            regional.light_cull(cull)
+        # at 480x270 a 16-px light tile straddles two bin rows (two ranks' depth): refused as well
+        frame2, draws2, _, cull2 = _small_c4(2, W=480, H=270)
+        c = ctxs[1]
+        frame2.shard_rank, frame2.shard_count = 1, count
+        cull2.shard_rank, cull2.shard_count = 1, count
+        c.render_pbr_forward(frame2, _prepass(draws2))
+        with pytest.raises(shs_gpu.ShsError):
+            c.light_cull(cull2)
+    finally:
+        for c in ctxs + [ref]:
+            c.close()
+        frame.shard_rank, frame.shard_count = 0, 1
+        cull.shard_rank, cull.shard_count = 0, 1

@@ -136,6 +136,7 @@ def _gloo_padded_worker(rank, world, port, q, present=False, regions=False):
         buf[:mine.size] = mine
         t = torch.from_numpy(buf.view(np.int32))
         recvs = [torch.zeros_like(t) for _ in range(world)]
+        shard.ensure_group_ready(dist)   # what gather_frame_device does before the first batch
         shard.send_to_root(dist, t, recvs, sizes)
         if rank == 0:
             out = np.zeros_like(color)
@@ -163,3 +164,23 @@ def test_gloo_device_protocol_gather(present, regions, world):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert all(q.get(timeout=5) for _ in range(world))
+
+
+@pytest.mark.parametrize("w,h,count,regions", [
+    (3840, 2160, 8, None), (333, 241, 3, None), (333, 241, 2, _REGIONS[2]), (333, 241, 3, _REGIONS[3]),
+    (3840, 2160, 1, None)])
+def test_owned_pixels_partition_the_frame(w, h, count, regions):
+    """shard.owned_pixels (bench.py's N > 1 roofline: rank 0's camera-pass bytes are its owned pixels x
+    32 B, not the whole frame's): the ranks' shares add up to W*H, and rank r's share is the number of
+    pixels its tiles cover, edge tiles clipped."""
+    shares = [shard.owned_pixels(w, h, T, r, count, regions) for r in range(count)]
+    assert sum(shares) == w * h
+    for r in range(count):
+        m = np.zeros((h, w), bool)
+        for t in shard.owned_tiles(w, h, T, r, count, regions):
+            y0, y1, x0, x1 = shard._tile_slices(t, w, h, T)
+            m[y0:y1, x0:x1] = True
+        assert shares[r] == int(m.sum())
+    if regions is None and count == 8:
+        # 120 x 68 bin tiles, the last row 16 px high: interleaved ranks get 1020 tiles each
+        assert shares[0] == 1020 * 1024 - 120 // 8 * 16 * 32
