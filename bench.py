@@ -269,7 +269,15 @@ def rank_owned_pixels(ctx, frame, rank, world, regions_layout):
     return shard.owned_pixels(frame.width, frame.height, 32, rank, world, regions)
 
 
-def lib_timed_loop(args, slots, frame_fn, dist, frame=None, rank=0, world=1):
+def shadow_pass_texels(ctx, S):
+    """Texels the context's last shadow pass rendered (its footprint's 32x32 tiles, or the whole map)."""
+    x0, y0, x1, y1 = ctx.shadow_region()
+    if x1 < x0 or y1 < y0:
+        return 0
+    return (min(S, (x1 + 1) * 32) - x0 * 32) * (min(S, (y1 + 1) * 32) - y0 * 32)
+
+
+def lib_timed_loop(args, slots, frame_fn, dist, frame=None, rank=0, world=1, on_last=None):
     """Warm-up, then exactly args.steps frames round-robin over the slots (frame i on slot i % D) between
     two barriers; then kernel event times of 20 frames on slot 0 alone (nothing else in flight: the
     roofline's kernel durations).  -> (elapsed s, stats, (n_frames, kms), pixels this rank owned in the
@@ -301,6 +309,8 @@ def lib_timed_loop(args, slots, frame_fn, dist, frame=None, rank=0, world=1):
     barrier_sync()
     n_passes, kms = ctx.lib_timing_read()
     ctx.enable_timing(False)
+    if on_last is not None:
+        on_last(ctx)
     owned = None
     if frame is not None:
         owned = rank_owned_pixels(ctx, frame, rank, world, dist is not None and args.shard_layout == "regions")
@@ -367,6 +377,9 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
     for _ in range(args.inflight):
         sl = LibSlot(local_rank, dist, args)
         ctx = sl.ctx
+        # SHS_OPT_SHADOW_FOOTPRINT: the camera pass enqueues the shadow pass over only the shadow-map tiles
+        # its pixels' PCF reads (every N alike; the images are the oracle's either way)
+        ctx.set_shadow_footprint(not args.shadow_full)
         lvp = ctx.render_shadow_map(S, sun, casters)
         scene_lib.wire_shadow(draws, lvp)
         sl.prepared = ctx.prepare_lib(frame, draws)
@@ -384,12 +397,15 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
         if dist is not None:
             sl.gather(dist)
 
-    elapsed, stats, (n_cam, kms), owned = lib_timed_loop(args, slots, one_frame, dist, frame, rank, world)
+    shadow_texels = []
+    elapsed, stats, (n_cam, kms), owned = lib_timed_loop(args, slots, one_frame, dist, frame, rank, world,
+                                                         on_last=lambda ctx: shadow_texels.append(shadow_pass_texels(ctx, S)))
     B_cam_raster = camera_phase_bytes(frame.width, frame.height, owned, S)
+    # the shadow map written and read once: the whole map, or the texels of the footprint the pass covered
     B_frame = (sum(lib_mesh_bytes(d.mesh) for d in draws) + sum(lib_mesh_bytes(c.mesh, False) for c in casters)
-               + 2 * S * S * 4 + frame.width * frame.height * 32)
+               + 2 * shadow_texels[0] * 4 + frame.width * frame.height * 32)
     n_tri = sum(d.mesh.n_tris for d in draws)
-    return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, S, owned
+    return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, (S, shadow_texels[0]), owned
 
 
 def collect_pmc(args):
@@ -597,6 +613,9 @@ def main():
                     help="c4/c5 at N > 1: tile ownership (one cost-balanced rectangle per rank, or tile %% N)")
     ap.add_argument("--root-share", type=float, default=0.85,
                     help="c4/c5 regions: rank 0's share of the predicted cost (it also unpacks the gather)")
+    ap.add_argument("--shadow-full", action="store_true",
+                    help="c5: render the whole shadow map every frame (default: the camera pass's footprint, "
+                         "SHS_OPT_SHADOW_FOOTPRINT)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -738,7 +757,8 @@ def main():
 
 def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     runner = run_gpu_c4 if args.config == "c4" else run_gpu_lib
-    frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, S, owned = runner(args, rank, local_rank, world, dist)
+    frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, shadow, owned = runner(args, rank, local_rank, world, dist)
+    S, shadow_texels = shadow if shadow else (None, 0)
     world_tri = n_tri              # one frame per step, split over the ranks at N > 1 (strong scaling)
     el_max = elapsed
     covered_total = float(stats["covered_pixels"])
@@ -784,7 +804,9 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     else:
         data = ("synthetic: Suzanne (indexed from the reference's monkey.rawobj) + make_plane floor, reference "
                 "defaults (sun normalize(0.4668,-0.3487,0.8127), intensity 5, PCF 2, bias 0.0008/0.0015)")
-        parallelism = (f"tile-sharded x{world} ({args.shard_layout}; shadow map on every rank) + RCCL gather of RGBA8 "
+        shadow_how = ("the whole shadow map on every rank" if args.shadow_full else
+                      "each rank's shadow pass over its own PCF footprint, no shadow-map exchange")
+        parallelism = (f"tile-sharded x{world} ({args.shard_layout}; {shadow_how}) + RCCL gather of RGBA8 "
                        "present tiles to rank 0") if world > 1 else "single GPU"
     line = {
         "metric": METRIC, "value": round(world_tri * steps / el_max / 1e6, 3), "unit": "Mtri/s", "n_gpus": world,
@@ -792,6 +814,10 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
         "config": {"workload": WORKLOADS[args.config], "width": frame.width, "height": frame.height,
                    "shadow_map": S, "tris_per_frame": n_tri, "frames_per_step_per_gpu": 1,
+                   "shadow_pass": None if S is None else (
+                       "whole map" if args.shadow_full else
+                       f"footprint of the camera pass's PCF reads (SHS_OPT_SHADOW_FOOTPRINT): {shadow_texels} of "
+                       f"{S * S} texels on rank 0"),
                    "frames_in_flight": args.inflight, "parallelism": parallelism},
         "shaded_mpix_s": round(covered_total * steps / el_max / 1e6, 3),
         "frame_stats": stats, "kernels_ms": {k: round(v, 5) for k, v in kms.items()},

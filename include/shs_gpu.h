@@ -214,6 +214,15 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * ranks' (default 1000).  Rank 0 also unpacks every peer's tiles of the gathered frame; a smaller share
  * leaves it room for that.  Every rank must use the same value. */
 #define SHS_OPT_SHARD_ROOT_SHARE 10
+/* SHS_OPT_SHADOW_FOOTPRINT: 1 = shs_render_shadow_map records the pass (light camera computed and
+ * returned as before) and the next shs_render_pbr_forward enqueues it over only the 32x32 shadow-map
+ * tiles that pass's pixels can read: for each draw with `shadow`, the light-space bounds of (its world
+ * box) ∩ (the camera frustum slice of the pixels the rank shades -- its region, or the whole frame),
+ * widened by the PCF reach (shadow_sample.hpp:65-104) -- so a region-sharded rank renders only its own
+ * shadow footprint and no shadow map crosses between ranks.  Texels outside are not written that pass;
+ * the frame's images are identical.  shs_resolve_shadow_map of a recorded pass renders it whole.
+ * 0 (default): every shadow pass renders the whole map when it is called. */
+#define SHS_OPT_SHADOW_FOOTPRINT 11
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 /* The regions of the last region-sharded camera pass: rects[4 r .. 4 r + 3] = (bx0, by0, bx1, by1) of
  * rank r, bin tiles, inclusive (bx1 < bx0: rank r owns nothing). */
@@ -346,6 +355,16 @@ typedef struct shs_shadow_caster {
 int shs_render_shadow_map(shs_ctx *ctx, int32_t w, int32_t h, const float sun_dir[3], const shs_shadow_caster *casters,
                           int32_t n_casters, float light_viewproj_out[16]);
 int shs_resolve_shadow_map(shs_ctx *ctx, float *depth);
+/* The bin tiles (32x32 texels, inclusive) the last enqueued shadow pass rendered: the whole map, or
+ * under SHS_OPT_SHADOW_FOOTPRINT the camera pass's footprint (rect[2] < rect[0]: none, or still recorded). */
+int shs_get_shadow_region(shs_ctx *ctx, int32_t rect[4]);
+/* Host-only (no device): the footprint itself, for tests -- the texels (inclusive; texel_rect[2] <
+ * texel_rect[0]: none) of an sm_w x sm_h map, through light_viewproj, that a PCF of `reach` texels reads
+ * from points of the world box [world_min, world_max] whose camera_viewproj projection falls on the pixel
+ * rectangle px_rect = {x0, y0, x1, y1} (inclusive, rows y up) of a width x height frame. */
+int shs_shadow_footprint(const float light_viewproj[16], int32_t sm_w, int32_t sm_h, const float camera_viewproj[16],
+                         int32_t width, int32_t height, const int32_t px_rect[4], const float world_min[3],
+                         const float world_max[3], int32_t reach, int32_t texel_rect[4]);
 
 /* ---- Forward+ light-list binning ---------------------------------------
  * CullingLightGPU (lighting/light_types.hpp:141-166), the std430 record the reference uploads for

@@ -138,6 +138,10 @@ int shs_mesh_upload_soup(shs_ctx *ctx, const float *positions, const float *norm
 int shs_mesh_release(shs_ctx *ctx, int32_t id) {
     if (!ctx || id < 0 || id >= (int32_t)ctx->meshes.size() || !ctx->meshes[id].live) return SHS_ERR_INVALID;
     if (set_dev(ctx)) return SHS_ERR_HIP;
+    if (ctx->shadow_pending) {   // a recorded footprint shadow pass may read the mesh: render it first
+        const int rc = shs_lib_flush_shadow(ctx);
+        if (rc) return rc;
+    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     Mesh &m = ctx->meshes[id];
@@ -716,6 +720,15 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
         if (value < 0 || value > 1000) return SHS_ERR_INVALID;
         ctx->shard_root_permille = (int)value;
         ctx->reg_next_fresh = false;
+        return SHS_OK;
+    }
+    if (option == SHS_OPT_SHADOW_FOOTPRINT) {
+        if (value < 0 || value > 1) return SHS_ERR_INVALID;
+        if (value == 0 && ctx->shadow_pending) {   // a recorded pass is rendered whole now
+            const int rc = shs_lib_flush_shadow(ctx);
+            if (rc) return rc;
+        }
+        ctx->shadow_footprint = value != 0;
         return SHS_OK;
     }
     if (option == SHS_OPT_LIB_PART) {

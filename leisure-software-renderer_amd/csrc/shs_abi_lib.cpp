@@ -11,6 +11,7 @@
 
 #include "../../include/shs_gpu.h"
 #include "shs_ctx.hpp"
+#include "shs_footprint.hpp"
 #include "shs_glm.hpp"
 #include "shs_lib_device.hpp"
 #include "shs_lib_internal.hpp"
@@ -794,15 +795,69 @@ int shs_render_shadow_map(shs_ctx *ctx, int32_t w, int32_t h, const float sun_di
     LibFrameParams fp;
     std::memset(&fp, 0, sizeof fp);
     fp.W = w; fp.H = h;
-    fp.rank = 0; fp.count = 1;   // every device renders the whole shadow map (sampled anywhere)
+    fp.rank = 0; fp.count = 1;   // the whole shadow map (SHS_OPT_SHADOW_FOOTPRINT: the next camera pass narrows it)
     wk.last_fp = fp;
     ctx->shadow_w = w;
     ctx->shadow_h = h;
     ctx->cam_after_shadow = false;
-    const int rc = enqueue_pass(ctx, wk, true);
-    if (rc) return rc;
     ctx->have_shadow = true;
-    return SHS_OK;
+    if (ctx->shadow_footprint) {   // recorded; shs_render_pbr_forward enqueues it for the texels it reads
+        ctx->shadow_pending = true;
+        return SHS_OK;
+    }
+    ctx->shadow_pending = false;
+    ctx->shadow_reg = shs_dev::ShardRegion{0, 0, 0, 0, 0};
+    return enqueue_pass(ctx, wk, true);
+}
+
+// Enqueue the recorded shadow pass over the bin tiles of `reg` (reg.on = 0: the whole map).
+static int enqueue_shadow(shs_ctx *ctx, const shs_dev::ShardRegion &reg) {
+    Work &wk = ctx->lib_shadow;
+    wk.last_fp.reg = reg;
+    wk.last_fp.rank = 0;
+    wk.last_fp.count = reg.on ? 2 : 1;   // a region pass: only the rectangle's tiles are owned
+    ctx->shadow_pending = false;
+    ctx->shadow_reg = reg;
+    return enqueue_pass(ctx, wk, true);
+}
+
+}  // extern "C"
+
+int shs_lib_flush_shadow(shs_ctx *ctx) {
+    if (!ctx->shadow_pending) return SHS_OK;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    return enqueue_shadow(ctx, shs_dev::ShardRegion{0, 0, 0, 0, 0});
+}
+
+extern "C" {
+
+// SHS_OPT_SHADOW_FOOTPRINT: the shadow-map bin tiles the camera pass about to be enqueued can read
+// (shs_footprint.hpp): the union over its shadowed draws of the light-space bounds of (the draw's world
+// box) ∩ (the camera frustum slice of the pixels this rank shades), widened by the PCF reach.
+static shs_dev::ShardRegion shadow_region_for(const shs_ctx *ctx, const shs_lib_frame &f, const shs_lib_draw *draws,
+                                              int32_t n_draws, const shs_dev::ShardRegion &cam_reg) {
+    const int W = f.width, H = f.height;
+    int px[4] = {0, 0, W - 1, H - 1};
+    if (f.shard_count > 1 && cam_reg.on) {
+        px[0] = cam_reg.x0 * shs_dev::TILE;
+        px[1] = cam_reg.y0 * shs_dev::TILE;
+        px[2] = std::min(W, (cam_reg.x1 + 1) * shs_dev::TILE) - 1;
+        px[3] = std::min(H, (cam_reg.y1 + 1) * shs_dev::TILE) - 1;
+    }
+    shs_fp::TexelRect t;
+    for (int i = 0; i < n_draws; ++i) {
+        const shs_lib_draw &d = draws[i];
+        if (!d.shadow) continue;
+        const Mesh &m = ctx->meshes[d.mesh_id];
+        double bmin[3], bmax[3];
+        shs_fp::world_box(d.model, m.bmin, m.bmax, bmin, bmax);
+        const int rad = std::max(0, d.shadow_pcf_radius);
+        const int step = std::max(1, (int)std::round((1.0f < d.shadow_pcf_step) ? d.shadow_pcf_step : 1.0f));
+        t = shs_fp::unite(t, shs_fp::shadow_footprint(d.light_viewproj, ctx->shadow_w, ctx->shadow_h, d.viewproj, W, H, px,
+                                                      bmin, bmax, rad * step));
+    }
+    const int T = shs_dev::TILE;
+    return t.empty() ? shs_dev::ShardRegion{1, 0, 0, -1, -1} : shs_dev::ShardRegion{1, t.x0 / T, t.y0 / T, t.x1 / T, t.y1 / T};
 }
 
 int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_lib_draw *draws, int32_t n_draws) {
@@ -874,6 +929,10 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
         fp.lt_zn = c.zn; fp.lt_zf = c.zf;
     }
     wk.last_fp = fp;
+    if (ctx->shadow_pending) {   // the recorded shadow pass, narrowed to what this pass reads
+        const int rc = enqueue_shadow(ctx, shadow_region_for(ctx, f, draws, n_draws, fp.reg));
+        if (rc) return rc;
+    }
     ctx->lib_frame = f;
     ctx->cam_after_shadow = ctx->have_shadow;
     wk.tm_fused = ctx->tm_fuse;
@@ -911,11 +970,36 @@ int shs_resolve_lib(shs_ctx *ctx, float *hdr, float *depth, float *motion) {
     return SHS_OK;
 }
 
+int shs_get_shadow_region(shs_ctx *ctx, int32_t rect[4]) {
+    if (!ctx || !rect) return SHS_ERR_INVALID;
+    if (!ctx->have_shadow) { ctx->err = "no shadow map rendered"; return SHS_ERR_INVALID; }
+    const shs_dev::ShardRegion &g = ctx->shadow_reg;
+    const int tx = (ctx->shadow_w + shs_dev::TILE - 1) / shs_dev::TILE, ty = (ctx->shadow_h + shs_dev::TILE - 1) / shs_dev::TILE;
+    if (ctx->shadow_pending) { rect[0] = 1; rect[1] = 1; rect[2] = 0; rect[3] = 0; return SHS_OK; }
+    rect[0] = g.on ? g.x0 : 0; rect[1] = g.on ? g.y0 : 0;
+    rect[2] = g.on ? g.x1 : tx - 1; rect[3] = g.on ? g.y1 : ty - 1;
+    return SHS_OK;
+}
+
+int shs_shadow_footprint(const float light_viewproj[16], int32_t sm_w, int32_t sm_h, const float camera_viewproj[16],
+                         int32_t width, int32_t height, const int32_t px_rect[4], const float world_min[3],
+                         const float world_max[3], int32_t reach, int32_t texel_rect[4]) {
+    if (!light_viewproj || !camera_viewproj || !px_rect || !world_min || !world_max || !texel_rect || reach < 0)
+        return SHS_ERR_INVALID;
+    const int px[4] = {px_rect[0], px_rect[1], px_rect[2], px_rect[3]};
+    const double b0[3] = {world_min[0], world_min[1], world_min[2]}, b1[3] = {world_max[0], world_max[1], world_max[2]};
+    const shs_fp::TexelRect t = shs_fp::shadow_footprint(light_viewproj, sm_w, sm_h, camera_viewproj, width, height, px, b0, b1, reach);
+    texel_rect[0] = t.x0; texel_rect[1] = t.y0; texel_rect[2] = t.x1; texel_rect[3] = t.y1;
+    return SHS_OK;
+}
+
 int shs_resolve_shadow_map(shs_ctx *ctx, float *depth) {
     if (!ctx || !depth) return SHS_ERR_INVALID;
     if (!ctx->have_shadow) { ctx->err = "no shadow map rendered"; return SHS_ERR_INVALID; }
     if (set_dev(ctx)) return SHS_ERR_HIP;
-    int rc = lib_finish(ctx);
+    int rc = shs_lib_flush_shadow(ctx);   // a recorded footprint pass is rendered whole for a readback
+    if (rc) return rc;
+    rc = lib_finish(ctx);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(depth, ctx->shadow_map.p, (size_t)ctx->shadow_w * ctx->shadow_h * sizeof(float), hipMemcpyDeviceToHost));
     return SHS_OK;

@@ -190,6 +190,9 @@ struct shs_ctx {
     int reg_next_count = 0, reg_next_w = 0, reg_next_h = 0, reg_last_count = 0;
     bool reg_next_fresh = false;
     int shard_root_permille = 1000;       // SHS_OPT_SHARD_ROOT_SHARE: rank 0's share of a region layout (it also unpacks)
+    bool shadow_footprint = false;        // SHS_OPT_SHADOW_FOOTPRINT: shadow passes render only what the next camera pass reads
+    bool shadow_pending = false;          // a footprint shadow pass recorded, not enqueued yet (the camera pass does it)
+    shs_dev::ShardRegion shadow_reg{0, 0, 0, 0, 0};   // the bin tiles the last enqueued shadow pass rendered (on = 0: all)
     std::vector<uint4> reg_in;            // the block bounds reg_next was last balanced from (identical: reused)
     int reg_in_count = -1, reg_in_w = 0, reg_in_h = 0, reg_in_root = 0;
     // Tile orders / owned-list tables by geometry + ownership, uploaded once into their own buffers (a
@@ -267,6 +270,8 @@ int shs_tonemap_reissue(shs_ctx *ctx);
 // the context stream afterwards sees the final frame (shs_abi.cpp: legacy; shs_abi_lib.cpp: library).
 int shs_legacy_ensure_final(shs_ctx *ctx);
 int shs_lib_ensure_final(shs_ctx *ctx);
+// A shadow pass recorded under SHS_OPT_SHADOW_FOOTPRINT and not yet enqueued: enqueue it for the whole map.
+int shs_lib_flush_shadow(shs_ctx *ctx);
 // Region layout (shs_abi_shard.cpp).  shs_shard_balance: `count` rectangles of the tiles_x x tiles_y bin
 // grid of a W x H frame with equal predicted cost, from n_blk setup-block bounds (null: pixels only).
 void shs_shard_balance(const uint4 *blk, int n_blk, int tiles_x, int tiles_y, int W, int H, int count,

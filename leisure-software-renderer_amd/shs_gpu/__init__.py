@@ -496,6 +496,23 @@ class Context:
             raise ShsError(rc, "shs_shard_balance_rects")
         return [tuple(int(v) for v in out[4 * r:4 * r + 4]) for r in range(count)]
 
+    @staticmethod
+    def shadow_footprint(light_vp, sm_size, camera_vp, width, height, px_rect, world_min, world_max, reach):
+        """Host-side footprint (shs_shadow_footprint): the texel rectangle (x0, y0, x1, y1), inclusive, of an
+        sm_size = (w, h) shadow map that PCF of `reach` texels reads from the points of the world box whose
+        camera projection lands on px_rect (x0, y0, x1, y1; rows y up) of a width x height frame."""
+        sw, sh = (sm_size, sm_size) if isinstance(sm_size, int) else sm_size
+        f16 = lambda m: np.ascontiguousarray(np.asarray(m, np.float32).reshape(16))
+        f3 = lambda v: np.ascontiguousarray(np.asarray(v, np.float32).reshape(3))
+        lv, cv, b0, b1 = f16(light_vp), f16(camera_vp), f3(world_min), f3(world_max)
+        px = np.ascontiguousarray(np.asarray(px_rect, np.int32).reshape(4))
+        out = np.zeros(4, np.int32)
+        rc = lib().shs_shadow_footprint(lv.ctypes.data, int(sw), int(sh), cv.ctypes.data, int(width), int(height),
+                                        px.ctypes.data, b0.ctypes.data, b1.ctypes.data, int(reach), out.ctypes.data)
+        if rc != 0:
+            raise ShsError(rc, "shs_shadow_footprint")
+        return tuple(int(v) for v in out)
+
     LIB_TIMELINE_FIELDS = ("start", "end", "gather", "pairs", "shade", "clear", "n_busy", "n_clear", "chunks",
                            "n_pairs", "n_cand", "max_tile")
 
@@ -551,6 +568,17 @@ class Context:
     def set_shard_root_share(self, share: float):
         """SHS_OPT_SHARD_ROOT_SHARE: rank 0's share of a region layout relative to the others (0..1)."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_SHARD_ROOT_SHARE, int(round(share * 1000))))
+
+    def set_shadow_footprint(self, on: bool):
+        """SHS_OPT_SHADOW_FOOTPRINT: shadow passes are recorded and rendered by the next camera pass over
+        only the shadow-map tiles its pixels' PCF can read (default off: the whole map when called)."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_SHADOW_FOOTPRINT, 1 if on else 0))
+
+    def shadow_region(self):
+        """The last enqueued shadow pass's bin tiles (bx0, by0, bx1, by1), inclusive; bx1 < bx0: none."""
+        arr = (ctypes.c_int32 * 4)()
+        self._check(self._lib.shs_get_shadow_region(self._h, arr))
+        return tuple(arr)
 
     def shard_regions(self, count):
         """The last region-sharded camera pass's layout: [(bx0, by0, bx1, by1)] per rank (bin tiles, inclusive)."""

@@ -36,6 +36,7 @@ OPT_SHARD_LAYOUT = 9
 SHARD_INTERLEAVED = 0
 SHARD_REGIONS = 1
 OPT_SHARD_ROOT_SHARE = 10
+OPT_SHADOW_FOOTPRINT = 11
 
 
 class LegacyDraw(ctypes.Structure):
@@ -276,6 +277,9 @@ SIGNATURES = [
     ("shs_render_shadow_map", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _F, ctypes.POINTER(ShadowCasterC),
                                              ctypes.c_int32, _F]),
     ("shs_resolve_shadow_map", ctypes.c_int, [_P, _P]),
+    ("shs_get_shadow_region", ctypes.c_int, [_P, _P]),
+    ("shs_shadow_footprint", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, _P,
+                                            ctypes.c_int32, _P]),
     ("shs_tiles_packed_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_tiles_rank_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_get_shard_regions", ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),

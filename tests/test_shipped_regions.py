@@ -76,8 +76,10 @@ def test_region_sharded_4k_frames_compose_to_oracle(oracle_mod, c4_ref, c5_ref, 
             c.fuse_tonemap(1.0, 2.2, ldr=False, present=True)     # bench.py's N > 1 frame
             if cfg == "c4":
                 c.upload_lights(lights)
+            else:
+                c.set_shadow_footprint(True)   # bench.py's C5: each rank's shadow pass covers its own footprint
         for it in range(2):
-            lib_bufs, pres_bufs, regs = [None] * RANKS, [None] * RANKS, []
+            lib_bufs, pres_bufs, regs, shadow_tiles = [None] * RANKS, [None] * RANKS, [], []
             got_counts = np.zeros_like(rc) if cfg == "c4" else None
             listed = np.zeros(rc.shape[0], bool) if cfg == "c4" else None
             for r, c in enumerate(ctxs):
@@ -89,6 +91,9 @@ def test_region_sharded_4k_frames_compose_to_oracle(oracle_mod, c4_ref, c5_ref, 
                     lvp = c.render_shadow_map(S, sun, casters)
                     assert np.array_equal(lvp.view(np.uint32), lvp_ref.view(np.uint32))
                 c.render_pbr_forward(frame, draws)
+                if cfg == "c5":
+                    sx0, sy0, sx1, sy1 = c.shadow_region()
+                    shadow_tiles.append(max(0, sx1 - sx0 + 1) * max(0, sy1 - sy0 + 1))
                 reg = c.shard_regions(RANKS)
                 regs.append(reg)
                 if cfg == "c4":
@@ -122,7 +127,10 @@ def test_region_sharded_4k_frames_compose_to_oracle(oracle_mod, c4_ref, c5_ref, 
                 assert listed.all(), "some light list has no owner"
                 assert np.array_equal(got_counts, rc)
             owned = [int(_mask(W, H, reg).sum()) for reg in regs[0]]
-            print(f"{cfg} frame {it}: layout {regs[0]}, owned px {owned}, {n} HDR channels not bit-identical")
+            print(f"{cfg} frame {it}: layout {regs[0]}, owned px {owned}, shadow tiles {shadow_tiles}, "
+                  f"{n} HDR channels not bit-identical")
+            if cfg == "c5":
+                assert max(shadow_tiles) < 64 * 64, "a rank rendered the whole shadow map"
     finally:
         for c in ctxs:
             c.close()
