@@ -309,7 +309,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.n_tris = n_tris; fp.n_draws = n_draws;
     fp.clear_rgba = (uint32_t)f.clear_color[0] | ((uint32_t)f.clear_color[1] << 8) | ((uint32_t)f.clear_color[2] << 16) |
                     ((uint32_t)f.clear_color[3] << 24);
-    fp.flags = (f.flags & ~shs_dev::RF_PER_PIXEL) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
+    fp.flags = (f.flags & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ws.spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ws.frags.cap, 0xffffffffu);
@@ -326,6 +326,14 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.epoch = ctx->busy_epoch;
     fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
     if (!fp.scan_mode) HIP_TRY(ctx, hipMemsetAsync(ws.tile_count.p, 0, n_bt_all * sizeof(uint32_t), sst));
+    // Binned frames keep no per-triangle records (k_raster recomputes them from the resident mesh);
+    // SHS_LEGACY_RECS=1 stores them anyway (timing experiments).
+    static const bool keep_recs_env = std::getenv("SHS_LEGACY_RECS") && std::atoi(std::getenv("SHS_LEGACY_RECS")) != 0;
+    const bool no_recs = !fp.scan_mode && !keep_recs_env;
+    if (no_recs) {
+        fp.flags |= shs_dev::RF_NO_RECS;
+        if (ensure(ctx, ws.tdraw, nt_all)) return SHS_ERR_HIP;
+    }
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;
     fp.setup_blocks = setup_blocks;
@@ -371,6 +379,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fb.rstat = ws.rstat.p;
     fb.timeline = ctx->want_timeline ? ctx->timeline.p : nullptr;
     fb.boxes = ws.boxes.p;
+    fb.tdraw = no_recs ? ws.tdraw.p : nullptr;
     fb.color = ctx->color.p; fb.depth = ctx->depth.p; fb.prequant = want_pq ? ctx->prequant.p : nullptr;
     fb.present = want_present ? ctx->present.p : nullptr;
     fb.ov_host = const_cast<uint32_t *>(ws.h_ov);
@@ -401,6 +410,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     ws.used = true;
     ctx->last_parity = fp.parity;
     ctx->last_slot = slot;
+    ctx->last_no_recs = no_recs;
     ctx->frame_index++;
     ctx->have_frame = true;
     ctx->need_check = true;
@@ -662,6 +672,7 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
     if (set_dev(ctx)) return SHS_ERR_HIP;
     int rc = finish_frame(ctx);
     if (rc) return rc;
+    if (ctx->last_no_recs) { ctx->err = "binned frames keep no triangle records (SHS_LEGACY_RECS=1 stores them)"; return SHS_ERR_INVALID; }
     *n_out = ctx->last_n_tris;
     if (out && capacity > 0) {
         const size_t n = (size_t)std::min<int64_t>(capacity, ctx->last_n_tris);

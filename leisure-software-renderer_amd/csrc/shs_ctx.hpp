@@ -70,6 +70,7 @@ struct shs_ctx {
         DevBuf<shs_dev::GhostFrag> frags;    // ghost fragments
         DevBuf<uint32_t> slivers;            // unbounded sliver ids (ghost_list mode)
         DevBuf<uint2> boxes;                 // per-triangle bin boxes
+        DevBuf<int32_t> tdraw;               // per-triangle draw (binned frames: no records kept)
         DevBuf<uint32_t> busy;               // per raster tile: the epoch of the last batch that marked it
         DevBuf<uint32_t> busy_list;          // busy tiles of the batch (k_raster's work items)
         DevBuf<uint4> blk_stat;              // per setup block
@@ -86,6 +87,7 @@ struct shs_ctx {
     DevBuf<uint32_t> counters;       // 2 sets (one per slot) of CSET words
     uint32_t busy_epoch = 0;         // FrameParams::epoch of the last launch (never 0)
     int last_slot = 0;
+    bool last_no_recs = false;       // the last legacy batch was binned without stored records (RF_NO_RECS)
     DevBuf<uint64_t> timeline;       // SHS_OPT_TIMELINE
     bool want_timeline = false;
     int last_setup_grid = 0, last_ghost_blocks = 0, last_clear_blocks = 0;

@@ -102,6 +102,12 @@ constexpr uint32_t DBG_SKIP_GHOST = 1u << 8, DBG_SKIP_SHADE = 1u << 9, DBG_CLEAR
 // Raster inner loop (frame flags bit 16, set by the context from SHS_OPT_RASTER_LOOP): per-pixel
 // candidate loop instead of (candidate, pixel) pair tasks.  Results are identical either way.
 constexpr uint32_t RF_PER_PIXEL = 1u << 16;
+// Binned (large) frames keep no per-triangle records in HBM (frame flags bit 17, set by the context in
+// bin mode): k_setup writes only the bin box and the draw of each triangle (12 B instead of the 184-B
+// TriRec + ShadeRec), and k_raster recomputes a staged candidate's record -- and a winner's shading
+// varyings -- from the resident mesh with the identical arithmetic (a quad of lanes per candidate, as
+// k_setup).  Unbounded slivers (TRI_UNBOUNDED) still store their record for k_ghost.
+constexpr uint32_t RF_NO_RECS = 1u << 17;
 
 // Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);
 // larger scenes read the device draw table.
@@ -162,6 +168,7 @@ struct FrameBuffers {
     GhostFrag *frags;                // tile-clamp pixels of unbounded slivers that pass (frag_cap)
     uint32_t *slivers;               // n_frames * n_tris: unbounded slivers, f * n_tris + tri (ghost_list)
     uint2 *boxes;                    // per frame: n_tris packed bin boxes (gbx, gby); empty for culled
+    int32_t *tdraw;                  // per frame: n_tris, the triangle's draw in the frame's slice (RF_NO_RECS)
     uint32_t *counters;              // 2 * CSET
     uint32_t *busy;                  // per frame, per raster tile: == fp.epoch when the tile has
                                      // candidates / fragments in this launch (no reset needed)
@@ -195,6 +202,7 @@ __device__ __forceinline__ FrameBuffers frame_view(const FrameParams &fp, const 
     v.recs += f * nt;
     v.shade += f * nt;
     v.boxes += f * nt;
+    if (v.tdraw) v.tdraw += f * nt;
     v.tile_count += f * n_bt;
     v.bins += f * n_bt * fp.bin_cap;
     v.busy += f * n_rt;

@@ -103,6 +103,10 @@ __device__ __forceinline__ int floor_clamped(float x, int lo, int hi) {
     return (int)fminf(fmaxf(floorf(x), (float)lo), (float)hi);
 }
 
+// RF_NO_RECS: the per-triangle word k_setup stores -- the triangle's draw in the frame's slice and its
+// record flags (TRI_*, from danger_margin's double-precision bound, which k_raster then need not redo).
+__device__ __forceinline__ int32_t tdraw_word(int d, uint32_t flags) { return (int32_t)((uint32_t)d | (flags << 29)); }
+
 __device__ __forceinline__ TriRec rec_from(const float4 *s) {
     TriRec r;
     float4 *d = reinterpret_cast<float4 *>(&r);
@@ -535,8 +539,7 @@ __device__ __forceinline__ void corner_varyings(const DrawGPU &dr, const float (
 
 // Quad: corner varyings of lane q (< 3), assembled into the triangle's 80-B ShadeRec; lane q
 // stores floats [5q, 5q + 5) so the quad writes the record contiguously.
-__device__ __forceinline__ void quad_store_shade(const FrameBuffers &fb, int tri, int draw, int shading, const f3 &a,
-                                                 const f3 &nr) {
+__device__ __forceinline__ void quad_store_shade_at(ShadeRec *rec, int draw, int shading, const f3 &a, const f3 &nr) {
     const int q = __lane_id() & 3;
     float f[20];
 #pragma unroll
@@ -546,7 +549,7 @@ __device__ __forceinline__ void quad_store_shade(const FrameBuffers &fb, int tri
     }
     f[18] = __int_as_float(shading);
     f[19] = __int_as_float(draw);
-    float *dst = reinterpret_cast<float *>(&fb.shade[tri]) + 5 * q;
+    float *dst = reinterpret_cast<float *>(rec) + 5 * q;
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
         float x = f[j];
@@ -556,11 +559,16 @@ __device__ __forceinline__ void quad_store_shade(const FrameBuffers &fb, int tri
     }
 }
 
-// Quad: lane q stores floats [6q, 6q + 6) of the 96-B record.
-__device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, const TriRec &r) {
+__device__ __forceinline__ void quad_store_shade(const FrameBuffers &fb, int tri, int draw, int shading, const f3 &a,
+                                                 const f3 &nr) {
+    quad_store_shade_at(&fb.shade[tri], draw, shading, a, nr);
+}
+
+// Quad: lane q stores floats [6q, 6q + 6) of the 96-B record (global memory or an LDS copy).
+__device__ __forceinline__ void quad_store_rec_at(TriRec *rec, const TriRec &r) {
     const int q = __lane_id() & 3;
     const float *f = reinterpret_cast<const float *>(&r);
-    float2 *dst = reinterpret_cast<float2 *>(reinterpret_cast<float *>(&fb.recs[tri]) + 6 * q);
+    float2 *dst = reinterpret_cast<float2 *>(reinterpret_cast<float *>(rec) + 6 * q);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         float x = f[2 * j], y = f[2 * j + 1];
@@ -573,21 +581,34 @@ __device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, 
     }
 }
 
+__device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, const TriRec &r) { quad_store_rec_at(&fb.recs[tri], r); }
+
 // Record, varyings and their stores for the quad's triangle; returns the flags and the bin box.
 __device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU &dr, int d,
                                                int dbase, int tri, uint2 &gbox) {
     const int q = __lane_id() & 3, qv = q < 3 ? q : 2;
     const int local = tri - dr.tri_base;
     const float *P = dr.pos + 9 * (size_t)local + 3 * qv;
-    const float *Nn = dr.nrm + 9 * (size_t)local + 3 * qv;
     const float p3[3] = {P[0], P[1], P[2]};
-    const float n3[3] = {Nn[0], Nn[1], Nn[2]};
+    const bool recs = !(fp.flags & RF_NO_RECS);
+    float n3[3] = {0.0f, 0.0f, 0.0f};
+    if (recs) {   // issued with the position loads (their latency overlaps the record's arithmetic)
+        const float *Nn = dr.nrm + 9 * (size_t)local + 3 * qv;
+        n3[0] = Nn[0]; n3[1] = Nn[1]; n3[2] = Nn[2];
+    }
     const TriRec r = quad_make_rec(fp, dr, d, local, p3);
     tl_mark(fb.timeline, blockIdx.x, 4);
-    f3 a, nr;
-    corner_varyings(dr, p3, n3, a, nr);
-    quad_store_rec(fb, tri, r);
-    quad_store_shade(fb, tri, dbase + d, dr.shading, a, nr);   // the draw-table index of the batch
+    if (!recs) {
+        // binned frame: k_raster recomputes records and varyings from the mesh; only k_ghost's
+        // unbounded slivers keep their record (quad-uniform condition)
+        if ((r.flags & (TRI_UNBOUNDED | TRI_CULLED)) == TRI_UNBOUNDED) quad_store_rec(fb, tri, r);
+        if (q == 0) fb.tdraw[tri] = tdraw_word(d, r.flags);
+    } else {
+        f3 a, nr;
+        corner_varyings(dr, p3, n3, a, nr);
+        quad_store_rec(fb, tri, r);
+        quad_store_shade(fb, tri, dbase + d, dr.shading, a, nr);   // the draw-table index of the batch
+    }
     if (q == 0) fb.boxes[tri] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
     gbox = make_uint2(r.gbx, r.gby);
     return r.flags;
@@ -782,13 +803,16 @@ __global__ __launch_bounds__(256) void k_ghost(FrameParams fp, FrameBuffers fb_a
 // Fragment shaders of the four legacy pipelines for the winning triangle, from its per-corner
 // varyings.  Returns the pre-truncation floats; the caller truncates to uint8 like the reference.
 // du = the draw's {light, cam, ocol, colf} float4s (DrawGPU::light.. or the LDS copy).
-__device__ __forceinline__ void shade_winner(const float4 *du, const ShadeRec &sr, float u, float v, float w, float pre[3]) {
+// The FS from the interpolated varyings: A = (a0 u + a1 v) + a2 w of the ShadeRec's first three
+// vectors (world position / Gouraud colour / Flat normal), N = the same of the normals (Phong,
+// Blinn-Phong).  Split from the interpolation so a winner's varyings can be accumulated corner by
+// corner in the same operation order (recs_from_mesh's caller).
+__device__ __forceinline__ void shade_interp(const float4 (&du)[4], int shading, f3 A, f3 N, float pre[3]) {
     const float4 dl = du[0], dc = du[1], doc = du[2], dcf = du[3];
-    const f3 a0 = {sr.v[0], sr.v[1], sr.v[2]}, a1 = {sr.v[3], sr.v[4], sr.v[5]}, a2 = {sr.v[6], sr.v[7], sr.v[8]};
-    if (sr.shading == 0) {
+    if (shading == 0) {
         // Flat FS (flat_shading.cpp:69-98): the interpolated normal is normalised in
         // draw_triangle_tile and again in the FS; intensity = min(0.2 + max(n.l, 0), 1)
-        const f3 in_n = normalize3(add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w)));
+        const f3 in_n = normalize3(A);
         const f3 nn = normalize3(in_n);
         const f3 l = {dl.x, dl.y, dl.z};
         const float diffuse = g_max(dot3(nn, l), 0.0f);
@@ -799,25 +823,24 @@ __device__ __forceinline__ void shade_winner(const float4 *du, const ShadeRec &s
         pre[2] = dcf.z * intensity;
         return;
     }
-    if (sr.shading == 1) {
+    if (shading == 1) {
         // Gouraud FS (gouraud_shading.cpp:80-89): interpolated colour * 255
-        const f3 c = add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w));
+        const f3 c = A;
         pre[0] = c.x * 255.0f;
         pre[1] = c.y * 255.0f;
         pre[2] = c.z * 255.0f;
         return;
     }
     // Phong / Blinn-Phong: normal and world position interpolated (blinn_phong_shading.cpp:235-236)
-    const f3 n0 = {sr.v[9], sr.v[10], sr.v[11]}, n1 = {sr.v[12], sr.v[13], sr.v[14]}, n2 = {sr.v[15], sr.v[16], sr.v[17]};
-    const f3 in_n = normalize3(add3(add3(sc3(n0, u), sc3(n1, v)), sc3(n2, w)));
-    const f3 in_w = add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w));
+    const f3 in_n = normalize3(N);
+    const f3 in_w = A;
     const f3 L = {dl.x, dl.y, dl.z};
     const f3 cam = {dc.x, dc.y, dc.z};
     const f3 norm = normalize3(in_n);
     const f3 viewDir = normalize3(sub3(cam, in_w));
     const float diff = g_max(dot3(norm, L), 0.0f);
     float specular;
-    if (sr.shading == 2) {
+    if (shading == 2) {
         // Phong (phong_shading.cpp:70-108): reflect(-L, N) = I - N*dot(N,I)*2, spec 0.8,
         // pow(float, int 32) resolves to std::pow(double, double)
         const f3 I = {-L.x, -L.y, -L.z};
@@ -837,6 +860,31 @@ __device__ __forceinline__ void shade_winner(const float4 *du, const ShadeRec &s
     pre[0] = g_clamp01(s * oc.x) * 255.0f;
     pre[1] = g_clamp01(s * oc.y) * 255.0f;
     pre[2] = g_clamp01(s * oc.z) * 255.0f;
+}
+
+// The ShadeRec's varyings at barycentrics (u, v, w): A = (a0 u + a1 v) + a2 w, N likewise (Phong,
+// Blinn-Phong) -- blinn_phong_shading.cpp:235-236's operation order.
+__device__ __forceinline__ void interp_varyings(const ShadeRec &sr, float u, float v, float w, f3 &A, f3 &N) {
+    const f3 a0 = {sr.v[0], sr.v[1], sr.v[2]}, a1 = {sr.v[3], sr.v[4], sr.v[5]}, a2 = {sr.v[6], sr.v[7], sr.v[8]};
+    A = add3(add3(sc3(a0, u), sc3(a1, v)), sc3(a2, w));
+    N = f3{0.0f, 0.0f, 0.0f};
+    if (sr.shading >= 2) {
+        const f3 n0 = {sr.v[9], sr.v[10], sr.v[11]}, n1 = {sr.v[12], sr.v[13], sr.v[14]}, n2 = {sr.v[15], sr.v[16], sr.v[17]};
+        N = add3(add3(sc3(n0, u), sc3(n1, v)), sc3(n2, w));
+    }
+}
+
+__device__ __forceinline__ void shade_winner(const float4 *du, const ShadeRec &sr, float u, float v, float w, float pre[3]) {
+    const float4 d4[4] = {du[0], du[1], du[2], du[3]};
+    f3 A, N;
+    interp_varyings(sr, u, v, w, A, N);
+    shade_interp(d4, sr.shading, A, N, pre);
+}
+
+// The draw's {light, cam, ocol, colf} (DrawGPU::light.., or its LDS copy) into registers.
+__device__ __forceinline__ void load_du(const float4 *p, float4 (&du)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) du[k] = p[k];
 }
 
 // The z test (ZBuffer::test_and_set_depth, strict '<' in submission order) resolves through z_key
@@ -892,12 +940,114 @@ struct RasterShared {
     uint8_t wown[PAIR_WORDS];         // staged candidate owning each bitmap word's first pair
 };
 
+// The record rebuilt from the screen corners with the stored flags and bin box: rec_from_screen's
+// float arithmetic (the Gram terms, z, float bbox, integer bbox) without danger_margin -- its only
+// outputs, the flags and the bin box, come from k_setup.  Candidates are never culled (their bin box
+// is non-empty), so the integer bbox is always the clamped floor.
+__device__ __forceinline__ TriRec rec_from_stored(const FrameParams &fp, int draw, int local, const float (&sx)[3],
+                                                  const float (&sy)[3], const float (&sz)[3], uint32_t flags, uint2 gbox) {
+    TriRec r;
+    r.ax = sx[0]; r.ay = sy[0];
+    r.v0x = sx[1] - sx[0]; r.v0y = sy[1] - sy[0];
+    r.v1x = sx[2] - sx[0]; r.v1y = sy[2] - sy[0];
+    {
+        const float a = r.v0x * r.v0x, b = r.v0y * r.v0y; r.d00 = a + b;
+        const float c = r.v0x * r.v1x, d = r.v0y * r.v1y; r.d01 = c + d;
+        const float e = r.v1x * r.v1x, f = r.v1y * r.v1y; r.d11 = e + f;
+    }
+    r.denom = r.d00 * r.d11 - r.d01 * r.d01;
+    r.z0 = sz[0]; r.z1 = sz[1]; r.z2 = sz[2];
+    r.draw = draw;
+    r.local = local;
+    r.fminx = g_min(g_min(sx[0], sx[1]), sx[2]);
+    r.fmaxx = g_max(g_max(sx[0], sx[1]), sx[2]);
+    r.fminy = g_min(g_min(sy[0], sy[1]), sy[2]);
+    r.fmaxy = g_max(g_max(sy[0], sy[1]), sy[2]);
+    r.flags = flags;
+    r.ibx = pack16(floor_clamped(r.fminx, 0, fp.W), floor_clamped(r.fmaxx, -1, fp.W - 1));
+    r.iby = pack16(floor_clamped(r.fminy, 0, fp.H), floor_clamped(r.fmaxy, -1, fp.H - 1));
+    r.gbx = gbox.x; r.gby = gbox.y;
+    return r;
+}
+
+// RF_NO_RECS (binned frames): staged candidate `id`'s record -- and for single-pass tiles its shading
+// varyings -- recomputed from the resident mesh by the quad of lanes 4c .. 4c + 3 exactly as k_setup's
+// setup_quad computes them (same functions, same operands: identical bits), into the LDS copies.
+// fdraws: the frame's draw slice (batch table entries dbase ..).
+__device__ __forceinline__ void stage_from_mesh(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *fdraws, int dbase,
+                                                uint32_t id, bool shade, float4 *rec, float4 *srec) {
+    const int q = __lane_id() & 3, qv = q < 3 ? q : 2;
+    const uint32_t word = (uint32_t)fb.tdraw[id];
+    const uint2 gbox = fb.boxes[id];
+    const int d = (int)(word & 0x1fffffffu);
+    const DrawGPU &dr = fdraws[d];
+    const int local = (int)id - dr.tri_base;
+    const float *P = dr.pos + 9 * (size_t)local + 3 * qv;
+    const float p3[3] = {P[0], P[1], P[2]};
+    float n3[3] = {0.0f, 0.0f, 0.0f};
+    if (shade) {
+        const float *Nn = dr.nrm + 9 * (size_t)local + 3 * qv;
+        n3[0] = Nn[0]; n3[1] = Nn[1]; n3[2] = Nn[2];
+    }
+    float vx, vy, vz;
+    vertex_screen(fp, dr.mvp, p3[0], p3[1], p3[2], vx, vy, vz);
+    float sx[3], sy[3], sz[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sx[k] = quad_bcast(vx, k); sy[k] = quad_bcast(vy, k); sz[k] = quad_bcast(vz, k); }
+    const TriRec r = rec_from_stored(fp, d, local, sx, sy, sz, word >> 29, gbox);
+    quad_store_rec_at(reinterpret_cast<TriRec *>(rec), r);
+    if (shade) {
+        f3 a, nr;
+        corner_varyings(dr, p3, n3, a, nr);
+        quad_store_shade_at(reinterpret_cast<ShadeRec *>(srec), dbase + d, dr.shading, a, nr);
+    }
+}
+
+// RF_NO_RECS: one thread's winner (tiles whose winners are not staged: several staging passes, ghost
+// fragments) re-evaluated from the mesh -- the record's barycentric terms, the pixel's (u, v, w) and
+// depth, then the corners' varyings accumulated one corner at a time in shade_winner's operation order
+// ((a0 u + a1 v) + a2 w) -- and shaded.  draws: the batch table; dbase: the frame's slice.
+__device__ __forceinline__ void resolve_from_mesh(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, int dbase,
+                                                  uint32_t id, int px, int py, const float4 *lds_du, bool shade, float &depth,
+                                                  f3 &A, f3 &N, int &shading, float4 (&du)[4]) {
+    const int d = (int)((uint32_t)fb.tdraw[id] & 0x1fffffffu);
+    const DrawGPU &dr = draws[dbase + d];
+    const int local = (int)id - dr.tri_base;
+    const float *P = dr.pos + 9 * (size_t)local;
+    float u, v, w;
+    {
+        float sx[3], sy[3], sz[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) vertex_screen(fp, dr.mvp, P[3 * k], P[3 * k + 1], P[3 * k + 2], sx[k], sy[k], sz[k]);
+        const TriRec r = rec_from_stored(fp, d, local, sx, sy, sz, 0u, make_uint2(0u, 0u));
+        bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
+        depth = (u * r.z0 + v * r.z1) + w * r.z2;
+    }
+    if (!shade) return;
+    const float *Nn = dr.nrm + 9 * (size_t)local;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float p3[3] = {P[3 * k], P[3 * k + 1], P[3 * k + 2]};
+        const float n3[3] = {Nn[3 * k], Nn[3 * k + 1], Nn[3 * k + 2]};
+        f3 a, nr;
+        corner_varyings(dr, p3, n3, a, nr);
+        const float b = k == 0 ? u : k == 1 ? v : w;
+        A = k == 0 ? sc3(a, b) : add3(A, sc3(a, b));
+        N = k == 0 ? sc3(nr, b) : add3(N, sc3(nr, b));
+    }
+    const int bd = dbase + d;
+    if (bd < LDS_DRAWS) load_du(&lds_du[bd * 4], du);
+    else load_du(reinterpret_cast<const float4 *>(dr.light), du);
+    shading = dr.shading;
+}
+
 // One busy raster tile.  Candidates (bin box overlaps the tile) are staged in LDS; every (candidate,
 // pixel of its clipped bin box) pair is one lane-task, dealt evenly over the workgroup by a prefix
 // sum of the box areas; passing pairs atomic-min their key into the tile's LDS key array.  Then
 // each thread owns one pixel: the winner's record and varyings are fetched by index, (u, v, w)
 // recomputed with the identical arithmetic, the pixel shaded and written.
 // fb: the frame's view (frame_view); draws: the whole batch's draw table; rt: raster tile of the frame.
+template <bool NO_RECS>
 __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
                                             const uint32_t *cnt, uint32_t n_frag, int frame, int rt,
                                             const uint2 (&pbx)[CAND / 256], bool prefetched, RasterShared &sh, uint64_t *tl) {
@@ -908,6 +1058,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     const int X1 = X0 + RTW - 1, Y1 = Y0 + RTH - 1;
     const int bt = (row / (TILE / RTH)) * fp.tiles_x + col;
     const int bt_spill = frame * fp.tiles_x * fp.tiles_y + bt;   // the bin tile's key in spill entries
+    constexpr bool no_recs = NO_RECS;   // == (fp.flags & RF_NO_RECS): a kernel variant each
+    const int dbase = frame * fp.n_draws;                       // the frame's slice of the draw table
     __syncthreads();   // the previous tile's key resets are done
 
     // candidate sources.  scan mode: every triangle's bin box.  bin mode: the bin tile's list, then
@@ -983,7 +1135,11 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             // consecutive lanes load consecutive float4s of one record; all loads in one round trip
             if (tid < m) sh.id[tid] = sh.cand[c + tid];
             for (int i = tid; i < m * (RTW * RTH / 64); i += 256) sh.bits[i] = 0ull;
-            {
+            if constexpr (no_recs) {   // a quad of lanes per candidate (RCHUNK * 4 == 256)
+                const int ci = tid >> 2;
+                if (ci < m)
+                    stage_from_mesh(fp, fb, draws + dbase, dbase, sh.cand[c + ci], single, &sh.rec[ci * 6], &sh.srec[ci * 5]);
+            } else {
                 constexpr int NQ = (RCHUNK * 6 + 255) / 256, NS = (RCHUNK * 5 + 255) / 256;
                 float4 q[NQ], s[NS];
 #pragma unroll
@@ -1110,37 +1266,83 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     if (covered) {
         const uint32_t lo = (uint32_t)key;
         const uint32_t id = slot_keys ? lo >> 7 : lo, slot = slot_keys ? lo & SLOT_NONE : SLOT_NONE;
-        TriRec r;
-        ShadeRec sr;
-        {
-            float4 *d4 = reinterpret_cast<float4 *>(&r);
-            float4 *e4 = reinterpret_cast<float4 *>(&sr);
-            if (slot != SLOT_NONE) {   // only single-pass tiles encode a slot: the staged copies
+        if constexpr (!no_recs) {   // stored records: the staged copies (single-pass tiles) or HBM
+            TriRec r;
+            ShadeRec sr;
+            {
+                float4 *d4 = reinterpret_cast<float4 *>(&r);
+                float4 *e4 = reinterpret_cast<float4 *>(&sr);
+                if (slot != SLOT_NONE) {   // only single-pass tiles encode a slot: the staged copies
 #pragma unroll
-                for (int k = 0; k < 6; ++k) d4[k] = sh.rec[slot * 6 + k];
+                    for (int k = 0; k < 6; ++k) d4[k] = sh.rec[slot * 6 + k];
 #pragma unroll
-                for (int k = 0; k < 5; ++k) e4[k] = sh.srec[slot * 5 + k];
+                    for (int k = 0; k < 5; ++k) e4[k] = sh.srec[slot * 5 + k];
+                } else {
+                    const float4 *s4 = reinterpret_cast<const float4 *>(&fb.recs[id]);
+                    const float4 *h4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) d4[k] = s4[k];
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) e4[k] = h4[k];
+                }
+            }
+            float u, v, w;
+            bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
+            depth = (u * r.z0 + v * r.z1) + w * r.z2;
+            if (!(fp.flags & DBG_SKIP_SHADE)) {
+                const float4 *du = sr.draw < LDS_DRAWS ? &sh.du[sr.draw * 4] : reinterpret_cast<const float4 *>(draws[sr.draw].light);
+                float pre[3];
+                shade_winner(du, sr, u, v, w, pre);
+                const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
+                rgba = cr | (cg << 8) | (cb << 16) | (255u << 24);
+                pq = make_float4(pre[0], pre[1], pre[2], 1.0f);
+            }
+        } else {
+            const bool shade = !(fp.flags & DBG_SKIP_SHADE);
+            f3 A = {0.f, 0.f, 0.f}, N = {0.f, 0.f, 0.f};   // interpolated varyings (shade_interp's inputs)
+            int shading = 0;
+            float4 du[4];
+            if (no_recs && slot == SLOT_NONE) {   // binned frame, winner not staged: recomputed from the mesh
+                resolve_from_mesh(fp, fb, draws, dbase, id, px, py, sh.du, shade, depth, A, N, shading, du);
             } else {
-                const float4 *s4 = reinterpret_cast<const float4 *>(&fb.recs[id]);
-                const float4 *h4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
-#pragma unroll
-                for (int k = 0; k < 6; ++k) d4[k] = s4[k];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) e4[k] = h4[k];
+                TriRec r;
+                ShadeRec sr;
+                {
+                    float4 *d4 = reinterpret_cast<float4 *>(&r);
+                    float4 *e4 = reinterpret_cast<float4 *>(&sr);
+                    if (slot != SLOT_NONE) {   // only single-pass tiles encode a slot: the staged copies
+    #pragma unroll
+                        for (int k = 0; k < 6; ++k) d4[k] = sh.rec[slot * 6 + k];
+    #pragma unroll
+                        for (int k = 0; k < 5; ++k) e4[k] = sh.srec[slot * 5 + k];
+                    } else {
+                        const float4 *s4 = reinterpret_cast<const float4 *>(&fb.recs[id]);
+                        const float4 *h4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
+    #pragma unroll
+                        for (int k = 0; k < 6; ++k) d4[k] = s4[k];
+    #pragma unroll
+                        for (int k = 0; k < 5; ++k) e4[k] = h4[k];
+                    }
+                }
+                float u, v, w;
+                bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
+                depth = (u * r.z0 + v * r.z1) + w * r.z2;
+                if (shade) {
+                    if (sr.draw < LDS_DRAWS) load_du(&sh.du[sr.draw * 4], du);
+                    else load_du(reinterpret_cast<const float4 *>(draws[sr.draw].light), du);
+                    shading = sr.shading;
+                    interp_varyings(sr, u, v, w, A, N);
+                }
+            }
+            if (shade) {
+                float pre[3];
+                shade_interp(du, shading, A, N, pre);
+                const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
+                rgba = cr | (cg << 8) | (cb << 16) | (255u << 24);
+                pq = make_float4(pre[0], pre[1], pre[2], 1.0f);
             }
         }
-        float u, v, w;
-        bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
-        depth = (u * r.z0 + v * r.z1) + w * r.z2;
-        if (!(fp.flags & DBG_SKIP_SHADE)) {
-            const float4 *du = sr.draw < LDS_DRAWS ? &sh.du[sr.draw * 4] : reinterpret_cast<const float4 *>(draws[sr.draw].light);
-            float pre[3];
-            shade_winner(du, sr, u, v, w, pre);
-            const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
-            rgba = cr | (cg << 8) | (cb << 16) | (255u << 24);
-            pq = make_float4(pre[0], pre[1], pre[2], 1.0f);
         }
-    }
     tl_mark(tl, tls, 4);
     if (tl && tid == 0) { tl[TL_STRIDE * tls + 8] = seq; tl[TL_STRIDE * tls + 9] = (uint64_t)pairs; }
     const uint64_t cm = __ballot(covered);
@@ -1227,7 +1429,7 @@ constexpr int STRIP_RT = 2;   // raster-tile rows per clear item
 #ifndef SHS_LEGACY_RASTER_WAVES
 #define SHS_LEGACY_RASTER_WAVES 4   // minimum waves per SIMD (-D...: timing experiments)
 #endif
-template <bool KARG>
+template <bool KARG, bool NO_RECS>
 __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
     const int tid = threadIdx.x;
@@ -1287,9 +1489,9 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
                 __syncthreads();
                 clear_tile(fp, fv, rt);
             } else {
-                if (fp.flags & DBG_TWICE) raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
+                if (fp.flags & DBG_TWICE) raster_tile<NO_RECS>(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
                 tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
-                raster_tile(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
+                raster_tile<NO_RECS>(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
                 first = false;
             }
         }
@@ -1332,10 +1534,15 @@ hipError_t launch_ghost(const FrameParams &fp, const FrameBuffers &fb, hipStream
 }
 
 hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, int grid, hipStream_t s) {
-    if (fp.n_draws * fp.n_frames <= KARG_DRAWS)   // the whole batch's draws travel as kernel arguments
-        hipLaunchKernelGGL(k_raster<true>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
-    else
-        hipLaunchKernelGGL(k_raster<false>, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fp, fb, ka);
+    const dim3 g(grid > 0 ? grid : 1);
+    const bool karg = fp.n_draws * fp.n_frames <= KARG_DRAWS;   // the whole batch's draws as kernel arguments
+    if (fp.flags & RF_NO_RECS) {   // binned frames: records recomputed from the mesh
+        if (karg) hipLaunchKernelGGL((k_raster<true, true>), g, dim3(256), 0, s, fp, fb, ka);
+        else hipLaunchKernelGGL((k_raster<false, true>), g, dim3(256), 0, s, fp, fb, ka);
+    } else {
+        if (karg) hipLaunchKernelGGL((k_raster<true, false>), g, dim3(256), 0, s, fp, fb, ka);
+        else hipLaunchKernelGGL((k_raster<false, false>), g, dim3(256), 0, s, fp, fb, ka);
+    }
     return hipGetLastError();
 }
 
