@@ -106,6 +106,31 @@ def run_gpu(args, rank, local_rank, world, dist):
         ctx.set_raster_loop(args.raster_loop)
     prepared = [ctx.prepare_batch(frame, fds) for fds in sets]
     render = ctx.render_batch_prepared
+    # The auxiliary legs run BEFORE the headline loop: every frame they render is measured for its own
+    # figure, and the loop that follows starts on a GPU that has been rendering (clocks up), as a render
+    # loop's frames do -- not right after process start-up (tools/diag_short_window.py).
+    single = None
+    if F > 1 and not args.child and not args.no_single:
+        # the single-frame latency figure: one shs_render_legacy per step
+        one = ctx.prepare(frame, sets[0][0])
+        for _ in range(10):
+            ctx.render_prepared(one)
+        ctx.synchronize()
+        n1 = max(20, min(args.steps * 4, 400))
+        ctx.enable_timing(True)
+        ctx.timing_reset()
+        t1 = time.perf_counter()
+        for _ in range(n1):
+            ctx.render_prepared(one)
+        ctx.synchronize()
+        el1 = time.perf_counter() - t1
+        _, k1 = ctx.timing_read()
+        ctx.enable_timing(False)
+        single = {"ms_per_frame": round(el1 / n1 * 1e3, 5), "steps": n1,
+                  "kernels_ms": {k: round(v, 5) for k, v in k1.items()}}
+    pcie = None
+    if F > 1 and world == 1 and not args.child and not args.no_pcie:
+        pcie = seam1_pcie(args, ctx, frame, sets)
     for i in range(max(args.warmup, 1)):
         render(prepared[i % POSE_SETS])
     ctx.synchronize()
@@ -130,32 +155,8 @@ def run_gpu(args, rank, local_rank, world, dist):
     elapsed = time.perf_counter() - t0
     n_launches, kms = ctx.timing_read()
     ctx.enable_timing(False)
-    single = None
-    if F > 1 and not args.child and not args.no_single:
-        # the single-frame latency figure beside it: one shs_render_legacy per step
-        one = ctx.prepare(frame, sets[0][0])
-        for _ in range(10):
-            ctx.render_prepared(one)
-        ctx.synchronize()
-        n1 = max(20, min(args.steps * 4, 400))
-        ctx.enable_timing(True)
-        ctx.timing_reset()
-        t1 = time.perf_counter()
-        for _ in range(n1):
-            ctx.render_prepared(one)
-        ctx.synchronize()
-        el1 = time.perf_counter() - t1
-        _, k1 = ctx.timing_read()
-        ctx.enable_timing(False)
-        single = {"ms_per_frame": round(el1 / n1 * 1e3, 5), "steps": n1,
-                  "kernels_ms": {k: round(v, 5) for k, v in k1.items()}}
-    if F > 1 and world == 1 and not args.child and not args.no_pcie:
-        single = single or {}
-        pcie = seam1_pcie(args, ctx, frame, sets)
-        ctx.close()
-        return frame, sets[0][0], stats, elapsed, n_launches, kms, single, pcie
     ctx.close()
-    return frame, sets[0][0], stats, elapsed, n_launches, kms, single, None
+    return frame, sets[0][0], stats, elapsed, n_launches, kms, single, pcie
 
 
 def seam1_pcie(args, ctx, frame, sets):

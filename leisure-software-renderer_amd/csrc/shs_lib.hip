@@ -1398,7 +1398,76 @@ struct LtWave {
     uint32_t list = 0xffffffffu;
     uint32_t count = 0;
     const uint32_t *ids = nullptr;   // LDS
+    uint32_t *fids = nullptr;        // LDS, 128 entries: the list culled by the wave's world box
+    uint32_t *box = nullptr;         // LDS, 6 words: the wave's world box (orderable bits)
 };
+
+// float <-> unsigned with the same order (box reductions through LDS unsigned atomics)
+__device__ __forceinline__ uint32_t f2ord(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t o) { return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o); }
+
+// The wave's light list culled by the box of its shading lanes' world positions (the active lanes;
+// a wave-uniform list, LtWave): point_light adds exactly nothing for a light whose range sphere the
+// pixel lies outside -- it returns before touching `lit` when its float d2 > range^2 (1 + 2^-20) or
+// sqrt(d2) > range -- and the float d2 of any pixel in the box is at least the box's exact squared
+// distance to the light times (1 - 2^-21) (three roundings of the differences, squares and sums).
+// The box distance here, computed in float (a few roundings, relative 2^-22), is compared with
+// range^2 * (1 + 2^-10): a culled light is out of every lane's range with a wide margin, so the
+// survivors in list order give bit-identical sums.  Lanes with a non-finite world position keep the
+// whole list (their sums depend on every light).  Returns the culled count; ids -> lw.fids.
+__device__ __forceinline__ uint32_t cull_wave_list(const LibFrameParams &fp, const LibBuffers &fb, const LtWave &lw, f3 world,
+                                                   bool lds) {
+    const uint64_t ex = __ballot(1);
+    const bool fin = isfinite(world.x) && isfinite(world.y) && isfinite(world.z);
+    if (!lds || __ballot(!fin) != 0ull) return 0xffffffffu;   // (lights staged in LDS: <= LIB_LDS_LIGHTS)
+    const int lane = __lane_id();
+    const int first = __ffsll((unsigned long long)ex) - 1;
+    uint32_t *bx = lw.box;
+    __builtin_amdgcn_wave_barrier();   // the previous call's reads of the box are issued
+    if (lane == first) {
+        bx[0] = bx[1] = bx[2] = 0xffffffffu;
+        bx[3] = bx[4] = bx[5] = 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    atomicMin(&bx[0], f2ord(world.x)); atomicMin(&bx[1], f2ord(world.y)); atomicMin(&bx[2], f2ord(world.z));
+    atomicMax(&bx[3], f2ord(world.x)); atomicMax(&bx[4], f2ord(world.y)); atomicMax(&bx[5], f2ord(world.z));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const float lx = ord2f(bx[0]), ly = ord2f(bx[1]), lz = ord2f(bx[2]);
+    const float hx = ord2f(bx[3]), hy = ord2f(bx[4]), hz = ord2f(bx[5]);
+    const uint32_t n_act = (uint32_t)__popcll(ex);
+    const uint32_t rank = (uint32_t)__popcll(ex & ((1ull << lane) - 1ull));
+    uint32_t w = 0u;
+    for (uint32_t base = 0; base < lw.count; base += n_act) {
+        const uint32_t i = base + rank;
+        bool keep = false;
+        uint32_t idx = 0u;
+        if (i < lw.count) {
+            idx = lw.ids[i];
+            if (idx < fp.n_lights) {
+                const float4 pr = lib_lds_lights[4 * idx];
+                // (fmaxf, not s_max: ROCm 7.2's instruction selection crashes on the select form here;
+                // a NaN difference gives gap 0 -- kept -- and an infinite light position an infinite gap,
+                // which point_light's d2 test rejects as well)
+                const float gx = fmaxf(0.0f, fmaxf(lx - pr.x, pr.x - hx));
+                const float gy = fmaxf(0.0f, fmaxf(ly - pr.y, pr.y - hy));
+                const float gz = fmaxf(0.0f, fmaxf(lz - pr.z, pr.z - hz));
+                const float d2 = (gx * gx + gy * gy) + gz * gz;
+                keep = !(d2 > (pr.w * pr.w) * (1.0f + 0x1p-10f));   // NaN / inf ranges: kept
+            }
+        }
+        const uint64_t m = __ballot(keep);
+        if (keep) lw.fids[w + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = idx;
+        w += (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    return w;
+}
 
 // The pixel's tile list (tiled modes; fp_stress_scene.frag:644-652 tile index).
 __device__ __forceinline__ uint32_t lt_tile_list(const LibFrameParams &fp, int px, int py) {
@@ -1410,6 +1479,7 @@ __device__ __forceinline__ uint32_t lt_tile_list(const LibFrameParams &fp, int p
 // Forward+ program: the pixel's light list (fp_stress_scene.frag:644-685 selection: a saturated list
 // falls back to every light) through PointLightModel::sample, combined as the software light-culling
 // demo does (hello_light_types_culling_sw.cpp:404-416): ambient hemisphere + sum, clamped to [0,1].
+template <bool CULL>
 __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const LibDrawGPU &dr, f3 world, f3 nrm, int px, int py,
                            const LtWave &lw) {
     const f3 N = normalize3(nrm);
@@ -1438,8 +1508,14 @@ __device__ f3 forward_plus(const LibFrameParams &fp, const LibBuffers &fb, const
         for (uint32_t i = 0; i < fp.n_lights; ++i)
             point_light(lds ? plight_lds(i) : plight_global(fb.lights[i]), world, N, V, base, lit);
     } else if (uni) {   // the list in the wave's LDS slice: one broadcast index per light
-        for (uint32_t i = 0; i < count; ++i) {   // C4 0.828 -> 0.815 ms against LDS-staged lights
-            const uint32_t idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)lw.ids[i]);   // uniform
+        const uint32_t *ids = lw.ids;
+        uint32_t n = count;
+        if (CULL && lw.fids) {   // culled by the wave's world box (exact: cull_wave_list)
+            const uint32_t nc = (uint32_t)__builtin_amdgcn_readfirstlane((int)cull_wave_list(fp, fb, lw, world, lds));
+            if (nc != 0xffffffffu) { ids = lw.fids; n = nc; }
+        }
+        for (uint32_t i = 0; i < n; ++i) {   // C4 0.828 -> 0.815 ms against LDS-staged lights
+            const uint32_t idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)ids[i]);   // uniform
             if (idx < fp.n_lights) point_light(plight_uniform(fb.lights, idx), world, N, V, base, lit);
         }
     } else {
@@ -1489,7 +1565,7 @@ __device__ f3 lib_fragment(const LibFrameParams &fp, const LibBuffers &fb, const
                            int px, int py, const LtWave &st, f3 tex = f3{1.0f, 1.0f, 1.0f}) {
     const f3 bc = {dr.base[0], dr.base[1], dr.base[2]};
     const int program = PROG >= 0 ? PROG : dr.program;
-    if (program == 5) return forward_plus(fp, fb, dr, world, nrm, px, py, st);
+    if (program == 5) return forward_plus<true>(fp, fb, dr, world, nrm, px, py, st);
     if (program == 2) return bc;                                                   // debug albedo
     if (program == 3) return add3(sc3(normalize3(nrm), 0.5f), f3{0.5f, 0.5f, 0.5f});  // debug normal
     if (program == 4) {                                                            // debug depth
@@ -2277,6 +2353,8 @@ __global__ __launch_bounds__(256, PROG == 5 ? SHS_RESOLVE_WAVES_FP : PROG == 0 ?
 void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
     __shared__ float tm_thr[256];
     __shared__ uint32_t wlist[PROG == 0 ? 1 : 4][128];   // per wave: its block's light list (LtWave)
+    __shared__ uint32_t wflist[PROG == 0 ? 1 : 4][128];  // ... culled by the wave's world box
+    __shared__ uint32_t wbox[PROG == 0 ? 1 : 4][8];      // ... and that box
     __shared__ uint32_t s_cov;                            // covered pixels of this workgroup's blocks
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) s_cov = 0u;
@@ -2317,6 +2395,10 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
                 lw.list = l0;
                 lw.count = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
                 lw.ids = wl;
+                if (!(fp.exp_flags & 16u)) {   // (exp bit 4: no wave culling -- timing experiments)
+                    lw.fids = wflist[PROG == 0 ? 0 : wave];
+                    lw.box = wbox[PROG == 0 ? 0 : wave];
+                }
                 __builtin_amdgcn_wave_barrier();   // the previous block's reads of the slice are issued
                 if ((uint32_t)lane < lw.count) wl[lane] = ids[lane];
                 if ((uint32_t)(64 + lane) < lw.count) wl[64 + lane] = ids[64 + lane];
