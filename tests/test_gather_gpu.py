@@ -29,6 +29,7 @@ def test_lib_shards_gather_on_device(W, H, count):
         h, d, m = _render_lib(c, frame, draws)
         words = c.tiles_packed_words(c.TARGET_LIB, count)
         buf = torch.zeros(words, dtype=torch.int32, device="cuda:0")
+        torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
         c.tiles_pack(c.TARGET_LIB, r, count, buf.data_ptr())
         c.synchronize_lib()
         host = shard.pack_padded(shard.planes_of([(h, False), (d, False), (m, False)]), W, H, r, count)
@@ -62,6 +63,7 @@ def test_legacy_shards_gather_on_device():
         c.render(shs_gpu.Frame(640, 480, shard_rank=r, shard_count=count), draws)
         c.resolve()
         buf = torch.zeros(c.tiles_packed_words(c.TARGET_LEGACY, count), dtype=torch.int32, device="cuda:0")
+        torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
         c.tiles_pack(c.TARGET_LEGACY, r, count, buf.data_ptr())
         c.synchronize()
         ctxs.append(c)
@@ -100,6 +102,7 @@ def test_lib_present_gather_after_sharded_tonemap(count, fused):
             c.render_pbr_forward(frame, draws)
             c.tonemap(1.0, 2.2, ldr=False, present=True)
         buf = torch.zeros(c.tiles_packed_words(c.TARGET_LIB_PRESENT, count), dtype=torch.int32, device="cuda:0")
+        torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
         c.tiles_pack(c.TARGET_LIB_PRESENT, r, count, buf.data_ptr())   # finishes the pass chain first
         c.synchronize_lib()
         _, pres = c.resolve_ldr()
@@ -132,6 +135,7 @@ def test_legacy_present_gather():
         f.present = True
         c.render(f, draws)
         buf = torch.zeros(c.tiles_packed_words(c.TARGET_PRESENT, count), dtype=torch.int32, device="cuda:0")
+        torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
         c.tiles_pack(c.TARGET_PRESENT, r, count, buf.data_ptr())
         c.synchronize()
         ctxs.append(c)
@@ -223,6 +227,7 @@ def test_gather_frame_device_reuses_buffers():
                 c.fuse_tonemap(1.0, 2.2, ldr=False, present=True)
                 c.render_pbr_forward(frame, draws)
                 b = torch.zeros(c.tiles_packed_words(c.TARGET_LIB_PRESENT, count), dtype=torch.int32, device="cuda:0")
+                torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
                 c.tiles_pack(c.TARGET_LIB_PRESENT, r, count, b.data_ptr())
                 c.synchronize_lib()
                 packed.append(b)

@@ -146,6 +146,7 @@ def test_region_gather_device_present(oracle_mod):
                 frame.shard_rank, frame.shard_count = r, count
                 c.render_pbr_forward(frame, draws)
                 b = torch.zeros(c.tiles_packed_words(c.TARGET_LIB_PRESENT, count), dtype=torch.int32, device="cuda:0")
+                torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
                 c.tiles_pack(c.TARGET_LIB_PRESENT, r, count, b.data_ptr())
                 c.synchronize_lib()
                 packed.append(b)

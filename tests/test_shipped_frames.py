@@ -99,6 +99,7 @@ def test_sharded_4k_frame_composes_to_oracle(oracle_mod, cfg):
             ctx.render_pbr_forward(frame, draws)
             for target, keep in ((ctx.TARGET_LIB, lib_bufs), (ctx.TARGET_LIB_PRESENT, pres_bufs)):
                 buf = torch.zeros(ctx.tiles_packed_words(target, count), dtype=torch.int32, device="cuda:0")
+                torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
                 ctx.tiles_pack(target, r, count, buf.data_ptr())
                 keep.append(buf)
             ctx.synchronize_lib()

@@ -109,6 +109,7 @@ def test_region_sharded_4k_frames_compose_to_oracle(oracle_mod, c4_ref, c5_ref, 
                         words = c.tiles_packed_words(target, RANKS)
                         assert c.tiles_rank_words(target, r, RANKS) <= words
                         buf = torch.zeros(max(words, 1), dtype=torch.int32, device="cuda:0")
+                        torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
                         c.tiles_pack(target, r, RANKS, buf.data_ptr())
                         keep[r] = buf
                 c.synchronize_lib()
