@@ -131,6 +131,19 @@ def run_gpu(args, rank, local_rank, world, dist):
     pcie = None
     if F > 1 and world == 1 and not args.child and not args.no_pcie:
         pcie = seam1_pcie(args, ctx, frame, sets)
+    # Clock ramp: the GPU reaches its steady-state clocks only after ~15-20 ms of continuous rendering
+    # (tools/diag_short_window.py: consecutive 20-step windows right after 5 warm-up steps run 0.304,
+    # 0.294, then 0.285 ms/step, k_raster 0.260 -> 0.242 ms; profiles/r04_c2_short_window.txt).  A render
+    # loop runs continuously, so the headline window starts after args.ramp_ms of the same batches
+    # (untimed, like the warm-up steps that follow it).
+    t_ramp = time.perf_counter()
+    n_ramp = 0
+    while args.ramp_ms > 0 and (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
+        for _ in range(8):
+            render(prepared[n_ramp % POSE_SETS])
+            n_ramp += 1
+        ctx.synchronize()
+    ramp = {"ms": round((time.perf_counter() - t_ramp) * 1e3, 1), "batches": n_ramp}
     for i in range(max(args.warmup, 1)):
         render(prepared[i % POSE_SETS])
     ctx.synchronize()
@@ -156,7 +169,7 @@ def run_gpu(args, rank, local_rank, world, dist):
     n_launches, kms = ctx.timing_read()
     ctx.enable_timing(False)
     ctx.close()
-    return frame, sets[0][0], stats, elapsed, n_launches, kms, single, pcie
+    return frame, sets[0][0], stats, elapsed, n_launches, kms, single, pcie, ramp
 
 
 def seam1_pcie(args, ctx, frame, sets):
@@ -614,6 +627,8 @@ def main():
                     help="c4/c5 at N > 1: tile ownership (one cost-balanced rectangle per rank, or tile %% N)")
     ap.add_argument("--root-share", type=float, default=0.85,
                     help="c4/c5 regions: rank 0's share of the predicted cost (it also unpacks the gather)")
+    ap.add_argument("--ramp-ms", type=float, default=60.0,
+                    help="legacy configs: untimed rendering before the warm-up so the GPU clocks reach steady state")
     ap.add_argument("--shadow-full", action="store_true",
                     help="c5: render the whole shadow map every frame (default: the camera pass's footprint, "
                          "SHS_OPT_SHADOW_FOOTPRINT)")
@@ -669,7 +684,7 @@ def main():
 
     if args.config in LIB_CONFIGS:
         return main_lib(args, world, rank, local_rank, dist, pmc, pmc_err)
-    frame, draws, stats, elapsed, n_launches, kms, single, pcie = run_gpu(args, rank, local_rank, world, dist)
+    frame, draws, stats, elapsed, n_launches, kms, single, pcie, ramp = run_gpu(args, rank, local_rank, world, dist)
     B1, n_tri1 = algorithmic_bytes(frame, draws)
     F = args.frames_per_step
     B, n_tri = B1 * F, n_tri1 * F          # per step (= per k_raster launch)
@@ -744,6 +759,7 @@ def main():
         "timed_launches_with_events": n_launches,
         "roofline": roofline,
     }
+    line["clock_ramp"] = dict(ramp, what="untimed batches before the warm-up: steady-state GPU clocks")
     if single:
         line["single_frame"] = single
     if pcie is not None:

@@ -326,10 +326,12 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.epoch = ctx->busy_epoch;
     fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
     if (!fp.scan_mode) HIP_TRY(ctx, hipMemsetAsync(ws.tile_count.p, 0, n_bt_all * sizeof(uint32_t), sst));
-    // Binned frames keep no per-triangle records (k_raster recomputes them from the resident mesh);
-    // SHS_LEGACY_RECS=1 stores them anyway (timing experiments).
-    static const bool keep_recs_env = std::getenv("SHS_LEGACY_RECS") && std::atoi(std::getenv("SHS_LEGACY_RECS")) != 0;
-    const bool no_recs = !fp.scan_mode && !keep_recs_env;
+    // SHS_LEGACY_NORECS=1: binned frames keep no per-triangle records, k_raster recomputes them from the
+    // resident mesh (RF_NO_RECS).  Off by default: measured C3 0.670 -> 0.699 ms per 16-frame step (the
+    // staged candidates' draw -> matrix -> position chain costs more raster latency than the 184 B of
+    // record traffic it removes).
+    static const bool no_recs_env = std::getenv("SHS_LEGACY_NORECS") && std::atoi(std::getenv("SHS_LEGACY_NORECS")) != 0;
+    const bool no_recs = !fp.scan_mode && no_recs_env;
     if (no_recs) {
         fp.flags |= shs_dev::RF_NO_RECS;
         if (ensure(ctx, ws.tdraw, nt_all)) return SHS_ERR_HIP;
@@ -672,7 +674,7 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
     if (set_dev(ctx)) return SHS_ERR_HIP;
     int rc = finish_frame(ctx);
     if (rc) return rc;
-    if (ctx->last_no_recs) { ctx->err = "binned frames keep no triangle records (SHS_LEGACY_RECS=1 stores them)"; return SHS_ERR_INVALID; }
+    if (ctx->last_no_recs) { ctx->err = "SHS_LEGACY_NORECS frames keep no triangle records"; return SHS_ERR_INVALID; }
     *n_out = ctx->last_n_tris;
     if (out && capacity > 0) {
         const size_t n = (size_t)std::min<int64_t>(capacity, ctx->last_n_tris);

@@ -102,11 +102,12 @@ constexpr uint32_t DBG_SKIP_GHOST = 1u << 8, DBG_SKIP_SHADE = 1u << 9, DBG_CLEAR
 // Raster inner loop (frame flags bit 16, set by the context from SHS_OPT_RASTER_LOOP): per-pixel
 // candidate loop instead of (candidate, pixel) pair tasks.  Results are identical either way.
 constexpr uint32_t RF_PER_PIXEL = 1u << 16;
-// Binned (large) frames keep no per-triangle records in HBM (frame flags bit 17, set by the context in
-// bin mode): k_setup writes only the bin box and the draw of each triangle (12 B instead of the 184-B
-// TriRec + ShadeRec), and k_raster recomputes a staged candidate's record -- and a winner's shading
-// varyings -- from the resident mesh with the identical arithmetic (a quad of lanes per candidate, as
-// k_setup).  Unbounded slivers (TRI_UNBOUNDED) still store their record for k_ghost.
+// Binned frames without per-triangle records in HBM (frame flags bit 17; SHS_LEGACY_NORECS=1, a
+// measured alternative, off by default): k_setup writes only the bin box and a draw|flags word of each
+// triangle (12 B instead of the 184-B TriRec + ShadeRec), and k_raster recomputes a staged candidate's
+// record -- and a winner's shading varyings -- from the resident mesh with the identical arithmetic (a
+// quad of lanes per candidate, as k_setup).  Unbounded slivers (TRI_UNBOUNDED) still store their
+// record for k_ghost.
 constexpr uint32_t RF_NO_RECS = 1u << 17;
 
 // Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);

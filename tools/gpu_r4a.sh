@@ -12,11 +12,11 @@ for c in c3 c4 c5; do
   timeout -k 10 200 python bench.py --config $c --no-pmc --no-cpu --steps 100 --warmup 10 > gpurun_out/r4a_$c.log 2>&1 || exit 1
 done
 SHS_LIB_EXP=16 timeout -k 10 200 python bench.py --config c4 --no-pmc --no-cpu --steps 100 --warmup 10 > gpurun_out/r4a_c4_nocull.log 2>&1 || exit 1
-SHS_LEGACY_RECS=1 timeout -k 10 200 python bench.py --config c3 --no-pmc --no-cpu --steps 100 --warmup 10 > gpurun_out/r4a_c3_recs.log 2>&1 || exit 1
+SHS_LEGACY_NORECS=1 timeout -k 10 200 python bench.py --config c3 --no-pmc --no-cpu --steps 100 --warmup 10 > gpurun_out/r4a_c3_norecs.log 2>&1 || exit 1
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-pmc --no-cpu > gpurun_out/r4a_c2_short.log 2>&1 || exit 1
 timeout -k 10 200 python bench.py --steps 200 --warmup 20 --no-pmc --no-cpu > gpurun_out/r4a_c2_long.log 2>&1 || exit 1
 cat gpurun_out/r4a_win.log gpurun_out/r4a_win_pre.log
-for f in c3 c3_recs c4 c4_nocull c5 c2_short c2_long; do
+for f in c3 c3_norecs c4 c4_nocull c5 c2_short c2_long; do
   python - gpurun_out/r4a_$f.log $f <<'PY'
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith('{')][-1]
