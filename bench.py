@@ -136,6 +136,8 @@ def run_gpu(args, rank, local_rank, world, dist):
     # 0.294, then 0.285 ms/step, k_raster 0.260 -> 0.242 ms; profiles/r04_c2_short_window.txt).  A render
     # loop runs continuously, so the headline window starts after args.ramp_ms of the same batches
     # (untimed, like the warm-up steps that follow it).
+    if args.pipeline:   # SHS_OPT_LEGACY_PIPELINE: a batch's raster in the next batch's launch (k_pipe)
+        ctx.set_legacy_pipeline(True)
     t_ramp = time.perf_counter()
     n_ramp = 0
     while args.ramp_ms > 0 and (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
@@ -627,6 +629,9 @@ def main():
                     help="c4/c5 at N > 1: tile ownership (one cost-balanced rectangle per rank, or tile %% N)")
     ap.add_argument("--root-share", type=float, default=0.85,
                     help="c4/c5 regions: rank 0's share of the predicted cost (it also unpacks the gather)")
+    ap.add_argument("--pipeline", type=int, default=1, choices=[0, 1],
+                    help="legacy configs: SHS_OPT_LEGACY_PIPELINE for the timed batches (each batch's raster in the "
+                         "next batch's launch; eligible: multi-draw scan-mode batches, i.e. C1 / C2)")
     ap.add_argument("--ramp-ms", type=float, default=60.0,
                     help="legacy configs: untimed rendering before the warm-up so the GPU clocks reach steady state")
     ap.add_argument("--shadow-full", action="store_true",
@@ -751,7 +756,7 @@ def main():
                 "reference scene constants (camera (0,5,-20) fov60, light, colour)",
         "config": {"workload": WORKLOADS[args.config], "width": frame.width, "height": frame.height,
                    "tris_per_frame": n_tri1, "frames_per_step_per_gpu": F,
-                   "pose_sets": POSE_SETS,
+                   "pose_sets": POSE_SETS, "legacy_pipeline": bool(args.pipeline),
                    "parallelism": f"frame-parallel x{world}" if world > 1 else "single GPU"},
         "shaded_mpix_s": round(mpix, 3),
         "batch_stats": stats,

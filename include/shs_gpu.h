@@ -223,6 +223,13 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * the frame's images are identical.  shs_resolve_shadow_map of a recorded pass renders it whole.
  * 0 (default): every shadow pass renders the whole map when it is called. */
 #define SHS_OPT_SHADOW_FOOTPRINT 11
+/* SHS_OPT_LEGACY_PIPELINE: 1 = multi-draw scan-mode legacy batches (shs_render_legacy_batch with more
+ * than 6 draws in all, scenes up to 4096 triangles) are pipelined: batch k's raster runs in the same
+ * launch as batch k + 1's setup, or at the next call that needs the frames (shs_synchronize, every
+ * resolve / present / tiles call, a non-pipelined render, shs_set_stream).  The frames are identical;
+ * what changes is that a batch's frames are final only after such a call -- work the caller queues on
+ * the context stream right after shs_render_legacy_batch does not see them.  0 (default): off. */
+#define SHS_OPT_LEGACY_PIPELINE 12
 int shs_set_option(shs_ctx *ctx, int option, int64_t value);
 /* The regions of the last region-sharded camera pass: rects[4 r .. 4 r + 3] = (bx0, by0, bx1, by1) of
  * rank r, bin tiles, inclusive (bx1 < bx0: rank r owns nothing). */

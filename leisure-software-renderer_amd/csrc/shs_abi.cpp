@@ -25,6 +25,8 @@ using shs_dev::TriRec;
 
 extern "C" {
 
+static int flush_pending(shs_ctx *ctx);   // SHS_OPT_LEGACY_PIPELINE (below enqueue_frame's helpers)
+
 int shs_abi_version(void) { return 1; }
 
 int shs_gpu_tile_size(void) { return shs_dev::TILE; }
@@ -111,6 +113,7 @@ const char *shs_last_error(shs_ctx *ctx) { return ctx ? ctx->err.c_str() : "null
 
 int shs_set_stream(shs_ctx *ctx, void *s) {
     if (!ctx) return SHS_ERR_INVALID;
+    if (flush_pending(ctx)) return SHS_ERR_HIP;   // on the stream its setup ran on
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
     ctx->stream = s ? reinterpret_cast<hipStream_t>(s) : ctx->own_stream;
@@ -142,6 +145,7 @@ int shs_mesh_release(shs_ctx *ctx, int32_t id) {
         const int rc = shs_lib_flush_shadow(ctx);
         if (rc) return rc;
     }
+    if (flush_pending(ctx)) return SHS_ERR_HIP;   // a pending legacy raster may read it too
     HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     Mesh &m = ctx->meshes[id];
@@ -194,7 +198,7 @@ static int harvest_slot(shs_ctx *ctx, int k) {
     HIP_TRY(ctx, hipEventElapsedTime(&ms[0], ctx->ring_ev[k][0], ctx->ring_ev[k][1]));
     HIP_TRY(ctx, hipEventElapsedTime(&ms[3], ctx->ring_ev[k][3], ctx->ring_ev[k][2]));
     for (int i = 0; i < 4; ++i) { ctx->acc_ms[i] += ms[i]; ctx->last_ms[i] = ms[i]; }
-    ctx->acc_frames++;
+    if (ctx->ring_counts[k]) ctx->acc_frames++;
     ctx->ring_pending[k] = false;
     return SHS_OK;
 }
@@ -205,6 +209,41 @@ static int harvest_all(shs_ctx *ctx) {
         int rc = harvest_slot(ctx, (ctx->ring_next + j) % shs_ctx::RING);
         if (rc) return rc;
     }
+    return SHS_OK;
+}
+
+// The next ring entry's events (timing on), or nullptr; counts: the entry is a batch's enqueue.
+static int ring_take(shs_ctx *ctx, bool counts, hipEvent_t *&ev) {
+    ev = nullptr;
+    if (!ctx->timing) return SHS_OK;
+    const int k = ctx->ring_next;
+    ctx->ring_next = (k + 1) % shs_ctx::RING;
+    if (harvest_slot(ctx, k)) return SHS_ERR_HIP;
+    if (!ctx->ring_ev[k][0])
+        for (int i = 0; i < 5; ++i) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ring_ev[k][i], hipEventDisableSystemFence));
+    ev = ctx->ring_ev[k];
+    ctx->ring_pending[k] = true;
+    ctx->ring_counts[k] = counts;
+    return SHS_OK;
+}
+
+// SHS_OPT_LEGACY_PIPELINE: launch the pending batch's raster on its own (k_raster), stream-ordered after
+// its setup.  Everything that reads a batch's frames, or enqueues work that is not pipelined, calls this.
+static int flush_pending(shs_ctx *ctx) {
+    if (!ctx->pend.on) return SHS_OK;
+    ctx->pend.on = false;
+    static const shs_dev::KArgDraws no_karg = {};   // pipelined batches use the device draw table
+    hipEvent_t *ev = nullptr;
+    if (ring_take(ctx, false, ev)) return SHS_ERR_HIP;
+    hipStream_t st = ctx->stream;
+    if (ev) {   // the raster's time joins the batch sums (no batch of its own)
+        HIP_TRY(ctx, hipEventRecord(ev[0], st));
+        HIP_TRY(ctx, hipEventRecord(ev[1], st));
+        HIP_TRY(ctx, hipEventRecord(ev[3], st));
+    }
+    HIP_TRY(ctx, shs_internal::launch_raster(ctx->pend.fp, ctx->pend.fb, no_karg, ctx->pend.grid, st));
+    if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));
+    HIP_TRY(ctx, hipEventRecord(ctx->lslot[ctx->pend.slot].raster_done, st));
     return SHS_OK;
 }
 
@@ -225,13 +264,24 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (total * n_frames > 0x3fffffff) { ctx->err = "too many triangles in one batch"; return SHS_ERR_INVALID; }
     const int n_tris = (int)total;   // per frame (every frame of a batch has the same count)
     const size_t nt_all = (size_t)std::max(n_tris, 1) * n_frames;
+    static const bool ghost_list_env = std::getenv("SHS_GHOST_LIST") && std::atoi(std::getenv("SHS_GHOST_LIST")) != 0;
+    const bool scan = ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS);
+    // pipelined (SHS_OPT_LEGACY_PIPELINE): scan-mode batches (their ghost waves live in k_setup) with a
+    // device draw table; the frame buffers the pending raster writes must not be reallocated under it
+    const size_t npx0 = (size_t)f.width * f.height;
+    const bool pipe = ctx->legacy_pipeline && scan && !ghost_list_env && n_draws_all > shs_dev::KARG_DRAWS && !ctx->want_timeline;
+    const bool grows = ctx->color.cap < npx0 * 4 * n_frames || ctx->depth.cap < npx0 * n_frames ||
+                       ((f.flags & SHS_FRAME_PREQUANT) && ctx->prequant.cap < npx0 * n_frames) ||
+                       ((f.flags & SHS_FRAME_PRESENT) && ctx->present.cap < npx0 * n_frames);
+    if ((!pipe || grows) && flush_pending(ctx)) return SHS_ERR_HIP;
 
     // This batch's workspace slot.  Its previous user (batch n - 2) is complete on the host side once
     // its k_setup is (the pinned draw table is rewritten below), and on the device side once its
     // k_raster is (setup_stream waits for raster_done before reusing the slot's buffers).
     const int slot = (int)(ctx->frame_index & 1u);
     shs_ctx::LegacySlot &ws = ctx->lslot[slot];
-    hipStream_t sst = ctx->setup_stream, st = ctx->stream;
+    // pipelined batches run everything on the context stream (one launch per batch)
+    hipStream_t sst = pipe ? ctx->stream : ctx->setup_stream, st = ctx->stream;
     if (ws.used) HIP_TRY(ctx, hipEventSynchronize(ws.setup_done));
     *ws.h_ov = 0u;   // the slot's previous setup (the only other writer) is done
 
@@ -262,6 +312,7 @@ static int enqueue_frame(shs_ctx *ctx) {
 
     // ---- setup_stream: wait for the slot's last k_raster, reset, upload, set up ----
     if (ws.used) HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.raster_done, 0));
+    if (pipe && ws.used) HIP_TRY(ctx, hipStreamWaitEvent(sst, ws.setup_done, 0));   // (a non-pipelined setup)
     if (reset) {
         HIP_TRY(ctx, hipMemsetAsync(ws.busy.p, 0, ws.busy.cap * sizeof(uint32_t), sst));
         ctx->geom_key[slot] = gkey;
@@ -324,7 +375,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.zero_set = (uint32_t)((ctx->frame_index + 1) % shs_dev::N_CSETS);   // previous batch's k_setup)
     if (++ctx->busy_epoch == 0u) ctx->busy_epoch = 1u;   // busy[] is zeroed on reset; 0 is never an epoch
     fp.epoch = ctx->busy_epoch;
-    fp.scan_mode = (ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS)) ? 1u : 0u;
+    fp.scan_mode = scan ? 1u : 0u;
     if (!fp.scan_mode) HIP_TRY(ctx, hipMemsetAsync(ws.tile_count.p, 0, n_bt_all * sizeof(uint32_t), sst));
     // SHS_LEGACY_NORECS=1: binned frames keep no per-triangle records, k_raster recomputes them from the
     // resident mesh (RF_NO_RECS).  Off by default: measured C3 0.670 -> 0.699 ms per 16-frame step (the
@@ -344,7 +395,6 @@ static int enqueue_frame(shs_ctx *ctx) {
     // batches keep the ghost waves inside k_setup: one launch fewer on the latency path between two
     // batches (C2: 0.282-0.285 vs 0.288-0.297 ms per 64-frame step).  SHS_GHOST_LIST=1 lists them in
     // scan mode too (timing experiments).
-    static const bool ghost_list_env = std::getenv("SHS_GHOST_LIST") && std::atoi(std::getenv("SHS_GHOST_LIST")) != 0;
     fp.ghost_list = (fp.scan_mode && !ghost_list_env) ? 0u : 1u;
     fp.ghost_blocks = fp.ghost_list ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
     fp.clear_blocks = 0;
@@ -387,15 +437,30 @@ static int enqueue_frame(shs_ctx *ctx) {
     fb.ov_host = const_cast<uint32_t *>(ws.h_ov);
 
     hipEvent_t *ev = nullptr;
-    if (ctx->timing) {
-        const int k = ctx->ring_next;
-        ctx->ring_next = (k + 1) % shs_ctx::RING;
-        if (harvest_slot(ctx, k)) return SHS_ERR_HIP;
-        if (!ctx->ring_ev[k][0])
-            for (int i = 0; i < 5; ++i) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ring_ev[k][i], hipEventDisableSystemFence));
-        ev = ctx->ring_ev[k];
-        ctx->ring_pending[k] = true;
-    }
+    if (ring_take(ctx, true, ev)) return SHS_ERR_HIP;
+    if (pipe) {
+        // one launch: the pending batch's raster with this batch's setup (k_pipe), or this setup alone;
+        // this batch's raster is pending until the next batch or a flush.  Timing: the launch counts as
+        // this batch's "raster" (setup 0): the sums over a run are then the device time per batch.
+        if (ev) {
+            HIP_TRY(ctx, hipEventRecord(ev[0], st));
+            HIP_TRY(ctx, hipEventRecord(ev[1], st));
+            HIP_TRY(ctx, hipEventRecord(ev[3], st));
+        }
+        if (ctx->pend.on) {
+            HIP_TRY(ctx, shs_internal::launch_pipe(ctx->pend.fp, ctx->pend.fb, ctx->pend.grid, fp, fb, st));
+            HIP_TRY(ctx, hipEventRecord(ctx->lslot[ctx->pend.slot].raster_done, st));
+        } else {
+            HIP_TRY(ctx, shs_internal::launch_setup(fp, fb, ka, st));
+        }
+        if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));
+        HIP_TRY(ctx, hipEventRecord(ws.setup_done, st));
+        ctx->pend.on = true;
+        ctx->pend.fp = fp;
+        ctx->pend.fb = fb;
+        ctx->pend.grid = raster_grid;
+        ctx->pend.slot = slot;
+    } else {
     // kernel durations: [0]..[1] k_setup (+ k_ghost in ghost_list mode) on setup_stream,
     // [3]..[2] k_raster on stream
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[0], sst));
@@ -409,6 +474,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     HIP_TRY(ctx, shs_internal::launch_raster(fp, fb, ka, raster_grid, st));
     if (ev) HIP_TRY(ctx, hipEventRecord(ev[2], st));
     HIP_TRY(ctx, hipEventRecord(ws.raster_done, st));
+    }
     ws.used = true;
     ctx->last_parity = fp.parity;
     ctx->last_slot = slot;
@@ -434,6 +500,7 @@ static uint32_t next_pow2(uint32_t v) {
 
 // Wait for the frame and read its counters; if a capacity overflowed, grow it and re-issue the frame.
 static int finish_frame(shs_ctx *ctx) {
+    if (flush_pending(ctx)) return SHS_ERR_HIP;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // k_raster waited for its k_setup
     if (!ctx->need_check) return SHS_OK;
     for (int attempt = 0; attempt < 6; ++attempt) {
@@ -477,6 +544,7 @@ static int finish_frame(shs_ctx *ctx) {
         }
         int rc = enqueue_frame(ctx);
         if (rc) return rc;
+        if (flush_pending(ctx)) return SHS_ERR_HIP;
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     if (ctx->h_counters[shs_dev::C_OVERFLOW]) { ctx->err = "capacity overflow persisted"; return SHS_ERR_OVERFLOW; }
@@ -488,6 +556,7 @@ static int finish_frame(shs_ctx *ctx) {
 }  // extern "C"
 
 int shs_legacy_ensure_final(shs_ctx *ctx) {
+    if (flush_pending(ctx)) return SHS_ERR_HIP;
     if (!ctx->have_frame || !ctx->need_check) return SHS_OK;
     const shs_ctx::LegacySlot &p = ctx->lslot[ctx->last_slot];
     HIP_TRY(ctx, hipEventSynchronize(p.setup_done));
@@ -529,7 +598,10 @@ int shs_render_legacy_batch(shs_ctx *ctx, const shs_frame_desc *frame, const shs
     // consumer of its frames (a copy queued behind it) must not see a batch that overflowed a
     // capacity.  Its overflow word is final once its setup is (long before its raster ends); if it is
     // set, the batch is finished -- re-issued with grown capacities -- before this one is enqueued.
-    {
+    // (A pending pipelined batch is superseded without the check: its raster still runs -- in this
+    // batch's launch or at the flush enqueue_frame does -- but its frames are overwritten by this batch
+    // before any call can read them.)
+    if (!ctx->pend.on) {
         const int rc = shs_legacy_ensure_final(ctx);
         if (rc) return rc;
     }
@@ -733,6 +805,15 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
         if (value < 0 || value > 1000) return SHS_ERR_INVALID;
         ctx->shard_root_permille = (int)value;
         ctx->reg_next_fresh = false;
+        return SHS_OK;
+    }
+    if (option == SHS_OPT_LEGACY_PIPELINE) {
+        if (value < 0 || value > 1) return SHS_ERR_INVALID;
+        if (value == 0) {
+            if (set_dev(ctx)) return SHS_ERR_HIP;
+            if (flush_pending(ctx)) return SHS_ERR_HIP;
+        }
+        ctx->legacy_pipeline = value != 0;
         return SHS_OK;
     }
     if (option == SHS_OPT_SHADOW_FOOTPRINT) {

@@ -126,9 +126,21 @@ struct shs_ctx {
     static constexpr int RING = 64;
     hipEvent_t ring_ev[RING][5] = {};
     bool ring_pending[RING] = {};
+    bool ring_counts[RING] = {};     // the entry is a batch's enqueue (a pipeline flush adds time, no batch)
     int ring_next = 0;
     double acc_ms[4] = {0, 0, 0, 0};
     int64_t acc_frames = 0;
+
+    // SHS_OPT_LEGACY_PIPELINE: batch k's raster runs inside batch k + 1's launch (k_pipe) or at the next
+    // flush (anything that reads the frames, a non-pipelined batch, a stream change); `pend` is that
+    // not yet launched raster.
+    bool legacy_pipeline = false;
+    struct PendingRaster {
+        bool on = false;
+        shs_dev::FrameParams fp;
+        shs_dev::FrameBuffers fb;
+        int grid = 0, slot = 0;
+    } pend;
 
     // ---- library path (shs_abi_lib.cpp): one workspace per pass ----
     struct LibWork {

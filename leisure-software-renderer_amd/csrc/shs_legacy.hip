@@ -740,20 +740,18 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     if (tid == 0) fb.blk_stat[frame * fp.setup_blocks + lb] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
 }
 
-template <bool KARG>
-__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
-    __shared__ GhostScratch s_ghost[4];
-    __shared__ uint32_t s_stat[4];
-    __shared__ NewBusy s_new;
+// One k_setup block b of the batch (setup or ghost role by its index in its frame); draw_tab = the
+// batch's draw table (kernel arguments or the device table).
+__device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuffers &fb_all, const DrawGPU *draw_tab, int b,
+                                           GhostScratch (&s_ghost)[4], uint32_t (&s_stat)[4], NewBusy &s_new) {
     uint32_t *cnt = fb_all.counters + fp.parity * CSET;
-    const int b = (int)blockIdx.x;
     if (b == 0)   // the next batch's counter set (its previous user, batch k - 2, has finished)
         for (int i = (int)threadIdx.x; i < CSET; i += 256) fb_all.counters[(size_t)fp.zero_set * CSET + i] = 0u;
     // frame of the batch and the block's role inside it
     const int frame = b / fp.frame_blocks, lb = b - frame * fp.frame_blocks;
     const FrameBuffers fb = frame_view(fp, fb_all, frame);
     const int dbase = frame * fp.n_draws;
-    const DrawGPU *draws = draw_table<KARG>(fb_all, ka) + dbase;
+    const DrawGPU *draws = draw_tab + dbase;
     const uint64_t t_start = fb.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     // (the counter set and the bin counts were zeroed on the setup stream before this launch)
@@ -775,6 +773,14 @@ __global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_a
             fb.timeline[TL_STRIDE * b + 11] = __builtin_amdgcn_s_memtime();
         }
     }
+}
+
+template <bool KARG>
+__global__ __launch_bounds__(256) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
+    __shared__ GhostScratch s_ghost[4];
+    __shared__ uint32_t s_stat[4];
+    __shared__ NewBusy s_new;
+    setup_item(fp, fb_all, draw_table<KARG>(fb_all, ka), (int)blockIdx.x, s_ghost, s_stat, s_new);
 }
 
 // ---- k_ghost (ghost_list mode) -----------------------------------------------------------------
@@ -1513,6 +1519,74 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
     }
 }
 
+// Pipelined batches (SHS_OPT_LEGACY_PIPELINE, shs_abi.cpp): ONE persistent launch renders batch k - 1's
+// raster (fpR / fbR: its busy tiles and clear strips, exactly k_raster's items) and runs batch k's setup
+// (fpS / fbS: exactly k_setup's blocks).  Nothing in the launch waits on anything else in it: batch
+// k - 1's setup finished in the previous launch, and batch k's raster runs in the next.  The setup
+// blocks are dealt among the raster items in proportion (item i is a setup block when the count of
+// setup blocks among items < i + 1 grows), so they fill the raster's latency gaps and its tail instead
+// of running as a kernel of their own between two rasters (the cross-queue hop and the wait for CUs
+// of the two-stream pipeline).  Scan-mode batches with a device draw table only
+// (no k_ghost, no kernel-argument draws).
+__global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_pipe(FrameParams fp, FrameBuffers fb, FrameParams fpS,
+                                                                       FrameBuffers fbS) {
+    __shared__ RasterShared sh;
+    __shared__ GhostScratch s_ghost[4];
+    __shared__ uint32_t s_stat[4];
+    __shared__ NewBusy s_new;
+    const int tid = threadIdx.x;
+    uint32_t *cnt = fb.counters + fp.parity * CSET;
+    const DrawGPU *draws = fb.draws;
+    const int n_rt = fp.tiles_x * fp.rtiles_y;            // raster tiles per frame
+    if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
+    sh.key[tid] = KEY_EMPTY;
+    const uint32_t n_busy = min(cnt[C_BUSY], (uint32_t)(n_rt * fp.n_frames));
+    const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
+    const int n_draws_all = fp.n_draws * fp.n_frames;
+    const float4 du_first = tid < min(n_draws_all, LDS_DRAWS) * 4 ? reinterpret_cast<const float4 *>(draws[tid >> 2].light)[tid & 3]
+                                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    const uint2 pbx[CAND / 256] = {};   // (batches never prefetch boxes)
+    if (tid < min(n_draws_all, LDS_DRAWS) * 4) sh.du[tid] = du_first;
+    const int strips_y = (fp.rtiles_y + STRIP_RT - 1) / STRIP_RT;
+    const uint32_t n_strips = (uint32_t)(strips_y * fp.n_frames);
+    const uint64_t n_raster = (uint64_t)n_strips + n_busy;
+    const uint32_t n_setup = (uint32_t)fpS.setup_grid;
+    const uint64_t n_items = n_raster + n_setup;
+    const uint32_t G = gridDim.x, q = blockIdx.x % (uint32_t)N_WORKQ;
+    uint32_t *queue = &cnt[C_WORK + WORKQ_STRIDE * q];
+    const bool queued = (uint64_t)G + q < n_items;
+    uint32_t item = blockIdx.x, ticket = 0u;
+    while ((uint64_t)item < n_items) {
+        if (tid == 0 && queued) ticket = atomicAdd(queue, 1u);   // the next item, in flight meanwhile
+        const uint32_t k_lo = (uint32_t)(((uint64_t)item * n_setup) / n_items);
+        const uint32_t k_hi = (uint32_t)(((uint64_t)(item + 1) * n_setup) / n_items);
+        if (k_hi > k_lo) {
+            setup_item(fpS, fbS, fbS.draws, (int)k_lo, s_ghost, s_stat, s_new);
+        } else {
+            const uint32_t j = item - k_lo;                   // raster item j of n_raster (k_raster's order)
+            const uint32_t s_lo = (uint32_t)(((uint64_t)j * n_strips) / n_raster);
+            const uint32_t s_hi = (uint32_t)(((uint64_t)(j + 1) * n_strips) / n_raster);
+            if (s_hi > s_lo) {
+                const int f = (int)(s_lo / (uint32_t)strips_y);
+                const int sy = (int)s_lo - f * strips_y;
+                for (int ry = sy * STRIP_RT; ry < min((sy + 1) * STRIP_RT, fp.rtiles_y); ++ry) clear_strip(fp, fb, f, ry);
+            } else {
+                const uint32_t g = fb.busy_list[j - s_lo];
+                const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
+                const FrameBuffers fv = frame_view(fp, fb, f);
+                raster_tile<false>(fp, fv, draws, cnt, n_frag, f, rt, pbx, false, sh, nullptr);
+            }
+        }
+        if (!queued) break;
+        __syncthreads();   // every thread is done with sh.item of the previous round
+        if (tid == 0) sh.item = G + q + (uint32_t)N_WORKQ * ticket;
+        __syncthreads();
+        item = sh.item;
+    }
+    __syncthreads();
+    if (tid == 0) fb.rstat[blockIdx.x] = make_uint2(sh.cov, sh.maxbin);
+}
+
 }  // namespace shs_dev
 
 // ---- launch wrappers (called by shs_abi.cpp) -----------------------------------------------
@@ -1530,6 +1604,12 @@ hipError_t launch_setup(const FrameParams &fp, const FrameBuffers &fb, const KAr
 
 hipError_t launch_ghost(const FrameParams &fp, const FrameBuffers &fb, hipStream_t s) {
     hipLaunchKernelGGL(k_ghost, dim3(GHOST_LIST_BLOCKS), dim3(256), 0, s, fp, fb);
+    return hipGetLastError();
+}
+
+hipError_t launch_pipe(const FrameParams &fpR, const FrameBuffers &fbR, int grid, const FrameParams &fpS, const FrameBuffers &fbS,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(k_pipe, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, fpR, fbR, fpS, fbS);
     return hipGetLastError();
 }
 

@@ -569,6 +569,11 @@ class Context:
         """SHS_OPT_SHARD_ROOT_SHARE: rank 0's share of a region layout relative to the others (0..1)."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_SHARD_ROOT_SHARE, int(round(share * 1000))))
 
+    def set_legacy_pipeline(self, on: bool):
+        """SHS_OPT_LEGACY_PIPELINE: a multi-draw scan-mode batch's raster runs in the next batch's launch
+        (or at the next call that reads frames); results identical, frames final only after such a call."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_LEGACY_PIPELINE, 1 if on else 0))
+
     def set_shadow_footprint(self, on: bool):
         """SHS_OPT_SHADOW_FOOTPRINT: shadow passes are recorded and rendered by the next camera pass over
         only the shadow-map tiles its pixels' PCF can read (default off: the whole map when called)."""

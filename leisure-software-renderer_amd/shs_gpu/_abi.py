@@ -37,6 +37,7 @@ SHARD_INTERLEAVED = 0
 SHARD_REGIONS = 1
 OPT_SHARD_ROOT_SHARE = 10
 OPT_SHADOW_FOOTPRINT = 11
+OPT_LEGACY_PIPELINE = 12
 
 
 class LegacyDraw(ctypes.Structure):

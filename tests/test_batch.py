@@ -171,3 +171,40 @@ def test_batch_validation(gpu_ctx):
         gpu_ctx.resolve_frame(2)
     c, z = gpu_ctx.resolve_frame(1)
     assert (z < FLT_MAX).sum() > 0
+
+
+def test_legacy_pipeline_matches_unpipelined():
+    """SHS_OPT_LEGACY_PIPELINE (k_pipe: batch k's raster in batch k + 1's launch, the last one at the
+    flush): a sequence of C2-sized batches -- consecutive batches, a resolve between two of them (a
+    flush), a frame-size change (the framebuffers grow: the pending raster is flushed first), a
+    single-frame render in between (not pipelined) -- resolves to byte-identical frames, and the
+    statistics of the last batch agree."""
+    import shs_gpu
+    import bench
+    frame, sets = bench.batch_poses("c2", 16)
+    small, ssets = bench.batch_poses("c1", 16)
+    ref, pip = shs_gpu.Context(0), shs_gpu.Context(0)
+    try:
+        pip.set_legacy_pipeline(True)
+        plan = [(frame, sets[0]), (frame, sets[1]), "resolve", (frame, sets[2]), (frame, sets[3]), (small, ssets[0]),
+                "resolve", (small, ssets[1]), ("single", sets[0][3]), (frame, sets[1]), (frame, sets[2])]
+        for step in plan:
+            if step == "resolve":
+                for k in (0, 7, 15):
+                    a, b = ref.resolve_frame(k), pip.resolve_frame(k)
+                    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)), k
+                continue
+            if step[0] == "single":
+                ref.render(frame, step[1])
+                pip.render(frame, step[1])
+                continue
+            fr, fds = step
+            ref.render_batch_prepared(ref.prepare_batch(fr, fds))
+            pip.render_batch_prepared(pip.prepare_batch(fr, fds))
+        for k in range(16):
+            a, b = ref.resolve_frame(k), pip.resolve_frame(k)
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)), k
+        assert ref.stats() == pip.stats()
+    finally:
+        ref.close()
+        pip.close()
