@@ -629,9 +629,10 @@ def main():
                     help="c4/c5 at N > 1: tile ownership (one cost-balanced rectangle per rank, or tile %% N)")
     ap.add_argument("--root-share", type=float, default=0.85,
                     help="c4/c5 regions: rank 0's share of the predicted cost (it also unpacks the gather)")
-    ap.add_argument("--pipeline", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--pipeline", type=int, default=0, choices=[0, 1],
                     help="legacy configs: SHS_OPT_LEGACY_PIPELINE for the timed batches (each batch's raster in the "
-                         "next batch's launch; eligible: multi-draw scan-mode batches, i.e. C1 / C2)")
+                         "next batch's launch; eligible: multi-draw scan-mode batches, i.e. C1 / C2).  Off: measured "
+                         "slower (C2 0.328 vs 0.284 ms/step: the fused kernel spills 120 B/lane, DESIGN.md 4)")
     ap.add_argument("--ramp-ms", type=float, default=60.0,
                     help="legacy configs: untimed rendering before the warm-up so the GPU clocks reach steady state")
     ap.add_argument("--shadow-full", action="store_true",

@@ -29,7 +29,6 @@ def test_c2_bench_batch_every_frame_vs_oracle(oracle_mod, pose_set):
     assert (frame.width, frame.height) == (1920, 1080) and len(fds) == 64
     ctx = shs_gpu.Context(0)
     try:
-        ctx.set_legacy_pipeline(True)                                      # the bench's pipelined batches
         ctx.render_batch_prepared(ctx.prepare_batch(frame, fds))          # the bench's flags
         plain = [ctx.resolve_frame(k) for k in range(64)]
         pframe = dataclasses.replace(frame, prequant=True)
