@@ -30,6 +30,8 @@ def make_ctx(cfg):
         extra = cull
     else:
         frame, draws, casters, sun, S = scene_lib.c5_scene(3840, 2160, 2048)
+        # SPLIT_FOOTPRINT (default 1, bench.py's C5): the shadow pass over the camera pass's PCF footprint
+        ctx.set_shadow_footprint(os.environ.get("SPLIT_FOOTPRINT", "1") == "1")
         lvp = ctx.render_shadow_map(S, sun, casters)
         scene_lib.wire_shadow(draws, lvp)
         extra = (casters, sun, S)

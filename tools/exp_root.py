@@ -28,6 +28,8 @@ def make(cfg, share):
         extra = cull
     else:
         frame, draws, casters, sun, S = scene_lib.c5_scene(3840, 2160, 2048)
+        # SPLIT_FOOTPRINT (default 1, bench.py's C5): the shadow pass over the camera pass's PCF footprint
+        ctx.set_shadow_footprint(os.environ.get("SPLIT_FOOTPRINT", "1") == "1")
         lvp = ctx.render_shadow_map(S, sun, casters)
         scene_lib.wire_shadow(draws, lvp)
         extra = (casters, sun, S)
@@ -75,6 +77,7 @@ def main():
         if r > 0:   # this rank's packed present tiles, for rank 0's unpacks
             ctx = pool[0][0]
             b = torch.zeros(max(ctx.tiles_rank_words(T, r, N), 1), dtype=torch.int32, device="cuda:0")
+            torch.cuda.synchronize()   # torch's fill (its own stream) before the pack
             ctx.tiles_pack(T, r, N, b.data_ptr())
             ctx.synchronize_lib()
             packed[r] = b
