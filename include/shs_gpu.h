@@ -462,6 +462,9 @@ int shs_tiles_rank_words(shs_ctx *ctx, int target, int32_t shard_rank, int32_t s
  * so the packed tiles are final without a host wait for the render. */
 int shs_tiles_pack(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, void *dst_dev);
 int shs_tiles_unpack(shs_ctx *ctx, int target, int32_t shard_rank, int32_t shard_count, const void *src_dev);
+/* shs_tiles_unpack of several ranks' packed buffers in one launch (rank 0's side of the gather):
+ * src_dev[r] = rank r's packed buffer, or NULL to skip rank r (rank 0 itself, empty ranks). */
+int shs_tiles_unpack_ranks(shs_ctx *ctx, int target, int32_t count, const void *const *src_dev);
 
 /* Host GLM restatements for non-C++ callers (camera/convention.hpp; pass_pbr_forward.hpp:136-141). */
 int shs_look_at_lh(const float eye[3], const float center[3], const float up[3], float out16[16]);

@@ -1259,6 +1259,33 @@ int shs_tiles_unpack(shs_ctx *ctx, int target, int32_t rank, int32_t count, cons
     return SHS_OK;
 }
 
+int shs_tiles_unpack_ranks(shs_ctx *ctx, int target, int32_t count, const void *const *src_dev) {
+    if (!ctx || !src_dev || count <= 0) return SHS_ERR_INVALID;
+    if (set_dev(ctx)) return SHS_ERR_HIP;
+    shs_dev::TileUnpackMulti m;
+    std::memset(&m, 0, sizeof m);
+    for (int32_t r = 0; r < count; ++r) {
+        if (!src_dev[r]) continue;
+        shs_dev::TileCopyParams p;
+        if (tile_params(ctx, target, r, count, p)) return SHS_ERR_INVALID;
+        const int n_tiles = ((p.W + shs_dev::TILE - 1) / shs_dev::TILE) * ((p.H + shs_dev::TILE - 1) / shs_dev::TILE);
+        const int owned = shs_dev::shard_n_owned(p.rank, p.count, p.reg, n_tiles);
+        if (owned <= 0) continue;
+        if (m.n == shs_dev::UNPACK_PEERS) {   // a launch per UNPACK_PEERS peers
+            HIP_TRY(ctx, shs_internal::launch_tiles_unpack_multi(m, ctx->stream));
+            std::memset(&m, 0, sizeof m);
+        }
+        m.p = p;
+        m.rank[m.n] = r;
+        m.reg[m.n] = p.reg;
+        m.src[m.n] = static_cast<const uint32_t *>(src_dev[r]);
+        m.first[m.n + 1] = m.first[m.n] + owned;
+        ++m.n;
+    }
+    HIP_TRY(ctx, shs_internal::launch_tiles_unpack_multi(m, ctx->stream));
+    return SHS_OK;
+}
+
 int shs_lib_timing_reset(shs_ctx *ctx) {
     if (!ctx) return SHS_ERR_INVALID;
     if (set_dev(ctx)) return SHS_ERR_HIP;

@@ -12,9 +12,9 @@
 
 namespace shs_dev {
 
+// Owned tile i of p's rank: its pixels <-> the i-th 32x32-padded block of `packed`.
 template <bool PACK>
-__global__ __launch_bounds__(256) void k_tiles_copy(TileCopyParams p, uint32_t *packed) {
-    const int i = (int)blockIdx.x;
+__device__ __forceinline__ void tile_copy(const TileCopyParams &p, int i, uint32_t *packed) {
     const int tiles_x = (p.W + TILE - 1) / TILE;
     const int t = shard_tile(p.rank, p.count, p.reg, i, tiles_x);
     const int x0 = (t % tiles_x) * TILE, y0 = (t / tiles_x) * TILE;
@@ -42,6 +42,23 @@ __global__ __launch_bounds__(256) void k_tiles_copy(TileCopyParams p, uint32_t *
     }
 }
 
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_tiles_copy(TileCopyParams p, uint32_t *packed) {
+    tile_copy<PACK>(p, (int)blockIdx.x, packed);
+}
+
+// Rank 0's unpack of several peers' packed tiles in one launch (the gather's receive side): block b is
+// owned tile b - first[k] of peer k (ranks rank[k], buffers src[k]; a uniform search over <= 16 peers).
+__global__ __launch_bounds__(256) void k_tiles_unpack_multi(TileUnpackMulti m) {
+    const int b = (int)blockIdx.x;
+    int k = 0;
+    while (k + 1 < m.n && m.first[k + 1] <= b) ++k;
+    TileCopyParams p = m.p;
+    p.rank = m.rank[k];
+    p.reg = m.reg[k];
+    tile_copy<false>(p, b - m.first[k], const_cast<uint32_t *>(m.src[k]));
+}
+
 }  // namespace shs_dev
 
 namespace shs_internal {
@@ -53,6 +70,12 @@ hipError_t launch_tiles_copy(const TileCopyParams &p, bool pack, void *packed, h
     if (n_owned <= 0) return hipSuccess;
     if (pack) hipLaunchKernelGGL(k_tiles_copy<true>, dim3(n_owned), dim3(256), 0, s, p, static_cast<uint32_t *>(packed));
     else hipLaunchKernelGGL(k_tiles_copy<false>, dim3(n_owned), dim3(256), 0, s, p, static_cast<uint32_t *>(packed));
+    return hipGetLastError();
+}
+
+hipError_t launch_tiles_unpack_multi(const TileUnpackMulti &m, hipStream_t s) {
+    if (m.n <= 0 || m.first[m.n] <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tiles_unpack_multi, dim3(m.first[m.n]), dim3(256), 0, s, m);
     return hipGetLastError();
 }
 

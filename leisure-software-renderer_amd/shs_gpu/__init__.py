@@ -715,6 +715,12 @@ class Context:
     def tiles_unpack(self, target, rank, count, src_ptr):
         self._check(self._lib.shs_tiles_unpack(self._h, target, rank, count, ctypes.c_void_p(src_ptr)))
 
+    def tiles_unpack_ranks(self, target, count, src_ptrs):
+        """shs_tiles_unpack_ranks: every rank's packed device buffer (src_ptrs[r]; 0 / None skips rank r)
+        unpacked into this context's frame by one launch."""
+        arr = (ctypes.c_void_p * count)(*[int(p) if p else None for p in src_ptrs])
+        self._check(self._lib.shs_tiles_unpack_ranks(self._h, int(target), int(count), arr))
+
     def upload_lights(self, lights):
         """lights: numpy LIGHT_DTYPE array (CullingLightGPU records)."""
         from ._abi import CullingLightC

@@ -288,6 +288,7 @@ SIGNATURES = [
                                                ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     ("shs_tiles_pack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
     ("shs_tiles_unpack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, _P]),
+    ("shs_tiles_unpack_ranks", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     ("shs_lights_upload", ctypes.c_int, [_P, ctypes.POINTER(CullingLightC), ctypes.c_int32]),
     ("shs_light_cull", ctypes.c_int, [_P, ctypes.POINTER(LightCullDescC)]),
     ("shs_light_bin_culling", ctypes.c_int, [_P, ctypes.POINTER(LightBinDescC), _P, ctypes.c_int32, _P, _P, _P]),

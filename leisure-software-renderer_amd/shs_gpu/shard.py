@@ -160,10 +160,9 @@ def gather_frame_device(dist, ctx, target, stream=None, out=None):
         buf = out[0]
         ctx.tiles_pack(target, rank, count, buf.data_ptr())
         send_to_root(dist, buf, out[1:], sizes)
-        if rank == 0:
-            for r in range(1, count):
-                if sizes[r] > 0:
-                    ctx.tiles_unpack(target, r, count, out[1 + r].data_ptr())
+        if rank == 0:   # every peer's tiles by one launch
+            ctx.tiles_unpack_ranks(target, count, [0] + [out[1 + r].data_ptr() if sizes[r] > 0 else 0
+                                                          for r in range(1, count)])
     return out
 
 

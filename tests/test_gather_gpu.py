@@ -244,3 +244,39 @@ def test_gather_frame_device_reuses_buffers():
     finally:
         for c in [root, full] + peers:
             c.close()
+
+
+@pytest.mark.parametrize("count", [3, 20])
+def test_unpack_ranks_equals_per_rank_unpacks(count):
+    """shs_tiles_unpack_ranks (rank 0's side of the gather in one launch; more than 16 peers take a
+    launch per 16): the composed frame equals the one shs_tiles_unpack builds rank by rank."""
+    import torch
+    import shs_gpu
+    from shs_gpu import scene_lib
+    frame, draws, _, _, _ = scene_lib.c5_scene(400, 260)
+    ctxs = [shs_gpu.Context(0) for _ in range(3)]   # peer renderer, per-rank composer, one-launch composer
+    try:
+        peer, one, many = ctxs
+        bufs = [None] * count
+        for r in range(count):
+            frame.shard_rank, frame.shard_count = r, count
+            peer.render_pbr_forward(frame, draws)
+            if r == 0:
+                continue
+            b = torch.zeros(max(peer.tiles_packed_words(peer.TARGET_LIB, count), 1), dtype=torch.int32, device="cuda:0")
+            torch.cuda.synchronize()   # torch's fill runs on its own stream: done before the pack
+            peer.tiles_pack(peer.TARGET_LIB, r, count, b.data_ptr())
+            peer.synchronize_lib()
+            bufs[r] = b
+        frame.shard_rank, frame.shard_count = 0, count
+        for c in (one, many):
+            c.render_pbr_forward(frame, draws)
+        for r in range(1, count):
+            one.tiles_unpack(one.TARGET_LIB, r, count, bufs[r].data_ptr())
+        many.tiles_unpack_ranks(many.TARGET_LIB, count, [0] + [bufs[r].data_ptr() for r in range(1, count)])
+        for a, b in zip(one.resolve_lib(), many.resolve_lib()):
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    finally:
+        frame.shard_rank, frame.shard_count = 0, 1
+        for c in ctxs:
+            c.close()

@@ -92,8 +92,7 @@ def main():
 
         def with_unpack(f=f, ctx=ctx):
             f()
-            for r in range(1, N):
-                ctx.tiles_unpack(T, r, N, packed[r].data_ptr())
+            ctx.tiles_unpack_ranks(T, N, [0] + [packed[r].data_ptr() for r in range(1, N)])
         ones.append(with_unpack)
     for i in range(3 * D):
         ones[i % D]()
