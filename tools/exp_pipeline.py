@@ -47,7 +47,7 @@ def main():
     pool = [make_ctx(cfg) for _ in range(max(depths))]
     for N in ns:
         for D in depths:
-            per_rank, host_ms = [], []
+            per_rank, host_ms, sh_regs = [], [], []
             only = os.environ.get("SPLIT_ONLY")
             for r in ([int(only)] if only is not None and N > 1 else range(N)):
                 ones = []
@@ -78,11 +78,15 @@ def main():
                     ctx.synchronize_lib()
                 per_rank.append((time.perf_counter() - t0) / nf * 1e3)
                 host_ms.append(host / nf * 1e3)
+                if cfg == "c5" and N > 1:
+                    sh_regs.append(tuple(pool[0][0].shadow_region()))
             ms = np.array(per_rank)
             print(f"{cfg} N={N} frames in flight {D}: per-rank ms/frame max {ms.max():.4f} mean {ms.mean():.4f}"
                   f" | " + " ".join(f"{x:.4f}" for x in ms) + f" | host enqueue ms/frame {np.mean(host_ms):.4f}", flush=True)
             if N > 1 and os.environ.get("SPLIT_REGIONS") == "1":
                 print(f"   regions {pool[0][0].shard_regions(N)}", flush=True)
+            if sh_regs:
+                print(f"   shadow-map tiles per rank {sh_regs}", flush=True)
     for ctx, *_ in pool:
         ctx.close()
 
