@@ -143,8 +143,11 @@ def main():
     print("regions", regs)
     for r, (x0, y0, x1, y1) in enumerate(regs):
         s = (slice(y0, y1 + 1), slice(x0, x1 + 1))
+        # setup blocks the rank runs: bounds meeting its rectangle, or unbounded (never skipped)
+        hit = (rects[:, 5] == 0) | ((rects[:, 0] <= x1) & (rects[:, 1] >= x0) & (rects[:, 2] <= y1) & (rects[:, 3] >= y0)
+                                    & (rects[:, 0] <= rects[:, 1]))
         print(f"rank {r}: px {px[s].sum() / 1e6:7.3f}M covered px {covpx[s].sum() / 1e6:7.3f}M tri {tri[s].sum() / 1e3:8.1f}K "
-              f"cov {cov[s].sum() / 1e6:8.2f}M")
+              f"cov {cov[s].sum() / 1e6:8.2f}M setup blocks {int(hit.sum())}")
 
 
 if __name__ == "__main__":
