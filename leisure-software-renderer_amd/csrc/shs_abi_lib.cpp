@@ -618,7 +618,7 @@ void shs_lib_release(shs_ctx *ctx) {
         if (t.texels) (void)hipFree(t.texels);
     ctx->textures.clear();
     release(ctx->srgb_lut);
-    release(ctx->lib_hdr); release(ctx->lib_keys); release(ctx->lib_blkcov); release(ctx->tm_thr_dev); ctx->tm_thr_dev_gamma = -1.0f; release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
+    release(ctx->lib_hdr); release(ctx->lib_keys); release(ctx->lib_blkcov); ctx->blkcov_zero_at = nullptr; release(ctx->tm_thr_dev); ctx->tm_thr_dev_gamma = -1.0f; release(ctx->lib_depth); release(ctx->lib_motion); release(ctx->shadow_map);
     release(ctx->lights); release(ctx->depth_ranges);
     release(ctx->list_counts); release(ctx->list_indices); release(ctx->lib_timeline); release(ctx->lib_stimeline);
     release(ctx->lib_ldr); release(ctx->lib_present); release(ctx->lib_mb); release(ctx->lib_mb_present);
@@ -892,6 +892,17 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     if (ensure(ctx, ctx->lib_hdr, npx) || ensure(ctx, ctx->lib_keys, npx)) return SHS_ERR_HIP;
     const size_t n_blk = (size_t)((f.width + 31) / 32) * ((f.height + 7) / 8) * 4;   // 16x4 blocks
     if (ensure(ctx, ctx->lib_blkcov, n_blk)) return SHS_ERR_HIP;
+    {   // the block flags start at zero (then every resolve leaves them so); rare: a sync memset
+        const uint64_t bk = (uint64_t)(uint32_t)f.width | ((uint64_t)(uint32_t)f.height << 32);
+        if (ctx->blkcov_zero_at != ctx->lib_blkcov.p || ctx->blkcov_zero_cap != ctx->lib_blkcov.cap || ctx->blkcov_zero_key != bk) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->setup_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
+            HIP_TRY(ctx, hipMemset(ctx->lib_blkcov.p, 0, ctx->lib_blkcov.cap * sizeof(uint32_t)));
+            ctx->blkcov_zero_at = ctx->lib_blkcov.p;
+            ctx->blkcov_zero_cap = ctx->lib_blkcov.cap;
+            ctx->blkcov_zero_key = bk;
+        }
+    }
     const bool dm = (f.flags & SHS_LIB_DEPTH_MOTION) != 0;
     if (dm && (ensure(ctx, ctx->lib_depth, npx) || ensure(ctx, ctx->lib_motion, npx))) return SHS_ERR_HIP;
 

@@ -223,6 +223,11 @@ struct shs_ctx {
     DevBuf<float4> lib_hdr;
     DevBuf<unsigned long long> lib_keys;  // camera pass winner keys (k_lib_raster -> k_lib_resolve)
     DevBuf<uint32_t> lib_blkcov;          // ... and per 16x4 block whether it holds any
+    // lib_blkcov is all zero between camera passes (k_lib_resolve resets the flags it read; the raster sets
+    // only its busy tiles'): zeroed once per allocation and frame size
+    const uint32_t *blkcov_zero_at = nullptr;
+    size_t blkcov_zero_cap = 0;
+    uint64_t blkcov_zero_key = 0;
     int lib_resolve_resident[3] = {0, 0, 0};   // resident k_lib_resolve workgroups (Forward+, PBR, mixed)
     DevBuf<float> srgb_lut;               // srgb_to_linear_rgb table (texture sampling)
     DevBuf<float> lib_depth;

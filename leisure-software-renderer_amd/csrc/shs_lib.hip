@@ -1630,6 +1630,7 @@ __device__ __forceinline__ float4 bg_color(const LibFrameParams &fp, int y) {
 }
 
 constexpr int LIB_PAIR_WORDS = LIB_CHUNK * LIB_RTW * LIB_RTH / 64;   // pair-start bitmap words
+constexpr int LIB_MAX_STATIC = 256;                                  // static work items per raster workgroup
 
 template <int LIB_CAND>
 struct LibShared {
@@ -1644,15 +1645,14 @@ struct LibShared {
     uint32_t lid[LIB_CAND];               //   slots
     uint32_t lkey[LIB_CAND];              //   and depth bounds (lib_zmin_ord; 0 without a depth test)
     uint32_t sel[LIB_CHUNK];              // list positions staged by the current pass
-    union alignas(16) {   // span rows are read 8 at a time (ds_read_b128)
-        uint32_t hist[256];               // depth buckets: counts, then first positions (the sort)
-        uint16_t span[LIB_CHUNK * LIB_RTH]; // staging passes: row spans of the staged boxes (x0 | x1 << 8, tile-relative)
-    };
+    uint32_t hist[256];                   // depth buckets: counts, then first positions (the sort)
     uint32_t zlo, zhi;
     uint32_t wtot[4][2];                  // per wave: surviving candidates, pairs
+    uint32_t wmax[4];                     // deep camera raster: per wave, the largest key z of its pixels after a pass
     uint32_t colmax[2][LIB_RTW];          // per pixel column: max key z (orderable bits) over its rows, by chunk parity
     uint32_t nc, nbusy, cov, maxbin, npairs;
     int next[3];                          // the workgroup's next run, queue, queues tried
+    uint32_t sitem[LIB_MAX_STATIC];       // the workgroup's static work items (k_lib_raster)
     uint64_t tl[LTL_STRIDE];              // SHS_OPT_TIMELINE accumulators (thread 0)
     // segment (deep) or staged box (shallow) owning each bitmap word's first pair
     typename std::conditional<LIB_CAND == LIB_CAND_DEEP, uint16_t, uint8_t>::type wown[LIB_PAIR_WORDS];
@@ -1762,9 +1762,9 @@ __device__ __forceinline__ void shade_px(const LibFrameParams &fp, const LibBuff
 // e = E (...) at E = 2^-18, 16x the bound: the slack absorbs this computation's own roundings (a few
 // ulps of |e| + |c|, divided by a), and 2^-12 px more covers the conversion to pixel indices.
 // Non-finite inputs keep the whole box row.
-__device__ __forceinline__ void lib_row_span(const float4 *rec, int py, int bx0, int bx1, int &x0, int &x1) {
+__device__ __forceinline__ void lib_row_span(const float4 r0, const float4 r1, int py, int bx0, int bx1, int &x0, int &x1) {
     x0 = bx0; x1 = bx1;
-    const float4 r0 = rec[0], r1 = rec[1];   // ax ay v0x v0y | v1x v1y inv_den z0
+    // r0, r1: the record's first two float4s, ax ay v0x v0y | v1x v1y inv_den z0
     const float ax = r0.x, ay = r0.y, v0x = r0.z, v0y = r0.w, v1x = r1.x, v1y = r1.y, id = r1.z;
     if (!(isfinite(ax) && isfinite(ay) && isfinite(v0x) && isfinite(v0y) && isfinite(v1x) && isfinite(v1y) && isfinite(id)))
         return;
@@ -1933,6 +1933,147 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         __syncthreads();
         if (tlon) { t_gather += tl_now() - t_g0; sh.tl[LTL_NCAND] += nc; }
 
+        if constexpr (LIB_CAND == LIB_CAND_DEEP && !SHADOW) {
+            // (3) deep camera raster: passes over LIB_CHUNK list positions, a pair of threads per position
+            //     (position c = tid / 2; half h = tid & 1 takes the tile rows 4h .. 4h + 3), three barriers
+            //     per pass.  A position is staged when its depth bound can still beat the key z of some
+            //     pixel of its box (hierarchical z against the keys themselves: exact, never drops a
+            //     possible winner); its pair of threads loads the record, solves its row spans in
+            //     registers and lays its segments out after one block prefix.  In a sorted list, once the
+            //     item's largest key z (a per-wave maximum read after the previous pass, stale only
+            //     upwards) sorts into a lower bucket than the next position's bound, the rest is skipped.
+            static_assert(2 * LIB_CHUNK == 256 && LIB_PAIR_WORDS == 512, "a thread pair per staged position");
+            const int c = tid >> 1, h = tid & 1;
+            const uint32_t *keyhi = reinterpret_cast<const uint32_t *>(sh.key);   // [2 * pixel + 1]: key z
+            uint32_t p = 0;
+            while (p < nc) {
+                __syncthreads();   // [A] the previous pass's pairs are resolved; its bits, segments, records free
+                const uint64_t t_a = tlon ? tl_now() : 0ull;
+                const bool first = chunk == chunk0;   // no key of the tile written yet
+                const uint32_t ordmax = first ? 0xffffffffu : max(max(sh.wmax[0], sh.wmax[1]), max(sh.wmax[2], sh.wmax[3]));
+                // (the list is front to back only when sorted; the per-position test below holds either way)
+                if (sorted && ordmax != 0xffffffffu && (ordmax < s_lo || bucket(ordmax) < bucket(sh.lkey[p]))) break;
+                ++chunk;
+                sh.bits[tid] = 0ull;
+                sh.bits[tid + 256] = 0ull;
+                const uint32_t q = p + (uint32_t)c;
+                bool alive = false;
+                int bx0 = 0, bx1 = -1, by0 = 0, by1 = -1;
+                uint32_t zk = 0u;
+                if (q < nc) {
+                    const uint2 b = sh.lbox[q];
+                    bx0 = max(lo16(b.x), X0); bx1 = min(hi16(b.x), X1);
+                    by0 = max(lo16(b.y), Y0); by1 = min(hi16(b.y), Y1);
+                    zk = sh.lkey[q];
+                    alive = bx0 <= bx1 && by0 <= by1;
+                    if (alive && hiz && !first) {
+                        if (zk > ordmax) {
+                            alive = false;
+                        } else if ((bx1 - bx0 + 1) * (by1 - by0 + 1) <= 16) {
+                            uint32_t mx = 0u;
+                            for (int y = by0; y <= by1; ++y)
+                                for (int x = bx0; x <= bx1; ++x) mx = max(mx, keyhi[2 * ((y - TY0) * LIB_RTW + (x - TX0)) + 1]);
+                            alive = zk <= mx;
+                        }
+                    }
+                }
+                // the record: half h loads and stages its two float4s; both need the first two (the spans)
+                float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
+                if (alive) {
+                    const float4 *src = reinterpret_cast<const float4 *>(&fb.recs[sh.lid[q]]) + 2 * h;
+                    ra = src[0];
+                    rb = src[1];
+                    sh.rec[c * 4 + 2 * h] = ra;
+                    sh.rec[c * 4 + 2 * h + 1] = rb;
+                    if (h == 0) sh.zord[c] = zk;
+                }
+                const float4 oa = make_float4(__shfl_xor(ra.x, 1), __shfl_xor(ra.y, 1), __shfl_xor(ra.z, 1), __shfl_xor(ra.w, 1));
+                const float4 ob = make_float4(__shfl_xor(rb.x, 1), __shfl_xor(rb.y, 1), __shfl_xor(rb.z, 1), __shfl_xor(rb.w, 1));
+                const float4 r0 = h ? oa : ra, r1 = h ? ob : rb;
+                // this half's four row spans (tile-relative x0 | x1 << 8; 0x1f: empty)
+                uint32_t spw[4];
+                uint32_t pk = 0u;   // pairs << 11 | segments
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int py = TY0 + 4 * h + k;
+                    int s0 = 1, s1 = 0;
+                    if (alive && py >= by0 && py <= by1) lib_row_span(r0, r1, py, bx0, bx1, s0, s1);
+                    spw[k] = s1 >= s0 ? (uint32_t)(s0 - TX0) | ((uint32_t)(s1 - TX0) << 8) : 0x1fu;
+                    if (s1 >= s0) pk += ((uint32_t)(s1 - s0 + 1) << 11) + 1u;
+                }
+                uint32_t incl = pk;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t vv = (uint32_t)__shfl_up((int)incl, o);
+                    if (lane >= o) incl += vv;
+                }
+                if (lane == 63) sh.wtot[wave][1] = incl;
+                __syncthreads();   // [B] every wave's total, the zeroed bits
+                const uint64_t t_b = tlon ? tl_now() : 0ull;
+                uint32_t pbase = 0, ptot = 0;
+#pragma unroll
+                for (int w2 = 0; w2 < 4; ++w2) {
+                    const uint32_t p2 = sh.wtot[w2][1];
+                    if (w2 < wave) pbase += p2;
+                    ptot += p2;
+                }
+                if (pk) {
+                    const uint32_t ex = pbase + incl - pk;
+                    uint32_t ps = ex >> 11, sg = ex & 2047u;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int s0 = (int)(spw[k] & 0xffu), s1 = (int)(spw[k] >> 8);
+                        if (s1 < s0) continue;
+                        const uint32_t wdt = (uint32_t)(s1 - s0 + 1);
+                        sh.seg[sg] = ps | ((uint32_t)s0 << 16) | ((uint32_t)(4 * h + k) << 21) | ((uint32_t)c << 24);
+                        atomicOr(&sh.bits[ps >> 6], 1ull << (ps & 63u));
+                        for (uint32_t wd = (ps + 63u) >> 6; wd * 64u < ps + wdt; ++wd) sh.wown[wd] = (uint16_t)sg;
+                        ps += wdt;
+                        ++sg;
+                    }
+                }
+                __syncthreads();   // [C] segments, starts and staged records complete
+                const int total = (int)(ptot >> 11);
+                if (tlon) {
+                    const uint64_t t_c = tl_now();
+                    sh.tl[LTL_NPAIRS] += (uint32_t)total;
+                    sh.tl[LTL_STAGE] += t_b - t_a;
+                    sh.tl[LTL_SEG] += t_c - t_b;
+                }
+                const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
+                for (int k0 = 64 * wave; k0 < total; k0 += 256) {
+                    const int k = k0 + lane;
+                    if (k >= total) continue;
+                    const unsigned long long wb = sh.bits[k0 >> 6];
+                    const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
+                    const uint32_t sgi = sh.seg[o];
+                    const int lx = (int)((sgi >> 16) & 31u) + (k - (int)(sgi & 0xffffu)), ly = (int)((sgi >> 21) & 7u);
+                    const int slot = (int)(sgi >> 24);
+                    const int kp = ly * LIB_RTW + lx;
+                    // per-pixel hierarchical z: the pixel's current key already beats the primitive's
+                    // depth bound (a stale, higher key only skips less)
+                    if (sh.zord[slot] > keyhi[2 * kp + 1]) continue;
+                    const LibRec r = lib_rec_from(&sh.rec[slot * 4]);
+                    float z01, u, v, w, idn;
+                    if (lib_test<SHADOW>(fp, r, TX0 + lx, TY0 + ly, z01, u, v, w, idn))
+                        atomicMin(&sh.key[kp], lib_key(fp, z01, r.seq, SHADOW));
+                }
+                // this wave's largest key z for the next pass (read under the other waves' atomics: stale
+                // only upwards, which selects more, never less); a part counts its own pixels only
+                {
+                    uint32_t o = keyhi[2 * tid + 1];
+                    if (parts > 1u) {
+                        const int cx = TX0 + (tid & (LIB_RTW - 1)), cy = TY0 + tid / LIB_RTW;
+                        if (cx < X0 || cx > X1 || cy < Y0 || cy > Y1) o = 0u;
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) o = max(o, (uint32_t)__shfl_xor((int)o, off));
+                    if (lane == 0) sh.wmax[wave] = o;
+                }
+                p += LIB_CHUNK;
+            }
+            continue;   // the next candidate round
+        }
         // (3) staging passes.  Each selects, in list order, the entries that can still win a pixel
         //     -- depth bound <= the largest current key z over the pixel columns their box covers
         //     (hierarchical z; 0xffffffff = an uncovered pixel) -- stages up to LIB_CHUNK of them and
@@ -2019,94 +2160,12 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 }
             }
             __syncthreads();
-            // Pair tasks.  Deep camera-pass raster (C4: many small primitives per tile): each staged
-            // box's rows narrowed to conservative spans (lib_row_span), the nonempty spans (segments)
-            // laid end to end (block prefix of (pairs, segments) per primitive).  Shallow raster and
-            // shadow pass (C5: few, mostly large primitives; the span arithmetic would spill the shallow
-            // raster's 80 registers, and measured 10 % slower on C5's shadow map): the boxes laid end to end.
-            // Every (primitive, pixel) pair is dealt to one lane, 64-pair windows round-robin over the
-            // waves (start bitmap + word owners, as in shs_legacy.hip).
-            if constexpr (LIB_CAND == LIB_CAND_DEEP && !SHADOW) {
-                // the spans, one (staged primitive, row) per thread and step
-                for (int i = tid; i < (int)m * LIB_RTH; i += 256) {
-                    const int c = i / LIB_RTH, py = TY0 + i % LIB_RTH;
-                    const uint2 b = sh.lbox[sh.sel[c]];
-                    const int x0 = max(lo16(b.x), X0), x1 = min(hi16(b.x), X1);
-                    const int y0 = max(lo16(b.y), Y0), y1 = min(hi16(b.y), Y1);
-                    int s0 = 1, s1 = 0;
-                    if (py >= y0 && py <= y1) lib_row_span(&sh.rec[c * 4], py, x0, x1, s0, s1);
-                    sh.span[i] = s1 >= s0 ? (uint16_t)((s0 - TX0) | ((s1 - TX0) << 8)) : (uint16_t)0x001fu;   // empty: 31 > 0
-                }
-                __syncthreads();
-                uint4 spv = make_uint4(0x001f001fu, 0x001f001fu, 0x001f001fu, 0x001f001fu);
-                uint32_t pk = 0u;   // pairs << 11 | segments
-                if (tid < (int)m) {
-                    sh.zord[tid] = sh.lkey[sh.sel[tid]];
-                    spv = reinterpret_cast<const uint4 *>(sh.span)[tid];
-#pragma unroll
-                    for (int r = 0; r < LIB_RTH; ++r) {
-                        const uint32_t wv = r < 2 ? spv.x : r < 4 ? spv.y : r < 6 ? spv.z : spv.w;
-                        const uint32_t e = (wv >> (16 * (r & 1))) & 0xffffu;
-                        const int s0 = (int)(e & 0xffu), s1 = (int)(e >> 8);
-                        if (s1 >= s0) pk += ((uint32_t)(s1 - s0 + 1) << 11) + 1u;
-                    }
-                }
-                uint32_t incl = pk;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t vv = (uint32_t)__shfl_up((int)incl, o);
-                    if (lane >= o) incl += vv;
-                }
-                if (lane == 63) sh.wtot[wave][1] = incl;
-                __syncthreads();
-                uint32_t pbase = 0, ptot = 0;
-#pragma unroll
-                for (int w2 = 0; w2 < 4; ++w2) {
-                    const uint32_t p2 = sh.wtot[w2][1];
-                    if (w2 < wave) pbase += p2;
-                    ptot += p2;
-                }
-                if (pk) {
-                    const uint32_t ex = pbase + incl - pk;
-                    uint32_t ps = ex >> 11, sg = ex & 2047u;
-#pragma unroll
-                    for (int r = 0; r < LIB_RTH; ++r) {
-                        const uint32_t wv = r < 2 ? spv.x : r < 4 ? spv.y : r < 6 ? spv.z : spv.w;
-                        const uint32_t e = (wv >> (16 * (r & 1))) & 0xffffu;
-                        const int s0 = (int)(e & 0xffu), s1 = (int)(e >> 8);
-                        if (s1 < s0) continue;
-                        const uint32_t wdt = (uint32_t)(s1 - s0 + 1);
-                        sh.seg[sg] = ps | ((uint32_t)s0 << 16) | ((uint32_t)r << 21) | ((uint32_t)tid << 24);
-                        atomicOr(&sh.bits[ps >> 6], 1ull << (ps & 63u));
-                        for (uint32_t wd = (ps + 63u) >> 6; wd * 64u < ps + wdt; ++wd) sh.wown[wd] = (uint16_t)sg;
-                        ps += wdt;
-                        ++sg;
-                    }
-                }
-                __syncthreads();
-                const int total = (int)(ptot >> 11);
-                if (tlon) sh.tl[LTL_NPAIRS] += (uint32_t)total;
-                const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
-                // one pair: its segment (word's first owner + starts up to it), pixel, then the test
-                auto pair = [&](int k0) {
-                    const int k = k0 + lane;
-                    if (k >= total) return;
-                    const unsigned long long wb = sh.bits[k0 >> 6];
-                    const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
-                    const uint32_t sgi = sh.seg[o];
-                    const int lx = (int)((sgi >> 16) & 31u) + (k - (int)(sgi & 0xffffu)), ly = (int)((sgi >> 21) & 7u);
-                    const int slot = (int)(sgi >> 24);
-                    const int kp = ly * LIB_RTW + lx;
-                    // per-pixel hierarchical z: the pixel's current key already beats the
-                    // primitive's depth bound (a stale, higher key only skips less)
-                    if (sh.zord[slot] > reinterpret_cast<const uint32_t *>(sh.key)[2 * kp + 1]) return;
-                    const LibRec r = lib_rec_from(&sh.rec[slot * 4]);
-                    float z01, u, v, w, idn;
-                    if (lib_test<SHADOW>(fp, r, TX0 + lx, TY0 + ly, z01, u, v, w, idn))
-                        atomicMin(&sh.key[kp], lib_key(fp, z01, r.seq, SHADOW));
-                };
-                for (int k0 = 64 * wave; k0 < total; k0 += 256) pair(k0);
-            } else {
+            // Pair tasks (shallow raster and shadow pass -- the deep camera raster takes its own passes
+            // above): the staged boxes laid end to end (C5: few, mostly large primitives; the span
+            // arithmetic would spill the shallow raster's 80 registers, and measured 10 % slower on C5's
+            // shadow map).  Every (primitive, pixel) pair is dealt to one lane, 64-pair windows
+            // round-robin over the waves (start bitmap + word owners, as in shs_legacy.hip).
+            {
                 uint4 *pinfo = reinterpret_cast<uint4 *>(sh.seg);   // per staged box: first pair, x0 | y0 << 16, width | slot << 16, 2^16/width
                 int area = 0, bx0 = 0, by0 = 0, bw = 1;
                 uint32_t zord = 0u;
@@ -2204,17 +2263,13 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     }
 }
 
-template <bool SHADOW>
-__device__ __forceinline__ void lib_clear_tile(const LibFrameParams &fp, const LibBuffers &fb, int rt) {
+// A shadow-map raster tile no primitive touches: its texels get the clear depth.
+__device__ __forceinline__ void lib_clear_shadow_tile(const LibFrameParams &fp, const LibBuffers &fb, int rt) {
     const int tid = threadIdx.x;
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
     const int px = col * LIB_RTW + (tid & 31), py = row * LIB_RTH + (tid >> 5);
-    if (SHADOW) {
-        bool covered;
-        lib_resolve<SHADOW>(fp, fb, KEY_EMPTY, px, py, covered);
-    } else if (tid < 4) {
-        fb.blkcov[(size_t)rt * 4 + tid] = 0u;   // no winner anywhere: k_lib_resolve reads no key
-    }
+    bool covered;
+    lib_resolve<true>(fp, fb, KEY_EMPTY, px, py, covered);
 }
 
 // The camera pass's raster work plan, after the marks are final (one thread per owned raster tile):
@@ -2263,67 +2318,80 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
     sh.key[tid] = KEY_EMPTY;
     uint32_t chunk = 0;   // staging passes so far (selects the colmax slot)
     if (fb.timeline && tid < LTL_STRIDE) sh.tl[tid] = tid == LTL_START ? tl_now() : 0ull;
-    // Owned raster tiles: the first S * G statically interleaved (tile b + i * G, i < S: no ticket
-    // latency), the rest from LIB_NQ ticket queues (the next ticket requested while the current tile
-    // renders; an exhausted queue sends the workgroup on to the others).  S covers about half of the
-    // tiles, so the dense tiles that end up late in some workgroup's static list are balanced by the
-    // dynamic half; one tile per ticket keeps a dense bin tile's 4 rows on different workgroups.
+    // Owned raster tiles: the first S * G statically interleaved (tile b + i * G, i < S), the rest
+    // from LIB_NQ ticket queues (the next ticket requested while the current tile renders; an
+    // exhausted queue sends the workgroup on to the others).  S covers about half of the tiles, so the
+    // dense tiles that end up late in some workgroup's static list are balanced by the dynamic half;
+    // one tile per ticket keeps a dense bin tile's 4 rows on different workgroups.  The static items'
+    // tiles and busy flags come in one round trip at the start, so a tile nothing touches costs the
+    // workgroup nothing: the camera pass has no pixel to write there (k_lib_resolve writes the clear
+    // values and resets the block flags it read), the shadow pass clears its depth.
     uint32_t *rq = fb.rqueue + (size_t)fp.parity * LIB_NQ * LIB_QSTRIDE;
     // work items: the owned raster tiles, or k_lib_plan's list (split tiles' parts first)
     const int n_split = (!SHADOW && fp.part) ? (int)cnt[LC_ITEMS] : 0;
     const int n_work = n_split + fp.n_owned_rt;
-    const int S = max(1, n_work / (2 * G));
+    const int S = min(max(1, n_work / (2 * G)), LIB_MAX_STATIC);
     const int dyn0 = S * G;
-    int j = (int)blockIdx.x;
-    int i_static = 0, q = (int)(blockIdx.x & (LIB_NQ - 1)), tried = 0;
-    while (j < n_work) {   // block-uniform
-        const bool dynamic_next = i_static + 1 >= S;
-        uint32_t tk = 0;
-        if (tid == 0 && dynamic_next) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
-        // owned raster tile j (the host's XCD-coherent order, rows inside the frame only)
-        {
-            int rt;
-            uint32_t part = 0u, parts = 1u;
-            bool skip = false;
-            if (j < n_split) {
-                const uint2 it = fb.items[j];
-                rt = (int)it.x;
-                part = it.y & 0xffffu;
-                parts = it.y >> 16;
-            } else {
-                rt = fb.rt_order[j - n_split];
-                skip = !SHADOW && fb.busy[rt] == 2u;   // rendered as parts (k_lib_plan)
+    // item word of position j: rt | min(busy, 3) << 28, or 0x80000000 | j for a split tile's part
+    auto item_word = [&](int jj) -> uint32_t {
+        if (jj < n_split) return 0x80000000u | (uint32_t)jj;
+        const int rt = fb.rt_order[jj - n_split];
+        return (uint32_t)rt | (min(fb.busy[rt], 3u) << 28);
+    };
+    if (tid < S) {
+        const int jj = (int)blockIdx.x + tid * G;
+        sh.sitem[tid] = jj < n_work ? item_word(jj) : 0xffffffffu;
+    }
+    __syncthreads();
+    int q = (int)(blockIdx.x & (LIB_NQ - 1)), tried = 0;
+    const bool dynamic = dyn0 < n_work;   // (then every static position is a work item)
+    uint32_t tk = 0;
+    for (int i = 0;; ++i) {   // block-uniform; one call site of the tile raster (its code is large)
+        uint32_t w;
+        if (i < S) {
+            w = sh.sitem[i];
+            if (w == 0xffffffffu) break;
+            if (i == S - 1 && dynamic && tid == 0) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);   // under the last static tile
+        } else {
+            if (!dynamic) break;
+            if (tid == 0) {
+                int nj = dyn0 + q + LIB_NQ * (int)tk;
+                while (nj >= n_work && ++tried < LIB_NQ) {
+                    q = (q + 1) & (LIB_NQ - 1);
+                    nj = dyn0 + q + LIB_NQ * (int)atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
+                }
+                sh.next[0] = nj < n_work ? nj : n_work;
+                sh.next[1] = q;
+                sh.next[2] = tried;
             }
-            if (skip) {
-            } else if (parts > 1u || fb.busy[rt]) {
-                lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk, part, parts);
-            } else {
-                const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
-                lib_clear_tile<SHADOW>(fp, fb, rt);
-                if (fb.timeline && tid == 0) { sh.tl[LTL_CLEAR] += tl_now() - t_c; sh.tl[LTL_NCLEAR] += 1ull; }
-            }
+            __syncthreads();
+            const int j = sh.next[0];
+            q = sh.next[1];
+            tried = sh.next[2];
+            __syncthreads();
+            if (j >= n_work) break;
+            if (tid == 0) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);   // the next ticket, under this tile
+            w = item_word(j);
         }
-        if (!dynamic_next) {
-            ++i_static;
-            j += G;
-            continue;
+        int rt;
+        uint32_t part = 0u, parts = 1u, busy = 1u;
+        if (w & 0x80000000u) {   // a split tile's part
+            const uint2 it = fb.items[w & 0x7fffffffu];
+            rt = (int)it.x;
+            part = it.y & 0xffffu;
+            parts = it.y >> 16;
+        } else {
+            rt = (int)(w & 0x0fffffffu);
+            busy = w >> 28;
+            if (!SHADOW && busy == 2u) continue;   // rendered as parts (k_lib_plan)
         }
-        i_static = S;
-        if (tid == 0) {
-            int nj = dyn0 + q + LIB_NQ * (int)tk;
-            while (nj >= n_work && ++tried < LIB_NQ) {
-                q = (q + 1) & (LIB_NQ - 1);
-                nj = dyn0 + q + LIB_NQ * (int)atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
-            }
-            sh.next[0] = nj < n_work ? nj : n_work;
-            sh.next[1] = q;
-            sh.next[2] = tried;
+        if (busy) {
+            lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk, part, parts);
+        } else {
+            const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
+            if (SHADOW) lib_clear_shadow_tile(fp, fb, rt);
+            if (fb.timeline && tid == 0) { sh.tl[LTL_CLEAR] += tl_now() - t_c; sh.tl[LTL_NCLEAR] += 1ull; }
         }
-        __syncthreads();
-        j = sh.next[0];
-        q = sh.next[1];
-        tried = sh.next[2];
-        __syncthreads();
     }
     __syncthreads();
     if (tid == 0) fb.rstat[blockIdx.x] = make_uint2(sh.cov, sh.maxbin);
@@ -2379,6 +2447,7 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
         const bool inb = px < fp.W && py < fp.H;
         const bool any = fb.blkcov[(size_t)rt * 4 + sub] != 0u;   // wave-uniform
         if (sub == 0 && lane == 0) fb.busy[rt] = 0u;   // the raster's busy / split flag, for the next pass
+        if (any && lane == 0) fb.blkcov[(size_t)rt * 4 + sub] = 0u;   // the next pass's raster sets only its busy tiles' flags
         const unsigned long long key = inb && any ? fb.keys[(size_t)py * fp.W + px] : KEY_EMPTY;
         LtWave lw;
 #ifdef SHS_RESOLVE_NO_LTWAVE

@@ -178,8 +178,8 @@ constexpr int STL_STRIDE = 8;
 
 // Library raster timeline slots (s_memrealtime, 100 MHz ticks): per workgroup start, end, summed
 // phase ticks over its busy tiles (gather, stage + pairs, resolve + shade), clear ticks, counts.
-constexpr int LTL_STRIDE = 12;
+constexpr int LTL_STRIDE = 14;
 enum : int { LTL_START = 0, LTL_END, LTL_GATHER, LTL_PAIRS, LTL_SHADE, LTL_CLEAR, LTL_NBUSY, LTL_NCLEAR, LTL_CHUNKS,
-             LTL_NPAIRS, LTL_NCAND, LTL_MAXTILE };
+             LTL_NPAIRS, LTL_NCAND, LTL_MAXTILE, LTL_STAGE, LTL_SEG };
 
 }  // namespace shs_dev
