@@ -1808,7 +1808,8 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     const int my_lx = 16 * (wave & 1) + (lane & 15), my_ly = 4 * (wave >> 1) + (lane >> 4);
     const bool mine = TX0 + my_lx >= X0 && TX0 + my_lx <= X1 && TY0 + my_ly >= Y0 && TY0 + my_ly <= Y1;
     const int bt = (row / (TILE / LIB_RTH)) * fp.tiles_x + col;
-    __syncthreads();   // the previous tile's key resets are done
+    // (no barrier here: the previous tile ended with each thread resetting its own pixel's key, and
+    // every round below starts with one before any shared state is touched)
     const bool tlon = fb.timeline != nullptr && tid == 0;
     const uint64_t t_tile = tlon ? tl_now() : 0ull;
     uint64_t t_gather = 0ull;
@@ -2364,11 +2365,10 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
                 sh.next[1] = q;
                 sh.next[2] = tried;
             }
-            __syncthreads();
+            __syncthreads();   // (sh.next is rewritten only after a whole tile, past many barriers)
             const int j = sh.next[0];
             q = sh.next[1];
             tried = sh.next[2];
-            __syncthreads();
             if (j >= n_work) break;
             if (tid == 0) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);   // the next ticket, under this tile
             w = item_word(j);
