@@ -387,7 +387,11 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     // the shallow raster (256-candidate rounds, twice the workgroups per CU) when the previous frame's
     // fullest bin tile fit one such round (scan mode: every primitive is a candidate)
     const uint64_t fullest = fp.scan_mode ? (uint64_t)n_tris + (shadow ? 0u : w.st_extra) : w.st_maxbin;
-    const bool shallow = w.st_checked && fullest <= 256u;
+    static const int force_deep = [] {   // SHS_LIB_DEEP=1 (timing experiments): the deep raster for every camera pass
+        const char *e = std::getenv("SHS_LIB_DEEP");
+        return e ? std::atoi(e) : 0;
+    }();
+    const bool shallow = w.st_checked && fullest <= 256u && !(force_deep && !shadow);
     int &resident = ctx->lib_resident[shadow ? 1 : 0][shallow ? 1 : 0];
     if (resident <= 0) resident = shs_internal::lib_raster_resident_blocks(ctx->device, shadow, shallow);
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt, resident));
