@@ -245,10 +245,10 @@ int shs_shard_balance_rects(const uint32_t *blocks, int32_t n_blocks, int32_t wi
  * phase marks of the workgroup's thread 0 (0 where a phase did not run). */
 int shs_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out);
 /* Debug / profiling hook: the last camera pass's k_lib_raster workgroup timeline (SHS_OPT_TIMELINE),
- * 14 uint64 per workgroup: start, end, summed ticks of gather / stage + pairs / resolve + shade over
+ * 16 uint64 per workgroup: start, end, summed ticks of gather / stage + pairs / resolve + shade over
  * its busy tiles, clear ticks, busy tiles, cleared tiles, staging passes, pairs, candidates, longest
  * busy tile, and (deep camera raster) the staging passes' selection + record + span ticks and segment
- * ticks (s_memrealtime, 100 MHz).  out = NULL: *n_out = the count only. */
+ * ticks, all busy tiles' ticks, the last busy tile's end (s_memrealtime, 100 MHz).  out = NULL: *n_out = the count only. */
 int shs_lib_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out);
 /* The same for the last camera pass's k_lib_setup: 6 uint64 per workgroup -- start, after its
  * triangles, after the deferred marks, end, large primitives, deferred union width x height. */

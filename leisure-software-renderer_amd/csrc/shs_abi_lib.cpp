@@ -57,7 +57,7 @@ void release_work(Work &w) {
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.dynq); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
     if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
@@ -309,7 +309,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         reset = true;
     }
     if (!w.counters.p) {
-        if (ensure(ctx, w.counters, 2 * shs_dev::LC_N) || ensure(ctx, w.rqueue, 2 * shs_dev::LIB_NQ * shs_dev::LIB_QSTRIDE))
+        if (ensure(ctx, w.counters, 2 * shs_dev::LC_N) || ensure(ctx, w.rqueue, 2 * shs_dev::LIB_NQW * shs_dev::LIB_QSTRIDE))
             return SHS_ERR_HIP;
         reset = true;
     }
@@ -396,6 +396,16 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (resident <= 0) resident = shs_internal::lib_raster_resident_blocks(ctx->device, shadow, shallow);
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt, resident));
     if (ensure(ctx, w.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
+    fp.raster_grid = raster_grid;
+    {   // static share of the raster items (SHS_LIB_STATIC_DIV: timing experiments)
+        static const int div = [] { const char *e = std::getenv("SHS_LIB_STATIC_DIV"); return e ? std::atoi(e) : 2; }();
+        fp.static_div = div;
+    }
+    if (!shadow) {   // k_lib_dyn's per-queue lists: every work position could be dynamic
+        const size_t n_max = (size_t)std::max(fp.n_owned_rt, 1) * (fp.part ? 1 + shs_dev::LIB_MAXK : 1);
+        fp.dyn_cap = (uint32_t)((n_max + shs_dev::LIB_NQ - 1) / shs_dev::LIB_NQ + 1);
+        if (ensure(ctx, w.dynq, (size_t)shs_dev::LIB_NQ * fp.dyn_cap)) return SHS_ERR_HIP;
+    }
 
     LibBuffers fb;
     std::memset(&fb, 0, sizeof fb);
@@ -406,6 +416,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.dbase = reinterpret_cast<int32_t *>(w.draws.p + nd);
     fb.bdraw = fb.dbase + nd + 1;
     fb.rqueue = w.rqueue.p;
+    fb.dynq = shadow ? nullptr : w.dynq.p;
     fb.items = fp.part ? w.items.p : nullptr;
     // Tile-sharded camera pass in bin mode: each setup workgroup first keeps the rank's triangles of its
     // inputs, positions only (SHS_OPT_SHARD_CULL 0: off).

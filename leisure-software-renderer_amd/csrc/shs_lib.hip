@@ -771,7 +771,7 @@ __device__ __forceinline__ void wave_append(uint32_t *counter, T *queue, bool pr
 // Setup workgroup start: LDS state, and the next frame's counter set, raster queues and bin counts zeroed.
 __device__ __forceinline__ void setup_zero_next(const LibFrameParams &fp, const LibBuffers &fb, int b, int tid) {
     if (b == 0 && tid < LC_N) fb.counters[(fp.parity ^ 1u) * LC_N + tid] = 0u;
-    if (b == 0 && tid < LIB_NQ) fb.rqueue[((fp.parity ^ 1u) * LIB_NQ + tid) * LIB_QSTRIDE] = 0u;
+    if (b == 0 && tid < LIB_NQW) fb.rqueue[((fp.parity ^ 1u) * LIB_NQW + tid) * LIB_QSTRIDE] = 0u;
     {
         const int n_bt = fp.tiles_x * fp.tiles_y;
         uint32_t *next_count = fb.tile_count + (size_t)(fp.parity ^ 1u) * n_bt;
@@ -1651,7 +1651,8 @@ struct LibShared {
     uint32_t wmax[4];                     // deep camera raster: per wave, the largest key z of its pixels after a pass
     uint32_t colmax[2][LIB_RTW];          // per pixel column: max key z (orderable bits) over its rows, by chunk parity
     uint32_t nc, nbusy, cov, maxbin, npairs;
-    int next[3];                          // the workgroup's next run, queue, queues tried
+    int next[4];                          // the workgroup's next item: any, queue, queues tried, its word
+    uint32_t qlen[LIB_NQ];                // camera pass: k_lib_dyn's list lengths
     uint32_t sitem[LIB_MAX_STATIC];       // the workgroup's static work items (k_lib_raster)
     uint64_t tl[LTL_STRIDE];              // SHS_OPT_TIMELINE accumulators (thread 0)
     // segment (deep) or staged box (shallow) owning each bitmap word's first pair
@@ -2261,6 +2262,8 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         sh.tl[LTL_NBUSY] += 1;
         sh.tl[LTL_CHUNKS] += chunk - chunk0;
         sh.tl[LTL_MAXTILE] = max(sh.tl[LTL_MAXTILE], t_end - t_tile);
+        sh.tl[LTL_TILES] += t_end - t_tile;
+        sh.tl[LTL_LAST] = t_end;
     }
 }
 
@@ -2284,6 +2287,45 @@ __device__ __forceinline__ uint32_t plan_parts(const LibFrameParams &fp, const L
     const uint32_t total = fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + (row / (TILE / LIB_RTH)) * fp.tiles_x + col];
     const uint32_t n = min(total, fp.bin_cap) + (total > fp.bin_cap ? min(cnt[LC_SPILL], fp.spill_cap) : 0u);
     return n > 4u * fp.part ? 4u : n > fp.part ? 2u : 1u;
+}
+
+// k_lib_raster's work items: position j < n_split is k_lib_plan's part j (word 0x80000000 | j), the rest
+// the owned raster tiles in rt_order (word rt | min(busy, 3) << 28).  Workgroup b takes positions
+// b + i * G, i < S (static), the rest (from dyn0 = S * G on) come from LIB_NQ ticket queues, position p
+// in queue (p - dyn0) % LIB_NQ.
+__device__ __forceinline__ int lib_static_items(int n_work, int G, int div) { return min(max(1, n_work / (max(div, 1) * G)), LIB_MAX_STATIC); }
+__device__ __forceinline__ uint32_t lib_item_word(const LibBuffers &fb, int n_split, int j) {
+    if (j < n_split) return 0x80000000u | (uint32_t)j;
+    const int rt = fb.rt_order[j - n_split];
+    return (uint32_t)rt | (min(fb.busy[rt], 3u) << 28);
+}
+
+// Camera pass: the dynamic positions that have anything to render (parts, busy tiles), compacted per
+// queue into LibBuffers::dynq (lengths in the queue's second counter), so a raster ticket never lands
+// on a tile nothing touches -- each such ticket cost a workgroup an atomic and two dependent loads, and
+// at the end of the pass, when only those were left, ~25 us of every workgroup's life.  Order inside a
+// queue: per wave (the waves' appends race), which the raster does not depend on.
+__global__ __launch_bounds__(256) void k_lib_dyn(LibFrameParams fp, LibBuffers fb) {
+    const uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    uint32_t *rq = fb.rqueue + (size_t)fp.parity * LIB_NQW * LIB_QSTRIDE;
+    const int n_split = fp.part ? (int)cnt[LC_ITEMS] : 0;
+    const int n_work = n_split + fp.n_owned_rt;
+    const int dyn0 = lib_static_items(n_work, fp.raster_grid, fp.static_div) * fp.raster_grid;
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int p = dyn0 + i;
+    uint32_t w = 0u;
+    bool keep = false;
+    if (p < n_work) {
+        w = lib_item_word(fb, n_split, p);
+        keep = (w & 0x80000000u) || (w >> 28) == 1u;
+    }
+    const int lane = __lane_id(), q = i & (LIB_NQ - 1);   // (a wave's lanes cycle through the queues)
+    const uint64_t mine = __ballot(keep) & (0x0101010101010101ull << (lane & 7));
+    const int lead = mine ? __ffsll((unsigned long long)mine) - 1 : lane;
+    uint32_t base = 0u;
+    if (keep && lane == lead) base = atomicAdd(&rq[(LIB_NQ + q) * LIB_QSTRIDE], (uint32_t)__popcll(mine));
+    base = (uint32_t)__shfl((int)base, lead);
+    if (keep) fb.dynq[(size_t)q * fp.dyn_cap + base + lanes_below(mine)] = w;
 }
 
 __global__ __launch_bounds__(256) void k_lib_plan(LibFrameParams fp, LibBuffers fb) {
@@ -2327,23 +2369,22 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
     // tiles and busy flags come in one round trip at the start, so a tile nothing touches costs the
     // workgroup nothing: the camera pass has no pixel to write there (k_lib_resolve writes the clear
     // values and resets the block flags it read), the shadow pass clears its depth.
-    uint32_t *rq = fb.rqueue + (size_t)fp.parity * LIB_NQ * LIB_QSTRIDE;
+    uint32_t *rq = fb.rqueue + (size_t)fp.parity * LIB_NQW * LIB_QSTRIDE;
     // work items: the owned raster tiles, or k_lib_plan's list (split tiles' parts first)
     const int n_split = (!SHADOW && fp.part) ? (int)cnt[LC_ITEMS] : 0;
     const int n_work = n_split + fp.n_owned_rt;
-    const int S = min(max(1, n_work / (2 * G)), LIB_MAX_STATIC);
+    const int S = lib_static_items(n_work, G, fp.static_div);
     const int dyn0 = S * G;
-    // item word of position j: rt | min(busy, 3) << 28, or 0x80000000 | j for a split tile's part
-    auto item_word = [&](int jj) -> uint32_t {
-        if (jj < n_split) return 0x80000000u | (uint32_t)jj;
-        const int rt = fb.rt_order[jj - n_split];
-        return (uint32_t)rt | (min(fb.busy[rt], 3u) << 28);
-    };
+    // the camera pass's dynamic items come from k_lib_dyn's per-queue lists (busy tiles and parts only)
+    constexpr bool listed = !SHADOW;
     if (tid < S) {
         const int jj = (int)blockIdx.x + tid * G;
-        sh.sitem[tid] = jj < n_work ? item_word(jj) : 0xffffffffu;
+        sh.sitem[tid] = jj < n_work ? lib_item_word(fb, n_split, jj) : 0xffffffffu;
     }
+    if (listed && tid < LIB_NQ) sh.qlen[tid] = rq[(LIB_NQ + tid) * LIB_QSTRIDE];
     __syncthreads();
+    // queue q's end: its list length (camera pass) or its share of the positions
+    auto q_end = [&](int qq) -> int { return listed ? (int)sh.qlen[qq] : (n_work - dyn0 - qq + LIB_NQ - 1) / LIB_NQ; };
     int q = (int)(blockIdx.x & (LIB_NQ - 1)), tried = 0;
     const bool dynamic = dyn0 < n_work;   // (then every static position is a work item)
     uint32_t tk = 0;
@@ -2356,22 +2397,23 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
         } else {
             if (!dynamic) break;
             if (tid == 0) {
-                int nj = dyn0 + q + LIB_NQ * (int)tk;
-                while (nj >= n_work && ++tried < LIB_NQ) {
+                int t = (int)tk;
+                while (t >= q_end(q) && ++tried < LIB_NQ) {   // this queue is exhausted: the next one
                     q = (q + 1) & (LIB_NQ - 1);
-                    nj = dyn0 + q + LIB_NQ * (int)atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
+                    t = (int)atomicAdd(&rq[q * LIB_QSTRIDE], 1u);
                 }
-                sh.next[0] = nj < n_work ? nj : n_work;
+                const bool more = t < q_end(q);
+                sh.next[0] = more ? 1 : 0;
                 sh.next[1] = q;
                 sh.next[2] = tried;
+                if (more) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);   // the next ticket, under this tile
+                sh.next[3] = !more ? 0 : listed ? (int)fb.dynq[(size_t)q * fp.dyn_cap + t] : (int)lib_item_word(fb, n_split, dyn0 + q + LIB_NQ * t);
             }
             __syncthreads();   // (sh.next is rewritten only after a whole tile, past many barriers)
-            const int j = sh.next[0];
+            if (!sh.next[0]) break;
             q = sh.next[1];
             tried = sh.next[2];
-            if (j >= n_work) break;
-            if (tid == 0) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);   // the next ticket, under this tile
-            w = item_word(j);
+            w = (uint32_t)sh.next[3];
         }
         int rt;
         uint32_t part = 0u, parts = 1u, busy = 1u;
@@ -2557,6 +2599,10 @@ hipError_t launch_lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, in
 
 hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, bool shadow, bool shallow, int grid, hipStream_t s) {
     if (!shadow && fp.part) hipLaunchKernelGGL(k_lib_plan, dim3(std::max(1, (fp.n_owned_rt + 255) / 256)), dim3(256), 0, s, fp, fb);
+    if (!shadow) {   // every position could be dynamic (a grid of one workgroup); threads past the end exit
+        const int64_t n_max = (int64_t)fp.n_owned_rt * (fp.part ? 1 + LIB_MAXK : 1);
+        hipLaunchKernelGGL(k_lib_dyn, dim3((unsigned)std::max<int64_t>(1, (n_max + 255) / 256)), dim3(256), 0, s, fp, fb);
+    }
     hipLaunchKernelGGL(SHS_RASTER_KERNEL(shadow, shallow), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }

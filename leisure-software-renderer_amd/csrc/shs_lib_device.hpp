@@ -120,6 +120,9 @@ struct LibFrameParams {
     float tm_exposure, tm_inv_gamma; // fused PassTonemap (LibBuffers::tm_thr)
     uint32_t part;                   // camera pass: k_lib_plan splits a tile's list into parts of this many
                                      // entries (0: one work item per owned raster tile, no plan)
+    int32_t raster_grid;             // k_lib_raster's workgroups (k_lib_dyn derives the same static share)
+    int32_t static_div;              // k_lib_raster: n_work / (static_div * workgroups) static items per workgroup
+    uint32_t dyn_cap;                // camera pass: entries per queue of LibBuffers::dynq
     ShardRegion reg;                 // count > 1 with reg.on: this rank's rectangle of bin tiles
 };
 
@@ -149,7 +152,8 @@ struct LibBuffers {
     uint32_t *bigpre;                // exclusive task prefix of bigq (written with the entries)
     const int32_t *dbase;            // draws[i].tri_base, compact (+ n_tris): the triangle -> draw search
     const int32_t *bdraw;            // per setup block: the draw of its first triangle
-    uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQ x LIB_QSTRIDE words
+    uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQW x LIB_QSTRIDE words
+    uint32_t *dynq;                  // camera pass: k_lib_dyn's work item words per queue (LIB_NQ x dyn_cap)
     const int32_t *rt_order;         // the owned raster tiles in processing order (n_owned_rt; XCD-coherent)
     unsigned long long *keys;        // camera pass: W*H winning (z, submission) keys, k_lib_raster -> k_lib_resolve
     uint32_t *blkcov;                // camera pass: per 16x4 block (4 per raster tile, rt * 4 + sub): keys written
@@ -170,6 +174,8 @@ constexpr int LIB_MAXK = 16;
 // k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket
 // counters a cache line apart (k_lib_setup zeroes the next frame's set).
 constexpr int LIB_NQ = 8, LIB_QSTRIDE = 32;
+// per parity: LIB_NQ ticket counters, then (camera pass) LIB_NQ k_lib_dyn list lengths
+constexpr int LIB_NQW = 2 * LIB_NQ;
 
 // Library setup timeline slots: start, after the per-triangle work, after the deferred marks,
 // after the large-primitive marks (= end), large primitives, deferred-union width x height, after the
@@ -178,8 +184,8 @@ constexpr int STL_STRIDE = 8;
 
 // Library raster timeline slots (s_memrealtime, 100 MHz ticks): per workgroup start, end, summed
 // phase ticks over its busy tiles (gather, stage + pairs, resolve + shade), clear ticks, counts.
-constexpr int LTL_STRIDE = 14;
+constexpr int LTL_STRIDE = 16;
 enum : int { LTL_START = 0, LTL_END, LTL_GATHER, LTL_PAIRS, LTL_SHADE, LTL_CLEAR, LTL_NBUSY, LTL_NCLEAR, LTL_CHUNKS,
-             LTL_NPAIRS, LTL_NCAND, LTL_MAXTILE, LTL_STAGE, LTL_SEG };
+             LTL_NPAIRS, LTL_NCAND, LTL_MAXTILE, LTL_STAGE, LTL_SEG, LTL_TILES, LTL_LAST };
 
 }  // namespace shs_dev

@@ -514,10 +514,10 @@ class Context:
         return tuple(int(v) for v in out)
 
     LIB_TIMELINE_FIELDS = ("start", "end", "gather", "pairs", "shade", "clear", "n_busy", "n_clear", "chunks",
-                           "n_pairs", "n_cand", "max_tile", "stage", "seg")
+                           "n_pairs", "n_cand", "max_tile", "stage", "seg", "tiles", "last")
 
     def lib_debug_timeline(self):
-        """Last camera pass's k_lib_raster workgroup timeline: uint64 [grid, 14] (LIB_TIMELINE_FIELDS;
+        """Last camera pass's k_lib_raster workgroup timeline: uint64 [grid, 16] (LIB_TIMELINE_FIELDS;
         times in 10-ns ticks)."""
         n = ctypes.c_int64()
         self._check(self._lib.shs_lib_debug_timeline(self._h, None, 0, ctypes.byref(n)))

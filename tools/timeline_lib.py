@@ -60,8 +60,10 @@ def main():
             print(f"  {name:10s} med {np.median(v):9.2f} p90 {np.percentile(v, 90):9.2f} max {v.max():9.2f} "
                   f"sum {v.sum():12.1f}")
         dist("wg us", dur)
-        for n in ("gather", "pairs", "stage", "seg", "shade", "clear", "max_tile"):
+        for n in ("gather", "pairs", "stage", "seg", "shade", "clear", "max_tile", "tiles"):
             dist(n + " us", f[n] / 100.0)
+        dist("after us", (f["end"] - f["last"]) / 100.0)
+        dist("between us", ((f["end"] - f["start"]) - f["tiles"] - (f["end"] - f["last"])) / 100.0)
         for n in ("n_busy", "n_clear", "chunks", "n_pairs", "n_cand"):
             dist(n, f[n].astype(np.float64))
         st = ctx.lib_debug_setup_timeline().astype(np.int64)
@@ -77,7 +79,7 @@ def main():
               f"{int((st[:, 4] > 0).sum())}, no-agg unions {int((st[:, 5] > 256).sum())}")
         k = int(np.argmax(dur))
         print("  slowest wg %d: %s" % (k, " ".join(
-            "%s=%s" % (n, ("%.1f" % (f[n][k] / 100.0)) if n in ("gather", "pairs", "stage", "seg", "shade", "clear", "max_tile")
+            "%s=%s" % (n, ("%.1f" % (f[n][k] / 100.0)) if n in ("gather", "pairs", "stage", "seg", "shade", "clear", "max_tile", "tiles")
                        else int(f[n][k])) for n in names[2:])))
     ctx.close()
 
