@@ -404,7 +404,10 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (!shadow) {   // k_lib_dyn's per-queue lists: every work position could be dynamic
         const size_t n_max = (size_t)std::max(fp.n_owned_rt, 1) * (fp.part ? 1 + shs_dev::LIB_MAXK : 1);
         fp.dyn_cap = (uint32_t)((n_max + shs_dev::LIB_NQ - 1) / shs_dev::LIB_NQ + 1);
-        if (ensure(ctx, w.dynq, (size_t)shs_dev::LIB_NQ * fp.dyn_cap)) return SHS_ERR_HIP;
+        if (ensure(ctx, w.dynq, (size_t)2 * shs_dev::LIB_NQ * fp.dyn_cap)) return SHS_ERR_HIP;
+        // heavy tiles (bin list entries; SHS_LIB_HEAVY: timing experiments, 0 = none)
+        static const int heavy = [] { const char *e = std::getenv("SHS_LIB_HEAVY"); return e ? std::atoi(e) : 2048; }();
+        fp.heavy_min = (uint32_t)std::max(heavy, 0);
     }
 
     LibBuffers fb;

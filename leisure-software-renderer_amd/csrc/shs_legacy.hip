@@ -1066,7 +1066,6 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     const int bt_spill = frame * fp.tiles_x * fp.tiles_y + bt;   // the bin tile's key in spill entries
     constexpr bool no_recs = NO_RECS;   // == (fp.flags & RF_NO_RECS): a kernel variant each
     const int dbase = frame * fp.n_draws;                       // the frame's slice of the draw table
-    __syncthreads();   // the previous tile's key resets are done
 
     // candidate sources.  scan mode: every triangle's bin box.  bin mode: the bin tile's list, then
     // the spill list (entries of this bin tile).
@@ -1080,6 +1079,9 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
         n_items = n_bin + n_spill;
         if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
     }
+    // the previous tile's key resets (each thread its own pixel) precede every shared write of this
+    // one: a candidate round starts with a barrier; without one, the ghost fragments below need it
+    if (n_items == 0u) __syncthreads();
     const uint32_t *bin = fb.bins + (size_t)bt * fp.bin_cap;
     uint32_t seq = 0;   // candidates processed (profiling)
     int pairs = 0;      // (candidate, pixel) tasks (profiling)

@@ -1652,7 +1652,7 @@ struct LibShared {
     uint32_t colmax[2][LIB_RTW];          // per pixel column: max key z (orderable bits) over its rows, by chunk parity
     uint32_t nc, nbusy, cov, maxbin, npairs;
     int next[4];                          // the workgroup's next item: any, queue, queues tried, its word
-    uint32_t qlen[LIB_NQ];                // camera pass: k_lib_dyn's list lengths
+    uint32_t qlen[2 * LIB_NQ];            // camera pass: k_lib_dyn's light, then heavy list lengths
     uint32_t sitem[LIB_MAX_STATIC];       // the workgroup's static work items (k_lib_raster)
     uint64_t tl[LTL_STRIDE];              // SHS_OPT_TIMELINE accumulators (thread 0)
     // segment (deep) or staged box (shallow) owning each bitmap word's first pair
@@ -2290,42 +2290,59 @@ __device__ __forceinline__ uint32_t plan_parts(const LibFrameParams &fp, const L
 }
 
 // k_lib_raster's work items: position j < n_split is k_lib_plan's part j (word 0x80000000 | j), the rest
-// the owned raster tiles in rt_order (word rt | min(busy, 3) << 28).  Workgroup b takes positions
-// b + i * G, i < S (static), the rest (from dyn0 = S * G on) come from LIB_NQ ticket queues, position p
-// in queue (p - dyn0) % LIB_NQ.
+// the owned raster tiles in rt_order (word rt | min(busy, 3) << 28, | LIB_HEAVY for a heavy camera-pass
+// tile: its bin list holds >= fp.heavy_min entries).  Workgroup b takes positions b + i * G, i < S
+// (static), the rest (from dyn0 = S * G on) come from LIB_NQ ticket queues, position p in queue
+// (p - dyn0) % LIB_NQ.
+constexpr uint32_t LIB_HEAVY = 0x40000000u;
 __device__ __forceinline__ int lib_static_items(int n_work, int G, int div) { return min(max(1, n_work / (max(div, 1) * G)), LIB_MAX_STATIC); }
-__device__ __forceinline__ uint32_t lib_item_word(const LibBuffers &fb, int n_split, int j) {
+__device__ __forceinline__ uint32_t lib_item_word(const LibFrameParams &fp, const LibBuffers &fb, int n_split, int j) {
     if (j < n_split) return 0x80000000u | (uint32_t)j;
     const int rt = fb.rt_order[j - n_split];
-    return (uint32_t)rt | (min(fb.busy[rt], 3u) << 28);
+    const uint32_t busy = min(fb.busy[rt], 3u);
+    uint32_t w = (uint32_t)rt | (busy << 28);
+    if (fp.heavy_min && busy == 1u) {
+        const int bt = (rt / fp.tiles_x / (TILE / LIB_RTH)) * fp.tiles_x + rt % fp.tiles_x;
+        if (fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + bt] >= fp.heavy_min) w |= LIB_HEAVY;
+    }
+    return w;
 }
 
-// Camera pass: the dynamic positions that have anything to render (parts, busy tiles), compacted per
-// queue into LibBuffers::dynq (lengths in the queue's second counter), so a raster ticket never lands
-// on a tile nothing touches -- each such ticket cost a workgroup an atomic and two dependent loads, and
-// at the end of the pass, when only those were left, ~25 us of every workgroup's life.  Order inside a
-// queue: per wave (the waves' appends race), which the raster does not depend on.
+// Camera pass: the work items a raster ticket can hand out, compacted per queue into LibBuffers::dynq --
+// the dynamic positions that have anything to render (parts, busy tiles) into the light lists, and the
+// heavy tiles of every position, static ones included, into the heavy lists that the tickets serve first
+// (the longest tiles start early instead of ending the pass; a static workgroup skips its heavy items).
+// A ticket never lands on a tile nothing touches: each such ticket cost a workgroup an atomic and two
+// dependent loads, and at the end of the pass, when only those were left, ~25 us of every workgroup's
+// life.  Order inside a list: per wave (the waves' appends race), which the raster does not depend on.
 __global__ __launch_bounds__(256) void k_lib_dyn(LibFrameParams fp, LibBuffers fb) {
     const uint32_t *cnt = fb.counters + fp.parity * LC_N;
     uint32_t *rq = fb.rqueue + (size_t)fp.parity * LIB_NQW * LIB_QSTRIDE;
     const int n_split = fp.part ? (int)cnt[LC_ITEMS] : 0;
     const int n_work = n_split + fp.n_owned_rt;
     const int dyn0 = lib_static_items(n_work, fp.raster_grid, fp.static_div) * fp.raster_grid;
-    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
-    const int p = dyn0 + i;
+    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
     uint32_t w = 0u;
-    bool keep = false;
-    if (p < n_work) {
-        w = lib_item_word(fb, n_split, p);
-        keep = (w & 0x80000000u) || (w >> 28) == 1u;
+    bool keep = false, heavy = false;
+    int q = 0;
+    if (p < n_work && (p >= dyn0 || fp.heavy_min)) {
+        w = lib_item_word(fp, fb, n_split, p);
+        heavy = (w & LIB_HEAVY) != 0u;
+        keep = heavy || (p >= dyn0 && ((w & 0x80000000u) || ((w >> 28) & 3u) == 1u));
+        q = (p >= dyn0 ? p - dyn0 : p) & (LIB_NQ - 1);
     }
-    const int lane = __lane_id(), q = i & (LIB_NQ - 1);   // (a wave's lanes cycle through the queues)
-    const uint64_t mine = __ballot(keep) & (0x0101010101010101ull << (lane & 7));
-    const int lead = mine ? __ffsll((unsigned long long)mine) - 1 : lane;
-    uint32_t base = 0u;
-    if (keep && lane == lead) base = atomicAdd(&rq[(LIB_NQ + q) * LIB_QSTRIDE], (uint32_t)__popcll(mine));
-    base = (uint32_t)__shfl((int)base, lead);
-    if (keep) fb.dynq[(size_t)q * fp.dyn_cap + base + lanes_below(mine)] = w;
+    const int lane = __lane_id();
+    for (int qq = 0; qq < LIB_NQ; ++qq)
+        for (int hv = 0; hv < 2; ++hv) {
+            const bool me = keep && q == qq && heavy == (hv == 1);
+            const uint64_t m = __ballot(me);
+            if (m == 0ull) continue;   // wave-uniform
+            const int lead = __ffsll((unsigned long long)m) - 1;
+            uint32_t base = 0u;
+            if (lane == lead) base = atomicAdd(&rq[((hv ? 2 : 1) * LIB_NQ + qq) * LIB_QSTRIDE], (uint32_t)__popcll(m));
+            base = (uint32_t)__shfl((int)base, lead);
+            if (me) fb.dynq[(size_t)(2 * qq + (hv ? 0 : 1)) * fp.dyn_cap + base + lanes_below(m)] = w;
+        }
 }
 
 __global__ __launch_bounds__(256) void k_lib_plan(LibFrameParams fp, LibBuffers fb) {
@@ -2379,14 +2396,23 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
     constexpr bool listed = !SHADOW;
     if (tid < S) {
         const int jj = (int)blockIdx.x + tid * G;
-        sh.sitem[tid] = jj < n_work ? lib_item_word(fb, n_split, jj) : 0xffffffffu;
+        sh.sitem[tid] = jj < n_work ? lib_item_word(fp, fb, n_split, jj) : 0xffffffffu;
     }
-    if (listed && tid < LIB_NQ) sh.qlen[tid] = rq[(LIB_NQ + tid) * LIB_QSTRIDE];
+    if (listed && tid < 2 * LIB_NQ) sh.qlen[tid] = rq[(LIB_NQ + tid) * LIB_QSTRIDE];   // light lengths, then heavy
     __syncthreads();
-    // queue q's end: its list length (camera pass) or its share of the positions
-    auto q_end = [&](int qq) -> int { return listed ? (int)sh.qlen[qq] : (n_work - dyn0 - qq + LIB_NQ - 1) / LIB_NQ; };
+    // queue q's end: its two list lengths (camera pass) or its share of the positions
+    auto q_end = [&](int qq) -> int {
+        return listed ? (int)(sh.qlen[LIB_NQ + qq] + sh.qlen[qq]) : (n_work - dyn0 - qq + LIB_NQ - 1) / LIB_NQ;
+    };
+    // ticket t of queue q (camera pass): the heavy list first, then the light one
+    auto q_item = [&](int qq, int t) -> uint32_t {
+        const int nh = (int)sh.qlen[LIB_NQ + qq];
+        return t < nh ? fb.dynq[(size_t)(2 * qq) * fp.dyn_cap + t] : fb.dynq[(size_t)(2 * qq + 1) * fp.dyn_cap + (t - nh)];
+    };
     int q = (int)(blockIdx.x & (LIB_NQ - 1)), tried = 0;
-    const bool dynamic = dyn0 < n_work;   // (then every static position is a work item)
+    // (dyn0 <= n_work always: every static position is a work item); the camera pass's heavy static
+    // items wait in the heavy lists, so its workgroups always go on to the tickets
+    const bool dynamic = listed || dyn0 < n_work;
     uint32_t tk = 0;
     for (int i = 0;; ++i) {   // block-uniform; one call site of the tile raster (its code is large)
         uint32_t w;
@@ -2407,7 +2433,7 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
                 sh.next[1] = q;
                 sh.next[2] = tried;
                 if (more) tk = atomicAdd(&rq[q * LIB_QSTRIDE], 1u);   // the next ticket, under this tile
-                sh.next[3] = !more ? 0 : listed ? (int)fb.dynq[(size_t)q * fp.dyn_cap + t] : (int)lib_item_word(fb, n_split, dyn0 + q + LIB_NQ * t);
+                sh.next[3] = !more ? 0 : listed ? (int)q_item(q, t) : (int)lib_item_word(fp, fb, n_split, dyn0 + q + LIB_NQ * t);
             }
             __syncthreads();   // (sh.next is rewritten only after a whole tile, past many barriers)
             if (!sh.next[0]) break;
@@ -2424,8 +2450,9 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
             parts = it.y >> 16;
         } else {
             rt = (int)(w & 0x0fffffffu);
-            busy = w >> 28;
+            busy = (w >> 28) & 3u;
             if (!SHADOW && busy == 2u) continue;   // rendered as parts (k_lib_plan)
+            if (i < S && (w & LIB_HEAVY)) continue;   // static, heavy: served first from the heavy lists
         }
         if (busy) {
             lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk, part, parts);

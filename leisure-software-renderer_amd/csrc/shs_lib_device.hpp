@@ -122,6 +122,8 @@ struct LibFrameParams {
                                      // entries (0: one work item per owned raster tile, no plan)
     int32_t raster_grid;             // k_lib_raster's workgroups (k_lib_dyn derives the same static share)
     int32_t static_div;              // k_lib_raster: n_work / (static_div * workgroups) static items per workgroup
+    uint32_t heavy_min;              // camera pass: a busy tile whose bin list holds >= this many entries is
+                                     // rendered from k_lib_dyn's heavy lists, first (0: no heavy lists)
     uint32_t dyn_cap;                // camera pass: entries per queue of LibBuffers::dynq
     ShardRegion reg;                 // count > 1 with reg.on: this rank's rectangle of bin tiles
 };
@@ -153,7 +155,8 @@ struct LibBuffers {
     const int32_t *dbase;            // draws[i].tri_base, compact (+ n_tris): the triangle -> draw search
     const int32_t *bdraw;            // per setup block: the draw of its first triangle
     uint32_t *rqueue;                // k_lib_raster ticket queues: 2 parities x LIB_NQW x LIB_QSTRIDE words
-    uint32_t *dynq;                  // camera pass: k_lib_dyn's work item words per queue (LIB_NQ x dyn_cap)
+    uint32_t *dynq;                  // camera pass: k_lib_dyn's work item words, per queue q a heavy (2q) and a
+                                     // light (2q + 1) list of dyn_cap entries
     const int32_t *rt_order;         // the owned raster tiles in processing order (n_owned_rt; XCD-coherent)
     unsigned long long *keys;        // camera pass: W*H winning (z, submission) keys, k_lib_raster -> k_lib_resolve
     uint32_t *blkcov;                // camera pass: per 16x4 block (4 per raster tile, rt * 4 + sub): keys written
@@ -174,8 +177,8 @@ constexpr int LIB_MAXK = 16;
 // k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket
 // counters a cache line apart (k_lib_setup zeroes the next frame's set).
 constexpr int LIB_NQ = 8, LIB_QSTRIDE = 32;
-// per parity: LIB_NQ ticket counters, then (camera pass) LIB_NQ k_lib_dyn list lengths
-constexpr int LIB_NQW = 2 * LIB_NQ;
+// per parity: LIB_NQ ticket counters, then (camera pass) LIB_NQ light and LIB_NQ heavy k_lib_dyn list lengths
+constexpr int LIB_NQW = 3 * LIB_NQ;
 
 // Library setup timeline slots: start, after the per-triangle work, after the deferred marks,
 // after the large-primitive marks (= end), large primitives, deferred-union width x height, after the
