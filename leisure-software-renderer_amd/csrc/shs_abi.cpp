@@ -360,7 +360,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.n_tris = n_tris; fp.n_draws = n_draws;
     fp.clear_rgba = (uint32_t)f.clear_color[0] | ((uint32_t)f.clear_color[1] << 8) | ((uint32_t)f.clear_color[2] << 16) |
                     ((uint32_t)f.clear_color[3] << 24);
-    fp.flags = (f.flags & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
+    fp.flags = (f.flags & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS | shs_dev::RF_SHARED_VARY)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ws.spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ws.frags.cap, 0xffffffffu);
@@ -386,6 +386,23 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (no_recs) {
         fp.flags |= shs_dev::RF_NO_RECS;
         if (ensure(ctx, ws.tdraw, nt_all)) return SHS_ERR_HIP;
+    }
+    // Shared varyings (RF_SHARED_VARY): every frame of the batch draws frame 0's meshes with Phong /
+    // Blinn-Phong shading and bitwise the same model matrices -- a static scene under a batch of camera
+    // poses -- so the corners' world positions and normals are computed and stored once for the batch.
+    // SHS_LEGACY_SHARE_VARY=0 turns it off (timing experiments).
+    static const bool share_env = [] { const char *e = std::getenv("SHS_LEGACY_SHARE_VARY"); return !e || std::atoi(e) != 0; }();
+    if (share_env && !no_recs && n_frames > 1) {
+        bool share = true;
+        for (int i = 0; i < n_draws && share; ++i) {
+            const shs_legacy_draw &d0 = ctx->last_draws[i];
+            share = d0.shading == SHS_SHADING_PHONG || d0.shading == SHS_SHADING_BLINN_PHONG;
+            for (int fr = 1; fr < n_frames && share; ++fr) {
+                const shs_legacy_draw &d = ctx->last_draws[(size_t)fr * n_draws + i];
+                share = d.mesh_id == d0.mesh_id && d.shading == d0.shading && std::memcmp(d.model, d0.model, sizeof d.model) == 0;
+            }
+        }
+        if (share) fp.flags |= shs_dev::RF_SHARED_VARY;
     }
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;

@@ -109,6 +109,13 @@ constexpr uint32_t RF_PER_PIXEL = 1u << 16;
 // quad of lanes per candidate, as k_setup).  Unbounded slivers (TRI_UNBOUNDED) still store their
 // record for k_ghost.
 constexpr uint32_t RF_NO_RECS = 1u << 17;
+// Varyings shared by the batch's frames (frame flags bit 18, set by the host): every frame's draws have
+// frame 0's meshes, Phong / Blinn-Phong shading and model matrices (a static scene seen from a batch of
+// camera poses), so each triangle's ShadeRec -- world positions and normals of its corners, which
+// depend on the model matrix alone -- is the same in every frame.  Frame 0's k_setup blocks store it
+// once, the other frames' skip the normals and the varyings, and every frame's winners read frame 0's
+// copy (frame_view).  The draw uniforms a winner shades with come from its TriRec's per-frame draw.
+constexpr uint32_t RF_SHARED_VARY = 1u << 18;
 
 // Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);
 // larger scenes read the device draw table.
@@ -201,7 +208,7 @@ __device__ __forceinline__ FrameBuffers frame_view(const FrameParams &fp, const 
     const size_t nt = (size_t)fp.n_tris, n_bt = (size_t)fp.tiles_x * fp.tiles_y;
     const size_t npx = (size_t)fp.W * fp.H, n_rt = (size_t)fp.tiles_x * fp.rtiles_y;
     v.recs += f * nt;
-    v.shade += f * nt;
+    if (!(fp.flags & RF_SHARED_VARY)) v.shade += f * nt;
     v.boxes += f * nt;
     if (v.tdraw) v.tdraw += f * nt;
     v.tile_count += f * n_bt;

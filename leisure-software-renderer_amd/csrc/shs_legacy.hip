@@ -584,15 +584,16 @@ __device__ __forceinline__ void quad_store_rec_at(TriRec *rec, const TriRec &r) 
 __device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, const TriRec &r) { quad_store_rec_at(&fb.recs[tri], r); }
 
 // Record, varyings and their stores for the quad's triangle; returns the flags and the bin box.
+// vary: this frame stores the varyings (false: RF_SHARED_VARY and not frame 0 -- frame 0's are read).
 __device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU &dr, int d,
-                                               int dbase, int tri, uint2 &gbox) {
+                                               int dbase, int tri, uint2 &gbox, bool vary) {
     const int q = __lane_id() & 3, qv = q < 3 ? q : 2;
     const int local = tri - dr.tri_base;
     const float *P = dr.pos + 9 * (size_t)local + 3 * qv;
     const float p3[3] = {P[0], P[1], P[2]};
     const bool recs = !(fp.flags & RF_NO_RECS);
     float n3[3] = {0.0f, 0.0f, 0.0f};
-    if (recs) {   // issued with the position loads (their latency overlaps the record's arithmetic)
+    if (recs && vary) {   // issued with the position loads (their latency overlaps the record's arithmetic)
         const float *Nn = dr.nrm + 9 * (size_t)local + 3 * qv;
         n3[0] = Nn[0]; n3[1] = Nn[1]; n3[2] = Nn[2];
     }
@@ -604,10 +605,12 @@ __device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const Fram
         if ((r.flags & (TRI_UNBOUNDED | TRI_CULLED)) == TRI_UNBOUNDED) quad_store_rec(fb, tri, r);
         if (q == 0) fb.tdraw[tri] = tdraw_word(d, r.flags);
     } else {
-        f3 a, nr;
-        corner_varyings(dr, p3, n3, a, nr);
         quad_store_rec(fb, tri, r);
-        quad_store_shade(fb, tri, dbase + d, dr.shading, a, nr);   // the draw-table index of the batch
+        if (vary) {
+            f3 a, nr;
+            corner_varyings(dr, p3, n3, a, nr);
+            quad_store_shade(fb, tri, dbase + d, dr.shading, a, nr);   // the draw-table index of the batch
+        }
     }
     if (q == 0) fb.boxes[tri] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
     gbox = make_uint2(r.gbx, r.gby);
@@ -628,6 +631,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     __syncthreads();
     QuadTri qt = quad_tri(draws, fp.n_draws, fp.n_tris, lb * 64 + (tid >> 2));
     const int tri = qt.tri;
+    const bool vary = !(fp.flags & RF_SHARED_VARY) || frame == 0;
     uint32_t flags = TRI_CULLED;
     int gx0 = 0, gx1 = -1, gy0 = 0, gy1 = -1;
     tl_mark(fb.timeline, blockIdx.x, 0);
@@ -635,9 +639,9 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
         uint2 gb;
         if (qt.uniform) {
             const int d = __builtin_amdgcn_readfirstlane(qt.draw);
-            flags = setup_quad(fp, fb, draws[d], d, dbase, tri, gb);
+            flags = setup_quad(fp, fb, draws[d], d, dbase, tri, gb, vary);
         } else {
-            flags = setup_quad(fp, fb, draws[qt.draw], qt.draw, dbase, tri, gb);
+            flags = setup_quad(fp, fb, draws[qt.draw], qt.draw, dbase, tri, gb, vary);
         }
         gx0 = lo16(gb.x); gx1 = hi16(gb.x); gy0 = lo16(gb.y); gy1 = hi16(gb.y);
     }
@@ -793,18 +797,33 @@ __global__ __launch_bounds__(256, BIN ? 8 : 1) void k_setup(FrameParams fp, Fram
 // records come from k_setup's stores (identical to the ghost waves' recomputation).
 constexpr int GHOST_LIST_BLOCKS = 512;
 
+// A wave's items are known up front: lane j loads the sliver entry of its j-th next item in one round
+// trip, and the next item's record is loaded while the current sliver's pixels are tested, so a
+// sliver costs its tests rather than two dependent memory round trips.
 __global__ __launch_bounds__(256) void k_ghost(FrameParams fp, FrameBuffers fb_all) {
     uint32_t *cnt = fb_all.counters + fp.parity * CSET;
     const int n = (int)min(cnt[C_SLIVER], (uint32_t)fp.n_tris * (uint32_t)fp.n_frames);
-    const int waves = (int)gridDim.x * 4, gw = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    const int waves = (int)gridDim.x * 4, gw = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = __lane_id();
     const int slices = n > 0 ? max(1, min(16, waves / n)) : 1;
-    for (int item = gw; item < n * slices; item += waves) {
-        const int s = item / slices, slice = item - s * slices;
-        const uint32_t e = fb_all.slivers[s];   // frame * n_tris + triangle
+    const int n_items = n * slices;
+    auto record = [&](uint32_t e) {   // e = frame * n_tris + triangle
         const uint32_t frame = e / (uint32_t)fp.n_tris, tri = e - frame * (uint32_t)fp.n_tris;
-        const FrameBuffers fb = frame_view(fp, fb_all, (int)frame);
-        const TriRec t = rec_from(reinterpret_cast<const float4 *>(&fb.recs[tri]));
-        sliver_pixels(fp, fb, cnt, t, tri, frame, slice, 64 * slices);
+        return rec_from(reinterpret_cast<const float4 *>(&frame_view(fp, fb_all, (int)frame).recs[tri]));
+    };
+    for (int base = gw; base < n_items; base += 64 * waves) {   // wave-uniform
+        const int mine = base + lane * waves;
+        const uint32_t my_e = mine < n_items ? fb_all.slivers[mine / slices] : 0u;
+        const int m = min(64, (n_items - base + waves - 1) / waves);
+        TriRec nxt = record((uint32_t)__shfl((int)my_e, 0));
+        for (int j = 0; j < m; ++j) {
+            const int item = base + j * waves;
+            const int s = item / slices, slice = item - s * slices;
+            const uint32_t e = (uint32_t)__shfl((int)my_e, j);
+            const uint32_t frame = e / (uint32_t)fp.n_tris, tri = e - frame * (uint32_t)fp.n_tris;
+            const TriRec t = nxt;
+            if (j + 1 < m) nxt = record((uint32_t)__shfl((int)my_e, j + 1));
+            sliver_pixels(fp, frame_view(fp, fb_all, (int)frame), cnt, t, tri, frame, slice, 64 * slices);
+        }
     }
 }
 
@@ -1302,7 +1321,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
             depth = (u * r.z0 + v * r.z1) + w * r.z2;
             if (!(fp.flags & DBG_SKIP_SHADE)) {
-                const float4 *du = sr.draw < LDS_DRAWS ? &sh.du[sr.draw * 4] : reinterpret_cast<const float4 *>(draws[sr.draw].light);
+                const int wd = dbase + r.draw;   // the frame's draw (ShadeRec::draw is frame 0's when shared)
+                const float4 *du = wd < LDS_DRAWS ? &sh.du[wd * 4] : reinterpret_cast<const float4 *>(draws[wd].light);
                 float pre[3];
                 shade_winner(du, sr, u, v, w, pre);
                 const uint32_t cr = (uint32_t)(uint8_t)pre[0], cg = (uint32_t)(uint8_t)pre[1], cb = (uint32_t)(uint8_t)pre[2];
@@ -1340,8 +1360,9 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                 bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
                 depth = (u * r.z0 + v * r.z1) + w * r.z2;
                 if (shade) {
-                    if (sr.draw < LDS_DRAWS) load_du(&sh.du[sr.draw * 4], du);
-                    else load_du(reinterpret_cast<const float4 *>(draws[sr.draw].light), du);
+                    const int wd = dbase + r.draw;   // the frame's draw (ShadeRec::draw is frame 0's when shared)
+                    if (wd < LDS_DRAWS) load_du(&sh.du[wd * 4], du);
+                    else load_du(reinterpret_cast<const float4 *>(draws[wd].light), du);
                     shading = sr.shading;
                     interp_varyings(sr, u, v, w, A, N);
                 }
