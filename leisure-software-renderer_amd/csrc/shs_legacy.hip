@@ -795,33 +795,43 @@ __global__ __launch_bounds__(256, BIN ? 8 : 1) void k_setup(FrameParams fp, Fram
 // The listed unbounded slivers' tile-clamp pixels: wave w takes items w, w + waves, ... of
 // (sliver, slice); each sliver is cut into enough slices that the grid's waves stay busy.  The
 // records come from k_setup's stores (identical to the ghost waves' recomputation).
-constexpr int GHOST_LIST_BLOCKS = 512;
+#ifndef SHS_GHOST_BLOCKS
+#define SHS_GHOST_BLOCKS 512
+#endif
+constexpr int GHOST_LIST_BLOCKS = SHS_GHOST_BLOCKS;
 
 // A wave's items are known up front: lane j loads the sliver entry of its j-th next item in one round
-// trip, and the next item's record is loaded while the current sliver's pixels are tested, so a
-// sliver costs its tests rather than two dependent memory round trips.
+// trip.
 __global__ __launch_bounds__(256) void k_ghost(FrameParams fp, FrameBuffers fb_all) {
     uint32_t *cnt = fb_all.counters + fp.parity * CSET;
     const int n = (int)min(cnt[C_SLIVER], (uint32_t)fp.n_tris * (uint32_t)fp.n_frames);
     const int waves = (int)gridDim.x * 4, gw = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = __lane_id();
     const int slices = n > 0 ? max(1, min(16, waves / n)) : 1;
     const int n_items = n * slices;
-    auto record = [&](uint32_t e) {   // e = frame * n_tris + triangle
+    // the sliver's record is wave-uniform: scalar loads through the constant address space (the records
+    // are read-only here), so it occupies SGPRs and the kernel's VGPRs stay few -- it runs beside the
+    // previous batch's raster, in the VGPRs the raster leaves free
+    typedef const __attribute__((address_space(4))) float ConstF;
+    auto record = [&](uint32_t e) {   // e = frame * n_tris + triangle (wave-uniform)
+        e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
         const uint32_t frame = e / (uint32_t)fp.n_tris, tri = e - frame * (uint32_t)fp.n_tris;
-        return rec_from(reinterpret_cast<const float4 *>(&frame_view(fp, fb_all, (int)frame).recs[tri]));
+        ConstF *src = (ConstF *)(fb_all.recs + (size_t)frame * fp.n_tris + tri);
+        TriRec r;
+        float *d = reinterpret_cast<float *>(&r);
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(TriRec) / 4); ++k) d[k] = src[k];
+        return r;
     };
     for (int base = gw; base < n_items; base += 64 * waves) {   // wave-uniform
         const int mine = base + lane * waves;
         const uint32_t my_e = mine < n_items ? fb_all.slivers[mine / slices] : 0u;
         const int m = min(64, (n_items - base + waves - 1) / waves);
-        TriRec nxt = record((uint32_t)__shfl((int)my_e, 0));
         for (int j = 0; j < m; ++j) {
             const int item = base + j * waves;
             const int s = item / slices, slice = item - s * slices;
-            const uint32_t e = (uint32_t)__shfl((int)my_e, j);
+            const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)my_e, j));
             const uint32_t frame = e / (uint32_t)fp.n_tris, tri = e - frame * (uint32_t)fp.n_tris;
-            const TriRec t = nxt;
-            if (j + 1 < m) nxt = record((uint32_t)__shfl((int)my_e, j + 1));
+            const TriRec t = record(e);
             sliver_pixels(fp, frame_view(fp, fb_all, (int)frame), cnt, t, tri, frame, slice, 64 * slices);
         }
     }
