@@ -360,7 +360,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.n_tris = n_tris; fp.n_draws = n_draws;
     fp.clear_rgba = (uint32_t)f.clear_color[0] | ((uint32_t)f.clear_color[1] << 8) | ((uint32_t)f.clear_color[2] << 16) |
                     ((uint32_t)f.clear_color[3] << 24);
-    fp.flags = (f.flags & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS | shs_dev::RF_SHARED_VARY)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
+    fp.flags = (f.flags & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS | shs_dev::RF_SHARED_VARY | shs_dev::RF_GHOST_INLINE)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ws.spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ws.frags.cap, 0xffffffffu);
@@ -413,7 +413,12 @@ static int enqueue_frame(shs_ctx *ctx) {
     // batches (C2: 0.282-0.285 vs 0.288-0.297 ms per 64-frame step).  SHS_GHOST_LIST=1 lists them in
     // scan mode too (timing experiments).
     fp.ghost_list = (fp.scan_mode && !ghost_list_env) ? 0u : 1u;
-    fp.ghost_blocks = fp.ghost_list ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
+    // Scan mode: each setup wave enumerates its own unbounded slivers (RF_GHOST_INLINE) instead of
+    // ghost blocks recomputing every triangle's record (C2: 976 ghost blocks per batch for ~17
+    // slivers per frame).  SHS_GHOST_INLINE=0: the ghost blocks (timing experiments).
+    static const bool ghost_inline_env = [] { const char *e = std::getenv("SHS_GHOST_INLINE"); return !e || std::atoi(e) != 0; }();
+    if (!fp.ghost_list && ghost_inline_env) fp.flags |= shs_dev::RF_GHOST_INLINE;
+    fp.ghost_blocks = (fp.ghost_list || (fp.flags & shs_dev::RF_GHOST_INLINE)) ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
     fp.clear_blocks = 0;
     fp.n_owned_rt = owned_bt * (shs_dev::TILE / shs_dev::RTH);
     fp.n_frames = n_frames;

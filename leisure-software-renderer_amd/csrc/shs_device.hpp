@@ -116,6 +116,10 @@ constexpr uint32_t RF_NO_RECS = 1u << 17;
 // once, the other frames' skip the normals and the varyings, and every frame's winners read frame 0's
 // copy (frame_view).  The draw uniforms a winner shades with come from its TriRec's per-frame draw.
 constexpr uint32_t RF_SHARED_VARY = 1u << 18;
+// Scan-mode batches without ghost waves (frame flags bit 19, set by the host): a setup wave that finds
+// unbounded slivers among its own triangles enumerates their tile-clamp pixels itself, from the
+// records it keeps in LDS, instead of ghost blocks recomputing every triangle's record.
+constexpr uint32_t RF_GHOST_INLINE = 1u << 19;
 
 // Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);
 // larger scenes read the device draw table.

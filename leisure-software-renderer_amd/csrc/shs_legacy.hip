@@ -363,6 +363,10 @@ struct GhostScratch {           // per-wave LDS
     float4 rec[6];
 };
 
+struct SliverRecs {             // per-wave LDS (RF_GHOST_INLINE): the records of the wave's 16 triangles' slivers
+    float4 rec[16 * 6];
+};
+
 // The quad's triangle index, draw and this lane's corner, with the wave-uniform draw fast path.
 struct QuadTri {
     int tri, draw, local;
@@ -585,8 +589,9 @@ __device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, 
 
 // Record, varyings and their stores for the quad's triangle; returns the flags and the bin box.
 // vary: this frame stores the varyings (false: RF_SHARED_VARY and not frame 0 -- frame 0's are read).
+// sliv: the wave's 16 record slots in LDS (RF_GHOST_INLINE), or nullptr.
 __device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU &dr, int d,
-                                               int dbase, int tri, uint2 &gbox, bool vary) {
+                                               int dbase, int tri, uint2 &gbox, bool vary, float4 *sliv) {
     const int q = __lane_id() & 3, qv = q < 3 ? q : 2;
     const int local = tri - dr.tri_base;
     const float *P = dr.pos + 9 * (size_t)local + 3 * qv;
@@ -613,6 +618,8 @@ __device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const Fram
         }
     }
     if (q == 0) fb.boxes[tri] = make_uint2(r.gbx, r.gby);   // culled: the empty box (0, -1)
+    if (sliv && (r.flags & (TRI_UNBOUNDED | TRI_CULLED)) == TRI_UNBOUNDED)   // quad-uniform
+        quad_store_rec_at(reinterpret_cast<TriRec *>(sliv + ((__lane_id() >> 2) & 15) * 6), r);
     gbox = make_uint2(r.gbx, r.gby);
     return r.flags;
 }
@@ -624,7 +631,8 @@ constexpr int SMALL_BT = 8;   // bin tiles a quad appends to by itself (2 per la
 // frame / lb: the batch frame and this block's index among the frame's setup blocks; draws = the
 // frame's draw slice (table entries dbase ..).
 __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, int dbase,
-                                            int frame, int lb, uint32_t *cnt, uint32_t (&s_stat)[4], NewBusy &nb) {
+                                            int frame, int lb, uint32_t *cnt, uint32_t (&s_stat)[4], NewBusy &nb,
+                                            float4 *sliv) {
     const int tid = threadIdx.x, lane = __lane_id(), q = lane & 3;
     if (tid < 4) s_stat[tid] = 0u;
     if (tid == 0) nb.n = 0u;
@@ -639,9 +647,9 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
         uint2 gb;
         if (qt.uniform) {
             const int d = __builtin_amdgcn_readfirstlane(qt.draw);
-            flags = setup_quad(fp, fb, draws[d], d, dbase, tri, gb, vary);
+            flags = setup_quad(fp, fb, draws[d], d, dbase, tri, gb, vary, sliv);
         } else {
-            flags = setup_quad(fp, fb, draws[qt.draw], qt.draw, dbase, tri, gb, vary);
+            flags = setup_quad(fp, fb, draws[qt.draw], qt.draw, dbase, tri, gb, vary, sliv);
         }
         gx0 = lo16(gb.x); gx1 = hi16(gb.x); gy0 = lo16(gb.y); gy1 = hi16(gb.y);
     }
@@ -742,12 +750,23 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     }
     __syncthreads();
     if (tid == 0) fb.blk_stat[frame * fp.setup_blocks + lb] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
+    if (sliv && !(fp.flags & DBG_SKIP_GHOST)) {   // RF_GHOST_INLINE: this wave's unbounded slivers, one at a time
+        uint64_t todo = m_unb;
+        while (todo) {
+            const int src = __ffsll((unsigned long long)todo) - 1;
+            todo &= todo - 1;
+            wave_lds_sync();   // the quads' record stores are complete
+            const TriRec t = rec_from(sliv + (src >> 2) * 6);
+            sliver_pixels(fp, fb, cnt, t, (uint32_t)__shfl(tri, src), (uint32_t)frame, 0, 64);
+        }
+    }
 }
 
 // One k_setup block b of the batch (setup or ghost role by its index in its frame); draw_tab = the
 // batch's draw table (kernel arguments or the device table).
 __device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuffers &fb_all, const DrawGPU *draw_tab, int b,
-                                           GhostScratch (&s_ghost)[4], uint32_t (&s_stat)[4], NewBusy &s_new) {
+                                           GhostScratch (&s_ghost)[4], uint32_t (&s_stat)[4], NewBusy &s_new,
+                                           SliverRecs (&s_sliv)[4]) {
     uint32_t *cnt = fb_all.counters + fp.parity * CSET;
     if (b == 0)   // the next batch's counter set (its previous user, batch k - 2, has finished)
         for (int i = (int)threadIdx.x; i < CSET; i += 256) fb_all.counters[(size_t)fp.zero_set * CSET + i] = 0u;
@@ -760,7 +779,8 @@ __device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuf
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     // (the counter set and the bin counts were zeroed on the setup stream before this launch)
     if (lb < fp.setup_blocks) {
-        setup_block(fp, fb, draws, dbase, frame, lb, cnt, s_stat, s_new);
+        setup_block(fp, fb, draws, dbase, frame, lb, cnt, s_stat, s_new,
+                    (fp.flags & RF_GHOST_INLINE) ? s_sliv[threadIdx.x >> 6].rec : nullptr);
     } else if (lb < fp.setup_blocks + fp.ghost_blocks) {
         const int wave = threadIdx.x >> 6;
         const int gw = (lb - fp.setup_blocks) * 4 + wave;
@@ -788,7 +808,8 @@ __global__ __launch_bounds__(256, BIN ? 8 : 1) void k_setup(FrameParams fp, Fram
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
     __shared__ NewBusy s_new;
-    setup_item(fp, fb_all, draw_table<KARG>(fb_all, ka), (int)blockIdx.x, s_ghost, s_stat, s_new);
+    __shared__ SliverRecs s_sliv[4];
+    setup_item(fp, fb_all, draw_table<KARG>(fb_all, ka), (int)blockIdx.x, s_ghost, s_stat, s_new, s_sliv);
 }
 
 // ---- k_ghost (ghost_list mode) -----------------------------------------------------------------
@@ -1568,6 +1589,7 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
 __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_pipe(FrameParams fp, FrameBuffers fb, FrameParams fpS,
                                                                        FrameBuffers fbS) {
     __shared__ RasterShared sh;
+    __shared__ SliverRecs s_sliv[4];
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
     __shared__ NewBusy s_new;
@@ -1598,7 +1620,7 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_pipe(FramePara
         const uint32_t k_lo = (uint32_t)(((uint64_t)item * n_setup) / n_items);
         const uint32_t k_hi = (uint32_t)(((uint64_t)(item + 1) * n_setup) / n_items);
         if (k_hi > k_lo) {
-            setup_item(fpS, fbS, fbS.draws, (int)k_lo, s_ghost, s_stat, s_new);
+            setup_item(fpS, fbS, fbS.draws, (int)k_lo, s_ghost, s_stat, s_new, s_sliv);
         } else {
             const uint32_t j = item - k_lo;                   // raster item j of n_raster (k_raster's order)
             const uint32_t s_lo = (uint32_t)(((uint64_t)j * n_strips) / n_raster);
