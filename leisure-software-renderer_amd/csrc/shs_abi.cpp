@@ -408,15 +408,14 @@ static int enqueue_frame(shs_ctx *ctx) {
     const int n_groups = (n_tris + 15) / 16;
     fp.setup_blocks = setup_blocks;
     // Binned (large) scenes list their unbounded slivers in k_setup and enumerate them in k_ghost: ghost
-    // waves would recompute every triangle's record (C3: ~1/3 of k_setup's time).  Scan-mode frames and
-    // batches keep the ghost waves inside k_setup: one launch fewer on the latency path between two
-    // batches (C2: 0.282-0.285 vs 0.288-0.297 ms per 64-frame step).  SHS_GHOST_LIST=1 lists them in
-    // scan mode too (timing experiments).
-    fp.ghost_list = (fp.scan_mode && !ghost_list_env) ? 0u : 1u;
-    // Scan mode: each setup wave enumerates its own unbounded slivers (RF_GHOST_INLINE) instead of
-    // ghost blocks recomputing every triangle's record (C2: 976 ghost blocks per batch for ~17
-    // slivers per frame).  SHS_GHOST_INLINE=0: the ghost blocks (timing experiments).
+    // waves would recompute every triangle's record (C3: ~1/3 of k_setup's time).  (Not inline as below:
+    // a bin-mode tile's first appender marks its rows busy with plain stores, which a sliver fragment's
+    // busy mark in the same kernel would race.)  Scan-mode setup waves enumerate their own unbounded
+    // slivers (RF_GHOST_INLINE) instead of ghost blocks recomputing every triangle's record (C2: 976
+    // ghost blocks per batch for ~17 slivers per frame).  SHS_GHOST_INLINE=0 restores the ghost blocks,
+    // SHS_GHOST_LIST=1 lists scan-mode slivers for k_ghost (timing experiments).
     static const bool ghost_inline_env = [] { const char *e = std::getenv("SHS_GHOST_INLINE"); return !e || std::atoi(e) != 0; }();
+    fp.ghost_list = (fp.scan_mode && !ghost_list_env) ? 0u : 1u;
     if (!fp.ghost_list && ghost_inline_env) fp.flags |= shs_dev::RF_GHOST_INLINE;
     fp.ghost_blocks = (fp.ghost_list || (fp.flags & shs_dev::RF_GHOST_INLINE)) ? 0 : (n_groups * (int)fp.ghost_slices + 3) / 4;
     fp.clear_blocks = 0;
