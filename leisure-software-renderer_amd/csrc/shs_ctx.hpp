@@ -222,7 +222,7 @@ struct shs_ctx {
     DevBuf<uint64_t> lib_timeline;        // SHS_OPT_TIMELINE, camera pass raster
     DevBuf<uint64_t> lib_stimeline;       // SHS_OPT_TIMELINE, camera pass setup
     DevBuf<float4> lib_hdr;
-    DevBuf<unsigned long long> lib_keys;  // camera pass winner keys (k_lib_raster -> k_lib_resolve)
+    DevBuf<uint32_t> lib_keys;            // camera pass winners (k_lib_raster -> k_lib_resolve, LibBuffers::keys)
     DevBuf<uint32_t> lib_blkcov;          // ... and per 16x4 block whether it holds any
     // lib_blkcov is all zero between camera passes (k_lib_resolve resets the flags it read; the raster sets
     // only its busy tiles'): zeroed once per allocation and frame size

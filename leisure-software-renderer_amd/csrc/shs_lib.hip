@@ -1223,6 +1223,21 @@ __device__ __forceinline__ unsigned long long lib_key(const LibFrameParams &fp, 
     return (shadow || (fp.flags & LF_DEPTH)) ? z_key(z01, seq) : (unsigned long long)(0xffffffffu - seq);
 }
 
+// The camera pass hands each pixel's winner to k_lib_resolve as 4 B: lib_resolve reads only the key's
+// low word (the submission sequence, painter's order inverted) and whether it is empty, and recomputes
+// z from the record.  Word = sequence + 1 (sequences are < 2^31), 0 = no winner.
+__device__ __forceinline__ uint32_t lib_winner_word(const LibFrameParams &fp, unsigned long long key) {
+    if (key == KEY_EMPTY) return 0u;
+    const uint32_t seq = (fp.flags & LF_DEPTH) ? (uint32_t)key : 0xffffffffu - (uint32_t)key;
+    return seq + 1u;
+}
+// The key lib_resolve decodes for a word: its low word and emptiness are the original key's.
+__device__ __forceinline__ unsigned long long lib_winner_key(const LibFrameParams &fp, uint32_t w) {
+    if (w == 0u) return KEY_EMPTY;
+    const uint32_t seq = w - 1u;
+    return (fp.flags & LF_DEPTH) ? (unsigned long long)seq : (unsigned long long)(0xffffffffu - seq);
+}
+
 // (2R+1)^2 PCF taps with every fetch issued before the first compare (one memory round trip).
 template <int R>
 __device__ __forceinline__ float pcf_fixed(const LibFrameParams &fp, const LibBuffers &fb, int cx, int cy, int step, float z_test) {
@@ -2247,7 +2262,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
         const bool any = __ballot(covered) != 0ull;
         if (mine) {
-            if (any && px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = key;
+            if (any && px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = lib_winner_word(fp, key);
             if (lane == 0) fb.blkcov[(size_t)rt * 4 + wave] = any ? 1u : 0u;
         }
     }
@@ -2517,7 +2532,7 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
         const bool any = fb.blkcov[(size_t)rt * 4 + sub] != 0u;   // wave-uniform
         if (sub == 0 && lane == 0) fb.busy[rt] = 0u;   // the raster's busy / split flag, for the next pass
         if (any && lane == 0) fb.blkcov[(size_t)rt * 4 + sub] = 0u;   // the next pass's raster sets only its busy tiles' flags
-        const unsigned long long key = inb && any ? fb.keys[(size_t)py * fp.W + px] : KEY_EMPTY;
+        const unsigned long long key = lib_winner_key(fp, inb && any ? fb.keys[(size_t)py * fp.W + px] : 0u);
         LtWave lw;
 #ifdef SHS_RESOLVE_NO_LTWAVE
         if (false) {

@@ -158,7 +158,8 @@ struct LibBuffers {
     uint32_t *dynq;                  // camera pass: k_lib_dyn's work item words, per queue q a heavy (2q) and a
                                      // light (2q + 1) list of dyn_cap entries
     const int32_t *rt_order;         // the owned raster tiles in processing order (n_owned_rt; XCD-coherent)
-    unsigned long long *keys;        // camera pass: W*H winning (z, submission) keys, k_lib_raster -> k_lib_resolve
+    uint32_t *keys;                  // camera pass: W*H winners, k_lib_raster -> k_lib_resolve: the winning key's
+                                     // submission sequence + 1 (0: no winner; the resolve recomputes z)
     uint32_t *blkcov;                // camera pass: per 16x4 block (4 per raster tile, rt * 4 + sub): keys written
     // fused PassTonemap (shs_lib_fuse_tonemap): k_lib_resolve also writes the tonemapped bytes
     const float *tm_thr;             // the 256 byte thresholds (shs_post_internal.hpp), null: not fused
