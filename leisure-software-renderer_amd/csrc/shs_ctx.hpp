@@ -148,7 +148,8 @@ struct shs_ctx {
         DevBuf<shs_dev::LibRec> recs;
         DevBuf<shs_dev::LibShade> shade;
         DevBuf<uint2> boxes;
-        DevBuf<uint32_t> xbase, zord, tile_count, bins, counters, busy, clipq, bigpre;
+        DevBuf<uint32_t> xbase, zord, tile_count, counters, busy, clipq, bigpre;
+        DevBuf<uint4> bins;                                // per bin tile, bin_cap entries (slot, box, depth bound)
         DevBuf<uint4> bigq;
         DevBuf<uint32_t> rqueue;
         bool tm_fused = false;                             // camera pass: the fused tonemap of tm_desc

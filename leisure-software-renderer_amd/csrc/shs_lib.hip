@@ -279,13 +279,16 @@ __device__ __forceinline__ int clip_frustum_group(LVert &v, int li, int seg, int
     return n;
 }
 
+// A bin entry carries the primitive's box and depth bound beside its slot (e = slot, box x, box y,
+// zord), so the raster's gather reads its candidates' boxes and bounds from the tile's contiguous list
+// instead of one scattered 8-B and 4-B load per candidate.  (Spilled entries keep the slot only.)
 __device__ __forceinline__ void lib_append_bin(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int t,
-                                               uint32_t pos, uint32_t id) {
+                                               uint32_t pos, uint4 e) {
     if (pos < fp.bin_cap) {
-        fb.bins[(size_t)t * fp.bin_cap + pos] = id;
+        fb.bins[(size_t)t * fp.bin_cap + pos] = e;
     } else {
         const uint32_t sp = atomicAdd(&cnt[LC_SPILL], 1u);
-        if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t, id);
+        if (sp < fp.spill_cap) fb.spill[sp] = make_uint2((uint32_t)t, e.x);
         else raise_overflow(&cnt[LC_OVERFLOW], LOV_SPILL, fb.ov_host);
     }
 }
@@ -293,7 +296,7 @@ __device__ __forceinline__ void lib_append_bin(const LibFrameParams &fp, const L
 // Busy marks on the owned raster tiles of [x0,x1] x [y0,y1] and (bin mode) per-bin-tile appends,
 // tiles k0, k0 + dk, ... of the box (one thread: k0 = 0, dk = 1; a whole block: k0 = tid, dk = 256).
 __device__ __forceinline__ void lib_mark_range(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
-                               uint32_t slot, int k0, int dk) {
+                               uint32_t slot, int k0, int dk, uint32_t zk) {
     const bool sharded = fp.count > 1;
     {
         const int rx0 = x0 / LIB_RTW, ry0 = y0 / LIB_RTH, nx = x1 / LIB_RTW - rx0 + 1, n = nx * (y1 / LIB_RTH - ry0 + 1);
@@ -309,7 +312,7 @@ __device__ __forceinline__ void lib_mark_range(const LibFrameParams &fp, const L
         const int bx = bx0 + k % nx, by = by0 + k / nx;
         if (sharded && !lib_owned(fp, bx, by)) continue;
         const int t = by * fp.tiles_x + bx;
-        lib_append_bin(fp, fb, cnt, t, atomicAdd(&tcount[t], 1u), slot);
+        lib_append_bin(fp, fb, cnt, t, atomicAdd(&tcount[t], 1u), make_uint4(slot, pack16(x0, x1), pack16(y0, y1), zk));
     }
 }
 
@@ -345,7 +348,7 @@ constexpr int AGG_BINS = 256;             // union capacity in bin tiles (else t
 #endif
 constexpr int DEFER_BT = SHS_DEFER_BT;    // deferred primitives span at most DEFER_BT x DEFER_BT bin tiles
 struct Pend {
-    uint32_t slot = 0;
+    uint32_t slot = 0, zk = 0;
     int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
     bool valid = false;
 };
@@ -360,20 +363,20 @@ struct SetupShared {
 };
 
 __device__ __forceinline__ void lib_mark(const LibFrameParams &fp, const LibBuffers &fb, uint32_t *cnt, int x0, int x1, int y0, int y1,
-                         uint32_t slot, SetupShared &ss, Pend &pend) {
+                         uint32_t slot, SetupShared &ss, Pend &pend, uint32_t zk) {
     if (!pend.valid && (x1 / TILE - x0 / TILE) < DEFER_BT && (y1 / TILE - y0 / TILE) < DEFER_BT) {
-        pend.slot = slot; pend.x0 = x0; pend.x1 = x1; pend.y0 = y0; pend.y1 = y1; pend.valid = true;
+        pend.slot = slot; pend.zk = zk; pend.x0 = x0; pend.x1 = x1; pend.y0 = y0; pend.y1 = y1; pend.valid = true;
         return;
     }
     const int n_rt = (x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1);
     if (n_rt > SMALL_MARK) {
         const uint32_t q = atomicAdd(&ss.nbig, 1u);
         if (q < BIG_CAP) {
-            ss.big[q] = make_uint4(slot, pack16(x0, x1), pack16(y0, y1), 0u);
+            ss.big[q] = make_uint4(slot, pack16(x0, x1), pack16(y0, y1), zk);
             return;
         }
     }
-    lib_mark_range(fp, fb, cnt, x0, x1, y0, y1, slot, 0, 1);   // small, or the queue is full
+    lib_mark_range(fp, fb, cnt, x0, x1, y0, y1, slot, 0, 1, zk);   // small, or the queue is full
 }
 
 __device__ __forceinline__ void store_box(const LibBuffers &fb, uint32_t slot, int x0, int x1, int y0, int y1) {
@@ -467,7 +470,8 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     r.seq = seq;
     r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
     if (!(fp.exp_flags & 4u)) fb.recs[slot] = r;
-    fb.zord[slot] = (fp.flags & LF_DEPTH) ? lib_zmin_ord<false>(fp, r) : 0u;
+    const uint32_t zk = (fp.flags & LF_DEPTH) ? lib_zmin_ord<false>(fp, r) : 0u;
+    fb.zord[slot] = zk;
     LibShade s;
     const float iw[3] = {iw0, iw1, iw2};
 #pragma unroll
@@ -487,16 +491,16 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     if (DIRECT) {
         const int n_rt = (x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1);
         if (n_rt > SMALL_MARK) {
-            const uint4 e = make_uint4(slot, pack16(x0, x1), pack16(y0, y1), 0u);
+            const uint4 e = make_uint4(slot, pack16(x0, x1), pack16(y0, y1), zk);
             uint32_t nb;
             const uint2 at = bigq_reserve(cnt, 1u, big_tasks(fp, e, nb));
             fb.bigq[at.x] = e;
             fb.bigpre[at.x] = at.y;
         } else {
-            lib_mark_range(fp, fb, cnt, x0, x1, y0, y1, slot, 0, 1);
+            lib_mark_range(fp, fb, cnt, x0, x1, y0, y1, slot, 0, 1, zk);
         }
     } else {
-        lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot, ss, pend);
+        lib_mark(fp, fb, cnt, x0, x1, y0, y1, slot, ss, pend, zk);
     }
 }
 
@@ -627,9 +631,10 @@ __device__ __forceinline__ void setup_shadow_tri(const LibFrameParams &fp, const
     r.seq = (uint32_t)tri * 16u;
     r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
     fb.recs[tri] = r;
-    fb.zord[tri] = lib_zmin_ord<true>(fp, r);
+    const uint32_t zk = lib_zmin_ord<true>(fp, r);
+    fb.zord[tri] = zk;
     store_box(fb, (uint32_t)tri, x0, x1, y0, y1);
-    lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri, ss, pend);
+    lib_mark(fp, fb, cnt, x0, x1, y0, y1, (uint32_t)tri, ss, pend, zk);
 }
 
 __device__ __forceinline__ void setup_shared_init(SetupShared &ss, int tid) {
@@ -670,7 +675,7 @@ __device__ int setup_deferred(const LibFrameParams &fp, const LibBuffers &fb, ui
     uint32_t pos[DEFER_BT][DEFER_BT] = {};
     if (pend.valid) {
         if (!agg) {
-            lib_mark_range(fp, fb, cnt, pend.x0, pend.x1, pend.y0, pend.y1, pend.slot, 0, 1);
+            lib_mark_range(fp, fb, cnt, pend.x0, pend.x1, pend.y0, pend.y1, pend.slot, 0, 1, pend.zk);
         } else {
             for (int ry = pend.y0 / LIB_RTH; ry <= pend.y1 / LIB_RTH; ++ry) {
                 const int by = ry / RPB;
@@ -709,7 +714,8 @@ __device__ int setup_deferred(const LibFrameParams &fp, const LibBuffers &fb, ui
                 for (int i = 0; i < DEFER_BT; ++i)
                     if (bx0 + i <= bx1 && by0 + j <= by1 && (!sharded || lib_owned(fp, bx0 + i, by0 + j))) {
                         const int u = (by0 + j - uby0) * uw + (bx0 + i - ubx0);
-                        lib_append_bin(fp, fb, cnt, (by0 + j) * fp.tiles_x + bx0 + i, ss.bcnt[u] + pos[j][i], pend.slot);
+                        lib_append_bin(fp, fb, cnt, (by0 + j) * fp.tiles_x + bx0 + i, ss.bcnt[u] + pos[j][i],
+                                       make_uint4(pend.slot, pack16(pend.x0, pend.x1), pack16(pend.y0, pend.y1), pend.zk));
                     }
         }
     }
@@ -1178,7 +1184,7 @@ __global__ __launch_bounds__(256) void k_lib_bigmark(LibFrameParams fp, LibBuffe
                 const int cx = x0 / TILE + kb % nx, cy = y0 / TILE + kb / nx;
                 if (!sharded || lib_owned(fp, cx, cy)) {
                     const int bt = cy * fp.tiles_x + cx;
-                    lib_append_bin(fp, fb, cnt, bt, atomicAdd(&tcount[bt], 1u), e.x);
+                    lib_append_bin(fp, fb, cnt, bt, atomicAdd(&tcount[bt], 1u), e);
                 }
             }
         }
@@ -1841,7 +1847,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         n_items = n_bin + n_spill;
         if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
     }
-    const uint32_t *bin = fb.bins + (size_t)bt * fp.bin_cap;
+    const uint4 *bin = fb.bins + (size_t)bt * fp.bin_cap;
 
     for (uint32_t base = 0; base < n_items; base += LIB_CAND) {
         __syncthreads();
@@ -1855,26 +1861,35 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         uint32_t ids[NG], zk[NG];
         uint2 bx[NG];
         bool hit[NG];
+        if (fp.scan_mode) {
 #pragma unroll
-        for (int k = 0; k < NG; ++k) {
-            const uint32_t item = base + tid + 256u * k;
-            uint32_t id = 0xffffffffu;
-            if (item < n_items) {
-                if (fp.scan_mode) {
-                    id = item;
-                } else if (item < n_bin) {
-                    id = bin[item];
-                } else {
-                    const uint2 e = fb.spill[item - n_bin];
-                    if ((int)e.x == bt) id = e.y;
-                }
+            for (int k = 0; k < NG; ++k) {
+                const uint32_t item = base + tid + 256u * k;
+                ids[k] = item < n_items ? item : 0xffffffffu;
             }
-            ids[k] = id;
-        }
 #pragma unroll
-        for (int k = 0; k < NG; ++k) {
-            bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
-            zk[k] = hiz && ids[k] != 0xffffffffu ? fb.zord[ids[k]] : 0u;
+            for (int k = 0; k < NG; ++k) {
+                bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
+                zk[k] = hiz && ids[k] != 0xffffffffu ? fb.zord[ids[k]] : 0u;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                const uint32_t item = base + tid + 256u * k;
+                uint4 e = make_uint4(0xffffffffu, 0u, 0u, 0u);
+                if (item < n_bin) {   // the entry carries the box and the depth bound
+                    e = bin[item];
+                } else if (item < n_items) {   // spilled entries hold the slot only (rare)
+                    const uint2 sp = fb.spill[item - n_bin];
+                    if ((int)sp.x == bt) {
+                        const uint2 b = fb.boxes[sp.y];
+                        e = make_uint4(sp.y, b.x, b.y, fb.zord[sp.y]);
+                    }
+                }
+                ids[k] = e.x;
+                bx[k] = e.x != 0xffffffffu ? make_uint2(e.y, e.z) : make_uint2(0u, 0u);
+                zk[k] = hiz && e.x != 0xffffffffu ? e.w : 0u;
+            }
         }
         uint32_t zlo = 0xffffffffu, zhi = 0u, nhit = 0u;
 #pragma unroll

@@ -135,7 +135,8 @@ struct LibBuffers {
     uint2 *boxes;                    // per slot: packed pixel bbox, empty (0,-1) when not rasterised
     uint32_t *zord;                  // per slot: orderable bits of a lower bound of its depth (front-to-back sort key)
     uint32_t *xbase;                 // per input triangle: slot of its fan triangle 1
-    uint32_t *tile_count, *bins;
+    uint32_t *tile_count;
+    uint4 *bins;                     // per bin tile: bin_cap entries (slot, box x, box y, depth bound zord)
     uint2 *spill;
     uint32_t *counters;
     uint32_t *busy;                  // per 32x8 raster tile
