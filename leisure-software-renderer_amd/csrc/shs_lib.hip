@@ -1276,6 +1276,25 @@ __device__ float shadow_visibility(const LibFrameParams &fp, const LibBuffers &f
         return (z_test <= z_ref) ? 1.0f : 0.0f;
     }
     const int step = max(1, (int)roundf(dr.shp[3]));
+    if (rad == 2 && step == 1 && cx >= 2 && cx + 2 < fp.sm_w && cy >= 2 && cy + 2 < fp.sm_h) {
+        // the reference default (5x5, step 1) away from the map's edges: each row's five texels as one
+        // dword-aligned 16-B load and one 4-B load (10 loads instead of 25), compared in the same order
+        typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+        f4u q[5];
+        float e[5];
+#pragma unroll
+        for (int oy = 0; oy < 5; ++oy) {
+            const float *p = fb.shadow_map + (size_t)(cy - 2 + oy) * fp.sm_w + (cx - 2);
+            q[oy] = *reinterpret_cast<const f4u *>(p);
+            e[oy] = p[4];
+        }
+        int lit = 0;
+#pragma unroll
+        for (int oy = 0; oy < 5; ++oy)
+            lit += ((z_test <= q[oy].x) ? 1 : 0) + ((z_test <= q[oy].y) ? 1 : 0) + ((z_test <= q[oy].z) ? 1 : 0) +
+                   ((z_test <= q[oy].w) ? 1 : 0) + ((z_test <= e[oy]) ? 1 : 0);
+        return (float)lit / 25.0f;
+    }
     if (rad == 1) return pcf_fixed<1>(fp, fb, cx, cy, step, z_test);
     if (rad == 2) return pcf_fixed<2>(fp, fb, cx, cy, step, z_test);   // the reference default (5x5)
     int count = 0, lit = 0;
