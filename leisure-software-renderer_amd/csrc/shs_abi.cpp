@@ -323,6 +323,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     shs_dev::KArgDraws ka;
     std::memset(&ka, 0, sizeof ka);
     int32_t base = 0;
+    const int32_t *bdraw = nullptr;   // FrameBuffers::bdraw
     if (n_draws_all <= shs_dev::KARG_DRAWS) {
         for (int i = 0; i < n_draws_all; ++i) {
             if (i % std::max(n_draws, 1) == 0) base = 0;
@@ -331,11 +332,19 @@ static int enqueue_frame(shs_ctx *ctx) {
             base += ctx->meshes[d.mesh_id].n_tris;
         }
     } else {
-        if (ensure(ctx, ws.draws, n_draws_all)) return SHS_ERR_HIP;
-        if ((size_t)n_draws_all > ws.h_cap) {
+        // Every frame with frame 0's draw layout (the same mesh per draw index): the table travels with
+        // one int per setup block appended, the frame-local draw of the block's first triangle
+        // (FrameBuffers::bdraw), so k_setup finds a triangle's draw with one tri_base load.
+        bool same_layout = n_draws > 1;
+        for (int i = n_draws; i < n_draws_all && same_layout; ++i)
+            same_layout = ctx->last_draws[i].mesh_id == ctx->last_draws[i % n_draws].mesh_id;
+        const size_t n_extra = same_layout ? ((size_t)setup_blocks * sizeof(int32_t) + sizeof(DrawGPU) - 1) / sizeof(DrawGPU) : 0;
+        const size_t n_tab = (size_t)n_draws_all + n_extra;
+        if (ensure(ctx, ws.draws, n_tab)) return SHS_ERR_HIP;
+        if (n_tab > ws.h_cap) {
             if (ws.h_draws) HIP_TRY(ctx, hipHostFree(ws.h_draws));
             ws.h_draws = nullptr;
-            const size_t cap = std::max<size_t>(n_draws_all, 64);
+            const size_t cap = std::max<size_t>(n_tab, 64);
             HIP_TRY(ctx, hipHostMalloc(reinterpret_cast<void **>(&ws.h_draws), cap * sizeof(DrawGPU)));
             ws.h_cap = cap;
         }
@@ -345,7 +354,15 @@ static int enqueue_frame(shs_ctx *ctx) {
             build_draw(d, ctx->meshes[d.mesh_id], base, ws.h_draws[i]);
             base += ctx->meshes[d.mesh_id].n_tris;
         }
-        HIP_TRY(ctx, hipMemcpyAsync(ws.draws.p, ws.h_draws, n_draws_all * sizeof(DrawGPU), hipMemcpyHostToDevice, sst));
+        if (same_layout) {
+            int32_t *bd = reinterpret_cast<int32_t *>(ws.h_draws + n_draws_all);
+            for (int b = 0, d = 0; b < setup_blocks; ++b) {
+                while (d + 1 < n_draws && ws.h_draws[d + 1].tri_base <= b * 64) ++d;
+                bd[b] = d;
+            }
+            bdraw = reinterpret_cast<const int32_t *>(ws.draws.p + n_draws_all);
+        }
+        HIP_TRY(ctx, hipMemcpyAsync(ws.draws.p, ws.h_draws, n_tab * sizeof(DrawGPU), hipMemcpyHostToDevice, sst));
     }
 
     FrameParams fp;
@@ -446,7 +463,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     }
 
     FrameBuffers fb;
-    fb.draws = ws.draws.p; fb.recs = ws.recs.p; fb.shade = ws.shade.p; fb.tile_count = ws.tile_count.p; fb.bins = ws.bins.p;
+    fb.draws = ws.draws.p; fb.bdraw = bdraw; fb.recs = ws.recs.p; fb.shade = ws.shade.p; fb.tile_count = ws.tile_count.p; fb.bins = ws.bins.p;
     fb.spill = ws.spill.p; fb.frags = ws.frags.p; fb.counters = ctx->counters.p;
     fb.slivers = ws.slivers.p;
     fb.busy = ws.busy.p;

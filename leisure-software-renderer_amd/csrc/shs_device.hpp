@@ -172,6 +172,8 @@ struct FrameParams {
 // the others are shared by the batch.
 struct FrameBuffers {
     const DrawGPU *draws;            // device draw table (n_frames * n_draws > KARG_DRAWS)
+    const int32_t *bdraw;            // per setup block: the frame-local draw of its first triangle when
+                                     // every frame has the same draw layout (device table only), or null
     TriRec *recs;                    // per frame: n_tris
     ShadeRec *shade;                 // per frame: n_tris
     uint32_t *tile_count;            // per frame: n_bin_tiles counts (zeroed before each launch)

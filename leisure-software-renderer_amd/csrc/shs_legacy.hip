@@ -367,6 +367,16 @@ struct SliverRecs {             // per-wave LDS (RF_GHOST_INLINE): the records o
     float4 rec[16 * 6];
 };
 
+// The draw of triangle gid from its setup block's first draw d0 (FrameBuffers::bdraw): a block of 64
+// triangles rarely crosses a draw boundary, so this is one tri_base load instead of a binary search.
+__device__ __forceinline__ int wave_draw_from(const DrawGPU *draws, int n_draws, int gid, bool valid, int d0, bool &uniform) {
+    int d = d0;
+    if (valid)
+        while (d + 1 < n_draws && draws[d + 1].tri_base <= gid) ++d;
+    uniform = __ballot(valid && d != d0) == 0;
+    return d;
+}
+
 // The quad's triangle index, draw and this lane's corner, with the wave-uniform draw fast path.
 struct QuadTri {
     int tri, draw, local;
@@ -637,7 +647,14 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     if (tid < 4) s_stat[tid] = 0u;
     if (tid == 0) nb.n = 0u;
     __syncthreads();
-    QuadTri qt = quad_tri(draws, fp.n_draws, fp.n_tris, lb * 64 + (tid >> 2));
+    QuadTri qt;
+    if (fb.bdraw) {
+        qt.tri = lb * 64 + (tid >> 2);
+        qt.valid = qt.tri < fp.n_tris;
+        qt.draw = wave_draw_from(draws, fp.n_draws, qt.tri, qt.valid, fb.bdraw[lb], qt.uniform);
+    } else {
+        qt = quad_tri(draws, fp.n_draws, fp.n_tris, lb * 64 + (tid >> 2));
+    }
     const int tri = qt.tri;
     const bool vary = !(fp.flags & RF_SHARED_VARY) || frame == 0;
     uint32_t flags = TRI_CULLED;
