@@ -289,7 +289,7 @@ static int enqueue_frame(shs_ctx *ctx) {
         ensure(ctx, ws.slivers, nt_all))
         return SHS_ERR_HIP;
     const size_t n_bt_all = (size_t)n_tiles * n_frames;
-    if (ensure(ctx, ws.tile_count, n_bt_all) || ensure(ctx, ws.busy_list, (size_t)n_rt * n_frames)) return SHS_ERR_HIP;
+    if (ensure(ctx, ws.tile_count, n_bt_all) || ensure(ctx, ws.busy_list, std::max((size_t)n_rt, (size_t)n_tiles * (shs_dev::TILE / shs_dev::RTH)) * n_frames)) return SHS_ERR_HIP;
     // busy flags hold the epoch of the batch that marked them: reset only when the buffer is new or the
     // tile geometry / shard / batch size changes
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32) ^ ((uint64_t)f.shard_rank << 16) ^
@@ -377,7 +377,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.n_tris = n_tris; fp.n_draws = n_draws;
     fp.clear_rgba = (uint32_t)f.clear_color[0] | ((uint32_t)f.clear_color[1] << 8) | ((uint32_t)f.clear_color[2] << 16) |
                     ((uint32_t)f.clear_color[3] << 24);
-    fp.flags = (f.flags & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS | shs_dev::RF_SHARED_VARY | shs_dev::RF_GHOST_INLINE)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
+    fp.flags = (f.flags & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS | shs_dev::RF_SHARED_VARY | shs_dev::RF_GHOST_INLINE | shs_dev::RF_XCD_ROWS)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ws.spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ws.frags.cap, 0xffffffffu);
@@ -421,6 +421,10 @@ static int enqueue_frame(shs_ctx *ctx) {
         }
         if (share) fp.flags |= shs_dev::RF_SHARED_VARY;
     }
+    // Bin-mode row groups dealt to one XCD (RF_XCD_ROWS): SHS_LEGACY_XCD_ROWS=0 turns it off (timing
+    // experiments).
+    static const bool xcd_rows_env = [] { const char *e = std::getenv("SHS_LEGACY_XCD_ROWS"); return !e || std::atoi(e) != 0; }();
+    if (!fp.scan_mode && xcd_rows_env) fp.flags |= shs_dev::RF_XCD_ROWS;
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;
     fp.setup_blocks = setup_blocks;

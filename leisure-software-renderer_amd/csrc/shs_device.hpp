@@ -120,6 +120,13 @@ constexpr uint32_t RF_SHARED_VARY = 1u << 18;
 // unbounded slivers among its own triangles enumerates their tile-clamp pixels itself, from the
 // records it keeps in LDS, instead of ghost blocks recomputing every triangle's record.
 constexpr uint32_t RF_GHOST_INLINE = 1u << 19;
+// Bin-mode batches whose bin tiles' raster rows run on one XCD (frame flags bit 20, set by the host):
+// a bin tile's first appender lists its four raster rows as one 4-aligned group of the busy list
+// (BUSY_SKIP pads the rows below the screen), and k_raster deals busy items so that the four rows of a
+// group land on the same ticket queue -- the same XCD, whose L2 then serves the group's bin list, boxes
+// and records to the three rows after the first.
+constexpr uint32_t RF_XCD_ROWS = 1u << 20;
+constexpr uint32_t BUSY_SKIP = 0xffffffffu;   // a padding entry of the busy list: no tile
 
 // Uniforms of up to KARG_DRAWS draws travel in the kernel arguments (no per-frame copy);
 // larger scenes read the device draw table.

@@ -295,6 +295,18 @@ __device__ __forceinline__ void mark_busy(const FrameParams &fp, const FrameBuff
 __device__ __forceinline__ void mark_bin_rows(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int frame, int t,
                                               NewBusy &nb) {
     const int bx = t % fp.tiles_x, ry0 = (t / fp.tiles_x) * (TILE / RTH);
+    if (fp.flags & RF_XCD_ROWS) {   // the rows as one 4-aligned group (every bin-mode append is 4 entries)
+        static_assert(TILE / RTH == 4 && NEW_BUSY_CAP % 4 == 0, "row groups of four");
+        const uint32_t k = atomicAdd(&nb.n, 4u);
+        uint32_t *dst = k < (uint32_t)NEW_BUSY_CAP ? &nb.e[k] : &fb.busy_list[atomicAdd(&cnt[C_BUSY], 4u)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int rt = (ry0 + r) * fp.tiles_x + bx;
+            if (ry0 + r < fp.rtiles_y) fb.busy[rt] = fp.epoch;
+            dst[r] = ry0 + r < fp.rtiles_y ? busy_entry(fp, frame, rt) : BUSY_SKIP;
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < TILE / RTH; ++r) {
         const int ry = ry0 + r;
@@ -1524,7 +1536,7 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
     // Every independent first-touch load is issued up front so their round trips overlap: the
     // busy-list length, the ghost-fragment count, the draws' shading uniforms and, for a small
     // single-frame scan-mode scene, every bin box (into registers).
-    const uint32_t n_busy = min(cnt[C_BUSY], (uint32_t)(n_rt * fp.n_frames));
+    const uint32_t n_busy = min(cnt[C_BUSY], (uint32_t)(fp.tiles_x * fp.tiles_y * (TILE / RTH) * fp.n_frames));
     const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
     static_assert(LDS_DRAWS * 4 == 256, "one per-draw uniform float4 per thread");
     const int n_draws_all = fp.n_draws * fp.n_frames;
@@ -1563,10 +1575,15 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
             const int sy = (int)s_lo - f * strips_y;
             for (int ry = sy * STRIP_RT; ry < min((sy + 1) * STRIP_RT, fp.rtiles_y); ++ry) clear_strip(fp, fb, f, ry);
         } else {
-            const uint32_t g = fb.busy_list[item - s_lo];
+            uint32_t k = item - s_lo;
+            if ((fp.flags & RF_XCD_ROWS) && k < (n_busy & ~31u))   // busy item 32B + 8r + x <- entry 32B + 4x + r:
+                k = (k & ~31u) | ((k & 7u) << 2) | ((k >> 3) & 3u);  // a row group's items 8 apart (one queue)
+            const uint32_t g = fb.busy_list[k];
             const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
             const FrameBuffers fv = frame_view(fp, fb, f);
-            if (fp.flags & DBG_CLEAR_ONLY) {
+            if (g == BUSY_SKIP) {
+                // padding of a row group (a bin tile's row below the screen): nothing to draw
+            } else if (fp.flags & DBG_CLEAR_ONLY) {
                 __syncthreads();
                 clear_tile(fp, fv, rt);
             } else {
