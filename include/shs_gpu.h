@@ -167,7 +167,8 @@ int shs_mat4_mul(const float a16[16], const float b16[16], float out16[16]);
 int shs_mat4_inverse(const float m16[16], float out16[16]);
 
 /* Debug / test hook: copy the last frame's per-triangle raster records (96 B each, layout
- * shs_dev::TriRec in csrc/shs_device.hpp) into caller memory; returns the count via n_out. */
+ * shs_dev::TriRec in csrc/shs_device.hpp) into caller memory; returns the count via n_out.
+ * Records of culled triangles are not written by the legacy setup (stale entries). */
 int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out);
 
 /* Tuning knobs.  SHS_OPT_BIN_CAPACITY: initial per-tile bin capacity (entries past it spill to a

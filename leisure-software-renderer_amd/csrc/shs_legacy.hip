@@ -632,8 +632,11 @@ __device__ __forceinline__ uint32_t setup_quad(const FrameParams &fp, const Fram
         if ((r.flags & (TRI_UNBOUNDED | TRI_CULLED)) == TRI_UNBOUNDED) quad_store_rec(fb, tri, r);
         if (q == 0) fb.tdraw[tri] = tdraw_word(d, r.flags);
     } else {
-        quad_store_rec(fb, tri, r);
-        if (vary) {
+        // a culled triangle's record is never read (its bin box is empty: never binned, staged or a
+        // winner); its varyings are, in the other frames, when frame 0's are shared (quad-uniform tests)
+        const bool culled = r.flags & TRI_CULLED;
+        if (!culled) quad_store_rec(fb, tri, r);
+        if (vary && (!culled || (fp.flags & RF_SHARED_VARY))) {
             f3 a, nr;
             corner_varyings(dr, p3, n3, a, nr);
             quad_store_shade(fb, tri, dbase + d, dr.shading, a, nr);   // the draw-table index of the batch
