@@ -1513,7 +1513,14 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
     }
 }
 
-constexpr int STRIP_RT = 2;   // raster-tile rows per clear item
+// Raster-tile rows per clear item.  Eight (a 64-row strip of one frame) against two: C2 0.275 ->
+// 0.272 ms per step in five A/B pairs, C3 unchanged.  The k_raster event grows (C2 0.242 -> 0.248 ms),
+// but fewer, longer strip items let the next batch's setup take CUs sooner; 16 rows was slower
+// (0.287 ms).  -DSHS_STRIP_RT=...: timing experiments.
+#ifndef SHS_STRIP_RT
+#define SHS_STRIP_RT 8
+#endif
+constexpr int STRIP_RT = SHS_STRIP_RT;
 
 // Persistent raster over the whole batch.  Work items are the busy tiles (the busy list k_setup /
 // k_ghost built: latency-bound raster) and the clear strips (one raster-tile row of one frame:
