@@ -1516,7 +1516,7 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
 // Raster-tile rows per clear item.  Eight (a 64-row strip of one frame) against two: C2 0.275 ->
 // 0.272 ms per step in five A/B pairs, C3 unchanged.  The k_raster event grows (C2 0.242 -> 0.248 ms),
 // but fewer, longer strip items let the next batch's setup take CUs sooner; 16 rows was slower
-// (0.287 ms).  -DSHS_STRIP_RT=...: timing experiments.
+// (0.287 ms), 6 or 12 no better.  -DSHS_STRIP_RT=...: timing experiments.
 #ifndef SHS_STRIP_RT
 #define SHS_STRIP_RT 8
 #endif
