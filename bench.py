@@ -98,7 +98,7 @@ def run_gpu(args, rank, local_rank, world, dist):
     import shs_gpu
     F = args.frames_per_step
     frame, sets = batch_poses(args.config, F, rank)
-    frame.debug_flags = args.debug_flags   # timing experiments only (wrong images)
+    frame.debug_flags = args.debug_flags   # timing experiments only (wrong images; read only by libshs_gpu_exp.so)
     ctx = shs_gpu.Context(local_rank)
     if args.raster_mode:
         ctx.set_raster_mode(args.raster_mode)
@@ -254,14 +254,22 @@ class LibSlot:
             self.ctx.set_stream(self.stream.cuda_stream)
         self.gbufs = [None]
         self.prepared = None
+        self.gather_events = None   # [(start, end)] HIP events around each gather while timing
 
     def gather(self, dist):
         """The frame's owned present tiles into rank 0 over RCCL, ordered on this slot's stream."""
         import torch
         from shs_gpu import shard
         with torch.cuda.stream(self.stream):
+            ev = None
+            if self.gather_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(self.stream)
             self.gbufs[0] = shard.gather_frame_device(dist, self.ctx, self.ctx.TARGET_LIB_PRESENT, stream=self.stream,
                                                       out=self.gbufs[0])
+            if ev is not None:
+                ev[1].record(self.stream)
+                self.gather_events.append(ev)
 
 
 def camera_phase_bytes(width, height, owned_px, shadow_size=None):
@@ -320,11 +328,16 @@ def lib_timed_loop(args, slots, frame_fn, dist, frame=None, rank=0, world=1, on_
     ctx = slots[0].ctx
     ctx.enable_timing(True)
     ctx.lib_timing_reset()
+    if dist is not None:
+        slots[0].gather_events = []
     for _ in range(20):
         frame_fn(slots[0])
     barrier_sync()
     n_passes, kms = ctx.lib_timing_read()
     ctx.enable_timing(False)
+    if slots[0].gather_events:   # the gather's own time on the slot stream (rank 0: receives + unpack)
+        kms = dict(kms, gather=float(np.mean([a.elapsed_time(b) for a, b in slots[0].gather_events])))
+        slots[0].gather_events = None
     if on_last is not None:
         on_last(ctx)
     owned = None
@@ -362,7 +375,7 @@ def run_gpu_c4(args, rank, local_rank, world, dist):
             sl.gather(dist)
 
     elapsed, stats, (n_cam, kms), owned = lib_timed_loop(args, slots, one_frame, dist, frame, rank, world)
-    kms = {"setup": kms["setup"], "raster": kms["raster"]}
+    kms = {k: kms[k] for k in ("setup", "raster", "gather") if k in kms}
     n_tri = sum(d.mesh.n_tris for d in draws)
     # the raster phase writes HDR + depth + motion (28 B/px) and the fused tonemap's RGBA8 present staging
     # (4 B/px) for the pixels this rank owns
@@ -422,6 +435,58 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
                + 2 * shadow_texels[0] * 4 + frame.width * frame.height * 32)
     n_tri = sum(d.mesh.n_tris for d in draws)
     return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, (S, shadow_texels[0]), owned
+
+
+def strong_summary(cfg, n_tri, frames, elapsed_max, rank_kernels_ms, rank_gather_ms, rank_owned, layout, inflight):
+    """One strong-scaling leg's keys (the 4K tile-sharded frame of north_star's >= 6x target) from the
+    per-rank measurements rank 0 collected: frames per second over the whole job between two barriers,
+    the worst rank's isolated camera-frame kernels, each rank's gather time and owned pixels."""
+    world = len(rank_kernels_ms)
+    worst = int(np.argmax(rank_kernels_ms))
+    return {
+        "workload": WORKLOADS[cfg],
+        "n_gpus": world,
+        "frames": frames,
+        "ms_per_frame": round(elapsed_max / frames * 1e3, 5),
+        "mtri_s": round(n_tri * frames / elapsed_max / 1e6, 3),
+        "worst_rank": worst,
+        "worst_rank_kernels_ms": round(float(rank_kernels_ms[worst]), 5),
+        "rank_kernels_ms": [round(float(x), 5) for x in rank_kernels_ms],
+        "gather_ms": [round(float(x), 5) for x in rank_gather_ms],
+        "owned_pixels": [int(x) for x in rank_owned],
+        "layout": layout if world > 1 else "whole frame",
+        "frames_in_flight": inflight,
+        "what": "one frame per step split over the ranks (strong scaling): region-sharded camera pass + fused "
+                "tonemap, RGBA8 present tiles gathered into rank 0 over RCCL every frame; ms_per_frame = max-over-"
+                "ranks wall time between barriers / frames; kernels: each rank's shadow + camera pass kernels, "
+                "one frame in flight (HIP events); gather: HIP events around the gather on the frame's stream",
+    }
+
+
+def strong_legs(args, rank, local_rank, world, dist):
+    """The bounded C4 / C5 tile-sharded legs run after the headline C2 loop at every N (N = 1 is the
+    denominator of the driver's 1 -> 8 curve): -> {"strong_c4": {...}, "strong_c5": {...}} on rank 0."""
+    import copy
+    out = {}
+    for cfg in args.strong:
+        a = copy.copy(args)
+        a.config, a.steps, a.warmup = cfg, args.strong_frames, 10
+        a.shard_layout, a.inflight = "regions", 3
+        runner = run_gpu_c4 if cfg == "c4" else run_gpu_lib
+        frame, stats, elapsed, n_frames, kms, _, _, n_tri, _, owned = runner(a, rank, local_rank, world, dist)
+        k_ms = sum(v for k, v in kms.items() if k != "gather")
+        mine = [elapsed, k_ms, kms.get("gather", 0.0), float(owned)]
+        if dist is not None:
+            import torch
+            t = torch.zeros((world, 4), dtype=torch.float64, device=args.reduce_device)
+            t[rank] = torch.tensor(mine, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            rows = t.cpu().numpy()
+        else:
+            rows = np.asarray([mine])
+        out["strong_" + cfg] = strong_summary(cfg, n_tri, a.steps, float(rows[:, 0].max()), rows[:, 1], rows[:, 2],
+                                              rows[:, 3], a.shard_layout, a.inflight)
+    return out
 
 
 def collect_pmc(args):
@@ -639,6 +704,10 @@ def main():
                     help="c5: render the whole shadow map every frame (default: the camera pass's footprint, "
                          "SHS_OPT_SHADOW_FOOTPRINT)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--strong", default="c4,c5", type=lambda x: [c for c in x.split(",") if c],
+                    help="legacy configs: the tile-sharded 4K legs run after the headline loop at every N "
+                         "(strong_c4 / strong_c5 keys; '' to skip)")
+    ap.add_argument("--strong-frames", type=int, default=60, help="timed frames of each strong leg")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-frame latency leg (profiling)")
@@ -691,6 +760,7 @@ def main():
     if args.config in LIB_CONFIGS:
         return main_lib(args, world, rank, local_rank, dist, pmc, pmc_err)
     frame, draws, stats, elapsed, n_launches, kms, single, pcie, ramp = run_gpu(args, rank, local_rank, world, dist)
+    strong = strong_legs(args, rank, local_rank, world, dist) if args.strong and not args.child else {}
     B1, n_tri1 = algorithmic_bytes(frame, draws)
     F = args.frames_per_step
     B, n_tri = B1 * F, n_tri1 * F          # per step (= per k_raster launch)
@@ -770,6 +840,7 @@ def main():
         line["single_frame"] = single
     if pcie is not None:
         line["seam1_pcie"] = pcie
+    line.update(strong)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(line), flush=True)
@@ -801,7 +872,7 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
     steps = args.steps
     t_k = kms["raster"]
     achieved = B_k / (t_k * 1e-3) / 1e9 if t_k > 0 else None
-    t_frame = sum(kms.values())
+    t_frame = sum(v for k, v in kms.items() if k != "gather")
     # at N > 1 the timed kernels are rank 0's: its frame bytes are the whole frame's minus the 32 B of
     # every pixel another rank renders (geometry and the shadow map are still read whole on every rank)
     B_frame -= (frame.width * frame.height - owned) * 32

@@ -144,6 +144,9 @@ int shs_mesh_release(shs_ctx *ctx, int32_t id) {
     if (ctx->shadow_pending) {   // a recorded footprint shadow pass may read the mesh: render it first
         const int rc = shs_lib_flush_shadow(ctx);
         if (rc) return rc;
+    } else if (ctx->meshes[id].lib) {   // a footprint-restricted map that reads it is rendered whole
+        const int rc = shs_lib_widen_shadow(ctx, ctx->meshes[id].pos);
+        if (rc) return rc;
     }
     if (flush_pending(ctx)) return SHS_ERR_HIP;   // a pending legacy raster may read it too
     HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
@@ -264,7 +267,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (total * n_frames > 0x3fffffff) { ctx->err = "too many triangles in one batch"; return SHS_ERR_INVALID; }
     const int n_tris = (int)total;   // per frame (every frame of a batch has the same count)
     const size_t nt_all = (size_t)std::max(n_tris, 1) * n_frames;
-    static const bool ghost_list_env = std::getenv("SHS_GHOST_LIST") && std::atoi(std::getenv("SHS_GHOST_LIST")) != 0;
+    static const bool ghost_list_env = shs_exp_env("SHS_GHOST_LIST") && std::atoi(shs_exp_env("SHS_GHOST_LIST")) != 0;
     const bool scan = ctx->force_mode == 1 || (ctx->force_mode == 0 && n_tris <= shs_dev::SCAN_MAX_TRIS);
     // pipelined (SHS_OPT_LEGACY_PIPELINE): scan-mode batches (their ghost waves live in k_setup) with a
     // device draw table; the frame buffers the pending raster writes must not be reallocated under it
@@ -377,7 +380,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     fp.n_tris = n_tris; fp.n_draws = n_draws;
     fp.clear_rgba = (uint32_t)f.clear_color[0] | ((uint32_t)f.clear_color[1] << 8) | ((uint32_t)f.clear_color[2] << 16) |
                     ((uint32_t)f.clear_color[3] << 24);
-    fp.flags = (f.flags & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS | shs_dev::RF_SHARED_VARY | shs_dev::RF_GHOST_INLINE | shs_dev::RF_XCD_ROWS)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
+    fp.flags = (f.flags & (SHS_EXPERIMENTS ? ~0u : ~shs_dev::DBG_MASK) & ~(shs_dev::RF_PER_PIXEL | shs_dev::RF_NO_RECS | shs_dev::RF_SHARED_VARY | shs_dev::RF_GHOST_INLINE | shs_dev::RF_XCD_ROWS)) | (ctx->pair_loop ? 0u : shs_dev::RF_PER_PIXEL);
     fp.bin_cap = ctx->bin_cap;
     fp.spill_cap = (uint32_t)std::min<size_t>(ws.spill.cap, 0xffffffffu);
     fp.frag_cap = (uint32_t)std::min<size_t>(ws.frags.cap, 0xffffffffu);
@@ -398,7 +401,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     // resident mesh (RF_NO_RECS).  Off by default: measured C3 0.670 -> 0.699 ms per 16-frame step (the
     // staged candidates' draw -> matrix -> position chain costs more raster latency than the 184 B of
     // record traffic it removes).
-    static const bool no_recs_env = std::getenv("SHS_LEGACY_NORECS") && std::atoi(std::getenv("SHS_LEGACY_NORECS")) != 0;
+    static const bool no_recs_env = shs_exp_env("SHS_LEGACY_NORECS") && std::atoi(shs_exp_env("SHS_LEGACY_NORECS")) != 0;
     const bool no_recs = !fp.scan_mode && no_recs_env;
     if (no_recs) {
         fp.flags |= shs_dev::RF_NO_RECS;
@@ -408,7 +411,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     // Blinn-Phong shading and bitwise the same model matrices -- a static scene under a batch of camera
     // poses -- so the corners' world positions and normals are computed and stored once for the batch.
     // SHS_LEGACY_SHARE_VARY=0 turns it off (timing experiments).
-    static const bool share_env = [] { const char *e = std::getenv("SHS_LEGACY_SHARE_VARY"); return !e || std::atoi(e) != 0; }();
+    static const bool share_env = [] { const char *e = shs_exp_env("SHS_LEGACY_SHARE_VARY"); return !e || std::atoi(e) != 0; }();
     if (share_env && !no_recs && n_frames > 1) {
         bool share = true;
         for (int i = 0; i < n_draws && share; ++i) {
@@ -423,7 +426,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     }
     // Bin-mode row groups dealt to one XCD (RF_XCD_ROWS): SHS_LEGACY_XCD_ROWS=0 turns it off (timing
     // experiments).
-    static const bool xcd_rows_env = [] { const char *e = std::getenv("SHS_LEGACY_XCD_ROWS"); return !e || std::atoi(e) != 0; }();
+    static const bool xcd_rows_env = [] { const char *e = shs_exp_env("SHS_LEGACY_XCD_ROWS"); return !e || std::atoi(e) != 0; }();
     if (!fp.scan_mode && xcd_rows_env) fp.flags |= shs_dev::RF_XCD_ROWS;
     const int owned_bt = (n_tiles - f.shard_rank + f.shard_count - 1) / f.shard_count;
     const int n_groups = (n_tris + 15) / 16;
@@ -435,7 +438,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     // slivers (RF_GHOST_INLINE) instead of ghost blocks recomputing every triangle's record (C2: 976
     // ghost blocks per batch for ~17 slivers per frame).  SHS_GHOST_INLINE=0 restores the ghost blocks,
     // SHS_GHOST_LIST=1 lists scan-mode slivers for k_ghost (timing experiments).
-    static const bool ghost_inline_env = [] { const char *e = std::getenv("SHS_GHOST_INLINE"); return !e || std::atoi(e) != 0; }();
+    static const bool ghost_inline_env = [] { const char *e = shs_exp_env("SHS_GHOST_INLINE"); return !e || std::atoi(e) != 0; }();
     fp.ghost_list = (fp.scan_mode && !ghost_list_env) ? 0u : 1u;
     // (only when the ghost waves would take one slice per group anyway: a single frame's few slivers,
     // cut into up to 16 slices over the ghost blocks, finish sooner than walked by their setup waves --
@@ -452,7 +455,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     // C3: 0.76 -> 0.68 ms per 16-frame step; scan-mode C2 is best at 4).  SHS_RASTER_PER_CU overrides
     // (timing experiments).
     static const int rbpc_env = [] {
-        const char *e = std::getenv("SHS_RASTER_PER_CU");
+        const char *e = shs_exp_env("SHS_RASTER_PER_CU");
         const int v = e ? std::atoi(e) : 0;
         return v >= 1 && v <= 4 ? v : 0;
     }();

@@ -296,7 +296,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     // every slot enters the large-primitive queue at most once
     if (ensure(ctx, w.bigq, n_slots) || ensure(ctx, w.bigpre, n_slots)) return SHS_ERR_HIP;
     int st = 2;   // supertile edge in bin tiles (SHS_LIB_XCD_ST: timing experiments; 0 = plain order)
-    if (const char *e = std::getenv("SHS_LIB_XCD_ST")) st = (int)std::strtol(e, nullptr, 0);
+    if (const char *e = shs_exp_env("SHS_LIB_XCD_ST")) st = (int)std::strtol(e, nullptr, 0);
     const uint64_t gkey = ((uint64_t)tiles_x << 48) ^ ((uint64_t)tiles_y << 32);
     // rtiles_y too: a height change inside the same bin-tile rows changes the raster-tile rows
     bool reset = gkey != w.geom_key || rtiles_y != w.geom_rtiles_y;
@@ -365,13 +365,13 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fp.parity = w.frame_index & 1u;
     // scan mode (every busy tile tests every primitive's box) for small passes, per-tile bins above
     {
-        const char *e = std::getenv("SHS_LIB_SCAN_MAX");   // timing experiments: the scan / bin threshold
+        const char *e = shs_exp_env("SHS_LIB_SCAN_MAX");   // timing experiments: the scan / bin threshold
         const long scan_max = e ? std::strtol(e, nullptr, 0) : SCAN_MAX_PRIMS;
         fp.scan_mode = n_tris <= scan_max ? 1u : 0u;
     }
     fp.setup_blocks = setup_blocks;
     {
-        const char *e = std::getenv("SHS_LIB_EXP");   // timing experiments only: parts of the setup skipped
+        const char *e = shs_exp_env("SHS_LIB_EXP");   // timing experiments only: parts of the setup skipped
         fp.exp_flags = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
     }
     fp.n_owned_rt = order->n;
@@ -388,7 +388,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     // fullest bin tile fit one such round (scan mode: every primitive is a candidate)
     const uint64_t fullest = fp.scan_mode ? (uint64_t)n_tris + (shadow ? 0u : w.st_extra) : w.st_maxbin;
     static const int force_deep = [] {   // SHS_LIB_DEEP=1 (timing experiments): the deep raster for every camera pass
-        const char *e = std::getenv("SHS_LIB_DEEP");
+        const char *e = shs_exp_env("SHS_LIB_DEEP");
         return e ? std::atoi(e) : 0;
     }();
     const bool shallow = w.st_checked && fullest <= 256u && !(force_deep && !shadow);
@@ -398,7 +398,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (ensure(ctx, w.rstat, (size_t)raster_grid)) return SHS_ERR_HIP;
     fp.raster_grid = raster_grid;
     {   // static share of the raster items (SHS_LIB_STATIC_DIV: timing experiments)
-        static const int div = [] { const char *e = std::getenv("SHS_LIB_STATIC_DIV"); return e ? std::atoi(e) : 2; }();
+        static const int div = [] { const char *e = shs_exp_env("SHS_LIB_STATIC_DIV"); return e ? std::atoi(e) : 2; }();
         fp.static_div = div;
     }
     if (!shadow) {   // k_lib_dyn's per-queue lists: every work position could be dynamic
@@ -406,7 +406,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         fp.dyn_cap = (uint32_t)((n_max + shs_dev::LIB_NQ - 1) / shs_dev::LIB_NQ + 1);
         if (ensure(ctx, w.dynq, (size_t)2 * shs_dev::LIB_NQ * fp.dyn_cap)) return SHS_ERR_HIP;
         // heavy tiles (bin list entries; SHS_LIB_HEAVY: timing experiments, 0 = none)
-        static const int heavy = [] { const char *e = std::getenv("SHS_LIB_HEAVY"); return e ? std::atoi(e) : 2048; }();
+        static const int heavy = [] { const char *e = shs_exp_env("SHS_LIB_HEAVY"); return e ? std::atoi(e) : 2048; }();
         fp.heavy_min = (uint32_t)std::max(heavy, 0);
     }
 
@@ -847,6 +847,17 @@ int shs_lib_flush_shadow(shs_ctx *ctx) {
     return enqueue_shadow(ctx, shs_dev::ShardRegion{0, 0, 0, 0, 0});
 }
 
+// A footprint-restricted shadow map whose casters include `pos` (a mesh about to be released) is
+// rendered whole first: a later camera pass that reads beyond the footprint could not re-render it.
+int shs_lib_widen_shadow(shs_ctx *ctx, const float *pos) {
+    if (ctx->shadow_pending || !ctx->have_shadow || !ctx->shadow_reg.on) return SHS_OK;
+    bool reads = false;
+    for (const LibDrawGPU &d : ctx->lib_shadow.last_draws) reads = reads || d.pos == pos;
+    if (!reads) return SHS_OK;
+    const int rc = check_superseded(ctx, ctx->lib_shadow);
+    return rc ? rc : enqueue_shadow(ctx, shs_dev::ShardRegion{0, 0, 0, 0, 0});
+}
+
 extern "C" {
 
 // SHS_OPT_SHADOW_FOOTPRINT: the shadow-map bin tiles the camera pass about to be enqueued can read
@@ -961,6 +972,28 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     if (ctx->shadow_pending) {   // the recorded shadow pass, narrowed to what this pass reads
         const int rc = enqueue_shadow(ctx, shadow_region_for(ctx, f, draws, n_draws, fp.reg));
         if (rc) return rc;
+    } else if (ctx->have_shadow && ctx->shadow_reg.on) {
+        // A map rendered for an earlier camera pass's footprint, sampled again (a static sun reused over
+        // frames, another view or region): the texels this pass reads must lie inside what was
+        // rendered, or the pass is enqueued again over the union (stream-ordered after the earlier
+        // camera passes; re-rendered texels get the same values).
+        bool shadowed = false;
+        for (int i = 0; i < n_draws; ++i) shadowed = shadowed || draws[i].shadow;
+        if (shadowed) {
+            const shs_dev::ShardRegion need = shadow_region_for(ctx, f, draws, n_draws, fp.reg);
+            const shs_dev::ShardRegion &have = ctx->shadow_reg;
+            auto empty = [](const shs_dev::ShardRegion &r) { return r.x1 < r.x0 || r.y1 < r.y0; };
+            const bool inside = empty(need) || (!empty(have) && need.x0 >= have.x0 && need.y0 >= have.y0 &&
+                                                need.x1 <= have.x1 && need.y1 <= have.y1);
+            if (!inside) {
+                const shs_dev::ShardRegion u = empty(have) ? need
+                    : shs_dev::ShardRegion{1, std::min(need.x0, have.x0), std::min(need.y0, have.y0),
+                                           std::max(need.x1, have.x1), std::max(need.y1, have.y1)};
+                int rc = check_superseded(ctx, ctx->lib_shadow);
+                if (!rc) rc = enqueue_shadow(ctx, u);
+                if (rc) return rc;
+            }
+        }
     }
     ctx->lib_frame = f;
     ctx->cam_after_shadow = ctx->have_shadow;
@@ -1264,16 +1297,21 @@ int shs_tiles_packed_words(shs_ctx *ctx, int target, int32_t count, int64_t *wor
     return SHS_OK;
 }
 
+// A frame whose capacity overflowed is re-issued before its tiles leave the rank or peers' tiles land in
+// it (legacy: the batch, a pipelined batch's pending raster included -- it clears the whole frame;
+// library: the pass chain, tonemap included).  Only its setup is waited for: the overflow word is final
+// then, and the copy is stream-ordered after the (possibly re-issued) frame.
+static int final_before_copy(shs_ctx *ctx, int target) {
+    return (target == SHS_TARGET_LEGACY || target == SHS_TARGET_PRESENT) ? shs_legacy_ensure_final(ctx)
+                                                                        : shs_lib_ensure_final(ctx);
+}
+
 int shs_tiles_pack(shs_ctx *ctx, int target, int32_t rank, int32_t count, void *dst_dev) {
     if (!ctx || !dst_dev) return SHS_ERR_INVALID;
     shs_dev::TileCopyParams p;
     if (tile_params(ctx, target, rank, count, p)) return SHS_ERR_INVALID;
     if (set_dev(ctx)) return SHS_ERR_HIP;
-    // A frame whose capacity overflowed is re-issued before its tiles leave the rank (legacy: the batch;
-    // library: the pass chain, tonemap included).  Only its setup is waited for: the overflow word is
-    // final then, and the pack below is stream-ordered after the (possibly re-issued) frame.
-    const int rc = (target == SHS_TARGET_LEGACY || target == SHS_TARGET_PRESENT) ? shs_legacy_ensure_final(ctx)
-                                                                                : shs_lib_ensure_final(ctx);
+    const int rc = final_before_copy(ctx, target);
     if (rc) return rc;
     HIP_TRY(ctx, shs_internal::launch_tiles_copy(p, true, dst_dev, ctx->stream));
     return SHS_OK;
@@ -1284,6 +1322,8 @@ int shs_tiles_unpack(shs_ctx *ctx, int target, int32_t rank, int32_t count, cons
     shs_dev::TileCopyParams p;
     if (tile_params(ctx, target, rank, count, p)) return SHS_ERR_INVALID;
     if (set_dev(ctx)) return SHS_ERR_HIP;
+    const int rc = final_before_copy(ctx, target);
+    if (rc) return rc;
     HIP_TRY(ctx, shs_internal::launch_tiles_copy(p, false, const_cast<void *>(src_dev), ctx->stream));
     return SHS_OK;
 }
@@ -1291,6 +1331,10 @@ int shs_tiles_unpack(shs_ctx *ctx, int target, int32_t rank, int32_t count, cons
 int shs_tiles_unpack_ranks(shs_ctx *ctx, int target, int32_t count, const void *const *src_dev) {
     if (!ctx || !src_dev || count <= 0) return SHS_ERR_INVALID;
     if (set_dev(ctx)) return SHS_ERR_HIP;
+    {
+        const int rc = final_before_copy(ctx, target);
+        if (rc) return rc;
+    }
     shs_dev::TileUnpackMulti m;
     std::memset(&m, 0, sizeof m);
     for (int32_t r = 0; r < count; ++r) {

@@ -94,7 +94,7 @@ extern "C" int shs_occlusion_pass(shs_ctx *ctx, const shs_occlusion_desc *desc, 
     p.occluded = ctx->occ_flags.p;
     p.visible = ctx->occ_visible.p + 1;
     p.n_visible = ctx->occ_visible.p;
-    p.prof = std::getenv("SHS_OCC_PROF") != nullptr;
+    p.prof = shs_exp_env("SHS_OCC_PROF") != nullptr;
     HIP_TRY(ctx, shs_internal::launch_occlusion(p, ctx->stream));
     std::vector<uint32_t> vis(order.size() + 1);
     HIP_TRY(ctx, hipMemcpyAsync(vis.data(), ctx->occ_visible.p, vis.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));

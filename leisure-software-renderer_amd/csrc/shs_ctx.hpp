@@ -15,6 +15,18 @@
 #include "shs_lightbin_internal.hpp"
 #include "shs_occlusion_internal.hpp"
 
+// Timing-experiment switches (SHS_* environment variables and the frame's DBG_* debug bits; several give
+// wrong images).  Only the -DSHS_TIMING_EXPERIMENTS build (`make exp` -> shs_gpu/libshs_gpu_exp.so,
+// loaded by tools/ through SHS_GPU_LIB) reads them; the product library ignores the environment.
+#ifdef SHS_TIMING_EXPERIMENTS
+#include <cstdlib>
+inline const char *shs_exp_env(const char *name) { return std::getenv(name); }
+constexpr bool SHS_EXPERIMENTS = true;
+#else
+inline const char *shs_exp_env(const char *) { return nullptr; }
+constexpr bool SHS_EXPERIMENTS = false;
+#endif
+
 namespace shs_host_detail {
 struct Mesh {
     float *pos = nullptr;            // legacy soup: 9 floats per triangle; library mesh: 3 per vertex
@@ -293,6 +305,7 @@ int shs_legacy_ensure_final(shs_ctx *ctx);
 int shs_lib_ensure_final(shs_ctx *ctx);
 // A shadow pass recorded under SHS_OPT_SHADOW_FOOTPRINT and not yet enqueued: enqueue it for the whole map.
 int shs_lib_flush_shadow(shs_ctx *ctx);
+int shs_lib_widen_shadow(shs_ctx *ctx, const float *pos);
 // Region layout (shs_abi_shard.cpp).  shs_shard_balance: `count` rectangles of the tiles_x x tiles_y bin
 // grid of a W x H frame with equal predicted cost, from n_blk setup-block bounds (null: pixels only).
 void shs_shard_balance(const uint4 *blk, int n_blk, int tiles_x, int tiles_y, int W, int H, int count,

@@ -363,6 +363,69 @@ static void *worker(void *arg) {
     return NULL;
 }
 
+/* The tile-job executor: worker threads created once and reused across frames, as the reference's
+   ThreadedPriorityJobSystem (hello-shs-renderer/shs_renderer.hpp:1534-1564) keeps its workers for the
+   whole run.  A frame publishes its job context, wakes the workers, and waits until each has drained the
+   shared tile counter -- the reference's WaitGroup (:1597-1630); the submitting thread runs no tile,
+   as the reference's render loop only waits.  (Until round 4 the threads were created and joined every
+   frame, which at 256 threads cost more than the frame.) */
+typedef struct {
+    pthread_t th[256];
+    int n;
+    pthread_mutex_t mu;
+    pthread_cond_t go, done;
+    unsigned gen;
+    int busy, quit;
+    job_ctx *job;
+} tile_pool;
+static tile_pool g_pool = {.mu = PTHREAD_MUTEX_INITIALIZER, .go = PTHREAD_COND_INITIALIZER, .done = PTHREAD_COND_INITIALIZER};
+static pthread_mutex_t g_pool_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static void *pool_worker(void *arg) {
+    unsigned seen = (unsigned)(uintptr_t)arg;   /* the generation at creation: later frames wake it */
+    pthread_mutex_lock(&g_pool.mu);
+    for (;;) {
+        while (!g_pool.quit && g_pool.gen == seen) pthread_cond_wait(&g_pool.go, &g_pool.mu);
+        if (g_pool.quit) break;
+        seen = g_pool.gen;
+        job_ctx *c = g_pool.job;
+        pthread_mutex_unlock(&g_pool.mu);
+        worker(c);
+        pthread_mutex_lock(&g_pool.mu);
+        if (--g_pool.busy == 0) pthread_cond_signal(&g_pool.done);
+    }
+    pthread_mutex_unlock(&g_pool.mu);
+    return NULL;
+}
+
+/* (caller holds g_pool_lock) the pool with n workers; returns the workers running */
+static int pool_resize(int n) {
+    if (g_pool.n == n) return n;
+    pthread_mutex_lock(&g_pool.mu);
+    g_pool.quit = 1;
+    pthread_cond_broadcast(&g_pool.go);
+    pthread_mutex_unlock(&g_pool.mu);
+    for (int i = 0; i < g_pool.n; ++i) pthread_join(g_pool.th[i], NULL);
+    g_pool.n = 0;
+    g_pool.quit = 0;
+    for (int i = 0; i < n; ++i) {
+        if (pthread_create(&g_pool.th[i], NULL, pool_worker, (void *)(uintptr_t)g_pool.gen) != 0) break;
+        g_pool.n++;
+    }
+    return g_pool.n;
+}
+
+/* (caller holds g_pool_lock) one frame's tiles over the pool */
+static void pool_run(job_ctx *c) {
+    pthread_mutex_lock(&g_pool.mu);
+    g_pool.job = c;
+    g_pool.busy = g_pool.n;
+    g_pool.gen++;
+    pthread_cond_broadcast(&g_pool.go);
+    while (g_pool.busy > 0) pthread_cond_wait(&g_pool.done, &g_pool.mu);
+    pthread_mutex_unlock(&g_pool.mu);
+}
+
 int ora_render_legacy(int W, int H, int tile_w, int tile_h, int n_threads, const ora_draw *draws, int n_draws,
                       uint8_t *color_out, float *depth_out, float *prequant_out) {
     if (W <= 0 || H <= 0 || tile_w <= 0 || tile_h <= 0 || !color_out || !depth_out) return -1;
@@ -379,12 +442,10 @@ int ora_render_legacy(int W, int H, int tile_w, int tile_h, int n_threads, const
     atomic_init(&c.next, 0);
     if (n_threads <= 1) { worker(&c); return 0; }
     if (n_threads > 256) n_threads = 256;
-    pthread_t th[256];
-    int started = 0;
-    for (int i = 0; i < n_threads; ++i)
-        if (pthread_create(&th[i], NULL, worker, &c) == 0) started++; else break;
-    if (started == 0) worker(&c);
-    for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
+    pthread_mutex_lock(&g_pool_lock);   /* one frame at a time on the pool */
+    if (pool_resize(n_threads) == 0) worker(&c);   /* no thread could be started */
+    else pool_run(&c);
+    pthread_mutex_unlock(&g_pool_lock);
     return 0;
 }
 

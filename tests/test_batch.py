@@ -218,7 +218,8 @@ def test_legacy_pipeline_matches_unpipelined():
     try:
         pip.set_legacy_pipeline(True)
         plan = [(frame, sets[0]), (frame, sets[1]), "resolve", (frame, sets[2]), (frame, sets[3]), (small, ssets[0]),
-                "resolve", (small, ssets[1]), ("single", sets[0][3]), (frame, sets[1]), (frame, sets[2])]
+                "resolve", (small, ssets[1]), ("single", sets[0][3]), (frame, sets[1]), (frame, sets[2]),
+                (frame, sets[3])]
         for step in plan:
             if step == "resolve":
                 for k in (0, 7, 15):
@@ -232,10 +233,48 @@ def test_legacy_pipeline_matches_unpipelined():
             fr, fds = step
             ref.render_batch_prepared(ref.prepare_batch(fr, fds))
             pip.render_batch_prepared(pip.prepare_batch(fr, fds))
-        for k in range(16):
+        # the framebuffers grow (32 frames) while the previous batch's raster is pending --
+        # enqueue_frame flushes it before the reallocation
+        frame32, sets32 = bench.batch_poses("c2", 32)
+        ref.render_batch_prepared(ref.prepare_batch(frame32, sets32[0]))
+        pip.render_batch_prepared(pip.prepare_batch(frame32, sets32[0]))
+        for k in range(32):
             a, b = ref.resolve_frame(k), pip.resolve_frame(k)
             assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)), k
         assert ref.stats() == pip.stats()
+    finally:
+        ref.close()
+        pip.close()
+
+
+def test_legacy_pipeline_unpack_after_pending_raster():
+    """peers' tiles unpacked into a pipelined legacy frame whose raster is still pending land
+    after that raster (shs_tiles_unpack flushes it first), so the raster's clear strips cannot overwrite
+    them: the owned pixels of rank 1 of 2 hold the unpacked words, the others the rendered frame."""
+    import torch
+    import shs_gpu
+    import bench
+    frame, sets = bench.batch_poses("c2", 16)
+    ref, pip = shs_gpu.Context(0), shs_gpu.Context(0)
+    try:
+        pip.set_legacy_pipeline(True)
+        ref.render_batch_prepared(ref.prepare_batch(frame, sets[0]))
+        rc, rd = ref.resolve_frame(0)
+        pip.render_batch_prepared(pip.prepare_batch(frame, sets[0]))   # its raster is pending now
+        words = pip.tiles_rank_words(pip.TARGET_LEGACY, 1, 2)
+        buf = torch.full((words,), 0x5A5A5A5A, dtype=torch.int32, device="cuda:0")
+        torch.cuda.synchronize()
+        pip.tiles_unpack(pip.TARGET_LEGACY, 1, 2, buf.data_ptr())
+        gc, gd = pip.resolve_frame(0)
+        W, H = frame.width, frame.height
+        tx = (W + 31) // 32
+        owned = int(((np.arange(H)[:, None] // 32 * tx + np.arange(W)[None, :] // 32) % 2 == 1).sum())
+        cw = np.ascontiguousarray(gc).view(np.uint32).reshape(H, W)
+        dw = gd.view(np.uint32)
+        assert int((cw == 0x5A5A5A5A).sum()) == owned and int((dw == 0x5A5A5A5A).sum()) == owned
+        rcw = np.ascontiguousarray(rc).view(np.uint32).reshape(H, W)
+        assert np.array_equal(cw[cw != 0x5A5A5A5A], rcw[cw != 0x5A5A5A5A])
+        assert np.array_equal(dw[dw != 0x5A5A5A5A], rd.view(np.uint32)[dw != 0x5A5A5A5A])
     finally:
         ref.close()
         pip.close()

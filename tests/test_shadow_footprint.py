@@ -151,3 +151,82 @@ def test_footprint_frames_match_oracle(oracle_mod, count):
         for c in ctxs:
             c.close()
         frame.shard_rank, frame.shard_count = 0, 1
+
+
+def _own_mask(c, count, rank, W, H):
+    if count == 1:
+        return np.ones((H, W), bool)
+    rx0, ry0, rx1, ry1 = c.shard_regions(count)[rank]
+    own = np.zeros((H, W), bool)
+    own[ry0 * 32:(ry1 + 1) * 32, rx0 * 32:(rx1 + 1) * 32] = True
+    return own
+
+
+@pytest.mark.gpu
+def test_footprint_map_reused_by_later_passes(oracle_mod):
+    """one footprint-restricted shadow map sampled by several camera passes (a static sun
+    reused over frames): another region of the same view, then another view.  Each pass whose footprint
+    leaves what was rendered re-renders the map over the union; every pass matches the oracle."""
+    from helpers import assert_depth_bitexact, assert_float_close
+    W, H, S, count = 960, 540, 1024, 3
+    frame, draws, casters, sun, _ = scene_lib.c5_scene(W, H, S)
+    sm_ref, lvp_ref = oracle_mod.shadow_map(S, sun, casters)
+    c = shs_gpu.Context(0)
+    try:
+        c.set_shadow_footprint(True)
+        c.set_shard_layout(True)
+        lvp = c.render_shadow_map(S, sun, casters)
+        assert np.array_equal(lvp.view(np.uint32), lvp_ref.view(np.uint32))
+        regions = []
+        for yaw, rank in [(0.0, 0), (0.0, 2), (55.0, 1), (-70.0, 0)]:
+            frame, draws, _, _, _ = scene_lib.c5_scene(W, H, S, yaw=yaw)
+            scene_lib.wire_shadow(draws, lvp_ref)
+            rh, rd, rm, _ = oracle_mod.pbr_forward(frame, draws, sm_ref)
+            frame.shard_rank, frame.shard_count = rank, count
+            c.render_pbr_forward(frame, draws)
+            regions.append(c.shadow_region())
+            h, d, m = c.resolve_lib()
+            own = _own_mask(c, count, rank, W, H)
+            assert_depth_bitexact(np.where(own, d, rd), rd)
+            assert_float_close(np.where(own[..., None], m, rm), rm, what="motion")
+            assert_float_close(np.where(own[..., None], h, rh), rh, what="hdr")
+        for a, b in zip(regions, regions[1:]):   # the rendered rectangle only grows
+            assert b[0] <= a[0] and b[1] <= a[1] and b[2] >= a[2] and b[3] >= a[3], regions
+        assert regions[-1] != regions[0], "no later pass read beyond the first footprint"
+    finally:
+        c.close()
+
+
+@pytest.mark.gpu
+def test_footprint_empty_for_a_rank(oracle_mod):
+    """a rank whose rectangle no shadowed draw reaches (only Suzanne samples the map) records
+    an empty footprint: its shadow pass renders nothing, the region reads as empty and its pixels still
+    match the oracle."""
+    from helpers import assert_depth_bitexact, assert_float_close
+    W, H, S, count = 960, 540, 1024, 8
+    frame, draws, casters, sun, _ = scene_lib.c5_scene(W, H, S)
+    sm_ref, lvp_ref = oracle_mod.shadow_map(S, sun, casters)
+    scene_lib.wire_shadow(draws, lvp_ref)
+    draws[0].shadow = False                     # the floor does not sample the map
+    rh, rd, rm, _ = oracle_mod.pbr_forward(frame, draws, sm_ref)
+    n_empty = 0
+    for rank in range(count):
+        c = shs_gpu.Context(0)
+        try:
+            c.set_shadow_footprint(True)
+            c.set_shard_layout(True)
+            for _ in range(2):                      # the second pass balances on the first one's bounds
+                c.render_shadow_map(S, sun, casters)
+                frame.shard_rank, frame.shard_count = rank, count
+                c.render_pbr_forward(frame, draws)
+                h, d, m = c.resolve_lib()
+            reg = c.shadow_region()
+            n_empty += reg[2] < reg[0] or reg[3] < reg[1]
+            own = _own_mask(c, count, rank, W, H)
+            assert_depth_bitexact(np.where(own, d, rd), rd)
+            assert_float_close(np.where(own[..., None], m, rm), rm, what="motion")
+            assert_float_close(np.where(own[..., None], h, rh), rh, what="hdr")
+        finally:
+            c.close()
+            frame.shard_rank, frame.shard_count = 0, 1
+    assert n_empty >= 1, "every rank's rectangle reached Suzanne's shadow reads"

@@ -3,7 +3,7 @@
 frames; for every rank the owned pixels' HDR / depth are compared with the oracle frame and the worst
 mismatches printed with the rank's rectangle, the pixel's light-list tile and its list count.
 
-  SHS_LIB_EXP=16 python tools/dbg_regions_c4.py     # with the wave light-list culling disabled"""
+  SHS_GPU_LIB=leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so SHS_LIB_EXP=16 python tools/dbg_regions_c4.py     # with the wave light-list culling disabled"""
 import os
 import sys
 

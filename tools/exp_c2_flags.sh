@@ -1,4 +1,6 @@
 #!/bin/bash
+# The switches below are read only by the timing-experiments build (make -C leisure-software-renderer_amd exp).
+export SHS_GPU_LIB=${SHS_GPU_LIB:-$PWD/leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so}
 # C2 k_raster split (timing only; debug flags make wrong images): default, busy tiles cleared instead
 # of rastered (DBG_CLEAR_ONLY 0x400), no clear strips (DBG_SKIP_CLEAR 0x1000).
 set -o pipefail

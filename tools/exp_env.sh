@@ -1,4 +1,6 @@
 #!/bin/bash
+# The switches below are read only by the timing-experiments build (make -C leisure-software-renderer_amd exp).
+export SHS_GPU_LIB=${SHS_GPU_LIB:-$PWD/leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so}
 # Timing A/B of environment switches on one config: ENVS="A=0 A=1" CONFIG=c5 bash tools/exp_env.sh
 set -o pipefail
 mkdir -p gpurun_out

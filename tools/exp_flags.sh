@@ -1,4 +1,6 @@
 #!/bin/bash
+# The switches below are read only by the timing-experiments build (make -C leisure-software-renderer_amd exp).
+export SHS_GPU_LIB=${SHS_GPU_LIB:-$PWD/leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so}
 # Timing attribution with debug flags (wrong images): CONFIG=c3 FLAGS="0 0x800" bash tools/exp_flags.sh
 # (DBG_SKIP_GHOST 0x100, DBG_SKIP_SHADE 0x200, DBG_CLEAR_ONLY 0x400, DBG_SKIP_BIN 0x800, DBG_SKIP_CLEAR 0x1000)
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# The switches below are read only by the timing-experiments build (make -C leisure-software-renderer_amd exp).
+export SHS_GPU_LIB=${SHS_GPU_LIB:-$PWD/leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so}
 # Library setup cost split (timing only; SHS_LIB_EXP makes wrong images): no LibShade stores (1),
 # no marks / bin appends (2), no LibRec stores (4), at full C4 and as rank 0 of 8.
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# The switches below are read only by the timing-experiments build (make -C leisure-software-renderer_amd exp).
+export SHS_GPU_LIB=${SHS_GPU_LIB:-$PWD/leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so}
 # k_lib_raster tile order experiment: bench C4 / C5 per supertile edge (SHS_LIB_XCD_ST).
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,4 +1,6 @@
 #!/bin/bash
+# The switches below are read only by the timing-experiments build (make -C leisure-software-renderer_amd exp).
+export SHS_GPU_LIB=${SHS_GPU_LIB:-$PWD/leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so}
 # Round-4 GPU check: the whole -m gpu suite, then the C2 short-window diagnostic, then A/B bench lines
 # (C3 record-free binned raster; C4 wave light-list culling on / off via SHS_LIB_EXP=16).
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# The switches below are read only by the timing-experiments build (make -C leisure-software-renderer_amd exp).
+export SHS_GPU_LIB=${SHS_GPU_LIB:-$PWD/leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so}
 # parity (library + legacy suites), then variant timing: C4 / C5 prev / heavy / default, C2 / C3 prev / default
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,6 +1,7 @@
 """Per-workgroup timeline of one frame (SHS_OPT_TIMELINE): where each kernel's time goes.
 
 usage (GPU box): python tools/timeline.py [c2|c1|c3] [debug_flags]
+(debug_flags act only in the experiments build: SHS_GPU_LIB=leisure-software-renderer_amd/shs_gpu/libshs_gpu_exp.so)
 Prints, per kernel and block role, start/end offsets (us) relative to the first k_setup workgroup
 start, and duration percentiles."""
 import os
