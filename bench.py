@@ -470,7 +470,7 @@ def strong_legs(args, rank, local_rank, world, dist):
     out = {}
     for cfg in args.strong:
         a = copy.copy(args)
-        a.config, a.steps, a.warmup = cfg, args.strong_frames, 10
+        a.config, a.steps, a.warmup = cfg, args.strong_frames, 20
         a.shard_layout, a.inflight = "regions", 3
         runner = run_gpu_c4 if cfg == "c4" else run_gpu_lib
         frame, stats, elapsed, n_frames, kms, _, _, n_tri, _, owned = runner(a, rank, local_rank, world, dist)
@@ -548,13 +548,29 @@ def cpu_model():
 
 def hw_threads():
     """std::thread::hardware_concurrency() (the reference's worker count, SURVEY 8d) and the cores this
-    process may run on (its affinity set)."""
+    process may run on: its affinity set, capped by the cgroup CPU quota (cpu.max) when there is one --
+    a container's share of a many-core host, which neither the affinity nor the core count shows."""
     hc = os.cpu_count() or 1
     try:
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = hc
+    q = cgroup_cpu_quota()
+    if q is not None:
+        usable = max(1, min(usable, int(q)))
     return hc, usable
+
+
+def cgroup_cpu_quota():
+    """Cores granted by the cgroup v2 CPU quota (cpu.max "quota period"), or None when unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota == "max":
+            return None
+        return float(quota) / float(period)
+    except (OSError, ValueError):
+        return None
 
 
 def _timed_frames(fn, seconds, max_frames=100000):
@@ -631,6 +647,8 @@ def cpu_baseline(args):
     covered = int((depth.view(np.uint32) != np.float32(np.finfo(np.float32).max).view(np.uint32)).sum())
     legs = [("single_thread", 1)] if args.config == "c1" else [("hardware_concurrency", hc), ("thread_count_20", 20),
                                                                 ("usable_cores", usable)]
+    # (the tile jobs run on a pool of persistent workers, as the reference's ThreadedPriorityJobSystem;
+    # hardware_concurrency threads on a cgroup quota of fewer cores stall frames on descheduled workers)
     out = {}
     for name, threads in legs:
         frames, el, med = _timed_frames(
@@ -643,7 +661,7 @@ def cpu_baseline(args):
     head = out[head_name]
     return {"value": head["mtri_s"], "unit": "Mtri/s", "cores": head["threads"], "kind": "port",
             "median_ms_per_frame": head["median_ms_per_frame"], "mpix_s": head["mpix_s"], "cpu_model": cpu_model(),
-            "hardware_concurrency": hc, "usable_cores": usable, "legs": out,
+            "hardware_concurrency": hc, "usable_cores": usable, "cgroup_cpu_quota": cgroup_cpu_quota(), "legs": out,
             "sample": f"{head['frames']} frames of the same workload ({frame.width}x{frame.height}, {n_tri} tris, "
                       f"{covered} covered px) in {head['seconds']} s, 80x80 tile jobs on {head['threads']} threads "
                       f"({head_name}; oracle/shs_oracle.c, gcc -O3)"}
@@ -707,7 +725,7 @@ def main():
     ap.add_argument("--strong", default="c4,c5", type=lambda x: [c for c in x.split(",") if c],
                     help="legacy configs: the tile-sharded 4K legs run after the headline loop at every N "
                          "(strong_c4 / strong_c5 keys; '' to skip)")
-    ap.add_argument("--strong-frames", type=int, default=60, help="timed frames of each strong leg")
+    ap.add_argument("--strong-frames", type=int, default=200, help="timed frames of each strong leg")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-frame latency leg (profiling)")

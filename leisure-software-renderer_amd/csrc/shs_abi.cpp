@@ -83,6 +83,7 @@ int shs_destroy(shs_ctx *ctx) {
         if (m.nrm) (void)hipFree(m.nrm);
         if (m.uv) (void)hipFree(m.uv);
         if (m.idx) (void)hipFree(m.idx);
+        if (m.orig) (void)hipFree(m.orig);
         if (m.cbox) (void)hipFree(m.cbox);
     }
     shs_lib_release(ctx);
@@ -156,6 +157,7 @@ int shs_mesh_release(shs_ctx *ctx, int32_t id) {
     HIP_TRY(ctx, hipFree(m.nrm));
     if (m.uv) HIP_TRY(ctx, hipFree(m.uv));
     if (m.idx) HIP_TRY(ctx, hipFree(m.idx));
+    if (m.orig) HIP_TRY(ctx, hipFree(m.orig));
     if (m.cbox) HIP_TRY(ctx, hipFree(m.cbox));
     m = Mesh{};
     return SHS_OK;

@@ -52,7 +52,7 @@ void release_work(Work &w) {
     for (auto &ev : w.ring_ev)
         for (auto &e : ev)
             if (e) { (void)hipEventDestroy(e); e = nullptr; }
-    release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase); release(w.zord);
+    release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase); release(w.zord); release(w.s2s);
     w.dev_table.clear();
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
@@ -86,6 +86,7 @@ void build_lib_draw(const shs_lib_draw &in, const Mesh &m, int32_t base, LibDraw
     std::memset(&o, 0, sizeof o);
     o.pos = m.pos; o.nrm = m.nrm; o.uv = m.uv; o.idx = m.idx;
     o.cbox = m.cbox;
+    o.orig = m.orig;
     o.n_verts = m.n_verts;
     o.tri_base = base;
     o.n_tris = m.n_tris;
@@ -282,6 +283,14 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     if (!shadow && (ensure(ctx, w.shade, n_slots) || ensure(ctx, w.xbase, (size_t)std::max(n_tris, 1)) ||
                     ensure(ctx, w.clipq, (size_t)std::max(n_tris, 1))))
         return SHS_ERR_HIP;
+    bool permuted = false;   // a spatially ordered mesh: the resolve maps winners to slots through s2s
+    for (const auto &d : w.last_draws) permuted = permuted || d.orig != nullptr;
+    if (!shadow && permuted) {
+        if (ensure(ctx, w.s2s, (size_t)std::max(n_tris, 1))) return SHS_ERR_HIP;
+        fp.flags |= shs_dev::LF_PERM;
+    } else {
+        fp.flags &= ~shs_dev::LF_PERM;
+    }
     bool textured = false;
     for (const auto &d : w.last_draws) textured = textured || d.tex != nullptr;
     if (textured && !shadow) {
@@ -416,6 +425,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.tile_count = w.tile_count.p; fb.bins = w.bins.p; fb.spill = w.spill.p; fb.counters = w.counters.p;
     fb.busy = w.busy.p; fb.blk_stat = w.blk_stat.p; fb.rstat = w.rstat.p;
     fb.clipq = w.clipq.p; fb.bigq = w.bigq.p; fb.bigpre = w.bigpre.p;
+    fb.s2s = (fp.flags & shs_dev::LF_PERM) ? w.s2s.p : nullptr;
     fb.dbase = reinterpret_cast<int32_t *>(w.draws.p + nd);
     fb.bdraw = fb.dbase + nd + 1;
     fb.rqueue = w.rqueue.p;
@@ -649,6 +659,63 @@ void shs_lib_release(shs_ctx *ctx) {
     ctx->h_lib_counters = nullptr;
 }
 
+// The stored order of a library mesh's triangles: MeshData indices sorted by the 30-bit Morton code of
+// the centroid in the mesh's bounds (stable; triangles with an out-of-range index or a non-finite
+// centroid last).  Empty when the mesh fits one chunk or the order is the identity.
+static std::vector<uint32_t> spatial_order(const float *pos, int32_t n_verts, const uint32_t *idx, int32_t n_tris) {
+    std::vector<uint32_t> order;
+    if (n_tris <= 256) return order;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    std::vector<float> cen((size_t)n_tris * 3);
+    std::vector<uint8_t> ok((size_t)n_tris);
+    for (int32_t t = 0; t < n_tris; ++t) {
+        bool good = true;
+        float c[3] = {0.0f, 0.0f, 0.0f};
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t v = idx ? idx[3 * (size_t)t + k] : (uint32_t)(3 * t + k);
+            if (v >= (uint32_t)n_verts) { good = false; break; }
+            for (int q = 0; q < 3; ++q) c[q] += pos[3 * (size_t)v + q];
+        }
+        for (int q = 0; q < 3 && good; ++q) good = std::isfinite(c[q]);
+        ok[t] = good;
+        for (int q = 0; q < 3; ++q) {
+            cen[3 * (size_t)t + q] = c[q];
+            if (good) { lo[q] = std::min(lo[q], c[q]); hi[q] = std::max(hi[q], c[q]); }
+        }
+    }
+    auto spread = [](uint32_t x) {   // 10 bits -> every third bit
+        x &= 0x3ffu;
+        x = (x | (x << 16)) & 0x030000ffu;
+        x = (x | (x << 8)) & 0x0300f00fu;
+        x = (x | (x << 4)) & 0x030c30c3u;
+        x = (x | (x << 2)) & 0x09249249u;
+        return x;
+    };
+    std::vector<uint64_t> key((size_t)n_tris);
+    for (int32_t t = 0; t < n_tris; ++t) {
+        uint32_t code = 0xffffffffu;
+        if (ok[t]) {
+            code = 0u;
+            for (int q = 0; q < 3; ++q) {
+                const float ext = hi[q] - lo[q];
+                const float u = ext > 0.0f ? (cen[3 * (size_t)t + q] - lo[q]) / ext : 0.0f;
+                const uint32_t b = (uint32_t)std::min(1023.0f, std::max(0.0f, u * 1024.0f));
+                code |= spread(b) << q;
+            }
+        }
+        key[t] = ((uint64_t)code << 32) | (uint32_t)t;   // ties keep the MeshData order
+    }
+    std::sort(key.begin(), key.end());
+    order.resize((size_t)n_tris);
+    bool identity = true;
+    for (int32_t p = 0; p < n_tris; ++p) {
+        order[p] = (uint32_t)key[p];
+        identity = identity && order[p] == (uint32_t)p;
+    }
+    if (identity) order.clear();
+    return order;
+}
+
 extern "C" {
 
 int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const float *normals, int32_t n_normals,
@@ -672,6 +739,39 @@ int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const
     m.lib = true;
     m.n_verts = n_verts;
     m.n_tris = (int32_t)n_tris;
+    if (indices && n_indices < 3) m.n_tris = 0;
+    // Spatial order (meshes over one 256-triangle chunk): the triangles are stored sorted by the Morton
+    // code of their centroid, so a setup block's chunk box is tight and a region-sharded rank skips the
+    // blocks that miss its rectangle.  The submission order stays the MeshData order:
+    // `orig` gives every stored triangle its MeshData index, the sequence the z ties and the clipped
+    // fans are ordered by (rasterizer.hpp:181-442 draws in index order).  A soup's vertices move with
+    // their triangle; an indexed mesh keeps its vertices and reorders its index triples.
+    const std::vector<uint32_t> order = spatial_order(positions, n_verts, indices, m.n_tris);
+    std::vector<float> pos_s, nrm_s, uv_s;
+    std::vector<uint32_t> idx_s;
+    if (!order.empty()) {
+        if (indices) {
+            idx_s.resize((size_t)m.n_tris * 3);
+            for (size_t p = 0; p < order.size(); ++p)
+                for (int k = 0; k < 3; ++k) idx_s[3 * p + k] = indices[3 * (size_t)order[p] + k];
+            indices = idx_s.data();
+        } else {
+            pos_s.assign(positions, positions + (size_t)n_verts * 3);
+            nrm_s = nrm;
+            uv_s = uv;
+            for (size_t p = 0; p < order.size(); ++p)
+                for (int k = 0; k < 3; ++k) {
+                    const size_t dv = 3 * p + k, sv = 3 * (size_t)order[p] + k;
+                    for (int q = 0; q < 3; ++q) { pos_s[3 * dv + q] = positions[3 * sv + q]; nrm_s[3 * dv + q] = nrm[3 * sv + q]; }
+                    uv_s[2 * dv] = uv[2 * sv]; uv_s[2 * dv + 1] = uv[2 * sv + 1];
+                }
+            positions = pos_s.data();
+            nrm.swap(nrm_s);
+            uv.swap(uv_s);
+        }
+        HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.orig), order.size() * sizeof(uint32_t)));
+        HIP_TRY(ctx, hipMemcpy(m.orig, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     // model-space bounds (PassShadowMap's mesh_bounds_cache, pass_shadow_map.hpp:90-102)
     for (int k = 0; k < 3; ++k) { m.bmin[k] = 3.402823466e38f; m.bmax[k] = -3.402823466e38f; }
     for (int32_t i = 0; i < n_verts; ++i)
@@ -689,8 +789,6 @@ int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const
     if (indices && n_indices >= 3) {
         HIP_TRY(ctx, hipMalloc(reinterpret_cast<void **>(&m.idx), (size_t)n_tris * 3 * sizeof(uint32_t)));
         HIP_TRY(ctx, hipMemcpy(m.idx, indices, (size_t)n_tris * 3 * sizeof(uint32_t), hipMemcpyHostToDevice));
-    } else if (indices) {
-        m.n_tris = 0;
     }
     if (m.n_tris > 0) {   // chunk boxes (k_lib_setup's block bounds): out-of-range indices are skipped there
         const int64_t n_chunks = ((int64_t)m.n_tris + 255) / 256;

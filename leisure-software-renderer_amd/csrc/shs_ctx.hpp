@@ -40,6 +40,7 @@ struct Mesh {
     int32_t n_verts = 0;
     float bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
     float4 *cbox = nullptr;          // library mesh: per 256-triangle chunk its model-space box (min, max)
+    uint32_t *orig = nullptr;        // library mesh stored in spatial order: per stored triangle its MeshData index
 };
 
 // A Texture2DData (resources/texture.hpp:23-49) on the device: w * h Color texels, y * w + x.
@@ -161,6 +162,7 @@ struct shs_ctx {
         DevBuf<shs_dev::LibShade> shade;
         DevBuf<uint2> boxes;
         DevBuf<uint32_t> xbase, zord, tile_count, counters, busy, clipq, bigpre;
+        DevBuf<uint32_t> s2s;                              // LF_PERM: per input triangle (submission order) its slot
         DevBuf<uint4> bins;                                // per bin tile, bin_cap entries (slot, box, depth bound)
         DevBuf<uint4> bigq;
         DevBuf<uint32_t> rqueue;

@@ -25,7 +25,8 @@
 //                 every output byte is written exactly once per pass.
 // Primitive order: input triangle t's fan triangle k has submission index t*16 + k (a clipped
 // triangle yields at most 7 fans in exact arithmetic, MAX_POLY - 2 with rounding); fan 0 lives in
-// slot t, fans >= 1 in extra slots from xbase[t].
+// slot t, fans >= 1 in extra slots from xbase[t].  t is the submission index (draw base + MeshData
+// index); a spatially ordered mesh stores triangle t at another slot, which the setup records in s2s.
 #include <float.h>
 
 #include <algorithm>
@@ -515,6 +516,12 @@ __device__ __forceinline__ int lib_find_draw(const int32_t *dbase, int n_draws, 
     return lo;
 }
 
+// The submission index of pass triangle `tri` (its slot): the draw's base + the triangle's MeshData index
+// (a spatially ordered mesh stores its triangles in another order, LibDrawGPU::orig).
+__device__ __forceinline__ uint32_t lib_sub_tri(const LibDrawGPU &dr, int tri) {
+    return dr.orig ? (uint32_t)dr.tri_base + dr.orig[tri - dr.tri_base] : (uint32_t)tri;
+}
+
 __device__ __forceinline__ bool read_tri(const LibDrawGPU &dr, int local, uint32_t (&id)[3]) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) id[k] = dr.idx ? dr.idx[3 * (size_t)local + k] : (uint32_t)(3 * local + k);
@@ -561,7 +568,9 @@ __device__ __forceinline__ bool setup_camera_tri(const LibFrameParams &fp, const
     LVert t[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) t[k] = vertex_pos(dr, id[k]);
-    const uint32_t seq0 = (uint32_t)tri * 16u;
+    const uint32_t sub = lib_sub_tri(dr, tri);
+    if (fp.flags & LF_PERM) fb.s2s[sub] = (uint32_t)tri;   // the resolve's winner -> slot map
+    const uint32_t seq0 = sub * 16u;
     if (fully_inside(t[0]) && fully_inside(t[1]) && fully_inside(t[2])) {
         emit_fan(fp, fb, cnt, dr, d, seq0, (uint32_t)tri, t[0], t[1], t[2], n_clip, n_rast, ss, pend, id);
         return false;
@@ -1116,7 +1125,7 @@ __global__ __launch_bounds__(256) void k_lib_clip(LibFrameParams fp, LibBuffers 
         const LVert pk1 = grp_shfl_v(v, seg + (k < m ? l2 : 0));
         if (k >= 1 && k + 1 < m) {
             const uint32_t slot = k == 1 ? (uint32_t)tri : xb + (uint32_t)(k - 2);
-            emit_fan<true>(fp, fb, cnt, dr, d, (uint32_t)tri * 16u + (uint32_t)(k - 1), slot, p0, pk, pk1, n_clip, n_rast,
+            emit_fan<true>(fp, fb, cnt, dr, d, lib_sub_tri(dr, tri) * 16u + (uint32_t)(k - 1), slot, p0, pk, pk1, n_clip, n_rast,
                            ss_unused, pend);
         }
     }
@@ -1730,7 +1739,8 @@ __device__ __forceinline__ float4 lib_resolve(const LibFrameParams &fp, const Li
     float2 mv = make_float2(0.0f, 0.0f);
     if (covered) {
         const uint32_t seq = (fp.flags & LF_DEPTH) ? (uint32_t)key : 0xffffffffu - (uint32_t)key;
-        const uint32_t tri = seq >> 4, k = seq & 15u;
+        const uint32_t k = seq & 15u;
+        const uint32_t tri = (fp.flags & LF_PERM) ? fb.s2s[seq >> 4] : seq >> 4;   // submission -> stored order
         const uint32_t slot = k == 0 ? tri : fb.xbase[tri] + k - 1u;
         const LibRec r = fb.recs[slot];
         const LibShade s = fb.shade[slot];

@@ -35,6 +35,7 @@ struct alignas(16) LibDrawGPU {
     const uint32_t *tex;     // u.base_color_tex: Texture2DData texels (Color RGBA8, y * w + x), or null
     int32_t tex_w, tex_h;
     const float4 *cbox;      // model-space bounds of the mesh's 256-triangle chunks (min, max per chunk)
+    const uint32_t *orig;    // spatially ordered mesh: per stored triangle its submission (MeshData) index, or null
 };
 
 // Raster record of one primitive (a fan triangle of a clipped input triangle, or a shadow-pass
@@ -87,6 +88,7 @@ constexpr uint32_t LF_DEPTH = 1u;       // target.depth_motion present: strict-l
 constexpr uint32_t LF_LINZ = 2u;        // ... with zf > zn + 1e-6: linear view depth
 constexpr uint32_t LF_MOTION = 4u;      // motion buffer written (per draw: enable_motion_vectors)
 constexpr uint32_t LF_GRADIENT = 8u;    // PassPBRForward's no-sky background gradient, else clear[]
+constexpr uint32_t LF_PERM = 16u;       // a draw's mesh is stored in spatial order: winners map to slots via s2s
 
 // counters[] (two parity sets, frame f uses set f & 1, k_lib_setup zeroes the other)
 // LC_CLIPQ: input triangles queued for k_lib_clip; LC_BIGT / LC_BIGQ: the large-primitive queue's
@@ -169,6 +171,7 @@ struct LibBuffers {
     float4 *uvw;                     // per slot, 2 float4: UV0 varying * 1/w of the 3 corners (textured draws)
     const float *srgb_lut;           // srgb_to_linear_rgb's 256 values, std::pow(c / 255.0f, 2.2f) on the host
     uint2 *items;                    // k_lib_plan: raster work items (rt_order position, part | parts << 16)
+    uint32_t *s2s;                   // camera pass with LF_PERM: per input triangle in submission order, its slot
     uint4 *blkrect;                  // camera pass: per setup block (bx0 | bx1 << 16, by0 | by1 << 16, triangles,
                                      // bounded) of its chunk bounds, mapped host memory (the region balancer's input)
 };
