@@ -52,12 +52,12 @@ void release_work(Work &w) {
     for (auto &ev : w.ring_ev)
         for (auto &e : ev)
             if (e) { (void)hipEventDestroy(e); e = nullptr; }
-    release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase); release(w.zord); release(w.s2s);
+    release(w.draws); release(w.recs); release(w.shade); release(w.boxes); release(w.xbase); release(w.zord); release(w.s2s); release(w.blist);
     w.dev_table.clear();
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.dynq); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.pkeys); release(w.pcount); release(w.dynq); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
     if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
@@ -393,6 +393,15 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         else if (ctx->lib_part < 0 && fp.count > 1) fp.part = 512u;
     }
     if (fp.part && ensure(ctx, w.items, (size_t)std::max(fp.n_owned_rt, 1) * shs_dev::LIB_MAXK)) return SHS_ERR_HIP;
+    if (fp.part) {   // split tiles' key slots: KEY_EMPTY / 0 once, then reset by each tile's last part
+        fp.split_cap = (uint32_t)std::min(std::max(fp.n_owned_rt, 1), 8192);
+        const size_t nk = (size_t)fp.split_cap * shs_dev::LIB_RTH_PX;
+        if (w.pkeys.cap < nk || w.pcount.cap < fp.split_cap) {
+            if (ensure(ctx, w.pkeys, nk) || ensure(ctx, w.pcount, fp.split_cap)) return SHS_ERR_HIP;
+            HIP_TRY(ctx, hipMemsetAsync(w.pkeys.p, 0xff, w.pkeys.cap * sizeof(unsigned long long), ps));
+            HIP_TRY(ctx, hipMemsetAsync(w.pcount.p, 0, w.pcount.cap * sizeof(uint32_t), ps));
+        }
+    }
     // the shallow raster (256-candidate rounds, twice the workgroups per CU) when the previous frame's
     // fullest bin tile fit one such round (scan mode: every primitive is a candidate)
     const uint64_t fullest = fp.scan_mode ? (uint64_t)n_tris + (shadow ? 0u : w.st_extra) : w.st_maxbin;
@@ -431,6 +440,8 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.rqueue = w.rqueue.p;
     fb.dynq = shadow ? nullptr : w.dynq.p;
     fb.items = fp.part ? w.items.p : nullptr;
+    fb.pkeys = fp.part ? w.pkeys.p : nullptr;
+    fb.pcount = fp.part ? w.pcount.p : nullptr;
     // Tile-sharded camera pass in bin mode: each setup workgroup first keeps the rank's triangles of its
     // inputs, positions only (SHS_OPT_SHARD_CULL 0: off).
     const bool listed = !shadow && !fp.scan_mode && fp.count > 1 && !fp.reg.on && ctx->shard_cull;
@@ -451,6 +462,8 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
             w.blkrect_cap = cap;
         }
         fb.blkrect = w.h_blkrect;
+        if (ensure(ctx, w.blist, (size_t)setup_blocks)) return SHS_ERR_HIP;
+        fb.blist = w.blist.p;
         w.blkrect_n = setup_blocks;
         w.blkrect_w = W;
         w.blkrect_h = H;

@@ -162,6 +162,9 @@ struct shs_ctx {
         DevBuf<shs_dev::LibShade> shade;
         DevBuf<uint2> boxes;
         DevBuf<uint32_t> xbase, zord, tile_count, counters, busy, clipq, bigpre;
+        DevBuf<unsigned long long> pkeys;                 // split tiles' merged keys (k_lib_plan parts)
+        DevBuf<uint32_t> pcount;                          // ... and finished parts
+        DevBuf<uint32_t> blist;                            // region-sharded camera pass: listed setup blocks
         DevBuf<uint32_t> s2s;                              // LF_PERM: per input triangle (submission order) its slot
         DevBuf<uint4> bins;                                // per bin tile, bin_cap entries (slot, box, depth bound)
         DevBuf<uint4> bigq;

@@ -832,84 +832,97 @@ __device__ __forceinline__ bool cull_keep(const LibFrameParams &fp, const LibDra
     return clip_reaches_rank(fp, t);
 }
 
-// Camera pass: the screen bounds of setup block b's triangles from their 256-triangle chunks'
-// model-space boxes (LibDrawGPU::cbox; wave 0, one lane per box corner).  Every point of a box whose
-// corners are all in front of the eye projects inside the hull of the projected corners, so the bin
-// tiles of that bbox (2 px of margin for the rounding of the per-vertex transforms, as
-// clip_reaches_rank) bound every fan of every triangle of the block ("bounded").  A box with corners
-// behind the eye gets an estimate instead: the hull of the part of the box with clip w >= 1e-3 of its
-// largest |w| (corners there and box edges cut at that w) -- what a floor reaching behind the camera
-// covers -- used as a cost estimate only, never to skip.  The bounds go to fb.blkrect (the region
-// balancer's input, shs_abi_shard.cpp; w: 1 bounded, 2 estimate, 0 none -- a block straddling draws).
-// -> true when the pass is region-sharded and bounded bounds miss the rank's rectangle: no triangle of
-// the block can reach this rank.  Block-uniform.
-__device__ bool setup_block_bounds(const LibFrameParams &fp, const LibBuffers &fb, int b, int tid) {
-    __shared__ int s_skip;
-    if (tid < 64) {
+// Region-sharded camera pass, before k_lib_setup (one thread per setup block): the screen bounds of
+// block b's triangles from their 256-triangle chunks' model-space boxes (LibDrawGPU::cbox, 8 corners
+// each).  Every point of a box whose corners are all in front of the eye projects inside the hull of
+// the projected corners, so the bin tiles of that bbox (2 px of margin for the rounding of the
+// per-vertex transforms, as clip_reaches_rank) bound every fan of every triangle of the block
+// ("bounded").  A box with corners behind the eye gets an estimate instead: the hull of the part of the
+// box with clip w >= 1e-3 of its largest |w| (corners there and box edges cut at that w) -- what a floor
+// reaching behind the camera covers -- used as a cost estimate only, never to skip.  The bounds go to
+// fb.blkrect (the region balancer's input, shs_abi_shard.cpp; w: 1 bounded, 2 estimate, 0 none -- a
+// block straddling draws).  A block whose bounded bounds miss the rank's rectangle needs no setup (its
+// statistics are zero; scan mode: its slots read as not rasterised); the others are listed in
+// fb.blist, and k_lib_setup's workgroup i sets up listed block i -- the rank's setup grid holds no
+// workgroup that only finds it has nothing to do (C4 rank 3 of 8: 2,100 of its 3,907 workgroups were
+// such, ~4.6 us of a workgroup slot each, a quarter of the kernel).
+__global__ __launch_bounds__(256) void k_lib_blocks(LibFrameParams fp, LibBuffers fb) {
+    const int b = (int)(blockIdx.x * 256 + threadIdx.x);
+    uint32_t *cnt = fb.counters + fp.parity * LC_N;
+    bool keep = false;
+    if (b < fp.setup_blocks) {
         const int t0 = b * 256, t1 = min(t0 + 255, fp.n_tris - 1);
         const int d = fb.bdraw[b];
         const LibDrawGPU &dr = fb.draws[d];
         const bool have = t0 <= t1 && (d + 1 >= fp.n_draws || fb.dbase[d + 1] > t1) && dr.cbox != nullptr;
         bool bounded = false, finite = false;
         float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
-        if (have) {   // wave-uniform
+        if (have) {
             const int c0 = (t0 - dr.tri_base) >> 8, c1 = (t1 - dr.tri_base) >> 8;   // at most two chunks
-            const int c = c0 + ((tid >> 3) & 1);
-            const bool mine = tid < 16 && c <= c1;
-            f4 cp = {0.0f, 0.0f, 0.0f, 1.0f};
-            if (mine) {
-                const float4 mn = dr.cbox[2 * c], mx = dr.cbox[2 * c + 1];
-                const int k = tid & 7;
-                cp = m4v(dr.viewproj, m4v(dr.model, f4{(k & 1) ? mx.x : mn.x, (k & 2) ? mx.y : mn.y, (k & 4) ? mx.z : mn.z, 1.0f}));
-            }
-            const bool fin = !mine || (isfinite(cp.x) && isfinite(cp.y) && isfinite(cp.w));
-            finite = __ballot(!fin) == 0ull;
-            bounded = finite && __ballot(mine && !(cp.w > 0.0f)) == 0ull;
-            float wmax = fabsf(cp.w);
-            for (int o = 1; o < 16; o <<= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o));
-            const float eps = bounded ? 0.0f : 1e-3f * wmax;
             auto add = [&](float cx, float cy, float cw) {
                 const float sx = (cx / cw * 0.5f + 0.5f) * (float)(fp.W - 1);
                 const float sy = (cy / cw * 0.5f + 0.5f) * (float)(fp.H - 1);
                 x0 = fminf(x0, sx); x1 = fmaxf(x1, sx); y0 = fminf(y0, sy); y1 = fmaxf(y1, sy);
             };
-            if (mine && cp.w > eps) add(cp.x, cp.y, cp.w);
+            finite = true;
+            bounded = true;
+            float wmax = 0.0f;
+            f4 cp[2][8];
 #pragma unroll
-            for (int m = 1; m < 8; m <<= 1) {   // the box edges from this corner, cut at w = eps
-                const float nx = __shfl_xor(cp.x, m), ny = __shfl_xor(cp.y, m), nw = __shfl_xor(cp.w, m);
-                if (mine && !bounded && (cp.w - eps) * (nw - eps) < 0.0f) {
-                    const float t = (eps - cp.w) / (nw - cp.w);
-                    add(cp.x + (nx - cp.x) * t, cp.y + (ny - cp.y) * t, eps);
+            for (int ci = 0; ci < 2; ++ci) {
+                const int c = min(c0 + ci, c1);
+                const float4 mn = dr.cbox[2 * c], mx = dr.cbox[2 * c + 1];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    cp[ci][k] = m4v(dr.viewproj, m4v(dr.model, f4{(k & 1) ? mx.x : mn.x, (k & 2) ? mx.y : mn.y, (k & 4) ? mx.z : mn.z, 1.0f}));
+                    finite = finite && isfinite(cp[ci][k].x) && isfinite(cp[ci][k].y) && isfinite(cp[ci][k].w);
+                    bounded = bounded && cp[ci][k].w > 0.0f;
+                    wmax = fmaxf(wmax, fabsf(cp[ci][k].w));
                 }
             }
-            for (int o = 1; o < 16; o <<= 1) {
-                x0 = fminf(x0, __shfl_xor(x0, o));
-                x1 = fmaxf(x1, __shfl_xor(x1, o));
-                y0 = fminf(y0, __shfl_xor(y0, o));
-                y1 = fmaxf(y1, __shfl_xor(y1, o));
+            bounded = bounded && finite;
+            const float eps = bounded ? 0.0f : 1e-3f * wmax;
+            if (finite) {
+#pragma unroll
+                for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const f4 p = cp[ci][k];
+                        if (p.w > eps) add(p.x, p.y, p.w);
+                        if (bounded) continue;
+#pragma unroll
+                        for (int m = 1; m < 8; m <<= 1) {   // the box edges from this corner, cut at w = eps
+                            const f4 n = cp[ci][k ^ m];
+                            if ((p.w - eps) * (n.w - eps) < 0.0f) {
+                                const float t = (eps - p.w) / (n.w - p.w);
+                                add(p.x + (n.x - p.x) * t, p.y + (n.y - p.y) * t, eps);
+                            }
+                        }
+                    }
             }
         }
-        if (tid == 0) {
-            int bx0 = 0, bx1 = fp.tiles_x - 1, by0 = 0, by1 = fp.tiles_y - 1;
-            const bool est = finite && !(x1 < x0);   // some point in front of the eye
-            if (finite && (bounded || est)) {
-                if (!(x1 >= -2.0f && y1 >= -2.0f && x0 <= (float)fp.W + 1.0f && y0 <= (float)fp.H + 1.0f)) {
-                    bx0 = 1; bx1 = 0; by0 = 1; by1 = 0;   // off screen: no fan reaches a pixel
-                } else {
-                    bx0 = max(0, (int)fmaxf(x0 - 2.0f, 0.0f) / TILE);
-                    bx1 = min(fp.tiles_x - 1, (int)fminf(x1 + 2.0f, (float)(fp.W - 1)) / TILE);
-                    by0 = max(0, (int)fmaxf(y0 - 2.0f, 0.0f) / TILE);
-                    by1 = min(fp.tiles_y - 1, (int)fminf(y1 + 2.0f, (float)(fp.H - 1)) / TILE);
-                }
+        int bx0 = 0, bx1 = fp.tiles_x - 1, by0 = 0, by1 = fp.tiles_y - 1;
+        const bool est = finite && !(x1 < x0);   // some point in front of the eye
+        if (finite && (bounded || est)) {
+            if (!(x1 >= -2.0f && y1 >= -2.0f && x0 <= (float)fp.W + 1.0f && y0 <= (float)fp.H + 1.0f)) {
+                bx0 = 1; bx1 = 0; by0 = 1; by1 = 0;   // off screen: no fan reaches a pixel
+            } else {
+                bx0 = max(0, (int)fmaxf(x0 - 2.0f, 0.0f) / TILE);
+                bx1 = min(fp.tiles_x - 1, (int)fminf(x1 + 2.0f, (float)(fp.W - 1)) / TILE);
+                by0 = max(0, (int)fmaxf(y0 - 2.0f, 0.0f) / TILE);
+                by1 = min(fp.tiles_y - 1, (int)fminf(y1 + 2.0f, (float)(fp.H - 1)) / TILE);
             }
-            fb.blkrect[b] = make_uint4((uint32_t)bx0 | ((uint32_t)bx1 << 16), (uint32_t)by0 | ((uint32_t)by1 << 16),
-                                       (uint32_t)max(0, t1 - t0 + 1), bounded ? 1u : (finite && est) ? 2u : 0u);
-            s_skip = (fp.count > 1 && fp.reg.on && bounded && !shard_owns_any(fp.rank, fp.count, fp.reg, bx0, bx1, by0, by1, fp.tiles_x))
-                         ? 1 : 0;
+        }
+        fb.blkrect[b] = make_uint4((uint32_t)bx0 | ((uint32_t)bx1 << 16), (uint32_t)by0 | ((uint32_t)by1 << 16),
+                                   (uint32_t)max(0, t1 - t0 + 1), bounded ? 1u : (finite && est) ? 2u : 0u);
+        keep = !(bounded && !shard_owns_any(fp.rank, fp.count, fp.reg, bx0, bx1, by0, by1, fp.tiles_x));
+        if (!keep) {   // no triangle of the block reaches this rank
+            fb.blk_stat[b] = make_uint2(0u, 0u);
+            if (fp.scan_mode)
+                for (int t = t0; t <= t1; ++t) store_box(fb, (uint32_t)t, 0, -1, 0, -1);
         }
     }
-    __syncthreads();
-    return s_skip != 0;
+    wave_append(&cnt[LC_BLOCKS], fb.blist, keep, (uint32_t)b);
 }
 
 template <bool SHADOW, bool LISTED = false>
@@ -918,27 +931,30 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     constexpr bool listed = !SHADOW && LISTED;
     __shared__ uint2 s_kept[listed ? 256 * CULL_PER : 1];   // (triangle, draw)
     __shared__ uint32_t s_nkept;
-    const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
+    int b = (int)blockIdx.x;   // the setup block (triangles b * 256 ...)
+    const int tid = (int)threadIdx.x;
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
     const bool stl = fb.stimeline != nullptr && tid == 0;
     const uint64_t st0 = stl ? tl_now() : 0ull;
     if (listed && tid == 0) s_nkept = 0u;
+    // region-sharded camera pass: workgroup i sets up k_lib_blocks' listed block i; the workgroups past
+    // the list only do their share of the next frame's zeroing
+    const int wg = b;
     if constexpr (!SHADOW && !listed) {
-        if (fb.blkrect != nullptr && setup_block_bounds(fp, fb, b, tid)) {
-            // region-sharded pass, block off the rank's rectangle: its share of the next frame's zeroing,
-            // and its slots read as not rasterised
-            setup_zero_next(fp, fb, b, tid);
-            const int t = b * 256 + tid;
-            if (t < fp.n_tris) store_box(fb, (uint32_t)t, 0, -1, 0, -1);
-            if (tid == 0 && b < fp.setup_blocks) fb.blk_stat[b] = make_uint2(0u, 0u);
-            if (fb.stimeline && tid == 0) {
-                uint64_t *o = fb.stimeline + (size_t)b * STL_STRIDE;
-                o[0] = st0; o[1] = o[2] = o[3] = tl_now(); o[4] = o[5] = o[6] = o[7] = 0ull;
+        if (fb.blist != nullptr) {
+            const uint32_t n_listed = cnt[LC_BLOCKS];
+            if ((uint32_t)wg >= n_listed) {
+                setup_zero_next(fp, fb, wg, tid);
+                if (fb.stimeline && tid == 0) {
+                    uint64_t *o = fb.stimeline + (size_t)wg * STL_STRIDE;
+                    o[0] = st0; o[1] = o[2] = o[3] = tl_now(); o[4] = o[5] = o[6] = o[7] = 0ull;
+                }
+                return;
             }
-            return;
+            b = (int)fb.blist[wg];
         }
     }
-    setup_prologue(fp, fb, ss, b, tid);
+    setup_prologue(fp, fb, ss, wg, tid);
     // the triangles: b * 256 + tid (one chunk per block), or (tile-sharded camera pass) the block's kept
     // triangles of its CULL_PER x 256 inputs, 256 per round
     uint32_t pre_clip = 0u, pre_rast = 0u;
@@ -1068,7 +1084,7 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
     if (fb.stimeline) {
         __syncthreads();
         if (tid == 0) {
-            uint64_t *o = fb.stimeline + (size_t)b * STL_STRIDE;
+            uint64_t *o = fb.stimeline + (size_t)wg * STL_STRIDE;
             o[0] = st0; o[1] = st1; o[2] = st2; o[3] = tl_now(); o[4] = nbig; o[5] = (uint64_t)uwh;
             o[6] = stf; o[7] = listed ? (uint64_t)n_items : 0ull;
         }
@@ -1698,6 +1714,7 @@ struct LibShared {
     uint32_t zlo, zhi;
     uint32_t wtot[4][2];                  // per wave: surviving candidates, pairs
     uint32_t wmax[4];                     // deep camera raster: per wave, the largest key z of its pixels after a pass
+    uint32_t last;                        // split tile: this part finished last (it writes the merged keys)
     uint32_t colmax[2][LIB_RTW];          // per pixel column: max key z (orderable bits) over its rows, by chunk parity
     uint32_t nc, nbusy, cov, maxbin, npairs;
     int next[4];                          // the workgroup's next item: any, queue, queues tried, its word
@@ -1842,22 +1859,19 @@ __device__ __forceinline__ void lib_row_span(const float4 r0, const float4 r1, i
     x1 = min(bx1, (int)floorf(fmaxf(fminf(fhi + shi, 1e9f), -1e9f)));
 }
 
-// One work item: raster tile rt, or (k_lib_plan) part `part` of `parts` (2: the 32x4 halves, 4: the
-// 16x4 blocks) of it.  A part gathers the tile's list but tests only the pixels of its rectangle and
-// writes only its blocks' keys and flags, so the parts of a hot tile render on several workgroups at
-// once with no merge.  T0 = the tile origin (LDS key layout); X0..Y1 = the item's rectangle.
+// One work item: raster tile rt, or (k_lib_plan, camera pass) part `part` of `parts` of it: the list
+// positions [part n / parts, (part + 1) n / parts) over the whole tile, its keys merged with the other
+// parts' in fb.pkeys[sid] (plan_parts).  T0 = the tile origin (LDS key layout); X0..Y1 = the tile.
 template <bool SHADOW, int LIB_CAND>
 __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt, LibShared<LIB_CAND> &sh,
-                                uint32_t &chunk, uint32_t part = 0u, uint32_t parts = 1u) {
+                                uint32_t &chunk, uint32_t part = 0u, uint32_t parts = 1u, uint32_t sid = 0u) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool hiz = SHADOW || (fp.flags & LF_DEPTH);   // painter's order (no depth target): never
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
     const int TX0 = col * LIB_RTW, TY0 = row * LIB_RTH;
-    const int X0 = TX0 + (parts == 4u ? 16 * (int)(part & 1u) : 0), Y0 = TY0 + (parts == 1u ? 0 : 4 * (int)(part >> (parts == 4u ? 1 : 0)));
-    const int X1 = X0 + (parts == 4u ? 15 : LIB_RTW - 1), Y1 = Y0 + (parts == 1u ? LIB_RTH - 1 : 3);
-    // this thread's pixel (tile layout: wave w = 16x4 block w) and whether the item covers it
+    const int X0 = TX0, Y0 = TY0, X1 = TX0 + LIB_RTW - 1, Y1 = TY0 + LIB_RTH - 1;
+    // this thread's pixel (tile layout: wave w = 16x4 block w)
     const int my_lx = 16 * (wave & 1) + (lane & 15), my_ly = 4 * (wave >> 1) + (lane >> 4);
-    const bool mine = TX0 + my_lx >= X0 && TX0 + my_lx <= X1 && TY0 + my_ly >= Y0 && TY0 + my_ly <= Y1;
     const int bt = (row / (TILE / LIB_RTH)) * fp.tiles_x + col;
     // (no barrier here: the previous tile ended with each thread resetting its own pixel's key, and
     // every round below starts with one before any shared state is touched)
@@ -1877,8 +1891,11 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
     }
     const uint4 *bin = fb.bins + (size_t)bt * fp.bin_cap;
+    // a part's share of the list (positions [lo, n_items))
+    const uint32_t lo = (uint32_t)(((uint64_t)n_items * part) / parts);
+    n_items = (uint32_t)(((uint64_t)n_items * (part + 1u)) / parts);
 
-    for (uint32_t base = 0; base < n_items; base += LIB_CAND) {
+    for (uint32_t base = lo; base < n_items; base += LIB_CAND) {
         __syncthreads();
         if (tid == 0) { sh.nc = 0; sh.zlo = 0xffffffffu; sh.zhi = 0u; }
         sh.hist[tid] = 0u;
@@ -2123,10 +2140,6 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 // only upwards, which selects more, never less); a part counts its own pixels only
                 {
                     uint32_t o = keyhi[2 * tid + 1];
-                    if (parts > 1u) {
-                        const int cx = TX0 + (tid & (LIB_RTW - 1)), cy = TY0 + tid / LIB_RTW;
-                        if (cx < X0 || cx > X1 || cy < Y0 || cy > Y1) o = 0u;
-                    }
 #pragma unroll
                     for (int off = 32; off > 0; off >>= 1) o = max(o, (uint32_t)__shfl_xor((int)o, off));
                     if (lane == 0) sh.wmax[wave] = o;
@@ -2153,10 +2166,6 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
             } else {
                 if (hiz) {   // per pixel column, the largest key z so far
                     uint32_t o = (uint32_t)(sh.key[tid] >> 32);
-                    if (parts > 1u) {   // only the item's pixels bound its hierarchical z
-                        const int cx = TX0 + (tid & (LIB_RTW - 1)), cy = TY0 + tid / LIB_RTW;
-                        if (cx < X0 || cx > X1 || cy < Y0 || cy > Y1) o = 0u;
-                    }
                     o = max(o, (uint32_t)__shfl_xor((int)o, 32));   // a wave holds two rows of the column
                     if (lane < LIB_RTW) atomicMax(&sh.colmax[chunk & 1u][lane], o);
                 }
@@ -2294,21 +2303,35 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     // resolves here, the camera pass hands its keys to k_lib_resolve
     const int lx = my_lx, ly = my_ly;
     const int px = TX0 + lx, py = TY0 + ly;
-    const unsigned long long key = sh.key[ly * LIB_RTW + lx];
+    unsigned long long key = sh.key[ly * LIB_RTW + lx];
     sh.key[ly * LIB_RTW + lx] = KEY_EMPTY;   // this thread's pixel only: clean for the next tile
-    bool covered;
+    bool covered = false;
+    bool write = true;
+    if (!SHADOW && parts > 1u) {
+        // a split tile: merge this part's keys into the tile's pkeys slot; the part that finishes last
+        // takes the merged keys (resetting the slot for the next pass) and writes the winners
+        unsigned long long *pk = fb.pkeys + (size_t)sid * (LIB_RTH * LIB_RTW) + ly * LIB_RTW + lx;
+        if (key != KEY_EMPTY) atomicMin(pk, key);
+        __threadfence();
+        __syncthreads();
+        if (tid == 0) sh.last = atomicAdd(&fb.pcount[sid], 1u) == parts - 1u ? 1u : 0u;
+        __syncthreads();
+        write = sh.last != 0u;   // block-uniform
+        if (write) {
+            __threadfence();
+            key = atomicExch(pk, KEY_EMPTY);   // (device-scope: never a stale L1 line)
+            if (tid == 0) fb.pcount[sid] = 0u;
+        }
+    }
     if (SHADOW) {
         lib_resolve<SHADOW>(fp, fb, key, px, py, covered);
-    } else {
+    } else if (write) {
         // keys only for 16x4 blocks holding a winner; the block's flag tells k_lib_resolve which
         // (the wave's block is sub-block `wave` of the tile, k_lib_resolve's numbering)
-        // (a part writes only its own blocks: `mine` is wave-uniform)
         covered = key != KEY_EMPTY && px < fp.W && py < fp.H;
         const bool any = __ballot(covered) != 0ull;
-        if (mine) {
-            if (any && px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = lib_winner_word(fp, key);
-            if (lane == 0) fb.blkcov[(size_t)rt * 4 + wave] = any ? 1u : 0u;
-        }
+        if (any && px < fp.W && py < fp.H) fb.keys[(size_t)py * fp.W + px] = lib_winner_word(fp, key);
+        if (lane == 0) fb.blkcov[(size_t)rt * 4 + wave] = any ? 1u : 0u;
     }
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
@@ -2336,16 +2359,20 @@ __device__ __forceinline__ void lib_clear_shadow_tile(const LibFrameParams &fp, 
 }
 
 // The camera pass's raster work plan, after the marks are final (one thread per owned raster tile):
-// a busy tile whose bin list holds more than fp.part entries is split into its two 32x4 halves, above
-// 4 * fp.part into its four 16x4 blocks; the parts (cnt[LC_ITEMS] of them, in fb.items) are rendered
-// first, by any workgroups at once, then the owned tiles in order with the split ones skipped.  The
-// hottest tiles no longer bound the raster (C4 at 8 shards: ~2 busy tiles per workgroup, 20-75 us each).
+// a busy tile whose candidate list holds more than fp.part entries is split into ceil(n / fp.part)
+// parts (at most LIB_MAXK), part j taking list positions [j n / k, (j + 1) n / k) over the whole tile.
+// Each part resolves its own candidates' keys in LDS and merges them into the tile's slot of
+// fb.pkeys with 64-bit atomicMin -- min is order-free, so the merged keys are the tile's keys -- and
+// the part that finishes last writes the winners.  The parts (cnt[LC_ITEMS] of them, in fb.items) are
+// the first work items, rendered by any workgroups at once, then the owned tiles in order with the
+// split ones skipped.  The densest tiles no longer bound a sharded rank's raster (C4 rank 3 of 8: a
+// ~2,800-candidate tile took one workgroup 72-84 us of a 119-us raster).
 __device__ __forceinline__ uint32_t plan_parts(const LibFrameParams &fp, const LibBuffers &fb, const uint32_t *cnt, int rt) {
     if (!fb.busy[rt]) return 1u;
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
     const uint32_t total = fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + (row / (TILE / LIB_RTH)) * fp.tiles_x + col];
     const uint32_t n = min(total, fp.bin_cap) + (total > fp.bin_cap ? min(cnt[LC_SPILL], fp.spill_cap) : 0u);
-    return n > 4u * fp.part ? 4u : n > fp.part ? 2u : 1u;
+    return min((uint32_t)LIB_MAXK, (n + fp.part - 1u) / fp.part);
 }
 
 // k_lib_raster's work items: position j < n_split is k_lib_plan's part j (word 0x80000000 | j), the rest
@@ -2408,11 +2435,20 @@ __global__ __launch_bounds__(256) void k_lib_plan(LibFrameParams fp, LibBuffers 
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
     const int j = (int)(blockIdx.x * 256 + threadIdx.x);
     const int rt = j < fp.n_owned_rt ? fb.rt_order[j] : 0;
-    const uint32_t k = j < fp.n_owned_rt ? plan_parts(fp, fb, cnt, rt) : 1u;
+    uint32_t k = j < fp.n_owned_rt ? plan_parts(fp, fb, cnt, rt) : 1u;
+    const int lane = __lane_id();
+    // a pkeys slot per split tile (wave-aggregated); past fp.split_cap the tile stays whole
+    const uint64_t sm = __ballot(k > 1u);
+    uint32_t sid = 0u;
+    if (sm) {
+        const int lead = __ffsll((unsigned long long)sm) - 1;
+        if (lane == lead) sid = atomicAdd(&cnt[LC_SPLITS], (uint32_t)__popcll(sm));
+        sid = (uint32_t)__shfl((int)sid, lead) + lanes_below(sm);
+        if (k > 1u && sid >= fp.split_cap) k = 1u;
+    }
     const uint32_t kk = k > 1u ? k : 0u;
     // wave-aggregated reservation of this wave's parts
     uint32_t incl = kk;
-    const int lane = __lane_id();
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t a = (uint32_t)__shfl_up((int)incl, o);
@@ -2422,7 +2458,7 @@ __global__ __launch_bounds__(256) void k_lib_plan(LibFrameParams fp, LibBuffers 
     uint32_t base = 0u;
     if (lane == 63 && tot) base = atomicAdd(&cnt[LC_ITEMS], tot);
     base = (uint32_t)__shfl((int)base, 63) + incl - kk;
-    for (uint32_t p = 0; p < kk; ++p) fb.items[base + p] = make_uint2((uint32_t)rt, p | (k << 16));
+    for (uint32_t p = 0; p < kk; ++p) fb.items[base + p] = make_uint2((uint32_t)rt, p | (k << 8) | (sid << 16));
     if (kk) fb.busy[rt] = 2u;   // split: the in-order pass skips it (k_lib_resolve resets the flag)
 }
 
@@ -2501,12 +2537,13 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
             w = (uint32_t)sh.next[3];
         }
         int rt;
-        uint32_t part = 0u, parts = 1u, busy = 1u;
+        uint32_t part = 0u, parts = 1u, busy = 1u, sid = 0u;
         if (w & 0x80000000u) {   // a split tile's part
             const uint2 it = fb.items[w & 0x7fffffffu];
             rt = (int)it.x;
-            part = it.y & 0xffffu;
-            parts = it.y >> 16;
+            part = it.y & 0xffu;
+            parts = (it.y >> 8) & 0xffu;
+            sid = it.y >> 16;
         } else {
             rt = (int)(w & 0x0fffffffu);
             busy = (w >> 28) & 3u;
@@ -2514,7 +2551,7 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
             if (i < S && (w & LIB_HEAVY)) continue;   // static, heavy: served first from the heavy lists
         }
         if (busy) {
-            lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk, part, parts);
+            lib_raster_tile<SHADOW, LIB_CAND>(fp, fb, cnt, rt, sh, chunk, part, parts, sid);
         } else {
             const uint64_t t_c = fb.timeline && tid == 0 ? tl_now() : 0ull;
             if (SHADOW) lib_clear_shadow_tile(fp, fb, rt);
@@ -2568,8 +2605,13 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
     // tiled Forward+ lists can be wave-uniform (LtWave); clustered ones depend on the pixel's depth
     const bool tiled = PROG != 0 && fb.tile_counts && (fp.lt_mode == 1u || fp.lt_mode == 2u) && fp.lt_maxp <= 128u;
     const int n_blocks = 4 * fp.n_owned_rt;
-    for (int blk = 4 * (int)blockIdx.x + wave; blk < n_blocks; blk += 4 * (int)gridDim.x) {   // wave-uniform
-        const int rt = fb.rt_order[blk >> 2], sub = blk & 3;
+    const int bstep = 4 * (int)gridDim.x;
+    // the next block's raster tile is loaded a block ahead (off the block's dependent chain of loads:
+    // C4 0.614 -> 0.607, C5 0.390 -> 0.387 ms per frame)
+    int rt_next = 4 * (int)blockIdx.x < n_blocks ? fb.rt_order[blockIdx.x] : 0;
+    for (int blk = 4 * (int)blockIdx.x + wave; blk < n_blocks; blk += bstep) {   // wave-uniform
+        const int rt = rt_next, sub = blk & 3;
+        if (blk + bstep < n_blocks) rt_next = fb.rt_order[(blk + bstep) >> 2];
         const int px = (rt % fp.tiles_x) * LIB_RTW + 16 * (sub & 1) + (lane & 15);
         const int py = (rt / fp.tiles_x) * LIB_RTH + 4 * (sub >> 1) + (lane >> 4);
         const bool inb = px < fp.W && py < fp.H;
@@ -2639,6 +2681,7 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
     if (shadow) {
         hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     } else {
+        if (fb.blist) hipLaunchKernelGGL(k_lib_blocks, dim3((fp.setup_blocks + 255) / 256), dim3(256), 0, s, fp, fb);
         if (listed) {   // tile-sharded: each workgroup culls CULL_PER x 256 triangles, then sets up the kept ones
             hipLaunchKernelGGL((k_lib_setup<false, true>), dim3(grid), dim3(256), 0, s, fp, fb);
         } else {

@@ -96,8 +96,9 @@ constexpr uint32_t LF_PERM = 16u;       // a draw's mesh is stored in spatial or
 // atomicAdd hands an appender both bases and the queue's task prefix stays monotone; LC_N even keeps
 // the second parity set's word 8-B aligned.
 // LC_ITEMS: k_lib_plan's raster work items; LC_COVERED: camera-pass covered pixels (k_lib_resolve);
+// LC_SPLITS: k_lib_plan's split tiles (their pkeys slots); LC_BLOCKS: k_lib_blocks' listed setup blocks.
 constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT = 4, LC_BIGQ = 5, LC_ITEMS = 6, LC_COVERED = 7,
-              LC_N = 8;
+              LC_SPLITS = 8, LC_BLOCKS = 9, LC_N = 10;
 static_assert(LC_BIGQ == LC_BIGT + 1 && LC_BIGT % 2 == 0 && LC_N % 2 == 0, "64-bit big-queue word");
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
@@ -120,8 +121,9 @@ struct LibFrameParams {
     float lt_view_z[4];              // view matrix row 2 (view-space z, cluster slice)
     float lt_zn, lt_zf;              // the light cull's depth_params
     float tm_exposure, tm_inv_gamma; // fused PassTonemap (LibBuffers::tm_thr)
-    uint32_t part;                   // camera pass: k_lib_plan splits a tile's list into parts of this many
-                                     // entries (0: one work item per owned raster tile, no plan)
+    uint32_t part;                   // camera pass: k_lib_plan splits a tile's list into parts of about this
+                                     // many entries (0: one work item per owned raster tile, no plan)
+    uint32_t split_cap;              // ... at most this many split tiles per pass (LibBuffers::pkeys slots)
     int32_t raster_grid;             // k_lib_raster's workgroups (k_lib_dyn derives the same static share)
     int32_t static_div;              // k_lib_raster: n_work / (static_div * workgroups) static items per workgroup
     uint32_t heavy_min;              // camera pass: a busy tile whose bin list holds >= this many entries is
@@ -170,7 +172,11 @@ struct LibBuffers {
     uint32_t *ov_host;               // the pass's overflow word in mapped host memory (raise_overflow)
     float4 *uvw;                     // per slot, 2 float4: UV0 varying * 1/w of the 3 corners (textured draws)
     const float *srgb_lut;           // srgb_to_linear_rgb's 256 values, std::pow(c / 255.0f, 2.2f) on the host
-    uint2 *items;                    // k_lib_plan: raster work items (rt_order position, part | parts << 16)
+    uint2 *items;                    // k_lib_plan: raster work items (raster tile, part | parts << 8 | split id << 16)
+    unsigned long long *pkeys;       // per split tile (split id): its 32x8 keys, merged by the parts (atomicMin),
+                                     // KEY_EMPTY between passes (the last part resets them)
+    uint32_t *pcount;                // per split tile: parts finished (the last part resets it)
+    uint32_t *blist;                 // region-sharded camera pass: the setup blocks that can reach the rank (k_lib_blocks)
     uint32_t *s2s;                   // camera pass with LF_PERM: per input triangle in submission order, its slot
     uint4 *blkrect;                  // camera pass: per setup block (bx0 | bx1 << 16, by0 | by1 << 16, triangles,
                                      // bounded) of its chunk bounds, mapped host memory (the region balancer's input)
@@ -178,6 +184,7 @@ struct LibBuffers {
 
 // k_lib_plan: at most this many parts per raster tile (capacity: LIB_MAXK * owned raster tiles).
 constexpr int LIB_MAXK = 16;
+constexpr int LIB_RTH_PX = 32 * 8;   // pixels of a 32x8 raster tile (a split tile's pkeys slot)
 
 // k_lib_raster's work distribution: owned raster tile b to workgroup b, the rest from LIB_NQ ticket
 // counters a cache line apart (k_lib_setup zeroes the next frame's set).

@@ -286,3 +286,43 @@ def test_shard_cull_prepass_identical(count):
             assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
         for k in ("tri_input", "tri_after_clip", "tri_raster", "covered_pixels"):
             assert a[3][k] == b[3][k], (k, a[3][k], b[3][k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("part", [8, 300])
+def test_split_parts_painter_and_regions(oracle_mod, part):
+    """Candidate-range parts (k_lib_plan): without a depth target (the merge's min is over the inverted
+    submission order: the last submitted fragment still wins), and under the region layout with two
+    passes (the split tiles' key slots and counters are reset by each tile's last part)."""
+    import shs_gpu
+    from shs_gpu import scene_lib
+    from shs_gpu.lib_path import LibFrame
+    frame, draws, lights, cull = scene_lib.c4_scene(512, 288, n_objects=60, tris_per_object=500)
+    rc, ri = oracle_mod.light_cull(cull, lights)[:2]
+    ctx = shs_gpu.Context(0)
+    try:
+        ctx.set_lib_part(part)
+        ctx.upload_lights(lights)
+        ctx.light_cull(cull)
+        pf = LibFrame(512, 288, depth_motion=False, bg_gradient=False, clear_hdr=(0.1, 0.2, 0.3, 1.0))
+        rh, _, _, _ = oracle_mod.forward_plus(pf, draws, lights, cull, (rc, ri))
+        ctx.render_pbr_forward(pf, draws)
+        gh, _, _ = ctx.resolve_lib()
+        assert_float_close(gh, rh, what="painter split hdr")
+        rh, rd, rm, _ = oracle_mod.forward_plus(frame, draws, lights, cull, (rc, ri))
+        ctx.set_shard_layout(True)
+        for rank in (1, 2, 1):
+            frame.shard_rank, frame.shard_count = rank, 3
+            cull.shard_rank, cull.shard_count = rank, 3
+            ctx.light_cull(cull)
+            ctx.render_pbr_forward(frame, draws)
+            h, d, m = ctx.resolve_lib()
+            x0, y0, x1, y1 = ctx.shard_regions(3)[rank]
+            own = np.zeros(d.shape, bool)
+            own[y0 * 32:(y1 + 1) * 32, x0 * 32:(x1 + 1) * 32] = True
+            assert_depth_bitexact(np.where(own, d, rd), rd)
+            assert_float_close(np.where(own[..., None], h, rh), rh, what="region split hdr")
+    finally:
+        frame.shard_rank, frame.shard_count = 0, 1
+        cull.shard_rank, cull.shard_count = 0, 1
+        ctx.close()

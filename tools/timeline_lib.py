@@ -1,6 +1,6 @@
 """Per-workgroup timeline of the library camera pass (SHS_OPT_TIMELINE): where k_lib_raster's time goes.
 
-usage (GPU box): python tools/timeline_lib.py [c4|c5] [n_objects] [tris_per_object] [shard_count]
+usage (GPU box): [SPLIT_REGIONS=1] python tools/timeline_lib.py [c4|c5] [n_objects] [tris_per_object] [shard_count] [rank]
 Per workgroup: duration, summed phase times over its busy tiles (gather / stage + pairs / resolve +
 shade), clear time, tile / chunk / pair / candidate counts; distribution over workgroups and the
 slowest workgroup."""
@@ -37,9 +37,12 @@ def main():
         def one():
             ctx.render_pbr_forward_prepared(prepared)
     count = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-    frame.shard_rank, frame.shard_count = 0, count
+    rank = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    if count > 1 and os.environ.get("SPLIT_REGIONS") == "1":   # the region layout (balanced on this context's passes)
+        ctx.set_shard_layout(True)
+    frame.shard_rank, frame.shard_count = rank, count
     if cfg == "c4":
-        cull.shard_rank, cull.shard_count = 0, count
+        cull.shard_rank, cull.shard_count = rank, count
         ctx.light_cull(cull)
     prepared = ctx.prepare_lib(frame, draws)
     for _ in range(5):
