@@ -1006,6 +1006,53 @@ __device__ __forceinline__ bool pixel_test(const FrameParams &fp, const TriRec &
     return z < FLT_MAX;   // NaN and FLT_MAX never beat the FLT_MAX clear
 }
 
+// Conservative row span of a staged candidate inside its clipped box [bx0, bx1]: the pixels of row py
+// that can pass bary_pass (barycentric_coordinate, shs_renderer.hpp:802-821).  With t = px + 0.5 - ax,
+// Y = py + 0.5 - ay the exact Gram-form barycentrics of the record's float values are linear in t:
+//   v = av t + cv,  w = aw t + cw,  u = 1 - v - w,
+//   av = (d11 v0x - d01 v1x) / denom, cv = Y (d11 v0y - d01 v1y) / denom (w: d00 / v1 and v0 swapped).
+// bary_pass's float evaluation (no contraction) is within ~8 u Mv of v, Mv = (|d11| S0 + |d01| S1) /
+// |denom| with S0 = |v0x| |t| + |v0y| |Y|, S1 likewise (u = 2^-24: the rounding of t, the products
+// and sums of d20 / d21, the outer products, the difference and the division; likewise w), and u's
+// within ~10 u (1 + Mv + Mw).  A pixel can pass only where every exact barycentric is >= minus its
+// bound; each half-line a t >= -e - c is solved here in float with e = E (...) at E = 2^-18 (>= 6x the
+// bound: the slack absorbs this computation's own roundings, a few u of the magnitudes), and 2^-12 px
+// more covers the conversion to pixel indices.  Non-finite records keep the whole box row.  The bound
+// holds outside the triangle's bbox too (the 80x80 tile clamp's ghost pixels, section 5 of DESIGN.md).
+// tests/test_legacy_row_spans.py restates this in numpy and checks it against the per-pixel test.
+__device__ __forceinline__ void legacy_row_span(const float4 r0, const float4 r1, const float4 r2, int py, int bx0, int bx1,
+                                                int &x0, int &x1) {
+    x0 = bx0; x1 = bx1;
+    // r0, r1, r2: the record's first three float4s: ax ay v0x v0y | v1x v1y d00 d01 | d11 denom ...
+    const float ax = r0.x, ay = r0.y, v0x = r0.z, v0y = r0.w, v1x = r1.x, v1y = r1.y, d00 = r1.z, d01 = r1.w;
+    const float d11 = r2.x, den = r2.y;
+    if (!(isfinite(ax) && isfinite(ay) && isfinite(v0x) && isfinite(v0y) && isfinite(v1x) && isfinite(v1y) && isfinite(d00) &&
+          isfinite(d01) && isfinite(d11) && isfinite(den) && fabsf(den) > 0.0f))
+        return;
+    constexpr float E = 0x1p-18f;
+    const float Y = ((float)py + 0.5f) - ay, aY = fabsf(Y);
+    const float T = fmaxf(fabsf(((float)bx0 + 0.5f) - ax), fabsf(((float)bx1 + 0.5f) - ax));
+    const float idn = 1.0f / den, aid = fabsf(idn);
+    const float s0 = fabsf(v0x) * T + fabsf(v0y) * aY, s1 = fabsf(v1x) * T + fabsf(v1y) * aY;
+    const float mv = aid * (fabsf(d11) * s0 + fabsf(d01) * s1), mw = aid * (fabsf(d00) * s1 + fabsf(d01) * s0);
+    const float av = (d11 * v0x - d01 * v1x) * idn, cv = ((d11 * v0y - d01 * v1y) * idn) * Y;
+    const float aw = (d00 * v1x - d01 * v0x) * idn, cw = ((d00 * v1y - d01 * v0y) * idn) * Y;
+    float lo = -1e30f, hi = 1e30f;
+    auto edge = [&](float a, float c, float e) {   // a t + c >= -e
+        const float b = -e - c;
+        if (a > 0.0f) lo = fmaxf(lo, b / a);
+        else if (a < 0.0f) hi = fminf(hi, b / a);
+        else if (b > 0.0f) { lo = 1e30f; hi = -1e30f; }
+    };
+    edge(av, cv, E * mv);
+    edge(aw, cw, E * mw);
+    edge(-(av + aw), 1.0f - (cv + cw), E * (1.0f + 2.0f * (mv + mw)));
+    const float flo = (lo + ax) - 0.5f, fhi = (hi + ax) - 0.5f;
+    const float slo = 0x1p-12f * ((fabsf(lo) + fabsf(ax)) + 1.0f), shi = 0x1p-12f * ((fabsf(hi) + fabsf(ax)) + 1.0f);
+    x0 = max(bx0, (int)ceilf(fmaxf(fminf(flo - slo, 1e9f), -1e9f)));
+    x1 = min(bx1, (int)floorf(fmaxf(fminf(fhi + shi, 1e9f), -1e9f)));
+}
+
 constexpr int RCHUNK = 64;         // candidate records staged per pass (one wave scans their areas)
 constexpr int LDS_DRAWS = 64;      // draws whose shading uniforms are kept in LDS
 constexpr int PAIR_WORDS = RCHUNK * RTW * RTH / 64;   // pair-start bitmap words (a box is <= 256 px)
@@ -1023,13 +1070,15 @@ struct RasterShared {
     float4 srec[RCHUNK * 5];          // staged shading records (single-pass tiles, 5 KB)
     unsigned long long key[RTH * RTW];// per-pixel (z, index) keys (2 KB)
     unsigned long long bits[PAIR_WORDS]; // bit k: a staged candidate's pairs start at pair k (2 KB)
-    uint4 pinfo[RCHUNK];              // per staged candidate: first pair, x0 | y0 << 16, box width, 2^16/width
+    uint32_t seg[RCHUNK * RTH];       // spans: per nonempty row span, first pair | x0 << 14 | row << 19 | candidate << 22
+    uint4 pinfo[RCHUNK];              // boxes: per staged candidate first pair, x0 | y0 << 16, box width, 2^16/width
+    uint32_t wtot[4];                 // per wave: pairs << 11 | segments (the staging pass's block prefix)
     uint32_t id[RCHUNK];
     uint32_t cand[CAND];
     float4 du[LDS_DRAWS * 4];         // per-draw {light, cam, ocol, colf} (4 KB)
     uint8_t skip[512];                // clear strip: per raster tile across, 1 = not cleared (busy / not owned)
     uint32_t nc, item, cov, maxbin, npairs;
-    uint8_t wown[PAIR_WORDS];         // staged candidate owning each bitmap word's first pair
+    uint16_t wown[PAIR_WORDS];        // segment (boxes: staged candidate) owning each bitmap word's first pair
 };
 
 // The record rebuilt from the screen corners with the stored flags and bin box: rec_from_screen's
@@ -1139,7 +1188,7 @@ __device__ __forceinline__ void resolve_from_mesh(const FrameParams &fp, const F
 // each thread owns one pixel: the winner's record and varyings are fetched by index, (u, v, w)
 // recomputed with the identical arithmetic, the pixel shaded and written.
 // fb: the frame's view (frame_view); draws: the whole batch's draw table; rt: raster tile of the frame.
-template <bool NO_RECS>
+template <bool NO_RECS, bool SPANS>
 __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
                                             const uint32_t *cnt, uint32_t n_frag, int frame, int rt,
                                             const uint2 (&pbx)[CAND / 256], bool prefetched, RasterShared &sh, uint64_t *tl) {
@@ -1284,53 +1333,139 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                 seq += (uint32_t)m;
                 continue;
             }
-            // Pair tasks, dealt evenly over the workgroup.  Wave 0 lays the staged candidates' clipped
-            // bin boxes end to end (prefix of the areas; every staged box holds >= 1 pixel of the tile,
-            // so the starts are distinct) and marks each start in a bitmap over the pairs, plus the
-            // owner of every bitmap word's first pair.  Wave w then takes the 64-pair windows w, w + 4,
-            // ...: a pair's owner = that word's first owner + the starts in the word up to it.
-            if (wave == 0) {
-                int area = 0, bx0 = 0, by0 = 0, bw = 1;
-                if (lane < m) {
-                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[lane * 6])[4];   // ibx iby gbx gby
-                    const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
-                    const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
-                    if (x0 <= x1 && y0 <= y1) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
+            if constexpr (SPANS) {
+                // Pair tasks over conservative row spans (legacy_row_span), dealt evenly over the workgroup:
+                // thread (ci = tid / 4, q = tid % 4) takes staged candidate ci's tile rows 2q and 2q + 1; their
+                // spans inside its clipped bin box are laid end to end as segments after one block prefix of
+                // (pairs, segments), and each segment's first pair is marked in a bitmap over the pairs, plus
+                // the segment owning every bitmap word's first pair.  Wave w then takes the 64-pair windows w,
+                // w + 4, ...: a pair's segment = that word's first owner + the starts in the word up to it.
+                // (Whole bin boxes made ~2,600 pairs for ~42 candidates per C3 tile: thin triangles' boxes are
+                // mostly empty.)
+                uint32_t ptot = 0u;
+                {
+                    const int ci = tid >> 2, q = tid & 3;
+                    uint32_t spw[2] = {0x1fu, 0x1fu};   // tile-relative x0 | x1 << 8; 0x1f: empty
+                    uint32_t pk = 0u;                   // pairs << 11 | segments
+                    if (ci < m) {
+                        const float4 *rc = &sh.rec[ci * 6];
+                        const uint4 bb = reinterpret_cast<const uint4 *>(rc)[4];   // ibx iby gbx gby
+                        const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
+                        const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
+                        if (x0 <= x1 && y0 <= y1) {
+                            const float4 r0 = rc[0], r1 = rc[1], r2 = rc[2];
+    #pragma unroll
+                            for (int j = 0; j < 2; ++j) {
+                                const int py = Y0 + 2 * q + j;
+                                if (py < y0 || py > y1) continue;
+                                int s0, s1;
+                                legacy_row_span(r0, r1, r2, py, x0, x1, s0, s1);
+                                if (s1 < s0) continue;
+                                spw[j] = (uint32_t)(s0 - X0) | ((uint32_t)(s1 - X0) << 8);
+                                pk += ((uint32_t)(s1 - s0 + 1) << 11) + 1u;
+                            }
+                        }
+                    }
+                    uint32_t incl = pk;
+    #pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const uint32_t vv = (uint32_t)__shfl_up((int)incl, o);
+                        if (lane >= o) incl += vv;
+                    }
+                    if (lane == 63) sh.wtot[wave] = incl;
+                    __syncthreads();
+                    uint32_t pbase = 0u;
+    #pragma unroll
+                    for (int w2 = 0; w2 < 4; ++w2) {
+                        const uint32_t p2 = sh.wtot[w2];
+                        if (w2 < wave) pbase += p2;
+                        ptot += p2;
+                    }
+                    if (pk) {
+                        const uint32_t ex = pbase + incl - pk;
+                        uint32_t ps = ex >> 11, sg = ex & 2047u;
+    #pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            if (spw[j] == 0x1fu) continue;
+                            const uint32_t s0 = spw[j] & 0xffu, wdt = (spw[j] >> 8) - s0 + 1u;
+                            sh.seg[sg] = ps | (s0 << 14) | ((uint32_t)(2 * q + j) << 19) | ((uint32_t)ci << 22);
+                            atomicOr(&sh.bits[ps >> 6], 1ull << (ps & 63u));
+                            for (uint32_t wd = (ps + 63u) >> 6; wd * 64u < ps + wdt; ++wd) sh.wown[wd] = (uint16_t)sg;
+                            ps += wdt;
+                            ++sg;
+                        }
+                    }
                 }
-                int incl = area;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int v = __shfl_up(incl, o);
-                    if (lane >= o) incl += v;
+                __syncthreads();
+                const int total = (fp.flags & DBG_SKIP_PAIRS) ? 0 : (int)(ptot >> 11);
+                pairs += total;
+                for (int k0 = 64 * wave; k0 < total; k0 += 256) {
+                    const int k = k0 + lane;
+                    if (k < total) {
+                        const unsigned long long wb = sh.bits[k0 >> 6];
+                        const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
+                        const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
+                        const uint32_t sgi = sh.seg[o];
+                        const int cc = (int)(sgi >> 22);
+                        const int px = X0 + (int)((sgi >> 14) & 31u) + (k - (int)(sgi & 0x3fffu)), py = Y0 + (int)((sgi >> 19) & 7u);
+                        const TriRec r = rec_from(&sh.rec[cc * 6]);
+                        float z;
+                        if (pixel_test(fp, r, px, py, z))
+                            atomicMin(&sh.key[(py - Y0) * RTW + (px - X0)],
+                                      cand_key(z, sh.id[cc], slot_keys, single ? (uint32_t)cc : SLOT_NONE));
+                    }
                 }
-                const int start = incl - area;
-                if (area > 0) {
-                    // 2^16 / width rounded up: (local * magic) >> 16 == local / width for local < 256
-                    sh.pinfo[lane] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16), (uint32_t)bw,
-                                                (65536u + (uint32_t)bw - 1u) / (uint32_t)bw);
-                    atomicOr(&sh.bits[start >> 6], 1ull << (start & 63));
-                    for (int wd = (start + 63) >> 6; wd * 64 < incl; ++wd) sh.wown[wd] = (uint8_t)lane;
+            } else {
+                // (scan-mode frames: whole clipped bin boxes -- C2's Suzanne triangles fill most of their boxes,
+                // and the spans measured slower there: 0.271 -> 0.278 ms per step)
+                // Pair tasks, dealt evenly over the workgroup.  Wave 0 lays the staged candidates' clipped
+                // bin boxes end to end (prefix of the areas; every staged box holds >= 1 pixel of the tile,
+                // so the starts are distinct) and marks each start in a bitmap over the pairs, plus the
+                // owner of every bitmap word's first pair.  Wave w then takes the 64-pair windows w, w + 4,
+                // ...: a pair's owner = that word's first owner + the starts in the word up to it.
+                if (wave == 0) {
+                    int area = 0, bx0 = 0, by0 = 0, bw = 1;
+                    if (lane < m) {
+                        const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[lane * 6])[4];   // ibx iby gbx gby
+                        const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
+                        const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
+                        if (x0 <= x1 && y0 <= y1) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
+                    }
+                    int incl = area;
+    #pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int v = __shfl_up(incl, o);
+                        if (lane >= o) incl += v;
+                    }
+                    const int start = incl - area;
+                    if (area > 0) {
+                        // 2^16 / width rounded up: (local * magic) >> 16 == local / width for local < 256
+                        sh.pinfo[lane] = make_uint4((uint32_t)start, (uint32_t)bx0 | ((uint32_t)by0 << 16), (uint32_t)bw,
+                                                    (65536u + (uint32_t)bw - 1u) / (uint32_t)bw);
+                        atomicOr(&sh.bits[start >> 6], 1ull << (start & 63));
+                        for (int wd = (start + 63) >> 6; wd * 64 < incl; ++wd) sh.wown[wd] = (uint16_t)lane;
+                    }
+                    if (lane == 63) sh.npairs = (uint32_t)incl;
                 }
-                if (lane == 63) sh.npairs = (uint32_t)incl;
-            }
-            __syncthreads();
-            const int total = (fp.flags & DBG_SKIP_PAIRS) ? 0 : (int)sh.npairs;
-            pairs += total;
-            for (int k0 = 64 * wave; k0 < total; k0 += 256) {
-                const int k = k0 + lane;
-                if (k < total) {
-                    const unsigned long long wb = sh.bits[k0 >> 6];
-                    const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
-                    const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
-                    const uint4 pi = sh.pinfo[o];
-                    const int local = k - (int)pi.x;
-                    const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * (int)pi.z;
-                    const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
-                    const TriRec r = rec_from(&sh.rec[o * 6]);
-                    float z;
-                    if (pixel_test(fp, r, px, py, z))
-                        atomicMin(&sh.key[(py - Y0) * RTW + (px - X0)],
-                                  cand_key(z, sh.id[o], slot_keys, single ? (uint32_t)o : SLOT_NONE));
+                __syncthreads();
+                const int total = (fp.flags & DBG_SKIP_PAIRS) ? 0 : (int)sh.npairs;
+                pairs += total;
+                for (int k0 = 64 * wave; k0 < total; k0 += 256) {
+                    const int k = k0 + lane;
+                    if (k < total) {
+                        const unsigned long long wb = sh.bits[k0 >> 6];
+                        const unsigned long long upto = ((2ull << lane) - 1ull) & ~1ull;   // bits 1..lane
+                        const int o = (int)sh.wown[k0 >> 6] + __popcll(wb & upto);
+                        const uint4 pi = sh.pinfo[o];
+                        const int local = k - (int)pi.x;
+                        const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * (int)pi.z;
+                        const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
+                        const TriRec r = rec_from(&sh.rec[o * 6]);
+                        float z;
+                        if (pixel_test(fp, r, px, py, z))
+                            atomicMin(&sh.key[(py - Y0) * RTW + (px - X0)],
+                                      cand_key(z, sh.id[o], slot_keys, single ? (uint32_t)o : SLOT_NONE));
+                    }
                 }
             }
             seq += (uint32_t)m;
@@ -1532,7 +1667,7 @@ constexpr int STRIP_RT = SHS_STRIP_RT;
 #ifndef SHS_LEGACY_RASTER_WAVES
 #define SHS_LEGACY_RASTER_WAVES 4   // minimum waves per SIMD (-D...: timing experiments)
 #endif
-template <bool KARG, bool NO_RECS>
+template <bool KARG, bool NO_RECS, bool SPANS>
 __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
     const int tid = threadIdx.x;
@@ -1597,9 +1732,9 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
                 __syncthreads();
                 clear_tile(fp, fv, rt);
             } else {
-                if (fp.flags & DBG_TWICE) raster_tile<NO_RECS>(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
+                if (fp.flags & DBG_TWICE) raster_tile<NO_RECS, SPANS>(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
                 tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
-                raster_tile<NO_RECS>(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
+                raster_tile<NO_RECS, SPANS>(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
                 first = false;
             }
         }
@@ -1677,7 +1812,7 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_pipe(FramePara
                 const uint32_t g = fb.busy_list[j - s_lo];
                 const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
                 const FrameBuffers fv = frame_view(fp, fb, f);
-                raster_tile<false>(fp, fv, draws, cnt, n_frag, f, rt, pbx, false, sh, nullptr);
+                raster_tile<false, false>(fp, fv, draws, cnt, n_frag, f, rt, pbx, false, sh, nullptr);
             }
         }
         if (!queued) break;
@@ -1724,12 +1859,16 @@ hipError_t launch_pipe(const FrameParams &fpR, const FrameBuffers &fbR, int grid
 hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, int grid, hipStream_t s) {
     const dim3 g(grid > 0 ? grid : 1);
     const bool karg = fp.n_draws * fp.n_frames <= KARG_DRAWS;   // the whole batch's draws as kernel arguments
+    // binned frames test conservative row spans, scan-mode frames whole boxes (raster_tile)
     if (fp.flags & RF_NO_RECS) {   // binned frames: records recomputed from the mesh
-        if (karg) hipLaunchKernelGGL((k_raster<true, true>), g, dim3(256), 0, s, fp, fb, ka);
-        else hipLaunchKernelGGL((k_raster<false, true>), g, dim3(256), 0, s, fp, fb, ka);
+        if (karg) hipLaunchKernelGGL((k_raster<true, true, true>), g, dim3(256), 0, s, fp, fb, ka);
+        else hipLaunchKernelGGL((k_raster<false, true, true>), g, dim3(256), 0, s, fp, fb, ka);
+    } else if (!fp.scan_mode) {
+        if (karg) hipLaunchKernelGGL((k_raster<true, false, true>), g, dim3(256), 0, s, fp, fb, ka);
+        else hipLaunchKernelGGL((k_raster<false, false, true>), g, dim3(256), 0, s, fp, fb, ka);
     } else {
-        if (karg) hipLaunchKernelGGL((k_raster<true, false>), g, dim3(256), 0, s, fp, fb, ka);
-        else hipLaunchKernelGGL((k_raster<false, false>), g, dim3(256), 0, s, fp, fb, ka);
+        if (karg) hipLaunchKernelGGL((k_raster<true, false, false>), g, dim3(256), 0, s, fp, fb, ka);
+        else hipLaunchKernelGGL((k_raster<false, false, false>), g, dim3(256), 0, s, fp, fb, ka);
     }
     return hipGetLastError();
 }

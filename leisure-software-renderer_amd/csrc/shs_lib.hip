@@ -1766,11 +1766,20 @@ __device__ __forceinline__ float4 lib_resolve(const LibFrameParams &fp, const Li
         if (__ballot(s.draw != d0) == 0) shade_px<PROG>(fp, fb, fb.draws[d0], r, s, slot, px, py, color, depth, mv, st);
         else shade_px<PROG>(fp, fb, fb.draws[s.draw], r, s, slot, px, py, color, depth, mv, st);
     }
+#ifdef SHS_EXP_RESOLVE_STORES   // timing experiments (wrong images): bit 1 no HDR, 2 no depth, 4 no motion
+    if (!(SHS_EXP_RESOLVE_STORES & 1)) fb.hdr[o] = color;
+    if (fp.flags & LF_DEPTH) {
+        if (!(SHS_EXP_RESOLVE_STORES & 2)) fb.depth[o] = depth;
+        if (!(SHS_EXP_RESOLVE_STORES & 4)) fb.motion[o] = mv;
+    }
+    if (color.x == -1234.5f && depth == -2.0f && mv.x == -3.0f) fb.hdr[o] = color;   // keeps the shading live
+#else
     fb.hdr[o] = color;
     if (fp.flags & LF_DEPTH) {
         fb.depth[o] = depth;
         fb.motion[o] = mv;
     }
+#endif
     return color;
 }
 
@@ -2654,7 +2663,11 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
                                   (tonemap_byte(c.y, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) << 8) |
                                   (tonemap_byte(c.z, fp.tm_exposure, fp.tm_inv_gamma, tm_thr) << 16) | (255u << 24);
             if (fb.tm_ldr) __builtin_nontemporal_store(rgba, &fb.tm_ldr[(size_t)py * fp.W + px]);
+#if defined(SHS_EXP_RESOLVE_STORES) && (SHS_EXP_RESOLVE_STORES & 8)
+            if (fb.tm_present && rgba == 0x12345678u) __builtin_nontemporal_store(rgba, &fb.tm_present[(size_t)(fp.H - 1 - py) * fp.W + px]);
+#else
             if (fb.tm_present) __builtin_nontemporal_store(rgba, &fb.tm_present[(size_t)(fp.H - 1 - py) * fp.W + px]);
+#endif
         }
     }
     __syncthreads();
