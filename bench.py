@@ -70,6 +70,7 @@ def build_workload(name, rank=0):
 
 
 POSE_SETS = 4   # distinct batches of camera poses the timed steps cycle through
+LEGACY_FRAMES = {"c1": 128, "c2": 128, "c3": 16}   # default frames per step (one shs_render_legacy_batch)
 
 
 def batch_poses(name, n_frames, rank=0):
@@ -705,7 +706,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--frames-per-step", type=int, default=0,
-                    help="legacy configs: frames per shs_render_legacy_batch step (default 64 for c1/c2, 16 for c3)")
+                    help="legacy configs: frames per shs_render_legacy_batch step (default 128 for c1/c2, 16 for c3; C2 measured 64 / 128 / 256: 230 / 248 / 255 Mtri/s, DESIGN.md 6)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="c4/c5: frames in flight (contexts rendering consecutive frames round-robin)")
     ap.add_argument("--shard-layout", default="regions", choices=["regions", "interleaved"],
@@ -738,7 +739,7 @@ def main():
                     help="rank launcher check: every rank joins a gloo group and rank 0 prints the ranks (no GPU)")
     args = ap.parse_args()
     if args.frames_per_step <= 0:
-        args.frames_per_step = {"c1": 64, "c2": 64, "c3": 16}.get(args.config, 1)
+        args.frames_per_step = LEGACY_FRAMES.get(args.config, 1)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.child:
         # `python bench.py --gpus N` started directly: start the N ranks as child processes (one per

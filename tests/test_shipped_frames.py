@@ -1,6 +1,6 @@
 """Oracle checks of exactly what bench.py times and ships.
 
-* C2: the bench's timed steps are batches of 64 camera poses at 1920x1080 (bench.batch_poses); pose
+* C2: the bench's timed steps are batches of bench.LEGACY_FRAMES['c2'] (128) camera poses at 1920x1080 (bench.batch_poses); pose
   sets 0 and 3 are rendered as one batch each, exactly as the timed loop does (prepare_batch +
   render_batch_prepared), and every frame is compared with the oracle: depth bit-exact, colour under
   the pre-truncation rule with that frame's own prequant floats.  The same batches rendered without
@@ -24,17 +24,18 @@ def test_c2_bench_batch_every_frame_vs_oracle(oracle_mod, pose_set):
     import dataclasses
     import bench
     import shs_gpu
-    frame, sets = bench.batch_poses("c2", 64)
+    F = bench.LEGACY_FRAMES["c2"]
+    frame, sets = bench.batch_poses("c2", F)
     fds = sets[pose_set]
-    assert (frame.width, frame.height) == (1920, 1080) and len(fds) == 64
+    assert (frame.width, frame.height) == (1920, 1080) and len(fds) == F
     ctx = shs_gpu.Context(0)
     try:
         ctx.render_batch_prepared(ctx.prepare_batch(frame, fds))          # the bench's flags
-        plain = [ctx.resolve_frame(k) for k in range(64)]
+        plain = [ctx.resolve_frame(k) for k in range(F)]
         pframe = dataclasses.replace(frame, prequant=True)
         ctx.render_batch_prepared(ctx.prepare_batch(pframe, fds))
         boundary = 0
-        for k in range(64):
+        for k in range(F):
             c, z = ctx.resolve_frame(k)
             pq = ctx.resolve_prequant(k)
             assert np.array_equal(c, plain[k][0]) and np.array_equal(z.view(np.uint32), plain[k][1].view(np.uint32)), \
@@ -42,7 +43,7 @@ def test_c2_bench_batch_every_frame_vs_oracle(oracle_mod, pose_set):
             rc, rd, rpq = oracle_mod.render_legacy(1920, 1080, fds[k], threads=16, prequant=True)
             assert_depth_bitexact(z, rd)
             boundary += assert_color_parity(c, rc, pq, rpq)
-        print(f"pose set {pose_set}: 64 frames exact, {boundary} truncation-boundary bytes")
+        print(f"pose set {pose_set}: {F} frames exact, {boundary} truncation-boundary bytes")
     finally:
         ctx.close()
 
