@@ -779,7 +779,8 @@ def main():
     if args.config in LIB_CONFIGS:
         return main_lib(args, world, rank, local_rank, dist, pmc, pmc_err)
     frame, draws, stats, elapsed, n_launches, kms, single, pcie, ramp = run_gpu(args, rank, local_rank, world, dist)
-    strong = strong_legs(args, rank, local_rank, world, dist) if args.strong and not args.child else {}
+    # the strong-scaling legs ride on the headline configuration's line (the driver's `--gpus N` run)
+    strong = strong_legs(args, rank, local_rank, world, dist) if args.strong and not args.child and args.config == "c2" else {}
     B1, n_tri1 = algorithmic_bytes(frame, draws)
     F = args.frames_per_step
     B, n_tri = B1 * F, n_tri1 * F          # per step (= per k_raster launch)

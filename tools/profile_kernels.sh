@@ -9,7 +9,7 @@ TAG=$1; shift
 R=$(pwd)
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --no-pmc --no-cpu --no-single --no-pcie "$@" > "$R/gpurun_out/prof_$TAG.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --no-pmc --no-cpu --no-single --no-pcie --strong '' "$@" > "$R/gpurun_out/prof_$TAG.log" 2>&1
 cd "$R"
 cp gpurun_out/prof_$TAG/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
 python3 tools/kstats.py gpurun_out/prof_$TAG "" --skip-first 40 > gpurun_out/${TAG}_kernel_timed.txt
