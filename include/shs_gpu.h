@@ -189,10 +189,11 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * superseded); results are identical. */
 #define SHS_OPT_SPILL_CAPACITY 5
 #define SHS_OPT_FRAG_CAPACITY 6
-/* SHS_OPT_LIB_PART: library camera passes split a busy 32x8 raster tile whose bin list holds more than
- * `value` entries into spatial parts (32x4 halves or 16x4 blocks) rendered by several workgroups at
- * once, each over the whole list but only its own pixels (no merge; results identical).  -1: 512 for
- * tile-sharded passes, off otherwise; 0 (default): off. */
+/* SHS_OPT_LIB_PART: library camera passes split a busy 32x8 raster tile whose candidate list holds more
+ * than `value` entries into ceil(n / value) parts (at most 16) rendered by several workgroups at once,
+ * part j over list positions [j n / k, (j + 1) n / k) of the whole tile; the parts merge their keys
+ * with 64-bit atomicMin and the last one writes the winners (results identical).  -1: 512 for
+ * tile-sharded passes, off otherwise; 0 (default): off (measured slower). */
 #define SHS_OPT_LIB_PART 7
 /* SHS_OPT_SHARD_CULL: 1 = each setup workgroup of a tile-sharded camera pass first keeps the triangles
  * of its inputs that can reach the rank's tiles (positions only) and sets up only those; 0 (default) =
@@ -221,7 +222,10 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * box) ∩ (the camera frustum slice of the pixels the rank shades -- its region, or the whole frame),
  * widened by the PCF reach (shadow_sample.hpp:65-104) -- so a region-sharded rank renders only its own
  * shadow footprint and no shadow map crosses between ranks.  Texels outside are not written that pass;
- * the frame's images are identical.  shs_resolve_shadow_map of a recorded pass renders it whole.
+ * the frame's images are identical.  A later camera pass that samples the same map (another view or
+ * region) and reads beyond the rendered tiles enqueues the shadow pass again over the union first;
+ * releasing a caster mesh of a footprint-restricted map renders the map whole first.
+ * shs_resolve_shadow_map of a recorded pass renders it whole.
  * 0 (default): every shadow pass renders the whole map when it is called. */
 #define SHS_OPT_SHADOW_FOOTPRINT 11
 /* SHS_OPT_LEGACY_PIPELINE: 1 = multi-draw scan-mode legacy batches (shs_render_legacy_batch with more
@@ -277,7 +281,9 @@ int shs_gpu_tile_size(void);
 
 /* MeshData (resources/mesh.hpp:23-43): n_verts vec3 positions; normals / uvs may be shorter than
  * positions (missing entries read as (0,1,0) / (0,0), rasterizer.hpp:196-202) or NULL; indices NULL
- * = non-indexed soup (3 consecutive positions per triangle).  Device resident from here on. */
+ * = non-indexed soup (3 consecutive positions per triangle).  Device resident from here on, a mesh of
+ * more than 256 triangles stored in the spatial (Morton) order of its triangles' centroids; the
+ * submission order -- z ties, clipped fans, draws without a depth target -- stays the MeshData order. */
 int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const float *normals, int32_t n_normals,
                     const float *uvs, int32_t n_uvs, const uint32_t *indices, int64_t n_indices, int32_t *mesh_id);
 
