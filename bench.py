@@ -655,14 +655,21 @@ def cpu_baseline(args):
         frames, el, med = _timed_frames(
             lambda: oracle.render_legacy(frame.width, frame.height, draws, threads=threads), args.cpu_seconds / len(legs))
         out[name] = {"threads": threads, "frames": frames, "seconds": round(el, 2), "median_ms_per_frame": round(med, 3),
+                     "mean_ms_per_frame": round(el / frames * 1e3, 3),
                      "mtri_s": round(n_tri * frames / el / 1e6, 4), "mpix_s": round(covered * frames / el / 1e6, 3)}
     # the headline is the fastest leg: the baseline the GPU is compared with is the CPU at its best
     # (hardware_concurrency oversubscribes a host whose process share is smaller than its core count)
     head_name = max(out, key=lambda k: out[k]["mtri_s"])
     head = out[head_name]
+    quota = cgroup_cpu_quota()
+    note = None
+    if quota is not None and hc > quota:
+        note = (f"hardware_concurrency ({hc}) workers on a cgroup CPU quota of {quota:g} cores: the persistent pool's "
+                "frames stall on descheduled workers (median vs mean ms per frame in the legs), so that leg is slower "
+                "than the quota-sized ones")
     return {"value": head["mtri_s"], "unit": "Mtri/s", "cores": head["threads"], "kind": "port",
             "median_ms_per_frame": head["median_ms_per_frame"], "mpix_s": head["mpix_s"], "cpu_model": cpu_model(),
-            "hardware_concurrency": hc, "usable_cores": usable, "cgroup_cpu_quota": cgroup_cpu_quota(), "legs": out,
+            "hardware_concurrency": hc, "usable_cores": usable, "cgroup_cpu_quota": quota, "note": note, "legs": out,
             "sample": f"{head['frames']} frames of the same workload ({frame.width}x{frame.height}, {n_tri} tris, "
                       f"{covered} covered px) in {head['seconds']} s, 80x80 tile jobs on {head['threads']} threads "
                       f"({head_name}; oracle/shs_oracle.c, gcc -O3)"}
