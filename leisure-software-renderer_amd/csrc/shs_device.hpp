@@ -98,7 +98,7 @@ constexpr uint32_t OV_SPILL = 1u, OV_FRAG = 2u;
 // let bench --debug-flags attribute kernel time to phases.  Never set by the product path.
 constexpr uint32_t DBG_SKIP_GHOST = 1u << 8, DBG_SKIP_SHADE = 1u << 9, DBG_CLEAR_ONLY = 1u << 10,
                    DBG_SKIP_BIN = 1u << 11, DBG_SKIP_CLEAR = 1u << 12,
-                   DBG_TWICE = 1u << 13, DBG_SKIP_PAIRS = 1u << 14;
+                   DBG_TWICE = 1u << 13, DBG_SKIP_PAIRS = 1u << 14, DBG_SKIP_TILE_STORES = 1u << 15;
 constexpr uint32_t DBG_MASK = 0xffu << 8;   // dropped from the caller's flags outside the experiments build
 // Raster inner loop (frame flags bit 16, set by the context from SHS_OPT_RASTER_LOOP): per-pixel
 // candidate loop instead of (candidate, pixel) pair tasks.  Results are identical either way.

@@ -1578,7 +1578,9 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     if (tl && tid == 0) { tl[TL_STRIDE * tls + 8] = seq; tl[TL_STRIDE * tls + 9] = (uint64_t)pairs; }
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
-    if (px < fp.W && py < fp.H) {
+    // (DBG_SKIP_TILE_STORES, timing experiments: the busy tile's stores dropped, its values kept live)
+    const bool dbg_nost = (fp.flags & DBG_SKIP_TILE_STORES) && !(rgba == 0x12345678u && depth == -1.0f);
+    if (px < fp.W && py < fp.H && !dbg_nost) {
         __builtin_nontemporal_store(rgba, &reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - py) * fp.W + px]);
         __builtin_nontemporal_store(depth, &fb.depth[(size_t)py * fp.W + px]);
         if (fb.prequant) fb.prequant[(size_t)(fp.H - 1 - py) * fp.W + px] = pq;
