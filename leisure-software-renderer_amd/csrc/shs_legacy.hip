@@ -36,6 +36,14 @@
 #include "shs_internal.hpp"
 #include "shs_wave.hpp"
 
+// Framebuffer stores of the raster and the clears: non-temporal (streamed past the caches) unless
+// -DSHS_LEGACY_PLAIN_STORES (timing experiments).
+#ifdef SHS_LEGACY_PLAIN_STORES
+template <typename T> __device__ __forceinline__ void LEGACY_STORE(T v, T *p) { *p = v; }
+#else
+#define LEGACY_STORE(v, p) __builtin_nontemporal_store(v, p)
+#endif
+
 namespace shs_dev {
 
 // ---- k_setup --------------------------------------------------------------------------------
@@ -1581,11 +1589,11 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     // (DBG_SKIP_TILE_STORES, timing experiments: the busy tile's stores dropped, its values kept live)
     const bool dbg_nost = (fp.flags & DBG_SKIP_TILE_STORES) && !(rgba == 0x12345678u && depth == -1.0f);
     if (px < fp.W && py < fp.H && !dbg_nost) {
-        __builtin_nontemporal_store(rgba, &reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - py) * fp.W + px]);
-        __builtin_nontemporal_store(depth, &fb.depth[(size_t)py * fp.W + px]);
+        LEGACY_STORE(rgba, &reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - py) * fp.W + px]);
+        LEGACY_STORE(depth, &fb.depth[(size_t)py * fp.W + px]);
         if (fb.prequant) fb.prequant[(size_t)(fp.H - 1 - py) * fp.W + px] = pq;
         // copy_to_SDLSurface: surface row h-1-y takes canvas row y, i.e. the screen row
-        if (fb.present) __builtin_nontemporal_store(rgba, &fb.present[(size_t)py * fp.W + px]);
+        if (fb.present) LEGACY_STORE(rgba, &fb.present[(size_t)py * fp.W + px]);
     }
     tl_mark(tl, tls, 5);
 }
@@ -1597,10 +1605,10 @@ __device__ __forceinline__ void clear_tile(const FrameParams &fp, const FrameBuf
     const int px = col * RTW + (tid & 31), py = row * RTH + (tid >> 5);
     if (px < fp.W && py < fp.H) {
         const size_t c = (size_t)(fp.H - 1 - py) * fp.W + px;
-        __builtin_nontemporal_store(fp.clear_rgba, &reinterpret_cast<uint32_t *>(fb.color)[c]);
-        __builtin_nontemporal_store(FLT_MAX, &fb.depth[(size_t)py * fp.W + px]);
+        LEGACY_STORE(fp.clear_rgba, &reinterpret_cast<uint32_t *>(fb.color)[c]);
+        LEGACY_STORE(FLT_MAX, &fb.depth[(size_t)py * fp.W + px]);
         if (fb.prequant) fb.prequant[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (fb.present) __builtin_nontemporal_store(fp.clear_rgba, &fb.present[(size_t)py * fp.W + px]);
+        if (fb.present) LEGACY_STORE(fp.clear_rgba, &fb.present[(size_t)py * fp.W + px]);
     }
 }
 
@@ -1626,9 +1634,9 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
             const int t = g >> 3;   // 8 groups of 4 px per 32-px tile
             if (fv.busy[ry * fp.tiles_x + t] == fp.epoch || (fp.count > 1 && !owned_bin_tile(fp, t, by))) continue;
             for (int y = y0; y < y1; ++y) {
-                __builtin_nontemporal_store(c4, &reinterpret_cast<u32x4 *>(color + (size_t)(fp.H - 1 - y) * fp.W)[g]);
-                __builtin_nontemporal_store(d4, &reinterpret_cast<f32x4 *>(fv.depth + (size_t)y * fp.W)[g]);
-                if (fv.present) __builtin_nontemporal_store(c4, &reinterpret_cast<u32x4 *>(fv.present + (size_t)y * fp.W)[g]);
+                LEGACY_STORE(c4, &reinterpret_cast<u32x4 *>(color + (size_t)(fp.H - 1 - y) * fp.W)[g]);
+                LEGACY_STORE(d4, &reinterpret_cast<f32x4 *>(fv.depth + (size_t)y * fp.W)[g]);
+                if (fv.present) LEGACY_STORE(c4, &reinterpret_cast<u32x4 *>(fv.present + (size_t)y * fp.W)[g]);
                 if (fv.prequant) {
                     float4 *pq = fv.prequant + (size_t)(fp.H - 1 - y) * fp.W + 4 * g;
                     pq[0] = pq[1] = pq[2] = pq[3] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1641,10 +1649,10 @@ __device__ __forceinline__ void clear_strip(const FrameParams &fp, const FrameBu
             if (fv.busy[ry * fp.tiles_x + t] == fp.epoch || (fp.count > 1 && !owned_bin_tile(fp, t, by))) continue;
             for (int y = y0; y < y1; ++y) {
                 const size_t c = (size_t)(fp.H - 1 - y) * fp.W + x;
-                __builtin_nontemporal_store(fp.clear_rgba, &color[c]);
-                __builtin_nontemporal_store(FLT_MAX, &fv.depth[(size_t)y * fp.W + x]);
+                LEGACY_STORE(fp.clear_rgba, &color[c]);
+                LEGACY_STORE(FLT_MAX, &fv.depth[(size_t)y * fp.W + x]);
                 if (fv.prequant) fv.prequant[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (fv.present) __builtin_nontemporal_store(fp.clear_rgba, &fv.present[(size_t)y * fp.W + x]);
+                if (fv.present) LEGACY_STORE(fp.clear_rgba, &fv.present[(size_t)y * fp.W + x]);
             }
         }
     }

@@ -166,22 +166,24 @@ def gather_frame_device(dist, ctx, target, stream=None, out=None):
     return out
 
 
-_READY = set()
+_READY = []   # the group objects already barriered (held, so a re-created group is never mistaken for one)
 
 
 def ensure_group_ready(dist):
     """One barrier per process group before its first point-to-point batch.  batch_isend_irecv must be
     joined by every rank when it is the group's first NCCL collective, but a rank whose region is empty
     (or rank 0 with no non-empty peer) posts no operation at all; a barrier first makes the batches
-    ordinary point-to-point traffic on an initialised communicator."""
+    ordinary point-to-point traffic on an initialised communicator.  The groups are kept by reference,
+    not by id(): after destroy_process_group and a re-init, CPython could hand the new default group
+    the old one's id while the old object is gone."""
     world = getattr(getattr(dist, "group", None), "WORLD", None)   # the default group (a new one after re-init)
-    key = id(world if world is not None else dist)
-    if key in _READY:
+    key = world if world is not None else dist
+    if any(g is key for g in _READY):
         return
     barrier = getattr(dist, "barrier", None)
     if barrier is not None:
         barrier()
-    _READY.add(key)
+    _READY.append(key)
 
 
 def send_to_root(dist, buf, recvs, sizes):

@@ -184,3 +184,24 @@ def test_owned_pixels_partition_the_frame(w, h, count, regions):
     if regions is None and count == 8:
         # 120 x 68 bin tiles, the last row 16 px high: interleaved ranks get 1020 tiles each
         assert shares[0] == 1020 * 1024 - 120 // 8 * 16 * 32
+
+
+def test_ensure_group_ready_after_reinit():
+    """the barrier before a group's first point-to-point batch runs once per group object --
+    a re-initialised default group gets its own barrier even where CPython reuses the old one's id."""
+    import types
+    from shs_gpu import shard
+    calls = []
+
+    def fake_dist():
+        d = types.SimpleNamespace()
+        d.group = types.SimpleNamespace(WORLD=object())
+        d.barrier = lambda: calls.append(1)
+        return d
+    d = fake_dist()
+    shard.ensure_group_ready(d)
+    shard.ensure_group_ready(d)
+    assert len(calls) == 1
+    d.group.WORLD = object()          # destroy_process_group + init_process_group
+    shard.ensure_group_ready(d)
+    assert len(calls) == 2
