@@ -6,9 +6,12 @@ one cost-balanced rectangle of tiles per rank.  The owned tiles of every rank ar
 the full frame on rank 0.  On GPUs the collective runs over RCCL ("nccl" backend) on device tensors;
 the same code runs over gloo on CPU tensors (tests/test_shard.py).
 
-Only the owned tiles travel: each rank packs its tiles' pixels contiguously (colour RGBA8 as int32
-words, depth as f32 bits), the ranks exchange equal-size padded buffers with all_gather, and rank 0
-scatters them back into canvas / screen rows.
+Only the owned tiles travel.  The device path (gather_frame_device, what bench.py and the C ABI's
+Seam-2 binding use): every rank packs its owned tiles with shs_tiles_pack, sends exactly its packed
+size to rank 0 in one batch of point-to-point operations (send_to_root; region ranks differ in size),
+and rank 0 unpacks every peer's tiles with one shs_tiles_unpack_ranks launch, all ordered on the
+frame's stream.  The host-array path (gather_frame, tests and debugging) packs numpy planes and
+exchanges equal-size padded buffers with all_gather.
 """
 import numpy as np
 
