@@ -1208,12 +1208,13 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     const int bt = (row / (TILE / RTH)) * fp.tiles_x + col;
     const int bt_spill = frame * fp.tiles_x * fp.tiles_y + bt;   // the bin tile's key in spill entries
     constexpr bool no_recs = NO_RECS;   // == (fp.flags & RF_NO_RECS): a kernel variant each
+    const bool scan = !SPANS && fp.scan_mode;   // (SPANS: binned frames only)
     const int dbase = frame * fp.n_draws;                       // the frame's slice of the draw table
 
     // candidate sources.  scan mode: every triangle's bin box.  bin mode: the bin tile's list, then
     // the spill list (entries of this bin tile).
     uint32_t n_bin_total = 0, n_bin = 0, n_spill = 0, n_items;
-    if (fp.scan_mode) {
+    if (scan) {
         n_items = (uint32_t)fp.n_tris;
     } else {
         n_bin_total = fb.tile_count[bt];
@@ -1244,7 +1245,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             const uint32_t item = base + tid + 256u * k;
             uint32_t id = 0xffffffffu;
             if (item < n_items) {
-                if (fp.scan_mode) {
+                if (scan) {
                     id = item;
                 } else if (item < n_bin) {
                     id = bin[item];
@@ -1699,7 +1700,8 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
                                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
     // small single-frame scan-mode scenes: every bin box in registers from the start (batches load
     // each busy tile's frame's boxes, L2-resident)
-    const bool prefetched = fp.scan_mode && fp.n_tris <= CAND && fp.n_frames == 1;
+    // (SPANS: binned frames, never scan mode -- no registers held for the boxes)
+    const bool prefetched = !SPANS && fp.scan_mode && fp.n_tris <= CAND && fp.n_frames == 1;
     uint2 pbx[CAND / 256];
 #pragma unroll
     for (int k = 0; k < CAND / 256; ++k) {
@@ -1707,8 +1709,10 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
         pbx[k] = (prefetched && i < fp.n_tris) ? fb.boxes[i] : make_uint2(0u, 0u);
     }
     // pin the box loads here (the compiler would otherwise sink them to their first use)
+    if constexpr (!SPANS) {
 #pragma unroll
-    for (int k = 0; k < CAND / 256; ++k) asm volatile("" : "+v"(pbx[k].x), "+v"(pbx[k].y));
+        for (int k = 0; k < CAND / 256; ++k) asm volatile("" : "+v"(pbx[k].x), "+v"(pbx[k].y));
+    }
     if (tid < min(n_draws_all, LDS_DRAWS) * 4) sh.du[tid] = du_first;
     // a strip item clears STRIP_RT raster-tile rows of one frame (fewer items: fewer tickets and
     // barriers per cleared byte)
@@ -1728,7 +1732,8 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
         if (s_hi > s_lo) {
             const int f = (int)(s_lo / (uint32_t)strips_y);
             const int sy = (int)s_lo - f * strips_y;
-            for (int ry = sy * STRIP_RT; ry < min((sy + 1) * STRIP_RT, fp.rtiles_y); ++ry) clear_strip(fp, fb, f, ry);
+            if (!(fp.flags & DBG_SKIP_CLEAR))   // (timing experiments: the busy tiles alone)
+                for (int ry = sy * STRIP_RT; ry < min((sy + 1) * STRIP_RT, fp.rtiles_y); ++ry) clear_strip(fp, fb, f, ry);
         } else {
             uint32_t k = item - s_lo;
             if ((fp.flags & RF_XCD_ROWS) && k < (n_busy & ~31u))   // busy item 32B + 8r + x <- entry 32B + 4x + r:
