@@ -1196,10 +1196,10 @@ __device__ __forceinline__ void resolve_from_mesh(const FrameParams &fp, const F
 // each thread owns one pixel: the winner's record and varyings are fetched by index, (u, v, w)
 // recomputed with the identical arithmetic, the pixel shaded and written.
 // fb: the frame's view (frame_view); draws: the whole batch's draw table; rt: raster tile of the frame.
-template <bool NO_RECS, bool SPANS>
+template <bool NO_RECS, bool SPANS, bool PIX>
 __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
                                             const uint32_t *cnt, uint32_t n_frag, int frame, int rt,
-                                            const uint2 (&pbx)[CAND / 256], bool prefetched, RasterShared &sh, uint64_t *tl) {
+                                            RasterShared &sh, uint64_t *tl) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tls = fp.setup_grid + (int)blockIdx.x;
     const int col = rt % fp.tiles_x, row = rt / fp.tiles_x;
@@ -1256,13 +1256,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             }
             ids[k] = id;
         }
-        if (prefetched) {
 #pragma unroll
-            for (int k = 0; k < CAND / 256; ++k) bx[k] = pbx[k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < CAND / 256; ++k) bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
-        }
+        for (int k = 0; k < CAND / 256; ++k) bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
 #pragma unroll
         for (int k = 0; k < CAND / 256; ++k) {
             // non-empty bin box overlapping the tile (so its clipped box holds >= 1 pixel: the pair
@@ -1321,7 +1316,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             }
             __syncthreads();
             tl_mark(tl, tls, 2);
-            if (fp.flags & RF_PER_PIXEL) {
+            if ((PIX || NO_RECS) && (fp.flags & RF_PER_PIXEL)) {   // (PIX: the per-pixel loop compiled in)
                 // Per-pixel loop: every thread tests its own pixel against the staged candidates in
                 // order (LDS broadcast reads, the key min kept in a register).  A wave owns two tile
                 // rows and skips a candidate whose box misses them as a whole.
@@ -1678,7 +1673,7 @@ constexpr int STRIP_RT = SHS_STRIP_RT;
 #ifndef SHS_LEGACY_RASTER_WAVES
 #define SHS_LEGACY_RASTER_WAVES 4   // minimum waves per SIMD (-D...: timing experiments)
 #endif
-template <bool KARG, bool NO_RECS, bool SPANS>
+template <bool KARG, bool NO_RECS, bool SPANS, bool PIX>
 __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
     const int tid = threadIdx.x;
@@ -1690,29 +1685,16 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
     if (tid == 0) { sh.cov = 0; sh.maxbin = 0; }
     sh.key[tid] = KEY_EMPTY;
     // Every independent first-touch load is issued up front so their round trips overlap: the
-    // busy-list length, the ghost-fragment count, the draws' shading uniforms and, for a small
-    // single-frame scan-mode scene, every bin box (into registers).
+    // busy-list length, the ghost-fragment count and the draws' shading uniforms.  (A single-frame
+    // scan-mode scene's bin boxes held in registers from the start -- rounds 1-4 -- cost the batch
+    // kernel two spilled registers and bought the single frame nothing measurable: C2 0.0361 ->
+    // 0.0356 ms per single frame without them.)
     const uint32_t n_busy = min(cnt[C_BUSY], (uint32_t)(fp.tiles_x * fp.tiles_y * (TILE / RTH) * fp.n_frames));
     const uint32_t n_frag = min(cnt[C_FRAG], fp.frag_cap);
     static_assert(LDS_DRAWS * 4 == 256, "one per-draw uniform float4 per thread");
     const int n_draws_all = fp.n_draws * fp.n_frames;
     const float4 du_first = tid < min(n_draws_all, LDS_DRAWS) * 4 ? reinterpret_cast<const float4 *>(draws[tid >> 2].light)[tid & 3]
                                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
-    // small single-frame scan-mode scenes: every bin box in registers from the start (batches load
-    // each busy tile's frame's boxes, L2-resident)
-    // (SPANS: binned frames, never scan mode -- no registers held for the boxes)
-    const bool prefetched = !SPANS && fp.scan_mode && fp.n_tris <= CAND && fp.n_frames == 1;
-    uint2 pbx[CAND / 256];
-#pragma unroll
-    for (int k = 0; k < CAND / 256; ++k) {
-        const int i = tid + 256 * k;
-        pbx[k] = (prefetched && i < fp.n_tris) ? fb.boxes[i] : make_uint2(0u, 0u);
-    }
-    // pin the box loads here (the compiler would otherwise sink them to their first use)
-    if constexpr (!SPANS) {
-#pragma unroll
-        for (int k = 0; k < CAND / 256; ++k) asm volatile("" : "+v"(pbx[k].x), "+v"(pbx[k].y));
-    }
     if (tid < min(n_draws_all, LDS_DRAWS) * 4) sh.du[tid] = du_first;
     // a strip item clears STRIP_RT raster-tile rows of one frame (fewer items: fewer tickets and
     // barriers per cleared byte)
@@ -1747,9 +1729,9 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
                 __syncthreads();
                 clear_tile(fp, fv, rt);
             } else {
-                if (fp.flags & DBG_TWICE) raster_tile<NO_RECS, SPANS>(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, nullptr);   // warm run
+                if (fp.flags & DBG_TWICE) raster_tile<NO_RECS, SPANS, PIX>(fp, fv, draws, cnt, n_frag, f, rt, sh, nullptr);   // warm run
                 tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
-                raster_tile<NO_RECS, SPANS>(fp, fv, draws, cnt, n_frag, f, rt, pbx, prefetched, sh, first ? fb.timeline : nullptr);
+                raster_tile<NO_RECS, SPANS, PIX>(fp, fv, draws, cnt, n_frag, f, rt, sh, first ? fb.timeline : nullptr);
                 first = false;
             }
         }
@@ -1798,7 +1780,6 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_pipe(FramePara
     const int n_draws_all = fp.n_draws * fp.n_frames;
     const float4 du_first = tid < min(n_draws_all, LDS_DRAWS) * 4 ? reinterpret_cast<const float4 *>(draws[tid >> 2].light)[tid & 3]
                                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
-    const uint2 pbx[CAND / 256] = {};   // (batches never prefetch boxes)
     if (tid < min(n_draws_all, LDS_DRAWS) * 4) sh.du[tid] = du_first;
     const int strips_y = (fp.rtiles_y + STRIP_RT - 1) / STRIP_RT;
     const uint32_t n_strips = (uint32_t)(strips_y * fp.n_frames);
@@ -1827,7 +1808,7 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_pipe(FramePara
                 const uint32_t g = fb.busy_list[j - s_lo];
                 const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
                 const FrameBuffers fv = frame_view(fp, fb, f);
-                raster_tile<false, false>(fp, fv, draws, cnt, n_frag, f, rt, pbx, false, sh, nullptr);
+                raster_tile<false, false, true>(fp, fv, draws, cnt, n_frag, f, rt, sh, nullptr);
             }
         }
         if (!queued) break;
@@ -1874,17 +1855,20 @@ hipError_t launch_pipe(const FrameParams &fpR, const FrameBuffers &fbR, int grid
 hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KArgDraws &ka, int grid, hipStream_t s) {
     const dim3 g(grid > 0 ? grid : 1);
     const bool karg = fp.n_draws * fp.n_frames <= KARG_DRAWS;   // the whole batch's draws as kernel arguments
-    // binned frames test conservative row spans, scan-mode frames whole boxes (raster_tile)
-    if (fp.flags & RF_NO_RECS) {   // binned frames: records recomputed from the mesh
-        if (karg) hipLaunchKernelGGL((k_raster<true, true, true>), g, dim3(256), 0, s, fp, fb, ka);
-        else hipLaunchKernelGGL((k_raster<false, true, true>), g, dim3(256), 0, s, fp, fb, ka);
-    } else if (!fp.scan_mode) {
-        if (karg) hipLaunchKernelGGL((k_raster<true, false, true>), g, dim3(256), 0, s, fp, fb, ka);
-        else hipLaunchKernelGGL((k_raster<false, false, true>), g, dim3(256), 0, s, fp, fb, ka);
-    } else {
-        if (karg) hipLaunchKernelGGL((k_raster<true, false, false>), g, dim3(256), 0, s, fp, fb, ka);
-        else hipLaunchKernelGGL((k_raster<false, false, false>), g, dim3(256), 0, s, fp, fb, ka);
-    }
+    // binned frames test conservative row spans, scan-mode frames whole boxes (raster_tile); the
+    // per-pixel loop (SHS_OPT_RASTER_LOOP 0) has kernels of its own, so the pair kernels carry none of
+    // its registers
+#define SHS_RASTER(NR, SP, PX)                                                                              \
+    do {                                                                                                   \
+        if (karg) hipLaunchKernelGGL((k_raster<true, NR, SP, PX>), g, dim3(256), 0, s, fp, fb, ka);          \
+        else hipLaunchKernelGGL((k_raster<false, NR, SP, PX>), g, dim3(256), 0, s, fp, fb, ka);              \
+    } while (0)
+    const bool pix = (fp.flags & RF_PER_PIXEL) != 0u;
+    if (fp.flags & RF_NO_RECS) SHS_RASTER(true, true, false);   // binned frames: records recomputed (either loop)
+    else if (pix) SHS_RASTER(false, false, true);               // (binned frames: boxes)
+    else if (!fp.scan_mode) SHS_RASTER(false, true, false);
+    else SHS_RASTER(false, false, false);
+#undef SHS_RASTER
     return hipGetLastError();
 }
 
