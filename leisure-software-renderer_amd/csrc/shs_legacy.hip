@@ -571,25 +571,20 @@ __device__ __forceinline__ void corner_varyings(const DrawGPU &dr, const float (
     nr = n;
 }
 
-// Quad: corner varyings of lane q (< 3), assembled into the triangle's 80-B ShadeRec; lane q
-// stores floats [5q, 5q + 5) so the quad writes the record contiguously.
+// Quad: the triangle's 80-B ShadeRec (corner k's a at floats 3k.., its nr at 9 + 3k.., then shading
+// and draw): lane q < 3 stores its own corner's six floats, lane 3 the two words.  (Round 4 assembled
+// the record in every lane with 18 quad broadcasts, each lane storing a contiguous fifth: the
+// broadcasts' registers were the bin-mode setup's register peak -- 80 VGPRs against its 64-VGPR
+// bound, spilled.)
 __device__ __forceinline__ void quad_store_shade_at(ShadeRec *rec, int draw, int shading, const f3 &a, const f3 &nr) {
     const int q = __lane_id() & 3;
-    float f[20];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        f[3 * k] = quad_bcast(a.x, k); f[3 * k + 1] = quad_bcast(a.y, k); f[3 * k + 2] = quad_bcast(a.z, k);
-        f[9 + 3 * k] = quad_bcast(nr.x, k); f[9 + 3 * k + 1] = quad_bcast(nr.y, k); f[9 + 3 * k + 2] = quad_bcast(nr.z, k);
-    }
-    f[18] = __int_as_float(shading);
-    f[19] = __int_as_float(draw);
-    float *dst = reinterpret_cast<float *>(rec) + 5 * q;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        float x = f[j];
-#pragma unroll
-        for (int qq = 1; qq < 4; ++qq) x = q == qq ? f[5 * qq + j] : x;
-        dst[j] = x;
+    float *dst = reinterpret_cast<float *>(rec);
+    if (q < 3) {
+        dst[3 * q] = a.x; dst[3 * q + 1] = a.y; dst[3 * q + 2] = a.z;
+        dst[9 + 3 * q] = nr.x; dst[9 + 3 * q + 1] = nr.y; dst[9 + 3 * q + 2] = nr.z;
+    } else {
+        dst[18] = __int_as_float(shading);
+        dst[19] = __int_as_float(draw);
     }
 }
 
@@ -662,7 +657,9 @@ constexpr int SMALL_BT = 8;   // bin tiles a quad appends to by itself (2 per la
 
 // One setup workgroup: 64 triangles, a quad of lanes each.
 // frame / lb: the batch frame and this block's index among the frame's setup blocks; draws = the
-// frame's draw slice (table entries dbase ..).
+// frame's draw slice (table entries dbase ..).  BIN: a bin-mode batch (k_setup<., true>: !fp.scan_mode,
+// fp.ghost_list set, no inline slivers) -- the scan-mode marks and sliver walks are not compiled in.
+template <bool BIN>
 __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws, int dbase,
                                             int frame, int lb, uint32_t *cnt, uint32_t (&s_stat)[4], NewBusy &nb,
                                             float4 *sliv) {
@@ -702,7 +699,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     //    quad's four lanes taking every fourth tile (bin mode marks whole bin tiles at their first
     //    append, below)
     const int rx0 = gx0 / RTW, rx1 = live ? gx1 / RTW : -1, ry0 = gy0 / RTH, ry1 = live ? gy1 / RTH : -1;
-    const int nrx = rx1 - rx0 + 1, n_rt = (live && fp.scan_mode) ? nrx * (ry1 - ry0 + 1) : 0;
+    const int nrx = rx1 - rx0 + 1, n_rt = (live && !BIN) ? nrx * (ry1 - ry0 + 1) : 0;
     if (n_rt > 0 && n_rt <= SMALL_RT) {
         for (int k = q; k < n_rt; k += 4) {
             const int rx = rx0 + k % nrx, ry = ry0 + k / nrx;
@@ -726,7 +723,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
 
     // -- bin appends (large scenes): bin tiles of the bin box, two per quad lane
     uint32_t n_bin = 0;
-    if (!fp.scan_mode && !(fp.flags & DBG_SKIP_BIN)) {
+    if (BIN && !(fp.flags & DBG_SKIP_BIN)) {
         uint32_t *tcount = fb.tile_count;
         const int bx0 = gx0 / TILE, bx1 = live ? gx1 / TILE : -1, by0 = gy0 / TILE, by1 = live ? gy1 / TILE : -1;
         const int nbx = max(bx1 - bx0 + 1, 1), n_bt = live ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0;
@@ -773,7 +770,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
 
     // -- per-block statistics (no same-address global atomics); one lane per quad counts
     const bool lead = qt.valid && q == 0 && !(flags & TRI_CULLED);
-    if (fp.ghost_list) {   // the unbounded slivers, listed for k_ghost (ids < n_tris: never overflows)
+    if (BIN || fp.ghost_list) {   // the unbounded slivers, listed for k_ghost (ids < n_tris: never overflows)
         const bool unb = lead && (flags & TRI_UNBOUNDED);
         const uint32_t slot = wave_append1(&cnt[C_SLIVER], unb);
         if (unb) fb.slivers[slot] = (uint32_t)(frame * fp.n_tris + tri);
@@ -790,7 +787,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     }
     __syncthreads();
     if (tid == 0) fb.blk_stat[frame * fp.setup_blocks + lb] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
-    if (sliv && !(fp.flags & DBG_SKIP_GHOST)) {   // RF_GHOST_INLINE: this wave's unbounded slivers, one at a time
+    if (!BIN && sliv && !(fp.flags & DBG_SKIP_GHOST)) {   // RF_GHOST_INLINE: this wave's unbounded slivers, one at a time
         uint64_t todo = m_unb;
         while (todo) {
             const int src = __ffsll((unsigned long long)todo) - 1;
@@ -803,7 +800,8 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
 }
 
 // One k_setup block b of the batch (setup or ghost role by its index in its frame); draw_tab = the
-// batch's draw table (kernel arguments or the device table).
+// batch's draw table (kernel arguments or the device table).  BIN: as setup_block's (no ghost roles).
+template <bool BIN>
 __device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuffers &fb_all, const DrawGPU *draw_tab, int b,
                                            GhostScratch (&s_ghost)[4], uint32_t (&s_stat)[4], NewBusy &s_new,
                                            SliverRecs (&s_sliv)[4]) {
@@ -819,9 +817,9 @@ __device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuf
     const uint64_t c_start = fb.timeline ? __builtin_amdgcn_s_memtime() : 0ull;
     // (the counter set and the bin counts were zeroed on the setup stream before this launch)
     if (lb < fp.setup_blocks) {
-        setup_block(fp, fb, draws, dbase, frame, lb, cnt, s_stat, s_new,
-                    (fp.flags & RF_GHOST_INLINE) ? s_sliv[threadIdx.x >> 6].rec : nullptr);
-    } else if (lb < fp.setup_blocks + fp.ghost_blocks) {
+        setup_block<BIN>(fp, fb, draws, dbase, frame, lb, cnt, s_stat, s_new,
+                         (!BIN && (fp.flags & RF_GHOST_INLINE)) ? s_sliv[threadIdx.x >> 6].rec : nullptr);
+    } else if (!BIN && lb < fp.setup_blocks + fp.ghost_blocks) {
         const int wave = threadIdx.x >> 6;
         const int gw = (lb - fp.setup_blocks) * 4 + wave;
         const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
@@ -843,13 +841,16 @@ __device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuf
 // 128 VGPRs per SIMD): at 64 VGPRs two setup workgroups fit in the rest instead of one (a few spilled
 // registers; C3 0.668 -> 0.646 ms per step).  Scan-mode setups run once the raster drains, where the
 // spills only cost (C2 0.279 -> 0.287), so they keep the unconstrained build.
+#ifndef SHS_BIN_SETUP_WAVES
+#define SHS_BIN_SETUP_WAVES 8   // (-D...: timing experiments)
+#endif
 template <bool KARG, bool BIN>
-__global__ __launch_bounds__(256, BIN ? 8 : 1) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
+__global__ __launch_bounds__(256, BIN ? SHS_BIN_SETUP_WAVES : 1) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
     __shared__ NewBusy s_new;
     __shared__ SliverRecs s_sliv[4];
-    setup_item(fp, fb_all, draw_table<KARG>(fb_all, ka), (int)blockIdx.x, s_ghost, s_stat, s_new, s_sliv);
+    setup_item<BIN>(fp, fb_all, draw_table<KARG>(fb_all, ka), (int)blockIdx.x, s_ghost, s_stat, s_new, s_sliv);
 }
 
 // ---- k_ghost (ghost_list mode) -----------------------------------------------------------------
@@ -1795,7 +1796,7 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_pipe(FramePara
         const uint32_t k_lo = (uint32_t)(((uint64_t)item * n_setup) / n_items);
         const uint32_t k_hi = (uint32_t)(((uint64_t)(item + 1) * n_setup) / n_items);
         if (k_hi > k_lo) {
-            setup_item(fpS, fbS, fbS.draws, (int)k_lo, s_ghost, s_stat, s_new, s_sliv);
+            setup_item<false>(fpS, fbS, fbS.draws, (int)k_lo, s_ghost, s_stat, s_new, s_sliv);
         } else {
             const uint32_t j = item - k_lo;                   // raster item j of n_raster (k_raster's order)
             const uint32_t s_lo = (uint32_t)(((uint64_t)j * n_strips) / n_raster);
