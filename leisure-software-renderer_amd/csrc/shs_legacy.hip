@@ -993,9 +993,12 @@ __device__ __forceinline__ void load_du(const float4 *p, float4 (&du)[4]) {
 
 // One (triangle, pixel) test: the pixel is in the reference's visited set for this triangle
 // (inside the ibox, or for a bounded ghost where its tile job's clamped rectangle covers it) and
-// its barycentrics pass; returns z.
+// its barycentrics pass; returns z.  The caller's pixel lies in the triangle's bin box (every raster
+// loop walks clipped bin boxes), which is the ibox itself unless the triangle is a ghost: only
+// ghosts test the ibox.
 __device__ __forceinline__ bool pixel_test(const FrameParams &fp, const TriRec &r, int px, int py, float &z) {
-    const bool in_ibox = px >= lo16(r.ibx) && px <= hi16(r.ibx) && py >= lo16(r.iby) && py <= hi16(r.iby);
+    const bool in_ibox = !(r.flags & TRI_GHOST) ||
+                         (px >= lo16(r.ibx) && px <= hi16(r.ibx) && py >= lo16(r.iby) && py <= hi16(r.iby));
     bool test = in_ibox;
     if (!in_ibox && (r.flags & TRI_GHOST)) {
         // draw_triangle_tile's visited rectangle in this pixel's tile job (blinn_phong_shading.cpp:208-224)
