@@ -286,7 +286,9 @@ static int enqueue_frame(shs_ctx *ctx) {
     const int slot = (int)(ctx->frame_index & 1u);
     shs_ctx::LegacySlot &ws = ctx->lslot[slot];
     // pipelined batches run everything on the context stream (one launch per batch)
-    hipStream_t sst = pipe ? ctx->stream : ctx->setup_stream, st = ctx->stream;
+    // SHS_LEGACY_ONE_STREAM=1 (timing experiments): the setup on the raster's stream, in order
+    static const bool one_stream_env = shs_exp_env("SHS_LEGACY_ONE_STREAM") && std::atoi(shs_exp_env("SHS_LEGACY_ONE_STREAM")) != 0;
+    hipStream_t sst = (pipe || one_stream_env) ? ctx->stream : ctx->setup_stream, st = ctx->stream;
     if (ws.used) HIP_TRY(ctx, hipEventSynchronize(ws.setup_done));
     *ws.h_ov = 0u;   // the slot's previous setup (the only other writer) is done
 
