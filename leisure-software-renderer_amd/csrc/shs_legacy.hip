@@ -31,6 +31,7 @@
 // reference visits outside it and hand the rare passing ones to k_raster as fragments.
 // DESIGN.md has the derivation.
 #include <float.h>
+#include <limits.h>
 
 #include "shs_device.hpp"
 #include "shs_internal.hpp"
@@ -432,20 +433,61 @@ __device__ __forceinline__ TriRec quad_record(const FrameParams &fp, const DrawG
     return r;
 }
 
-// q = n / d, r = n % d for 0 <= n < 2^24, 1 <= d < 2^24 (rd = 1.0f / d): the float quotient is
-// within 1 of the exact one, fixed up by the remainder.
-// q = n / d, r = n % d for 0 <= n < 2^31, 1 <= d, provided the true quotient is < 2^22 (the
-// float product's relative error 2^-23 then moves it by less than one).
-__device__ __forceinline__ void div_small(int n, int d, float rd, int &q, int &r) {
-    q = (int)((float)n * rd);
-    r = n - q * d;
-    if (r < 0) { --q; r += d; }
-    if (r >= d) { ++q; r -= d; }
+// Conservative row span of a staged candidate inside its clipped box [bx0, bx1]: the pixels of row py
+// that can pass bary_pass (barycentric_coordinate, shs_renderer.hpp:802-821).  With t = px + 0.5 - ax,
+// Y = py + 0.5 - ay the exact Gram-form barycentrics of the record's float values are linear in t:
+//   v = av t + cv,  w = aw t + cw,  u = 1 - v - w,
+//   av = (d11 v0x - d01 v1x) / denom, cv = Y (d11 v0y - d01 v1y) / denom (w: d00 / v1 and v0 swapped).
+// bary_pass's float evaluation (no contraction) is within ~8 u Mv of v, Mv = (|d11| S0 + |d01| S1) /
+// |denom| with S0 = |v0x| |t| + |v0y| |Y|, S1 likewise (u = 2^-24: the rounding of t, the products
+// and sums of d20 / d21, the outer products, the difference and the division; likewise w), and u's
+// within ~10 u (1 + Mv + Mw).  A pixel can pass only where every exact barycentric is >= minus its
+// bound; each half-line a t >= -e - c is solved here in float with e = E (...) at E = 2^-18 (>= 6x the
+// bound: the slack absorbs this computation's own roundings, a few u of the magnitudes), and 2^-12 px
+// more covers the conversion to pixel indices.  Non-finite records keep the whole box row.  The bound
+// holds outside the triangle's bbox too (the 80x80 tile clamp's ghost pixels, section 5 of DESIGN.md).
+// tests/test_legacy_row_spans.py restates this in numpy and checks it against the per-pixel test.
+__device__ __forceinline__ void legacy_row_span(const float4 r0, const float4 r1, const float4 r2, int py, int bx0, int bx1,
+                                                int &x0, int &x1) {
+    x0 = bx0; x1 = bx1;
+    // r0, r1, r2: the record's first three float4s: ax ay v0x v0y | v1x v1y d00 d01 | d11 denom ...
+    const float ax = r0.x, ay = r0.y, v0x = r0.z, v0y = r0.w, v1x = r1.x, v1y = r1.y, d00 = r1.z, d01 = r1.w;
+    const float d11 = r2.x, den = r2.y;
+    if (!(isfinite(ax) && isfinite(ay) && isfinite(v0x) && isfinite(v0y) && isfinite(v1x) && isfinite(v1y) && isfinite(d00) &&
+          isfinite(d01) && isfinite(d11) && isfinite(den) && fabsf(den) > 0.0f))
+        return;
+    constexpr float E = 0x1p-18f;
+    const float Y = ((float)py + 0.5f) - ay, aY = fabsf(Y);
+    const float T = fmaxf(fabsf(((float)bx0 + 0.5f) - ax), fabsf(((float)bx1 + 0.5f) - ax));
+    const float idn = 1.0f / den, aid = fabsf(idn);
+    const float s0 = fabsf(v0x) * T + fabsf(v0y) * aY, s1 = fabsf(v1x) * T + fabsf(v1y) * aY;
+    const float mv = aid * (fabsf(d11) * s0 + fabsf(d01) * s1), mw = aid * (fabsf(d00) * s1 + fabsf(d01) * s0);
+    const float av = (d11 * v0x - d01 * v1x) * idn, cv = ((d11 * v0y - d01 * v1y) * idn) * Y;
+    const float aw = (d00 * v1x - d01 * v0x) * idn, cw = ((d00 * v1y - d01 * v0y) * idn) * Y;
+    float lo = -1e30f, hi = 1e30f;
+    auto edge = [&](float a, float c, float e) {   // a t + c >= -e
+        const float b = -e - c;
+        if (a > 0.0f) lo = fmaxf(lo, b / a);
+        else if (a < 0.0f) hi = fminf(hi, b / a);
+        else if (b > 0.0f) { lo = 1e30f; hi = -1e30f; }
+    };
+    edge(av, cv, E * mv);
+    edge(aw, cw, E * mw);
+    edge(-(av + aw), 1.0f - (cv + cw), E * (1.0f + 2.0f * (mv + mw)));
+    const float flo = (lo + ax) - 0.5f, fhi = (hi + ax) - 0.5f;
+    const float slo = 0x1p-12f * ((fabsf(lo) + fabsf(ax)) + 1.0f), shi = 0x1p-12f * ((fabsf(hi) + fabsf(ax)) + 1.0f);
+    x0 = max(bx0, (int)ceilf(fmaxf(fminf(flo - slo, 1e9f), -1e9f)));
+    x1 = min(bx1, (int)floorf(fmaxf(fminf(fhi + shi, 1e9f), -1e9f)));
 }
 
-// Every pixel sliver `tri` (record t) visits outside its ibox in the reference's tile jobs, the
-// slice-th 64-pixel batch of every `stride`: passing ones become ghost fragments.  Wave-uniform
-// arguments, converged wave.
+// Every pixel sliver `tri` (record t) visits outside its ibox in the reference's tile jobs that can
+// pass: passing ones become ghost fragments.  The visited set is walked line by line -- the edge
+// columns over their rows (Yout u Yin), then the edge rows over Xin -- and on each line only the
+// pixels inside its conservative span (legacy_row_span: every pixel that can pass barycentric_coordinate
+// lies in it, outside the bbox too; a column's span is the row span of the record with x and y
+// swapped, which leaves every Gram term and every computed barycentric bit-identical).  Round 4 tested
+// every visited pixel: up to the edge columns times the bbox height per sliver.  The slice-th line
+// of every `stride` / 64 lines per lane.  Wave-uniform arguments, converged wave.
 __device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, const TriRec &t,
                                               uint32_t tri, uint32_t frame, int slice, int stride) {
     const int lane = __lane_id();
@@ -454,51 +496,71 @@ __device__ __forceinline__ void sliver_pixels(const FrameParams &fp, const Frame
     classify_axis(fp.rt_x, fp.rtw, fp.W, t.fminx, t.fmaxx, sp.cl, sp.cr, sp.xi0, sp.xi1);
     classify_axis(fp.rt_y, fp.rth, fp.H, t.fminy, t.fmaxy, sp.ru, sp.rd, sp.yi0, sp.yi1);
     const int nxo = sp.cl + sp.cr, nyo = sp.ru + sp.rd;
-    const int nxi = max(sp.xi1 - sp.xi0 + 1, 0), nyi = max(sp.yi1 - sp.yi0 + 1, 0);
-    const int ny = nyo + nyi;
-    // total <= W * H <= 2^28 (the ABI caps frames at 16384 x 16384): 32-bit indices.  Divisions by
-    // reciprocal with a +-1 fix: the quotients are pixel columns / rows (< 2^14 < 2^22), so the float
-    // estimate n * (1/d) is off by less than one and one correction step restores q and r exactly.
-    const int total_a = nxo * ny, total = total_a + nxi * nyo;
-    const float rny = 1.0f / (float)max(ny, 1), rnyo = 1.0f / (float)max(nyo, 1);
-    for (int kb = slice * 64; kb < total; kb += stride) {
-        const int k = kb + lane;
-        bool pass = false;
-        int px = 0, py = 0;
-        float z = 0.f, u = 0.f, v = 0.f, w = 0.f;
-        if (k < total) {
-            if (k < total_a) {
-                int xi, yi;
-                div_small(k, ny, rny, xi, yi);
-                px = edge_coord(xi, sp.cl, fp.rt_x, sp.cr, fp.rtw, fp.W);
-                py = yi < nyo ? edge_coord(yi, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H) : sp.yi0 + (yi - nyo);
-            } else {
-                int xi, yi;
-                div_small(k - total_a, nyo, rnyo, xi, yi);
-                px = sp.xi0 + xi;
-                py = edge_coord(yi, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H);
-            }
-            const bool in_ibox = px >= ix0 && px <= ix1 && py >= iy0 && py <= iy1;   // k_raster's part
-            if (!in_ibox && (fp.count == 1 || owned_bin_tile(fp, px / TILE, py / TILE)) && bary_pass(t, (float)px + 0.5f, (float)py + 0.5f, u, v, w)) {
-                z = (u * t.z0 + v * t.z1) + w * t.z2;
-                pass = z < FLT_MAX;   // NaN / FLT_MAX never pass the strict z test
-            }
+    const int n_lines = nxo + nyo;
+    // the rows an edge column visits span [y_lo, y_hi] (its span's distance bound)
+    const int yo0 = nyo ? edge_coord(0, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H) : INT_MAX;
+    const int yo1 = nyo ? edge_coord(nyo - 1, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H) : INT_MIN;
+    const bool yin = sp.yi0 <= sp.yi1;
+    const int y_lo = min(yo0, yin ? sp.yi0 : INT_MAX), y_hi = max(yo1, yin ? sp.yi1 : INT_MIN);
+    const float4 r2 = make_float4(t.d11, t.denom, 0.0f, 0.0f);
+    for (int lb = slice * 64; lb < n_lines; lb += stride) {
+        const int L = lb + lane;
+        // this lane's line: a column x over the Yin run [a0, a1] then the edge rows j in [0, nyo) inside
+        // [s0, s1]; or a row y over the Xin run [a0, a1]
+        const bool col = L < nxo;
+        const int fixed = col ? edge_coord(L, sp.cl, fp.rt_x, sp.cr, fp.rtw, fp.W)
+                              : edge_coord(L - nxo, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H);
+        int a0 = 0, a1 = -1, s0 = 1, s1 = 0;
+        if (L < n_lines && (col || sp.xi0 <= sp.xi1)) {
+            const float4 q0 = col ? make_float4(t.ay, t.ax, t.v0y, t.v0x) : make_float4(t.ax, t.ay, t.v0x, t.v0y);   // x <-> y
+            const float4 q1 = col ? make_float4(t.v1y, t.v1x, t.d00, t.d01) : make_float4(t.v1x, t.v1y, t.d00, t.d01);
+            legacy_row_span(q0, q1, r2, fixed, col ? y_lo : sp.xi0, col ? y_hi : sp.xi1, s0, s1);
+            a0 = col ? max(sp.yi0, s0) : s0;
+            a1 = col ? (yin ? min(sp.yi1, s1) : -1) : s1;
         }
-        const uint32_t slot = wave_append1(&cnt[C_FRAG], pass);
-        if (pass) {
-            if (slot < fp.frag_cap) {
-                GhostFrag g;
-                g.xy = (uint32_t)px | ((uint32_t)py << 16);
-                g.z = z;
-                g.id = tri;
-                g.v = v;
-                g.w = w;
-                g.frame = frame;
-                g.pad[0] = g.pad[1] = 0u;
-                fb.frags[slot] = g;
-                mark_busy_direct(fp, fb, cnt, (int)frame, (py / RTH) * fp.tiles_x + px / RTW);
-            } else {
-                raise_overflow(&cnt[C_OVERFLOW], OV_FRAG, fb.ov_host);
+        int i = a0, j = 0;   // next run pixel, next edge row
+        while (true) {
+            bool have = false;
+            int px = 0, py = 0;
+            if (i <= a1) {
+                have = true;
+                px = col ? fixed : i;
+                py = col ? i : fixed;
+                ++i;
+            } else if (col) {
+                while (j < nyo && !have) {
+                    const int y = edge_coord(j, sp.ru, fp.rt_y, sp.rd, fp.rth, fp.H);
+                    ++j;
+                    if (y >= s0 && y <= s1) { have = true; px = fixed; py = y; }
+                }
+            }
+            if (__ballot(have) == 0ull) break;
+            bool pass = false;
+            float z = 0.f, u = 0.f, v = 0.f, w = 0.f;
+            if (have) {
+                const bool in_ibox = px >= ix0 && px <= ix1 && py >= iy0 && py <= iy1;   // k_raster's part
+                if (!in_ibox && (fp.count == 1 || owned_bin_tile(fp, px / TILE, py / TILE)) &&
+                    bary_pass(t, (float)px + 0.5f, (float)py + 0.5f, u, v, w)) {
+                    z = (u * t.z0 + v * t.z1) + w * t.z2;
+                    pass = z < FLT_MAX;   // NaN / FLT_MAX never pass the strict z test
+                }
+            }
+            const uint32_t slot = wave_append1(&cnt[C_FRAG], pass);
+            if (pass) {
+                if (slot < fp.frag_cap) {
+                    GhostFrag g;
+                    g.xy = (uint32_t)px | ((uint32_t)py << 16);
+                    g.z = z;
+                    g.id = tri;
+                    g.v = v;
+                    g.w = w;
+                    g.frame = frame;
+                    g.pad[0] = g.pad[1] = 0u;
+                    fb.frags[slot] = g;
+                    mark_busy_direct(fp, fb, cnt, (int)frame, (py / RTH) * fp.tiles_x + px / RTW);
+                } else {
+                    raise_overflow(&cnt[C_OVERFLOW], OV_FRAG, fb.ov_host);
+                }
             }
         }
     }
@@ -840,12 +902,13 @@ __device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuf
 // BIN: a bin-mode batch's setup runs beside its raster, which keeps three workgroups per CU (3 waves x
 // 128 VGPRs per SIMD): at 64 VGPRs two setup workgroups fit in the rest instead of one (a few spilled
 // registers; C3 0.668 -> 0.646 ms per step).  Scan-mode setups run once the raster drains, where the
-// spills only cost (C2 0.279 -> 0.287), so they keep the unconstrained build.
+// spills only cost (C2 0.279 -> 0.287): they keep five waves per SIMD (96 VGPRs, none spilled; the
+// span-walked slivers would take 104 unbounded, four waves).
 #ifndef SHS_BIN_SETUP_WAVES
 #define SHS_BIN_SETUP_WAVES 8   // (-D...: timing experiments)
 #endif
 template <bool KARG, bool BIN>
-__global__ __launch_bounds__(256, BIN ? SHS_BIN_SETUP_WAVES : 1) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
+__global__ __launch_bounds__(256, BIN ? SHS_BIN_SETUP_WAVES : 5) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
     __shared__ NewBusy s_new;
@@ -1016,53 +1079,6 @@ __device__ __forceinline__ bool pixel_test(const FrameParams &fp, const TriRec &
     if (!(test && bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w))) return false;
     z = (u * r.z0 + v * r.z1) + w * r.z2;
     return z < FLT_MAX;   // NaN and FLT_MAX never beat the FLT_MAX clear
-}
-
-// Conservative row span of a staged candidate inside its clipped box [bx0, bx1]: the pixels of row py
-// that can pass bary_pass (barycentric_coordinate, shs_renderer.hpp:802-821).  With t = px + 0.5 - ax,
-// Y = py + 0.5 - ay the exact Gram-form barycentrics of the record's float values are linear in t:
-//   v = av t + cv,  w = aw t + cw,  u = 1 - v - w,
-//   av = (d11 v0x - d01 v1x) / denom, cv = Y (d11 v0y - d01 v1y) / denom (w: d00 / v1 and v0 swapped).
-// bary_pass's float evaluation (no contraction) is within ~8 u Mv of v, Mv = (|d11| S0 + |d01| S1) /
-// |denom| with S0 = |v0x| |t| + |v0y| |Y|, S1 likewise (u = 2^-24: the rounding of t, the products
-// and sums of d20 / d21, the outer products, the difference and the division; likewise w), and u's
-// within ~10 u (1 + Mv + Mw).  A pixel can pass only where every exact barycentric is >= minus its
-// bound; each half-line a t >= -e - c is solved here in float with e = E (...) at E = 2^-18 (>= 6x the
-// bound: the slack absorbs this computation's own roundings, a few u of the magnitudes), and 2^-12 px
-// more covers the conversion to pixel indices.  Non-finite records keep the whole box row.  The bound
-// holds outside the triangle's bbox too (the 80x80 tile clamp's ghost pixels, section 5 of DESIGN.md).
-// tests/test_legacy_row_spans.py restates this in numpy and checks it against the per-pixel test.
-__device__ __forceinline__ void legacy_row_span(const float4 r0, const float4 r1, const float4 r2, int py, int bx0, int bx1,
-                                                int &x0, int &x1) {
-    x0 = bx0; x1 = bx1;
-    // r0, r1, r2: the record's first three float4s: ax ay v0x v0y | v1x v1y d00 d01 | d11 denom ...
-    const float ax = r0.x, ay = r0.y, v0x = r0.z, v0y = r0.w, v1x = r1.x, v1y = r1.y, d00 = r1.z, d01 = r1.w;
-    const float d11 = r2.x, den = r2.y;
-    if (!(isfinite(ax) && isfinite(ay) && isfinite(v0x) && isfinite(v0y) && isfinite(v1x) && isfinite(v1y) && isfinite(d00) &&
-          isfinite(d01) && isfinite(d11) && isfinite(den) && fabsf(den) > 0.0f))
-        return;
-    constexpr float E = 0x1p-18f;
-    const float Y = ((float)py + 0.5f) - ay, aY = fabsf(Y);
-    const float T = fmaxf(fabsf(((float)bx0 + 0.5f) - ax), fabsf(((float)bx1 + 0.5f) - ax));
-    const float idn = 1.0f / den, aid = fabsf(idn);
-    const float s0 = fabsf(v0x) * T + fabsf(v0y) * aY, s1 = fabsf(v1x) * T + fabsf(v1y) * aY;
-    const float mv = aid * (fabsf(d11) * s0 + fabsf(d01) * s1), mw = aid * (fabsf(d00) * s1 + fabsf(d01) * s0);
-    const float av = (d11 * v0x - d01 * v1x) * idn, cv = ((d11 * v0y - d01 * v1y) * idn) * Y;
-    const float aw = (d00 * v1x - d01 * v0x) * idn, cw = ((d00 * v1y - d01 * v0y) * idn) * Y;
-    float lo = -1e30f, hi = 1e30f;
-    auto edge = [&](float a, float c, float e) {   // a t + c >= -e
-        const float b = -e - c;
-        if (a > 0.0f) lo = fmaxf(lo, b / a);
-        else if (a < 0.0f) hi = fminf(hi, b / a);
-        else if (b > 0.0f) { lo = 1e30f; hi = -1e30f; }
-    };
-    edge(av, cv, E * mv);
-    edge(aw, cw, E * mw);
-    edge(-(av + aw), 1.0f - (cv + cw), E * (1.0f + 2.0f * (mv + mw)));
-    const float flo = (lo + ax) - 0.5f, fhi = (hi + ax) - 0.5f;
-    const float slo = 0x1p-12f * ((fabsf(lo) + fabsf(ax)) + 1.0f), shi = 0x1p-12f * ((fabsf(hi) + fabsf(ax)) + 1.0f);
-    x0 = max(bx0, (int)ceilf(fmaxf(fminf(flo - slo, 1e9f), -1e9f)));
-    x1 = min(bx1, (int)floorf(fmaxf(fminf(fhi + shi, 1e9f), -1e9f)));
 }
 
 constexpr int RCHUNK = 64;         // candidate records staged per pass (one wave scans their areas)

@@ -156,3 +156,88 @@ def test_legacy_row_spans_sliver_rows_exhaustive():
                     missed += not (s0 <= px <= s1)
     assert missed == 0
     assert passing > 100
+
+
+def _inside_vec(rec, px, py):
+    """_inside over arrays of pixels (float32, the same operation order)."""
+    ax, ay, v0x, v0y, v1x, v1y, d00, d01, d11, den = rec
+    with np.errstate(all="ignore"):
+        vpx = (px.astype(f) + f(0.5)).astype(f) - ax
+        vpy = (py.astype(f) + f(0.5)).astype(f) - ay
+        d20 = (vpx * v0x).astype(f) + (vpy * v0y).astype(f)
+        d21 = (vpx * v1x).astype(f) + (vpy * v1y).astype(f)
+        nv = (d11 * d20).astype(f) - (d01 * d21).astype(f)
+        nw = (d00 * d21).astype(f) - (d01 * d20).astype(f)
+        v = (nv / den).astype(f)
+        w = (nw / den).astype(f)
+        u = ((f(1.0) - v).astype(f) - w).astype(f)
+    return ~((u < 0) | (v < 0) | (w < 0))
+
+
+def _classify(n_rt, rts, extent, fmin, fmax):
+    """classify_axis (shs_legacy.hip): reference-tile columns before / after [fmin, fmax], the span of the rest."""
+    before = sum(1 for c in range(n_rt) if f(min(c * rts + rts, extent) - 1) < fmin)
+    after = sum(1 for c in range(n_rt) if f(c * rts) > fmax)
+    lo, hi = 0, -1
+    if before + after < n_rt:
+        c0, c1 = before, n_rt - 1 - after
+        lo = int(max(f(c0 * rts), fmin))
+        hi = int(min(f(min(c1 * rts + rts, extent) - 1), fmax))
+    return before, after, lo, hi
+
+
+def _edge(i, before, n_rt, after, rts, extent):
+    return min((i + 1) * rts, extent) - 1 if i < before else (n_rt - after + (i - before)) * rts
+
+
+def test_legacy_spans_hold_tile_clamp_lines():
+    """sliver_pixels (shs_legacy.hip) walks an unbounded sliver's tile-clamp pixels line by line and
+    tests only each line's span: a row's is legacy_row_span of the record, a column's that of the
+    record with x and y swapped (every Gram term and computed barycentric is bit-identical under the
+    swap).  Every visited pixel that passes the reference's test must lie in its line's span, however
+    far from the bbox the reference tile's edge line is (80x80 tiles over 1920x1080)."""
+    rng = np.random.default_rng(4242)
+    W, H, T = 1920, 1080, 80
+    rt_x, rt_y = (W + T - 1) // T, (H + T - 1) // T
+    passing = missed = lines = 0
+    for it in range(120):
+        base = rng.uniform(40, 1880, 2).astype(np.float64)
+        d = rng.uniform(-900, 900, 2)
+        # near-degenerate slivers: the third corner within ~1e-3..1e-5 px of the first edge's line
+        pts = np.array([base, base + d, base + d * rng.uniform(0.05, 0.95) + rng.normal(0, 10.0 ** -rng.uniform(3, 5), 2)])
+        pts = np.clip(pts, -50, [W + 50, H + 50]).astype(f)
+        rec = _record(pts)
+        if not abs(rec[-1]) >= 1e-5:
+            continue
+        recs = _record(pts[:, ::-1])   # x <-> y
+        fminx, fmaxx = f(pts[:, 0].min()), f(pts[:, 0].max())
+        fminy, fmaxy = f(pts[:, 1].min()), f(pts[:, 1].max())
+        ix0, ix1 = max(0, int(np.floor(fminx))), min(W - 1, int(np.floor(fmaxx)))
+        iy0, iy1 = max(0, int(np.floor(fminy))), min(H - 1, int(np.floor(fmaxy)))
+        cl, cr, xi0, xi1 = _classify(rt_x, T, W, fminx, fmaxx)
+        ru, rd, yi0, yi1 = _classify(rt_y, T, H, fminy, fmaxy)
+        yout = [_edge(j, ru, rt_y, rd, T, H) for j in range(ru + rd)]
+        ys = np.array(yout + list(range(yi0, yi1 + 1)), dtype=np.int64)
+        if len(ys):
+            y_lo, y_hi = int(ys.min()), int(ys.max())
+            for i in range(cl + cr):   # edge columns over Yout u Yin
+                x = _edge(i, cl, rt_x, cr, T, W)
+                lines += 1
+                ok = _inside_vec(rec, np.full(len(ys), x), ys)
+                out = ~((x >= ix0) & (x <= ix1) & (ys >= iy0) & (ys <= iy1))
+                s0, s1 = legacy_span(recs, x, y_lo, y_hi)
+                hit = ok & out
+                passing += int(hit.sum())
+                missed += int((hit & ((ys < s0) | (ys > s1))).sum())
+        if xi0 <= xi1:
+            xs = np.arange(xi0, xi1 + 1)
+            for y in yout:   # edge rows over Xin
+                lines += 1
+                ok = _inside_vec(rec, xs, np.full(len(xs), y))
+                out = ~((xs >= ix0) & (xs <= ix1) & (y >= iy0) & (y <= iy1))
+                s0, s1 = legacy_span(rec, y, xi0, xi1)
+                hit = ok & out
+                passing += int(hit.sum())
+                missed += int((hit & ((xs < s0) | (xs > s1))).sum())
+    assert lines > 500
+    assert missed == 0, f"{missed} of {passing} passing tile-clamp pixels outside their line's span"
