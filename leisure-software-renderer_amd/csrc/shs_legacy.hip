@@ -289,12 +289,17 @@ struct NewBusy {
     uint32_t e[NEW_BUSY_CAP];
 };
 
-__device__ __forceinline__ void mark_busy(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int frame, int rt,
+// The tile's listing once its mark found it not yet busy (old != epoch).
+__device__ __forceinline__ void list_busy(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int frame, int rt,
                                           NewBusy &nb) {
-    if (atomicExch(&fb.busy[rt], fp.epoch) == fp.epoch) return;
     const uint32_t k = atomicAdd(&nb.n, 1u);
     if (k < (uint32_t)NEW_BUSY_CAP) nb.e[k] = busy_entry(fp, frame, rt);
     else fb.busy_list[atomicAdd(&cnt[C_BUSY], 1u)] = busy_entry(fp, frame, rt);
+}
+
+__device__ __forceinline__ void mark_busy(const FrameParams &fp, const FrameBuffers &fb, uint32_t *cnt, int frame, int rt,
+                                          NewBusy &nb) {
+    if (atomicExch(&fb.busy[rt], fp.epoch) != fp.epoch) list_busy(fp, fb, cnt, frame, rt, nb);
 }
 
 // Bin mode: the first append to bin tile t (its counter returned 0) makes the tile's raster rows busy.
@@ -763,10 +768,25 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     const int rx0 = gx0 / RTW, rx1 = live ? gx1 / RTW : -1, ry0 = gy0 / RTH, ry1 = live ? gy1 / RTH : -1;
     const int nrx = rx1 - rx0 + 1, n_rt = (live && !BIN) ? nrx * (ry1 - ry0 + 1) : 0;
     if (n_rt > 0 && n_rt <= SMALL_RT) {
-        for (int k = q; k < n_rt; k += 4) {
-            const int rx = rx0 + k % nrx, ry = ry0 + k / nrx;
-            if (!sharded || owned_bin_tile(fp, rx, ry / (TILE / RTH))) mark_busy(fp, fb, cnt, frame, ry * fp.tiles_x + rx, nb);
+        // every mark's exchange is issued before any result is used: one round trip, not one per tile
+        int rts[SMALL_RT / 4];
+        uint32_t old[SMALL_RT / 4];
+#pragma unroll
+        for (int i = 0; i < SMALL_RT / 4; ++i) {
+            const int k = q + 4 * i;
+            rts[i] = -1;
+            old[i] = fp.epoch;
+            if (k < n_rt) {
+                const int rx = rx0 + k % nrx, ry = ry0 + k / nrx;
+                if (!sharded || owned_bin_tile(fp, rx, ry / (TILE / RTH))) {
+                    rts[i] = ry * fp.tiles_x + rx;
+                    old[i] = atomicExch(&fb.busy[rts[i]], fp.epoch);
+                }
+            }
         }
+#pragma unroll
+        for (int i = 0; i < SMALL_RT / 4; ++i)
+            if (rts[i] >= 0 && old[i] != fp.epoch) list_busy(fp, fb, cnt, frame, rts[i], nb);
     }
     {
         uint64_t big = __ballot(n_rt > SMALL_RT && q == 0);

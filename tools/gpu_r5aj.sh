@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 5: scan-mode busy marks with every exchange issued before any result is used (working tree)
+# against HEAD (libshs_base.so): legacy parity, C2 / C3 A/B three times, the C2 batch timeline.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_gpu_parity.py tests/test_batch.py tests/test_shipped_frames.py > gpurun_out/r5aj_tests.log 2>&1 || { tail -30 gpurun_out/r5aj_tests.log; exit 1; }
+tail -1 gpurun_out/r5aj_tests.log
+for rep in 1 2 3; do
+  for c in c2 c3; do
+    for v in base gpu; do
+      SHS_GPU_LIB=$(pwd)/leisure-software-renderer_amd/shs_gpu/libshs_$v.so timeout -k 10 200 python bench.py --config $c --no-pmc --no-cpu --no-single --no-pcie --strong '' --steps 100 --warmup 10 \
+        > gpurun_out/r5aj_${c}_$v.log 2>&1 || { tail -20 gpurun_out/r5aj_${c}_$v.log; exit 1; }
+      python3 - gpurun_out/r5aj_${c}_$v.log $c $v <<'PY'
+import json,sys
+d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])
+print(sys.argv[2], sys.argv[3], 'ms/step', d['ms_per_step'], 'kernels', d.get('kernels_ms'))
+PY
+    done
+  done
+done
+timeout -k 10 200 python tools/timeline_batch.py c2 > gpurun_out/r5aj_tlb_c2.txt 2>&1 || exit 1
+grep -E "median of|ended by|span" gpurun_out/r5aj_tlb_c2.txt | tail -8
