@@ -869,6 +869,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     }
     __syncthreads();
     if (tid == 0) fb.blk_stat[frame * fp.setup_blocks + lb] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
+    tl_mark(fb.timeline, blockIdx.x, 5);
     if (!BIN && sliv && !(fp.flags & DBG_SKIP_GHOST)) {   // RF_GHOST_INLINE: this wave's unbounded slivers, one at a time
         uint64_t todo = m_unb;
         while (todo) {

@@ -35,7 +35,7 @@ def main():
         # (batches: ghost waves inline or in k_ghost, so every k_setup workgroup is a setup block)
         summarize("setup", s, t0)
         summarize("raster", r, t0)
-        phases(s, ["draw", "setup_tri", "busy", "bins", "make_rec"], "setup")
+        phases(s, ["draw", "setup_tri", "busy", "bins", "make_rec", "stats"], "setup")
         st = (s[:, 0].astype(np.int64) - t0) / 100.0
         en = (s[:, 1].astype(np.int64) - t0) / 100.0
         for q in (0.25, 0.5, 0.75, 0.9, 1.0):
