@@ -36,6 +36,7 @@ def main():
         summarize("setup", s, t0)
         summarize("raster", r, t0)
         phases(s, ["draw", "setup_tri", "busy", "bins", "make_rec", "stats"], "setup")
+        phases(r, ["busy_list", "gather", "staged", "rastered", "shaded", "written"], "raster first tile")
         st = (s[:, 0].astype(np.int64) - t0) / 100.0
         en = (s[:, 1].astype(np.int64) - t0) / 100.0
         for q in (0.25, 0.5, 0.75, 0.9, 1.0):
