@@ -1237,7 +1237,10 @@ __device__ __forceinline__ void resolve_from_mesh(const FrameParams &fp, const F
 // each thread owns one pixel: the winner's record and varyings are fetched by index, (u, v, w)
 // recomputed with the identical arithmetic, the pixel shaded and written.
 // fb: the frame's view (frame_view); draws: the whole batch's draw table; rt: raster tile of the frame.
-template <bool NO_RECS, bool SPANS, bool PIX>
+// SCAN: the frame's candidate source -- 0 binned, 1 scan mode (every bin box), 2 fp.scan_mode at run
+// time (the per-pixel kernels and k_pipe).
+constexpr int SCAN_BINNED = 0, SCAN_ALL = 1, SCAN_RUNTIME = 2;
+template <bool NO_RECS, bool SPANS, bool PIX, int SCAN>
 __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *draws,
                                             const uint32_t *cnt, uint32_t n_frag, int frame, int rt,
                                             RasterShared &sh, uint64_t *tl) {
@@ -1249,7 +1252,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     const int bt = (row / (TILE / RTH)) * fp.tiles_x + col;
     const int bt_spill = frame * fp.tiles_x * fp.tiles_y + bt;   // the bin tile's key in spill entries
     constexpr bool no_recs = NO_RECS;   // == (fp.flags & RF_NO_RECS): a kernel variant each
-    const bool scan = !SPANS && fp.scan_mode;   // (SPANS: binned frames only)
+    const bool scan = SCAN == SCAN_RUNTIME ? fp.scan_mode != 0u : SCAN == SCAN_ALL;
     const int dbase = frame * fp.n_draws;                       // the frame's slice of the draw table
 
     // candidate sources.  scan mode: every triangle's bin box.  bin mode: the bin tile's list, then
@@ -1714,7 +1717,7 @@ constexpr int STRIP_RT = SHS_STRIP_RT;
 #ifndef SHS_LEGACY_RASTER_WAVES
 #define SHS_LEGACY_RASTER_WAVES 4   // minimum waves per SIMD (-D...: timing experiments)
 #endif
-template <bool KARG, bool NO_RECS, bool SPANS, bool PIX>
+template <bool KARG, bool NO_RECS, bool SPANS, bool PIX, int SCAN>
 __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FrameParams fp, FrameBuffers fb, KArgDraws ka) {
     __shared__ RasterShared sh;
     const int tid = threadIdx.x;
@@ -1770,9 +1773,9 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
                 __syncthreads();
                 clear_tile(fp, fv, rt);
             } else {
-                if (fp.flags & DBG_TWICE) raster_tile<NO_RECS, SPANS, PIX>(fp, fv, draws, cnt, n_frag, f, rt, sh, nullptr);   // warm run
+                if (fp.flags & DBG_TWICE) raster_tile<NO_RECS, SPANS, PIX, SCAN>(fp, fv, draws, cnt, n_frag, f, rt, sh, nullptr);   // warm run
                 tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
-                raster_tile<NO_RECS, SPANS, PIX>(fp, fv, draws, cnt, n_frag, f, rt, sh, first ? fb.timeline : nullptr);
+                raster_tile<NO_RECS, SPANS, PIX, SCAN>(fp, fv, draws, cnt, n_frag, f, rt, sh, first ? fb.timeline : nullptr);
                 first = false;
             }
         }
@@ -1849,7 +1852,7 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_pipe(FramePara
                 const uint32_t g = fb.busy_list[j - s_lo];
                 const int f = (int)(g / (uint32_t)n_rt), rt = (int)g - f * n_rt;
                 const FrameBuffers fv = frame_view(fp, fb, f);
-                raster_tile<false, false, true>(fp, fv, draws, cnt, n_frag, f, rt, sh, nullptr);
+                raster_tile<false, false, true, SCAN_RUNTIME>(fp, fv, draws, cnt, n_frag, f, rt, sh, nullptr);
             }
         }
         if (!queued) break;
@@ -1899,16 +1902,20 @@ hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KA
     // binned frames test conservative row spans, scan-mode frames whole boxes (raster_tile); the
     // per-pixel loop (SHS_OPT_RASTER_LOOP 0) has kernels of its own, so the pair kernels carry none of
     // its registers
-#define SHS_RASTER(NR, SP, PX)                                                                              \
+#define SHS_RASTER(NR, SP, PX, SC)                                                                          \
     do {                                                                                                   \
-        if (karg) hipLaunchKernelGGL((k_raster<true, NR, SP, PX>), g, dim3(256), 0, s, fp, fb, ka);          \
-        else hipLaunchKernelGGL((k_raster<false, NR, SP, PX>), g, dim3(256), 0, s, fp, fb, ka);              \
+        if (karg) hipLaunchKernelGGL((k_raster<true, NR, SP, PX, SC>), g, dim3(256), 0, s, fp, fb, ka);      \
+        else hipLaunchKernelGGL((k_raster<false, NR, SP, PX, SC>), g, dim3(256), 0, s, fp, fb, ka);          \
     } while (0)
     const bool pix = (fp.flags & RF_PER_PIXEL) != 0u;
-    if (fp.flags & RF_NO_RECS) SHS_RASTER(true, true, false);   // binned frames: records recomputed (either loop)
-    else if (pix) SHS_RASTER(false, false, true);               // (binned frames: boxes)
-    else if (!fp.scan_mode) SHS_RASTER(false, true, false);
-    else SHS_RASTER(false, false, false);
+    if (fp.flags & RF_NO_RECS) SHS_RASTER(true, true, false, SCAN_BINNED);   // binned frames: records recomputed (either loop)
+    else if (pix) SHS_RASTER(false, false, true, SCAN_RUNTIME);              // (binned frames: boxes)
+    else if (!fp.scan_mode) SHS_RASTER(false, true, false, SCAN_BINNED);
+#ifdef SHS_SCAN_SPANS   // (timing experiments: scan-mode frames on row spans)
+    else SHS_RASTER(false, true, false, SCAN_ALL);
+#else
+    else SHS_RASTER(false, false, false, SCAN_ALL);
+#endif
 #undef SHS_RASTER
     return hipGetLastError();
 }
