@@ -100,6 +100,14 @@ constexpr uint32_t DBG_SKIP_GHOST = 1u << 8, DBG_SKIP_SHADE = 1u << 9, DBG_CLEAR
                    DBG_SKIP_BIN = 1u << 11, DBG_SKIP_CLEAR = 1u << 12,
                    DBG_TWICE = 1u << 13, DBG_SKIP_PAIRS = 1u << 14, DBG_SKIP_TILE_STORES = 1u << 15;
 constexpr uint32_t DBG_MASK = 0xffu << 8;   // dropped from the caller's flags outside the experiments build
+// The DBG_* checks are compiled only into the experiments build (-DSHS_TIMING_EXPERIMENTS): the
+// product kernels carry none of their code (DBG_TWICE alone inlined the whole raster tile twice).
+#ifdef SHS_TIMING_EXPERIMENTS
+constexpr bool DBG_BUILD = true;
+#else
+constexpr bool DBG_BUILD = false;
+#endif
+#define SHS_DBG(fp, bit) (::shs_dev::DBG_BUILD && ((fp).flags & (bit)))
 // Raster inner loop (frame flags bit 16, set by the context from SHS_OPT_RASTER_LOOP): per-pixel
 // candidate loop instead of (candidate, pixel) pair tasks.  Results are identical either way.
 constexpr uint32_t RF_PER_PIXEL = 1u << 16;

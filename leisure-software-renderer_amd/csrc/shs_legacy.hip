@@ -805,7 +805,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
 
     // -- bin appends (large scenes): bin tiles of the bin box, two per quad lane
     uint32_t n_bin = 0;
-    if (BIN && !(fp.flags & DBG_SKIP_BIN)) {
+    if (BIN && !SHS_DBG(fp, DBG_SKIP_BIN)) {
         uint32_t *tcount = fb.tile_count;
         const int bx0 = gx0 / TILE, bx1 = live ? gx1 / TILE : -1, by0 = gy0 / TILE, by1 = live ? gy1 / TILE : -1;
         const int nbx = max(bx1 - bx0 + 1, 1), n_bt = live ? (bx1 - bx0 + 1) * (by1 - by0 + 1) : 0;
@@ -870,7 +870,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
     __syncthreads();
     if (tid == 0) fb.blk_stat[frame * fp.setup_blocks + lb] = make_uint4(s_stat[0], s_stat[1], s_stat[2], s_stat[3]);
     tl_mark(fb.timeline, blockIdx.x, 5);
-    if (!BIN && sliv && !(fp.flags & DBG_SKIP_GHOST)) {   // RF_GHOST_INLINE: this wave's unbounded slivers, one at a time
+    if (!BIN && sliv && !SHS_DBG(fp, DBG_SKIP_GHOST)) {   // RF_GHOST_INLINE: this wave's unbounded slivers, one at a time
         uint64_t todo = m_unb;
         while (todo) {
             const int src = __ffsll((unsigned long long)todo) - 1;
@@ -906,7 +906,7 @@ __device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuf
         const int wave = threadIdx.x >> 6;
         const int gw = (lb - fp.setup_blocks) * 4 + wave;
         const int n_groups = (fp.n_tris + GHOST_GROUP - 1) / GHOST_GROUP;
-        if (gw < n_groups * (int)fp.ghost_slices && !(fp.flags & DBG_SKIP_GHOST))
+        if (gw < n_groups * (int)fp.ghost_slices && !SHS_DBG(fp, DBG_SKIP_GHOST))
             ghost_wave(fp, fb, draws, cnt, frame, gw / (int)fp.ghost_slices, gw % (int)fp.ghost_slices, s_ghost[wave]);
     }
     if (fb.timeline) {
@@ -1445,7 +1445,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                     }
                 }
                 __syncthreads();
-                const int total = (fp.flags & DBG_SKIP_PAIRS) ? 0 : (int)(ptot >> 11);
+                const int total = SHS_DBG(fp, DBG_SKIP_PAIRS) ? 0 : (int)(ptot >> 11);
                 pairs += total;
                 for (int k0 = 64 * wave; k0 < total; k0 += 256) {
                     const int k = k0 + lane;
@@ -1496,7 +1496,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                     if (lane == 63) sh.npairs = (uint32_t)incl;
                 }
                 __syncthreads();
-                const int total = (fp.flags & DBG_SKIP_PAIRS) ? 0 : (int)sh.npairs;
+                const int total = SHS_DBG(fp, DBG_SKIP_PAIRS) ? 0 : (int)sh.npairs;
                 pairs += total;
                 for (int k0 = 64 * wave; k0 < total; k0 += 256) {
                     const int k = k0 + lane;
@@ -1566,7 +1566,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             float u, v, w;
             bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
             depth = (u * r.z0 + v * r.z1) + w * r.z2;
-            if (!(fp.flags & DBG_SKIP_SHADE)) {
+            if (!SHS_DBG(fp, DBG_SKIP_SHADE)) {
                 const int wd = dbase + r.draw;   // the frame's draw (ShadeRec::draw is frame 0's when shared)
                 const float4 *du = wd < LDS_DRAWS ? &sh.du[wd * 4] : reinterpret_cast<const float4 *>(draws[wd].light);
                 float pre[3];
@@ -1576,7 +1576,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                 pq = make_float4(pre[0], pre[1], pre[2], 1.0f);
             }
         } else {
-            const bool shade = !(fp.flags & DBG_SKIP_SHADE);
+            const bool shade = !SHS_DBG(fp, DBG_SKIP_SHADE);
             f3 A = {0.f, 0.f, 0.f}, N = {0.f, 0.f, 0.f};   // interpolated varyings (shade_interp's inputs)
             int shading = 0;
             float4 du[4];
@@ -1627,7 +1627,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
     const uint64_t cm = __ballot(covered);
     if (lane == 0 && cm) atomicAdd(&sh.cov, (uint32_t)__popcll(cm));
     // (DBG_SKIP_TILE_STORES, timing experiments: the busy tile's stores dropped, its values kept live)
-    const bool dbg_nost = (fp.flags & DBG_SKIP_TILE_STORES) && !(rgba == 0x12345678u && depth == -1.0f);
+    const bool dbg_nost = SHS_DBG(fp, DBG_SKIP_TILE_STORES) && !(rgba == 0x12345678u && depth == -1.0f);
     if (px < fp.W && py < fp.H && !dbg_nost) {
         LEGACY_STORE(rgba, &reinterpret_cast<uint32_t *>(fb.color)[(size_t)(fp.H - 1 - py) * fp.W + px]);
         LEGACY_STORE(depth, &fb.depth[(size_t)py * fp.W + px]);
@@ -1758,7 +1758,7 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
         if (s_hi > s_lo) {
             const int f = (int)(s_lo / (uint32_t)strips_y);
             const int sy = (int)s_lo - f * strips_y;
-            if (!(fp.flags & DBG_SKIP_CLEAR))   // (timing experiments: the busy tiles alone)
+            if (!SHS_DBG(fp, DBG_SKIP_CLEAR))   // (timing experiments: the busy tiles alone)
                 for (int ry = sy * STRIP_RT; ry < min((sy + 1) * STRIP_RT, fp.rtiles_y); ++ry) clear_strip(fp, fb, f, ry);
         } else {
             uint32_t k = item - s_lo;
@@ -1769,11 +1769,11 @@ __global__ __launch_bounds__(256, SHS_LEGACY_RASTER_WAVES) void k_raster(FramePa
             const FrameBuffers fv = frame_view(fp, fb, f);
             if (g == BUSY_SKIP) {
                 // padding of a row group (a bin tile's row below the screen): nothing to draw
-            } else if (fp.flags & DBG_CLEAR_ONLY) {
+            } else if (SHS_DBG(fp, DBG_CLEAR_ONLY)) {
                 __syncthreads();
                 clear_tile(fp, fv, rt);
             } else {
-                if (fp.flags & DBG_TWICE) raster_tile<NO_RECS, SPANS, PIX, SCAN>(fp, fv, draws, cnt, n_frag, f, rt, sh, nullptr);   // warm run
+                if (SHS_DBG(fp, DBG_TWICE)) raster_tile<NO_RECS, SPANS, PIX, SCAN>(fp, fv, draws, cnt, n_frag, f, rt, sh, nullptr);   // warm run
                 tl_mark(first ? fb.timeline : nullptr, fp.setup_grid + (int)blockIdx.x, 0);
                 raster_tile<NO_RECS, SPANS, PIX, SCAN>(fp, fv, draws, cnt, n_frag, f, rt, sh, first ? fb.timeline : nullptr);
                 first = false;

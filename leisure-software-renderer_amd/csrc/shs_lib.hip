@@ -470,7 +470,7 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     r.z0 = a.cz * iw0; r.z1 = b.cz * iw1; r.z2 = c.cz * iw2;
     r.seq = seq;
     r.bx = pack16(x0, x1); r.by = pack16(y0, y1);
-    if (!(fp.exp_flags & 4u)) fb.recs[slot] = r;
+    if (!SHS_LIB_EXP(fp, 4u)) fb.recs[slot] = r;
     const uint32_t zk = (fp.flags & LF_DEPTH) ? lib_zmin_ord<false>(fp, r) : 0u;
     fb.zord[slot] = zk;
     LibShade s;
@@ -482,13 +482,13 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     }
     s.draw = d;
     s.pad = 0;
-    if (!(fp.exp_flags & 1u)) fb.shade[slot] = s;
+    if (!SHS_LIB_EXP(fp, 1u)) fb.shade[slot] = s;
     if (dr.tex) {   // UV0 varying * 1/w (varw, rasterizer.hpp:319-326)
         fb.uvw[2 * (size_t)slot] = make_float4(a.u * iw0, a.v * iw0, b.u * iw1, b.v * iw1);
         fb.uvw[2 * (size_t)slot + 1] = make_float4(c.u * iw2, c.v * iw2, 0.0f, 0.0f);
     }
     store_box(fb, slot, x0, x1, y0, y1);
-    if (fp.exp_flags & 2u) return;
+    if (SHS_LIB_EXP(fp, 2u)) return;
     if (DIRECT) {
         const int n_rt = (x1 / LIB_RTW - x0 / LIB_RTW + 1) * (y1 / LIB_RTH - y0 / LIB_RTH + 1);
         if (n_rt > SMALL_MARK) {
@@ -1028,7 +1028,7 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
         __syncthreads();
         n_items = (int)s_nkept;
         if (stl) stf = tl_now();
-        if (fp.exp_flags & 8u) n_items = 0;
+        if (SHS_LIB_EXP(fp, 8u)) n_items = 0;
     }
     uint32_t acc_clip = 0u, acc_rast = 0u, nbig = 0u;
     uint64_t st1 = 0ull, st2 = 0ull;
@@ -2643,7 +2643,7 @@ void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
                 lw.list = l0;
                 lw.count = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt);
                 lw.ids = wl;
-                if (!(fp.exp_flags & 16u)) {   // (exp bit 4: no wave culling -- timing experiments)
+                if (!SHS_LIB_EXP(fp, 16u)) {   // (exp bit 4: no wave culling -- timing experiments)
                     lw.fids = wflist[PROG == 0 ? 0 : wave];
                     lw.box = wbox[PROG == 0 ? 0 : wave];
                 }

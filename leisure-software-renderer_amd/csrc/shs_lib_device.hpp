@@ -10,6 +10,10 @@
 
 namespace shs_dev {
 
+// SHS_LIB_EXP bits (timing experiments, wrong images) are read only in the experiments build: the
+// product kernels carry none of their branches.
+#define SHS_LIB_EXP(fp, bit) (::shs_dev::DBG_BUILD && ((fp).exp_flags & (bit)))
+
 // Per-draw block of one rasterize_mesh call (ShaderUniforms, shader/types.hpp:87-116, reduced to
 // what the builtin programs read; uniform-only products are computed once on the host with the
 // same float operations the reference runs per vertex / per fragment).
