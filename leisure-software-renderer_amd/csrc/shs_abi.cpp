@@ -461,7 +461,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     static const int rbpc_env = [] {
         const char *e = shs_exp_env("SHS_RASTER_PER_CU");
         const int v = e ? std::atoi(e) : 0;
-        return v >= 1 && v <= 4 ? v : 0;
+        return v >= 1 && v <= 8 ? v : 0;
     }();
     const int rbpc = rbpc_env ? rbpc_env : (fp.scan_mode ? 4 : 3);
     const int raster_grid = std::max(1, std::min(fp.n_owned_rt * n_frames, 256 * rbpc));

@@ -1908,8 +1908,11 @@ hipError_t launch_raster(const FrameParams &fp, const FrameBuffers &fb, const KA
         else hipLaunchKernelGGL((k_raster<false, NR, SP, PX, SC>), g, dim3(256), 0, s, fp, fb, ka);          \
     } while (0)
     const bool pix = (fp.flags & RF_PER_PIXEL) != 0u;
-    if (fp.flags & RF_NO_RECS) SHS_RASTER(true, true, false, SCAN_BINNED);   // binned frames: records recomputed (either loop)
-    else if (pix) SHS_RASTER(false, false, true, SCAN_RUNTIME);              // (binned frames: boxes)
+    if (DBG_BUILD && (fp.flags & RF_NO_RECS)) {   // binned frames, records recomputed (either loop; experiments build)
+#ifdef SHS_TIMING_EXPERIMENTS
+        SHS_RASTER(true, true, false, SCAN_BINNED);
+#endif
+    } else if (pix) SHS_RASTER(false, false, true, SCAN_RUNTIME);              // (binned frames: boxes)
     else if (!fp.scan_mode) SHS_RASTER(false, true, false, SCAN_BINNED);
 #ifdef SHS_SCAN_SPANS   // (timing experiments: scan-mode frames on row spans)
     else SHS_RASTER(false, true, false, SCAN_ALL);
