@@ -832,7 +832,7 @@ __device__ __forceinline__ bool cull_keep(const LibFrameParams &fp, const LibDra
     return clip_reaches_rank(fp, t);
 }
 
-// Region-sharded camera pass, before k_lib_setup (one thread per setup block): the screen bounds of
+// Region-sharded camera pass, before k_lib_setup (BLK_G lanes per setup block): the screen bounds of
 // block b's triangles from their 256-triangle chunks' model-space boxes (LibDrawGPU::cbox, 8 corners
 // each).  Every point of a box whose corners are all in front of the eye projects inside the hull of
 // the projected corners, so the bin tiles of that bbox (2 px of margin for the rounding of the
@@ -846,61 +846,65 @@ __device__ __forceinline__ bool cull_keep(const LibFrameParams &fp, const LibDra
 // fb.blist, and k_lib_setup's workgroup i sets up listed block i -- the rank's setup grid holds no
 // workgroup that only finds it has nothing to do (C4 rank 3 of 8: 2,100 of its 3,907 workgroups were
 // such, ~4.6 us of a workgroup slot each, a quarter of the kernel).
+// BLK_G lanes per block: lane j transforms corner j & 7 of chunk j >> 3, the bounds are reduced across
+// the group with shuffles (fminf / fmaxf: the same bounds as a serial walk over the corners and edge
+// cuts); one thread per block took ~11 us per rank frame at C4 (16 workgroups, a 16-corner chain each).
+constexpr int BLK_G = 16;
 __global__ __launch_bounds__(256) void k_lib_blocks(LibFrameParams fp, LibBuffers fb) {
-    const int b = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int gid = (int)(blockIdx.x * 256 + threadIdx.x);
+    const int b = gid / BLK_G, j = gid % BLK_G;
+    const int ci = j >> 3, k = j & 7;
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
-    bool keep = false;
-    if (b < fp.setup_blocks) {
-        const int t0 = b * 256, t1 = min(t0 + 255, fp.n_tris - 1);
+    const bool valid = b < fp.setup_blocks;   // uniform over the group
+    int t0 = 0, t1 = -1;
+    bool have = false;
+    f4 p{0.0f, 0.0f, 0.0f, 1.0f};
+    if (valid) {
+        t0 = b * 256;
+        t1 = min(t0 + 255, fp.n_tris - 1);
         const int d = fb.bdraw[b];
         const LibDrawGPU &dr = fb.draws[d];
-        const bool have = t0 <= t1 && (d + 1 >= fp.n_draws || fb.dbase[d + 1] > t1) && dr.cbox != nullptr;
-        bool bounded = false, finite = false;
-        float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+        have = t0 <= t1 && (d + 1 >= fp.n_draws || fb.dbase[d + 1] > t1) && dr.cbox != nullptr;
         if (have) {
             const int c0 = (t0 - dr.tri_base) >> 8, c1 = (t1 - dr.tri_base) >> 8;   // at most two chunks
-            auto add = [&](float cx, float cy, float cw) {
-                const float sx = (cx / cw * 0.5f + 0.5f) * (float)(fp.W - 1);
-                const float sy = (cy / cw * 0.5f + 0.5f) * (float)(fp.H - 1);
-                x0 = fminf(x0, sx); x1 = fmaxf(x1, sx); y0 = fminf(y0, sy); y1 = fmaxf(y1, sy);
-            };
-            finite = true;
-            bounded = true;
-            float wmax = 0.0f;
-            f4 cp[2][8];
-#pragma unroll
-            for (int ci = 0; ci < 2; ++ci) {
-                const int c = min(c0 + ci, c1);
-                const float4 mn = dr.cbox[2 * c], mx = dr.cbox[2 * c + 1];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    cp[ci][k] = m4v(dr.viewproj, m4v(dr.model, f4{(k & 1) ? mx.x : mn.x, (k & 2) ? mx.y : mn.y, (k & 4) ? mx.z : mn.z, 1.0f}));
-                    finite = finite && isfinite(cp[ci][k].x) && isfinite(cp[ci][k].y) && isfinite(cp[ci][k].w);
-                    bounded = bounded && cp[ci][k].w > 0.0f;
-                    wmax = fmaxf(wmax, fabsf(cp[ci][k].w));
-                }
-            }
-            bounded = bounded && finite;
-            const float eps = bounded ? 0.0f : 1e-3f * wmax;
-            if (finite) {
-#pragma unroll
-                for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const f4 p = cp[ci][k];
-                        if (p.w > eps) add(p.x, p.y, p.w);
-                        if (bounded) continue;
-#pragma unroll
-                        for (int m = 1; m < 8; m <<= 1) {   // the box edges from this corner, cut at w = eps
-                            const f4 n = cp[ci][k ^ m];
-                            if ((p.w - eps) * (n.w - eps) < 0.0f) {
-                                const float t = (eps - p.w) / (n.w - p.w);
-                                add(p.x + (n.x - p.x) * t, p.y + (n.y - p.y) * t, eps);
-                            }
-                        }
-                    }
-            }
+            const int c = min(c0 + ci, c1);
+            const float4 mn = dr.cbox[2 * c], mx = dr.cbox[2 * c + 1];
+            p = m4v(dr.viewproj, m4v(dr.model, f4{(k & 1) ? mx.x : mn.x, (k & 2) ? mx.y : mn.y, (k & 4) ? mx.z : mn.z, 1.0f}));
         }
+    }
+    // group reductions (every lane of the wave takes part in the shuffles)
+    const int gsh = (int)(__lane_id() & ~(BLK_G - 1));
+    const uint64_t fin_m = __ballot(isfinite(p.x) && isfinite(p.y) && isfinite(p.w));
+    const uint64_t pos_m = __ballot(p.w > 0.0f);
+    const uint32_t gmask = (1u << BLK_G) - 1u;
+    const bool finite = have && ((uint32_t)(fin_m >> gsh) & gmask) == gmask;
+    const bool bounded = finite && ((uint32_t)(pos_m >> gsh) & gmask) == gmask;
+    float wmax = fabsf(p.w);
+#pragma unroll
+    for (int o = 1; o < BLK_G; o <<= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, o, BLK_G));
+    const float eps = bounded ? 0.0f : 1e-3f * wmax;
+    float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+    auto add = [&](float cx, float cy, float cw) {
+        const float sx = (cx / cw * 0.5f + 0.5f) * (float)(fp.W - 1);
+        const float sy = (cy / cw * 0.5f + 0.5f) * (float)(fp.H - 1);
+        x0 = fminf(x0, sx); x1 = fmaxf(x1, sx); y0 = fminf(y0, sy); y1 = fmaxf(y1, sy);
+    };
+    if (finite && p.w > eps) add(p.x, p.y, p.w);
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {   // the box edges from this corner, cut at w = eps
+        const f4 n{__shfl_xor(p.x, m, BLK_G), __shfl_xor(p.y, m, BLK_G), 0.0f, __shfl_xor(p.w, m, BLK_G)};
+        if (finite && !bounded && (p.w - eps) * (n.w - eps) < 0.0f) {
+            const float t = (eps - p.w) / (n.w - p.w);
+            add(p.x + (n.x - p.x) * t, p.y + (n.y - p.y) * t, eps);
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < BLK_G; o <<= 1) {
+        x0 = fminf(x0, __shfl_xor(x0, o, BLK_G)); x1 = fmaxf(x1, __shfl_xor(x1, o, BLK_G));
+        y0 = fminf(y0, __shfl_xor(y0, o, BLK_G)); y1 = fmaxf(y1, __shfl_xor(y1, o, BLK_G));
+    }
+    bool keep = false;
+    if (valid) {
         int bx0 = 0, bx1 = fp.tiles_x - 1, by0 = 0, by1 = fp.tiles_y - 1;
         const bool est = finite && !(x1 < x0);   // some point in front of the eye
         if (finite && (bounded || est)) {
@@ -913,14 +917,16 @@ __global__ __launch_bounds__(256) void k_lib_blocks(LibFrameParams fp, LibBuffer
                 by1 = min(fp.tiles_y - 1, (int)fminf(y1 + 2.0f, (float)(fp.H - 1)) / TILE);
             }
         }
-        fb.blkrect[b] = make_uint4((uint32_t)bx0 | ((uint32_t)bx1 << 16), (uint32_t)by0 | ((uint32_t)by1 << 16),
-                                   (uint32_t)max(0, t1 - t0 + 1), bounded ? 1u : (finite && est) ? 2u : 0u);
-        keep = !(bounded && !shard_owns_any(fp.rank, fp.count, fp.reg, bx0, bx1, by0, by1, fp.tiles_x));
-        if (!keep) {   // no triangle of the block reaches this rank
-            fb.blk_stat[b] = make_uint2(0u, 0u);
+        if (j == 0)
+            fb.blkrect[b] = make_uint4((uint32_t)bx0 | ((uint32_t)bx1 << 16), (uint32_t)by0 | ((uint32_t)by1 << 16),
+                                       (uint32_t)max(0, t1 - t0 + 1), bounded ? 1u : (finite && est) ? 2u : 0u);
+        const bool need = !(bounded && !shard_owns_any(fp.rank, fp.count, fp.reg, bx0, bx1, by0, by1, fp.tiles_x));
+        if (!need) {   // no triangle of the block reaches this rank
+            if (j == 0) fb.blk_stat[b] = make_uint2(0u, 0u);
             if (fp.scan_mode)
-                for (int t = t0; t <= t1; ++t) store_box(fb, (uint32_t)t, 0, -1, 0, -1);
+                for (int t = t0 + j; t <= t1; t += BLK_G) store_box(fb, (uint32_t)t, 0, -1, 0, -1);
         }
+        keep = need && j == 0;
     }
     wave_append(&cnt[LC_BLOCKS], fb.blist, keep, (uint32_t)b);
 }
@@ -2694,7 +2700,7 @@ hipError_t launch_lib_setup(const LibFrameParams &fp, const LibBuffers &fb, bool
     if (shadow) {
         hipLaunchKernelGGL(k_lib_setup<true>, dim3(grid), dim3(256), 0, s, fp, fb);
     } else {
-        if (fb.blist) hipLaunchKernelGGL(k_lib_blocks, dim3((fp.setup_blocks + 255) / 256), dim3(256), 0, s, fp, fb);
+        if (fb.blist) hipLaunchKernelGGL(k_lib_blocks, dim3((fp.setup_blocks * BLK_G + 255) / 256), dim3(256), 0, s, fp, fb);
         if (listed) {   // tile-sharded: each workgroup culls CULL_PER x 256 triangles, then sets up the kept ones
             hipLaunchKernelGGL((k_lib_setup<false, true>), dim3(grid), dim3(256), 0, s, fp, fb);
         } else {
