@@ -490,6 +490,16 @@ def strong_legs(args, rank, local_rank, world, dist):
     return out
 
 
+def strong_legs_guarded(args, rank, local_rank, world, dist):
+    """strong_legs, but a failure that every rank hits alike (an error in the sharded legs, not in the
+    headline) costs only the strong_* keys: the line then carries strong_error and the C2 value."""
+    try:
+        return strong_legs(args, rank, local_rank, world, dist)
+    except Exception as e:  # noqa: BLE001 -- reported in the line
+        print(f"bench: strong legs failed on rank {rank}: {e!r}", file=sys.stderr, flush=True)
+        return {"strong_error": repr(e)[:300]}
+
+
 def collect_pmc(args):
     """rocprofv3 --pmc child passes (one counter per pass: FETCH_SIZE costs 3 TCC slots and
     WRITE_SIZE 2, they do not fit together).  Returns bytes per dominant-phase dispatch (k_raster; for
@@ -787,7 +797,7 @@ def main():
         return main_lib(args, world, rank, local_rank, dist, pmc, pmc_err)
     frame, draws, stats, elapsed, n_launches, kms, single, pcie, ramp = run_gpu(args, rank, local_rank, world, dist)
     # the strong-scaling legs ride on the headline configuration's line (the driver's `--gpus N` run)
-    strong = strong_legs(args, rank, local_rank, world, dist) if args.strong and not args.child and args.config == "c2" else {}
+    strong = strong_legs_guarded(args, rank, local_rank, world, dist) if args.strong and not args.child and args.config == "c2" else {}
     B1, n_tri1 = algorithmic_bytes(frame, draws)
     F = args.frames_per_step
     B, n_tri = B1 * F, n_tri1 * F          # per step (= per k_raster launch)

@@ -52,3 +52,12 @@ def test_strong_legs_default_on():
     finally:
         sys.argv = old
     assert ap_args.strong == ["c4", "c5"] and ap_args.strong_frames > 0
+
+
+def test_strong_legs_failure_keeps_the_headline(monkeypatch):
+    """A sharded leg that raises on every rank leaves strong_error in the line instead of ending the bench."""
+    def boom(*a, **k):
+        raise RuntimeError("sharded leg failed")
+    monkeypatch.setattr(bench, "strong_legs", boom)
+    out = bench.strong_legs_guarded(None, 0, 0, 1, None)
+    assert set(out) == {"strong_error"} and "sharded leg failed" in out["strong_error"]
