@@ -308,8 +308,6 @@ def lib_timed_loop(args, slots, frame_fn, dist, frame=None, rank=0, world=1, on_
     roofline's kernel durations).  -> (elapsed s, stats, (n_frames, kms), pixels this rank owned in the
     timed kernels' passes)"""
     D = len(slots)
-    for i in range(max(args.warmup, D)):
-        frame_fn(slots[i % D])
 
     def barrier_sync():
         for sl in slots:
@@ -319,7 +317,29 @@ def lib_timed_loop(args, slots, frame_fn, dist, frame=None, rank=0, world=1, on_
             torch.cuda.synchronize()
             dist.barrier()
 
+    # clock ramp (as the legacy configs): untimed frames for args.ramp_ms of continuous rendering, so the
+    # timed window starts at steady-state clocks whatever ran before it (a `--config` run starts on an idle
+    # GPU, the strong legs after the C2 loop and their own host set-up)
+    # (N > 1: every frame gathers, a collective, so all ranks render the same number of ramp frames -- the
+    # loop goes on while any rank's clock says so)
+    t_ramp, n_ramp = time.perf_counter(), 0
+    more = True
+    while more:
+        for _ in range(D):
+            frame_fn(slots[n_ramp % D])
+            n_ramp += 1
+        for sl in slots:
+            sl.ctx.synchronize_lib()
+        more = (time.perf_counter() - t_ramp) * 1e3 < getattr(args, "ramp_ms", 0.0)
+        if dist is not None:
+            import torch
+            t = torch.tensor([1.0 if more else 0.0], dtype=torch.float64, device=args.reduce_device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            more = bool(t.item() > 0.0)
+    for i in range(max(args.warmup, D)):
+        frame_fn(slots[i % D])
     barrier_sync()
+    args.lib_ramp = {"ms": round((time.perf_counter() - t_ramp) * 1e3, 1), "frames": n_ramp}
     stats = slots[0].ctx.lib_stats()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -438,13 +458,39 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
     return frame, stats, elapsed, n_cam, kms, B_cam_raster, B_frame, n_tri, (S, shadow_texels[0]), owned
 
 
-def strong_summary(cfg, n_tri, frames, elapsed_max, rank_kernels_ms, rank_gather_ms, rank_owned, layout, inflight):
+def strong_roofline(frame_bytes, elapsed_max, frames, rank_cam_bytes, rank_cam_ms):
+    """A strong leg's HBM roofline (north_star: the 1/2/4/8 numbers "as absolute numbers and as fraction
+    of the HBM roofline"): the whole frame's algorithmic bytes (geometry, lights and lists,
+    shadow map, 32 B per output pixel) per ms_per_frame, against N x 8 TB/s; and each rank's camera
+    phase (k_lib_raster + k_lib_resolve, its owned pixels' 32 B, HIP events with one frame in flight)
+    against one GPU's 8 TB/s."""
+    world = len(rank_cam_ms)
+    achieved = frame_bytes * frames / elapsed_max / 1e9
+    cam = [b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0 for b, ms in zip(rank_cam_bytes, rank_cam_ms)]
+    return {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS * world,
+            "frame_algorithmic_bytes": int(frame_bytes),
+            "achieved": round(achieved, 2), "frac": round(achieved / (HBM_PEAK_GBS * world), 4),
+            "rank_camera_phase_frac": [round(c / HBM_PEAK_GBS, 4) for c in cam],
+            "rank0_camera_phase_frac": round(cam[0] / HBM_PEAK_GBS, 4),
+            "what": "frac: frame bytes x frames / wall time over N x 8 TB/s; camera phase: each rank's owned "
+                    "pixels x 32 B (+ its share of the shadow map's PCF reads) / its k_lib_raster + k_lib_resolve "
+                    "event time"}
+
+
+def strong_summary(cfg, n_tri, frames, elapsed_max, rank_kernels_ms, rank_gather_ms, rank_owned, layout, inflight,
+                   frame_bytes=None, rank_cam_bytes=None, rank_cam_ms=None, ramp=None):
     """One strong-scaling leg's keys (the 4K tile-sharded frame of north_star's >= 6x target) from the
     per-rank measurements rank 0 collected: frames per second over the whole job between two barriers,
-    the worst rank's isolated camera-frame kernels, each rank's gather time and owned pixels."""
+    the worst rank's isolated camera-frame kernels, each rank's gather time and owned pixels, and the
+    leg's roofline (strong_roofline)."""
     world = len(rank_kernels_ms)
     worst = int(np.argmax(rank_kernels_ms))
-    return {
+    extra = {}
+    if frame_bytes is not None:
+        extra["roofline"] = strong_roofline(frame_bytes, elapsed_max, frames, rank_cam_bytes, rank_cam_ms)
+    if ramp is not None:
+        extra["clock_ramp"] = ramp
+    return dict(extra, **{
         "workload": WORKLOADS[cfg],
         "n_gpus": world,
         "frames": frames,
@@ -461,7 +507,7 @@ def strong_summary(cfg, n_tri, frames, elapsed_max, rank_kernels_ms, rank_gather
                 "tonemap, RGBA8 present tiles gathered into rank 0 over RCCL every frame; ms_per_frame = max-over-"
                 "ranks wall time between barriers / frames; kernels: each rank's shadow + camera pass kernels, "
                 "one frame in flight (HIP events); gather: HIP events around the gather on the frame's stream",
-    }
+    })
 
 
 def strong_legs(args, rank, local_rank, world, dist):
@@ -474,19 +520,33 @@ def strong_legs(args, rank, local_rank, world, dist):
         a.config, a.steps, a.warmup = cfg, args.strong_frames, 20
         a.shard_layout, a.inflight = "regions", 3
         runner = run_gpu_c4 if cfg == "c4" else run_gpu_lib
-        frame, stats, elapsed, n_frames, kms, _, _, n_tri, _, owned = runner(a, rank, local_rank, world, dist)
-        k_ms = sum(v for k, v in kms.items() if k != "gather")
-        mine = [elapsed, k_ms, kms.get("gather", 0.0), float(owned)]
+        ok, err = 1.0, None
+        try:
+            frame, stats, elapsed, n_frames, kms, B_k, B_frame, n_tri, _, owned = runner(a, rank, local_rank, world, dist)
+            k_ms = sum(v for k, v in kms.items() if k != "gather")
+            mine = [elapsed, k_ms, kms.get("gather", 0.0), float(owned), float(B_k), kms.get("raster", 0.0)]
+        except Exception as e:  # noqa: BLE001 -- every rank learns of it below, then all raise alike
+            ok, err, mine = 0.0, e, [0.0] * 6
         if dist is not None:
+            # a common status point before the data reduction: a leg that failed on some rank (after its
+            # collectives) fails on every rank, instead of the others waiting in the reduction
             import torch
-            t = torch.zeros((world, 4), dtype=torch.float64, device=args.reduce_device)
+            st = torch.tensor([ok], dtype=torch.float64, device=args.reduce_device)
+            dist.all_reduce(st, op=dist.ReduceOp.MIN)
+            ok = float(st.item())
+        if ok < 1.0:
+            raise RuntimeError(f"strong leg {cfg} failed on " + (f"this rank: {err!r}" if err is not None else "another rank"))
+        if dist is not None:
+            t = torch.zeros((world, 6), dtype=torch.float64, device=args.reduce_device)
             t[rank] = torch.tensor(mine, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             rows = t.cpu().numpy()
         else:
             rows = np.asarray([mine])
         out["strong_" + cfg] = strong_summary(cfg, n_tri, a.steps, float(rows[:, 0].max()), rows[:, 1], rows[:, 2],
-                                              rows[:, 3], a.shard_layout, a.inflight)
+                                              rows[:, 3], a.shard_layout, a.inflight, frame_bytes=B_frame,
+                                              rank_cam_bytes=rows[:, 4], rank_cam_ms=rows[:, 5],
+                                              ramp=getattr(a, "lib_ramp", None))
     return out
 
 
@@ -735,7 +795,7 @@ def main():
                          "next batch's launch; eligible: multi-draw scan-mode batches, i.e. C1 / C2).  Off: measured "
                          "slower (C2 0.328 vs 0.284 ms/step: the fused kernel spills 120 B/lane, DESIGN.md 4)")
     ap.add_argument("--ramp-ms", type=float, default=60.0,
-                    help="legacy configs: untimed rendering before the warm-up so the GPU clocks reach steady state")
+                    help="untimed rendering before the warm-up so the GPU clocks reach steady state (every config and strong leg)")
     ap.add_argument("--shadow-full", action="store_true",
                     help="c5: render the whole shadow map every frame (default: the camera pass's footprint, "
                          "SHS_OPT_SHADOW_FOOTPRINT)")
@@ -954,6 +1014,7 @@ def main_lib(args, world, rank, local_rank, dist, pmc, pmc_err):
         "frame_stats": stats, "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
         "kernel_timing": f"{n_frames} frames on one context alone after the timed loop (HIP events)",
         "roofline": roofline,
+        "clock_ramp": dict(getattr(args, "lib_ramp", {}), what="untimed frames before the warm-up: steady-state GPU clocks"),
     }
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)

@@ -753,6 +753,16 @@ int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const
     m.n_verts = n_verts;
     m.n_tris = (int32_t)n_tris;
     if (indices && n_indices < 3) m.n_tris = 0;
+    // a HIP_TRY that returns early frees what this upload already allocated (the mesh is not registered)
+    struct Guard {
+        Mesh &m;
+        bool keep = false;
+        ~Guard() {
+            if (keep) return;
+            for (void *p : {(void *)m.orig, (void *)m.pos, (void *)m.nrm, (void *)m.uv, (void *)m.idx, (void *)m.cbox})
+                if (p) (void)hipFree(p);
+        }
+    } guard{m};
     // Spatial order (meshes over one 256-triangle chunk): the triangles are stored sorted by the Morton
     // code of their centroid, so a setup block's chunk box is tight and a region-sharded rank skips the
     // blocks that miss its rectangle.  The submission order stays the MeshData order:
@@ -827,6 +837,7 @@ int shs_mesh_upload(shs_ctx *ctx, const float *positions, int32_t n_verts, const
     }
     m.live = true;
     ctx->meshes.push_back(m);
+    guard.keep = true;
     *mesh_id = (int32_t)ctx->meshes.size() - 1;
     return SHS_OK;
 }

@@ -7,22 +7,30 @@
 // /root/reference/cpp-folders/src/shs-renderer-lib/include/shs/.
 //
 // Launches per pass, on one HIP stream:
+//   k_lib_blocks  (region-sharded camera pass) the setup sub-blocks whose projected chunk boxes can
+//                 reach the rank's rectangle, listed for k_lib_setup.
 //   k_lib_setup   one thread per input triangle: VS x3, trivial accept (or a queue entry for the
 //                 clipper), NDC -> screen (rows y-up), area / cull / bbox rejects, the per-primitive
-//                 half of barycentric_2d and the 1/w terms (a 64-B record + 112-B premultiplied
-//                 varyings per primitive), "busy" marks on the 32x8 raster tiles of its bbox and, for
-//                 large scenes, per-32x32-tile bin appends (block-aggregated in LDS); primitives over
-//                 many tiles go to a pass-wide queue with their task prefix.
+//                 half of barycentric_2d and the 1/w terms (a 64-B LibRec + an 80-B LibShade of
+//                 varyings premultiplied by 1/w per primitive), "busy" marks on the 32x8 raster tiles
+//                 of its bbox and, for large scenes, per-32x32-tile bin appends (block-aggregated in
+//                 LDS); primitives over many tiles go to a pass-wide queue with their task prefix.
 //   k_lib_clip    (camera pass) the queued triangles: Sutherland-Hodgman against the six clip planes
 //                 by 16-lane groups with the polygon in registers, then the fans as above.
 //   k_lib_bigmark the queued large primitives' (primitive, tile) marks / appends over the whole chip.
+//   k_lib_dyn     (camera pass) the raster's dynamic work items compacted per ticket queue, heavy
+//                 tiles first.
 //   k_lib_raster  persistent over the owned raster tiles: busy tiles stage their candidates'
 //                 records in LDS and deal every (primitive, pixel) pair to one lane; each passing
 //                 pair atomic-mins a 64-bit key (z01 bits, submission order) into LDS -- identical
-//                 to the reference's in-order strict-less test on a cleared buffer; the winner of
-//                 every pixel is shaded once and the tile's HDR colour, depth and motion are written
-//                 as whole row segments.  Idle tiles are written with the pass's clear values, so
-//                 every output byte is written exactly once per pass.
+//                 to the reference's in-order strict-less test on a cleared buffer.  The shadow pass
+//                 writes each texel's depth here (idle tiles get the clear depth); the camera pass
+//                 hands each 16x4 block's winners to k_lib_resolve as 4-B words, with a flag per block
+//                 that holds one.
+//   k_lib_resolve (camera pass) every owned pixel: the winner re-evaluated, its varyings interpolated,
+//                 the fragment program run (+ the fused PassTonemap), HDR colour, depth, motion written;
+//                 pixels without a winner get the clear values, so every output byte is written exactly
+//                 once per pass.
 // Primitive order: input triangle t's fan triangle k has submission index t*16 + k (a clipped
 // triangle yields at most 7 fans in exact arithmetic, MAX_POLY - 2 with rounding); fan 0 lives in
 // slot t, fans >= 1 in extra slots from xbase[t].  t is the submission index (draw base + MeshData

@@ -169,7 +169,7 @@ def gather_frame_device(dist, ctx, target, stream=None, out=None):
     return out
 
 
-_READY = []   # the group objects already barriered (held, so a re-created group is never mistaken for one)
+_READY = []   # the group objects already barriered: weak references (a strong one where the type has none)
 
 
 def ensure_group_ready(dist):
@@ -178,15 +178,22 @@ def ensure_group_ready(dist):
     (or rank 0 with no non-empty peer) posts no operation at all; a barrier first makes the batches
     ordinary point-to-point traffic on an initialised communicator.  The groups are kept by reference,
     not by id(): after destroy_process_group and a re-init, CPython could hand the new default group
-    the old one's id while the old object is gone."""
+    the old one's id while the old object is gone.  Weak references let a destroyed group (and the
+    communicator it holds) be collected; an entry is compared by identity while its object lives, so a
+    re-created group is still never mistaken for an old one."""
+    import weakref
     world = getattr(getattr(dist, "group", None), "WORLD", None)   # the default group (a new one after re-init)
     key = world if world is not None else dist
-    if any(g is key for g in _READY):
+    _READY[:] = [r for r in _READY if r() is not None]   # drop collected groups
+    if any(r() is key for r in _READY):
         return
     barrier = getattr(dist, "barrier", None)
     if barrier is not None:
         barrier()
-    _READY.append(key)
+    try:
+        _READY.append(weakref.ref(key))
+    except TypeError:   # no weak-reference support: hold it (the previous behaviour)
+        _READY.append(lambda k=key: k)
 
 
 def send_to_root(dist, buf, recvs, sizes):

@@ -398,9 +398,13 @@ static void *pool_worker(void *arg) {
     return NULL;
 }
 
-/* (caller holds g_pool_lock) the pool with n workers; returns the workers running */
+/* (caller holds g_pool_lock) the pool with n workers; returns the workers running.  The request is
+ * remembered apart from the count started: when pthread_create falls short (thread limits), later
+ * frames with the same request keep the smaller pool instead of re-creating it every frame. */
+static int g_pool_req = 0;
 static int pool_resize(int n) {
-    if (g_pool.n == n) return n;
+    if (g_pool.n == n || (g_pool_req == n && g_pool.n > 0)) return g_pool.n;
+    g_pool_req = n;
     pthread_mutex_lock(&g_pool.mu);
     g_pool.quit = 1;
     pthread_cond_broadcast(&g_pool.go);
