@@ -57,7 +57,7 @@ void release_work(Work &w) {
     w.dev_table_at = nullptr;
     w.dev_table_cap = 0;
     release(w.tile_count); release(w.bins); release(w.counters); release(w.busy);
-    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.pkeys); release(w.pcount); release(w.dynq); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
+    release(w.spill); release(w.blk_stat); release(w.rstat); release(w.uvw); release(w.items); release(w.pkeys); release(w.pcount); release(w.dynq); release(w.hsq); release(w.hsr); release(w.clipq); release(w.bigq); release(w.bigpre); release(w.rqueue);
     if (w.raster_ev) (void)hipEventDestroy(w.raster_ev);
     if (w.resolve_ev) (void)hipEventDestroy(w.resolve_ev);
     w.raster_ev = w.resolve_ev = nullptr;
@@ -427,6 +427,17 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         static const int heavy = [] { const char *e = shs_exp_env("SHS_LIB_HEAVY"); return e ? std::atoi(e) : 2048; }();
         fp.heavy_min = (uint32_t)std::max(heavy, 0);
     }
+    // Camera pass, deep raster: bin lists longer than one candidate round are depth-sorted whole
+    // (k_lib_hsort) when the previous pass had such lists (the raster trusts fp.hsort, never the
+    // statistics).  Not with k_lib_plan's parts (a part takes a range of list positions).
+    fp.hsort = 0u;
+    fp.hsort_min = shs_dev::LIB_HSORT_MIN;
+#ifndef SHS_EXP_NO_HSORT
+    if (!shadow && !fp.scan_mode && !fp.part && !shallow && (!w.st_checked || w.st_maxbin > fp.hsort_min)) {
+        if (ensure(ctx, w.hsq, (size_t)n_tiles) || ensure(ctx, w.hsr, (size_t)n_tiles)) return SHS_ERR_HIP;
+        fp.hsort = 1u;
+    }
+#endif
 
     LibBuffers fb;
     std::memset(&fb, 0, sizeof fb);
@@ -442,6 +453,8 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     fb.items = fp.part ? w.items.p : nullptr;
     fb.pkeys = fp.part ? w.pkeys.p : nullptr;
     fb.pcount = fp.part ? w.pcount.p : nullptr;
+    fb.hsq = fp.hsort ? w.hsq.p : nullptr;
+    fb.hsr = fp.hsort ? w.hsr.p : nullptr;
     // Tile-sharded camera pass in bin mode: each setup workgroup first keeps the rank's triangles of its
     // inputs, positions only (SHS_OPT_SHARD_CULL 0: off).
     const bool listed = !shadow && !fp.scan_mode && fp.count > 1 && !fp.reg.on && ctx->shard_cull;

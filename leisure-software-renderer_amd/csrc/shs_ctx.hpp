@@ -177,6 +177,8 @@ struct shs_ctx {
         DevBuf<float4> uvw;                                // UV0 varyings of textured draws' slots
         DevBuf<uint2> items;                               // k_lib_plan's raster work items
         DevBuf<uint32_t> dynq;                             // k_lib_dyn's per-queue dynamic work items (camera pass)
+        DevBuf<uint32_t> hsq;                              // k_lib_dyn's bin tiles for k_lib_hsort (camera pass)
+        DevBuf<uint2> hsr;                                 // per bin tile: the range its sorted list was bucketed over
         shs_dev::LibDrawGPU *h_draws[2] = {nullptr, nullptr};   // pinned staging, 2 slots
         size_t h_cap = 0;
         hipEvent_t slot_ev[2] = {nullptr, nullptr};

@@ -76,6 +76,7 @@ constexpr int LIB_RTW = 32, LIB_RTH = 8;   // raster tile (one 256-thread workgr
 // 256 (24 KB LDS, 80 VGPRs: 6 workgroups per CU): passes whose fullest bin tile fits one round (C5's
 // 62), chosen from the previous frame's statistics (LibWork::st_maxbin).
 constexpr int LIB_CAND_DEEP = 1024, LIB_CAND_SHALLOW = 256;
+static_assert(LIB_HSORT_MIN == (uint32_t)LIB_CAND_DEEP, "k_lib_hsort sorts the lists of more than one deep round");
 constexpr int LIB_CHUNK = 128;             // records staged in LDS per pass
 constexpr int MAX_POLY = 16;               // clipped polygon capacity (3 + 6 planes x up to 2 crossings)
 
@@ -115,6 +116,15 @@ __device__ __forceinline__ uint32_t lib_zmin_ord(const LibFrameParams &fp, const
 }
 
 __device__ __forceinline__ uint64_t tl_now() { return __builtin_amdgcn_s_memrealtime(); }
+
+// The depth bucket of a bound z over a sorted list's range (lo, hi): 256 buckets, monotone in z (the
+// float subtraction, product and truncation all are) -- k_lib_hsort sorts by it and k_lib_raster stops
+// a tile's candidate rounds by it, with the identical arithmetic.
+__device__ __forceinline__ uint32_t hs_bucket(uint2 range, uint32_t z) {
+    const float scale = range.y > range.x ? 255.0f / (float)(range.y - range.x) : 0.0f;
+    return z <= range.x ? 0u : min(255u, (uint32_t)((float)(z - range.x) * scale));
+}
+
 
 // ---- k_lib_setup ------------------------------------------------------------------------------
 
@@ -1735,6 +1745,7 @@ struct LibShared {
     uint32_t qlen[2 * LIB_NQ];            // camera pass: k_lib_dyn's light, then heavy list lengths
     uint32_t sitem[LIB_MAX_STATIC];       // the workgroup's static work items (k_lib_raster)
     uint64_t tl[LTL_STRIDE];              // SHS_OPT_TIMELINE accumulators (thread 0)
+    uint32_t tl_staged;                   // SHS_OPT_TIMELINE: candidates staged in the current tile
     // segment (deep) or staged box (shallow) owning each bitmap word's first pair
     typename std::conditional<LIB_CAND == LIB_CAND_DEEP, uint16_t, uint8_t>::type wown[LIB_PAIR_WORDS];
 };
@@ -1902,8 +1913,12 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
     const uint64_t t_tile = tlon ? tl_now() : 0ull;
     uint64_t t_gather = 0ull;
     const uint32_t chunk0 = chunk;
+    uint32_t t_rounds = 0u, t_pairs = 0u, t_breaks = 0u;   // (timeline, thread 0: this tile's counts)
+    if (tlon) sh.tl_staged = 0u;
 
     uint32_t n_bin = 0, n_spill = 0, n_items;
+    bool gsorted = false;   // the bin list is depth-sorted whole (k_lib_hsort) over hsr's range
+    uint2 hsr = make_uint2(0u, 0u);
     if (fp.scan_mode) {
         n_items = (uint32_t)fp.n_tris + (SHADOW ? 0u : min(cnt[LC_EXTRA], fp.extra_cap));
     } else {
@@ -1912,14 +1927,27 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         if (n_bin_total > fp.bin_cap) n_spill = min(cnt[LC_SPILL], fp.spill_cap);
         n_items = n_bin + n_spill;
         if (tid == 0) sh.maxbin = max(sh.maxbin, n_bin_total);
+        // (the predicate k_lib_dyn listed the tile's bin list by; this tile is busy, so it was listed)
+        gsorted = !SHADOW && LIB_CAND == LIB_CAND_DEEP && hiz && fp.hsort && parts == 1u && n_bin_total > fp.hsort_min &&
+                  n_bin_total <= min(fp.bin_cap, (uint32_t)LIB_HSORT_MAX);
+        if (gsorted) hsr = fb.hsr[bt];
     }
     const uint4 *bin = fb.bins + (size_t)bt * fp.bin_cap;
     // a part's share of the list (positions [lo, n_items))
     const uint32_t lo = (uint32_t)(((uint64_t)n_items * part) / parts);
     n_items = (uint32_t)(((uint64_t)n_items * (part + 1u)) / parts);
 
+    const uint32_t tl_items = n_items;
     for (uint32_t base = lo; base < n_items; base += LIB_CAND) {
         __syncthreads();
+        if (gsorted && base > lo && chunk != chunk0) {
+            // a sorted list: every entry from `base` on lies in hsr bucket >= the one of bin[base]; once the
+            // tile's largest key z (the waves' maxima after the last pass, stale only upwards) sorts into a
+            // lower bucket, or below the whole range, no later entry can beat any pixel -- the tile is done
+            const uint32_t om = max(max(sh.wmax[0], sh.wmax[1]), max(sh.wmax[2], sh.wmax[3]));
+            if (om < hsr.x || hs_bucket(hsr, om) < hs_bucket(hsr, bin[base].w)) break;
+        }
+        ++t_rounds;
         if (tid == 0) { sh.nc = 0; sh.zlo = 0xffffffffu; sh.zhi = 0u; }
         sh.hist[tid] = 0u;
         __syncthreads();
@@ -2053,7 +2081,10 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 const bool first = chunk == chunk0;   // no key of the tile written yet
                 const uint32_t ordmax = first ? 0xffffffffu : max(max(sh.wmax[0], sh.wmax[1]), max(sh.wmax[2], sh.wmax[3]));
                 // (the list is front to back only when sorted; the per-position test below holds either way)
-                if (sorted && ordmax != 0xffffffffu && (ordmax < s_lo || bucket(ordmax) < bucket(sh.lkey[p]))) break;
+                if (sorted && ordmax != 0xffffffffu && (ordmax < s_lo || bucket(ordmax) < bucket(sh.lkey[p]))) {
+                    ++t_breaks;
+                    break;
+                }
                 ++chunk;
                 sh.bits[tid] = 0ull;
                 sh.bits[tid + 256] = 0ull;
@@ -2077,6 +2108,10 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                             alive = zk <= mx;
                         }
                     }
+                }
+                if (fb.timeline) {   // (uniform) staged candidates of this tile
+                    const uint64_t am = __ballot(alive && h == 0);
+                    if (lane == 0 && am) atomicAdd(&sh.tl_staged, (uint32_t)__popcll(am));
                 }
                 // the record: half h loads and stages its two float4s; both need the first two (the spans)
                 float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
@@ -2137,6 +2172,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                 const int total = (int)(ptot >> 11);
                 if (tlon) {
                     const uint64_t t_c = tl_now();
+                    t_pairs += (uint32_t)total;
                     sh.tl[LTL_NPAIRS] += (uint32_t)total;
                     sh.tl[LTL_STAGE] += t_b - t_a;
                     sh.tl[LTL_SEG] += t_c - t_b;
@@ -2366,6 +2402,11 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
         sh.tl[LTL_SHADE] += t_end - t_res;
         sh.tl[LTL_NBUSY] += 1;
         sh.tl[LTL_CHUNKS] += chunk - chunk0;
+        if (t_end - t_tile > sh.tl[LTL_MAXTILE]) {   // this workgroup's longest tile so far
+            sh.tl[LTL_MT_RT] = (uint64_t)rt; sh.tl[LTL_MT_ITEMS] = tl_items; sh.tl[LTL_MT_ROUNDS] = t_rounds;
+            sh.tl[LTL_MT_PASSES] = chunk - chunk0; sh.tl[LTL_MT_STAGED] = sh.tl_staged; sh.tl[LTL_MT_PAIRS] = t_pairs;
+            sh.tl[LTL_MT_GATHER] = t_gather; sh.tl[LTL_MT_BREAKS] = t_breaks;
+        }
         sh.tl[LTL_MAXTILE] = max(sh.tl[LTL_MAXTILE], t_end - t_tile);
         sh.tl[LTL_TILES] += t_end - t_tile;
         sh.tl[LTL_LAST] = t_end;
@@ -2441,6 +2482,26 @@ __global__ __launch_bounds__(256) void k_lib_dyn(LibFrameParams fp, LibBuffers f
         q = (p >= dyn0 ? p - dyn0 : p) & (LIB_NQ - 1);
     }
     const int lane = __lane_id();
+    if (fp.hsort) {
+        // a bin list k_lib_hsort sorts: longer than one candidate round, held whole in its bin (no spill),
+        // listed once -- by its first busy raster row (every raster tile of an owned bin tile is owned)
+        bool hs = false;
+        uint32_t hbt = 0u;
+        if (p >= n_split && p < n_work) {
+            const int rt = fb.rt_order[p - n_split];
+            if (fb.busy[rt] == 1u) {
+                constexpr int RPB = TILE / LIB_RTH;
+                const int col = rt % fp.tiles_x, row = rt / fp.tiles_x, r = row % RPB;
+                hbt = (uint32_t)((row / RPB) * fp.tiles_x + col);
+                const uint32_t n = fb.tile_count[(size_t)fp.parity * fp.tiles_x * fp.tiles_y + hbt];
+                if (n > fp.hsort_min && n <= min(fp.bin_cap, (uint32_t)LIB_HSORT_MAX)) {
+                    hs = true;
+                    for (int k = 1; k <= r; ++k) hs = hs && fb.busy[rt - k * fp.tiles_x] == 0u;
+                }
+            }
+        }
+        wave_append(const_cast<uint32_t *>(&cnt[LC_HSORT]), fb.hsq, hs, hbt);
+    }
     for (int qq = 0; qq < LIB_NQ; ++qq)
         for (int hv = 0; hv < 2; ++hv) {
             const bool me = keep && q == qq && heavy == (hv == 1);
@@ -2452,6 +2513,81 @@ __global__ __launch_bounds__(256) void k_lib_dyn(LibFrameParams fp, LibBuffers f
             base = (uint32_t)__shfl((int)base, lead);
             if (me) fb.dynq[(size_t)(2 * qq + (hv ? 0 : 1)) * fp.dyn_cap + base + lanes_below(m)] = w;
         }
+}
+
+// Camera pass: each listed bin tile's list (k_lib_dyn: more than one candidate round of entries) sorted in
+// place by depth bound -- a counting sort over 256 buckets of its range, order inside a bucket free.
+// k_lib_raster's rounds over such a list then run front to back over the whole list, not over each
+// 1024-entry window of it: the first round sets the tile's keys from the list's true front, and a later
+// round whose first entry's bucket lies beyond the tile's largest key z is not gathered at all (C4's hot
+// tiles: ~5,000 entries in five rounds, each round's own front near the list's front).  The order of a
+// tile's list is free: the raster resolves by (z, submission) keys.
+__global__ __launch_bounds__(LIB_HSORT_T) void k_lib_hsort(LibFrameParams fp, LibBuffers fb) {
+    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_lo, s_hi, s_wsum[4];
+    const uint32_t n_list = fb.counters[fp.parity * LC_N + LC_HSORT];
+    const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t *tcount = fb.tile_count + (size_t)fp.parity * fp.tiles_x * fp.tiles_y;
+    for (uint32_t li = blockIdx.x; li < n_list; li += gridDim.x) {   // block-uniform
+        const uint32_t bt = fb.hsq[li];
+        const uint32_t n = tcount[bt];   // (hsort_min < n <= min(bin_cap, LIB_HSORT_MAX): k_lib_dyn)
+        uint4 *bin = fb.bins + (size_t)bt * fp.bin_cap;
+        if (tid < 256) s_hist[tid] = 0u;
+        if (tid == 0) { s_lo = 0xffffffffu; s_hi = 0u; }
+        __syncthreads();
+        uint4 e[LIB_HSORT_PER];
+        uint32_t zlo = 0xffffffffu, zhi = 0u;
+#pragma unroll
+        for (int k = 0; k < LIB_HSORT_PER; ++k) {
+            const uint32_t j = (uint32_t)(tid + LIB_HSORT_T * k);
+            e[k] = j < n ? bin[j] : make_uint4(0u, 0u, 0u, 0u);
+            if (j < n) { zlo = min(zlo, e[k].w); zhi = max(zhi, e[k].w); }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            zlo = min(zlo, (uint32_t)__shfl_xor((int)zlo, off));
+            zhi = max(zhi, (uint32_t)__shfl_xor((int)zhi, off));
+        }
+        if (lane == 0) { atomicMin(&s_lo, zlo); atomicMax(&s_hi, zhi); }
+        __syncthreads();
+        const uint2 range = make_uint2(s_lo, s_hi);
+        uint32_t br[LIB_HSORT_PER];   // bucket | rank in bucket << 8
+#pragma unroll
+        for (int k = 0; k < LIB_HSORT_PER; ++k) {
+            const uint32_t j = (uint32_t)(tid + LIB_HSORT_T * k);
+            br[k] = 0u;
+            if (j < n) {
+                const uint32_t b = hs_bucket(range, e[k].w);
+                br[k] = b | (atomicAdd(&s_hist[b], 1u) << 8);
+            }
+        }
+        __syncthreads();
+        uint32_t c = 0u, incl = 0u;
+        if (tid < 256) {   // exclusive prefix of the bucket counts (waves 0..3)
+            c = s_hist[tid];
+            incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
+                if (lane >= o) incl += v;
+            }
+            if (lane == 63) s_wsum[wave] = incl;
+        }
+        __syncthreads();
+        if (tid < 256) {
+            uint32_t base = 0u;
+            for (int w2 = 0; w2 < wave; ++w2) base += s_wsum[w2];
+            s_hist[tid] = base + incl - c;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < LIB_HSORT_PER; ++k) {
+            const uint32_t j = (uint32_t)(tid + LIB_HSORT_T * k);
+            if (j < n) bin[s_hist[br[k] & 255u] + (br[k] >> 8)] = e[k];
+        }
+        if (tid == 0) fb.hsr[bt] = range;
+        __syncthreads();   // LDS reused by the next listed tile
+    }
 }
 
 __global__ __launch_bounds__(256) void k_lib_plan(LibFrameParams fp, LibBuffers fb) {
@@ -2758,6 +2894,8 @@ hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, boo
     if (!shadow) {   // every position could be dynamic (a grid of one workgroup); threads past the end exit
         const int64_t n_max = (int64_t)fp.n_owned_rt * (fp.part ? 1 + LIB_MAXK : 1);
         hipLaunchKernelGGL(k_lib_dyn, dim3((unsigned)std::max<int64_t>(1, (n_max + 255) / 256)), dim3(256), 0, s, fp, fb);
+        // the listed bin tiles (at most one per owned bin tile), 512 workgroups striding the list
+        if (fp.hsort) hipLaunchKernelGGL(k_lib_hsort, dim3(512), dim3(LIB_HSORT_T), 0, s, fp, fb);
     }
     hipLaunchKernelGGL(SHS_RASTER_KERNEL(shadow, shallow), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();

@@ -100,9 +100,10 @@ constexpr uint32_t LF_PERM = 16u;       // a draw's mesh is stored in spatial or
 // atomicAdd hands an appender both bases and the queue's task prefix stays monotone; LC_N even keeps
 // the second parity set's word 8-B aligned.
 // LC_ITEMS: k_lib_plan's raster work items; LC_COVERED: camera-pass covered pixels (k_lib_resolve);
-// LC_SPLITS: k_lib_plan's split tiles (their pkeys slots); LC_BLOCKS: k_lib_blocks' listed setup blocks.
+// LC_SPLITS: k_lib_plan's split tiles (their pkeys slots); LC_BLOCKS: k_lib_blocks' listed setup blocks;
+// LC_HSORT: k_lib_dyn's bin tiles for k_lib_hsort.
 constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT = 4, LC_BIGQ = 5, LC_ITEMS = 6, LC_COVERED = 7,
-              LC_SPLITS = 8, LC_BLOCKS = 9, LC_N = 10;
+              LC_SPLITS = 8, LC_BLOCKS = 9, LC_HSORT = 10, LC_N = 12;
 static_assert(LC_BIGQ == LC_BIGT + 1 && LC_BIGT % 2 == 0 && LC_N % 2 == 0, "64-bit big-queue word");
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
@@ -133,6 +134,8 @@ struct LibFrameParams {
     uint32_t heavy_min;              // camera pass: a busy tile whose bin list holds >= this many entries is
                                      // rendered from k_lib_dyn's heavy lists, first (0: no heavy lists)
     uint32_t dyn_cap;                // camera pass: entries per queue of LibBuffers::dynq
+    uint32_t hsort;                  // camera pass: bin lists of more than hsort_min entries (and at most
+    uint32_t hsort_min;              //   min(bin_cap, LIB_HSORT_MAX)) are depth-sorted whole by k_lib_hsort
     ShardRegion reg;                 // count > 1 with reg.on: this rank's rectangle of bin tiles
 };
 
@@ -184,7 +187,14 @@ struct LibBuffers {
     uint32_t *s2s;                   // camera pass with LF_PERM: per input triangle in submission order, its slot
     uint4 *blkrect;                  // camera pass: per setup block (bx0 | bx1 << 16, by0 | by1 << 16, triangles,
                                      // bounded) of its chunk bounds, mapped host memory (the region balancer's input)
+    uint32_t *hsq;                   // camera pass with fp.hsort: the bin tiles k_lib_hsort sorts (k_lib_dyn)
+    uint2 *hsr;                      // ... per bin tile: the depth-bound range (lo, hi) its list was bucketed over
 };
+
+// k_lib_hsort: one 1024-thread workgroup per listed bin tile, LIB_HSORT_PER entries per thread in registers.
+// Lists of more than LIB_HSORT_MIN entries (one deep candidate round, LIB_CAND_DEEP) are sorted.
+constexpr int LIB_HSORT_T = 1024, LIB_HSORT_PER = 8, LIB_HSORT_MAX = LIB_HSORT_T * LIB_HSORT_PER;
+constexpr uint32_t LIB_HSORT_MIN = 1024;
 
 // k_lib_plan: at most this many parts per raster tile (capacity: LIB_MAXK * owned raster tiles).
 constexpr int LIB_MAXK = 16;
@@ -203,8 +213,12 @@ constexpr int STL_STRIDE = 8;
 
 // Library raster timeline slots (s_memrealtime, 100 MHz ticks): per workgroup start, end, summed
 // phase ticks over its busy tiles (gather, stage + pairs, resolve + shade), clear ticks, counts.
-constexpr int LTL_STRIDE = 16;
+// Slots 16..23: the workgroup's longest busy tile -- its raster tile, list entries, candidate rounds,
+// staging passes, staged candidates, pairs, gather ticks, passes that ended their round early.
+constexpr int LTL_STRIDE = 24;
 enum : int { LTL_START = 0, LTL_END, LTL_GATHER, LTL_PAIRS, LTL_SHADE, LTL_CLEAR, LTL_NBUSY, LTL_NCLEAR, LTL_CHUNKS,
-             LTL_NPAIRS, LTL_NCAND, LTL_MAXTILE, LTL_STAGE, LTL_SEG, LTL_TILES, LTL_LAST };
+             LTL_NPAIRS, LTL_NCAND, LTL_MAXTILE, LTL_STAGE, LTL_SEG, LTL_TILES, LTL_LAST,
+             LTL_MT_RT, LTL_MT_ITEMS, LTL_MT_ROUNDS, LTL_MT_PASSES, LTL_MT_STAGED, LTL_MT_PAIRS, LTL_MT_GATHER,
+             LTL_MT_BREAKS };
 
 }  // namespace shs_dev

@@ -514,11 +514,13 @@ class Context:
         return tuple(int(v) for v in out)
 
     LIB_TIMELINE_FIELDS = ("start", "end", "gather", "pairs", "shade", "clear", "n_busy", "n_clear", "chunks",
-                           "n_pairs", "n_cand", "max_tile", "stage", "seg", "tiles", "last")
+                           "n_pairs", "n_cand", "max_tile", "stage", "seg", "tiles", "last",
+                           "mt_rt", "mt_items", "mt_rounds", "mt_passes", "mt_staged", "mt_pairs", "mt_gather",
+                           "mt_breaks")
 
     def lib_debug_timeline(self):
-        """Last camera pass's k_lib_raster workgroup timeline: uint64 [grid, 16] (LIB_TIMELINE_FIELDS;
-        times in 10-ns ticks)."""
+        """Last camera pass's k_lib_raster workgroup timeline: uint64 [grid, 24] (LIB_TIMELINE_FIELDS;
+        times in 10-ns ticks; mt_*: the workgroup's longest busy tile)."""
         n = ctypes.c_int64()
         self._check(self._lib.shs_lib_debug_timeline(self._h, None, 0, ctypes.byref(n)))
         out = np.zeros(n.value, dtype=np.uint64)
