@@ -2894,8 +2894,8 @@ hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, boo
     if (!shadow) {   // every position could be dynamic (a grid of one workgroup); threads past the end exit
         const int64_t n_max = (int64_t)fp.n_owned_rt * (fp.part ? 1 + LIB_MAXK : 1);
         hipLaunchKernelGGL(k_lib_dyn, dim3((unsigned)std::max<int64_t>(1, (n_max + 255) / 256)), dim3(256), 0, s, fp, fb);
-        // the listed bin tiles (at most one per owned bin tile), 512 workgroups striding the list
-        if (fp.hsort) hipLaunchKernelGGL(k_lib_hsort, dim3(512), dim3(LIB_HSORT_T), 0, s, fp, fb);
+        // the listed bin tiles (at most one per owned bin tile), a workgroup per CU striding the list
+        if (fp.hsort) hipLaunchKernelGGL(k_lib_hsort, dim3(256), dim3(LIB_HSORT_T), 0, s, fp, fb);
     }
     hipLaunchKernelGGL(SHS_RASTER_KERNEL(shadow, shallow), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();

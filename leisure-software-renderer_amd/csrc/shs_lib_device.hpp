@@ -191,9 +191,10 @@ struct LibBuffers {
     uint2 *hsr;                      // ... per bin tile: the depth-bound range (lo, hi) its list was bucketed over
 };
 
-// k_lib_hsort: one 1024-thread workgroup per listed bin tile, LIB_HSORT_PER entries per thread in registers.
+// k_lib_hsort: one 512-thread workgroup per listed bin tile, LIB_HSORT_PER entries per thread in registers (a
+// 1024-thread workgroup waited for a whole free CU beside the other frames in flight: 8.5 -> 30 us at 8 ranks).
 // Lists of more than LIB_HSORT_MIN entries (one deep candidate round, LIB_CAND_DEEP) are sorted.
-constexpr int LIB_HSORT_T = 1024, LIB_HSORT_PER = 8, LIB_HSORT_MAX = LIB_HSORT_T * LIB_HSORT_PER;
+constexpr int LIB_HSORT_T = 512, LIB_HSORT_PER = 16, LIB_HSORT_MAX = LIB_HSORT_T * LIB_HSORT_PER;
 constexpr uint32_t LIB_HSORT_MIN = 1024;
 
 // k_lib_plan: at most this many parts per raster tile (capacity: LIB_MAXK * owned raster tiles).
