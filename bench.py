@@ -129,9 +129,6 @@ def run_gpu(args, rank, local_rank, world, dist):
         ctx.enable_timing(False)
         single = {"ms_per_frame": round(el1 / n1 * 1e3, 5), "steps": n1,
                   "kernels_ms": {k: round(v, 5) for k, v in k1.items()}}
-    pcie = None
-    if F > 1 and world == 1 and not args.child and not args.no_pcie:
-        pcie = seam1_pcie(args, ctx, frame, sets)
     # Clock ramp: the GPU reaches its steady-state clocks only after ~15-20 ms of continuous rendering
     # (tools/diag_short_window.py: consecutive 20-step windows right after 5 warm-up steps run 0.304,
     # 0.294, then 0.285 ms/step, k_raster 0.260 -> 0.242 ms; profiles/r04_c2_short_window.txt).  A render
@@ -172,14 +169,17 @@ def run_gpu(args, rank, local_rank, world, dist):
     n_launches, kms = ctx.timing_read()
     ctx.enable_timing(False)
     ctx.close()
-    return frame, sets[0][0], stats, elapsed, n_launches, kms, single, pcie, ramp
+    return frame, sets, stats, elapsed, n_launches, kms, single, ramp
 
 
-def seam1_pcie(args, ctx, frame, sets):
+def seam1_pcie(args, frame, sets):
     """The end-to-end Seam-1 figure: every frame crosses PCIe into pinned host memory as the SDL
     surface it is presented from (SHS_FRAME_PRESENT staging, 4 B/px, what copy_to_SDLSurface produces),
     D2H overlapped with rendering: two contexts alternate batches, each batch's D2H queued behind its
-    render on that context's stream, so one context's copy runs under the other's render."""
+    render on that context's stream, so one context's copy runs under the other's render.
+    It runs LAST in the process: it initialises torch (streams, pinned memory), after which the library
+    legs' streams measured 12 % slower in the same process (C4 0.579 -> 0.654 ms per frame,
+    profiles/r06_strong_gap.txt), so nothing timed for the line follows it."""
     import ctypes
     import dataclasses
     import shs_gpu
@@ -189,7 +189,7 @@ def seam1_pcie(args, ctx, frame, sets):
     hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
     pf = dataclasses.replace(frame, present=True)
     nbytes = F * pf.width * pf.height * 4
-    ctxs = [ctx, shs_gpu.Context(0)]
+    ctxs = [shs_gpu.Context(0), shs_gpu.Context(0)]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     hosts = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
     prepared = []
@@ -221,8 +221,8 @@ def seam1_pcie(args, ctx, frame, sets):
                            nbytes, 2, ctypes.c_void_p(streams[i % 2].cuda_stream))
     torch.cuda.synchronize()
     el_copy = time.perf_counter() - t1
-    ctxs[1].close()
-    ctx.set_stream(0)
+    for c in ctxs:
+        c.close()
     n_tri = sum(d.mesh.n_tris for d in sets[0][0])
     return {"frames": n * F, "ms_per_frame": round(el / (n * F) * 1e3, 5),
             "mtri_s": round(n_tri * n * F / el / 1e6, 3), "d2h_gb_s": round(n * nbytes / el / 1e9, 2),
@@ -855,9 +855,13 @@ def main():
 
     if args.config in LIB_CONFIGS:
         return main_lib(args, world, rank, local_rank, dist, pmc, pmc_err)
-    frame, draws, stats, elapsed, n_launches, kms, single, pcie, ramp = run_gpu(args, rank, local_rank, world, dist)
+    frame, sets, stats, elapsed, n_launches, kms, single, ramp = run_gpu(args, rank, local_rank, world, dist)
+    draws = sets[0][0]
     # the strong-scaling legs ride on the headline configuration's line (the driver's `--gpus N` run)
     strong = strong_legs_guarded(args, rank, local_rank, world, dist) if args.strong and not args.child and args.config == "c2" else {}
+    pcie = None   # (last: seam1_pcie)
+    if args.frames_per_step > 1 and world == 1 and not args.child and not args.no_pcie:
+        pcie = seam1_pcie(args, frame, sets)
     B1, n_tri1 = algorithmic_bytes(frame, draws)
     F = args.frames_per_step
     B, n_tri = B1 * F, n_tri1 * F          # per step (= per k_raster launch)
