@@ -250,9 +250,11 @@ class LibSlot:
             self.ctx.set_shard_root_share(args.root_share)
         self.stream = None
         if dist is not None:
+            # the gather is ordered on the context's own stream (wrapped for torch, not a new torch stream:
+            # every extra stream shares the process's 4 hardware queues with the contexts' streams, which
+            # cost the library legs 12 % at N = 1, profiles/r06_strong_gap.txt)
             import torch
-            self.stream = torch.cuda.Stream()
-            self.ctx.set_stream(self.stream.cuda_stream)
+            self.stream = torch.cuda.ExternalStream(self.ctx.stream, device=torch.device("cuda", local_rank))
         self.gbufs = [None]
         self.prepared = None
         self.gather_events = None   # [(start, end)] HIP events around each gather while timing
