@@ -26,7 +26,13 @@ namespace {
 // with the triangles' screen size, which grows with the bounds they spread over, so a block costs about
 // its triangles on each tile of its bounds).  Fitted to the measured per-rank times of the 8-way C4 frame
 // (tools/region_model.py): covered pixels about 19x a (triangle, tile) pair.
-constexpr double REGION_PX = 5.0, REGION_COVERED_PX = 15.0;
+#ifndef SHS_REGION_PX
+#define SHS_REGION_PX 5.0
+#endif
+#ifndef SHS_REGION_COVERED_PX
+#define SHS_REGION_COVERED_PX 15.0
+#endif
+constexpr double REGION_PX = SHS_REGION_PX, REGION_COVERED_PX = SHS_REGION_COVERED_PX;
 
 struct Sat {   // summed-area table over the bin grid
     int tx, ty;

@@ -78,6 +78,12 @@ constexpr int LIB_RTW = 32, LIB_RTH = 8;   // raster tile (one 256-thread workgr
 constexpr int LIB_CAND_DEEP = 1024, LIB_CAND_SHALLOW = 256;
 static_assert(LIB_HSORT_MIN == (uint32_t)LIB_CAND_DEEP, "k_lib_hsort sorts the lists of more than one deep round");
 constexpr int LIB_CHUNK = 128;             // records staged in LDS per pass
+#ifndef SHS_HIZ_BOX
+#define SHS_HIZ_BOX 16                     // deep raster: boxes up to this many pixels are tested against their pixels' keys
+#endif
+#ifndef SHS_HSORT_GRID
+#define SHS_HSORT_GRID 256                 // k_lib_hsort workgroups (one per CU)
+#endif
 constexpr int MAX_POLY = 16;               // clipped polygon capacity (3 + 6 planes x up to 2 crossings)
 
 __device__ __forceinline__ bool lib_owned(const LibFrameParams &fp, int bx, int by) {
@@ -2101,7 +2107,7 @@ __device__ void lib_raster_tile(const LibFrameParams &fp, const LibBuffers &fb, 
                     if (alive && hiz && !first) {
                         if (zk > ordmax) {
                             alive = false;
-                        } else if ((bx1 - bx0 + 1) * (by1 - by0 + 1) <= 16) {
+                        } else if ((bx1 - bx0 + 1) * (by1 - by0 + 1) <= SHS_HIZ_BOX) {
                             uint32_t mx = 0u;
                             for (int y = by0; y <= by1; ++y)
                                 for (int x = bx0; x <= bx1; ++x) mx = max(mx, keyhi[2 * ((y - TY0) * LIB_RTW + (x - TX0)) + 1]);
@@ -2895,7 +2901,7 @@ hipError_t launch_lib_raster(const LibFrameParams &fp, const LibBuffers &fb, boo
         const int64_t n_max = (int64_t)fp.n_owned_rt * (fp.part ? 1 + LIB_MAXK : 1);
         hipLaunchKernelGGL(k_lib_dyn, dim3((unsigned)std::max<int64_t>(1, (n_max + 255) / 256)), dim3(256), 0, s, fp, fb);
         // the listed bin tiles (at most one per owned bin tile), a workgroup per CU striding the list
-        if (fp.hsort) hipLaunchKernelGGL(k_lib_hsort, dim3(256), dim3(LIB_HSORT_T), 0, s, fp, fb);
+        if (fp.hsort) hipLaunchKernelGGL(k_lib_hsort, dim3(SHS_HSORT_GRID), dim3(LIB_HSORT_T), 0, s, fp, fb);
     }
     hipLaunchKernelGGL(SHS_RASTER_KERNEL(shadow, shallow), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
