@@ -254,12 +254,10 @@ uint64_t region_key(const shs_dev::ShardRegion &g) {
 // kernels.  shadow: PassShadowMap's depth pass into ctx->shadow_map.
 int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     LibFrameParams fp = w.last_fp;
-    // After a shadow pass, the camera pass's setup and raster run on the side stream
-    // (ctx->setup_stream): they read only the meshes and the draw table, so they overlap the shadow
-    // pass on the main stream (C5 0.573 -> 0.555 ms/frame; without one the two event hops cost more
-    // than the light cull they could overlap, C4 at N = 8 0.255 -> 0.279 ms).  They wait for the
-    // previous camera resolve (it reads the records, the draw table and the keys this pass rewrites);
-    // the resolve waits for the raster.
+    // With ctx->cam_after_shadow (timing experiments only since round 6, SHS_EXP_CAM_SIDE_STREAM) the camera
+    // pass's setup and raster run on the side stream (ctx->setup_stream) beside the shadow pass on the main
+    // stream; they read only the meshes and the draw table, and wait for the previous camera resolve (it
+    // reads the records, the draw table and the keys this pass rewrites); the resolve waits for the raster.
     hipStream_t ps = (shadow || !ctx->cam_after_shadow) ? ctx->stream : ctx->setup_stream;
     if (!shadow) {
         if (!w.raster_ev) {
@@ -1131,7 +1129,16 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
         }
     }
     ctx->lib_frame = f;
+    // The camera pass runs on the context's stream after its shadow pass (round 6): with three frames in
+    // flight the frames overlap each other, and a context with one busy stream keeps the process's 4
+    // hardware queues to one stream per frame -- on the side stream beside the shadow pass, C5's strong
+    // leg after the C4 leg read 0.394-0.405 against 0.370-0.371 ms per frame, --config c5 unchanged
+    // (profiles/r06_c5_one_stream_ab.txt).  (SHS_EXP_CAM_SIDE_STREAM: the side stream, timing only.)
+#ifdef SHS_EXP_CAM_SIDE_STREAM
     ctx->cam_after_shadow = ctx->have_shadow;
+#else
+    ctx->cam_after_shadow = false;
+#endif
     wk.tm_fused = ctx->tm_fuse;
     wk.tm_desc = ctx->tm_fuse_desc;
     const int rc = enqueue_pass(ctx, wk, false);
