@@ -166,8 +166,9 @@ int shs_model_trs(const float position[3], float rotation_deg_y, const float sca
 int shs_mat4_mul(const float a16[16], const float b16[16], float out16[16]);
 int shs_mat4_inverse(const float m16[16], float out16[16]);
 
-/* Debug / test hook: copy the last frame's per-triangle raster records (96 B each, layout
- * shs_dev::TriRec in csrc/shs_device.hpp) into caller memory; returns the count via n_out.
+/* Debug / test hook: copy the last frame's per-triangle raster records (64 B each, layout
+ * shs_dev::TriHot in csrc/shs_device.hpp: the pixel-independent barycentric terms, screen z, a
+ * draw | flags << 29 word and the packed bin box) into caller memory; returns the count via n_out.
  * Records of culled triangles are not written by the legacy setup (stale entries). */
 int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out);
 

@@ -21,7 +21,6 @@
 using shs_dev::DrawGPU;
 using shs_dev::FrameBuffers;
 using shs_dev::FrameParams;
-using shs_dev::TriRec;
 
 extern "C" {
 
@@ -88,7 +87,7 @@ int shs_destroy(shs_ctx *ctx) {
     }
     shs_lib_release(ctx);
     for (auto &w : ctx->lslot) {
-        release(w.draws); release(w.recs); release(w.shade); release(w.tile_count); release(w.bins);
+        release(w.draws); release(w.recs); release(w.rext); release(w.shade); release(w.tile_count); release(w.bins);
         release(w.spill); release(w.frags); release(w.busy); release(w.boxes); release(w.slivers); release(w.busy_list);
         release(w.blk_stat); release(w.rstat);
         if (w.h_draws) (void)hipHostFree(w.h_draws);
@@ -292,7 +291,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     if (ws.used) HIP_TRY(ctx, hipEventSynchronize(ws.setup_done));
     *ws.h_ov = 0u;   // the slot's previous setup (the only other writer) is done
 
-    if (ensure(ctx, ws.recs, nt_all) || ensure(ctx, ws.shade, nt_all) || ensure(ctx, ws.boxes, nt_all) ||
+    if (ensure(ctx, ws.recs, nt_all) || ensure(ctx, ws.rext, nt_all) || ensure(ctx, ws.shade, nt_all) || ensure(ctx, ws.boxes, nt_all) ||
         ensure(ctx, ws.slivers, nt_all))
         return SHS_ERR_HIP;
     const size_t n_bt_all = (size_t)n_tiles * n_frames;
@@ -474,7 +473,7 @@ static int enqueue_frame(shs_ctx *ctx) {
     }
 
     FrameBuffers fb;
-    fb.draws = ws.draws.p; fb.bdraw = bdraw; fb.recs = ws.recs.p; fb.shade = ws.shade.p; fb.tile_count = ws.tile_count.p; fb.bins = ws.bins.p;
+    fb.draws = ws.draws.p; fb.bdraw = bdraw; fb.recs = ws.recs.p; fb.rext = ws.rext.p; fb.shade = ws.shade.p; fb.tile_count = ws.tile_count.p; fb.bins = ws.bins.p;
     fb.spill = ws.spill.p; fb.frags = ws.frags.p; fb.counters = ctx->counters.p;
     fb.slivers = ws.slivers.p;
     fb.busy = ws.busy.p;
@@ -802,7 +801,7 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
     *n_out = ctx->last_n_tris;
     if (out && capacity > 0) {
         const size_t n = (size_t)std::min<int64_t>(capacity, ctx->last_n_tris);
-        HIP_TRY(ctx, hipMemcpy(out, ctx->lslot[ctx->last_slot].recs.p, n * sizeof(TriRec), hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(out, ctx->lslot[ctx->last_slot].recs.p, n * sizeof(shs_dev::TriHot), hipMemcpyDeviceToHost));
     }
     return SHS_OK;
 }

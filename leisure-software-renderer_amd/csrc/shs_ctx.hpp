@@ -75,7 +75,8 @@ struct shs_ctx {
         DevBuf<shs_dev::DrawGPU> draws;      // device draw table (> KARG_DRAWS draws)
         shs_dev::DrawGPU *h_draws = nullptr; // pinned staging of that table
         size_t h_cap = 0;
-        DevBuf<shs_dev::TriRec> recs;
+        DevBuf<shs_dev::TriHot> recs;        // per frame: 64-B stored records
+        DevBuf<float4> rext;                 // per frame: float bboxes of ghosts
         DevBuf<shs_dev::ShadeRec> shade;
         DevBuf<uint32_t> tile_count;         // per frame: per-bin-tile counts (zeroed per batch)
         DevBuf<uint32_t> bins;               // per frame: n_tiles * bin_cap

@@ -53,6 +53,22 @@ struct alignas(16) TriRec {
 };
 static_assert(sizeof(TriRec) == 96, "TriRec must stay 96 B");
 
+// The record as k_setup stores it in HBM (round 6): TriRec's pixel-independent terms, the draw | flags
+// word (draw | flags << 29) and the bin box, 64 B = four float4s, sector-aligned -- everything a staged
+// candidate's pair tests, row spans and resolve read.  The float bbox (and the integer bbox derived from
+// it) is needed only by ghosts (TRI_GHOST: the tile-clamp test) and k_ghost: it goes to a 16-B side
+// array (FrameBuffers::rext, fminx fmaxx fminy fmaxy), stored for ghosts only.  local is not stored.
+// (Was the whole 96-B TriRec per triangle: C3's raster staged 96 B per candidate and tile.)
+struct alignas(16) TriHot {
+    float ax, ay, v0x, v0y;
+    float v1x, v1y, d00, d01;
+    float d11, denom, z0, z1;
+    float z2;
+    uint32_t word;                   // draw | flags << 29
+    uint32_t gbx, gby;               // bin box
+};
+static_assert(sizeof(TriHot) == 64, "TriHot must stay 64 B");
+
 // Per-triangle shading varyings written by k_setup (the legacy VS outputs of the three corners the
 // winning pixels interpolate), 80 B: Blinn-Phong/Phong: world_pos[3] then normalize(N*n)[3];
 // Gouraud: the clamped per-vertex colour[3] (carried in world_pos, gouraud_shading.cpp:71);
@@ -190,7 +206,8 @@ struct FrameBuffers {
     const DrawGPU *draws;            // device draw table (n_frames * n_draws > KARG_DRAWS)
     const int32_t *bdraw;            // per setup block: the frame-local draw of its first triangle when
                                      // every frame has the same draw layout (device table only), or null
-    TriRec *recs;                    // per frame: n_tris
+    TriHot *recs;                    // per frame: n_tris
+    float4 *rext;                    // per frame: n_tris float bboxes (fminx, fmaxx, fminy, fmaxy), ghosts only
     ShadeRec *shade;                 // per frame: n_tris
     uint32_t *tile_count;            // per frame: n_bin_tiles counts (zeroed before each launch)
     uint32_t *bins;                  // per frame: n_bin_tiles * bin_cap
@@ -230,6 +247,7 @@ __device__ __forceinline__ FrameBuffers frame_view(const FrameParams &fp, const 
     const size_t nt = (size_t)fp.n_tris, n_bt = (size_t)fp.tiles_x * fp.tiles_y;
     const size_t npx = (size_t)fp.W * fp.H, n_rt = (size_t)fp.tiles_x * fp.rtiles_y;
     v.recs += f * nt;
+    v.rext += f * nt;
     if (!(fp.flags & RF_SHARED_VARY)) v.shade += f * nt;
     v.boxes += f * nt;
     if (v.tdraw) v.tdraw += f * nt;

@@ -124,6 +124,51 @@ __device__ __forceinline__ TriRec rec_from(const float4 *s) {
     return r;
 }
 
+// Bin and spill entries carry this tag on a ghost's id: k_raster stages the ghost's float bbox (the
+// tile-clamp test's input, FrameBuffers::rext) beside its record, in the same round trip.
+constexpr uint32_t BIN_GHOST = 0x80000000u;
+
+// The record from its stored 64-B part h (TriHot, four float4s) and float bbox e (fminx fmaxx fminy
+// fmaxy; read only when the flags say TRI_GHOST -- other triangles' e is never stored): the integer
+// bbox is the clamped floor of the float bbox, as rec_from_screen computes it for a kept triangle.
+__device__ __forceinline__ TriRec rec_from_hot(const FrameParams &fp, float4 h0, float4 h1, float4 h2, float4 h3, float4 e) {
+    TriRec r;
+    r.ax = h0.x; r.ay = h0.y; r.v0x = h0.z; r.v0y = h0.w;
+    r.v1x = h1.x; r.v1y = h1.y; r.d00 = h1.z; r.d01 = h1.w;
+    r.d11 = h2.x; r.denom = h2.y; r.z0 = h2.z; r.z1 = h2.w;
+    r.z2 = h3.x;
+    const uint32_t word = __float_as_uint(h3.y);
+    r.flags = word >> 29;
+    r.draw = (int32_t)(word & 0x1fffffffu);
+    r.local = 0;
+    r.gbx = __float_as_uint(h3.z); r.gby = __float_as_uint(h3.w);
+    r.fminx = e.x; r.fmaxx = e.y; r.fminy = e.z; r.fmaxy = e.w;
+    r.ibx = pack16(floor_clamped(e.x, 0, fp.W), floor_clamped(e.y, -1, fp.W - 1));
+    r.iby = pack16(floor_clamped(e.z, 0, fp.H), floor_clamped(e.w, -1, fp.H - 1));
+    return r;
+}
+
+__device__ __forceinline__ TriRec rec_from_hot(const FrameParams &fp, const float4 *h, const float4 *e) {
+    return rec_from_hot(fp, h[0], h[1], h[2], h[3], *e);
+}
+
+// Quad: lane q stores float4 q of the triangle's 64-B TriHot, lane 0 also its float bbox when ext.
+__device__ __forceinline__ void quad_store_hot(float4 *hot, float4 *bbox, const TriRec &r, bool ext) {
+    const int q = __lane_id() & 3;
+    const float f[16] = {r.ax, r.ay, r.v0x, r.v0y, r.v1x, r.v1y, r.d00, r.d01, r.d11, r.denom, r.z0, r.z1,
+                         r.z2, __uint_as_float(r.flags << 29 | (uint32_t)r.draw), __uint_as_float(r.gbx), __uint_as_float(r.gby)};
+    float x = f[0], y = f[1], z = f[2], w = f[3];
+#pragma unroll
+    for (int qq = 1; qq < 4; ++qq) {   // selects, not an indexed read (which would put the record in scratch)
+        x = q == qq ? f[4 * qq] : x;
+        y = q == qq ? f[4 * qq + 1] : y;
+        z = q == qq ? f[4 * qq + 2] : z;
+        w = q == qq ? f[4 * qq + 3] : w;
+    }
+    hot[q] = make_float4(x, y, z, w);
+    if (ext && q == 0) *bbox = make_float4(r.fminx, r.fmaxx, r.fminy, r.fmaxy);
+}
+
 __device__ __forceinline__ int find_draw(const DrawGPU *draws, int n_draws, int gid) {
     int lo = 0, hi = n_draws - 1;
     while (lo < hi) {
@@ -677,7 +722,10 @@ __device__ __forceinline__ void quad_store_rec_at(TriRec *rec, const TriRec &r) 
     }
 }
 
-__device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, const TriRec &r) { quad_store_rec_at(&fb.recs[tri], r); }
+// The stored record (TriHot) and, for ghosts, the float bbox.
+__device__ __forceinline__ void quad_store_rec(const FrameBuffers &fb, int tri, const TriRec &r) {
+    quad_store_hot(reinterpret_cast<float4 *>(&fb.recs[tri]), &fb.rext[tri], r, (r.flags & TRI_GHOST) != 0u);
+}
 
 // Record, varyings and their stores for the quad's triangle; returns the flags and the bin box.
 // vary: this frame stores the varyings (false: RF_SHARED_VARY and not frame 0 -- frame 0's are read).
@@ -818,10 +866,11 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
             key[k] = (n_bt <= SMALL_BT && i < n_bt && (!sharded || owned_bin_tile(fp, bx, by))) ? by * fp.tiles_x + bx : -1;
         }
         wave_append<2>(tcount, key, pos);
+        const uint32_t entry = (uint32_t)tri | ((flags & TRI_GHOST) ? BIN_GHOST : 0u);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             if (key[k] >= 0) {
-                append_bin(fp, fb, cnt, frame, key[k], pos[k], (uint32_t)tri);
+                append_bin(fp, fb, cnt, frame, key[k], pos[k], entry);
                 ++n_bin;
                 if (pos[k] == 0u) mark_bin_rows(fp, fb, cnt, frame, key[k], nb);
             }
@@ -830,7 +879,7 @@ __device__ __forceinline__ void setup_block(const FrameParams &fp, const FrameBu
             const int src = __ffsll((unsigned long long)big) - 1;
             big &= big - 1;
             const int cx0 = __shfl(bx0, src), cx1 = __shfl(bx1, src), cy0 = __shfl(by0, src), cy1 = __shfl(by1, src);
-            const uint32_t id = (uint32_t)__shfl(tri, src);
+            const uint32_t id = (uint32_t)__shfl((int)entry, src);
             const int nx = cx1 - cx0 + 1, n = nx * (cy1 - cy0 + 1);
             uint32_t mine = 0;
             for (int k = lane; k < n; k += 64) {
@@ -962,11 +1011,15 @@ __global__ __launch_bounds__(256) void k_ghost(FrameParams fp, FrameBuffers fb_a
         e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
         const uint32_t frame = e / (uint32_t)fp.n_tris, tri = e - frame * (uint32_t)fp.n_tris;
         ConstF *src = (ConstF *)(fb_all.recs + (size_t)frame * fp.n_tris + tri);
-        TriRec r;
-        float *d = reinterpret_cast<float *>(&r);
+        ConstF *ext = (ConstF *)(fb_all.rext + (size_t)frame * fp.n_tris + tri);   // stored: a sliver is a ghost
+        float h[16], bb[4];
 #pragma unroll
-        for (int k = 0; k < (int)(sizeof(TriRec) / 4); ++k) d[k] = src[k];
-        return r;
+        for (int k = 0; k < 16; ++k) h[k] = src[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bb[k] = ext[k];
+        return rec_from_hot(fp, make_float4(h[0], h[1], h[2], h[3]), make_float4(h[4], h[5], h[6], h[7]),
+                            make_float4(h[8], h[9], h[10], h[11]), make_float4(h[12], h[13], h[14], h[15]),
+                            make_float4(bb[0], bb[1], bb[2], bb[3]));
     };
     for (int base = gw; base < n_items; base += 64 * waves) {   // wave-uniform
         const int mine = base + lane * waves;
@@ -1115,7 +1168,8 @@ __device__ __forceinline__ unsigned long long cand_key(float z, uint32_t id, boo
 }
 
 struct RasterShared {
-    float4 rec[RCHUNK * 6];           // staged triangle records (6 KB)
+    float4 rec[RCHUNK * 4];           // staged triangle records (TriHot, 4 KB)
+    float4 ext[RCHUNK];               // ... their float bboxes (ghosts; every candidate in scan mode, 1 KB)
     float4 srec[RCHUNK * 5];          // staged shading records (single-pass tiles, 5 KB)
     unsigned long long key[RTH * RTW];// per-pixel (z, index) keys (2 KB)
     unsigned long long bits[PAIR_WORDS]; // bit k: a staged candidate's pairs start at pair k (2 KB)
@@ -1165,7 +1219,7 @@ __device__ __forceinline__ TriRec rec_from_stored(const FrameParams &fp, int dra
 // setup_quad computes them (same functions, same operands: identical bits), into the LDS copies.
 // fdraws: the frame's draw slice (batch table entries dbase ..).
 __device__ __forceinline__ void stage_from_mesh(const FrameParams &fp, const FrameBuffers &fb, const DrawGPU *fdraws, int dbase,
-                                                uint32_t id, bool shade, float4 *rec, float4 *srec) {
+                                                uint32_t id, bool shade, float4 *rec, float4 *ext, float4 *srec) {
     const int q = __lane_id() & 3, qv = q < 3 ? q : 2;
     const uint32_t word = (uint32_t)fb.tdraw[id];
     const uint2 gbox = fb.boxes[id];
@@ -1185,7 +1239,7 @@ __device__ __forceinline__ void stage_from_mesh(const FrameParams &fp, const Fra
 #pragma unroll
     for (int k = 0; k < 3; ++k) { sx[k] = quad_bcast(vx, k); sy[k] = quad_bcast(vy, k); sz[k] = quad_bcast(vz, k); }
     const TriRec r = rec_from_stored(fp, d, local, sx, sy, sz, word >> 29, gbox);
-    quad_store_rec_at(reinterpret_cast<TriRec *>(rec), r);
+    quad_store_hot(rec, ext, r, true);
     if (shade) {
         f3 a, nr;
         corner_varyings(dr, p3, n3, a, nr);
@@ -1301,7 +1355,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             ids[k] = id;
         }
 #pragma unroll
-        for (int k = 0; k < CAND / 256; ++k) bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k]] : make_uint2(0u, 0u);
+        for (int k = 0; k < CAND / 256; ++k) bx[k] = ids[k] != 0xffffffffu ? fb.boxes[ids[k] & ~BIN_GHOST] : make_uint2(0u, 0u);
 #pragma unroll
         for (int k = 0; k < CAND / 256; ++k) {
             // non-empty bin box overlapping the tile (so its clipped box holds >= 1 pixel: the pair
@@ -1324,34 +1378,41 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             if (c > 0) __syncthreads();
             // stage records (single-pass tiles: the shading records too, so the resolve reads no HBM):
             // consecutive lanes load consecutive float4s of one record; all loads in one round trip
-            if (tid < m) sh.id[tid] = sh.cand[c + tid];
+            if (tid < m) sh.id[tid] = sh.cand[c + tid] & ~BIN_GHOST;
             for (int i = tid; i < m * (RTW * RTH / 64); i += 256) sh.bits[i] = 0ull;
             if constexpr (no_recs) {   // a quad of lanes per candidate (RCHUNK * 4 == 256)
                 const int ci = tid >> 2;
                 if (ci < m)
-                    stage_from_mesh(fp, fb, draws + dbase, dbase, sh.cand[c + ci], single, &sh.rec[ci * 6], &sh.srec[ci * 5]);
+                    stage_from_mesh(fp, fb, draws + dbase, dbase, sh.cand[c + ci] & ~BIN_GHOST, single, &sh.rec[ci * 4], &sh.ext[ci],
+                                    &sh.srec[ci * 5]);
             } else {
-                constexpr int NQ = (RCHUNK * 6 + 255) / 256, NS = (RCHUNK * 5 + 255) / 256;
-                float4 q[NQ], s[NS];
+                // (the float bbox only for ghosts -- tagged entries -- or every candidate in scan mode)
+                constexpr int NQ = (RCHUNK * 4 + 255) / 256, NS = (RCHUNK * 5 + 255) / 256;
+                float4 q[NQ], s[NS], e = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) {
                     const int f = tid + 256 * k;
-                    const int ci = f / 6;
-                    q[k] = f < 6 * m ? reinterpret_cast<const float4 *>(&fb.recs[sh.cand[c + min(ci, m - 1)]])[f - 6 * ci]
+                    const int ci = f >> 2;
+                    q[k] = f < 4 * m ? reinterpret_cast<const float4 *>(&fb.recs[sh.cand[c + min(ci, m - 1)] & ~BIN_GHOST])[f & 3]
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                {
+                    const uint32_t ce = tid < m ? sh.cand[c + tid] : 0u;
+                    if (tid < m && (scan || (ce & BIN_GHOST))) e = fb.rext[ce & ~BIN_GHOST];
                 }
 #pragma unroll
                 for (int k = 0; k < NS; ++k) {
                     const int f = tid + 256 * k;
                     const int ci = f / 5;
-                    s[k] = single && f < 5 * m ? reinterpret_cast<const float4 *>(&fb.shade[sh.cand[min(ci, m - 1)]])[f - 5 * ci]
+                    s[k] = single && f < 5 * m ? reinterpret_cast<const float4 *>(&fb.shade[sh.cand[min(ci, m - 1)] & ~BIN_GHOST])[f - 5 * ci]
                                                : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) {
                     const int f = tid + 256 * k;
-                    if (f < 6 * m) sh.rec[f] = q[k];
+                    if (f < 4 * m) sh.rec[f] = q[k];
                 }
+                if (tid < m) sh.ext[tid] = e;
 #pragma unroll
                 for (int k = 0; k < NS; ++k) {
                     const int f = tid + 256 * k;
@@ -1367,11 +1428,11 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                 const int px = X0 + (tid & 31), py = Y0 + (tid >> 5);
                 const int wy0 = Y0 + 2 * wave, wy1 = wy0 + 1;
                 for (int cc = 0; cc < m; ++cc) {
-                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[cc * 6])[4];   // ibx iby gbx gby
+                    const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[cc * 4])[3];   // z2 word gbx gby
                     const int x0 = lo16(bb.z), x1 = hi16(bb.z), y0 = lo16(bb.w), y1 = hi16(bb.w);
                     if (y1 < wy0 || y0 > wy1) continue;                                     // wave-uniform
                     if (px < x0 || px > x1 || py < y0 || py > y1) continue;
-                    const TriRec r = rec_from(&sh.rec[cc * 6]);
+                    const TriRec r = rec_from_hot(fp, &sh.rec[cc * 4], &sh.ext[cc]);
                     float z;
                     if (pixel_test(fp, r, px, py, z)) {
                         const unsigned long long k = cand_key(z, sh.id[cc], slot_keys, single ? (uint32_t)cc : SLOT_NONE);
@@ -1396,8 +1457,8 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                     uint32_t spw[2] = {0x1fu, 0x1fu};   // tile-relative x0 | x1 << 8; 0x1f: empty
                     uint32_t pk = 0u;                   // pairs << 11 | segments
                     if (ci < m) {
-                        const float4 *rc = &sh.rec[ci * 6];
-                        const uint4 bb = reinterpret_cast<const uint4 *>(rc)[4];   // ibx iby gbx gby
+                        const float4 *rc = &sh.rec[ci * 4];
+                        const uint4 bb = reinterpret_cast<const uint4 *>(rc)[3];   // z2 word gbx gby
                         const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
                         const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
                         if (x0 <= x1 && y0 <= y1) {
@@ -1456,7 +1517,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                         const uint32_t sgi = sh.seg[o];
                         const int cc = (int)(sgi >> 22);
                         const int px = X0 + (int)((sgi >> 14) & 31u) + (k - (int)(sgi & 0x3fffu)), py = Y0 + (int)((sgi >> 19) & 7u);
-                        const TriRec r = rec_from(&sh.rec[cc * 6]);
+                        const TriRec r = rec_from_hot(fp, &sh.rec[cc * 4], &sh.ext[cc]);
                         float z;
                         if (pixel_test(fp, r, px, py, z))
                             atomicMin(&sh.key[(py - Y0) * RTW + (px - X0)],
@@ -1474,7 +1535,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                 if (wave == 0) {
                     int area = 0, bx0 = 0, by0 = 0, bw = 1;
                     if (lane < m) {
-                        const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[lane * 6])[4];   // ibx iby gbx gby
+                        const uint4 bb = reinterpret_cast<const uint4 *>(&sh.rec[lane * 4])[3];   // z2 word gbx gby
                         const int x0 = max(lo16(bb.z), X0), x1 = min(hi16(bb.z), X1);
                         const int y0 = max(lo16(bb.w), Y0), y1 = min(hi16(bb.w), Y1);
                         if (x0 <= x1 && y0 <= y1) { area = (x1 - x0 + 1) * (y1 - y0 + 1); bx0 = x0; by0 = y0; bw = x1 - x0 + 1; }
@@ -1508,7 +1569,7 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                         const int local = k - (int)pi.x;
                         const int ly = (int)(((uint32_t)local * pi.w) >> 16), lx = local - ly * (int)pi.z;
                         const int px = (int)(pi.y & 0xffffu) + lx, py = (int)(pi.y >> 16) + ly;
-                        const TriRec r = rec_from(&sh.rec[o * 6]);
+                        const TriRec r = rec_from_hot(fp, &sh.rec[o * 4], &sh.ext[o]);
                         float z;
                         if (pixel_test(fp, r, px, py, z))
                             atomicMin(&sh.key[(py - Y0) * RTW + (px - X0)],
@@ -1547,21 +1608,22 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
             TriRec r;
             ShadeRec sr;
             {
-                float4 *d4 = reinterpret_cast<float4 *>(&r);
+                float4 h4[4];   // the winner's stored record (its float bbox is not read here)
                 float4 *e4 = reinterpret_cast<float4 *>(&sr);
                 if (slot != SLOT_NONE) {   // only single-pass tiles encode a slot: the staged copies
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) d4[k] = sh.rec[slot * 6 + k];
+                    for (int k = 0; k < 4; ++k) h4[k] = sh.rec[slot * 4 + k];
 #pragma unroll
                     for (int k = 0; k < 5; ++k) e4[k] = sh.srec[slot * 5 + k];
                 } else {
                     const float4 *s4 = reinterpret_cast<const float4 *>(&fb.recs[id]);
-                    const float4 *h4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
+                    const float4 *g4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) d4[k] = s4[k];
+                    for (int k = 0; k < 4; ++k) h4[k] = s4[k];
 #pragma unroll
-                    for (int k = 0; k < 5; ++k) e4[k] = h4[k];
+                    for (int k = 0; k < 5; ++k) e4[k] = g4[k];
                 }
+                r = rec_from_hot(fp, h4[0], h4[1], h4[2], h4[3], make_float4(0.f, 0.f, 0.f, 0.f));
             }
             float u, v, w;
             bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values
@@ -1586,21 +1648,22 @@ __device__ __forceinline__ void raster_tile(const FrameParams &fp, const FrameBu
                 TriRec r;
                 ShadeRec sr;
                 {
-                    float4 *d4 = reinterpret_cast<float4 *>(&r);
+                    float4 h4[4];   // the winner's stored record (its float bbox is not read here)
                     float4 *e4 = reinterpret_cast<float4 *>(&sr);
                     if (slot != SLOT_NONE) {   // only single-pass tiles encode a slot: the staged copies
     #pragma unroll
-                        for (int k = 0; k < 6; ++k) d4[k] = sh.rec[slot * 6 + k];
+                        for (int k = 0; k < 4; ++k) h4[k] = sh.rec[slot * 4 + k];
     #pragma unroll
                         for (int k = 0; k < 5; ++k) e4[k] = sh.srec[slot * 5 + k];
                     } else {
                         const float4 *s4 = reinterpret_cast<const float4 *>(&fb.recs[id]);
-                        const float4 *h4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
+                        const float4 *g4 = reinterpret_cast<const float4 *>(&fb.shade[id]);
     #pragma unroll
-                        for (int k = 0; k < 6; ++k) d4[k] = s4[k];
+                        for (int k = 0; k < 4; ++k) h4[k] = s4[k];
     #pragma unroll
-                        for (int k = 0; k < 5; ++k) e4[k] = h4[k];
+                        for (int k = 0; k < 5; ++k) e4[k] = g4[k];
                     }
+                    r = rec_from_hot(fp, h4[0], h4[1], h4[2], h4[3], make_float4(0.f, 0.f, 0.f, 0.f));
                 }
                 float u, v, w;
                 bary_pass(r, (float)px + 0.5f, (float)py + 0.5f, u, v, w);   // the winner's own values

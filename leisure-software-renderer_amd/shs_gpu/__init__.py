@@ -236,11 +236,11 @@ class Context:
         k = max(n.value, 1)
         return n.value, {"setup": s[0] / k, "raster": s[3] / k}
 
+    # shs_dev::TriHot (64 B): word = draw | flags << 29
     TRIREC_DTYPE = np.dtype([
         ("ax", "<f4"), ("ay", "<f4"), ("v0x", "<f4"), ("v0y", "<f4"), ("v1x", "<f4"), ("v1y", "<f4"),
         ("d00", "<f4"), ("d01", "<f4"), ("d11", "<f4"), ("denom", "<f4"), ("z0", "<f4"), ("z1", "<f4"),
-        ("z2", "<f4"), ("flags", "<u4"), ("draw", "<i4"), ("local", "<i4"), ("ibx", "<u4"), ("iby", "<u4"),
-        ("gbx", "<u4"), ("gby", "<u4"), ("fminx", "<f4"), ("fmaxx", "<f4"), ("fminy", "<f4"), ("fmaxy", "<f4")])
+        ("z2", "<f4"), ("word", "<u4"), ("gbx", "<u4"), ("gby", "<u4")])
 
     def debug_records(self):
         """The last frame's per-triangle raster records (structured numpy array)."""
