@@ -179,7 +179,8 @@ int shs_debug_records(shs_ctx *ctx, void *out, int64_t capacity, int64_t *n_out)
  * build per-tile bins), 1 force scan, 2 force bins.  Results are identical in every mode. */
 #define SHS_OPT_RASTER_MODE 2
 /* SHS_OPT_TIMELINE: 1 = record every workgroup's start / end time (s_memrealtime, 100 MHz) of the
- * frames that follow (profiling aid; read with shs_debug_timeline), 0 = off. */
+ * frames that follow (profiling aid; read with shs_debug_timeline / shs_lib_debug_timeline), 2 = the
+ * same, with the library's shadow-pass raster recorded instead of the camera pass's, 0 = off. */
 #define SHS_OPT_TIMELINE 3
 /* SHS_OPT_RASTER_LOOP: 1 = (candidate, pixel) pair tasks dealt over the waves (default), 0 = each
  * thread loops over the tile's candidates for its own pixel.  Results are identical in both. */
@@ -250,7 +251,7 @@ int shs_shard_balance_rects(const uint32_t *blocks, int32_t n_blocks, int32_t wi
  * order), then S slots per k_setup workgroup followed by S per k_raster workgroup: start, end, and
  * phase marks of the workgroup's thread 0 (0 where a phase did not run). */
 int shs_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out);
-/* Debug / profiling hook: the last camera pass's k_lib_raster workgroup timeline (SHS_OPT_TIMELINE),
+/* Debug / profiling hook: the last camera pass's (SHS_OPT_TIMELINE 2: shadow pass's) k_lib_raster workgroup timeline,
  * 16 uint64 per workgroup: start, end, summed ticks of gather / stage + pairs / resolve + shade over
  * its busy tiles, clear ticks, busy tiles, cleared tiles, staging passes, pairs, candidates, longest
  * busy tile, and (deep camera raster) the staging passes' selection + record + span ticks and segment

@@ -837,8 +837,9 @@ int shs_set_option(shs_ctx *ctx, int option, int64_t value) {
         return SHS_OK;
     }
     if (option == SHS_OPT_TIMELINE) {
-        if (value < 0 || value > 1) return SHS_ERR_INVALID;
+        if (value < 0 || value > 2) return SHS_ERR_INVALID;
         ctx->want_timeline = value != 0;
+        ctx->timeline_shadow = value == 2;
         return SHS_OK;
     }
     if (option == SHS_OPT_SHARD_CULL) {

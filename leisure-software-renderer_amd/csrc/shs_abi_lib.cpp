@@ -482,6 +482,12 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
     }
     if (shadow) {
         fb.depth = ctx->shadow_map.p;
+        if (ctx->want_timeline && ctx->timeline_shadow) {   // (profiling: the shadow raster's workgroups)
+            const size_t n = (size_t)raster_grid * shs_dev::LTL_STRIDE;
+            if (ensure(ctx, ctx->lib_timeline, n)) return SHS_ERR_HIP;
+            HIP_TRY(ctx, hipMemsetAsync(ctx->lib_timeline.p, 0, n * sizeof(uint64_t), ps));
+            fb.timeline = ctx->lib_timeline.p;
+        }
     } else {
         fb.hdr = ctx->lib_hdr.p; fb.depth = ctx->lib_depth.p; fb.motion = ctx->lib_motion.p;
         fb.keys = ctx->lib_keys.p;
@@ -512,7 +518,7 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         fb.lights = ctx->lights.p;
         fb.tile_counts = ctx->list_counts.p;
         fb.tile_indices = ctx->list_indices.p;
-        if (ctx->want_timeline) {
+        if (ctx->want_timeline && !ctx->timeline_shadow) {
             const size_t n = (size_t)raster_grid * shs_dev::LTL_STRIDE;
             if (ensure(ctx, ctx->lib_timeline, n)) return SHS_ERR_HIP;
             HIP_TRY(ctx, hipMemsetAsync(ctx->lib_timeline.p, 0, n * sizeof(uint64_t), ps));
@@ -1227,11 +1233,12 @@ int shs_lib_debug_setup_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, 
 
 int shs_lib_debug_timeline(shs_ctx *ctx, uint64_t *out, int64_t capacity, int64_t *n_out) {
     if (!ctx || !n_out) return SHS_ERR_INVALID;
-    if (!ctx->want_timeline || !ctx->lib_timeline.p || ctx->lib_cam.last_raster_grid <= 0) {
-        ctx->err = "timeline not enabled or no camera pass yet";
+    const Work &tw = ctx->timeline_shadow ? ctx->lib_shadow : ctx->lib_cam;
+    if (!ctx->want_timeline || !ctx->lib_timeline.p || tw.last_raster_grid <= 0) {
+        ctx->err = "timeline not enabled or no such pass yet";
         return SHS_ERR_INVALID;
     }
-    const int64_t n = (int64_t)ctx->lib_cam.last_raster_grid * shs_dev::LTL_STRIDE;
+    const int64_t n = (int64_t)tw.last_raster_grid * shs_dev::LTL_STRIDE;
     *n_out = n;
     if (!out) return SHS_OK;
     if (capacity < n) { ctx->err = "capacity too small"; return SHS_ERR_INVALID; }

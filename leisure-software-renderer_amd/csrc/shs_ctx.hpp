@@ -104,6 +104,7 @@ struct shs_ctx {
     bool last_no_recs = false;       // the last legacy batch was binned without stored records (RF_NO_RECS)
     DevBuf<uint64_t> timeline;       // SHS_OPT_TIMELINE
     bool want_timeline = false;
+    bool timeline_shadow = false;    // SHS_OPT_TIMELINE 2: the library's shadow raster records it instead
     int last_setup_grid = 0, last_ghost_blocks = 0, last_clear_blocks = 0;
     std::vector<uint4> h_blk_stat;
     std::vector<uint2> h_rstat;

@@ -258,8 +258,10 @@ class Context:
         """Legacy raster inner loop: 1 (candidate, pixel) pair tasks (default), 0 per-pixel candidate loop."""
         self._check(self._lib.shs_set_option(self._h, _abi.OPT_RASTER_LOOP, int(loop)))
 
-    def set_timeline(self, enable: bool):
-        self._check(self._lib.shs_set_option(self._h, _abi.OPT_TIMELINE, 1 if enable else 0))
+    def set_timeline(self, enable: bool, shadow: bool = False):
+        """Workgroup timelines of the frames that follow; shadow: the library shadow pass's raster
+        (lib_debug_timeline) instead of the camera pass's."""
+        self._check(self._lib.shs_set_option(self._h, _abi.OPT_TIMELINE, (2 if shadow else 1) if enable else 0))
 
     # -- after the path: PassTonemap + present staging ------------------------------------------
     def tonemap(self, exposure: float = 1.0, gamma: float = 2.2, ldr: bool = True, present: bool = True):
