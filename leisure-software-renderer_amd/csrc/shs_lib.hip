@@ -506,16 +506,9 @@ __device__ __forceinline__ void emit_fan(const LibFrameParams &fp, const LibBuff
     }
     s.draw = d;
     s.pad = 0;
-    // non-temporal: only the resolve reads the varyings, after the raster, when a C4 frame's 80 MB of them
-    // are long out of L2; streamed past it they leave the L2 to the other frames' raster and resolve in
-    // flight (C4 0.580 -> 0.574 ms per frame in three A/B pairs, profiles/r06_shade_nt_ab.txt)
-    if (!SHS_LIB_EXP(fp, 1u)) {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        const v4f *s4 = reinterpret_cast<const v4f *>(&s);
-        v4f *d4 = reinterpret_cast<v4f *>(&fb.shade[slot]);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) __builtin_nontemporal_store(s4[k], &d4[k]);
-    }
+    // (plain stores: non-temporal 16-B stores measured 0.7 % faster per C4 frame but wrote every 80-B
+    // record as partial sectors, 207 -> 303 MB per frame; profiles/r06_shade_nt_ab.txt)
+    if (!SHS_LIB_EXP(fp, 1u)) fb.shade[slot] = s;
     if (dr.tex) {   // UV0 varying * 1/w (varw, rasterizer.hpp:319-326)
         fb.uvw[2 * (size_t)slot] = make_float4(a.u * iw0, a.v * iw0, b.u * iw1, b.v * iw1);
         fb.uvw[2 * (size_t)slot + 1] = make_float4(c.u * iw2, c.v * iw2, 0.0f, 0.0f);
