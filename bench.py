@@ -366,9 +366,17 @@ def lib_timed_loop(args, slots, frame_fn, dist, frame=None, rank=0, world=1, on_
     owned = None
     if frame is not None:
         owned = rank_owned_pixels(ctx, frame, rank, world, dist is not None and args.shard_layout == "regions")
-    for sl in slots:
+    for sl in reversed(slots):   # borrowers first: slots 1.. read slot 0's meshes (shs_mesh_share)
         sl.ctx.close()
     return elapsed, stats, (n_passes["camera"], kms), owned
+
+
+def share_meshes(args, sl, slots, meshes):
+    """Frames in flight read one device copy of each mesh: every slot after the first borrows the first
+    slot's buffers (shs_mesh_share) instead of uploading its own (--copy-meshes: one copy per slot)."""
+    if slots and not args.copy_meshes:
+        for m in meshes:
+            sl.ctx.share_lib_mesh(slots[0].ctx, m)
 
 
 def run_gpu_c4(args, rank, local_rank, world, dist):
@@ -385,6 +393,7 @@ def run_gpu_c4(args, rank, local_rank, world, dist):
     slots = []
     for _ in range(args.inflight):
         sl = LibSlot(local_rank, dist, args)
+        share_meshes(args, sl, slots, [d.mesh for d in draws])
         sl.ctx.upload_lights(lights)
         sl.ctx.light_cull(cull)
         sl.prepared = sl.ctx.prepare_lib(frame, draws)
@@ -428,6 +437,7 @@ def run_gpu_lib(args, rank, local_rank, world, dist):
     slots = []
     for _ in range(args.inflight):
         sl = LibSlot(local_rank, dist, args)
+        share_meshes(args, sl, slots, [d.mesh for d in draws] + [c.mesh for c in casters])
         ctx = sl.ctx
         # SHS_OPT_SHADOW_FOOTPRINT: the camera pass enqueues the shadow pass over only the shadow-map tiles
         # its pixels' PCF reads (every N alike; the images are the oracle's either way)
@@ -788,6 +798,8 @@ def main():
                     help="legacy configs: frames per shs_render_legacy_batch step (default 128 for c1/c2, 16 for c3; C2 measured 64 / 128 / 256: 230 / 248 / 255 Mtri/s, DESIGN.md 6)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="c4/c5: frames in flight (contexts rendering consecutive frames round-robin)")
+    ap.add_argument("--copy-meshes", action="store_true",
+                    help="c4/c5: every frame-in-flight context uploads its own mesh copies (default: one copy, shared)")
     ap.add_argument("--shard-layout", default="regions", choices=["regions", "interleaved"],
                     help="c4/c5 at N > 1: tile ownership (one cost-balanced rectangle per rank, or tile %% N)")
     ap.add_argument("--root-share", type=float, default=0.85,

@@ -99,6 +99,11 @@ int shs_synchronize(shs_ctx *ctx);
 int shs_mesh_upload_soup(shs_ctx *ctx, const float *positions, const float *normals, int32_t n_tris,
                          int32_t *mesh_id);
 int shs_mesh_release(shs_ctx *ctx, int32_t mesh_id);
+/* A handle in dst to src's uploaded mesh (legacy soup or library MeshData), on the same device, without
+ * a copy: frames in flight on several contexts read one device copy of each mesh.  The buffers stay
+ * src's: src must not release the mesh, nor be destroyed, while dst may still read it; releasing the
+ * shared handle in dst (or destroying dst) frees nothing. */
+int shs_mesh_share(shs_ctx *dst, shs_ctx *src, int32_t src_mesh_id, int32_t *mesh_id);
 
 /* ---- the hot path (Seam 1) --------------------------------------------------------------- */
 /* Clears the frame (Canvas::fill_pixel + ZBuffer::clear) and rasterises all draws in order,

@@ -78,6 +78,7 @@ int shs_destroy(shs_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->setup_stream) (void)hipStreamSynchronize(ctx->setup_stream);
     for (auto &m : ctx->meshes) {
+        if (m.borrowed) continue;   // the owning context frees them
         if (m.pos) (void)hipFree(m.pos);
         if (m.nrm) (void)hipFree(m.nrm);
         if (m.uv) (void)hipFree(m.uv);
@@ -152,6 +153,10 @@ int shs_mesh_release(shs_ctx *ctx, int32_t id) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->setup_stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     Mesh &m = ctx->meshes[id];
+    if (m.borrowed) {   // shs_mesh_share: this context's reads are done; the owner keeps the buffers
+        m = Mesh{};
+        return SHS_OK;
+    }
     HIP_TRY(ctx, hipFree(m.pos));
     HIP_TRY(ctx, hipFree(m.nrm));
     if (m.uv) HIP_TRY(ctx, hipFree(m.uv));
@@ -159,6 +164,16 @@ int shs_mesh_release(shs_ctx *ctx, int32_t id) {
     if (m.orig) HIP_TRY(ctx, hipFree(m.orig));
     if (m.cbox) HIP_TRY(ctx, hipFree(m.cbox));
     m = Mesh{};
+    return SHS_OK;
+}
+
+int shs_mesh_share(shs_ctx *dst, shs_ctx *src, int32_t src_mesh_id, int32_t *mesh_id) {
+    if (!dst || !src || !mesh_id || dst == src || dst->device != src->device) return SHS_ERR_INVALID;
+    if (src_mesh_id < 0 || src_mesh_id >= (int32_t)src->meshes.size() || !src->meshes[src_mesh_id].live) return SHS_ERR_INVALID;
+    Mesh m = src->meshes[src_mesh_id];   // (its upload copied synchronously: the buffers are complete)
+    m.borrowed = true;
+    dst->meshes.push_back(m);
+    *mesh_id = (int32_t)dst->meshes.size() - 1;
     return SHS_OK;
 }
 

@@ -41,6 +41,7 @@ struct Mesh {
     float bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
     float4 *cbox = nullptr;          // library mesh: per 256-triangle chunk its model-space box (min, max)
     uint32_t *orig = nullptr;        // library mesh stored in spatial order: per stored triangle its MeshData index
+    bool borrowed = false;           // shs_mesh_share: another context's buffers (never freed here)
 };
 
 // A Texture2DData (resources/texture.hpp:23-49) on the device: w * h Color texels, y * w + x.

@@ -606,6 +606,19 @@ class Context:
         self._check(self._lib.shs_set_stream(self._h, ctypes.c_void_p(hip_stream)))
 
     # -- library path (rasterize_mesh / PassShadowMap / PassPBRForward) ---------------------------
+    def share_lib_mesh(self, src, mesh) -> int:
+        """A handle to src's device copy of library mesh `mesh` (uploaded there if it is not yet), so
+        that later draws of `mesh` on this context read src's buffers (shs_mesh_share: frames in flight
+        on several contexts keep one copy).  src must outlive this context's use of it."""
+        key = ("lib", id(mesh))
+        if key in self._meshes:
+            return self._meshes[key][0]
+        sid = src.upload_lib_mesh(mesh)
+        mid = ctypes.c_int32()
+        self._check(self._lib.shs_mesh_share(self._h, src._h, sid, ctypes.byref(mid)))
+        self._meshes[key] = (mid.value, mesh)
+        return mid.value
+
     def upload_lib_mesh(self, mesh) -> int:
         key = ("lib", id(mesh))
         if key in self._meshes:

@@ -224,6 +224,7 @@ SIGNATURES = [
     ("shs_get_stream", _P, [_P]),
     ("shs_synchronize", ctypes.c_int, [_P]),
     ("shs_mesh_upload_soup", ctypes.c_int, [_P, _F, _F, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    ("shs_mesh_share", ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
     ("shs_mesh_release", ctypes.c_int, [_P, ctypes.c_int32]),
     ("shs_render_legacy", ctypes.c_int, [_P, ctypes.POINTER(FrameDesc), ctypes.POINTER(LegacyDraw), ctypes.c_int32]),
     ("shs_render_legacy_batch", ctypes.c_int, [_P, ctypes.POINTER(FrameDesc), ctypes.POINTER(LegacyDraw), ctypes.c_int32,
