@@ -2751,9 +2751,11 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
 #define SHS_RESOLVE_WAVES_FP 4
 #endif
 #ifndef SHS_RESOLVE_WAVES_PBR
-#define SHS_RESOLVE_WAVES_PBR 4
+#define SHS_RESOLVE_WAVES_PBR 5
 #endif
-// Minimum waves per SIMD: 4 for the single-program kernels (no spills), 3 for the mixed one
+// Minimum waves per SIMD: 4 for the Forward+ kernel (no spills; 5 measured +2.3 % per C4 frame), 5 for
+// the PBR one (96 VGPRs with 24 spilled, and still C5 0.350 -> 0.341 ms per frame in three A/B pairs, the
+// 8-way split unchanged: profiles/r06_resolve_waves_ab.txt), 3 for the mixed one
 // (-DSHS_RESOLVE_WAVES_FP / _PBR override: timing experiments).
 template <int PROG>
 __global__ __launch_bounds__(256, PROG == 5 ? SHS_RESOLVE_WAVES_FP : PROG == 0 ? SHS_RESOLVE_WAVES_PBR : 3)
