@@ -826,12 +826,15 @@ __device__ __forceinline__ void setup_prologue(const LibFrameParams &fp, const L
     __syncthreads();
 }
 
-// SHS_SETUP_WAVES (timing experiments): a minimum waves-per-SIMD bound for k_lib_setup.
-#ifdef SHS_SETUP_WAVES
-#define SHS_SETUP_BOUNDS __launch_bounds__(256, SHS_SETUP_WAVES)
-#else
-#define SHS_SETUP_BOUNDS __launch_bounds__(256)
+// A minimum of six waves per SIMD for k_lib_setup (80 VGPRs, 8 spilled in the camera instance): C4
+// 0.569 -> 0.563 ms per frame, C5 -0.5 %, the 8-way C4 split's worst rank -0.5 %, where eight waves (64
+// VGPRs, 71 spilled) were 4 % slower (profiles/r06_resolve_waves_ab.txt).  The tile-sharded (LISTED)
+// instance keeps the compiler's choice: at six waves it would spill 153 VGPRs.  SHS_SETUP_WAVES
+// (timing experiments) overrides the bound.
+#ifndef SHS_SETUP_WAVES
+#define SHS_SETUP_WAVES 6
 #endif
+#define SHS_SETUP_BOUNDS __launch_bounds__(256, LISTED ? 1 : SHS_SETUP_WAVES)
 // Tile-sharded camera pass (LISTED): a setup workgroup first reads the positions of CULL_PER x 256
 // consecutive input triangles and keeps in LDS those k_lib_setup would not drop -- a trivially inside
 // triangle whose fan_screen is live (on screen, not culled, on one of this rank's tiles), a triangle
