@@ -1130,7 +1130,12 @@ __global__ SHS_SETUP_BOUNDS void k_lib_setup(LibFrameParams fp, LibBuffers fb) {
 // the 6 planes and the fans (rasterizer.hpp:241-328), one 16-lane group per triangle striding the
 // queue, the fans emitted in parallel (lane k: fan k).  Same slots, submission order (tri * 16 + fan),
 // marks and counters as the reference's per-triangle clip.
-__global__ __launch_bounds__(256) void k_lib_clip(LibFrameParams fp, LibBuffers fb) {
+// six waves per SIMD (80 VGPRs, 19 spilled, instead of 103 at four): C4 0.564 -> 0.561, C5 0.340 -> 0.337 ms
+// per frame in two A/B pairs (profiles/r06_resolve_waves_ab.txt); SHS_CLIP_WAVES overrides (experiments)
+#ifndef SHS_CLIP_WAVES
+#define SHS_CLIP_WAVES 6
+#endif
+__global__ __launch_bounds__(256, SHS_CLIP_WAVES) void k_lib_clip(LibFrameParams fp, LibBuffers fb) {
     __shared__ SetupShared ss_unused;   // emit_fan<true> marks directly
     const int lane = __lane_id(), li = lane & (CLIP_G - 1), seg = lane & ~(CLIP_G - 1);
     uint32_t *cnt = fb.counters + fp.parity * LC_N;
