@@ -2761,12 +2761,13 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
 #ifndef SHS_RESOLVE_WAVES_PBR
 #define SHS_RESOLVE_WAVES_PBR 5
 #endif
-// Minimum waves per SIMD: 4 for the Forward+ kernel (no spills; 5 measured +2.3 % per C4 frame), 5 for
-// the PBR one (96 VGPRs with 24 spilled, and still C5 0.350 -> 0.341 ms per frame in three A/B pairs, the
-// 8-way split unchanged: profiles/r06_resolve_waves_ab.txt), 3 for the mixed one
-// (-DSHS_RESOLVE_WAVES_FP / _PBR override: timing experiments).
-template <int PROG>
-__global__ __launch_bounds__(256, PROG == 5 ? SHS_RESOLVE_WAVES_FP : PROG == 0 ? SHS_RESOLVE_WAVES_PBR : 3)
+// Minimum waves per SIMD: 4 for the Forward+ kernel (no spills; 5 measured +2.3 % per C4 frame), 3 for
+// the mixed one, and for the PBR one two builds: WIDE at 5 waves (96 VGPRs with 24 spilled) for a whole
+// frame's pass -- C5 0.350 -> 0.341 ms per frame in three A/B pairs -- and 4 waves (no spills) for a
+// sharded rank's, where the 5-wave build measured +4 % per rank frame at 8 ranks
+// (profiles/r06_resolve_waves_ab.txt).  (-DSHS_RESOLVE_WAVES_FP / _PBR override: timing experiments.)
+template <int PROG, bool WIDE = false>
+__global__ __launch_bounds__(256, PROG == 5 ? SHS_RESOLVE_WAVES_FP : PROG == 0 ? (WIDE ? SHS_RESOLVE_WAVES_PBR : 4) : 3)
 void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
     __shared__ float tm_thr[256];
     __shared__ uint32_t wlist[PROG == 0 ? 1 : 4][128];   // per wave: its block's light list (LtWave)
@@ -2898,19 +2899,20 @@ int lib_raster_resident_blocks(int device, bool shadow, bool shallow) {
 }
 
 // k_lib_resolve per program class: 5 (Forward+ only), 0 (PBR metallic-roughness only), -1 (any mix)
-#define SHS_RESOLVE_KERNEL(prog) (prog == 5 ? k_lib_resolve<5> : prog == 0 ? k_lib_resolve<0> : k_lib_resolve<-1>)
+#define SHS_RESOLVE_KERNEL(prog, wide) \
+    (prog == 5 ? k_lib_resolve<5> : prog == 0 ? ((wide) ? k_lib_resolve<0, true> : k_lib_resolve<0>) : k_lib_resolve<-1>)
 
-int lib_resolve_resident_blocks(int device, int prog) {
+int lib_resolve_resident_blocks(int device, int prog, bool wide) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, SHS_RESOLVE_KERNEL(prog), 256, 0) != hipSuccess || per_cu <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, SHS_RESOLVE_KERNEL(prog, wide), 256, 0) != hipSuccess || per_cu <= 0)
         per_cu = 2;
     (void)hipGetLastError();
     return cus * per_cu;
 }
 
-hipError_t launch_lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, int prog, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(SHS_RESOLVE_KERNEL(prog), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
+hipError_t launch_lib_resolve(const LibFrameParams &fp, const LibBuffers &fb, int prog, bool wide, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(SHS_RESOLVE_KERNEL(prog, wide), dim3(std::max(grid, 1)), dim3(256), 0, s, fp, fb);
     return hipGetLastError();
 }
 
