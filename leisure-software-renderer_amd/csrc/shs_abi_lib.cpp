@@ -564,8 +564,8 @@ int enqueue_pass(shs_ctx *ctx, Work &w, bool shadow) {
         for (const auto &d : w.last_draws)
             if (d.program != prog) prog = -1;
         if (prog != 5 && prog != 0) prog = -1;
-        const bool wide = prog == 0 && fp.count <= 1;   // the 5-wave PBR build for a whole frame only
-        int &res = ctx->lib_resolve_resident[prog == 5 ? 0 : prog == 0 ? (wide ? 1 : 3) : 2];
+        const bool wide = fp.count <= 1;   // the whole frame's build (PBR: 5 waves) or a sharded rank's
+        int &res = ctx->lib_resolve_resident[(prog == 5 ? 0 : prog == 0 ? 1 : 2) * 2 + wide];
         if (res <= 0) res = shs_internal::lib_resolve_resident_blocks(ctx->device, prog, wide);
         const int rgrid = std::max(1, std::min(fp.n_owned_rt, res));
         HIP_TRY(ctx, shs_internal::launch_lib_resolve(fp, fb, prog, wide, rgrid, ctx->stream));

@@ -252,8 +252,8 @@ struct shs_ctx {
     const uint32_t *blkcov_zero_at = nullptr;
     size_t blkcov_zero_cap = 0;
     uint64_t blkcov_zero_key = 0;
-    int lib_resolve_resident[4] = {0, 0, 0, 0};   // resident k_lib_resolve workgroups (Forward+, PBR, mixed,
-                                                  // PBR of a sharded frame)
+    int lib_resolve_resident[6] = {};   // resident k_lib_resolve workgroups ((Forward+, PBR, mixed) x (sharded
+                                        // rank's build, whole frame's build))
     DevBuf<float> srgb_lut;               // srgb_to_linear_rgb table (texture sampling)
     DevBuf<float> lib_depth;
     DevBuf<float2> lib_motion;

@@ -2761,13 +2761,21 @@ __global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_l
 #ifndef SHS_RESOLVE_WAVES_PBR
 #define SHS_RESOLVE_WAVES_PBR 5
 #endif
+#ifndef SHS_RESOLVE_WAVES_FP_SHARD
+#define SHS_RESOLVE_WAVES_FP_SHARD SHS_RESOLVE_WAVES_FP
+#endif
+#ifndef SHS_RESOLVE_WAVES_PBR_SHARD
+#define SHS_RESOLVE_WAVES_PBR_SHARD 3
+#endif
 // Minimum waves per SIMD: 4 for the Forward+ kernel (no spills; 5 measured +2.3 % per C4 frame), 3 for
 // the mixed one, and for the PBR one two builds: WIDE at 5 waves (96 VGPRs with 24 spilled) for a whole
-// frame's pass -- C5 0.350 -> 0.341 ms per frame in three A/B pairs -- and 4 waves (no spills) for a
-// sharded rank's, where the 5-wave build measured +4 % per rank frame at 8 ranks
-// (profiles/r06_resolve_waves_ab.txt).  (-DSHS_RESOLVE_WAVES_FP / _PBR override: timing experiments.)
+// frame's pass -- C5 0.350 -> 0.341 ms per frame in three A/B pairs -- and 3 waves (no spills) for a
+// sharded rank's, where the 5-wave build measured +4 % per rank frame at 8 ranks and the 3-wave one -4 %
+// against 4 waves (profiles/r06_resolve_waves_ab.txt).  (-DSHS_RESOLVE_WAVES_FP / _PBR / _FP_SHARD / _PBR_SHARD override:
+// timing experiments; the Forward+ kernel has one build unless _FP_SHARD differs.)
 template <int PROG, bool WIDE = false>
-__global__ __launch_bounds__(256, PROG == 5 ? SHS_RESOLVE_WAVES_FP : PROG == 0 ? (WIDE ? SHS_RESOLVE_WAVES_PBR : 4) : 3)
+__global__ __launch_bounds__(256, PROG == 5 ? (WIDE ? SHS_RESOLVE_WAVES_FP : SHS_RESOLVE_WAVES_FP_SHARD)
+                                  : PROG == 0 ? (WIDE ? SHS_RESOLVE_WAVES_PBR : SHS_RESOLVE_WAVES_PBR_SHARD) : 3)
 void k_lib_resolve(LibFrameParams fp, LibBuffers fb) {
     __shared__ float tm_thr[256];
     __shared__ uint32_t wlist[PROG == 0 ? 1 : 4][128];   // per wave: its block's light list (LtWave)
@@ -2899,8 +2907,13 @@ int lib_raster_resident_blocks(int device, bool shadow, bool shallow) {
 }
 
 // k_lib_resolve per program class: 5 (Forward+ only), 0 (PBR metallic-roughness only), -1 (any mix)
+#if SHS_RESOLVE_WAVES_FP_SHARD != SHS_RESOLVE_WAVES_FP
+#define SHS_RESOLVE_FP(wide) ((wide) ? k_lib_resolve<5, true> : k_lib_resolve<5>)
+#else
+#define SHS_RESOLVE_FP(wide) k_lib_resolve<5, true>
+#endif
 #define SHS_RESOLVE_KERNEL(prog, wide) \
-    (prog == 5 ? k_lib_resolve<5> : prog == 0 ? ((wide) ? k_lib_resolve<0, true> : k_lib_resolve<0>) : k_lib_resolve<-1>)
+    (prog == 5 ? SHS_RESOLVE_FP(wide) : prog == 0 ? ((wide) ? k_lib_resolve<0, true> : k_lib_resolve<0>) : k_lib_resolve<-1>)
 
 int lib_resolve_resident_blocks(int device, int prog, bool wide) {
     int cus = 0, per_cu = 0;

@@ -17,7 +17,7 @@ hipError_t launch_lib_raster(const shs_dev::LibFrameParams &fp, const shs_dev::L
                              int grid, hipStream_t s);
 // The camera pass's shading: every owned pixel's winner (fb.keys) shaded into hdr / depth / motion.
 // prog: the program every draw of the pass runs (5 Forward+, 0 PBR: specialised kernels) or -1.
-// CUs x occupancy of k_lib_resolve<prog> (wide: the 5-wave PBR build of an unsharded frame)
+// CUs x occupancy of k_lib_resolve<prog> (wide: the whole frame's build, else a sharded rank's)
 int lib_resolve_resident_blocks(int device, int prog, bool wide);
 hipError_t launch_lib_resolve(const shs_dev::LibFrameParams &fp, const shs_dev::LibBuffers &fb, int prog, bool wide,
                               int grid, hipStream_t s);
