@@ -387,6 +387,14 @@ int shs_get_shadow_region(shs_ctx *ctx, int32_t rect[4]);
 int shs_shadow_footprint(const float light_viewproj[16], int32_t sm_w, int32_t sm_h, const float camera_viewproj[16],
                          int32_t width, int32_t height, const int32_t px_rect[4], const float world_min[3],
                          const float world_max[3], int32_t reach, int32_t texel_rect[4]);
+/* Host-only, for tests: the same footprint per row of row_h texels (row r: texel rows r * row_h ..
+ * r * row_h + row_h - 1, r < n_rows) -- the texel columns [x0[r], x1[r]] (x1[r] < x0[r]: none) read there,
+ * from the convex hull of the footprint polytope's light-space image (round 6: a footprint shadow pass
+ * renders only these 32-texel rows' spans of its rectangle). */
+int shs_shadow_footprint_rows(const float light_viewproj[16], int32_t sm_w, int32_t sm_h, const float camera_viewproj[16],
+                              int32_t width, int32_t height, const int32_t px_rect[4], const float world_min[3],
+                              const float world_max[3], int32_t reach, int32_t row_h, int32_t n_rows, int32_t *x0,
+                              int32_t *x1);
 
 /* ---- Forward+ light-list binning ---------------------------------------
  * CullingLightGPU (lighting/light_types.hpp:141-166), the std430 record the reference uploads for

@@ -965,17 +965,23 @@ int shs_render_shadow_map(shs_ctx *ctx, int32_t w, int32_t h, const float sun_di
     }
     ctx->shadow_pending = false;
     ctx->shadow_reg = shs_dev::ShardRegion{0, 0, 0, 0, 0};
+    ctx->shadow_span.clear();
     return enqueue_pass(ctx, wk, true);
 }
 
-// Enqueue the recorded shadow pass over the bin tiles of `reg` (reg.on = 0: the whole map).
-static int enqueue_shadow(shs_ctx *ctx, const shs_dev::ShardRegion &reg) {
+// Enqueue the recorded shadow pass over the bin tiles of `reg` (reg.on = 0: the whole map), within it
+// only the row spans `span` (per bin-tile row, x0 | x1 << 16; empty: the whole rectangle).
+static int enqueue_shadow(shs_ctx *ctx, const shs_dev::ShardRegion &reg, const std::vector<uint32_t> &span = {}) {
     Work &wk = ctx->lib_shadow;
     wk.last_fp.reg = reg;
     wk.last_fp.rank = 0;
     wk.last_fp.count = reg.on ? 2 : 1;   // a region pass: only the rectangle's tiles are owned
+    const bool spans = reg.on && !span.empty() && span.size() <= (size_t)shs_dev::LIB_SPAN_ROWS;
+    wk.last_fp.span_rows = spans ? (int32_t)span.size() : 0;
+    for (size_t r = 0; spans && r < span.size(); ++r) wk.last_fp.span[r] = span[r];
     ctx->shadow_pending = false;
     ctx->shadow_reg = reg;
+    ctx->shadow_span = spans ? span : std::vector<uint32_t>{};
     return enqueue_pass(ctx, wk, true);
 }
 
@@ -1003,8 +1009,15 @@ extern "C" {
 // SHS_OPT_SHADOW_FOOTPRINT: the shadow-map bin tiles the camera pass about to be enqueued can read
 // (shs_footprint.hpp): the union over its shadowed draws of the light-space bounds of (the draw's world
 // box) ∩ (the camera frustum slice of the pixels this rank shades), widened by the PCF reach.
+// Also the rows' spans (shs_footprint.hpp footprint_rows, in bin tiles): empty when the map is taller
+// than LIB_SPAN_ROWS bin tiles or some draw has no bound.  (-DSHS_SHADOW_SPANS=0: rectangles only,
+// a timing comparison.)
+#ifndef SHS_SHADOW_SPANS
+#define SHS_SHADOW_SPANS 1
+#endif
 static shs_dev::ShardRegion shadow_region_for(const shs_ctx *ctx, const shs_lib_frame &f, const shs_lib_draw *draws,
-                                              int32_t n_draws, const shs_dev::ShardRegion &cam_reg) {
+                                              int32_t n_draws, const shs_dev::ShardRegion &cam_reg,
+                                              std::vector<uint32_t> &span) {
     const int W = f.width, H = f.height;
     int px[4] = {0, 0, W - 1, H - 1};
     if (f.shard_count > 1 && cam_reg.on) {
@@ -1013,6 +1026,11 @@ static shs_dev::ShardRegion shadow_region_for(const shs_ctx *ctx, const shs_lib_
         px[2] = std::min(W, (cam_reg.x1 + 1) * shs_dev::TILE) - 1;
         px[3] = std::min(H, (cam_reg.y1 + 1) * shs_dev::TILE) - 1;
     }
+    const int T = shs_dev::TILE;
+    const int rows = (ctx->shadow_h + T - 1) / T;
+    bool spans = SHS_SHADOW_SPANS && rows <= shs_dev::LIB_SPAN_ROWS;
+    std::vector<int> sx0((size_t)rows, 1), sx1((size_t)rows, 0);   // texel columns per row (x1 < x0: none)
+    double pts[220][2];
     shs_fp::TexelRect t;
     for (int i = 0; i < n_draws; ++i) {
         const shs_lib_draw &d = draws[i];
@@ -1022,11 +1040,43 @@ static shs_dev::ShardRegion shadow_region_for(const shs_ctx *ctx, const shs_lib_
         shs_fp::world_box(d.model, m.bmin, m.bmax, bmin, bmax);
         const int rad = std::max(0, d.shadow_pcf_radius);
         const int step = std::max(1, (int)std::round((1.0f < d.shadow_pcf_step) ? d.shadow_pcf_step : 1.0f));
+        int n_pts = 0;
         t = shs_fp::unite(t, shs_fp::shadow_footprint(d.light_viewproj, ctx->shadow_w, ctx->shadow_h, d.viewproj, W, H, px,
-                                                      bmin, bmax, rad * step));
+                                                      bmin, bmax, rad * step, pts, &n_pts));
+        if (n_pts < 0) spans = false;   // no bound: the whole map
+        else if (spans) shs_fp::footprint_rows(pts, n_pts, ctx->shadow_w, ctx->shadow_h, rad * step, T, rows, sx0.data(), sx1.data());
     }
-    const int T = shs_dev::TILE;
-    return t.empty() ? shs_dev::ShardRegion{1, 0, 0, -1, -1} : shs_dev::ShardRegion{1, t.x0 / T, t.y0 / T, t.x1 / T, t.y1 / T};
+    span.clear();
+    if (t.empty()) return shs_dev::ShardRegion{1, 0, 0, -1, -1};
+    const shs_dev::ShardRegion reg{1, t.x0 / T, t.y0 / T, t.x1 / T, t.y1 / T};
+    if (spans) {
+        span.resize((size_t)rows);
+        for (int r = 0; r < rows; ++r)
+            span[(size_t)r] = sx1[(size_t)r] < sx0[(size_t)r] ? 1u
+                              : (uint32_t)(sx0[(size_t)r] / T) | ((uint32_t)(sx1[(size_t)r] / T) << 16);
+    }
+    return reg;
+}
+
+// Is every tile of (need, need_span) rendered by (have, have_span)?  Spans as in enqueue_shadow.
+static bool shadow_covers(const shs_dev::ShardRegion &have, const std::vector<uint32_t> &have_span,
+                          const shs_dev::ShardRegion &need, const std::vector<uint32_t> &need_span) {
+    auto empty = [](const shs_dev::ShardRegion &r) { return r.x1 < r.x0 || r.y1 < r.y0; };
+    if (empty(need)) return true;
+    if (empty(have) || need.x0 < have.x0 || need.y0 < have.y0 || need.x1 > have.x1 || need.y1 > have.y1) return false;
+    if (have_span.empty()) return true;
+    for (int y = need.y0; y <= need.y1; ++y) {
+        int a = need.x0, b = need.x1;   // the row's needed columns
+        if (!need_span.empty()) {
+            if ((size_t)y >= need_span.size()) return false;
+            a = std::max(a, (int)(need_span[(size_t)y] & 0xffffu));
+            b = std::min(b, (int)(need_span[(size_t)y] >> 16));
+        }
+        if (a > b) continue;
+        if ((size_t)y >= have_span.size()) return false;
+        if (a < (int)(have_span[(size_t)y] & 0xffffu) || b > (int)(have_span[(size_t)y] >> 16)) return false;
+    }
+    return true;
 }
 
 int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_lib_draw *draws, int32_t n_draws) {
@@ -1110,7 +1160,9 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
     }
     wk.last_fp = fp;
     if (ctx->shadow_pending) {   // the recorded shadow pass, narrowed to what this pass reads
-        const int rc = enqueue_shadow(ctx, shadow_region_for(ctx, f, draws, n_draws, fp.reg));
+        std::vector<uint32_t> span;
+        const shs_dev::ShardRegion need = shadow_region_for(ctx, f, draws, n_draws, fp.reg, span);
+        const int rc = enqueue_shadow(ctx, need, span);
         if (rc) return rc;
     } else if (ctx->have_shadow && ctx->shadow_reg.on) {
         // A map rendered for an earlier camera pass's footprint, sampled again (a static sun reused over
@@ -1120,17 +1172,32 @@ int shs_render_pbr_forward(shs_ctx *ctx, const shs_lib_frame *frame, const shs_l
         bool shadowed = false;
         for (int i = 0; i < n_draws; ++i) shadowed = shadowed || draws[i].shadow;
         if (shadowed) {
-            const shs_dev::ShardRegion need = shadow_region_for(ctx, f, draws, n_draws, fp.reg);
-            const shs_dev::ShardRegion &have = ctx->shadow_reg;
-            auto empty = [](const shs_dev::ShardRegion &r) { return r.x1 < r.x0 || r.y1 < r.y0; };
-            const bool inside = empty(need) || (!empty(have) && need.x0 >= have.x0 && need.y0 >= have.y0 &&
-                                                need.x1 <= have.x1 && need.y1 <= have.y1);
-            if (!inside) {
+            std::vector<uint32_t> span;
+            const shs_dev::ShardRegion need = shadow_region_for(ctx, f, draws, n_draws, fp.reg, span);
+            const shs_dev::ShardRegion have = ctx->shadow_reg;
+            const std::vector<uint32_t> have_span = ctx->shadow_span;
+            if (!shadow_covers(have, have_span, need, span)) {
+                // re-rendered over the union: the rectangles' bounding rectangle, the rows' spans united
+                // (either side without spans: the whole rectangle)
+                auto empty = [](const shs_dev::ShardRegion &r) { return r.x1 < r.x0 || r.y1 < r.y0; };
                 const shs_dev::ShardRegion u = empty(have) ? need
                     : shs_dev::ShardRegion{1, std::min(need.x0, have.x0), std::min(need.y0, have.y0),
                                            std::max(need.x1, have.x1), std::max(need.y1, have.y1)};
+                std::vector<uint32_t> us;
+                if (empty(have)) us = span;
+                else if (!span.empty() && !have_span.empty() && span.size() == have_span.size()) {
+                    us.resize(span.size());
+                    for (size_t r = 0; r < span.size(); ++r) {
+                        const int a0 = (int)(span[r] & 0xffffu), a1 = (int)(span[r] >> 16);
+                        const int b0 = (int)(have_span[r] & 0xffffu), b1 = (int)(have_span[r] >> 16);
+                        const bool ea = a1 < a0 || (int)r < need.y0 || (int)r > need.y1;
+                        const bool eb = b1 < b0 || (int)r < have.y0 || (int)r > have.y1;
+                        us[r] = ea && eb ? 1u : ea ? have_span[r] : eb ? span[r]
+                              : (uint32_t)std::min(a0, b0) | ((uint32_t)std::max(a1, b1) << 16);
+                    }
+                }
                 int rc = check_superseded(ctx, ctx->lib_shadow);
-                if (!rc) rc = enqueue_shadow(ctx, u);
+                if (!rc) rc = enqueue_shadow(ctx, u, us);
                 if (rc) return rc;
             }
         }
@@ -1201,6 +1268,26 @@ int shs_shadow_footprint(const float light_viewproj[16], int32_t sm_w, int32_t s
     const double b0[3] = {world_min[0], world_min[1], world_min[2]}, b1[3] = {world_max[0], world_max[1], world_max[2]};
     const shs_fp::TexelRect t = shs_fp::shadow_footprint(light_viewproj, sm_w, sm_h, camera_viewproj, width, height, px, b0, b1, reach);
     texel_rect[0] = t.x0; texel_rect[1] = t.y0; texel_rect[2] = t.x1; texel_rect[3] = t.y1;
+    return SHS_OK;
+}
+
+int shs_shadow_footprint_rows(const float light_viewproj[16], int32_t sm_w, int32_t sm_h, const float camera_viewproj[16],
+                              int32_t width, int32_t height, const int32_t px_rect[4], const float world_min[3],
+                              const float world_max[3], int32_t reach, int32_t row_h, int32_t n_rows, int32_t *x0,
+                              int32_t *x1) {
+    if (!light_viewproj || !camera_viewproj || !px_rect || !world_min || !world_max || !x0 || !x1 || reach < 0 ||
+        row_h <= 0 || n_rows < 0)
+        return SHS_ERR_INVALID;
+    const int px[4] = {px_rect[0], px_rect[1], px_rect[2], px_rect[3]};
+    const double b0[3] = {world_min[0], world_min[1], world_min[2]}, b1[3] = {world_max[0], world_max[1], world_max[2]};
+    double pts[220][2];
+    int n_pts = 0;
+    shs_fp::shadow_footprint(light_viewproj, sm_w, sm_h, camera_viewproj, width, height, px, b0, b1, reach, pts, &n_pts);
+    for (int r = 0; r < n_rows; ++r) {
+        x0[r] = n_pts < 0 ? 0 : 1;
+        x1[r] = n_pts < 0 ? sm_w - 1 : 0;
+    }
+    if (n_pts > 0) shs_fp::footprint_rows(pts, n_pts, sm_w, sm_h, reach, row_h, n_rows, x0, x1);
     return SHS_OK;
 }
 

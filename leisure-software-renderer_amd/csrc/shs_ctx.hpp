@@ -231,6 +231,7 @@ struct shs_ctx {
     bool shadow_footprint = false;        // SHS_OPT_SHADOW_FOOTPRINT: shadow passes render only what the next camera pass reads
     bool shadow_pending = false;          // a footprint shadow pass recorded, not enqueued yet (the camera pass does it)
     shs_dev::ShardRegion shadow_reg{0, 0, 0, 0, 0};   // the bin tiles the last enqueued shadow pass rendered (on = 0: all)
+    std::vector<uint32_t> shadow_span;   // ... and within that rectangle the row spans (empty: all of it; round 6)
     std::vector<uint4> reg_in;            // the block bounds reg_next was last balanced from (identical: reused)
     int reg_in_count = -1, reg_in_w = 0, reg_in_h = 0, reg_in_root = 0;
     // Tile orders / owned-list tables by geometry + ownership, uploaded once into their own buffers (a

@@ -44,11 +44,15 @@ inline void mat_row(const float *m, int i, double out[4]) {
 // (camera frustum slice of the pixel rectangle px = {x0, y0, x1, y1}, inclusive, rows y up, of a W x H
 // frame) can read, for a light projection light_vp and a PCF reach of `reach` texels.  Anything that
 // cannot be bounded (non-finite input, a polytope point with light w <= 0) gives the whole map.
+// (pts / n_pts, when given: the polytope's vertices projected to texel space, at most 220 of them;
+// n_pts = -1 when the result is the whole map for lack of a bound.)
 inline TexelRect shadow_footprint(const float light_vp[16], int sm_w, int sm_h, const float camera_vp[16], int W, int H,
-                                  const int px[4], const double bmin[3], const double bmax[3], int reach) {
+                                  const int px[4], const double bmin[3], const double bmax[3], int reach,
+                                  double (*pts)[2] = nullptr, int *n_pts = nullptr) {
+    if (n_pts) *n_pts = -1;
     TexelRect full{0, 0, sm_w - 1, sm_h - 1};
-    if (sm_w <= 0 || sm_h <= 0) return TexelRect{};
-    if (px[2] < px[0] || px[3] < px[1]) return TexelRect{};   // no pixel: nothing is read
+    if (sm_w <= 0 || sm_h <= 0) { if (n_pts) *n_pts = 0; return TexelRect{}; }
+    if (px[2] < px[0] || px[3] < px[1]) { if (n_pts) *n_pts = 0; return TexelRect{}; }   // no pixel: nothing is read
     double pl[12][4];
     int n = 0;
     for (int a = 0; a < 3; ++a) {   // the world box: x - min >= 0, max - x >= 0
@@ -89,6 +93,7 @@ inline TexelRect shadow_footprint(const float light_vp[16], int sm_w, int sm_h, 
     for (int i = 0; i < 4; ++i) mat_row(light_vp, i, lv[i]);
     double ux0 = INFINITY, ux1 = -INFINITY, uy0 = INFINITY, uy1 = -INFINITY;
     bool any = false;
+    int np_ = 0;
     for (int i = 0; i < n; ++i)
         for (int j = i + 1; j < n; ++j)
             for (int k = j + 1; k < n; ++k) {
@@ -121,8 +126,11 @@ inline TexelRect shadow_footprint(const float light_vp[16], int sm_w, int sm_h, 
                 if (!(isfinite(u) && isfinite(v))) return full;
                 ux0 = std::min(ux0, u * (sm_w - 1)); ux1 = std::max(ux1, u * (sm_w - 1));
                 uy0 = std::min(uy0, v * (sm_h - 1)); uy1 = std::max(uy1, v * (sm_h - 1));
+                if (pts && np_ < 220) { pts[np_][0] = u * (sm_w - 1); pts[np_][1] = v * (sm_h - 1); }
+                ++np_;
                 any = true;
             }
+    if (n_pts) *n_pts = std::min(np_, 220);
     if (!any) return TexelRect{};   // the box misses the pixels' frustum slice: no point, no read
     const double m = (double)reach + 2.0;
     auto clampi = [](double v, int hi) { return (int)std::min<double>(std::max<double>(v, 0.0), (double)hi); };
@@ -132,6 +140,65 @@ inline TexelRect shadow_footprint(const float light_vp[16], int sm_w, int sm_h, 
     t.y0 = clampi(floor(uy0 - m), sm_h - 1);
     t.y1 = clampi(ceil(uy1 + m), sm_h - 1);
     return t;
+}
+
+// Per row of `row_h` texels (row r: texel rows r * row_h .. r * row_h + row_h - 1), the texel columns the
+// PCF can read: the x extent of the convex hull of the projected vertices (the polytope's image is that
+// hull) within the row's band widened by the reach + 2 margin above and below, widened by the same margin
+// left and right, clamped to the map.  x1 < x0: nothing in that row is read.  Rows are united into
+// x0[] / x1[] (min / max), so several draws' spans can be gathered into one table.  Since round 6: the
+// region-sharded shadow pass renders only these tiles of its rectangle.
+inline void footprint_rows(const double (*pts)[2], int n, int sm_w, int sm_h, int reach, int row_h, int n_rows, int *x0,
+                           int *x1) {
+    if (n <= 0) return;
+    // Andrew's monotone chain over the points (n <= 220)
+    int idx[220];
+    const int m_ = std::min(n, 220);
+    for (int i = 0; i < m_; ++i) idx[i] = i;
+    std::sort(idx, idx + m_, [&](int a, int b) {
+        return pts[a][0] < pts[b][0] || (pts[a][0] == pts[b][0] && pts[a][1] < pts[b][1]);
+    });
+    int hull[441], k = 0;
+    auto cross = [&](int o, int a, int b) {
+        return (pts[a][0] - pts[o][0]) * (pts[b][1] - pts[o][1]) - (pts[a][1] - pts[o][1]) * (pts[b][0] - pts[o][0]);
+    };
+    for (int i = 0; i < m_; ++i) {
+        while (k >= 2 && cross(hull[k - 2], hull[k - 1], idx[i]) <= 0.0) --k;
+        hull[k++] = idx[i];
+    }
+    for (int i = m_ - 2, lo = k + 1; i >= 0; --i) {
+        while (k >= lo && cross(hull[k - 2], hull[k - 1], idx[i]) <= 0.0) --k;
+        hull[k++] = idx[i];
+    }
+    if (k > 1) --k;   // the last point repeats the first
+    const double mg = (double)reach + 2.0;
+    for (int r = 0; r < n_rows; ++r) {
+        const double b0 = (double)r * row_h - mg, b1 = (double)r * row_h + (row_h - 1) + mg;
+        double lo = INFINITY, hi = -INFINITY;
+        for (int e = 0; e < k; ++e) {   // each hull edge (a single point: a degenerate edge) clipped to the band
+            const double *p = pts[hull[e]], *q = pts[hull[(e + 1) % k]];
+            double t0 = 0.0, t1 = 1.0;
+            const double dy = q[1] - p[1];
+            if (dy == 0.0) {
+                if (p[1] < b0 || p[1] > b1) continue;
+            } else {
+                double ta = (b0 - p[1]) / dy, tb = (b1 - p[1]) / dy;
+                if (ta > tb) std::swap(ta, tb);
+                t0 = std::max(t0, ta);
+                t1 = std::min(t1, tb);
+                if (t0 > t1) continue;
+            }
+            const double xa = p[0] + t0 * (q[0] - p[0]), xb = p[0] + t1 * (q[0] - p[0]);
+            lo = std::min(lo, std::min(xa, xb));
+            hi = std::max(hi, std::max(xa, xb));
+        }
+        if (!(lo <= hi)) continue;
+        const int a = (int)std::min<double>(std::max<double>(floor(lo - mg), 0.0), (double)(sm_w - 1));
+        const int b = (int)std::min<double>(std::max<double>(ceil(hi + mg), 0.0), (double)(sm_w - 1));
+        if (x1[r] < x0[r]) { x0[r] = a; x1[r] = b; }
+        else { x0[r] = std::min(x0[r], a); x1[r] = std::max(x1[r], b); }
+    }
+    (void)sm_h;
 }
 
 // The world box of a mesh's model-space box [b0, b1] under a model matrix (column-major), in double and

@@ -86,8 +86,31 @@ constexpr int LIB_CHUNK = 128;             // records staged in LDS per pass
 #endif
 constexpr int MAX_POLY = 16;               // clipped polygon capacity (3 + 6 planes x up to 2 crossings)
 
+// A footprint shadow pass's row spans (shs_footprint.hpp footprint_rows): a bin tile of the rectangle
+// outside its row's span is never read by the camera pass, so nothing is binned to or rasterised on it
+// (its raster tiles are only cleared).  span_rows 0: the whole rectangle.
+__device__ __forceinline__ bool lib_in_span(const LibFrameParams &fp, int bx, int by) {
+    if (fp.span_rows == 0) return true;
+    if (by < 0 || by >= fp.span_rows) return false;
+    const uint32_t s = fp.span[by];
+    return bx >= (int)(s & 0xffffu) && bx <= (int)(s >> 16);
+}
+
 __device__ __forceinline__ bool lib_owned(const LibFrameParams &fp, int bx, int by) {
-    return shard_owned(fp.rank, fp.count, fp.reg, bx, by, fp.tiles_x);
+    return shard_owned(fp.rank, fp.count, fp.reg, bx, by, fp.tiles_x) && lib_in_span(fp, bx, by);
+}
+
+// Does the bin-tile rectangle [tx0, tx1] x [ty0, ty1] hold a tile this pass renders?
+__device__ inline bool lib_owns_any(const LibFrameParams &fp, int tx0, int tx1, int ty0, int ty1) {
+    if (!shard_owns_any(fp.rank, fp.count, fp.reg, tx0, tx1, ty0, ty1, fp.tiles_x)) return false;
+    if (fp.span_rows == 0) return true;
+    const int xa = max(tx0, fp.reg.x0), xb = min(tx1, fp.reg.x1);
+    const int ya = max(ty0, fp.reg.y0), yb = min(ty1, min(fp.reg.y1, fp.span_rows - 1));
+    for (int y = ya; y <= yb; ++y) {
+        const uint32_t s = fp.span[y];
+        if (max(xa, (int)(s & 0xffffu)) <= min(xb, (int)(s >> 16))) return true;
+    }
+    return false;
 }
 
 // Orderable key bits (z_key's high word) of a conservative lower bound of the depth lib_test can
@@ -457,7 +480,7 @@ __device__ __forceinline__ bool fan_screen(const LibFrameParams &fp, const LibDr
         // still count it)
         const int tx0 = x0 / TILE, tx1 = x1 / TILE, ty0 = y0 / TILE, ty1 = y1 / TILE;
         if (fp.reg.on) {
-            live = shard_owns_any(fp.rank, fp.count, fp.reg, tx0, tx1, ty0, ty1, fp.tiles_x);
+            live = lib_owns_any(fp, tx0, tx1, ty0, ty1);
         } else if ((tx1 - tx0) < 2 && (ty1 - ty0) < 2) {
             bool mine = false;
             for (int ty = ty0; ty <= ty1; ++ty)
@@ -574,7 +597,7 @@ __device__ __forceinline__ bool clip_reaches_rank(const LibFrameParams &fp, cons
     const int tx0 = max(0, (int)fmaxf(x0 - 2.0f, 0.0f) / TILE), tx1 = min(fp.tiles_x - 1, (int)fminf(x1 + 2.0f, (float)(fp.W - 1)) / TILE);
     const int ty0 = max(0, (int)fmaxf(y0 - 2.0f, 0.0f) / TILE), ty1 = min(fp.tiles_y - 1, (int)fminf(y1 + 2.0f, (float)(fp.H - 1)) / TILE);
     if (!fp.reg.on && ty1 - ty0 >= 64) return true;
-    return shard_owns_any(fp.rank, fp.count, fp.reg, tx0, tx1, ty0, ty1, fp.tiles_x);
+    return lib_owns_any(fp, tx0, tx1, ty0, ty1);
 }
 
 // Camera pass: one input triangle of rasterize_mesh.  A triangle that is not trivially inside the
@@ -949,7 +972,7 @@ __global__ __launch_bounds__(256) void k_lib_blocks(LibFrameParams fp, LibBuffer
         if (j == 0)
             fb.blkrect[b] = make_uint4((uint32_t)bx0 | ((uint32_t)bx1 << 16), (uint32_t)by0 | ((uint32_t)by1 << 16),
                                        (uint32_t)max(0, t1 - t0 + 1), bounded ? 1u : (finite && est) ? 2u : 0u);
-        const bool need = !(bounded && !shard_owns_any(fp.rank, fp.count, fp.reg, bx0, bx1, by0, by1, fp.tiles_x));
+        const bool need = !(bounded && !lib_owns_any(fp, bx0, bx1, by0, by1));
         if (!need) {   // no triangle of the block reaches this rank
             if (j == 0) fb.blk_stat[b] = make_uint2(0u, 0u);
             if (fp.scan_mode)
@@ -2644,8 +2667,15 @@ __global__ __launch_bounds__(256) void k_lib_plan(LibFrameParams fp, LibBuffers 
     if (kk) fb.busy[rt] = 2u;   // split: the in-order pass skips it (k_lib_resolve resets the flag)
 }
 
+#ifndef SHS_RASTER_SHALLOW_WAVES
+#define SHS_RASTER_SHALLOW_WAVES 6
+#endif
+#ifndef SHS_RASTER_DEEP_WAVES
+#define SHS_RASTER_DEEP_WAVES 3
+#endif
 template <bool SHADOW, int LIB_CAND>
-__global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? 6 : 3) void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
+__global__ __launch_bounds__(256, LIB_CAND == LIB_CAND_SHALLOW ? SHS_RASTER_SHALLOW_WAVES : SHS_RASTER_DEEP_WAVES)
+void k_lib_raster(LibFrameParams fp, LibBuffers fb) {
     __shared__ LibShared<LIB_CAND> sh;
     const int tid = threadIdx.x;
     const uint32_t *cnt = fb.counters + fp.parity * LC_N;

@@ -107,6 +107,9 @@ constexpr int LC_OVERFLOW = 0, LC_SPILL = 1, LC_EXTRA = 2, LC_CLIPQ = 3, LC_BIGT
 static_assert(LC_BIGQ == LC_BIGT + 1 && LC_BIGT % 2 == 0 && LC_N % 2 == 0, "64-bit big-queue word");
 constexpr uint32_t LOV_SPILL = 1u, LOV_EXTRA = 2u;
 
+// Row spans of a footprint shadow pass (LibFrameParams::span): maps up to 64 bin tiles (2,048 texels) high.
+constexpr int LIB_SPAN_ROWS = 64;
+
 struct LibFrameParams {
     int32_t W, H;
     int32_t rank, count;             // shard ownership of 32x32 bin tiles (tile % count == rank, or reg)
@@ -137,6 +140,8 @@ struct LibFrameParams {
     uint32_t hsort;                  // camera pass: bin lists of more than hsort_min entries (and at most
     uint32_t hsort_min;              //   min(bin_cap, LIB_HSORT_MAX)) are depth-sorted whole by k_lib_hsort
     ShardRegion reg;                 // count > 1 with reg.on: this rank's rectangle of bin tiles
+    int32_t span_rows;               // shadow pass of a footprint (round 6): > 0 -- per bin-tile row y < span_rows
+    uint32_t span[LIB_SPAN_ROWS];    //   the bin columns x0 | x1 << 16 it renders (x1 < x0: none); 0 -- all of reg
 };
 
 struct LibBuffers {

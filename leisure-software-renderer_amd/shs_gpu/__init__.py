@@ -515,6 +515,25 @@ class Context:
             raise ShsError(rc, "shs_shadow_footprint")
         return tuple(int(v) for v in out)
 
+    @staticmethod
+    def shadow_footprint_rows(light_vp, sm_size, camera_vp, width, height, px_rect, world_min, world_max, reach,
+                              row_h=32):
+        """shs_shadow_footprint_rows: per row of row_h texels the read texel columns -> (x0[], x1[]) int32
+        arrays (x1 < x0: none), from the footprint polytope's convex light-space image."""
+        sw, sh = (sm_size, sm_size) if isinstance(sm_size, int) else sm_size
+        f16 = lambda m: np.ascontiguousarray(np.asarray(m, np.float32).reshape(16))
+        f3 = lambda v: np.ascontiguousarray(np.asarray(v, np.float32).reshape(3))
+        lv, cv, b0, b1 = f16(light_vp), f16(camera_vp), f3(world_min), f3(world_max)
+        px = np.ascontiguousarray(np.asarray(px_rect, np.int32).reshape(4))
+        n_rows = (int(sh) + row_h - 1) // row_h
+        x0, x1 = np.zeros(n_rows, np.int32), np.zeros(n_rows, np.int32)
+        rc = lib().shs_shadow_footprint_rows(lv.ctypes.data, int(sw), int(sh), cv.ctypes.data, int(width), int(height),
+                                             px.ctypes.data, b0.ctypes.data, b1.ctypes.data, int(reach), int(row_h),
+                                             n_rows, x0.ctypes.data, x1.ctypes.data)
+        if rc != 0:
+            raise ShsError(rc, "shs_shadow_footprint_rows")
+        return x0, x1
+
     LIB_TIMELINE_FIELDS = ("start", "end", "gather", "pairs", "shade", "clear", "n_busy", "n_clear", "chunks",
                            "n_pairs", "n_cand", "max_tile", "stage", "seg", "tiles", "last",
                            "mt_rt", "mt_items", "mt_rounds", "mt_passes", "mt_staged", "mt_pairs", "mt_gather",

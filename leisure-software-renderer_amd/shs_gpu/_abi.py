@@ -282,6 +282,8 @@ SIGNATURES = [
     ("shs_get_shadow_region", ctypes.c_int, [_P, _P]),
     ("shs_shadow_footprint", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, _P,
                                             ctypes.c_int32, _P]),
+    ("shs_shadow_footprint_rows", ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_int32, _P,
+                                                 _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     ("shs_tiles_packed_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_tiles_rank_words", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     ("shs_get_shard_regions", ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),

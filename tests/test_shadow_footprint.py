@@ -230,3 +230,49 @@ def test_footprint_empty_for_a_rank(oracle_mod):
             c.close()
             frame.shard_rank, frame.shard_count = 0, 1
     assert n_empty >= 1, "every rank's rectangle reached Suzanne's shadow reads"
+
+
+def _brute_texels(lvp, S, cvp, W, H, px, bmin, bmax, reach, n=400_000, seed=1):
+    """The brute force's read texels themselves: (cx, cy) of every kept point, before the +- reach."""
+    rng = np.random.default_rng(seed)
+    pts = rng.uniform(bmin, bmax, size=(n, 3))
+    ph = np.concatenate([pts, np.ones((n, 1))], axis=1)
+    c = ph @ _mat(cvp).T
+    w = c[:, 3]
+    ok = (w > 0) & (np.abs(c[:, 0]) <= w) & (np.abs(c[:, 1]) <= w) & (np.abs(c[:, 2]) <= w)
+    sx = (c[:, 0] / w * 0.5 + 0.5) * (W - 1)
+    sy = (c[:, 1] / w * 0.5 + 0.5) * (H - 1)
+    ok &= (sx >= px[0] + 0.5) & (sx <= px[2] + 0.5) & (sy >= px[1] + 0.5) & (sy <= px[3] + 0.5)
+    lp = ph[ok] @ _mat(lvp).T
+    u = (lp[:, 0] / lp[:, 3]) * 0.5 + 0.5
+    v = (lp[:, 1] / lp[:, 3]) * 0.5 + 0.5
+    inside = (u >= 0) & (u <= 1) & (v >= 0) & (v <= 1)
+    return np.round(u[inside] * (S - 1)).astype(np.int64), np.round(v[inside] * (S - 1)).astype(np.int64)
+
+
+@pytest.mark.parametrize("rect", [(0, 0, 3839, 2159), (1920, 1080, 3839, 2159), (960, 1080, 1919, 2159),
+                                  (1600, 900, 1663, 931)])
+@pytest.mark.parametrize("which", [0, 1])   # floor, Suzanne
+def test_footprint_rows_hold_every_read_texel(rect, which):
+    """Round 6: the per-row spans of the footprint (the convex hull of the polytope's light-space image,
+    what a footprint shadow pass renders of its rectangle) hold every texel the brute force reads,
+    PCF taps included, and for a partial view are much smaller than the rectangle."""
+    S, W, H, reach = 2048, 3840, 2160, 2
+    lvp = _light_vp(S)
+    frame, draws, _, _, _ = scene_lib.c5_scene(W, H, S)
+    d = draws[which]
+    bmin, bmax = _world_box(d)
+    x0, x1 = shs_gpu.Context.shadow_footprint_rows(lvp, S, d.viewproj, W, H, rect, bmin, bmax, reach)
+    cx, cy = _brute_texels(lvp, S, d.viewproj, W, H, rect, bmin, bmax, reach)
+    for ox in (-reach, reach):                         # the PCF taps' extreme columns and rows
+        for oy in (-reach, 0, reach):
+            tx, ty = np.clip(cx + ox, 0, S - 1), np.clip(cy + oy, 0, S - 1)
+            r = ty // 32
+            assert (x0[r] <= x1[r]).all(), "a read texel in a row with no span"
+            assert ((tx >= x0[r]) & (tx <= x1[r])).all(), (rect, which, ox, oy)
+    fp = shs_gpu.Context.shadow_footprint(lvp, S, d.viewproj, W, H, rect, bmin, bmax, reach)
+    if fp[2] >= fp[0]:
+        span = np.where(x1 >= x0, x1 - x0 + 1, 0).sum() * 32
+        assert span <= (fp[2] - fp[0] + 1) * (fp[3] // 32 - fp[1] // 32 + 1) * 32, (span, fp)   # within the rectangle's rows
+        if rect == (960, 1080, 1919, 2159) and which == 0:   # the far floor of a partial view: much smaller
+            assert span < 0.7 * (fp[2] - fp[0] + 1) * (fp[3] - fp[1] + 1), (span, fp)
