@@ -100,12 +100,15 @@ __device__ __forceinline__ bool lib_owned(const LibFrameParams &fp, int bx, int 
     return shard_owned(fp.rank, fp.count, fp.reg, bx, by, fp.tiles_x) && lib_in_span(fp, bx, by);
 }
 
-// Does the bin-tile rectangle [tx0, tx1] x [ty0, ty1] hold a tile this pass renders?
-__device__ inline bool lib_owns_any(const LibFrameParams &fp, int tx0, int tx1, int ty0, int ty1) {
+// Does the bin-tile rectangle [tx0, tx1] x [ty0, ty1] hold a tile this pass renders?  The span test
+// walks the rows (a kernel-argument load each): a rectangle over more than max_rows rows is kept
+// (conservative; its bin appends still test each tile).
+__device__ inline bool lib_owns_any(const LibFrameParams &fp, int tx0, int tx1, int ty0, int ty1, int max_rows = LIB_SPAN_ROWS) {
     if (!shard_owns_any(fp.rank, fp.count, fp.reg, tx0, tx1, ty0, ty1, fp.tiles_x)) return false;
     if (fp.span_rows == 0) return true;
     const int xa = max(tx0, fp.reg.x0), xb = min(tx1, fp.reg.x1);
     const int ya = max(ty0, fp.reg.y0), yb = min(ty1, min(fp.reg.y1, fp.span_rows - 1));
+    if (yb - ya >= max_rows) return true;
     for (int y = ya; y <= yb; ++y) {
         const uint32_t s = fp.span[y];
         if (max(xa, (int)(s & 0xffffu)) <= min(xb, (int)(s >> 16))) return true;
@@ -480,7 +483,7 @@ __device__ __forceinline__ bool fan_screen(const LibFrameParams &fp, const LibDr
         // still count it)
         const int tx0 = x0 / TILE, tx1 = x1 / TILE, ty0 = y0 / TILE, ty1 = y1 / TILE;
         if (fp.reg.on) {
-            live = lib_owns_any(fp, tx0, tx1, ty0, ty1);
+            live = lib_owns_any(fp, tx0, tx1, ty0, ty1, 2);   // per primitive: at most two rows walked
         } else if ((tx1 - tx0) < 2 && (ty1 - ty0) < 2) {
             bool mine = false;
             for (int ty = ty0; ty <= ty1; ++ty)
