@@ -977,8 +977,11 @@ __device__ __forceinline__ void setup_item(const FrameParams &fp, const FrameBuf
 #ifndef SHS_BIN_SETUP_WAVES
 #define SHS_BIN_SETUP_WAVES 8   // (-D...: timing experiments)
 #endif
+#ifndef SHS_SCAN_SETUP_WAVES
+#define SHS_SCAN_SETUP_WAVES 5  // (-D...: timing experiments)
+#endif
 template <bool KARG, bool BIN>
-__global__ __launch_bounds__(256, BIN ? SHS_BIN_SETUP_WAVES : 5) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
+__global__ __launch_bounds__(256, BIN ? SHS_BIN_SETUP_WAVES : SHS_SCAN_SETUP_WAVES) void k_setup(FrameParams fp, FrameBuffers fb_all, KArgDraws ka) {
     __shared__ GhostScratch s_ghost[4];
     __shared__ uint32_t s_stat[4];
     __shared__ NewBusy s_new;
